@@ -1,0 +1,255 @@
+"""Host-side data formats of the TNet training path (pure Python / numpy, no device code).
+
+* ``.nnet`` text weight files -- the boundary format read/written by
+  ``CuNetwork::ReadNetwork/WriteNetwork`` (src/CuTNetLib/cuNetwork.cc:47-73, factory/dumper
+  :211-387): ``<tag> nOut nIn`` lines, ``m R C`` + R rows holding W^T, ``v N`` + N floats
+  (src/KaldiLib/Matrix.tcc:521-600, Vector.tcc:525-571).
+* HTK feature files (12-byte big-endian header, big-endian f32 payload;
+  src/KaldiLib/Features.h:113-123) and HTK MLF label files
+  (src/KaldiLib/Labels.cc:44-187: ``beg end state`` in 100 ns units, frame interval
+  ``[(beg+P/2)/P, (end+P/2)/P)``).
+* ``gen_mlp_init`` -- a seeded Python-3 restatement of tools/init/gen_mlp_init.py:36-68
+  (``--gauss --negbias``: W ~ 0.1*N(0,1), hidden bias U[-4.1,-3.9], output bias 0).
+* deterministic synthetic corpora (features ~ N(0,1), teacher-MLP or uniform labels) used by the
+  tests and by bench.py.
+
+The C++ product library has its own reader/writer for the same format
+(nnet-asr_amd/csrc/host/nnet_io.cpp); this module exists so tests and the bench can build
+inputs without touching the device.
+"""
+from __future__ import annotations
+
+import io
+import os
+import struct
+from dataclasses import dataclass, field
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+# --------------------------------------------------------------------------------------
+# .nnet text format
+# --------------------------------------------------------------------------------------
+
+
+@dataclass
+class Layer:
+    tag: str                      # "<biasedlinearity>", "<sigmoid>", "<softmax>", "<rbm>", ...
+    n_out: int
+    n_in: int
+    W: Optional[np.ndarray] = None   # stored as in memory: [n_in x n_out] (file holds W^T)
+    b: Optional[np.ndarray] = None   # [n_out]
+    extra: dict = field(default_factory=dict)
+
+
+def _fmt(x: float, prec: int) -> str:
+    return format(float(x), f".{prec}g")
+
+
+def write_nnet(layers: Sequence[Layer], path_or_buf, precision: int = 6) -> None:
+    """Write layers in the reference text format (default ostream precision = 6 digits)."""
+    out = io.StringIO()
+    for L in layers:
+        out.write(f"{L.tag} {L.n_out} {L.n_in}\n")
+        if L.tag in ("<biasedlinearity>", "<rbm>", "<recurrent>"):
+            if L.tag == "<rbm>":
+                out.write(f"{L.extra.get('vis_type', 'bern')} {L.extra.get('hid_type', 'bern')}\n")
+            Wt = np.asarray(L.W, dtype=np.float32).T   # file holds [n_out x n_in(+n_out)]
+            out.write(f"m {Wt.shape[0]} {Wt.shape[1]}\n")
+            for row in Wt:
+                out.write(" ".join(_fmt(v, precision) for v in row))
+                out.write(" \n")
+            if L.tag == "<rbm>":
+                vb = np.asarray(L.extra["vis_bias"], dtype=np.float32)
+                out.write(f"v {vb.shape[0]}  " + " ".join(_fmt(v, precision) for v in vb) + " ")
+                out.write("\n")
+            b = np.asarray(L.b, dtype=np.float32)
+            out.write(f"v {b.shape[0]}  " + " ".join(_fmt(v, precision) for v in b) + " ")
+            out.write("\n\n")
+    text = out.getvalue()
+    if hasattr(path_or_buf, "write"):
+        path_or_buf.write(text)
+    else:
+        with open(path_or_buf, "w") as f:
+            f.write(text)
+
+
+def _tokens(text: str):
+    for tok in text.split():
+        yield tok
+
+
+def read_nnet(path_or_text: str) -> List[Layer]:
+    """Parse a .nnet text file (tags are case-insensitive; ``<endblock>`` terminates)."""
+    if os.path.exists(path_or_text):
+        with open(path_or_text) as f:
+            text = f.read()
+    else:
+        text = path_or_text
+    toks = text.split()
+    i = 0
+    layers: List[Layer] = []
+
+    def read_matrix():
+        nonlocal i
+        assert toks[i] == "m", toks[i]
+        r, c = int(toks[i + 1]), int(toks[i + 2])
+        i += 3
+        m = np.array(toks[i:i + r * c], dtype=np.float32).reshape(r, c)
+        i += r * c
+        return m
+
+    def read_vector():
+        nonlocal i
+        assert toks[i] == "v", toks[i]
+        n = int(toks[i + 1])
+        i += 2
+        v = np.array(toks[i:i + n], dtype=np.float32)
+        i += n
+        return v
+
+    while i < len(toks):
+        tag = toks[i].lower()
+        if tag == "<endblock>":
+            break
+        n_out, n_in = int(toks[i + 1]), int(toks[i + 2])
+        i += 3
+        L = Layer(tag, n_out, n_in)
+        if tag == "<biasedlinearity>" or tag == "<recurrent>":
+            L.W = np.ascontiguousarray(read_matrix().T)
+            L.b = read_vector()
+        elif tag == "<rbm>":
+            L.extra["vis_type"] = toks[i].lower()
+            L.extra["hid_type"] = toks[i + 1].lower()
+            i += 2
+            L.W = np.ascontiguousarray(read_matrix().T)
+            L.extra["vis_bias"] = read_vector()
+            L.b = read_vector()
+        layers.append(L)
+    return layers
+
+
+def gen_mlp_init(dims: Sequence[int], seed: int, gauss: bool = True, negbias: bool = True) -> List[Layer]:
+    """Seeded restatement of tools/init/gen_mlp_init.py:36-68 (numpy RNG, not Python 2's)."""
+    rng = np.random.default_rng(seed)
+    layers: List[Layer] = []
+    for li in range(len(dims) - 1):
+        n_in, n_out = dims[li], dims[li + 1]
+        if gauss:
+            Wt = (0.1 * rng.standard_normal((n_out, n_in))).astype(np.float32)
+        else:
+            Wt = (rng.random((n_out, n_in)) / 5.0 - 0.1).astype(np.float32)
+        last = li == len(dims) - 2
+        if last or not negbias:
+            b = np.zeros(n_out, np.float32)
+        else:
+            b = (rng.random(n_out) / 5.0 - 4.1).astype(np.float32)
+        layers.append(Layer("<biasedlinearity>", n_out, n_in, np.ascontiguousarray(Wt.T), b))
+        layers.append(Layer("<softmax>" if last else "<sigmoid>", n_out, n_out))
+    return layers
+
+
+def round_trip_text(layers: Sequence[Layer], precision: int = 6) -> List[Layer]:
+    """Weights exactly as a reader sees them after a text write at ``precision`` digits."""
+    buf = io.StringIO()
+    write_nnet(layers, buf, precision)
+    return read_nnet(buf.getvalue())
+
+
+# --------------------------------------------------------------------------------------
+# HTK features / MLF labels
+# --------------------------------------------------------------------------------------
+
+HTK_USER = 9
+
+
+def write_htk(path: str, feats: np.ndarray, samp_period: int = 100000, kind: int = HTK_USER) -> None:
+    feats = np.asarray(feats, dtype=np.float32)
+    n, d = feats.shape
+    with open(path, "wb") as f:
+        f.write(struct.pack(">iihh", n, samp_period, d * 4, kind))
+        f.write(feats.astype(">f4").tobytes())
+
+
+def read_htk(path: str) -> np.ndarray:
+    with open(path, "rb") as f:
+        n, period, size, kind = struct.unpack(">iihh", f.read(12))
+        data = np.frombuffer(f.read(n * size), dtype=">f4").astype(np.float32)
+    return data.reshape(n, size // 4)
+
+
+def write_mlf(path: str, utts: Sequence[str], labels: Sequence[np.ndarray], state_names: Sequence[str],
+              samp_period: int = 100000) -> None:
+    """One label segment per run of equal class ids; '*/<utt>.lab' patterns like examples/01."""
+    with open(path, "w") as f:
+        f.write("#!MLF!#\n")
+        for u, lab in zip(utts, labels):
+            f.write(f'"*/{u}.lab"\n')
+            lab = np.asarray(lab)
+            start = 0
+            for t in range(1, len(lab) + 1):
+                if t == len(lab) or lab[t] != lab[start]:
+                    f.write(f"{start * samp_period} {t * samp_period} {state_names[lab[start]]}\n")
+                    start = t
+            f.write(".\n")
+
+
+# --------------------------------------------------------------------------------------
+# Synthetic corpora
+# --------------------------------------------------------------------------------------
+
+
+@dataclass
+class Corpus:
+    feats: List[np.ndarray]      # per utterance [T x D] float32
+    labels: List[np.ndarray]     # per utterance [T] int32 class ids
+
+    @property
+    def frames(self) -> int:
+        return int(sum(len(l) for l in self.labels))
+
+
+def _teacher_labels(x: np.ndarray, teacher: List[np.ndarray], n_cls: int) -> np.ndarray:
+    h = x
+    for k, W in enumerate(teacher):
+        h = h @ W
+        if k < len(teacher) - 1:
+            h = np.tanh(h)
+    return np.argmax(h, axis=1).astype(np.int32)
+
+
+def synth_corpus(n_utts: int, dim: int, n_cls: int, seed: int = 0, min_len: int = 200, max_len: int = 1500,
+                 teacher: bool = True, teacher_hidden: int = 64) -> Corpus:
+    """Deterministic synthetic stacked-feature corpus: N(0,1) features, teacher-MLP labels."""
+    rng = np.random.default_rng(seed)
+    lens = rng.integers(min_len, max_len + 1, size=n_utts)
+    trng = np.random.default_rng(seed + 1)
+    T = [trng.standard_normal((dim, teacher_hidden)).astype(np.float32) / np.sqrt(dim),
+         trng.standard_normal((teacher_hidden, n_cls)).astype(np.float32) / np.sqrt(teacher_hidden) * 4.0]
+    feats, labels = [], []
+    for n in lens:
+        x = rng.standard_normal((int(n), dim)).astype(np.float32)
+        if teacher:
+            y = _teacher_labels(x, T, n_cls)
+        else:
+            y = rng.integers(0, n_cls, size=int(n)).astype(np.int32)
+        feats.append(x)
+        labels.append(y)
+    return Corpus(feats, labels)
+
+
+def write_corpus_htk(corpus: Corpus, outdir: str, n_cls: int) -> dict:
+    """Write HTK features, scp, MLF and a state map so the reference TNet can train on it."""
+    os.makedirs(os.path.join(outdir, "features"), exist_ok=True)
+    names = [f"u{i:05d}" for i in range(len(corpus.feats))]
+    scp = os.path.join(outdir, "train.scp")
+    with open(scp, "w") as f:
+        for n, x in zip(names, corpus.feats):
+            p = os.path.join(outdir, "features", n + ".fea")
+            write_htk(p, x)
+            f.write(p + "\n")
+    states = [f"s{k}" for k in range(n_cls)]
+    with open(os.path.join(outdir, "states"), "w") as f:
+        f.write("\n".join(states) + "\n")
+    write_mlf(os.path.join(outdir, "train.mlf"), names, corpus.labels, states)
+    return {"scp": scp, "mlf": os.path.join(outdir, "train.mlf"), "states": os.path.join(outdir, "states")}

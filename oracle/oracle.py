@@ -1,0 +1,147 @@
+"""ctypes wrapper around liboracle.so (oracle/tnet_oracle.c).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline
+leg, always as the checker.  The product package (nnet-asr_amd/tnet_amd) never imports it.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = None
+
+f32p = np.ctypeslib.ndpointer(np.float32, flags="C_CONTIGUOUS")
+i32p = np.ctypeslib.ndpointer(np.int32, flags="C_CONTIGUOUS")
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        path = os.path.join(_HERE, "liboracle.so")
+        if not os.path.exists(path):
+            raise RuntimeError(f"{path} missing: run `make -C oracle`")
+        L = C.CDLL(path)
+        L.orc_sgemm.argtypes = [C.c_char, C.c_char, C.c_int, C.c_int, C.c_int, C.c_float, f32p, C.c_int,
+                                f32p, C.c_int, C.c_float, f32p, C.c_int]
+        L.orc_sigmoid.argtypes = [f32p, f32p, C.c_long]
+        L.orc_diff_sigmoid.argtypes = [f32p, f32p, f32p, C.c_long]
+        L.orc_softmax.argtypes = [f32p, f32p, C.c_int, C.c_int]
+        L.orc_add_col_sum.argtypes = [C.c_float, f32p, C.c_int, C.c_int, C.c_float, f32p]
+        L.orc_xent_eval.argtypes = [f32p, i32p, C.c_int, C.c_int, C.c_void_p, C.POINTER(C.c_double),
+                                    C.POINTER(C.c_long)]
+        L.orc_epoch_schedule.argtypes = [i32p, C.c_int, C.c_int, C.c_int, C.c_long, C.c_int, i32p, C.c_long]
+        L.orc_epoch_schedule.restype = C.c_long
+        L.orc_mlp_step.argtypes = [C.c_int, i32p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, f32p, i32p,
+                                   C.c_int, C.c_float, C.c_float, C.c_float, C.c_int, C.c_int, f32p, f32p,
+                                   C.POINTER(C.c_double), C.POINTER(C.c_long)]
+        L.orc_mlp_forward.argtypes = [C.c_int, i32p, C.c_void_p, C.c_void_p, f32p, C.c_int, f32p]
+        _LIB = L
+    return _LIB
+
+
+def _ptrs(arrs):
+    return (C.c_void_p * len(arrs))(*[a.ctypes.data for a in arrs])
+
+
+def sgemm(ta, tb, A, B, alpha=1.0, beta=0.0, Cm=None):
+    A = np.ascontiguousarray(A, np.float32)
+    B = np.ascontiguousarray(B, np.float32)
+    M = A.shape[1] if ta == "T" else A.shape[0]
+    K = A.shape[0] if ta == "T" else A.shape[1]
+    N = B.shape[0] if tb == "T" else B.shape[1]
+    if Cm is None:
+        Cm = np.zeros((M, N), np.float32)
+    lib().orc_sgemm(ta.encode(), tb.encode(), M, N, K, alpha, A, A.shape[1], B, B.shape[1], beta, Cm, N)
+    return Cm
+
+
+def sigmoid(x):
+    x = np.ascontiguousarray(x, np.float32)
+    y = np.empty_like(x)
+    lib().orc_sigmoid(y, x, x.size)
+    return y
+
+
+def diff_sigmoid(e, y):
+    e = np.ascontiguousarray(e, np.float32)
+    y = np.ascontiguousarray(y, np.float32)
+    out = np.empty_like(e)
+    lib().orc_diff_sigmoid(out, e, y, e.size)
+    return out
+
+
+def softmax(x):
+    x = np.ascontiguousarray(x, np.float32)
+    y = np.empty_like(x)
+    lib().orc_softmax(y, x, x.shape[0], x.shape[1])
+    return y
+
+
+def add_col_sum(M, alpha=1.0, beta=0.0, v=None):
+    M = np.ascontiguousarray(M, np.float32)
+    if v is None:
+        v = np.zeros(M.shape[1], np.float32)
+    lib().orc_add_col_sum(alpha, M, M.shape[0], M.shape[1], beta, v)
+    return v
+
+
+def xent_eval(y, labels):
+    y = np.ascontiguousarray(y, np.float32)
+    labels = np.ascontiguousarray(labels, np.int32)
+    err = np.empty_like(y)
+    xe = C.c_double(0.0)
+    cor = C.c_long(0)
+    lib().orc_xent_eval(y, labels, y.shape[0], y.shape[1], err.ctypes.data, C.byref(xe), C.byref(cor))
+    return err, xe.value, cor.value
+
+
+def epoch_schedule(lens, cachesize, bunch, seed, randomize=True):
+    lens = np.ascontiguousarray(lens, np.int32)
+    cap = int(lens.sum()) // bunch + 1
+    out = np.zeros(cap * bunch, np.int32)
+    nb = lib().orc_epoch_schedule(lens, len(lens), cachesize, bunch, seed, int(randomize), out, cap)
+    return out[: nb * bunch].reshape(nb, bunch)
+
+
+class MLP:
+    """Oracle MLP state: weights W[l] [n_in x n_out], biases, momentum buffers."""
+
+    def __init__(self, Ws, bs):
+        self.W = [np.ascontiguousarray(w, np.float32).copy() for w in Ws]
+        self.b = [np.ascontiguousarray(x, np.float32).copy() for x in bs]
+        self.cW = [np.zeros_like(w) for w in self.W]
+        self.cb = [np.zeros_like(x) for x in self.b]
+        self.dims = np.array([self.W[0].shape[0]] + [w.shape[1] for w in self.W], np.int32)
+        self.xent = 0.0
+        self.correct = 0
+        self.frames = 0
+
+    @classmethod
+    def from_layers(cls, layers):
+        lin = [L for L in layers if L.tag == "<biasedlinearity>"]
+        return cls([L.W for L in lin], [L.b for L in lin])
+
+    def step(self, X, labels, lr, mmt=0.0, wc=0.0, graddivfrm=True, cpu_semantics=False):
+        X = np.ascontiguousarray(X, np.float32)
+        labels = np.ascontiguousarray(labels, np.int32)
+        B = X.shape[0]
+        Y = np.empty((B, self.dims[-1]), np.float32)
+        E = np.empty_like(Y)
+        xe = C.c_double(0.0)
+        cor = C.c_long(0)
+        lib().orc_mlp_step(len(self.W), self.dims, _ptrs(self.W), _ptrs(self.b), _ptrs(self.cW), _ptrs(self.cb),
+                           X, labels, B, lr, mmt, wc, int(graddivfrm), int(cpu_semantics), Y, E,
+                           C.byref(xe), C.byref(cor))
+        self.xent += xe.value
+        self.correct += cor.value
+        self.frames += B
+        return Y, E
+
+    def forward(self, X):
+        X = np.ascontiguousarray(X, np.float32)
+        Y = np.empty((X.shape[0], self.dims[-1]), np.float32)
+        lib().orc_mlp_forward(len(self.W), self.dims, _ptrs(self.W), _ptrs(self.b), X, X.shape[0], Y)
+        return Y

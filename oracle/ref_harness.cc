@@ -1,0 +1,135 @@
+// ref_harness.cc -- golden-vector generator for the parity tests (TEST INFRASTRUCTURE ONLY).
+//
+// Links the reference CPU TNetLib/KaldiLib objects (built by oracle/Makefile.ref from the
+// read-only sources under /root/reference/src) and drives them exactly the way the
+// reference's single-thread training platform does, dumping full-precision results:
+//
+//   step    : per-bunch SGD with TNet --THREADS=1 semantics, i.e. the Platform::Thread
+//             bunch loop (src/TNetLib/Platform.h:300-336): clone->Propagate,
+//             CrossEntropy::Evaluate, clone->Backpropagate (Gradient()), master
+//             AccuGradient/AccuBunchsize/Update(0,1)/ResetBunchsize.
+//   shuffle : the cache permutation produced by Cache::Init(seed)+AddData+Randomize
+//             (src/TNetLib/Cache.cc:23-192) -- lrand48 + libstdc++ random_shuffle.
+//
+// It is our own code; no reference source is copied.  Output is raw little-endian float32
+// / int32 files plus .nnet text written with 9 significant digits (exact float round trip).
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <iostream>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "Nnet.h"
+#include "ObjFun.h"
+#include "Cache.h"
+#include "Matrix.h"
+
+using namespace TNet;
+
+static std::vector<char> slurp(const std::string& path) {
+  std::ifstream f(path.c_str(), std::ios::binary);
+  if (!f.good()) { std::cerr << "cannot open " << path << "\n"; exit(2); }
+  return std::vector<char>((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
+}
+
+static void dump_matrix(const std::string& path, const Matrix<BaseFloat>& m) {
+  std::ofstream f(path.c_str(), std::ios::binary);
+  for (size_t r = 0; r < m.Rows(); r++)
+    for (size_t c = 0; c < m.Cols(); c++) {
+      float v = m(r, c);
+      f.write((const char*)&v, 4);
+    }
+}
+
+// step <nnet> <X.f32> <lab.i32> <nIn> <nClasses> <bunch> <nsteps> <lr> <wc> <outdir>
+static int cmd_step(int argc, char** argv) {
+  if (argc < 12) { std::cerr << "usage: step nnet X lab nIn nCls bunch nsteps lr wc outdir\n"; return 2; }
+  std::string nnet_path = argv[2], xpath = argv[3], lpath = argv[4];
+  int n_in = atoi(argv[5]), n_cls = atoi(argv[6]), bunch = atoi(argv[7]), nsteps = atoi(argv[8]);
+  float lr = (float)atof(argv[9]), wc = (float)atof(argv[10]);
+  std::string out = argv[11];
+
+  std::vector<char> xb = slurp(xpath), lb = slurp(lpath);
+  const float* X = (const float*)&xb[0];
+  const int* L = (const int*)&lb[0];
+  size_t nfr = xb.size() / 4 / n_in;
+  if ((size_t)bunch * nsteps > nfr) { std::cerr << "not enough frames\n"; return 2; }
+
+  Network nnet;
+  nnet.ReadNetwork(nnet_path.c_str());
+  nnet.SetLearnRate(lr);
+  nnet.SetWeightcost(wc);
+  Network* clone = nnet.Clone();
+  ObjectiveFunction* obj = ObjectiveFunction::Factory(ObjectiveFunction::CROSS_ENTROPY);
+
+  Matrix<BaseFloat> fea(bunch, n_in), lab(bunch, n_cls), outm, err;
+  for (int s = 0; s < nsteps; s++) {
+    lab.Zero();
+    for (int r = 0; r < bunch; r++) {
+      size_t fr = (size_t)s * bunch + r;
+      for (int c = 0; c < n_in; c++) fea(r, c) = X[fr * n_in + c];
+      if (L[fr] >= 0) lab(r, L[fr]) = 1.0f;   // -1 = unlabeled frame (all-zero target row)
+    }
+    clone->Propagate(fea, outm);
+    obj->Evaluate(outm, lab, &err);
+    clone->Backpropagate(err);
+    nnet.AccuGradient(*clone, 0, 1);
+    nnet.AccuBunchsize(*clone);
+    nnet.Update(0, 1);
+    nnet.ResetBunchsize();
+
+    std::ostringstream ys, es, ns;
+    ys << out << "/Y_" << s << ".f32";
+    es << out << "/E_" << s << ".f32";
+    ns << out << "/nnet_" << s << ".txt";
+    dump_matrix(ys.str(), outm);
+    dump_matrix(es.str(), err);
+    std::ofstream nf(ns.str().c_str());
+    nf.precision(9);
+    nnet.WriteNetwork(nf);
+  }
+  std::ofstream rep((out + "/report.txt").c_str());
+  rep.precision(17);
+  rep << obj->GetError() << " " << obj->GetFrames() << "\n" << obj->Report();
+  delete obj;
+  delete clone;
+  return 0;
+}
+
+// shuffle <seed> <n> <cachesize> <bunch> <out.i32> : emits the row order GetBunch returns
+static int cmd_shuffle(int argc, char** argv) {
+  if (argc < 7) { std::cerr << "usage: shuffle seed n cachesize bunch out\n"; return 2; }
+  long seed = atol(argv[2]);
+  int n = atoi(argv[3]), cachesize = atoi(argv[4]), bunch = atoi(argv[5]);
+  Cache cache;
+  cache.Init(cachesize, bunch, seed);
+  Matrix<BaseFloat> fea(n, 1), lab(n, 1);
+  for (int i = 0; i < n; i++) { fea(i, 0) = (float)i; lab(i, 0) = 1.0f; }
+  cache.AddData(fea, lab);
+  cache.Randomize();
+  std::ofstream f(argv[6], std::ios::binary);
+  Matrix<BaseFloat> f2, l2;
+  while (!cache.Empty()) {
+    cache.GetBunch(f2, l2);
+    for (size_t r = 0; r < f2.Rows(); r++) {
+      int v = (int)f2(r, 0);
+      f.write((const char*)&v, 4);
+    }
+  }
+  return 0;
+}
+
+int main(int argc, char** argv) try {
+  if (argc < 2) { std::cerr << "modes: step | shuffle\n"; return 2; }
+  std::string mode = argv[1];
+  if (mode == "step") return cmd_step(argc, argv);
+  if (mode == "shuffle") return cmd_shuffle(argc, argv);
+  std::cerr << "unknown mode\n";
+  return 2;
+} catch (std::exception& e) {
+  std::cerr << "exception: " << e.what() << "\n";
+  return 1;
+}
