@@ -1,0 +1,184 @@
+/*
+ * tnet_kernels.h -- C ABI of the MI355X (gfx950) device kernels of the TNet frame-batched
+ * forward / backward / SGD-update path.
+ *
+ * This is the drop-in replacement for the two device-side ABIs the reference CuBaseLib uses:
+ *   (1) the extern "C" cudaF_* kernel wrappers of src/CuBaseLib/cukernels.h:5-79 and
+ *       src/CuBaseLib/curandkernels.h:8-31, and
+ *   (2) the legacy cuBLAS calls cublasSgemm / cublasSgemv / cublasSger
+ *       (src/CuBaseLib/cumatrix.tcc:363,384, src/CuBaseLib/cumath.cc:105,237,334,358).
+ * plus the fused kernels the MI355X path is built from.
+ *
+ * Conventions (all functions):
+ *   - row-major matrices described by TnetMatrixDim {rows, cols, stride} (== MatrixDim,
+ *     cukernels.h:11-15); stride is in elements;
+ *   - raw device pointers, never owned, never freed here; no allocation inside except in the
+ *     documented workspaces the caller passes in;
+ *   - launch geometry is a kernel-internal detail (no dim3 in the ABI, unlike cukernels.h);
+ *   - every launch goes on the caller's stream (hipStream_t passed as void*; NULL = default);
+ *     no device synchronisation inside (the reference synchronised after every call,
+ *     cucommon.h:13-22);
+ *   - return 0 (TNET_OK) or a negative TNET_ERR_* status; the C++ layer maps a status to an
+ *     exception exactly like cuSafeCall (cucommon.h:13-22) minus the sync;
+ *   - thread-safe per stream.
+ */
+#ifndef TNET_KERNELS_H_
+#define TNET_KERNELS_H_
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct TnetMatrixDim_ {
+  int rows;
+  int cols;
+  int stride;
+} TnetMatrixDim;
+
+enum {
+  TNET_OK = 0,
+  TNET_ERR_ARG = -1,       /* bad dimension / stride / pointer alignment */
+  TNET_ERR_LAUNCH = -2,    /* hipGetLastError after launch */
+  TNET_ERR_RUNTIME = -3,   /* other HIP runtime failure */
+  TNET_ERR_UNSUPPORTED = -4
+};
+
+/* Returns a static string for a status code. */
+const char* tnet_status_str(int status);
+/* Build / device description ("gfx950 tnet_amd <version>"). */
+const char* tnet_version(void);
+
+/* ------------------------------------------------------------------------------------
+ * Element-wise matrix ops  (cukernels.h:21-31 -> cukernels.cu:11-141)
+ * ---------------------------------------------------------------------------------- */
+/* M[i,j] = v                                  -- cudaF_set_const (cukernels.cu:11-19) */
+int tnetF_set_const(float* mat, float value, TnetMatrixDim d, void* stream);
+/* M = log(M)                                  -- cudaF_apply_log (cukernels.cu:23-31) */
+int tnetF_apply_log(float* mat, TnetMatrixDim d, void* stream);
+/* M[mask==0] = 0                              -- cudaF_apply_mask (cukernels.cu:34-43) */
+int tnetF_apply_mask(float* mat, const float* mask, TnetMatrixDim dmat, TnetMatrixDim dmask, void* stream);
+/* soft threshold |x|<l1 -> 0, else x -+ l1    -- cudaF_apply_l1 (cukernels.cu:46-62) */
+int tnetF_apply_l1(float* mat, float l1, TnetMatrixDim d, void* stream);
+/* M[i,j] *= s[j]                              -- cudaF_scale_cols (cukernels.cu:65-73) */
+int tnetF_scale_cols(float* mat, const float* scale, TnetMatrixDim d, void* stream);
+/* M[i,j] *= s[i]                              -- cudaF_scale_rows (cukernels.cu:76-84) */
+int tnetF_scale_rows(float* mat, const float* scale, TnetMatrixDim d, void* stream);
+/* D = alpha*A + beta*D                        -- cudaF_add_scaled (cukernels.cu:87-95);
+ * A and D share dimensions d but may have different strides (strideA). */
+int tnetF_add_scaled(float alpha, const float* A, int strideA, float beta, float* dst, TnetMatrixDim d,
+                     void* stream);
+/* D[i,j] = alpha*row[j] + beta*D[i,j]         -- cudaF_add_scaled_row (cukernels.cu:98-117) */
+int tnetF_add_scaled_row(float alpha, const float* row, float beta, float* dst, TnetMatrixDim d, void* stream);
+/* M = M .* A                                  -- cudaF_mul_elem (cukernels.cu:120-128) */
+int tnetF_mul_elem(float* mat, const float* A, int strideA, TnetMatrixDim d, void* stream);
+/* M = log(max(M, FLT_MIN))                    -- cudaF_log_elem (cukernels.cu:131-141) */
+int tnetF_log_elem(float* mat, TnetMatrixDim d, void* stream);
+
+/* ------------------------------------------------------------------------------------
+ * Vector reductions  (cukernels.h:33-35)
+ * ---------------------------------------------------------------------------------- */
+/* v[j] = alpha * sum_i M[i,j] + beta * v[j]   -- cudaF_add_col_sum / _add_col_sum_reduce
+ * (cukernels.cu:147-187).  Deterministic: fixed-order partial sums in fp32, combined in fp64.
+ * `workspace` needs tnet_col_sum_workspace(d) bytes of device memory (or NULL to use an
+ * internal per-device buffer, not thread-safe). */
+long tnet_col_sum_workspace(TnetMatrixDim d);
+int tnetF_add_col_sum(float alpha, const float* mat, float beta, float* vec, TnetMatrixDim d, void* workspace,
+                      void* stream);
+
+/* ------------------------------------------------------------------------------------
+ * Activations / objective  (cukernels.h:38-41, 51-52)
+ * ---------------------------------------------------------------------------------- */
+/* y = 1/(1+exp(-x))                           -- cudaF_sigmoid (cukernels.cu:192-206) */
+int tnetF_sigmoid(float* y, const float* x, TnetMatrixDim d, void* stream);
+/* eout = y (1-y) e                            -- cudaF_diff_sigmoid (cukernels.cu:209-217) */
+int tnetF_diff_sigmoid(float* eout, const float* e, const float* y, TnetMatrixDim d, void* stream);
+/* row softmax, y = exp(x - max) / sum         -- cudaF_softmax / _softmax_reduce (cukernels.cu:220-343);
+ * one wavefront per row, any number of columns. */
+int tnetF_softmax(float* y, const float* x, TnetMatrixDim d, void* stream);
+/* match[i] = argmax(out[i,:]) == argmax(des[i,:]) (first max wins)
+ *                                             -- cudaF_check_class[_reduce] (cukernels.cu:396-483) */
+int tnetF_check_class(const float* out, const float* des, int* match, TnetMatrixDim d, void* stream);
+
+/* ------------------------------------------------------------------------------------
+ * Gathers / front-end transforms  (cukernels.h:43-45)
+ * ---------------------------------------------------------------------------------- */
+/* y[i,j] = x[i + off[j / in.cols], j % in.cols] with edge clamp  -- cudaF_expand (cukernels.cu:347-361) */
+int tnetF_expand(float* y, const float* x, const int* off, TnetMatrixDim dout, TnetMatrixDim din, void* stream);
+/* y[i,j] = x[i, copy_from[j]] (out of range -> +inf)            -- cudaF_rearrange (cukernels.cu:364-379) */
+int tnetF_rearrange(float* y, const float* x, const int* copy_from, TnetMatrixDim dout, TnetMatrixDim din,
+                    void* stream);
+/* y[i,:] = x[copy_from[i], :]                                    -- cudaF_randomize (cukernels.cu:382-393) */
+int tnetF_randomize(float* y, const float* x, const int* copy_from, TnetMatrixDim dout, TnetMatrixDim din,
+                    void* stream);
+/* labels_out[i] = labels_in[copy_from[i]]  (class-id twin of randomize for one-hot targets) */
+int tnet_gather_i32(int* out, const int* in, const int* copy_from, int n, void* stream);
+
+/* ------------------------------------------------------------------------------------
+ * GEMM (replaces cublasSgemm at cumatrix.tcc:336-370, row-major semantics)
+ *   C[m x n] = alpha * op(A) * op(B) + beta * C,  op(X) = X or X^T ('N' / 'T')
+ * fp32 in / fp32 accumulate on v_mfma_f32_32x32x2_f32 (exact f32 FMA chain per k).
+ * Requirements: lda/ldb/ldc multiples of 4 elements, pointers 16-byte aligned.
+ * ---------------------------------------------------------------------------------- */
+int tnet_sgemm(char transa, char transb, int m, int n, int k, float alpha, const float* A, int lda,
+               const float* B, int ldb, float beta, float* C, int ldc, void* stream);
+
+/* ------------------------------------------------------------------------------------
+ * Fused kernels of the MI355X SGD path (no reference counterpart: each replaces a chain of
+ * reference calls, cited per function).
+ * ---------------------------------------------------------------------------------- */
+/* Y = act(X W + b), act = 0 none | 1 sigmoid.  X [rows x n_in], W [n_in x n_out] (memory layout
+ * of CuBiasedLinearity::mLinearity), b [n_out].
+ * Replaces AddScaledRow + Gemm('N','N') + CuMath::Sigmoid (cuBiasedLinearity.cc:11-16,
+ * cuActivation.cc:11-14). */
+int tnet_affine_fwd(const float* X, TnetMatrixDim dX, const float* W, TnetMatrixDim dW, const float* b,
+                    float* Y, TnetMatrixDim dY, int act, void* stream);
+/* Eo = (E W^T) .* Ybelow (1 - Ybelow)  (dsig=1)  or  Eo = E W^T (dsig=0).
+ * Replaces Gemm('N','T') + CuMath::DiffSigmoid (cuBiasedLinearity.cc:21-25, cuActivation.cc:19-22). */
+int tnet_affine_bwd(const float* E, TnetMatrixDim dE, const float* W, TnetMatrixDim dW, const float* Ybelow,
+                    int strideYbelow, float* Eo, TnetMatrixDim dEo, int dsig, void* stream);
+/* Fused weight update of CuBiasedLinearity::Update (cuBiasedLinearity.cc:46-64):
+ *   G  = X^T E                       (X [rows x n_in], E [rows x n_out])
+ *   C  = G + mmt * corrW             (corrW may be NULL when mmt == 0; then C = G)
+ *   W  = W + scale * C ; W = W + l2 * W
+ *   corrW = C                        (if corrW != NULL)
+ * scale = -lr/N, l2 = -lr*wc*(gdf?1:rows) are computed by the caller. */
+int tnet_affine_update(const float* X, TnetMatrixDim dX, const float* E, TnetMatrixDim dE, float* W,
+                       TnetMatrixDim dW, float* corrW, int strideCorr, float scale, float mmt, float l2,
+                       void* stream);
+/* G = X^T E into a gradient buffer (data-parallel path: all-reduced before tnet_sgd_update). */
+int tnet_affine_grad(const float* X, TnetMatrixDim dX, const float* E, TnetMatrixDim dE, float* G,
+                     TnetMatrixDim dG, void* stream);
+/* Element-wise SGD of the same formula on flat arrays:  c = g + mmt*corr; p += scale*c; p += l2*p;
+ * corr = c (corr may be NULL when mmt == 0). */
+int tnet_sgd_update(float* p, const float* g, float* corr, long n, float scale, float mmt, float l2,
+                    void* stream);
+/* Bias update from the error matrix E (CuVector::AddColSum + AddScaled, cuBiasedLinearity.cc:56-59):
+ *   c = colsum(E) + mmt*corr_b ; b += scale * c ; corr_b = c   (corr_b may be NULL if mmt == 0)
+ * If grad_out != NULL the raw colsum is written there instead and b is not touched (DP path). */
+int tnet_bias_update(const float* E, TnetMatrixDim dE, float* b, float* corr_b, float* grad_out, float scale,
+                     float mmt, void* workspace, void* stream);
+/* Fused softmax + cross-entropy + error + accuracy for class-id targets
+ * (CuSoftmax::PropagateFnc + CuCrossEntropy::Evaluate, cuActivation.cc:28-31,
+ *  cuObjectiveFunction.cc:50-83; kernels _softmax, _add_scaled, _check_class, _log_elem,
+ *  _mul_elem, _add_col_sum):
+ *   y = softmax(Z row)          -> written to Y if Y != NULL
+ *   E = y - onehot(label)       (label < 0: all-zero target row)
+ *   stats[0] += -log(max(y[label], FLT_MIN)), stats[1] += #(argmax y == argmax target)
+ *   (stats: 2 doubles in device memory, accumulated with atomics; may be NULL).
+ * Z == NULL: Y already holds the network output (softmax not recomputed). */
+int tnet_softmax_xent(const float* Z, TnetMatrixDim dZ, const int* labels, float* Y, int strideY, float* E,
+                      int strideE, double* stats, void* stream);
+/* Same objective for dense desired matrices D (any soft targets; cuObjectiveFunction.cc:50-83):
+ * Y = softmax(Z) (if Z != NULL, else Y already holds the network output), E = Y - D, stats as above
+ * with xent = -sum D log(max(Y, FLT_MIN)). */
+int tnet_softmax_xent_dense(const float* Z, TnetMatrixDim dZ, const float* D, int strideD, float* Y,
+                            int strideY, float* E, int strideE, double* stats, void* stream);
+/* Mean-square-error objective (CuMeanSquareError::Evaluate, cuObjectiveFunction.cc:28-45):
+ * E = Y - D, stats[0] += sum E^2. */
+int tnet_mse(const float* Y, TnetMatrixDim dY, const float* D, int strideD, float* E, int strideE,
+             double* stats, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TNET_KERNELS_H_ */

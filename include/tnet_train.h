@@ -1,0 +1,114 @@
+/*
+ * tnet_train.h -- C ABI of the MI355X TNet training library (libtnet_amd.so), above the kernels.
+ *
+ * The reference exposes this layer as C++ classes only; these entry points are what an FFI
+ * (ctypes / cgo / JNI) binding of the CuComponent / CuNetwork / CuObjectiveFunction / CuCache /
+ * TNetCu-loop API binds to.  Each function names the reference interface it replaces.
+ * The C++ classes themselves (nnet-asr_amd/csrc/host/ headers) keep the reference names for C++ users.
+ *
+ * Conventions: opaque handles; device pointers are raw HIP device memory (see tnet_malloc);
+ * host pointers are plain arrays; all row-major with explicit leading dimensions (elements).
+ * Return 0 on success, a negative status on failure; tnet_last_error() gives the message of the
+ * last failure on the calling thread (the reference throws MyException, src/KaldiLib/Error.h).
+ */
+#ifndef TNET_TRAIN_H_
+#define TNET_TRAIN_H_
+
+#include <stddef.h>
+
+#include "tnet_kernels.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct TnetNetwork TnetNetwork;
+typedef struct TnetObjective TnetObjective;
+typedef struct TnetTrainer TnetTrainer;
+typedef struct TnetComm TnetComm;
+
+const char* tnet_last_error(void);
+
+/* ---- runtime (CuDevice, src/CuBaseLib/cudevice.h:15-73) ------------------------------ */
+int tnet_device_count(int* n);
+int tnet_select_gpu(int gpu_id);               /* CuDevice::SelectGPU (cudevice.cc:84-101) */
+int tnet_synchronize(void);                    /* drain the library stream */
+void* tnet_stream(void);                       /* the library's hipStream_t */
+int tnet_malloc(void** p, size_t bytes);
+int tnet_free(void* p);
+int tnet_memcpy_h2d(void* dst, const void* src, size_t bytes);
+int tnet_memcpy_d2h(void* dst, const void* src, size_t bytes);
+int tnet_memcpy_d2d(void* dst, const void* src, size_t bytes);
+int tnet_memset(void* dst, int value, size_t bytes);
+int tnet_set_profile(int on);                  /* CuDevice::Verbose + AccuProfile map */
+int tnet_profile_report(char* buf, int cap);
+/* Device-side timing of the enqueued work: start/stop return elapsed ms between two marks. */
+int tnet_timer_start(void);
+int tnet_timer_stop(float* ms);
+
+/* ---- network (CuNetwork, src/CuTNetLib/cuNetwork.h:22-194) ---------------------------- */
+TnetNetwork* tnet_net_read(const char* path);  /* ReadNetwork(const char*)   (cuNetwork.cc:27-37) */
+TnetNetwork* tnet_net_read_text(const char* text); /* ReadNetwork(istream&)  (cuNetwork.cc:53-61) */
+int tnet_net_write(TnetNetwork* net, const char* path); /* WriteNetwork       (cuNetwork.cc:40-50) */
+int tnet_net_free(TnetNetwork* net);
+int tnet_net_num_components(TnetNetwork* net);  /* Layers() */
+/* Layer(i): tag (GetName), inputs/outputs (GetNInputs/GetNOutputs) */
+int tnet_net_component(TnetNetwork* net, int i, char* tag, int cap, int* n_in, int* n_out);
+/* <biasedlinearity> parameters in memory layout: W [n_in x n_out] row-major, b [n_out] (host) */
+int tnet_net_get_params(TnetNetwork* net, int i, float* W, float* b);
+int tnet_net_set_params(TnetNetwork* net, int i, const float* W, const float* b);
+int tnet_net_set_learn_rate(TnetNetwork* net, float lr, const char* factors); /* SetLearnRate (cuNetwork.cc:80-134) */
+int tnet_net_set_momentum(TnetNetwork* net, float mmt);                       /* SetMomentum */
+int tnet_net_set_weightcost(TnetNetwork* net, float wc);                      /* SetWeightcost */
+int tnet_net_set_grad_div_frm(TnetNetwork* net, int div);                     /* SetGradDivFrm */
+/* Propagate (cuNetwork.h:137-165): X [rows x n_in] -> Y [rows x n_out], device pointers */
+int tnet_net_propagate(TnetNetwork* net, const float* dX, int rows, int ldx, float* dY, int ldy);
+/* Backpropagate (cuNetwork.h:170-194): global error [rows x n_out] of the LAST Propagate */
+int tnet_net_backpropagate(TnetNetwork* net, const float* dE, int rows, int lde);
+/* One fused SGD step (MI355X path): Propagate + CuCrossEntropy::Evaluate + Backpropagate with
+ * class-id targets (label < 0 = unlabeled frame); train = 0 -> forward + objective only */
+int tnet_net_train_bunch(TnetNetwork* net, TnetObjective* obj, const float* dX, int rows, int ldx,
+                         const int* dLabels, int train);
+/* Keep the softmax output of tnet_net_train_bunch readable via tnet_net_output (extra write) */
+int tnet_net_keep_output(TnetNetwork* net, int keep);
+/* output of component i (GetOutput) copied to host [rows x n_out] */
+int tnet_net_output(TnetNetwork* net, int i, float* host, int ld);
+
+/* ---- objective (CuObjectiveFunction, src/CuTNetLib/cuObjectiveFunction.h:20-157) ----- */
+TnetObjective* tnet_obj_create(int type);      /* 0 = CROSS_ENTROPY (xent), 1 = MEAN_SQUARE_ERROR (mse) */
+int tnet_obj_free(TnetObjective* obj);
+/* Evaluate(out, desired, err) with a dense desired matrix (cuObjectiveFunction.cc:28-83) */
+int tnet_obj_evaluate(TnetObjective* obj, const float* dOut, int rows, int cols, int ldo, const float* dDes,
+                      int ldd, float* dErr, int lde);
+/* class-id targets */
+int tnet_obj_evaluate_labels(TnetObjective* obj, const float* dOut, int rows, int cols, int ldo,
+                             const int* dLabels, float* dErr, int lde);
+/* GetError / GetFrames / correct count */
+int tnet_obj_stats(TnetObjective* obj, double* error, long* frames, double* correct);
+/* Report() line, e.g. "Xent:187469 frames:54720 err/frm:3.42598 correct[23.2365%]\n" */
+int tnet_obj_report(TnetObjective* obj, char* buf, int cap);
+int tnet_obj_reset(TnetObjective* obj);
+
+/* ---- trainer: the TNetCu SGD loop (src/TNetCu.cc:375-442) + CuCache (cuCache.h:12-70) ----- */
+TnetTrainer* tnet_trainer_create(TnetNetwork* net, TnetObjective* obj, int bunchsize, int cachesize, long seed,
+                                 int randomize, int crossval);
+int tnet_trainer_free(TnetTrainer* t);
+/* one utterance in scp order: features [rows x cols] (ld), class ids [rows] (host memory) */
+int tnet_trainer_add_utterance(TnetTrainer* t, const float* feats, int rows, int cols, int ld, const int* labels);
+int tnet_trainer_finish(TnetTrainer* t);       /* EndOfList */
+long tnet_trainer_steps(TnetTrainer* t);
+int tnet_trainer_replay(TnetTrainer* t, long nsteps); /* benchmark: more steps over the resident cache */
+int tnet_trainer_set_comm(TnetTrainer* t, TnetComm* comm);
+int tnet_trainer_trace(TnetTrainer* t, int trace);
+
+/* ---- data parallel (no reference counterpart: Platform.h:143-391 is the CPU analogue) ---- */
+int tnet_comm_unique_id(char out[128]);        /* rank 0 creates, the launcher broadcasts it */
+TnetComm* tnet_comm_create(int rank, int world, const char id[128]);
+int tnet_comm_free(TnetComm* comm);
+int tnet_comm_allreduce_host(TnetComm* comm, double* v, int n);
+int tnet_comm_allreduce_device(TnetComm* comm, float* dbuf, long n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TNET_TRAIN_H_ */

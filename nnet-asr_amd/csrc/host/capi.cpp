@@ -1,0 +1,376 @@
+// capi.cpp -- extern "C" entry points of include/tnet_train.h over the C++ classes.
+#include <cstring>
+#include <fstream>
+#include <memory>
+#include <sstream>
+#include <string>
+
+#include "tnet_train.h"
+#include "trainer.h"
+
+using namespace TNet;
+
+static thread_local std::string g_last_error;
+
+#define TRY_BEGIN try {
+#define TRY_END                              \
+  }                                          \
+  catch (std::exception & e) {               \
+    g_last_error = e.what();                 \
+    return TNET_ERR_RUNTIME;                 \
+  }                                          \
+  return TNET_OK;
+#define TRY_END_PTR                          \
+  catch (std::exception & e) {               \
+    g_last_error = e.what();                 \
+    return nullptr;                          \
+  }
+
+struct TnetNetwork {
+  CuNetwork net;
+  CuMatrix<BaseFloat> in_view, out, err_view, tmp_view;
+  CuVector<int> lab_view;
+};
+struct TnetObjective {
+  std::unique_ptr<CuObjectiveFunction> obj;
+  CuMatrix<BaseFloat> out_view, des_view, err;
+  CuVector<int> lab_view;
+};
+struct TnetTrainer {
+  std::unique_ptr<CuTrainer> t;
+};
+struct TnetComm {
+  std::unique_ptr<RcclExchange> ex;
+};
+
+extern "C" {
+
+const char* tnet_status_str(int st) {
+  switch (st) {
+    case TNET_OK: return "ok";
+    case TNET_ERR_ARG: return "invalid argument";
+    case TNET_ERR_LAUNCH: return "kernel launch failed";
+    case TNET_ERR_RUNTIME: return "runtime error";
+    case TNET_ERR_UNSUPPORTED: return "unsupported";
+    default: return "unknown status";
+  }
+}
+
+const char* tnet_version(void) { return "tnet_amd 0.1 gfx950 (fp32 MFMA 32x32x2)"; }
+
+const char* tnet_last_error(void) { return g_last_error.c_str(); }
+
+// ---------------------------------------------------------------------------------- runtime
+int tnet_device_count(int* n) {
+  hipError_t e = hipGetDeviceCount(n);
+  if (e != hipSuccess) {
+    *n = 0;
+    g_last_error = hipGetErrorString(e);
+    return TNET_ERR_RUNTIME;
+  }
+  return TNET_OK;
+}
+int tnet_select_gpu(int id) {
+  TRY_BEGIN CuDevice::Instantiate().SelectGPU(id);
+  TRY_END
+}
+int tnet_synchronize(void) {
+  TRY_BEGIN CuDevice::Instantiate().Synchronize();
+  TRY_END
+}
+void* tnet_stream(void) {
+  try {
+    return (void*)CuDevice::Instantiate().Stream();
+  } catch (std::exception& e) {
+    g_last_error = e.what();
+    return nullptr;
+  }
+}
+int tnet_malloc(void** p, size_t bytes) {
+  TRY_BEGIN CuDevice::Instantiate();
+  TNET_HIP_CALL(hipMalloc(p, bytes));
+  TRY_END
+}
+int tnet_free(void* p) {
+  TRY_BEGIN TNET_HIP_CALL(hipFree(p));
+  TRY_END
+}
+int tnet_memcpy_h2d(void* dst, const void* src, size_t bytes) {
+  TRY_BEGIN hipStream_t s = CuDevice::Instantiate().Stream();
+  TNET_HIP_CALL(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s));
+  TNET_HIP_CALL(hipStreamSynchronize(s));
+  TRY_END
+}
+int tnet_memcpy_d2h(void* dst, const void* src, size_t bytes) {
+  TRY_BEGIN hipStream_t s = CuDevice::Instantiate().Stream();
+  TNET_HIP_CALL(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, s));
+  TNET_HIP_CALL(hipStreamSynchronize(s));
+  TRY_END
+}
+int tnet_memcpy_d2d(void* dst, const void* src, size_t bytes) {
+  TRY_BEGIN TNET_HIP_CALL(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, CuDevice::Instantiate().Stream()));
+  TRY_END
+}
+int tnet_memset(void* dst, int value, size_t bytes) {
+  TRY_BEGIN TNET_HIP_CALL(hipMemsetAsync(dst, value, bytes, CuDevice::Instantiate().Stream()));
+  TRY_END
+}
+int tnet_set_profile(int on) {
+  TRY_BEGIN CuDevice::Instantiate().Profile(on != 0);
+  TRY_END
+}
+int tnet_profile_report(char* buf, int cap) {
+  TRY_BEGIN std::ostringstream os;
+  CuDevice::Instantiate().PrintProfile(os);
+  std::string s = os.str();
+  if (cap > 0) {
+    std::strncpy(buf, s.c_str(), (size_t)cap - 1);
+    buf[cap - 1] = 0;
+  }
+  TRY_END
+}
+
+static hipEvent_t g_t0 = nullptr, g_t1 = nullptr;
+int tnet_timer_start(void) {
+  TRY_BEGIN if (!g_t0) {
+    TNET_HIP_CALL(hipEventCreate(&g_t0));
+    TNET_HIP_CALL(hipEventCreate(&g_t1));
+  }
+  TNET_HIP_CALL(hipEventRecord(g_t0, CuDevice::Instantiate().Stream()));
+  TRY_END
+}
+int tnet_timer_stop(float* ms) {
+  TRY_BEGIN TNET_HIP_CALL(hipEventRecord(g_t1, CuDevice::Instantiate().Stream()));
+  TNET_HIP_CALL(hipEventSynchronize(g_t1));
+  TNET_HIP_CALL(hipEventElapsedTime(ms, g_t0, g_t1));
+  TRY_END
+}
+
+// ---------------------------------------------------------------------------------- network
+TnetNetwork* tnet_net_read(const char* path) {
+  try {
+    std::unique_ptr<TnetNetwork> h(new TnetNetwork);
+    h->net.ReadNetwork(path);
+    return h.release();
+  }
+  TRY_END_PTR
+}
+TnetNetwork* tnet_net_read_text(const char* text) {
+  try {
+    std::unique_ptr<TnetNetwork> h(new TnetNetwork);
+    std::istringstream is(text);
+    h->net.ReadNetwork(is);
+    return h.release();
+  }
+  TRY_END_PTR
+}
+int tnet_net_write(TnetNetwork* h, const char* path) {
+  TRY_BEGIN h->net.WriteNetwork(path);
+  TRY_END
+}
+int tnet_net_free(TnetNetwork* h) {
+  TRY_BEGIN delete h;
+  TRY_END
+}
+int tnet_net_num_components(TnetNetwork* h) { return h ? h->net.Layers() : TNET_ERR_ARG; }
+int tnet_net_component(TnetNetwork* h, int i, char* tag, int cap, int* n_in, int* n_out) {
+  TRY_BEGIN if (i < 0 || i >= h->net.Layers()) Error("component index out of range");
+  CuComponent& c = h->net.Layer(i);
+  if (tag && cap > 0) {
+    std::strncpy(tag, c.GetName(), (size_t)cap - 1);
+    tag[cap - 1] = 0;
+  }
+  if (n_in) *n_in = (int)c.GetNInputs();
+  if (n_out) *n_out = (int)c.GetNOutputs();
+  TRY_END
+}
+static CuBiasedLinearity& linear(TnetNetwork* h, int i) {
+  if (i < 0 || i >= h->net.Layers()) Error("component index out of range");
+  auto* p = dynamic_cast<CuBiasedLinearity*>(&h->net.Layer(i));
+  if (!p) Error("component is not <biasedlinearity>");
+  return *p;
+}
+int tnet_net_get_params(TnetNetwork* h, int i, float* W, float* b) {
+  TRY_BEGIN CuBiasedLinearity& L = linear(h, i);
+  if (W) L.Linearity().CopyToHost(W, L.Linearity().Cols());
+  if (b) L.Bias().CopyToHost(b);
+  TRY_END
+}
+int tnet_net_set_params(TnetNetwork* h, int i, const float* W, const float* b) {
+  TRY_BEGIN CuBiasedLinearity& L = linear(h, i);
+  if (W) {
+    CuMatrix<BaseFloat>& M = L.Linearity();
+    TNET_HIP_CALL(hipMemcpy2DAsync(M.pCUData(), M.Stride() * 4, W, M.Cols() * 4, M.Cols() * 4, M.Rows(),
+                                   hipMemcpyHostToDevice, CuDevice::Instantiate().Stream()));
+  }
+  if (b) TNET_HIP_CALL(hipMemcpyAsync(L.Bias().pCUData(), b, L.Bias().Dim() * 4, hipMemcpyHostToDevice,
+                                      CuDevice::Instantiate().Stream()));
+  CuDevice::Instantiate().Synchronize();
+  TRY_END
+}
+int tnet_net_set_learn_rate(TnetNetwork* h, float lr, const char* factors) {
+  TRY_BEGIN h->net.SetLearnRate(lr, factors);
+  TRY_END
+}
+int tnet_net_set_momentum(TnetNetwork* h, float mmt) {
+  TRY_BEGIN h->net.SetMomentum(mmt);
+  TRY_END
+}
+int tnet_net_set_weightcost(TnetNetwork* h, float wc) {
+  TRY_BEGIN h->net.SetWeightcost(wc);
+  TRY_END
+}
+int tnet_net_set_grad_div_frm(TnetNetwork* h, int div) {
+  TRY_BEGIN h->net.SetGradDivFrm(div != 0);
+  TRY_END
+}
+int tnet_net_propagate(TnetNetwork* h, const float* dX, int rows, int ldx, float* dY, int ldy) {
+  TRY_BEGIN CuMatrix<BaseFloat>::MakeView(h->in_view, const_cast<float*>(dX), rows, h->net.GetNInputs(), ldx);
+  h->net.Propagate(h->in_view, h->out);
+  if (dY)
+    TNET_HIP_CALL(hipMemcpy2DAsync(dY, (size_t)ldy * 4, h->out.pCUData(), h->out.Stride() * 4, h->out.Cols() * 4,
+                                   h->out.Rows(), hipMemcpyDeviceToDevice, CuDevice::Instantiate().Stream()));
+  TRY_END
+}
+int tnet_net_backpropagate(TnetNetwork* h, const float* dE, int rows, int lde) {
+  TRY_BEGIN CuMatrix<BaseFloat>::MakeView(h->err_view, const_cast<float*>(dE), rows, h->net.GetNOutputs(), lde);
+  h->net.Backpropagate(h->err_view);
+  TRY_END
+}
+int tnet_net_train_bunch(TnetNetwork* h, TnetObjective* o, const float* dX, int rows, int ldx, const int* dLabels,
+                         int train) {
+  TRY_BEGIN CuMatrix<BaseFloat>::MakeView(h->in_view, const_cast<float*>(dX), rows, h->net.GetNInputs(), ldx);
+  CuVector<int>::MakeView(h->lab_view, const_cast<int*>(dLabels), rows);
+  h->net.TrainBunch(h->in_view, h->lab_view, *o->obj, train != 0);
+  TRY_END
+}
+int tnet_net_keep_output(TnetNetwork* h, int keep) {
+  TRY_BEGIN h->net.KeepOutput(keep != 0);
+  TRY_END
+}
+int tnet_net_output(TnetNetwork* h, int i, float* host, int ld) {
+  TRY_BEGIN if (i < 0 || i >= h->net.Layers()) Error("component index out of range");
+  h->net.Layer(i).GetOutput().CopyToHost(host, (size_t)ld);
+  TRY_END
+}
+
+// -------------------------------------------------------------------------------- objective
+TnetObjective* tnet_obj_create(int type) {
+  try {
+    std::unique_ptr<TnetObjective> h(new TnetObjective);
+    h->obj.reset(CuObjectiveFunction::Factory(type == 1 ? CuObjectiveFunction::MEAN_SQUARE_ERROR
+                                                        : CuObjectiveFunction::CROSS_ENTROPY));
+    return h.release();
+  }
+  TRY_END_PTR
+}
+int tnet_obj_free(TnetObjective* o) {
+  TRY_BEGIN delete o;
+  TRY_END
+}
+int tnet_obj_evaluate(TnetObjective* o, const float* dOut, int rows, int cols, int ldo, const float* dDes, int ldd,
+                      float* dErr, int lde) {
+  TRY_BEGIN CuMatrix<BaseFloat>::MakeView(o->out_view, const_cast<float*>(dOut), rows, cols, ldo);
+  CuMatrix<BaseFloat>::MakeView(o->des_view, const_cast<float*>(dDes), rows, cols, ldd);
+  CuMatrix<BaseFloat> err;
+  CuMatrix<BaseFloat>::MakeView(err, dErr, rows, cols, lde);
+  o->obj->Evaluate(o->out_view, o->des_view, err);
+  TRY_END
+}
+int tnet_obj_evaluate_labels(TnetObjective* o, const float* dOut, int rows, int cols, int ldo, const int* dLabels,
+                             float* dErr, int lde) {
+  TRY_BEGIN CuMatrix<BaseFloat>::MakeView(o->out_view, const_cast<float*>(dOut), rows, cols, ldo);
+  CuVector<int>::MakeView(o->lab_view, const_cast<int*>(dLabels), rows);
+  CuMatrix<BaseFloat> err;
+  CuMatrix<BaseFloat>::MakeView(err, dErr, rows, cols, lde);
+  o->obj->EvaluateLabels(o->out_view, o->lab_view, err);
+  TRY_END
+}
+int tnet_obj_stats(TnetObjective* o, double* error, long* frames, double* correct) {
+  TRY_BEGIN if (error) *error = o->obj->GetError();
+  if (correct) *correct = o->obj->GetCorrect();
+  if (frames) *frames = (long)o->obj->GetFrames();
+  TRY_END
+}
+int tnet_obj_report(TnetObjective* o, char* buf, int cap) {
+  TRY_BEGIN std::string s = o->obj->Report();
+  if (cap > 0) {
+    std::strncpy(buf, s.c_str(), (size_t)cap - 1);
+    buf[cap - 1] = 0;
+  }
+  TRY_END
+}
+int tnet_obj_reset(TnetObjective* o) {
+  TRY_BEGIN o->obj->Reset();
+  TRY_END
+}
+
+// ---------------------------------------------------------------------------------- trainer
+TnetTrainer* tnet_trainer_create(TnetNetwork* net, TnetObjective* obj, int bunchsize, int cachesize, long seed,
+                                 int randomize, int crossval) {
+  try {
+    TrainerOptions opt;
+    opt.bunchsize = (size_t)bunchsize;
+    opt.cachesize = (size_t)cachesize;
+    opt.seed = seed;
+    opt.randomize = randomize != 0;
+    opt.crossval = crossval != 0;
+    std::unique_ptr<TnetTrainer> h(new TnetTrainer);
+    h->t.reset(new CuTrainer(&net->net, obj->obj.get(), opt));
+    return h.release();
+  }
+  TRY_END_PTR
+}
+int tnet_trainer_free(TnetTrainer* t) {
+  TRY_BEGIN delete t;
+  TRY_END
+}
+int tnet_trainer_add_utterance(TnetTrainer* t, const float* feats, int rows, int cols, int ld, const int* labels) {
+  TRY_BEGIN t->t->AddUtterance(feats, (size_t)rows, (size_t)cols, (size_t)ld, labels);
+  TRY_END
+}
+int tnet_trainer_finish(TnetTrainer* t) {
+  TRY_BEGIN t->t->Finish();
+  TRY_END
+}
+long tnet_trainer_steps(TnetTrainer* t) { return t ? t->t->Steps() : -1; }
+int tnet_trainer_replay(TnetTrainer* t, long n) {
+  TRY_BEGIN t->t->Replay(n);
+  TRY_END
+}
+int tnet_trainer_set_comm(TnetTrainer* t, TnetComm* c) {
+  TRY_BEGIN t->t->SetExchange(c ? c->ex.get() : nullptr);
+  TRY_END
+}
+int tnet_trainer_trace(TnetTrainer* t, int trace) {
+  TRY_BEGIN t->t->Cache().Trace(trace);
+  TRY_END
+}
+
+// -------------------------------------------------------------------------------------- DP
+int tnet_comm_unique_id(char out[128]) {
+  TRY_BEGIN RcclExchange::UniqueId(out);
+  TRY_END
+}
+TnetComm* tnet_comm_create(int rank, int world, const char id[128]) {
+  try {
+    std::unique_ptr<TnetComm> h(new TnetComm);
+    h->ex.reset(new RcclExchange(rank, world, id));
+    return h.release();
+  }
+  TRY_END_PTR
+}
+int tnet_comm_free(TnetComm* c) {
+  TRY_BEGIN delete c;
+  TRY_END
+}
+int tnet_comm_allreduce_host(TnetComm* c, double* v, int n) {
+  TRY_BEGIN c->ex->AllReduceHost(v, n);
+  TRY_END
+}
+int tnet_comm_allreduce_device(TnetComm* c, float* dbuf, long n) {
+  TRY_BEGIN c->ex->AllReduceDevice(dbuf, (size_t)n);
+  TRY_END
+}
+
+}  // extern "C"

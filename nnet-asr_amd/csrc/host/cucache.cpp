@@ -1,0 +1,229 @@
+// cucache.cpp -- see cucache.h.  State machine follows src/CuTNetLib/cuCache.cc:22-200.
+#include "cucache.h"
+
+#include <numeric>
+
+namespace TNet {
+
+Rng48& GlobalRng() {
+  static Rng48 rng(0);
+  return rng;
+}
+void SeedRandom(long seed) { GlobalRng().Seed(seed); }
+
+#define S ((void*)CuDevice::Instantiate().Stream())
+
+CuCache::CuCache() {}
+CuCache::~CuCache() {}
+
+void CuCache::Init(size_t cachesize, size_t bunchsize) {
+  if (bunchsize == 0 || (cachesize % bunchsize) != 0) Error("Non divisible cachesize by bunchsize");
+  mCachesize = cachesize;
+  mBunchsize = bunchsize;
+  mState = EMPTY;
+  mIntakePos = 0;
+  mExhaustPos = 0;
+  mRandomized = false;
+}
+
+void CuCache::CheckMode(Mode m) {
+  if (mMode == UNSET) mMode = m;
+  if (mMode != m) Error("CuCache: mixing dense targets and class-id targets");
+}
+
+void CuCache::WarnLong(size_t rows) {
+  if (rows > mCachesize / 2) {
+    std::ostringstream os;
+    os << "Too long segment and small feature cache!  cachesize: " << mCachesize << " segmentsize: " << rows;
+    Warning(os.str());
+  }
+}
+
+void CuCache::Alloc(size_t cols, size_t tcols) {
+  if (mFeatures.Rows() != mCachesize || mFeatures.Cols() != cols) mFeatures.Init(mCachesize, cols);
+  if (mMode == DENSE) {
+    if (mDesired.Rows() != mCachesize || mDesired.Cols() != tcols) mDesired.Init(mCachesize, tcols);
+  } else {
+    mLabels.Init(mCachesize);
+  }
+}
+
+void CuCache::BeginIntake() {
+  if (mState != EMPTY) return;
+  if (mTrace & 3) std::cout << "/" << std::flush;
+  mState = INTAKE;
+  mIntakePos = 0;
+  size_t leftover = mLeftoverRows;
+  if (leftover > mCachesize) {
+    std::ostringstream os;
+    os << "Too small feature cache: " << mCachesize << ", truncating: " << leftover - mCachesize
+       << " frames from previous segment leftover";
+    Warning(os.str());
+    leftover = mCachesize;
+  }
+  if (leftover > 0) {
+    mFeatures.CopyRows(leftover, 0, mFeaturesLeftover, 0);
+    if (mMode == DENSE) {
+      mDesired.CopyRows(leftover, 0, mDesiredLeftover, 0);
+    } else {
+      TNET_HIP_CALL(hipMemcpyAsync(mLabels.pCUData(), mLabelsLeftover.pCUData(), leftover * sizeof(int),
+                                   hipMemcpyDeviceToDevice, CuDevice::Instantiate().Stream()));
+    }
+    mFeaturesLeftover.Destroy();
+    mDesiredLeftover.Destroy();
+    mLabelsLeftover.Destroy();
+    mIntakePos += leftover;
+  }
+  mLeftoverRows = 0;
+}
+
+void CuCache::AddData(const CuMatrix<BaseFloat>& rFeatures, const CuMatrix<BaseFloat>& rDesired) {
+  if (rFeatures.Rows() != rDesired.Rows()) Error("CuCache::AddData: rows of features != rows of targets");
+  CheckMode(DENSE);
+  Alloc(rFeatures.Cols(), rDesired.Cols());
+  WarnLong(rFeatures.Rows());
+  BeginIntake();
+  if (mState != INTAKE) Error("CuCache::AddData: cache not in INTAKE state");
+  if (mTrace & 2) std::cout << "F" << std::flush;
+  const size_t space = mCachesize - mIntakePos, len = rFeatures.Rows();
+  const size_t fill = space < len ? space : len, leftover = len - fill;
+  mFeatures.CopyRows(fill, 0, rFeatures, mIntakePos);
+  mDesired.CopyRows(fill, 0, rDesired, mIntakePos);
+  if (leftover > 0) {
+    mFeaturesLeftover.Init(leftover, mFeatures.Cols());
+    mDesiredLeftover.Init(leftover, mDesired.Cols());
+    mFeaturesLeftover.CopyRows(leftover, fill, rFeatures, 0);
+    mDesiredLeftover.CopyRows(leftover, fill, rDesired, 0);
+    mLeftoverRows = leftover;
+  }
+  mIntakePos += fill;
+  if (mIntakePos == mCachesize) {
+    if (mTrace & 3) std::cout << "\\" << std::flush;
+    mState = FULL;
+  }
+}
+
+void CuCache::AddDataLabels(const CuMatrix<BaseFloat>& rFeatures, const CuVector<int>& rLabels) {
+  if (rFeatures.Rows() != rLabels.Dim()) Error("CuCache::AddDataLabels: rows of features != number of labels");
+  CheckMode(LABELS);
+  Alloc(rFeatures.Cols(), 0);
+  WarnLong(rFeatures.Rows());
+  BeginIntake();
+  if (mState != INTAKE) Error("CuCache::AddDataLabels: cache not in INTAKE state");
+  const size_t space = mCachesize - mIntakePos, len = rFeatures.Rows();
+  const size_t fill = space < len ? space : len, leftover = len - fill;
+  hipStream_t st = CuDevice::Instantiate().Stream();
+  mFeatures.CopyRows(fill, 0, rFeatures, mIntakePos);
+  TNET_HIP_CALL(hipMemcpyAsync(mLabels.pCUData() + mIntakePos, rLabels.pCUData(), fill * sizeof(int),
+                               hipMemcpyDeviceToDevice, st));
+  if (leftover > 0) {
+    mFeaturesLeftover.Init(leftover, mFeatures.Cols());
+    mFeaturesLeftover.CopyRows(leftover, fill, rFeatures, 0);
+    mLabelsLeftover.Init(leftover);
+    TNET_HIP_CALL(hipMemcpyAsync(mLabelsLeftover.pCUData(), rLabels.pCUData() + fill, leftover * sizeof(int),
+                                 hipMemcpyDeviceToDevice, st));
+    mLeftoverRows = leftover;
+  }
+  mIntakePos += fill;
+  if (mIntakePos == mCachesize) mState = FULL;
+}
+
+void CuCache::AddDataHost(const float* feats, size_t rows, size_t cols, size_t ld, const int* labels) {
+  CheckMode(LABELS);
+  Alloc(cols, 0);
+  WarnLong(rows);
+  BeginIntake();
+  if (mState != INTAKE) Error("CuCache::AddDataHost: cache not in INTAKE state");
+  const size_t space = mCachesize - mIntakePos;
+  const size_t fill = space < rows ? space : rows, leftover = rows - fill;
+  hipStream_t st = CuDevice::Instantiate().Stream();
+  if (fill) {
+    TNET_HIP_CALL(hipMemcpy2DAsync(mFeatures.pCURowData(mIntakePos), mFeatures.Stride() * sizeof(float), feats,
+                                   ld * sizeof(float), cols * sizeof(float), fill, hipMemcpyHostToDevice, st));
+    TNET_HIP_CALL(hipMemcpyAsync(mLabels.pCUData() + mIntakePos, labels, fill * sizeof(int), hipMemcpyHostToDevice, st));
+  }
+  if (leftover > 0) {
+    mFeaturesLeftover.Init(leftover, cols);
+    TNET_HIP_CALL(hipMemcpy2DAsync(mFeaturesLeftover.pCUData(), mFeaturesLeftover.Stride() * sizeof(float),
+                                   feats + fill * ld, ld * sizeof(float), cols * sizeof(float), leftover,
+                                   hipMemcpyHostToDevice, st));
+    mLabelsLeftover.Init(leftover);
+    TNET_HIP_CALL(hipMemcpyAsync(mLabelsLeftover.pCUData(), labels + fill, leftover * sizeof(int),
+                                 hipMemcpyHostToDevice, st));
+    mLeftoverRows = leftover;
+  }
+  TNET_HIP_CALL(hipStreamSynchronize(st));  // caller's host buffers may be reused
+  mIntakePos += fill;
+  if (mIntakePos == mCachesize) mState = FULL;
+}
+
+void CuCache::Randomize() {
+  if (!(mState == FULL || mState == INTAKE)) Error("CuCache::Randomize: cache not filled");
+  if (mTrace & 3) std::cout << "R" << std::flush;
+  mPermHost.resize(mIntakePos);
+  std::iota(mPermHost.begin(), mPermHost.end(), 0);
+  Rng48& rng = mRng ? *mRng : GlobalRng();
+  rng.RandomShuffle(mPermHost.data(), mIntakePos);
+  mPerm.CopyFromHost(mPermHost.data(), mIntakePos, /*sync=*/true);
+  mRandomized = true;
+}
+
+void CuCache::Rewind() {
+  if (mIntakePos < mBunchsize) Error("CuCache::Rewind: nothing to replay");
+  mState = FULL;
+  mExhaustPos = 0;
+}
+
+void CuCache::AdvanceAfterBunch() {
+  mExhaustPos += mBunchsize;
+  if (mExhaustPos > mIntakePos - mBunchsize) {
+    mDiscarded += (int)(mIntakePos - mExhaustPos);
+    mState = EMPTY;
+  }
+}
+
+void CuCache::GetBunch(CuMatrix<BaseFloat>& rFeatures, CuMatrix<BaseFloat>& rDesired) {
+  if (mState == EMPTY) Error("GetBunch on empty cache!!!");
+  if (mMode != DENSE) Error("CuCache::GetBunch: cache holds class ids, use GetBunchLabels");
+  if (mState == FULL || mState == INTAKE) {
+    mState = EXHAUST;
+    mExhaustPos = 0;
+  }
+  rFeatures.Init(mBunchsize, mFeatures.Cols());
+  rDesired.Init(mBunchsize, mDesired.Cols());
+  if (mRandomized) {
+    TnetMatrixDim df = rFeatures.Dim(), dd = rDesired.Dim();
+    TNET_SAFE_CALL(tnetF_randomize(rFeatures.pCUData(), mFeatures.pCUData(), mPerm.pCUData() + mExhaustPos, df,
+                                   mFeatures.Dim(), S));
+    TNET_SAFE_CALL(tnetF_randomize(rDesired.pCUData(), mDesired.pCUData(), mPerm.pCUData() + mExhaustPos, dd,
+                                   mDesired.Dim(), S));
+  } else {
+    rFeatures.CopyRows(mBunchsize, mExhaustPos, mFeatures, 0);
+    rDesired.CopyRows(mBunchsize, mExhaustPos, mDesired, 0);
+  }
+  AdvanceAfterBunch();
+}
+
+void CuCache::GetBunchLabels(CuMatrix<BaseFloat>& rFeatures, CuVector<int>& rLabels) {
+  if (mState == EMPTY) Error("GetBunch on empty cache!!!");
+  if (mMode != LABELS) Error("CuCache::GetBunchLabels: cache holds dense targets, use GetBunch");
+  if (mState == FULL || mState == INTAKE) {
+    mState = EXHAUST;
+    mExhaustPos = 0;
+  }
+  rFeatures.Init(mBunchsize, mFeatures.Cols());
+  rLabels.Init(mBunchsize);
+  if (mRandomized) {
+    TNET_SAFE_CALL(tnetF_randomize(rFeatures.pCUData(), mFeatures.pCUData(), mPerm.pCUData() + mExhaustPos,
+                                   rFeatures.Dim(), mFeatures.Dim(), S));
+    TNET_SAFE_CALL(tnet_gather_i32(rLabels.pCUData(), mLabels.pCUData(), mPerm.pCUData() + mExhaustPos,
+                                   (int)mBunchsize, S));
+  } else {
+    rFeatures.CopyRows(mBunchsize, mExhaustPos, mFeatures, 0);
+    TNET_HIP_CALL(hipMemcpyAsync(rLabels.pCUData(), mLabels.pCUData() + mExhaustPos, mBunchsize * sizeof(int),
+                                 hipMemcpyDeviceToDevice, CuDevice::Instantiate().Stream()));
+  }
+  AdvanceAfterBunch();
+}
+
+}  // namespace TNet

@@ -1,0 +1,80 @@
+// cucache.h -- GPU-resident feature/target cache (src/CuTNetLib/cuCache.h:12-70, .cc:22-200).
+//
+// Same state machine as the reference: EMPTY -> INTAKE -> FULL -> EXHAUST, leftover rows of the
+// utterance that overflowed carried into the next fill (truncated to the cache size), shuffle of
+// the intake rows with lrand48 + libstdc++ random_shuffle, consecutive bunches, tail < bunch
+// discarded.
+//
+// MI355X changes:
+//   * Randomize() only draws the permutation (host LCG, identical stream to srand48/lrand48) and
+//     uploads it; GetBunch() gathers the bunch rows straight from the intake buffer (one
+//     row-gather kernel) instead of materialising a shuffled copy of the whole cache -- same
+//     rows, half the HBM traffic;
+//   * one-hot targets are held as class ids (4 B/frame; a 4000-senone one-hot cache row is
+//     16 KB); a dense-target mode keeps the reference's AddData(features, desired) API.
+#pragma once
+
+#include "cumatrix.h"
+#include "rng48.h"
+
+namespace TNet {
+
+class CuCache {
+  typedef enum { EMPTY, INTAKE, FULL, EXHAUST } State;
+
+ public:
+  CuCache();
+  ~CuCache();
+
+  /// Initialize the cache (cachesize must be divisible by bunchsize)
+  void Init(size_t cachesize, size_t bunchsize);
+  /// Random stream used by Randomize (defaults to the process stream seeded by SeedRandom)
+  void SetRng(Rng48* rng) { mRng = rng; }
+
+  /// Dense targets (reference API)
+  void AddData(const CuMatrix<BaseFloat>& rFeatures, const CuMatrix<BaseFloat>& rDesired);
+  /// Class-id targets (device features + device labels)
+  void AddDataLabels(const CuMatrix<BaseFloat>& rFeatures, const CuVector<int>& rLabels);
+  /// Host utterance straight into the cache rows (no intermediate device copy)
+  void AddDataHost(const float* feats, size_t rows, size_t cols, size_t ld, const int* labels);
+
+  void Randomize();
+  void GetBunch(CuMatrix<BaseFloat>& rFeatures, CuMatrix<BaseFloat>& rDesired);
+  void GetBunchLabels(CuMatrix<BaseFloat>& rFeatures, CuVector<int>& rLabels);
+
+  bool Full() { return mState == FULL; }
+  bool Empty() { return mState == EMPTY || mIntakePos < mBunchsize; }
+  int Discarded() { return mDiscarded; }
+  void Trace(int trace) { mTrace = trace; }
+  size_t IntakePos() const { return mIntakePos; }
+  size_t Bunchsize() const { return mBunchsize; }
+  size_t Cachesize() const { return mCachesize; }
+  /// Re-arm the exhausted cache for another pass over the same intake (benchmark replay)
+  void Rewind();
+  /// host copy of the current permutation (tests)
+  const std::vector<int>& Permutation() const { return mPermHost; }
+
+ private:
+  enum Mode { UNSET, DENSE, LABELS };
+  void Alloc(size_t cols, size_t tcols);
+  void BeginIntake();
+  void CheckMode(Mode m);
+  void WarnLong(size_t rows);
+  void AdvanceAfterBunch();
+
+  State mState = EMPTY;
+  Mode mMode = UNSET;
+  size_t mIntakePos = 0, mExhaustPos = 0, mCachesize = 0, mBunchsize = 0;
+  int mDiscarded = 0;
+  bool mRandomized = false;
+  int mTrace = 0;
+  Rng48* mRng = nullptr;
+
+  CuMatrix<BaseFloat> mFeatures, mDesired, mFeaturesLeftover, mDesiredLeftover;
+  CuVector<int> mLabels, mLabelsLeftover;
+  size_t mLeftoverRows = 0;
+  CuVector<int> mPerm;          // device permutation of intake rows
+  std::vector<int> mPermHost;
+};
+
+}  // namespace TNet

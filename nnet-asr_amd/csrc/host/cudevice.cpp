@@ -1,0 +1,127 @@
+// cudevice.cpp -- see cudevice.h.
+#include "cudevice.h"
+
+#include <iomanip>
+#include <iostream>
+
+namespace TNet {
+
+CuDevice& CuDevice::Instantiate() {
+  static CuDevice dev;
+  dev.EnsureInit();
+  return dev;
+}
+
+CuDevice::CuDevice() {}
+
+void CuDevice::EnsureInit() {
+  if (mInit) return;
+  int n = 0;
+  TNET_HIP_CALL(hipGetDeviceCount(&n));
+  if (n <= 0) Error("CuDevice: no HIP device visible");
+  TNET_HIP_CALL(hipSetDevice(mDevice));
+  TNET_HIP_CALL(hipStreamCreateWithFlags(&mStream, hipStreamNonBlocking));
+  mOwnStream = true;
+  mInit = true;
+}
+
+void CuDevice::SelectGPU(int gpu_id) {
+  if (!mFree.empty() || mWs) Error("CuDevice::SelectGPU after allocation");
+  int n = 0;
+  TNET_HIP_CALL(hipGetDeviceCount(&n));
+  if (gpu_id < 0 || gpu_id >= n) Error("CuDevice::SelectGPU: invalid gpu id");
+  if (mOwnStream && mStream) (void)hipStreamDestroy(mStream);
+  mDevice = gpu_id;
+  TNET_HIP_CALL(hipSetDevice(mDevice));
+  TNET_HIP_CALL(hipStreamCreateWithFlags(&mStream, hipStreamNonBlocking));
+  mOwnStream = true;
+}
+
+void CuDevice::SetStream(hipStream_t s) {
+  if (mOwnStream && mStream) TNET_HIP_CALL(hipStreamSynchronize(mStream));
+  if (mOwnStream && mStream) (void)hipStreamDestroy(mStream);
+  mStream = s;
+  mOwnStream = false;
+}
+
+void CuDevice::AccuProfile(const std::string& key, double msec) { mProfileMap[key] += msec; }
+
+void CuDevice::PrintProfile(std::ostream& os) {
+  os << "== PROFILE ==\n";
+  for (auto& kv : mProfileMap) os << std::setw(24) << kv.first << " " << kv.second / 1000.0 << "\n";
+  os << "=============\n";
+}
+
+void* CuDevice::Alloc(size_t bytes) {
+  if (bytes == 0) return nullptr;
+  auto it = mFree.find(bytes);
+  if (it != mFree.end() && !it->second.empty()) {
+    void* p = it->second.back();
+    it->second.pop_back();
+    return p;
+  }
+  void* p = nullptr;
+  hipError_t e = hipMalloc(&p, bytes);
+  if (e != hipSuccess) {
+    // release the cache and retry once
+    TNET_HIP_CALL(hipStreamSynchronize(mStream));
+    for (auto& kv : mFree)
+      for (void* q : kv.second) (void)hipFree(q);
+    mFree.clear();
+    TNET_HIP_CALL(hipMalloc(&p, bytes));
+  }
+  return p;
+}
+
+void CuDevice::Free(void* p, size_t bytes) {
+  if (!p) return;
+  mFree[bytes].push_back(p);  // stream-ordered reuse: all library work is on mStream
+}
+
+void* CuDevice::Workspace(size_t bytes) {
+  if (bytes > mWsBytes) {
+    if (mWs) {
+      TNET_HIP_CALL(hipStreamSynchronize(mStream));
+      (void)hipFree(mWs);
+    }
+    size_t b = bytes < (1u << 20) ? (1u << 20) : bytes;
+    TNET_HIP_CALL(hipMalloc(&mWs, b));
+    mWsBytes = b;
+  }
+  return mWs;
+}
+
+void CuDevice::Synchronize() { TNET_HIP_CALL(hipStreamSynchronize(mStream)); }
+
+CuDevice::~CuDevice() {
+  // process teardown: the HIP runtime may already be gone; do not throw
+  if (!mInit) return;
+  (void)hipStreamSynchronize(mStream);
+  for (auto& kv : mFree)
+    for (void* q : kv.second) (void)hipFree(q);
+  if (mWs) (void)hipFree(mWs);
+  if (mOwnStream && mStream) (void)hipStreamDestroy(mStream);
+  if (mVerbose) PrintProfile(std::cout);
+}
+
+CuProfileScope::CuProfileScope(const char* key) : mKey(key) {
+  CuDevice& d = CuDevice::Instantiate();
+  if (!d.Profile()) return;
+  (void)hipEventCreate(&mStart);
+  (void)hipEventCreate(&mStop);
+  (void)hipEventRecord(mStart, d.Stream());
+}
+
+CuProfileScope::~CuProfileScope() {
+  if (!mStart) return;
+  CuDevice& d = CuDevice::Instantiate();
+  (void)hipEventRecord(mStop, d.Stream());
+  (void)hipEventSynchronize(mStop);
+  float ms = 0.f;
+  (void)hipEventElapsedTime(&ms, mStart, mStop);
+  d.AccuProfile(mKey, ms);
+  (void)hipEventDestroy(mStart);
+  (void)hipEventDestroy(mStop);
+}
+
+}  // namespace TNet

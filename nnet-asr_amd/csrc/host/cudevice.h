@@ -1,0 +1,79 @@
+// cudevice.h -- per-process device context of the MI355X TNet library.
+//
+// Counterpart of CuDevice (src/CuBaseLib/cudevice.h:15-73, cudevice.cc:23-121): GPU selection,
+// verbose/profile map (AccuProfile).  Differences, MI355X-first:
+//   * created lazily on first use (the reference builds it at static-init time, cudevice.cc:121),
+//     so loading the library never touches the GPU;
+//   * owns one HIP stream on which every operation of the library is enqueued asynchronously
+//     (no per-call device sync); host values are only read back where the API demands them;
+//   * owns a size-bucketed caching allocator (steady-state training performs no hipMalloc) and
+//     the stream-ordered scratch workspace the reduction kernels need;
+//   * profiling: when enabled, ops are bracketed by hipEvents and accumulated per name, the
+//     AccuProfile map of the reference (printed by PrintProfile).
+#pragma once
+
+#include <map>
+#include <string>
+#include <vector>
+
+#include "tnet_common.h"
+
+namespace TNet {
+
+class CuDevice {
+ public:
+  static CuDevice& Instantiate();
+
+  hipStream_t Stream() { return mStream; }
+  /// Use an external stream (e.g. a caller-owned one); the library does not destroy it.
+  void SetStream(hipStream_t s);
+  int DeviceId() const { return mDevice; }
+  /// SelectGPU (cudevice.cc:84-101): must be called before any allocation.
+  void SelectGPU(int gpu_id);
+
+  void Verbose(bool v) { mVerbose = v; }
+  bool Verbose() const { return mVerbose; }
+  void Profile(bool p) { mProfile = p; }
+  bool Profile() const { return mProfile; }
+  void AccuProfile(const std::string& key, double msec);
+  void PrintProfile(std::ostream& os);
+  const std::map<std::string, double>& ProfileMap() const { return mProfileMap; }
+
+  void* Alloc(size_t bytes);
+  void Free(void* p, size_t bytes);
+  /// Scratch buffer valid until the next Workspace() call on this stream (stream-ordered reuse).
+  void* Workspace(size_t bytes);
+  void Synchronize();
+
+  ~CuDevice();
+
+ private:
+  CuDevice();
+  CuDevice(const CuDevice&) = delete;
+  CuDevice& operator=(const CuDevice&) = delete;
+  void EnsureInit();
+
+  bool mInit = false;
+  int mDevice = 0;
+  hipStream_t mStream = nullptr;
+  bool mOwnStream = false;
+  bool mVerbose = false;
+  bool mProfile = false;
+  std::map<std::string, double> mProfileMap;
+  std::map<size_t, std::vector<void*>> mFree;
+  void* mWs = nullptr;
+  size_t mWsBytes = 0;
+};
+
+/// RAII profile scope: times the enqueued work of one op when profiling is on.
+class CuProfileScope {
+ public:
+  explicit CuProfileScope(const char* key);
+  ~CuProfileScope();
+
+ private:
+  const char* mKey;
+  hipEvent_t mStart = nullptr, mStop = nullptr;
+};
+
+}  // namespace TNet

@@ -1,0 +1,180 @@
+// culayers.cpp -- <biasedlinearity>, <sigmoid>, <softmax> on the fused gfx950 kernels.
+#include "culayers.h"
+
+#include <cctype>
+#include <cstdlib>
+
+namespace TNet {
+
+#define S ((void*)CuDevice::Instantiate().Stream())
+
+// ------------------------------------------------------------------------------ text parsing
+static bool next_token(std::streambuf* sb, char* buf, size_t cap) {
+  int c = sb->sgetc();
+  while (c != EOF && std::isspace(c)) c = sb->snextc();
+  if (c == EOF) return false;
+  size_t n = 0;
+  while (c != EOF && !std::isspace(c)) {
+    if (n + 1 < cap) buf[n++] = (char)c;
+    c = sb->snextc();
+  }
+  buf[n] = 0;
+  return true;
+}
+
+void ReadMatrixFast(std::istream& in, Matrix<BaseFloat>& m) {
+  in >> std::ws;
+  if (in.peek() != 'm') Error("Failed to read matrix from stream: expected 'm R C'");
+  in.get();
+  long long r = -1, c = -1;
+  in >> r >> c;
+  if (in.fail() || r < 0 || c < 0) Error("Failed to read matrix from stream: no size");
+  m.Init((size_t)r, (size_t)c);
+  std::streambuf* sb = in.rdbuf();
+  char tok[128];
+  float* p = m.pData();
+  for (long long i = 0; i < r * c; i++) {
+    if (!next_token(sb, tok, sizeof tok)) Error("Failed to read matrix from stream: truncated");
+    char* end = nullptr;
+    p[i] = std::strtof(tok, &end);
+    if (end == tok) Error(std::string("Failed to read matrix from stream: bad token ") + tok);
+  }
+}
+
+void ReadVectorFast(std::istream& in, Vector<BaseFloat>& v) {
+  in >> std::ws;
+  if (in.peek() != 'v') Error("Failed to read vector from stream: expected 'v N'");
+  in.get();
+  long long n = -1;
+  in >> n;
+  if (in.fail() || n < 0) Error("Failed to read vector from stream: no size");
+  v.Init((size_t)n);
+  std::streambuf* sb = in.rdbuf();
+  char tok[128];
+  for (long long i = 0; i < n; i++) {
+    if (!next_token(sb, tok, sizeof tok)) Error("Failed to read vector from stream: truncated");
+    char* end = nullptr;
+    v[(size_t)i] = std::strtof(tok, &end);
+    if (end == tok) Error(std::string("Failed to read vector from stream: bad token ") + tok);
+  }
+}
+
+// ------------------------------------------------------------------------- CuBiasedLinearity
+void CuBiasedLinearity::PropagateFnc(const CuMatrix<BaseFloat>& X, CuMatrix<BaseFloat>& Y) {
+  CuProfileScope p("CuBiasedLinearity::Propagate");
+  // Y = b + X W  (AddScaledRow + Gemm('N','N',1,X,W,1), cuBiasedLinearity.cc:11-16) in one kernel
+  TNET_SAFE_CALL(tnet_affine_fwd(X.pCUData(), X.Dim(), mLinearity.pCUData(), mLinearity.Dim(), mBias.pCUData(),
+                                 Y.pCUData(), Y.Dim(), 0, S));
+}
+
+void CuBiasedLinearity::BackpropagateFnc(const CuMatrix<BaseFloat>& X, CuMatrix<BaseFloat>& Y) {
+  CuProfileScope p("CuBiasedLinearity::Backpropagate");
+  // Y = X W^T  (Gemm('N','T',1,E,W,0), cuBiasedLinearity.cc:21-25)
+  TNET_SAFE_CALL(tnet_affine_bwd(X.pCUData(), X.Dim(), mLinearity.pCUData(), mLinearity.Dim(), nullptr, 0,
+                                 Y.pCUData(), Y.Dim(), 0, S));
+}
+
+void CuBiasedLinearity::UpdateConstants(size_t rows, float* scale, float* l2) const {
+  // cuBiasedLinearity.cc:46-64
+  BaseFloat N = 1;
+  if (mGradDivFrm) N = static_cast<BaseFloat>(rows);
+  BaseFloat mmt_gain = static_cast<BaseFloat>(1.0 / (1.0 - mMomentum));
+  N *= mmt_gain;
+  *scale = -mLearningRate / N;
+  *l2 = -mLearningRate * mWeightcost * (mGradDivFrm ? 1.0f : (BaseFloat)rows);
+}
+
+void CuBiasedLinearity::UpdateFrom(const CuMatrix<BaseFloat>& X, const CuMatrix<BaseFloat>& E) {
+  CuProfileScope p("CuBiasedLinearity::Update");
+  float scale, l2;
+  UpdateConstants(X.Rows(), &scale, &l2);
+  const bool mmt = mMomentum != 0.0f;
+  // bias first: it reads only E (the weight kernel rewrites W in place)
+  TnetMatrixDim dE = E.Dim();
+  void* ws = CuDevice::Instantiate().Workspace((size_t)tnet_col_sum_workspace(dE));
+  TNET_SAFE_CALL(tnet_bias_update(E.pCUData(), dE, mBias.pCUData(), mmt ? mBiasCorrection.pCUData() : nullptr,
+                                  nullptr, scale, mMomentum, ws, S));
+  // corrW = X^T E + mmt corrW ; W += scale corrW ; W += l2 W   -- one GEMM with an SGD epilogue.
+  // With momentum 0 the correction buffer is never read (momentum is fixed per run, TNetCu.cc:322),
+  // so it is not written either.
+  TNET_SAFE_CALL(tnet_affine_update(X.pCUData(), X.Dim(), E.pCUData(), dE, mLinearity.pCUData(), mLinearity.Dim(),
+                                    mmt ? mLinearityCorrection.pCUData() : nullptr,
+                                    (int)mLinearityCorrection.Stride(), scale, mMomentum, l2, S));
+}
+
+void CuBiasedLinearity::Update() { UpdateFrom(GetInput(), GetErrorInput()); }
+
+void CuBiasedLinearity::ComputeGradient() {
+  CuProfileScope p("CuBiasedLinearity::ComputeGradient");
+  const CuMatrix<BaseFloat>& X = GetInput();
+  const CuMatrix<BaseFloat>& E = GetErrorInput();
+  mGradW.Init(mLinearity.Rows(), mLinearity.Cols());
+  mGradB.Init(mBias.Dim());
+  TNET_SAFE_CALL(tnet_affine_grad(X.pCUData(), X.Dim(), E.pCUData(), E.Dim(), mGradW.pCUData(), mGradW.Dim(), S));
+  TnetMatrixDim dE = E.Dim();
+  void* ws = CuDevice::Instantiate().Workspace((size_t)tnet_col_sum_workspace(dE));
+  TNET_SAFE_CALL(tnet_bias_update(E.pCUData(), dE, nullptr, nullptr, mGradB.pCUData(), 0.f, 0.f, ws, S));
+}
+
+std::vector<CuParamBlock> CuBiasedLinearity::GradientBlocks() {
+  mGradW.Init(mLinearity.Rows(), mLinearity.Cols());
+  mGradB.Init(mBias.Dim());
+  return {CuParamBlock{mGradW.pCUData(), (long)(mGradW.Rows() * mGradW.Stride())},
+          CuParamBlock{mGradB.pCUData(), (long)mGradB.Dim()}};
+}
+
+void CuBiasedLinearity::ApplyGradient(size_t frames) {
+  CuProfileScope p("CuBiasedLinearity::ApplyGradient");
+  float scale, l2;
+  UpdateConstants(frames, &scale, &l2);
+  const bool mmt = mMomentum != 0.0f;
+  // padding columns of W and of the gradient are zero, so the flat update keeps them zero
+  TNET_SAFE_CALL(tnet_sgd_update(mLinearity.pCUData(), mGradW.pCUData(), mmt ? mLinearityCorrection.pCUData() : nullptr,
+                                 (long)(mLinearity.Rows() * mLinearity.Stride()), scale, mMomentum, l2, S));
+  TNET_SAFE_CALL(tnet_sgd_update(mBias.pCUData(), mGradB.pCUData(), mmt ? mBiasCorrection.pCUData() : nullptr,
+                                 (long)mBias.Dim(), scale, mMomentum, 0.f, S));
+}
+
+void CuBiasedLinearity::ReadFromStream(std::istream& rIn) {
+  // matrix is stored transposed as SNet does (cuBiasedLinearity.cc:70-102)
+  BfMatrix transpose;
+  ReadMatrixFast(rIn, transpose);
+  BfVector bias;
+  ReadVectorFast(rIn, bias);
+  if (transpose.Cols() * transpose.Rows() == 0) Error("Missing linearity matrix in network file");
+  if (bias.Dim() == 0) Error("Missing bias vector in network file");
+  if (transpose.Rows() != GetNOutputs() || transpose.Cols() != GetNInputs() || bias.Dim() != GetNOutputs()) {
+    std::ostringstream os;
+    os << "Wrong dimensionalities of matrix/vector in network file\n"
+       << "Inputs:" << GetNInputs() << "Outputs:" << GetNOutputs() << "\n"
+       << "linearityCols:" << transpose.Rows() << "linearityRows:" << transpose.Cols() << "biasDims:" << bias.Dim()
+       << "\n";
+    Error(os.str());
+  }
+  mLinearity.CopyFrom(BfMatrix(transpose, TRANS));
+  mBias.CopyFrom(bias);
+}
+
+void CuBiasedLinearity::WriteToStream(std::ostream& rOut) {
+  BfMatrix tmp;
+  mLinearity.CopyTo(tmp);
+  BfMatrix transpose(tmp, TRANS);
+  rOut << transpose;
+  BfVector vec;
+  mBias.CopyTo(vec);
+  rOut << vec;
+  rOut << std::endl;
+}
+
+// ----------------------------------------------------------------------- activations
+void CuSigmoid::PropagateFnc(const CuMatrix<BaseFloat>& X, CuMatrix<BaseFloat>& Y) { CuMath<BaseFloat>::Sigmoid(Y, X); }
+void CuSigmoid::BackpropagateFnc(const CuMatrix<BaseFloat>& X, CuMatrix<BaseFloat>& Y) {
+  CuMath<BaseFloat>::DiffSigmoid(Y, X, mOutput);
+}
+void CuSoftmax::PropagateFnc(const CuMatrix<BaseFloat>& X, CuMatrix<BaseFloat>& Y) { CuMath<BaseFloat>::Softmax(Y, X); }
+void CuSoftmax::BackpropagateFnc(const CuMatrix<BaseFloat>& X, CuMatrix<BaseFloat>& Y) {
+  // we assume X is already dE/dSoftmax_input (cuActivation.cc:37-40)
+  Y.CopyFrom(X);
+}
+
+}  // namespace TNet

@@ -1,0 +1,77 @@
+// culayers.h -- the hot-path components: <biasedlinearity>, <sigmoid>, <softmax>.
+//
+// CuBiasedLinearity : src/CuTNetLib/cuBiasedLinearity.h:15-85, .cc:11-119
+// CuSigmoid/CuSoftmax: src/CuTNetLib/cuActivation.h:16-56, .cc:11-41
+#pragma once
+
+#include "cucomponent.h"
+
+namespace TNet {
+
+class CuBiasedLinearity : public CuUpdatableComponent {
+ public:
+  CuBiasedLinearity(size_t nInputs, size_t nOutputs, CuComponent* pPred)
+      : CuUpdatableComponent(nInputs, nOutputs, pPred),
+        mLinearity(nInputs, nOutputs), mBias(nOutputs),
+        mLinearityCorrection(nInputs, nOutputs), mBiasCorrection(nOutputs) {}
+  ~CuBiasedLinearity() {}
+
+  ComponentType GetType() const override { return BIASED_LINEARITY; }
+  const char* GetName() const override { return "<biasedlinearity>"; }
+
+  void PropagateFnc(const CuMatrix<BaseFloat>& X, CuMatrix<BaseFloat>& Y) override;
+  void BackpropagateFnc(const CuMatrix<BaseFloat>& X, CuMatrix<BaseFloat>& Y) override;
+  void Update() override;
+  void ComputeGradient() override;
+  void ApplyGradient(size_t frames) override;
+  std::vector<CuParamBlock> GradientBlocks() override;
+
+  void ReadFromStream(std::istream& rIn) override;
+  void WriteToStream(std::ostream& rOut) override;
+
+  // ---- access for the fused network-level kernels and the C ABI
+  CuMatrix<BaseFloat>& Linearity() { return mLinearity; }
+  CuVector<BaseFloat>& Bias() { return mBias; }
+  CuMatrix<BaseFloat>& LinearityCorrection() { return mLinearityCorrection; }
+  CuVector<BaseFloat>& BiasCorrection() { return mBiasCorrection; }
+  /// SGD constants of CuBiasedLinearity::Update (cuBiasedLinearity.cc:46-64) for `rows` frames
+  void UpdateConstants(size_t rows, float* scale, float* l2) const;
+  /// Update from explicit input/error matrices (fused GEMM + SGD epilogue, + bias kernel)
+  void UpdateFrom(const CuMatrix<BaseFloat>& X, const CuMatrix<BaseFloat>& E);
+
+ protected:
+  CuMatrix<BaseFloat> mLinearity;            ///< [nIn x nOut] (file stores the transpose)
+  CuVector<BaseFloat> mBias;                 ///< [nOut]
+  CuMatrix<BaseFloat> mLinearityCorrection;  ///< momentum buffer
+  CuVector<BaseFloat> mBiasCorrection;       ///< momentum buffer
+  CuMatrix<BaseFloat> mGradW;                ///< data-parallel gradient buffers (lazy)
+  CuVector<BaseFloat> mGradB;
+};
+
+class CuSigmoid : public CuComponent {
+ public:
+  CuSigmoid(size_t nInputs, size_t nOutputs, CuComponent* pPred) : CuComponent(nInputs, nOutputs, pPred) {}
+  ComponentType GetType() const override { return SIGMOID; }
+  const char* GetName() const override { return "<sigmoid>"; }
+
+ protected:
+  void PropagateFnc(const CuMatrix<BaseFloat>& X, CuMatrix<BaseFloat>& Y) override;
+  void BackpropagateFnc(const CuMatrix<BaseFloat>& X, CuMatrix<BaseFloat>& Y) override;
+};
+
+class CuSoftmax : public CuComponent {
+ public:
+  CuSoftmax(size_t nInputs, size_t nOutputs, CuComponent* pPred) : CuComponent(nInputs, nOutputs, pPred) {}
+  ComponentType GetType() const override { return SOFTMAX; }
+  const char* GetName() const override { return "<softmax>"; }
+
+ protected:
+  void PropagateFnc(const CuMatrix<BaseFloat>& X, CuMatrix<BaseFloat>& Y) override;
+  void BackpropagateFnc(const CuMatrix<BaseFloat>& X, CuMatrix<BaseFloat>& Y) override;
+};
+
+/// Fast text parsing of "m R C ..." / "v N ..." blocks (strtof on a buffered stream).
+void ReadMatrixFast(std::istream& in, Matrix<BaseFloat>& m);
+void ReadVectorFast(std::istream& in, Vector<BaseFloat>& v);
+
+}  // namespace TNet

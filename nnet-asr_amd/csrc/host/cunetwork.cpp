@@ -1,0 +1,280 @@
+// cunetwork.cpp -- see cunetwork.h.
+#include "cunetwork.h"
+
+#include <algorithm>
+#include <cctype>
+#include <fstream>
+#include <list>
+
+#include "gradexchange.h"
+
+namespace TNet {
+
+#define S ((void*)CuDevice::Instantiate().Stream())
+
+CuNetwork::~CuNetwork() {
+  for (auto*& c : mNetComponents) {
+    delete c;
+    c = nullptr;
+  }
+}
+
+void CuNetwork::AddLayer(CuComponent* layer) {
+  if (!mNetComponents.empty()) {
+    if (GetNOutputs() != layer->GetNInputs()) Error("Nonmatching dims");
+    layer->SetInput(mNetComponents.back()->GetOutput());
+    mNetComponents.back()->SetErrorInput(layer->GetErrorOutput());
+  }
+  mNetComponents.push_back(layer);
+}
+
+size_t CuNetwork::GetNInputs() const { return mNetComponents.empty() ? 0 : mNetComponents.front()->GetNInputs(); }
+size_t CuNetwork::GetNOutputs() const { return mNetComponents.empty() ? 0 : mNetComponents.back()->GetNOutputs(); }
+
+void CuNetwork::Propagate(const CuMatrix<BaseFloat>& in, CuMatrix<BaseFloat>& out) {
+  if (mNetComponents.empty()) {
+    out.CopyFrom(in);
+    return;
+  }
+  if (in.Cols() != GetNInputs()) {
+    std::ostringstream os;
+    os << "Nonmatching dims data dim is: " << in.Cols() << " network needs: " << GetNInputs();
+    Error(os.str());
+  }
+  mNetComponents.front()->SetInput(in);
+  for (auto* c : mNetComponents) c->Propagate();
+  out.CopyFrom(mNetComponents.back()->GetOutput());
+}
+
+void CuNetwork::Backpropagate(const CuMatrix<BaseFloat>& globerr) {
+  mNetComponents.back()->SetErrorInput(globerr);
+  for (auto it = mNetComponents.rbegin(); it != mNetComponents.rend(); ++it) {
+    if (*it != mpPropagErrorStopper) (*it)->Backpropagate();
+    if ((*it)->IsUpdatable()) {
+      CuUpdatableComponent& rComp = dynamic_cast<CuUpdatableComponent&>(**it);
+      if (rComp.LearnRate() > 0.0f) rComp.Update();
+    }
+    if (mpPropagErrorStopper == *it) break;
+  }
+}
+
+void CuNetwork::ReadNetwork(const char* pSrc) {
+  std::ifstream in(pSrc);
+  if (!in.good()) Error(std::string("Error, cannot read model: ") + pSrc);
+  ReadNetwork(in);
+}
+
+void CuNetwork::WriteNetwork(const char* pDst) {
+  std::ofstream out(pDst);
+  if (!out.good()) Error(std::string("Error, cannot write model: ") + pDst);
+  WriteNetwork(out);
+}
+
+void CuNetwork::ReadNetwork(std::istream& rIn) {
+  CuComponent* pComp;
+  while (nullptr != (pComp = ComponentFactory(rIn))) mNetComponents.push_back(pComp);
+}
+
+void CuNetwork::WriteNetwork(std::ostream& rOut) {
+  for (auto* c : mNetComponents) ComponentDumper(rOut, *c);
+}
+
+void CuNetwork::SetLearnRate(BaseFloat learnRate, const char* pLearnRateFactors) {
+  // cuNetwork.cc:80-134
+  std::list<BaseFloat> lr_factors;
+  if (pLearnRateFactors) {
+    std::string str(pLearnRateFactors);
+    for (auto& ch : str)
+      if (ch == ':' || ch == ',') ch = ' ';
+    std::istringstream is(str);
+    BaseFloat f;
+    while (is >> f) lr_factors.push_back(f);
+    mLearnRateFactors = pLearnRateFactors;
+  }
+  BaseFloat scale = 1.0f;
+  mGlobLearnRate = learnRate;
+  bool stopper_given = false;
+  mpPropagErrorStopper = nullptr;
+  for (auto* c : mNetComponents) {
+    if (c->IsUpdatable()) {
+      if (pLearnRateFactors) {
+        if (lr_factors.empty()) Error("Too few learninig rate scale factors");
+        scale = lr_factors.front();
+        lr_factors.pop_front();
+      }
+      dynamic_cast<CuUpdatableComponent*>(c)->LearnRate(learnRate * scale);
+      if (!stopper_given && (learnRate * scale > 0.0)) {
+        mpPropagErrorStopper = c;
+        stopper_given = true;
+      }
+    }
+  }
+  if (!lr_factors.empty()) Error("Too much learninig rate scale factors");
+}
+
+void CuNetwork::PrintLearnRate() {
+  std::cout << "Learning rate: global " << mGlobLearnRate << " components' ";
+  for (auto* c : mNetComponents)
+    if (c->IsUpdatable()) std::cout << " " << dynamic_cast<CuUpdatableComponent*>(c)->LearnRate();
+  std::cout << "\n" << std::flush;
+}
+
+void CuNetwork::SetMomentum(BaseFloat momentum) {
+  for (auto* c : mNetComponents)
+    if (c->IsUpdatable()) dynamic_cast<CuUpdatableComponent*>(c)->Momentum(momentum);
+}
+void CuNetwork::SetWeightcost(BaseFloat weightcost) {
+  for (auto* c : mNetComponents)
+    if (c->IsUpdatable()) dynamic_cast<CuUpdatableComponent*>(c)->Weightcost(weightcost);
+}
+void CuNetwork::SetL1(BaseFloat l1) {
+  // only <sparselinearity> uses L1 (cuNetwork.cc:159-168); not part of this build's component set
+  (void)l1;
+}
+void CuNetwork::SetGradDivFrm(bool div) {
+  for (auto* c : mNetComponents)
+    if (c->IsUpdatable()) dynamic_cast<CuUpdatableComponent*>(c)->GradDivFrm(div);
+}
+
+CuComponent* CuNetwork::ComponentFactory(std::istream& rIn) {
+  rIn >> std::ws;
+  if (rIn.eof()) return nullptr;
+  std::string tag;
+  rIn >> tag;
+  if (tag.empty()) return nullptr;
+  std::transform(tag.begin(), tag.end(), tag.begin(), ::tolower);
+  if (tag[0] != '<' || tag[tag.size() - 1] != '>') Error(std::string("Invalid component tag:") + tag);
+  if (tag == "<endblock>") return nullptr;
+  size_t nInputs = 0, nOutputs = 0;
+  rIn >> std::ws >> nOutputs >> std::ws >> nInputs;
+  if (rIn.fail() || nInputs == 0 || nOutputs == 0) Error("Invalid component dimensions for " + tag);
+  CuComponent* pPred = mNetComponents.empty() ? nullptr : mNetComponents.back();
+  CuComponent* pRet = nullptr;
+  if (tag == "<biasedlinearity>") pRet = new CuBiasedLinearity(nInputs, nOutputs, pPred);
+  else if (tag == "<sigmoid>") pRet = new CuSigmoid(nInputs, nOutputs, pPred);
+  else if (tag == "<softmax>") pRet = new CuSoftmax(nInputs, nOutputs, pPred);
+  else Error(std::string("Unknown Component tag:") + tag);
+  pRet->ReadFromStream(rIn);
+  return pRet;
+}
+
+void CuNetwork::ComponentDumper(std::ostream& rOut, CuComponent& rComp) {
+  rOut << rComp.GetName() << " " << rComp.GetNOutputs() << " " << rComp.GetNInputs() << std::endl;
+  rComp.WriteToStream(rOut);
+}
+
+// ======================================================================================
+// fused training step
+// ======================================================================================
+bool CuNetwork::IsFusableMLP() const {
+  const size_t n = mNetComponents.size();
+  if (n < 2 || n % 2) return false;
+  for (size_t i = 0; i < n; i += 2) {
+    if (mNetComponents[i]->GetType() != CuComponent::BIASED_LINEARITY) return false;
+    const bool last = (i + 2 == n);
+    const CuComponent::ComponentType want = last ? CuComponent::SOFTMAX : CuComponent::SIGMOID;
+    if (mNetComponents[i + 1]->GetType() != want) return false;
+  }
+  return true;
+}
+
+void CuNetwork::TrainBunchGeneric(const CuMatrix<BaseFloat>& X, const CuVector<int>& labels,
+                                  CuObjectiveFunction& obj, bool train) {
+  CuMatrix<BaseFloat> out;
+  Propagate(X, out);
+  obj.EvaluateLabels(out, labels, mGlobErr);
+  if (train) Backpropagate(mGlobErr);
+}
+
+void CuNetwork::TrainBunch(const CuMatrix<BaseFloat>& X, const CuVector<int>& labels, CuObjectiveFunction& obj,
+                           bool train, GradExchange* exchange) {
+  if (!IsFusableMLP() || obj.GetTypeId() != CuObjectiveFunction::CROSS_ENTROPY) {
+    if (exchange) Error("CuNetwork::TrainBunch: data-parallel training needs the sigmoid-MLP topology");
+    TrainBunchGeneric(X, labels, obj, train);
+    return;
+  }
+  if (X.Cols() != GetNInputs()) Error("CuNetwork::TrainBunch: non-matching input dim");
+  if (labels.Dim() != X.Rows()) Error("CuNetwork::TrainBunch: number of labels != rows");
+  const size_t rows = X.Rows();
+  const int nl = (int)mNetComponents.size() / 2;
+  if (mErr.size() != (size_t)nl) {
+    mErr.clear();
+    for (int l = 0; l < nl; l++) mErr.emplace_back(new CuMatrix<BaseFloat>());
+  }
+  mNetComponents.front()->SetInput(X);
+
+  // ---- forward: act_{l+1} = sigmoid(act_l W_l + b_l) straight into the <sigmoid>'s output
+  const CuMatrix<BaseFloat>* act = &X;
+  std::vector<const CuMatrix<BaseFloat>*> acts(nl + 1);
+  acts[0] = &X;
+  for (int l = 0; l < nl; l++) {
+    auto* lin = static_cast<CuBiasedLinearity*>(mNetComponents[2 * l]);
+    CuComponent* actc = mNetComponents[2 * l + 1];
+    const bool last = (l == nl - 1);
+    CuMatrix<BaseFloat>& dst = last ? lin->Output() : actc->Output();
+    dst.Init(rows, lin->GetNOutputs());
+    TNET_SAFE_CALL(tnet_affine_fwd(act->pCUData(), act->Dim(), lin->Linearity().pCUData(), lin->Linearity().Dim(),
+                                   lin->Bias().pCUData(), dst.pCUData(), dst.Dim(), last ? 0 : 1, S));
+    act = &dst;
+    acts[l + 1] = &dst;
+  }
+  // ---- objective: softmax + xent + error (+ optional softmax output)
+  CuMatrix<BaseFloat>& logits = mNetComponents[2 * (nl - 1)]->Output();
+  CuComponent* smx = mNetComponents.back();
+  float* yout = nullptr;
+  int ystride = 0;
+  if (mKeepOutput) {
+    smx->Output().Init(rows, smx->GetNOutputs());
+    yout = smx->Output().pCUData();
+    ystride = (int)smx->Output().Stride();
+  }
+  mGlobErr.Init(rows, GetNOutputs());
+  TNET_SAFE_CALL(tnet_softmax_xent(logits.pCUData(), logits.Dim(), labels.pCUData(), yout, ystride,
+                                   mGlobErr.pCUData(), (int)mGlobErr.Stride(), obj.DeviceStats(), S));
+  obj.AddFrames(rows);
+  if (!train) return;
+
+  // ---- backward + update, top to bottom (error uses the pre-update weights of the layer)
+  const CuMatrix<BaseFloat>* err = &mGlobErr;
+  for (int l = nl - 1; l >= 0; l--) {
+    auto* lin = static_cast<CuBiasedLinearity*>(mNetComponents[2 * l]);
+    const bool stopper = (lin == mpPropagErrorStopper);
+    CuMatrix<BaseFloat>* eo = nullptr;
+    if (!stopper && l > 0) {
+      eo = mErr[l].get();
+      eo->Init(rows, lin->GetNInputs());
+      // E_l = (E_{l+1} W_l^T) .* y_l (1 - y_l)   (backprop through <biasedlinearity> and the <sigmoid> below)
+      TNET_SAFE_CALL(tnet_affine_bwd(err->pCUData(), err->Dim(), lin->Linearity().pCUData(), lin->Linearity().Dim(),
+                                     acts[l]->pCUData(), (int)acts[l]->Stride(), eo->pCUData(), eo->Dim(), 1, S));
+    }
+    if (lin->LearnRate() > 0.0f) {
+      if (exchange) {
+        lin->SetInput(*acts[l]);
+        lin->SetErrorInput(*err);
+        lin->ComputeGradient();
+        exchange->Submit(*lin);
+      } else {
+        lin->UpdateFrom(*acts[l], *err);
+      }
+    }
+    if (stopper || l == 0) break;
+    err = eo;
+  }
+  if (exchange) {
+    exchange->WaitAll();
+    const size_t grows = exchange->GlobalRows(rows);
+    for (int l = nl - 1; l >= 0; l--) {
+      auto* lin = static_cast<CuBiasedLinearity*>(mNetComponents[2 * l]);
+      if (lin->LearnRate() > 0.0f) lin->ApplyGradient(grows);
+      if (lin == mpPropagErrorStopper) break;
+    }
+  }
+  // restore the component wiring the generic path relies on
+  for (int l = 0; l < nl; l++) {
+    auto* lin = mNetComponents[2 * l];
+    if (l > 0) lin->SetInput(mNetComponents[2 * l - 1]->GetOutput());
+    lin->SetErrorInput(mNetComponents[2 * l + 1]->GetErrorOutput());
+  }
+}
+
+}  // namespace TNet

@@ -1,0 +1,42 @@
+// kcommon.h -- shared device-side helpers for the gfx950 kernels of the TNet SGD path.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "tnet_kernels.h"
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+#define TNET_WAVE 64
+
+namespace tnetk {
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// sigmoid with the reference's double constants (cukernels.cu:192-206): 1.0/(1.0+exp(-x))
+__device__ __forceinline__ float sigmoidf_ref(float x) { return 1.0f / (1.0f + expf(-x)); }
+
+inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }
+
+}  // namespace tnetk
+
+#define TNET_LAUNCH_CHECK()                                   \
+  do {                                                        \
+    hipError_t _e = hipGetLastError();                        \
+    if (_e != hipSuccess) return TNET_ERR_LAUNCH;             \
+  } while (0)

@@ -1,0 +1,349 @@
+// reduce.hip -- row / column reductions of the TNet path on gfx950:
+//   * column sums (bias gradient; _add_col_sum / _add_col_sum_reduce, cukernels.cu:147-187) as a
+//     deterministic two-stage reduction: fp32 partials over fixed row slabs, combined in fp64;
+//   * fused softmax + cross-entropy + error + frame accuracy, one wavefront per row
+//     (_softmax / _softmax_reduce / _check_class / _log_elem / _mul_elem, cukernels.cu:131-483,
+//     driven by CuCrossEntropy::Evaluate, cuObjectiveFunction.cc:50-83).  The reference runs
+//     one THREAD per row with three serial passes for rows > 256 columns; here the row is held
+//     in registers (16 B per lane per step) and every reduction is a 64-lane butterfly.
+#include <float.h>
+
+#include "kcommon.h"
+
+namespace tnetk {
+
+constexpr int CS_COLS = 64;     // columns per block (one per lane)
+constexpr int CS_WAVES = 4;     // row sub-groups per block
+constexpr int CS_ROWS = 128;    // rows per slab
+
+static int cs_slabs(int rows) {
+  int s = cdiv(rows, CS_ROWS);
+  if (s > 64) s = 64;
+  if (s < 1) s = 1;
+  return s;
+}
+
+// partial[s][c] = sum of rows of slab s in column c (fixed order)
+__global__ __launch_bounds__(256) void colsum_partial_kernel(const float* __restrict__ M, TnetMatrixDim d,
+                                                             float* __restrict__ partial, int slabs) {
+  __shared__ float red[CS_WAVES][CS_COLS];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = blockIdx.x * CS_COLS + lane;
+  const int s = blockIdx.y;
+  const int rows_per = (d.rows + slabs - 1) / slabs;
+  const int r0 = s * rows_per, r1 = min(d.rows, r0 + rows_per);
+  float acc = 0.f;
+  if (c < d.cols)
+    for (int r = r0 + w; r < r1; r += CS_WAVES) acc += M[(long)r * d.stride + c];
+  red[w][lane] = acc;
+  __syncthreads();
+  if (w == 0 && c < d.cols) {
+    float t = red[0][lane];
+#pragma unroll
+    for (int k = 1; k < CS_WAVES; ++k) t += red[k][lane];
+    partial[(long)s * d.cols + c] = t;
+  }
+}
+
+// mode 0: v = alpha*sum + beta*v ; mode 1: bias update (c = sum + mmt*corr; b += scale*c; corr=c)
+// mode 2: grad_out = sum
+__global__ __launch_bounds__(256) void colsum_final_kernel(const float* __restrict__ partial, int slabs, int cols,
+                                                           int mode, float alpha, float beta, float* __restrict__ v,
+                                                           float* __restrict__ corr, float scale, float mmt) {
+  for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < cols; c += gridDim.x * blockDim.x) {
+    double s = 0.0;
+    for (int k = 0; k < slabs; ++k) s += (double)partial[(long)k * cols + c];
+    if (mode == 0) {
+      v[c] = (float)(alpha * s + (beta == 0.f ? 0.0 : (double)beta * v[c]));
+    } else if (mode == 1) {
+      float g = (float)s;
+      if (corr) {
+        g = g + mmt * corr[c];
+        corr[c] = g;
+      }
+      v[c] = v[c] + scale * g;
+    } else {
+      v[c] = (float)s;
+    }
+  }
+}
+
+// internal fallback workspace (single device, not thread-safe; the C++ layer always passes one)
+static float* g_ws = nullptr;
+static long g_ws_bytes = 0;
+static float* get_ws(long bytes) {
+  if (bytes > g_ws_bytes) {
+    if (g_ws) (void)hipFree(g_ws);
+    if (hipMalloc(&g_ws, bytes) != hipSuccess) { g_ws = nullptr; g_ws_bytes = 0; return nullptr; }
+    g_ws_bytes = bytes;
+  }
+  return g_ws;
+}
+
+static int colsum_run(const float* M, TnetMatrixDim d, void* workspace, hipStream_t st, int mode, float alpha,
+                      float beta, float* v, float* corr, float scale, float mmt) {
+  if (d.rows < 0 || d.cols < 0 || d.stride < d.cols) return TNET_ERR_ARG;
+  if (d.cols == 0) return TNET_OK;
+  const int slabs = cs_slabs(d.rows);
+  float* ws = workspace ? (float*)workspace : get_ws((long)slabs * d.cols * 4);
+  if (!ws) return TNET_ERR_RUNTIME;
+  if (d.rows > 0) {
+    colsum_partial_kernel<<<dim3(cdiv(d.cols, CS_COLS), slabs), 256, 0, st>>>(M, d, ws, slabs);
+    TNET_LAUNCH_CHECK();
+  } else {
+    if (hipMemsetAsync(ws, 0, (size_t)slabs * d.cols * 4, st) != hipSuccess) return TNET_ERR_RUNTIME;
+  }
+  colsum_final_kernel<<<cdiv(d.cols, 256), 256, 0, st>>>(ws, slabs, d.cols, mode, alpha, beta, v, corr, scale, mmt);
+  TNET_LAUNCH_CHECK();
+  return TNET_OK;
+}
+
+// ---------------------------------------------------------------------------------------------
+// softmax / cross-entropy, one wave per row
+// ---------------------------------------------------------------------------------------------
+constexpr int SX_MAXV4 = 16;  // row held in registers up to 16 float4 per lane = 4096 columns
+
+struct ArgMax {
+  float v;
+  int i;
+};
+__device__ __forceinline__ ArgMax argmax_merge(ArgMax a, ArgMax b) {
+  // first maximum wins: larger value, or equal value with smaller index
+  if (b.v > a.v || (b.v == a.v && b.i < a.i)) return b;
+  return a;
+}
+__device__ __forceinline__ ArgMax wave_argmax(ArgMax a) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    ArgMax b{__shfl_xor(a.v, o, 64), __shfl_xor(a.i, o, 64)};
+    a = argmax_merge(a, b);
+  }
+  return a;
+}
+
+// KIND 0: class-id labels; KIND 1: dense targets D.  Z == nullptr: Y already holds softmax output.
+template <int KIND>
+__global__ __launch_bounds__(256) void softmax_xent_kernel(const float* __restrict__ Z, TnetMatrixDim d,
+                                                           const int* __restrict__ labels,
+                                                           const float* __restrict__ D, int strideD,
+                                                           float* __restrict__ Y, int strideY,
+                                                           float* __restrict__ E, int strideE,
+                                                           double* __restrict__ stats, int vec4) {
+  const int lane = threadIdx.x & 63;
+  const int row = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  if (row >= d.rows) return;
+  const int N = d.cols;
+  const float* src = Z ? Z + (long)row * d.stride : Y + (long)row * strideY;
+  const bool cached = vec4 && N <= SX_MAXV4 * 256;
+
+  // ---- pass 1: max
+  f32x4 rv[SX_MAXV4];
+  float m = -1e20f;
+  if (cached) {
+#pragma unroll
+    for (int j = 0; j < SX_MAXV4; ++j) {
+      const int c = j * 256 + lane * 4;
+      f32x4 x = {-1e30f, -1e30f, -1e30f, -1e30f};
+      if (c < N) x = *reinterpret_cast<const f32x4*>(src + c);
+      rv[j] = x;
+      m = fmaxf(m, fmaxf(fmaxf(x[0], x[1]), fmaxf(x[2], x[3])));
+    }
+  } else {
+    for (int c = lane; c < N; c += 64) m = fmaxf(m, src[c]);
+  }
+  m = wave_max(m);
+
+  // ---- pass 2: sum of exp (only when normalising logits)
+  float inv = 1.f;
+  double dsum = 0.0;
+  if (Z) {
+    float s = 0.f;
+    if (cached) {
+#pragma unroll
+      for (int j = 0; j < SX_MAXV4; ++j) {
+        const int c = j * 256 + lane * 4;
+        if (c < N) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const float e = expf(rv[j][k] - m);
+            rv[j][k] = e;
+            s += e;
+          }
+        }
+      }
+    } else {
+      for (int c = lane; c < N; c += 64) s += expf(src[c] - m);
+    }
+    dsum = wave_sum_d((double)s);
+  }
+  const float sum = (float)dsum;
+
+  // ---- pass 3: y, error, argmax, xent
+  ArgMax ay{-1e20f, 0x7fffffff}, ad{-1e20f, 0x7fffffff};
+  double xent = 0.0;
+  const int t = (KIND == 0) ? labels[row] : -1;
+  float* yrow = Y ? Y + (long)row * strideY : nullptr;
+  float* erow = E ? E + (long)row * strideE : nullptr;
+  const float* drow = (KIND == 1) ? D + (long)row * strideD : nullptr;
+  auto visit = [&](int c, float y) {
+    float dv;
+    if (KIND == 0) dv = (c == t) ? 1.f : 0.f;
+    else dv = drow[c];
+    if (y > ay.v) { ay.v = y; ay.i = c; }
+    if (KIND == 1 && dv > ad.v) { ad.v = dv; ad.i = c; }
+    if (KIND == 1 && dv != 0.f) xent -= (double)dv * (double)logf(fmaxf(y, FLT_MIN));
+    return dv;
+  };
+  if (cached) {
+#pragma unroll
+    for (int j = 0; j < SX_MAXV4; ++j) {
+      const int c = j * 256 + lane * 4;
+      if (c < N) {
+        f32x4 y, e;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          y[k] = Z ? rv[j][k] / sum : rv[j][k];
+          e[k] = y[k] - visit(c + k, y[k]);
+        }
+        if (yrow && Z) *reinterpret_cast<f32x4*>(yrow + c) = y;
+        if (erow) *reinterpret_cast<f32x4*>(erow + c) = e;
+      }
+    }
+  } else {
+    for (int c = lane; c < N; c += 64) {
+      const float y = Z ? expf(src[c] - m) / sum : src[c];
+      const float dv = visit(c, y);
+      if (yrow && Z) yrow[c] = y;
+      if (erow) erow[c] = y - dv;
+    }
+  }
+  ay = wave_argmax(ay);
+  int des;
+  if (KIND == 0) {
+    des = t >= 0 ? t : 0;  // all-zero target row: first max of zeros is column 0
+  } else {
+    ad = wave_argmax(ad);
+    des = ad.i;
+  }
+  if (KIND == 1) xent = wave_sum_d(xent);
+  if (lane == 0 && stats) {
+    if (KIND == 0 && t >= 0) {
+      const float yt = Z ? expf(src[t] - m) / sum : src[t];
+      xent = -(double)logf(fmaxf(yt, FLT_MIN));
+    }
+    atomicAdd(stats + 0, xent);
+    atomicAdd(stats + 1, (ay.i == des) ? 1.0 : 0.0);
+  }
+}
+
+__global__ __launch_bounds__(256) void mse_kernel(const float* __restrict__ Y, TnetMatrixDim d,
+                                                  const float* __restrict__ D, int strideD, float* __restrict__ E,
+                                                  int strideE, double* __restrict__ stats) {
+  const int lane = threadIdx.x & 63;
+  const int row = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  if (row >= d.rows) return;
+  double s = 0.0;
+  for (int c = lane; c < d.cols; c += 64) {
+    const float e = Y[(long)row * d.stride + c] - D[(long)row * strideD + c];
+    if (E) E[(long)row * strideE + c] = e;
+    s += (double)(e * e);
+  }
+  s = wave_sum_d(s);
+  if (lane == 0 && stats) atomicAdd(stats, s);
+}
+
+__global__ __launch_bounds__(256) void check_class_kernel(const float* __restrict__ out,
+                                                          const float* __restrict__ des, int* __restrict__ match,
+                                                          TnetMatrixDim d) {
+  const int lane = threadIdx.x & 63;
+  const int row = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  if (row >= d.rows) return;
+  ArgMax a{-1e20f, 0x7fffffff}, b{-1e20f, 0x7fffffff};
+  for (int c = lane; c < d.cols; c += 64) {
+    const float x = out[(long)row * d.stride + c], y = des[(long)row * d.stride + c];
+    if (x > a.v) { a.v = x; a.i = c; }
+    if (y > b.v) { b.v = y; b.i = c; }
+  }
+  a = wave_argmax(a);
+  b = wave_argmax(b);
+  if (lane == 0) match[row] = (a.i == b.i) ? 1 : 0;
+}
+
+}  // namespace tnetk
+
+using namespace tnetk;
+
+extern "C" long tnet_col_sum_workspace(TnetMatrixDim d) { return (long)cs_slabs(d.rows) * (d.cols > 0 ? d.cols : 1) * 4; }
+
+extern "C" int tnetF_add_col_sum(float alpha, const float* mat, float beta, float* vec, TnetMatrixDim d,
+                                 void* workspace, void* stream) {
+  return colsum_run(mat, d, workspace, (hipStream_t)stream, 0, alpha, beta, vec, nullptr, 0.f, 0.f);
+}
+
+extern "C" int tnet_bias_update(const float* E, TnetMatrixDim dE, float* b, float* corr_b, float* grad_out,
+                                float scale, float mmt, void* workspace, void* stream) {
+  if (mmt != 0.f && !corr_b && !grad_out) return TNET_ERR_ARG;
+  if (grad_out) return colsum_run(E, dE, workspace, (hipStream_t)stream, 2, 1.f, 0.f, grad_out, nullptr, 0.f, 0.f);
+  return colsum_run(E, dE, workspace, (hipStream_t)stream, 1, 1.f, 0.f, b, corr_b, scale, mmt);
+}
+
+static bool v4ok(const void* p, int stride) { return ((uintptr_t)p & 15) == 0 && (stride & 3) == 0; }
+
+extern "C" int tnet_softmax_xent(const float* Z, TnetMatrixDim dZ, const int* labels, float* Y, int strideY, float* E,
+                                 int strideE, double* stats, void* stream) {
+  if (dZ.rows < 0 || dZ.cols <= 0 || !labels || (!Z && !Y)) return TNET_ERR_ARG;
+  if (!dZ.rows) return TNET_OK;
+  const int v4 = (dZ.cols & 3) == 0 && (!Z || v4ok(Z, dZ.stride)) && (!Y || v4ok(Y, strideY)) &&
+                 (!E || v4ok(E, strideE));
+  // when Z == NULL, Y already holds the softmax output (read through strideY)
+  TnetMatrixDim dd = dZ;
+  if (!Z) dd.stride = strideY;
+  softmax_xent_kernel<0><<<cdiv((long)dZ.rows * 64, 256), 256, 0, (hipStream_t)stream>>>(
+      Z, dd, labels, nullptr, 0, Y, strideY, E, strideE, stats, v4);
+  TNET_LAUNCH_CHECK();
+  return TNET_OK;
+}
+
+extern "C" int tnet_softmax_xent_dense(const float* Z, TnetMatrixDim dZ, const float* D, int strideD, float* Y,
+                                       int strideY, float* E, int strideE, double* stats, void* stream) {
+  if (dZ.rows < 0 || dZ.cols <= 0 || !D || (!Z && !Y)) return TNET_ERR_ARG;
+  if (!dZ.rows) return TNET_OK;
+  const float* z = Z;
+  const int v4 = (dZ.cols & 3) == 0 && (!z || v4ok(z, dZ.stride)) && (!Y || v4ok(Y, strideY)) &&
+                 (!E || v4ok(E, strideE));
+  // when Z == NULL the kernel reads Y rows through the stride of dZ
+  TnetMatrixDim dd = dZ;
+  if (!z) dd.stride = strideY;
+  softmax_xent_kernel<1><<<cdiv((long)dZ.rows * 64, 256), 256, 0, (hipStream_t)stream>>>(
+      z, dd, nullptr, D, strideD, Y, strideY, E, strideE, stats, v4);
+  TNET_LAUNCH_CHECK();
+  return TNET_OK;
+}
+
+extern "C" int tnetF_softmax(float* y, const float* x, TnetMatrixDim d, void* stream) {
+  if (d.rows < 0 || d.cols <= 0) return TNET_ERR_ARG;
+  if (!d.rows) return TNET_OK;
+  // softmax only: no labels/targets -> reuse the class-id kernel with label -1 semantics disabled
+  const int v4 = (d.cols & 3) == 0 && v4ok(x, d.stride) && v4ok(y, d.stride);
+  softmax_xent_kernel<1><<<cdiv((long)d.rows * 64, 256), 256, 0, (hipStream_t)stream>>>(
+      x, d, nullptr, x /*unused targets*/, d.stride, y, d.stride, nullptr, 0, nullptr, v4);
+  TNET_LAUNCH_CHECK();
+  return TNET_OK;
+}
+
+extern "C" int tnet_mse(const float* Y, TnetMatrixDim dY, const float* D, int strideD, float* E, int strideE,
+                        double* stats, void* stream) {
+  if (dY.rows < 0 || dY.cols <= 0) return TNET_ERR_ARG;
+  if (!dY.rows) return TNET_OK;
+  mse_kernel<<<cdiv((long)dY.rows * 64, 256), 256, 0, (hipStream_t)stream>>>(Y, dY, D, strideD, E, strideE, stats);
+  TNET_LAUNCH_CHECK();
+  return TNET_OK;
+}
+
+extern "C" int tnetF_check_class(const float* out, const float* des, int* match, TnetMatrixDim d, void* stream) {
+  if (d.rows < 0 || d.cols <= 0) return TNET_ERR_ARG;
+  if (!d.rows) return TNET_OK;
+  check_class_kernel<<<cdiv((long)d.rows * 64, 256), 256, 0, (hipStream_t)stream>>>(out, des, match, d);
+  TNET_LAUNCH_CHECK();
+  return TNET_OK;
+}

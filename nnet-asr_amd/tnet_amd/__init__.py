@@ -1,0 +1,296 @@
+"""tnet_amd -- MI355X-native TNet frame-batched SGD path (Python host binding).
+
+The compute path is C++ + hand-written gfx950 HIP kernels in lib/libtnet_amd.so; this package
+is a thin host-side mirror of the reference C++ interface (CuNetwork, CuObjectiveFunction, the
+TNetCu loop) over its C ABI, used by the tests and bench.py.  Device memory is owned by
+DeviceArray (hipMalloc through the library), never by a CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Optional, Sequence
+
+import numpy as np
+
+from . import formats  # noqa: F401  (host formats; no device code)
+from ._lib import LIB_PATH, MatrixDim, TnetError, check, check_ptr, header_symbols, lib
+
+__all__ = ["DeviceArray", "Network", "Objective", "Trainer", "Comm", "TnetError", "synchronize", "pad_stride",
+           "device_count", "version", "LIB_PATH", "header_symbols", "formats"]
+
+
+def pad_stride(cols: int) -> int:
+    return ((cols + 63) // 64) * 64 if cols else 0
+
+
+def device_count() -> int:
+    n = C.c_int(0)
+    lib().tnet_device_count(C.byref(n))
+    return n.value
+
+
+def version() -> str:
+    return lib().tnet_version().decode()
+
+
+def synchronize() -> None:
+    check(lib().tnet_synchronize(), "synchronize")
+
+
+class DeviceArray:
+    """Row-major device matrix (rows x cols) with a padded stride (multiple of 64 elements)."""
+
+    def __init__(self, rows: int, cols: int = 1, dtype=np.float32, stride: Optional[int] = None, zero=True):
+        self.rows, self.cols = int(rows), int(cols)
+        self.dtype = np.dtype(dtype)
+        self.stride = int(stride) if stride is not None else pad_stride(self.cols)
+        self.nbytes = max(self.rows * self.stride * self.dtype.itemsize, 16)
+        p = C.c_void_p()
+        check(lib().tnet_malloc(C.byref(p), self.nbytes), "tnet_malloc")
+        self.ptr = p.value
+        if zero:
+            check(lib().tnet_memset(self.ptr, 0, self.nbytes), "tnet_memset")
+
+    @classmethod
+    def from_numpy(cls, a: np.ndarray, stride: Optional[int] = None) -> "DeviceArray":
+        a = np.asarray(a)
+        if a.ndim == 1:
+            a = a.reshape(1, -1) if a.dtype != np.int32 else a.reshape(-1, 1)
+        d = cls(a.shape[0], a.shape[1], a.dtype, stride=stride if stride is not None else
+                (pad_stride(a.shape[1]) if a.shape[1] > 1 else 1))
+        d.upload(a)
+        return d
+
+    @classmethod
+    def vector(cls, v: np.ndarray) -> "DeviceArray":
+        v = np.ascontiguousarray(v)
+        d = cls(v.shape[0], 1, v.dtype, stride=1)
+        d.upload(v.reshape(-1, 1))
+        return d
+
+    def upload(self, a: np.ndarray) -> None:
+        a = np.asarray(a, dtype=self.dtype).reshape(self.rows, self.cols)
+        host = np.zeros((self.rows, self.stride), self.dtype)
+        host[:, : self.cols] = a
+        check(lib().tnet_memcpy_h2d(self.ptr, host.ctypes.data, host.nbytes), "h2d")
+
+    def numpy(self) -> np.ndarray:
+        host = np.empty((self.rows, self.stride), self.dtype)
+        check(lib().tnet_memcpy_d2h(host.ctypes.data, self.ptr, host.nbytes), "d2h")
+        return host[:, : self.cols].copy()
+
+    @property
+    def dim(self) -> MatrixDim:
+        return MatrixDim(self.rows, self.cols, self.stride)
+
+    def __del__(self):
+        try:
+            if getattr(self, "ptr", None):
+                lib().tnet_synchronize()
+                lib().tnet_free(self.ptr)
+                self.ptr = None
+        except Exception:
+            pass
+
+
+class Network:
+    """CuNetwork (src/CuTNetLib/cuNetwork.h:22-194) handle."""
+
+    def __init__(self, path: Optional[str] = None, text: Optional[str] = None):
+        if path is not None:
+            self.h = check_ptr(lib().tnet_net_read(path.encode()), "tnet_net_read")
+        elif text is not None:
+            self.h = check_ptr(lib().tnet_net_read_text(text.encode()), "tnet_net_read_text")
+        else:
+            raise ValueError("path or text required")
+
+    @classmethod
+    def from_layers(cls, layers, precision: int = 9) -> "Network":
+        import io
+        buf = io.StringIO()
+        formats.write_nnet(layers, buf, precision=precision)
+        return cls(text=buf.getvalue())
+
+    def write(self, path: str) -> None:
+        check(lib().tnet_net_write(self.h, path.encode()), "tnet_net_write")
+
+    def components(self):
+        out = []
+        for i in range(lib().tnet_net_num_components(self.h)):
+            tag = C.create_string_buffer(64)
+            ni, no = C.c_int(), C.c_int()
+            check(lib().tnet_net_component(self.h, i, tag, 64, C.byref(ni), C.byref(no)), "component")
+            out.append((tag.value.decode(), ni.value, no.value))
+        return out
+
+    @property
+    def n_in(self) -> int:
+        return self.components()[0][1]
+
+    @property
+    def n_out(self) -> int:
+        return self.components()[-1][2]
+
+    def get_params(self, i: int):
+        tag, ni, no = self.components()[i]
+        W = np.empty((ni, no), np.float32)
+        b = np.empty(no, np.float32)
+        check(lib().tnet_net_get_params(self.h, i, W.ctypes.data, b.ctypes.data), "get_params")
+        return W, b
+
+    def linear_params(self):
+        return [self.get_params(i) for i, c in enumerate(self.components()) if c[0] == "<biasedlinearity>"]
+
+    def set_params(self, i: int, W: np.ndarray, b: np.ndarray) -> None:
+        W = np.ascontiguousarray(W, np.float32)
+        b = np.ascontiguousarray(b, np.float32)
+        check(lib().tnet_net_set_params(self.h, i, W.ctypes.data, b.ctypes.data), "set_params")
+
+    def set_learn_rate(self, lr: float, factors: Optional[str] = None) -> None:
+        check(lib().tnet_net_set_learn_rate(self.h, lr, factors.encode() if factors else None), "learn_rate")
+
+    def set_momentum(self, m: float) -> None:
+        check(lib().tnet_net_set_momentum(self.h, m), "momentum")
+
+    def set_weightcost(self, wc: float) -> None:
+        check(lib().tnet_net_set_weightcost(self.h, wc), "weightcost")
+
+    def set_grad_div_frm(self, div: bool) -> None:
+        check(lib().tnet_net_set_grad_div_frm(self.h, int(div)), "graddivfrm")
+
+    def propagate(self, X: DeviceArray, Y: Optional[DeviceArray] = None) -> DeviceArray:
+        if Y is None:
+            Y = DeviceArray(X.rows, self.n_out)
+        check(lib().tnet_net_propagate(self.h, X.ptr, X.rows, X.stride, Y.ptr, Y.stride), "propagate")
+        return Y
+
+    def backpropagate(self, E: DeviceArray) -> None:
+        check(lib().tnet_net_backpropagate(self.h, E.ptr, E.rows, E.stride), "backpropagate")
+
+    def train_bunch(self, obj: "Objective", X: DeviceArray, labels: DeviceArray, train: bool = True) -> None:
+        check(lib().tnet_net_train_bunch(self.h, obj.h, X.ptr, X.rows, X.stride, labels.ptr, int(train)),
+              "train_bunch")
+
+    def keep_output(self, keep: bool = True) -> None:
+        check(lib().tnet_net_keep_output(self.h, int(keep)), "keep_output")
+
+    def output(self, i: int, rows: int) -> np.ndarray:
+        no = self.components()[i][2]
+        out = np.empty((rows, no), np.float32)
+        check(lib().tnet_net_output(self.h, i, out.ctypes.data, no), "output")
+        return out
+
+    def __del__(self):
+        try:
+            if getattr(self, "h", None):
+                lib().tnet_net_free(self.h)
+                self.h = None
+        except Exception:
+            pass
+
+
+class Objective:
+    """CuObjectiveFunction (src/CuTNetLib/cuObjectiveFunction.h:20-157)."""
+
+    XENT, MSE = 0, 1
+
+    def __init__(self, kind: int = 0):
+        self.h = check_ptr(lib().tnet_obj_create(kind), "tnet_obj_create")
+
+    def evaluate(self, out: DeviceArray, des: DeviceArray, err: DeviceArray) -> None:
+        check(lib().tnet_obj_evaluate(self.h, out.ptr, out.rows, out.cols, out.stride, des.ptr, des.stride, err.ptr,
+                                      err.stride), "evaluate")
+
+    def evaluate_labels(self, out: DeviceArray, labels: DeviceArray, err: DeviceArray) -> None:
+        check(lib().tnet_obj_evaluate_labels(self.h, out.ptr, out.rows, out.cols, out.stride, labels.ptr, err.ptr,
+                                             err.stride), "evaluate_labels")
+
+    def stats(self):
+        e, c = C.c_double(), C.c_double()
+        f = C.c_long()
+        check(lib().tnet_obj_stats(self.h, C.byref(e), C.byref(f), C.byref(c)), "stats")
+        return e.value, f.value, c.value
+
+    def report(self) -> str:
+        buf = C.create_string_buffer(512)
+        check(lib().tnet_obj_report(self.h, buf, 512), "report")
+        return buf.value.decode()
+
+    def reset(self) -> None:
+        check(lib().tnet_obj_reset(self.h), "reset")
+
+    def __del__(self):
+        try:
+            if getattr(self, "h", None):
+                lib().tnet_obj_free(self.h)
+                self.h = None
+        except Exception:
+            pass
+
+
+class Trainer:
+    """The TNetCu SGD loop (src/TNetCu.cc:375-442) over a CuCache."""
+
+    def __init__(self, net: Network, obj: Objective, bunchsize=256, cachesize=12800, seed=0, randomize=True,
+                 crossval=False):
+        self.net, self.obj = net, obj
+        self.h = check_ptr(lib().tnet_trainer_create(net.h, obj.h, bunchsize, cachesize, seed, int(randomize),
+                                                     int(crossval)), "tnet_trainer_create")
+
+    def add_utterance(self, feats: np.ndarray, labels: np.ndarray) -> None:
+        feats = np.ascontiguousarray(feats, np.float32)
+        labels = np.ascontiguousarray(labels, np.int32)
+        check(lib().tnet_trainer_add_utterance(self.h, feats.ctypes.data, feats.shape[0], feats.shape[1],
+                                               feats.shape[1], labels.ctypes.data), "add_utterance")
+
+    def finish(self) -> None:
+        check(lib().tnet_trainer_finish(self.h), "finish")
+
+    def train_corpus(self, feats: Sequence[np.ndarray], labels: Sequence[np.ndarray]) -> None:
+        for x, l in zip(feats, labels):
+            self.add_utterance(x, l)
+        self.finish()
+
+    @property
+    def steps(self) -> int:
+        return lib().tnet_trainer_steps(self.h)
+
+    def replay(self, n: int) -> None:
+        check(lib().tnet_trainer_replay(self.h, n), "replay")
+
+    def set_comm(self, comm: Optional["Comm"]) -> None:
+        check(lib().tnet_trainer_set_comm(self.h, comm.h if comm else None), "set_comm")
+
+    def __del__(self):
+        try:
+            if getattr(self, "h", None):
+                lib().tnet_trainer_free(self.h)
+                self.h = None
+        except Exception:
+            pass
+
+
+class Comm:
+    """RCCL communicator (one process per GPU)."""
+
+    @staticmethod
+    def unique_id() -> bytes:
+        buf = C.create_string_buffer(128)
+        check(lib().tnet_comm_unique_id(buf), "unique_id")
+        return buf.raw
+
+    def __init__(self, rank: int, world: int, uid: bytes):
+        self.h = check_ptr(lib().tnet_comm_create(rank, world, C.c_char_p(uid)), "tnet_comm_create")
+
+    def allreduce_host(self, v: np.ndarray) -> np.ndarray:
+        v = np.ascontiguousarray(v, np.float64).copy()
+        check(lib().tnet_comm_allreduce_host(self.h, v.ctypes.data_as(C.POINTER(C.c_double)), v.size), "allreduce")
+        return v
+
+    def __del__(self):
+        try:
+            if getattr(self, "h", None):
+                lib().tnet_comm_free(self.h)
+                self.h = None
+        except Exception:
+            pass

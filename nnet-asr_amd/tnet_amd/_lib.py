@@ -1,0 +1,160 @@
+"""ctypes binding of lib/libtnet_amd.so (include/tnet_kernels.h + include/tnet_train.h).
+
+This is the reference-side binding INTEGRATION.md describes: plain C ABI, raw pointers, sizes,
+status codes.  Loading the library never touches the GPU; the first call that needs the device
+does.  There is no fallback: if the shared library is missing the import fails loudly.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import re
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "libtnet_amd.so")
+INCLUDE_DIR = os.path.join(os.path.dirname(os.path.dirname(_HERE)), "include")
+
+_lib = None
+
+
+class TnetError(RuntimeError):
+    pass
+
+
+class MatrixDim(C.Structure):
+    _fields_ = [("rows", C.c_int), ("cols", C.c_int), ("stride", C.c_int)]
+
+
+vp = C.c_void_p
+i32 = C.c_int
+f32 = C.c_float
+i64 = C.c_long
+dp = C.POINTER(C.c_double)
+
+# name -> (restype, argtypes)
+_SIGS = {
+    # tnet_kernels.h
+    "tnet_status_str": (C.c_char_p, [i32]),
+    "tnet_version": (C.c_char_p, []),
+    "tnetF_set_const": (i32, [vp, f32, MatrixDim, vp]),
+    "tnetF_apply_log": (i32, [vp, MatrixDim, vp]),
+    "tnetF_apply_mask": (i32, [vp, vp, MatrixDim, MatrixDim, vp]),
+    "tnetF_apply_l1": (i32, [vp, f32, MatrixDim, vp]),
+    "tnetF_scale_cols": (i32, [vp, vp, MatrixDim, vp]),
+    "tnetF_scale_rows": (i32, [vp, vp, MatrixDim, vp]),
+    "tnetF_add_scaled": (i32, [f32, vp, i32, f32, vp, MatrixDim, vp]),
+    "tnetF_add_scaled_row": (i32, [f32, vp, f32, vp, MatrixDim, vp]),
+    "tnetF_mul_elem": (i32, [vp, vp, i32, MatrixDim, vp]),
+    "tnetF_log_elem": (i32, [vp, MatrixDim, vp]),
+    "tnet_col_sum_workspace": (i64, [MatrixDim]),
+    "tnetF_add_col_sum": (i32, [f32, vp, f32, vp, MatrixDim, vp, vp]),
+    "tnetF_sigmoid": (i32, [vp, vp, MatrixDim, vp]),
+    "tnetF_diff_sigmoid": (i32, [vp, vp, vp, MatrixDim, vp]),
+    "tnetF_softmax": (i32, [vp, vp, MatrixDim, vp]),
+    "tnetF_check_class": (i32, [vp, vp, vp, MatrixDim, vp]),
+    "tnetF_expand": (i32, [vp, vp, vp, MatrixDim, MatrixDim, vp]),
+    "tnetF_rearrange": (i32, [vp, vp, vp, MatrixDim, MatrixDim, vp]),
+    "tnetF_randomize": (i32, [vp, vp, vp, MatrixDim, MatrixDim, vp]),
+    "tnet_gather_i32": (i32, [vp, vp, vp, i32, vp]),
+    "tnet_sgemm": (i32, [C.c_char, C.c_char, i32, i32, i32, f32, vp, i32, vp, i32, f32, vp, i32, vp]),
+    "tnet_affine_fwd": (i32, [vp, MatrixDim, vp, MatrixDim, vp, vp, MatrixDim, i32, vp]),
+    "tnet_affine_bwd": (i32, [vp, MatrixDim, vp, MatrixDim, vp, i32, vp, MatrixDim, i32, vp]),
+    "tnet_affine_update": (i32, [vp, MatrixDim, vp, MatrixDim, vp, MatrixDim, vp, i32, f32, f32, f32, vp]),
+    "tnet_affine_grad": (i32, [vp, MatrixDim, vp, MatrixDim, vp, MatrixDim, vp]),
+    "tnet_sgd_update": (i32, [vp, vp, vp, i64, f32, f32, f32, vp]),
+    "tnet_bias_update": (i32, [vp, MatrixDim, vp, vp, vp, f32, f32, vp, vp]),
+    "tnet_softmax_xent": (i32, [vp, MatrixDim, vp, vp, i32, vp, i32, vp, vp]),
+    "tnet_softmax_xent_dense": (i32, [vp, MatrixDim, vp, i32, vp, i32, vp, i32, vp, vp]),
+    "tnet_mse": (i32, [vp, MatrixDim, vp, i32, vp, i32, vp, vp]),
+    # tnet_train.h
+    "tnet_last_error": (C.c_char_p, []),
+    "tnet_device_count": (i32, [C.POINTER(i32)]),
+    "tnet_select_gpu": (i32, [i32]),
+    "tnet_synchronize": (i32, []),
+    "tnet_stream": (vp, []),
+    "tnet_malloc": (i32, [C.POINTER(vp), C.c_size_t]),
+    "tnet_free": (i32, [vp]),
+    "tnet_memcpy_h2d": (i32, [vp, vp, C.c_size_t]),
+    "tnet_memcpy_d2h": (i32, [vp, vp, C.c_size_t]),
+    "tnet_memcpy_d2d": (i32, [vp, vp, C.c_size_t]),
+    "tnet_memset": (i32, [vp, i32, C.c_size_t]),
+    "tnet_set_profile": (i32, [i32]),
+    "tnet_profile_report": (i32, [C.c_char_p, i32]),
+    "tnet_timer_start": (i32, []),
+    "tnet_timer_stop": (i32, [C.POINTER(f32)]),
+    "tnet_net_read": (vp, [C.c_char_p]),
+    "tnet_net_read_text": (vp, [C.c_char_p]),
+    "tnet_net_write": (i32, [vp, C.c_char_p]),
+    "tnet_net_free": (i32, [vp]),
+    "tnet_net_num_components": (i32, [vp]),
+    "tnet_net_component": (i32, [vp, i32, C.c_char_p, i32, C.POINTER(i32), C.POINTER(i32)]),
+    "tnet_net_get_params": (i32, [vp, i32, vp, vp]),
+    "tnet_net_set_params": (i32, [vp, i32, vp, vp]),
+    "tnet_net_set_learn_rate": (i32, [vp, f32, C.c_char_p]),
+    "tnet_net_set_momentum": (i32, [vp, f32]),
+    "tnet_net_set_weightcost": (i32, [vp, f32]),
+    "tnet_net_set_grad_div_frm": (i32, [vp, i32]),
+    "tnet_net_propagate": (i32, [vp, vp, i32, i32, vp, i32]),
+    "tnet_net_backpropagate": (i32, [vp, vp, i32, i32]),
+    "tnet_net_train_bunch": (i32, [vp, vp, vp, i32, i32, vp, i32]),
+    "tnet_net_keep_output": (i32, [vp, i32]),
+    "tnet_net_output": (i32, [vp, i32, vp, i32]),
+    "tnet_obj_create": (vp, [i32]),
+    "tnet_obj_free": (i32, [vp]),
+    "tnet_obj_evaluate": (i32, [vp, vp, i32, i32, i32, vp, i32, vp, i32]),
+    "tnet_obj_evaluate_labels": (i32, [vp, vp, i32, i32, i32, vp, vp, i32]),
+    "tnet_obj_stats": (i32, [vp, dp, C.POINTER(i64), dp]),
+    "tnet_obj_report": (i32, [vp, C.c_char_p, i32]),
+    "tnet_obj_reset": (i32, [vp]),
+    "tnet_trainer_create": (vp, [vp, vp, i32, i32, i64, i32, i32]),
+    "tnet_trainer_free": (i32, [vp]),
+    "tnet_trainer_add_utterance": (i32, [vp, vp, i32, i32, i32, vp]),
+    "tnet_trainer_finish": (i32, [vp]),
+    "tnet_trainer_steps": (i64, [vp]),
+    "tnet_trainer_replay": (i32, [vp, i64]),
+    "tnet_trainer_set_comm": (i32, [vp, vp]),
+    "tnet_trainer_trace": (i32, [vp, i32]),
+    "tnet_comm_unique_id": (i32, [C.c_char_p]),
+    "tnet_comm_create": (vp, [i32, i32, C.c_char_p]),
+    "tnet_comm_free": (i32, [vp]),
+    "tnet_comm_allreduce_host": (i32, [vp, dp, i32]),
+    "tnet_comm_allreduce_device": (i32, [vp, vp, i64]),
+}
+
+
+def header_symbols():
+    """Every function declared in include/tnet_kernels.h and include/tnet_train.h."""
+    names = []
+    for h in ("tnet_kernels.h", "tnet_train.h"):
+        text = open(os.path.join(INCLUDE_DIR, h)).read()
+        text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+        names += re.findall(r"\b(tnet\w*)\s*\(", text)
+    return sorted(set(names))
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise TnetError(f"{LIB_PATH} not built: run `make -C nnet-asr_amd` (or __graft_entry__.build())")
+        L = C.CDLL(LIB_PATH, mode=C.RTLD_GLOBAL)
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(status, what=""):
+    if status != 0:
+        L = lib()
+        msg = L.tnet_last_error().decode(errors="replace") or L.tnet_status_str(status).decode()
+        raise TnetError(f"{what}: status {status}: {msg}")
+    return status
+
+
+def check_ptr(p, what=""):
+    if not p:
+        raise TnetError(f"{what}: {lib().tnet_last_error().decode(errors='replace')}")
+    return p

@@ -1,0 +1,44 @@
+"""CPU-only checks of the drop-in boundary: the C-ABI library loads without a GPU and exports
+every entry point the public headers declare; the Python binding covers them all."""
+import ctypes
+import os
+import subprocess
+
+import pytest
+
+from tnet_amd import _lib
+
+
+def test_library_built():
+    assert os.path.exists(_lib.LIB_PATH), "run __graft_entry__.build() / make -C nnet-asr_amd"
+
+
+def test_exports_every_header_symbol():
+    L = ctypes.CDLL(_lib.LIB_PATH)
+    missing = [n for n in _lib.header_symbols() if not hasattr(L, n)]
+    assert not missing, f"declared in include/*.h but not exported: {missing}"
+
+
+def test_binding_covers_headers():
+    declared = set(_lib.header_symbols())
+    bound = set(_lib._SIGS)
+    assert declared == bound, (sorted(declared - bound), sorted(bound - declared))
+
+
+def test_no_torch_or_oracle_dependency():
+    """The product library links only the HIP runtime and RCCL (no torch, no oracle)."""
+    out = subprocess.run(["ldd", _lib.LIB_PATH], capture_output=True, text=True).stdout
+    assert "libtorch" not in out and "oracle" not in out
+    assert "libamdhip64" in out and "librccl" in out
+
+
+def test_gfx950_code_object():
+    out = subprocess.run(["/opt/rocm/llvm/bin/llvm-readelf", "-n", _lib.LIB_PATH], capture_output=True, text=True)
+    data = open(_lib.LIB_PATH, "rb").read()
+    assert b"gfx950" in data
+
+
+def test_version_and_status_strings_without_gpu():
+    L = _lib.lib()
+    assert b"gfx950" in L.tnet_version()
+    assert L.tnet_status_str(-1) == b"invalid argument"

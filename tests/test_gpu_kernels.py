@@ -1,0 +1,215 @@
+"""Kernel-level parity of the gfx950 HIP kernels (through the C ABI) against the oracle.
+
+Floating-point tolerances (fp32 in / fp32 accumulate vs an fp64-accumulated checker):
+  GEMM-shaped results: |got - ref| <= 2e-5 * (|A||B|)_ij + 1e-6  (k-ordered f32 FMA chain, K <= 4096)
+  element-wise maps:   rtol 2e-6 (expf/logf vs libm double)
+  reductions:          rtol 1e-5
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+import oracle as orc  # noqa: E402
+from tnet_amd import DeviceArray, _lib, synchronize  # noqa: E402
+from tnet_amd._lib import MatrixDim, check, lib  # noqa: E402
+
+
+def S():
+    """the library stream: kernels and the DeviceArray copies must be stream-ordered"""
+    return lib().tnet_stream()
+
+
+def rnd(shape, seed, scale=1.0):
+    return (np.random.default_rng(seed).standard_normal(shape) * scale).astype(np.float32)
+
+
+def gemm_ref(ta, tb, A, B):
+    a = A.astype(np.float64).T if ta == "T" else A.astype(np.float64)
+    b = B.astype(np.float64).T if tb == "T" else B.astype(np.float64)
+    return a @ b, np.abs(a) @ np.abs(b)
+
+
+GEMM_SHAPES = [(1, 1, 1), (7, 5, 3), (33, 65, 31), (64, 64, 32), (130, 70, 598), (200, 135, 1024),
+               (256, 384, 440), (1024, 2048, 2048), (1024, 4000, 2048), (2048, 2048, 1024), (440, 2048, 1024)]
+
+
+@pytest.mark.parametrize("ta,tb", [("N", "N"), ("N", "T"), ("T", "N"), ("T", "T")])
+@pytest.mark.parametrize("M,N,K", GEMM_SHAPES)
+def test_sgemm(ta, tb, M, N, K):
+    A = rnd((K, M) if ta == "T" else (M, K), 1)
+    B = rnd((N, K) if tb == "T" else (K, N), 2)
+    C0 = rnd((M, N), 3)
+    alpha, beta = 0.75, 0.5
+    dA, dB, dC = DeviceArray.from_numpy(A), DeviceArray.from_numpy(B), DeviceArray.from_numpy(C0)
+    check(lib().tnet_sgemm(ta.encode(), tb.encode(), M, N, K, alpha, dA.ptr, dA.stride, dB.ptr, dB.stride, beta,
+                           dC.ptr, dC.stride, S()), "sgemm")
+    got = dC.numpy()
+    ref, mag = gemm_ref(ta, tb, A, B)
+    ref = alpha * ref + beta * C0
+    err = np.abs(got - ref)
+    assert np.all(err <= 2e-5 * (alpha * mag + np.abs(beta * C0)) + 1e-6), err.max()
+
+
+def test_sgemm_beta_zero_ignores_garbage():
+    M, N, K = 70, 90, 50
+    A, B = rnd((M, K), 4), rnd((K, N), 5)
+    dA, dB = DeviceArray.from_numpy(A), DeviceArray.from_numpy(B)
+    dC = DeviceArray.from_numpy(np.full((M, N), np.nan, np.float32))
+    check(lib().tnet_sgemm(b"N", b"N", M, N, K, 1.0, dA.ptr, dA.stride, dB.ptr, dB.stride, 0.0, dC.ptr, dC.stride,
+                           S()))
+    assert np.isfinite(dC.numpy()).all()
+
+
+def test_sgemm_rejects_misaligned_stride():
+    d = DeviceArray(8, 8)
+    st = lib().tnet_sgemm(b"N", b"N", 8, 8, 8, 1.0, d.ptr, 6, d.ptr, 8, 0.0, d.ptr, 8, S())
+    assert st == -1
+
+
+@pytest.mark.parametrize("act", [0, 1])
+@pytest.mark.parametrize("rows,n_in,n_out", [(16, 24, 32), (1024, 440, 2048), (960, 598, 1024), (33, 1024, 135)])
+def test_affine_fwd(act, rows, n_in, n_out):
+    X, W, b = rnd((rows, n_in), 6), rnd((n_in, n_out), 7, 0.1), rnd(n_out, 8)
+    dX, dW, dY = DeviceArray.from_numpy(X), DeviceArray.from_numpy(W), DeviceArray(rows, n_out)
+    db = DeviceArray.vector(b)
+    check(lib().tnet_affine_fwd(dX.ptr, dX.dim, dW.ptr, dW.dim, db.ptr, dY.ptr, dY.dim, act, S()))
+    z, mag = gemm_ref("N", "N", X, W)
+    z = z + b
+    got = dY.numpy()
+    if act:
+        ref = 1.0 / (1.0 + np.exp(-z))
+        assert np.all(np.abs(got - ref) <= 2e-5 * mag * ref * (1 - ref) + 2e-6)
+    else:
+        assert np.all(np.abs(got - z) <= 2e-5 * mag + 1e-6)
+
+
+@pytest.mark.parametrize("rows,n_in,n_out", [(16, 32, 10), (1024, 2048, 2048), (1024, 2048, 4000)])
+def test_affine_bwd_dsig(rows, n_in, n_out):
+    E, W = rnd((rows, n_out), 9), rnd((n_in, n_out), 10, 0.1)
+    Yb = 1 / (1 + np.exp(-rnd((rows, n_in), 11)))
+    dE, dW, dY, dO = (DeviceArray.from_numpy(E), DeviceArray.from_numpy(W), DeviceArray.from_numpy(Yb),
+                      DeviceArray(rows, n_in))
+    check(lib().tnet_affine_bwd(dE.ptr, dE.dim, dW.ptr, dW.dim, dY.ptr, dY.stride, dO.ptr, dO.dim, 1, S()))
+    z, mag = gemm_ref("N", "T", E, W)
+    s = Yb * (1 - Yb)
+    assert np.all(np.abs(dO.numpy() - z * s) <= 2e-5 * mag * s + 1e-7)
+
+
+@pytest.mark.parametrize("mmt", [0.0, 0.5])
+@pytest.mark.parametrize("rows,n_in,n_out", [(16, 24, 32), (1024, 2048, 2048), (1024, 440, 2048), (960, 1024, 135)])
+def test_affine_update(mmt, rows, n_in, n_out):
+    X, E = rnd((rows, n_in), 12), rnd((rows, n_out), 13, 0.01)
+    W, corr = rnd((n_in, n_out), 14, 0.1), rnd((n_in, n_out), 15, 0.01)
+    scale, l2 = -0.3 / rows, -1e-4
+    dX, dE, dW = DeviceArray.from_numpy(X), DeviceArray.from_numpy(E), DeviceArray.from_numpy(W)
+    dC = DeviceArray.from_numpy(corr) if mmt else None
+    check(lib().tnet_affine_update(dX.ptr, dX.dim, dE.ptr, dE.dim, dW.ptr, dW.dim, dC.ptr if dC else None,
+                                   dC.stride if dC else 0, scale, mmt, l2, S()))
+    g, mag = gemm_ref("T", "N", X, E)
+    c = g + mmt * corr
+    w = W + scale * c
+    w = w + l2 * w
+    tol = 2e-5 * abs(scale) * mag + 2e-7 * np.abs(W) + 1e-7
+    assert np.all(np.abs(dW.numpy() - w) <= tol)
+    if mmt:
+        assert np.all(np.abs(dC.numpy() - c) <= 2e-5 * mag + 1e-6)
+
+
+@pytest.mark.parametrize("rows,cols", [(1, 1), (16, 10), (1024, 135), (1024, 4000), (300, 4099), (64, 5000)])
+def test_softmax_xent_labels(rows, cols):
+    Z = rnd((rows, cols), 16, 3.0)
+    lab = np.random.default_rng(17).integers(0, cols, size=rows).astype(np.int32)
+    lab[::7] = -1  # unlabeled frames: all-zero target rows
+    dZ, dL = DeviceArray.from_numpy(Z), DeviceArray.vector(lab)
+    dY, dE = DeviceArray(rows, cols), DeviceArray(rows, cols)
+    stats = DeviceArray(1, 4, np.float64, stride=4)
+    check(lib().tnet_softmax_xent(dZ.ptr, dZ.dim, dL.ptr, dY.ptr, dY.stride, dE.ptr, dE.stride, stats.ptr, S()))
+    Yref = orc.softmax(Z)
+    Eref, xent, correct = orc.xent_eval(Yref, lab)
+    np.testing.assert_allclose(dY.numpy(), Yref, rtol=2e-5, atol=1e-9)
+    np.testing.assert_allclose(dE.numpy(), Eref, rtol=2e-5, atol=1e-8)
+    s = stats.numpy()[0]
+    np.testing.assert_allclose(s[0], xent, rtol=1e-5, atol=1e-5)
+    assert int(round(s[1])) == correct
+
+
+def test_softmax_xent_extreme_logits():
+    """underflowing probabilities hit the FLT_MIN clamp of _log_elem (cukernels.cu:131-141)"""
+    rows, cols = 8, 300
+    Z = np.zeros((rows, cols), np.float32)
+    Z[:, 0] = 200.0
+    lab = np.full(rows, 5, np.int32)
+    dZ, dL = DeviceArray.from_numpy(Z), DeviceArray.vector(lab)
+    dE = DeviceArray(rows, cols)
+    stats = DeviceArray(1, 4, np.float64, stride=4)
+    check(lib().tnet_softmax_xent(dZ.ptr, dZ.dim, dL.ptr, None, 0, dE.ptr, dE.stride, stats.ptr, S()))
+    s = stats.numpy()[0]
+    np.testing.assert_allclose(s[0], -rows * np.log(np.float32(1.1754944e-38)), rtol=1e-6)
+    assert s[1] == 0
+
+
+@pytest.mark.parametrize("rows,cols", [(1, 1), (1024, 2048), (960, 135), (3, 4000), (2049, 77)])
+def test_col_sum_and_bias_update(rows, cols):
+    E = rnd((rows, cols), 18)
+    dE = DeviceArray.from_numpy(E)
+    v0 = rnd(cols, 19)
+    dv = DeviceArray.vector(v0)
+    ws = DeviceArray(1, max(1, lib().tnet_col_sum_workspace(dE.dim) // 4 + 64))
+    check(lib().tnetF_add_col_sum(0.5, dE.ptr, 2.0, dv.ptr, dE.dim, ws.ptr, S()))
+    ref = 0.5 * E.astype(np.float64).sum(0) + 2.0 * v0
+    np.testing.assert_allclose(dv.numpy()[:, 0], ref, rtol=1e-5, atol=1e-5)
+    # bias update with momentum
+    b0, cb0 = rnd(cols, 20), rnd(cols, 21)
+    db, dcb = DeviceArray.vector(b0), DeviceArray.vector(cb0)
+    check(lib().tnet_bias_update(dE.ptr, dE.dim, db.ptr, dcb.ptr, None, -0.01, 0.9, ws.ptr, S()))
+    c = E.astype(np.float64).sum(0) + 0.9 * cb0
+    np.testing.assert_allclose(dcb.numpy()[:, 0], c, rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(db.numpy()[:, 0], b0 - 0.01 * c, rtol=1e-5, atol=1e-6)
+
+
+def test_elementwise_ops():
+    rows, cols = 37, 131
+    X = rnd((rows, cols), 22)
+    Y = 1 / (1 + np.exp(-rnd((rows, cols), 23)))
+    dX, dY, dO = DeviceArray.from_numpy(X), DeviceArray.from_numpy(Y), DeviceArray(rows, cols)
+    check(lib().tnetF_sigmoid(dO.ptr, dX.ptr, dX.dim, S()))
+    np.testing.assert_allclose(dO.numpy(), orc.sigmoid(X), rtol=2e-6, atol=1e-7)
+    check(lib().tnetF_diff_sigmoid(dO.ptr, dX.ptr, dY.ptr, dX.dim, S()))
+    np.testing.assert_allclose(dO.numpy(), orc.diff_sigmoid(X, Y), rtol=2e-6, atol=1e-7)
+    r = rnd(cols, 24)
+    dr = DeviceArray.vector(r)
+    check(lib().tnetF_add_scaled_row(2.0, dr.ptr, 0.5, dX.ptr, dX.dim, S()))
+    np.testing.assert_allclose(dX.numpy(), 2.0 * r + 0.5 * X, rtol=1e-6, atol=1e-6)
+    check(lib().tnetF_set_const(dO.ptr, 3.5, dO.dim, S()))
+    assert np.all(dO.numpy() == 3.5)
+    P = np.abs(rnd((rows, cols), 25)) + 1e-3
+    P[0, 0] = 0.0
+    dP = DeviceArray.from_numpy(P)
+    check(lib().tnetF_log_elem(dP.ptr, dP.dim, S()))
+    ref = np.log(np.maximum(P, np.float32(1.1754944e-38)).astype(np.float64))
+    np.testing.assert_allclose(dP.numpy(), ref, rtol=2e-6, atol=2e-6)
+
+
+def test_randomize_and_gather():
+    rows, cols = 500, 440
+    X = rnd((rows, cols), 26)
+    lab = np.arange(rows, dtype=np.int32) * 3
+    perm = np.random.default_rng(27).permutation(rows).astype(np.int32)[:256]
+    dX, dP, dL = DeviceArray.from_numpy(X), DeviceArray.vector(perm), DeviceArray.vector(lab)
+    dY, dLo = DeviceArray(256, cols), DeviceArray.vector(np.zeros(256, np.int32))
+    check(lib().tnetF_randomize(dY.ptr, dX.ptr, dP.ptr, dY.dim, dX.dim, S()))
+    check(lib().tnet_gather_i32(dLo.ptr, dL.ptr, dP.ptr, 256, S()))
+    np.testing.assert_array_equal(dY.numpy(), X[perm])
+    np.testing.assert_array_equal(dLo.numpy()[:, 0], lab[perm])
+
+
+def test_check_class_first_max_wins():
+    out = np.array([[0.1, 0.5, 0.5, 0.2], [0.3, 0.3, 0.3, 0.3], [0, 0, 0, 1]], np.float32)
+    des = np.array([[0, 1, 0, 0], [1, 0, 0, 0], [0, 0, 1, 0]], np.float32)
+    dO, dD = DeviceArray.from_numpy(out), DeviceArray.from_numpy(des, stride=DeviceArray.from_numpy(out).stride)
+    m = DeviceArray.vector(np.zeros(3, np.int32))
+    check(lib().tnetF_check_class(dO.ptr, dD.ptr, m.ptr, dO.dim, S()))
+    np.testing.assert_array_equal(m.numpy()[:, 0], [1, 1, 0])
