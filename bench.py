@@ -1,0 +1,202 @@
+#!/usr/bin/env python3
+"""bench.py -- training frames/sec of the MI355X TNet SGD path (BASELINE.json metric).
+
+Workload (N=1 line): the metric's 440 -> 2048x4 -> 4000 sigmoid MLP, softmax + cross-entropy,
+bunch 1024 frames per GPU, GRADDIVFRM=T, fp32 end to end; synthetic 440-dim N(0,1) frames with
+uniform class ids resident in a GPU CuCache.  One "step" = one bunch:
+gather from the shuffled cache -> forward -> softmax/xent -> backward -> SGD update, exactly the
+TNetCu per-bunch loop (src/TNetCu.cc:427-441).
+
+Multi-GPU (launched by torch.distributed.run): one process per GPU, utterance-sharded caches
+(weak scaling: 1024 frames per GPU per step), per-layer RCCL all-reduce of the gradients over
+xGMI, global-bunch GRADDIVFRM normalisation.  torch is used only for the gloo rendezvous /
+barrier / max-reduce of the timings; it is imported after the HIP library so one HIP runtime is
+loaded.
+
+Extra JSON fields: roofline (dominant kernel = the 2048x2048 affine-layer GEMMs, timed with hipEvents
+on the library stream inside the timed region), kernels (per-kernel breakdown), cpu_baseline
+(the reference CPU TNet on this host, rank 0 at N=1).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "nnet-asr_amd"))
+sys.path.insert(0, os.path.join(REPO, "oracle"))
+
+import numpy as np  # noqa: E402
+
+import tnet_amd  # noqa: E402  (loads libtnet_amd.so before torch: one HIP runtime in the process)
+from tnet_amd import Comm, Network, Objective, Trainer, formats  # noqa: E402
+from tnet_amd._lib import check, lib  # noqa: E402
+
+CONFIGS = {
+    "dnn4": [440, 2048, 2048, 2048, 2048, 4000],        # metric: 440 -> 2048x4 -> senones
+    "dnn5": [440, 2048, 2048, 2048, 2048, 2048, 4000],  # BASELINE config 3
+    "mlp3": [598, 1024, 135],                           # BASELINE config 2
+}
+PEAK_FP32_MFMA = 157.3  # TFLOP/s, MI355X dense fp32 matrix (MI355X_MICROARCH.md)
+PEAK_HBM = 8000.0       # GB/s
+
+
+def flops_per_frame(dims):
+    W = sum(dims[i] * dims[i + 1] for i in range(len(dims) - 1))
+    return 2.0 * (3 * W - dims[0] * dims[1])  # fwd all, bwd-error all but first, dW all
+
+
+def build_network(dims, seed=2):
+    """Topology from a compact zero-weight text, then gen_mlp_init-style weights uploaded."""
+    parts = []
+    for i in range(len(dims) - 1):
+        ni, no = dims[i], dims[i + 1]
+        parts.append(f"<biasedlinearity> {no} {ni}\nm {no} {ni}\n" + ("0 " * ni + "\n") * no + f"v {no} " +
+                     "0 " * no + "\n")
+        parts.append(f"<{'softmax' if i == len(dims) - 2 else 'sigmoid'}> {no} {no}\n")
+    net = Network(text="".join(parts))
+    rng = np.random.default_rng(seed)
+    for k in range(len(dims) - 1):
+        W = (0.1 * rng.standard_normal((dims[k], dims[k + 1]))).astype(np.float32)
+        b = (np.zeros(dims[k + 1]) if k == len(dims) - 2 else rng.random(dims[k + 1]) / 5.0 - 4.1).astype(np.float32)
+        net.set_params(2 * k, W, b)
+    return net
+
+
+def synth_frames(n, dim, n_cls, seed):
+    rng = np.random.default_rng(seed)
+    return rng.standard_normal((n, dim)).astype(np.float32), rng.integers(0, n_cls, n).astype(np.int32)
+
+
+def parse_kernel_report(text):
+    out = {}
+    for line in text.strip().splitlines():
+        tag, n, ms, work = line.split()
+        out[tag] = {"launches": int(n), "ms": float(ms), "work": float(work)}
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--config", default="dnn4", choices=sorted(CONFIGS))
+    ap.add_argument("--bunch", type=int, default=1024)
+    ap.add_argument("--cache", type=int, default=65536, help="frames resident per GPU")
+    ap.add_argument("--lr", type=float, default=1.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--kernel-timing", type=int, default=1, help="hipEvent per-kernel timing in the timed region")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dims = CONFIGS[args.config]
+    B = args.bunch
+
+    check(lib().tnet_select_gpu(local_rank), "select_gpu")
+    dist = None
+    comm = None
+    if world > 1:
+        import torch.distributed as dist  # noqa: F811  (gloo only: rendezvous, barrier, max)
+        dist.init_process_group("gloo")
+        uid = [Comm.unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        comm = Comm(rank, world, uid[0])
+
+    net = build_network(dims)
+    net.set_learn_rate(args.lr)
+    net.set_grad_div_frm(True)
+    obj = Objective()
+    trainer = Trainer(net, obj, bunchsize=B, cachesize=args.cache, seed=123 + rank, randomize=True)
+    if comm is not None:
+        trainer.set_comm(comm)
+    X, L = synth_frames(args.cache, dims[0], dims[-1], seed=1000 + rank)
+    taken = lib().tnet_trainer_prefill(trainer.h, X.ctypes.data, X.shape[0], X.shape[1], X.shape[1], L.ctypes.data)
+    if taken != args.cache:
+        raise SystemExit(f"prefill took {taken} rows, expected {args.cache}")
+    del X, L
+
+    def barrier():
+        tnet_amd.synchronize()
+        if dist is not None:
+            dist.barrier()
+
+    trainer.replay(args.warmup)
+    barrier()
+    check(lib().tnet_kernel_timing(int(bool(args.kernel_timing))), "kernel_timing")
+    barrier()
+    t0 = time.perf_counter()
+    trainer.replay(args.steps)
+    barrier()
+    dt = time.perf_counter() - t0
+    check(lib().tnet_kernel_timing(0), "kernel_timing")
+    import ctypes
+    buf = ctypes.create_string_buffer(1 << 16)
+    check(lib().tnet_kernel_timing_report(buf, len(buf)), "kernel_timing_report")
+    kern = parse_kernel_report(buf.value.decode())
+    if dist is not None:
+        import torch
+        t = torch.tensor([dt], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+
+    frames = world * args.steps * B
+    value = frames / dt
+    ms_per_step = 1000.0 * dt / args.steps
+
+    # ---- roofline of the dominant kernel: the 2048x2048 affine-layer GEMMs (fwd + bwd + fused update)
+    hid = [v for k, v in kern.items() if k.startswith("gemm_") and k.endswith(":2048x2048")]
+    roof = None
+    if hid:
+        launches = sum(v["launches"] for v in hid)
+        ms = sum(v["ms"] for v in hid)
+        flops = sum(v["work"] for v in hid)
+        achieved = flops / (ms * 1e-3) / 1e12
+        roof = {"bound": "mfma", "kernel": "gemm_f32 2048x2048 (fwd/bwd/update)", "achieved": round(achieved, 2),
+                "peak": PEAK_FP32_MFMA, "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_MFMA, 4),
+                "traffic": None, "launches": launches, "avg_launch_us": round(1000.0 * ms / launches, 2),
+                "flops_per_launch": flops / launches}
+    all_gemm_ms = sum(v["ms"] for k, v in kern.items() if k.startswith("gemm_"))
+    all_ms = sum(v["ms"] for v in kern.values())
+    kernels = {k: {"launches": v["launches"], "avg_us": round(1000 * v["ms"] / v["launches"], 2),
+                   "rate": round(v["work"] / (v["ms"] * 1e-3) / (1e12 if k.startswith("gemm") else 1e9), 2),
+                   "rate_unit": "TFLOP/s" if k.startswith("gemm") else "GB/s"} for k, v in sorted(kern.items())}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        import cpu_baseline
+        try:
+            cpu = cpu_baseline.reference_cpu_baseline(dims, bunch=B, threads=args.cpu_threads or None)
+        except Exception as e:  # measurement infrastructure failure must not kill the GPU line
+            cpu = {"error": str(e)[:300]}
+        if cpu is None:
+            cpu = cpu_baseline.port_cpu_baseline(dims, bunch=B)
+
+    if rank == 0:
+        line = {
+            "metric": "training frames/sec (whole node), 440->2048x4->senone MLP",
+            "value": round(value, 1), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+            "config": {"workload": f"TNet SGD step, {'x'.join(map(str, dims))} sigmoid MLP + softmax xent",
+                       "bunch_per_gpu": B, "global_bunch": B * world, "frames_resident_per_gpu": args.cache,
+                       "parallelism": f"dp{world}" + (" (RCCL all-reduce)" if world > 1 else ""),
+                       "flops_per_frame": flops_per_frame(dims),
+                       "achieved_tflops_whole_step": round(value * flops_per_frame(dims) / 1e12 / world, 2),
+                       "gemm_share_of_kernel_time": round(all_gemm_ms / all_ms, 4) if all_ms else None},
+            "roofline": roof,
+            "cpu_baseline": cpu,
+            "kernels": kernels,
+        }
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -35,6 +35,10 @@ typedef struct TnetMatrixDim_ {
   int stride;
 } TnetMatrixDim;
 
+/* objective statistics accumulator: TNET_STATS_SLOTS pairs {error, correct} of doubles */
+#define TNET_STATS_SLOTS 512
+#define TNET_STATS_WORDS (2 * TNET_STATS_SLOTS)
+
 enum {
   TNET_OK = 0,
   TNET_ERR_ARG = -1,       /* bad dimension / stride / pointer alignment */
@@ -121,6 +125,9 @@ int tnet_gather_i32(int* out, const int* in, const int* copy_from, int n, void* 
  * ---------------------------------------------------------------------------------- */
 int tnet_sgemm(char transa, char transb, int m, int n, int k, float alpha, const float* A, int lda,
                const float* B, int ldb, float beta, float* C, int ldc, void* stream);
+/* Tuning knob: force one GEMM tile configuration for every later launch in this process
+ * ("auto" = per-shape heuristic; names as in gemm_f32.hip, e.g. "g128x64s4").  Not thread-safe. */
+int tnet_gemm_config(const char* name);
 
 /* ------------------------------------------------------------------------------------
  * Fused kernels of the MI355X SGD path (no reference counterpart: each replaces a chain of
@@ -163,8 +170,10 @@ int tnet_bias_update(const float* E, TnetMatrixDim dE, float* b, float* corr_b, 
  *  _mul_elem, _add_col_sum):
  *   y = softmax(Z row)          -> written to Y if Y != NULL
  *   E = y - onehot(label)       (label < 0: all-zero target row)
- *   stats[0] += -log(max(y[label], FLT_MIN)), stats[1] += #(argmax y == argmax target)
- *   (stats: 2 doubles in device memory, accumulated with atomics; may be NULL).
+ *   xent += -log(max(y[label], FLT_MIN)), correct += #(argmax y == argmax target)
+ *   stats: device array of TNET_STATS_WORDS doubles (or NULL), accumulated without contention:
+ *   workgroup w adds its rows into slot (w % TNET_STATS_SLOTS); totals are
+ *   xent = sum_i stats[2i], correct = sum_i stats[2i+1] (tnet_stats_fetch).
  * Z == NULL: Y already holds the network output (softmax not recomputed). */
 int tnet_softmax_xent(const float* Z, TnetMatrixDim dZ, const int* labels, float* Y, int strideY, float* E,
                       int strideE, double* stats, void* stream);
@@ -174,9 +183,11 @@ int tnet_softmax_xent(const float* Z, TnetMatrixDim dZ, const int* labels, float
 int tnet_softmax_xent_dense(const float* Z, TnetMatrixDim dZ, const float* D, int strideD, float* Y,
                             int strideY, float* E, int strideE, double* stats, void* stream);
 /* Mean-square-error objective (CuMeanSquareError::Evaluate, cuObjectiveFunction.cc:28-45):
- * E = Y - D, stats[0] += sum E^2. */
+ * E = Y - D, error += sum E^2 (stats layout as above). */
 int tnet_mse(const float* Y, TnetMatrixDim dY, const float* D, int strideD, float* E, int strideE,
              double* stats, void* stream);
+/* Synchronous read-back of a stats accumulator: totals of the error and correct slots. */
+int tnet_stats_fetch(const double* stats, double* error, double* correct, void* stream);
 
 #ifdef __cplusplus
 }

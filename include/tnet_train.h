@@ -42,6 +42,11 @@ int tnet_memcpy_d2d(void* dst, const void* src, size_t bytes);
 int tnet_memset(void* dst, int value, size_t bytes);
 int tnet_set_profile(int on);                  /* CuDevice::Verbose + AccuProfile map */
 int tnet_profile_report(char* buf, int cap);
+/* Per-kernel device timing (hipEvent pairs around each launch of the fused SGD step, on the
+ * library stream).  The report lists "tag count total_ms total_work" lines (work = algorithmic
+ * FLOPs for GEMMs, bytes for HBM-bound kernels) accumulated since the last report. */
+int tnet_kernel_timing(int on);
+int tnet_kernel_timing_report(char* buf, int cap);
 /* Device-side timing of the enqueued work: start/stop return elapsed ms between two marks. */
 int tnet_timer_start(void);
 int tnet_timer_stop(float* ms);
@@ -98,6 +103,8 @@ int tnet_trainer_add_utterance(TnetTrainer* t, const float* feats, int rows, int
 int tnet_trainer_finish(TnetTrainer* t);       /* EndOfList */
 long tnet_trainer_steps(TnetTrainer* t);
 int tnet_trainer_replay(TnetTrainer* t, long nsteps); /* benchmark: more steps over the resident cache */
+/* benchmark setup: load host frames into the cache without training; returns rows taken (<0 error) */
+long tnet_trainer_prefill(TnetTrainer* t, const float* feats, int rows, int cols, int ld, const int* labels);
 int tnet_trainer_set_comm(TnetTrainer* t, TnetComm* comm);
 int tnet_trainer_trace(TnetTrainer* t, int trace);
 

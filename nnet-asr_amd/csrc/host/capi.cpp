@@ -130,6 +130,17 @@ int tnet_profile_report(char* buf, int cap) {
   TRY_END
 }
 
+int tnet_kernel_timing(int on) {
+  TRY_BEGIN CuDevice::Instantiate().KernelTiming(on != 0);
+  TRY_END
+}
+int tnet_kernel_timing_report(char* buf, int cap) {
+  TRY_BEGIN std::string s = CuDevice::Instantiate().KTCollect();
+  if ((int)s.size() >= cap) Error("tnet_kernel_timing_report: buffer too small");
+  std::strncpy(buf, s.c_str(), (size_t)cap);
+  TRY_END
+}
+
 static hipEvent_t g_t0 = nullptr, g_t1 = nullptr;
 int tnet_timer_start(void) {
   TRY_BEGIN if (!g_t0) {
@@ -337,6 +348,14 @@ long tnet_trainer_steps(TnetTrainer* t) { return t ? t->t->Steps() : -1; }
 int tnet_trainer_replay(TnetTrainer* t, long n) {
   TRY_BEGIN t->t->Replay(n);
   TRY_END
+}
+long tnet_trainer_prefill(TnetTrainer* t, const float* feats, int rows, int cols, int ld, const int* labels) {
+  try {
+    return (long)t->t->Prefill(feats, (size_t)rows, (size_t)cols, (size_t)ld, labels);
+  } catch (std::exception& e) {
+    g_last_error = e.what();
+    return TNET_ERR_RUNTIME;
+  }
 }
 int tnet_trainer_set_comm(TnetTrainer* t, TnetComm* c) {
   TRY_BEGIN t->t->SetExchange(c ? c->ex.get() : nullptr);

@@ -214,6 +214,7 @@ void CuCache::GetBunchLabels(CuMatrix<BaseFloat>& rFeatures, CuVector<int>& rLab
   rFeatures.Init(mBunchsize, mFeatures.Cols());
   rLabels.Init(mBunchsize);
   if (mRandomized) {
+    KTScope kt("gather", 2.0 * mBunchsize * mFeatures.Cols() * 4.0);
     TNET_SAFE_CALL(tnetF_randomize(rFeatures.pCUData(), mFeatures.pCUData(), mPerm.pCUData() + mExhaustPos,
                                    rFeatures.Dim(), mFeatures.Dim(), S));
     TNET_SAFE_CALL(tnet_gather_i32(rLabels.pCUData(), mLabels.pCUData(), mPerm.pCUData() + mExhaustPos,

@@ -3,6 +3,7 @@
 
 #include <iomanip>
 #include <iostream>
+#include <sstream>
 
 namespace TNet {
 
@@ -102,6 +103,57 @@ CuDevice::~CuDevice() {
   if (mWs) (void)hipFree(mWs);
   if (mOwnStream && mStream) (void)hipStreamDestroy(mStream);
   if (mVerbose) PrintProfile(std::cout);
+}
+
+hipEvent_t CuDevice::KTEvent() {
+  if (mKTNext >= mKTPool.size()) {
+    hipEvent_t e;
+    TNET_HIP_CALL(hipEventCreate(&e));
+    mKTPool.push_back(e);
+  }
+  return mKTPool[mKTNext++];
+}
+
+void CuDevice::KTRecord(const std::string& tag, double work, hipEvent_t a, hipEvent_t b) {
+  mKT.push_back(KTRec{tag, work, a, b});
+}
+
+std::string CuDevice::KTCollect() {
+  TNET_HIP_CALL(hipStreamSynchronize(mStream));
+  struct Agg {
+    long n = 0;
+    double ms = 0, work = 0;
+  };
+  std::map<std::string, Agg> agg;
+  for (auto& r : mKT) {
+    float ms = 0.f;
+    TNET_HIP_CALL(hipEventElapsedTime(&ms, r.a, r.b));
+    Agg& g = agg[r.tag];
+    g.n++;
+    g.ms += ms;
+    g.work += r.work;
+  }
+  mKT.clear();
+  mKTNext = 0;
+  std::ostringstream os;
+  os.precision(10);
+  for (auto& kv : agg) os << kv.first << " " << kv.second.n << " " << kv.second.ms << " " << kv.second.work << "\n";
+  return os.str();
+}
+
+KTScope::KTScope(const std::string& tag, double work) : mTag(tag), mWork(work) {
+  CuDevice& d = CuDevice::Instantiate();
+  if (!d.KernelTiming()) return;
+  mA = d.KTEvent();
+  TNET_HIP_CALL(hipEventRecord(mA, d.Stream()));
+}
+
+KTScope::~KTScope() {
+  if (!mA) return;
+  CuDevice& d = CuDevice::Instantiate();
+  hipEvent_t b = d.KTEvent();
+  (void)hipEventRecord(b, d.Stream());
+  d.KTRecord(mTag, mWork, mA, b);
 }
 
 CuProfileScope::CuProfileScope(const char* key) : mKey(key) {

@@ -39,6 +39,14 @@ class CuDevice {
   void PrintProfile(std::ostream& os);
   const std::map<std::string, double>& ProfileMap() const { return mProfileMap; }
 
+  // ---- per-kernel device timing (hipEvent pairs around launches; off by default)
+  void KernelTiming(bool on) { mKTOn = on; }
+  bool KernelTiming() const { return mKTOn; }
+  void KTRecord(const std::string& tag, double work, hipEvent_t a, hipEvent_t b);
+  hipEvent_t KTEvent();
+  /// sync, aggregate "tag count total_ms total_work" lines, reset
+  std::string KTCollect();
+
   void* Alloc(size_t bytes);
   void Free(void* p, size_t bytes);
   /// Scratch buffer valid until the next Workspace() call on this stream (stream-ordered reuse).
@@ -63,6 +71,27 @@ class CuDevice {
   std::map<size_t, std::vector<void*>> mFree;
   void* mWs = nullptr;
   size_t mWsBytes = 0;
+  bool mKTOn = false;
+  struct KTRec {
+    std::string tag;
+    double work;
+    hipEvent_t a, b;
+  };
+  std::vector<KTRec> mKT;
+  std::vector<hipEvent_t> mKTPool;
+  size_t mKTNext = 0;
+};
+
+/// RAII device timing of the launches enqueued in its scope (when KernelTiming is on).
+class KTScope {
+ public:
+  KTScope(const std::string& tag, double work);
+  ~KTScope();
+
+ private:
+  std::string mTag;
+  double mWork;
+  hipEvent_t mA = nullptr;
 };
 
 /// RAII profile scope: times the enqueued work of one op when profiling is on.

@@ -92,11 +92,16 @@ void CuBiasedLinearity::UpdateFrom(const CuMatrix<BaseFloat>& X, const CuMatrix<
   // bias first: it reads only E (the weight kernel rewrites W in place)
   TnetMatrixDim dE = E.Dim();
   void* ws = CuDevice::Instantiate().Workspace((size_t)tnet_col_sum_workspace(dE));
-  TNET_SAFE_CALL(tnet_bias_update(E.pCUData(), dE, mBias.pCUData(), mmt ? mBiasCorrection.pCUData() : nullptr,
-                                  nullptr, scale, mMomentum, ws, S));
+  {
+    KTScope kt("bias_update:" + std::to_string(GetNOutputs()), 4.0 * dE.rows * dE.cols);
+    TNET_SAFE_CALL(tnet_bias_update(E.pCUData(), dE, mBias.pCUData(), mmt ? mBiasCorrection.pCUData() : nullptr,
+                                    nullptr, scale, mMomentum, ws, S));
+  }
   // corrW = X^T E + mmt corrW ; W += scale corrW ; W += l2 W   -- one GEMM with an SGD epilogue.
   // With momentum 0 the correction buffer is never read (momentum is fixed per run, TNetCu.cc:322),
   // so it is not written either.
+  KTScope kt("gemm_upd:" + std::to_string(GetNInputs()) + "x" + std::to_string(GetNOutputs()),
+             2.0 * X.Rows() * GetNInputs() * GetNOutputs());
   TNET_SAFE_CALL(tnet_affine_update(X.pCUData(), X.Dim(), E.pCUData(), dE, mLinearity.pCUData(), mLinearity.Dim(),
                                     mmt ? mLinearityCorrection.pCUData() : nullptr,
                                     (int)mLinearityCorrection.Stride(), scale, mMomentum, l2, S));
@@ -110,6 +115,8 @@ void CuBiasedLinearity::ComputeGradient() {
   const CuMatrix<BaseFloat>& E = GetErrorInput();
   mGradW.Init(mLinearity.Rows(), mLinearity.Cols());
   mGradB.Init(mBias.Dim());
+  KTScope kt("gemm_grad:" + std::to_string(GetNInputs()) + "x" + std::to_string(GetNOutputs()),
+             2.0 * X.Rows() * GetNInputs() * GetNOutputs());
   TNET_SAFE_CALL(tnet_affine_grad(X.pCUData(), X.Dim(), E.pCUData(), E.Dim(), mGradW.pCUData(), mGradW.Dim(), S));
   TnetMatrixDim dE = E.Dim();
   void* ws = CuDevice::Instantiate().Workspace((size_t)tnet_col_sum_workspace(dE));

@@ -213,6 +213,8 @@ void CuNetwork::TrainBunch(const CuMatrix<BaseFloat>& X, const CuVector<int>& la
     const bool last = (l == nl - 1);
     CuMatrix<BaseFloat>& dst = last ? lin->Output() : actc->Output();
     dst.Init(rows, lin->GetNOutputs());
+    const std::string shape = std::to_string(lin->GetNInputs()) + "x" + std::to_string(lin->GetNOutputs());
+    KTScope kt("gemm_fwd:" + shape, 2.0 * rows * lin->GetNInputs() * lin->GetNOutputs());
     TNET_SAFE_CALL(tnet_affine_fwd(act->pCUData(), act->Dim(), lin->Linearity().pCUData(), lin->Linearity().Dim(),
                                    lin->Bias().pCUData(), dst.pCUData(), dst.Dim(), last ? 0 : 1, S));
     act = &dst;
@@ -229,8 +231,12 @@ void CuNetwork::TrainBunch(const CuMatrix<BaseFloat>& X, const CuVector<int>& la
     ystride = (int)smx->Output().Stride();
   }
   mGlobErr.Init(rows, GetNOutputs());
-  TNET_SAFE_CALL(tnet_softmax_xent(logits.pCUData(), logits.Dim(), labels.pCUData(), yout, ystride,
-                                   mGlobErr.pCUData(), (int)mGlobErr.Stride(), obj.DeviceStats(), S));
+  {
+    KTScope kts("softmax_xent:" + std::to_string(GetNOutputs()),
+                (double)rows * GetNOutputs() * 4.0 * (mKeepOutput ? 3 : 2) + rows * 4.0);
+    TNET_SAFE_CALL(tnet_softmax_xent(logits.pCUData(), logits.Dim(), labels.pCUData(), yout, ystride,
+                                     mGlobErr.pCUData(), (int)mGlobErr.Stride(), obj.DeviceStats(), S));
+  }
   obj.AddFrames(rows);
   if (!train) return;
 
@@ -243,6 +249,8 @@ void CuNetwork::TrainBunch(const CuMatrix<BaseFloat>& X, const CuVector<int>& la
     if (!stopper && l > 0) {
       eo = mErr[l].get();
       eo->Init(rows, lin->GetNInputs());
+      KTScope kt("gemm_bwd:" + std::to_string(lin->GetNInputs()) + "x" + std::to_string(lin->GetNOutputs()),
+                 2.0 * rows * lin->GetNInputs() * lin->GetNOutputs());
       // E_l = (E_{l+1} W_l^T) .* y_l (1 - y_l)   (backprop through <biasedlinearity> and the <sigmoid> below)
       TNET_SAFE_CALL(tnet_affine_bwd(err->pCUData(), err->Dim(), lin->Linearity().pCUData(), lin->Linearity().Dim(),
                                      acts[l]->pCUData(), (int)acts[l]->Stride(), eo->pCUData(), eo->Dim(), 1, S));

@@ -15,22 +15,21 @@ CuObjectiveFunction* CuObjectiveFunction::Factory(ObjFunType type) {
 
 CuObjectiveFunction::CuObjectiveFunction() {
   CuDevice& d = CuDevice::Instantiate();
-  mDevStats = (double*)d.Alloc(64);
-  TNET_HIP_CALL(hipMemsetAsync(mDevStats, 0, 64, d.Stream()));
+  mDevStats = (double*)d.Alloc(TNET_STATS_WORDS * sizeof(double));
+  TNET_HIP_CALL(hipMemsetAsync(mDevStats, 0, TNET_STATS_WORDS * sizeof(double), d.Stream()));
 }
 
 CuObjectiveFunction::~CuObjectiveFunction() {
-  if (mDevStats) CuDevice::Instantiate().Free(mDevStats, 64);
+  if (mDevStats) CuDevice::Instantiate().Free(mDevStats, TNET_STATS_WORDS * sizeof(double));
 }
 
 void CuObjectiveFunction::Sync() {
   CuDevice& d = CuDevice::Instantiate();
-  double h[2];
-  TNET_HIP_CALL(hipMemcpyAsync(h, mDevStats, sizeof h, hipMemcpyDeviceToHost, d.Stream()));
-  TNET_HIP_CALL(hipStreamSynchronize(d.Stream()));
-  TNET_HIP_CALL(hipMemsetAsync(mDevStats, 0, sizeof h, d.Stream()));
-  mError += h[0];
-  mCorrect += h[1];
+  double e = 0.0, c = 0.0;
+  TNET_SAFE_CALL(tnet_stats_fetch(mDevStats, &e, &c, d.Stream()));
+  TNET_HIP_CALL(hipMemsetAsync(mDevStats, 0, TNET_STATS_WORDS * sizeof(double), d.Stream()));
+  mError += e;
+  mCorrect += c;
 }
 
 double CuObjectiveFunction::GetError() {

@@ -69,6 +69,15 @@ void CuTrainer::Finish() {
   }
 }
 
+size_t CuTrainer::Prefill(const float* feats, size_t rows, size_t cols, size_t ld, const int* labels) {
+  if (mCache.Full()) return 0;
+  const size_t space = mOpt.cachesize - mCache.IntakePos();
+  const size_t take = rows < space ? rows : space;
+  mCache.AddDataHost(feats, take, cols, ld, labels);
+  if (mCache.Full() && mOpt.randomize) mCache.Randomize();
+  return take;
+}
+
 void CuTrainer::Replay(long n) {
   for (long i = 0; i < n; i++) {
     if (mCache.Empty()) {

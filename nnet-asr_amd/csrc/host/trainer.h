@@ -41,6 +41,9 @@ class CuTrainer {
   void Finish();
   /// Steps (bunches) trained so far.
   long Steps() const { return mSteps; }
+  /// Fill the cache from host utterances WITHOUT training (benchmark setup); returns the
+  /// number of rows taken.  The cache is shuffled once filled.
+  size_t Prefill(const float* feats, size_t rows, size_t cols, size_t ld, const int* labels);
   /// Benchmark replay: run n more SGD steps over the resident cache contents, re-shuffling
   /// (same RNG stream) every time the cache is exhausted.  The cache must have been filled.
   void Replay(long n);

@@ -12,46 +12,69 @@
 
 namespace tnetk {
 
-constexpr int CS_COLS = 64;     // columns per block (one per lane)
+constexpr int CS_COLS = 64;     // scalar path: columns per block (one per lane)
 constexpr int CS_WAVES = 4;     // row sub-groups per block
-constexpr int CS_ROWS = 128;    // rows per slab
+constexpr int CS_ROWS = 32;     // rows per slab (8 per row sub-group: 8 loads in flight per lane)
 
 static int cs_slabs(int rows) {
   int s = cdiv(rows, CS_ROWS);
-  if (s > 64) s = 64;
+  if (s > 256) s = 256;
   if (s < 1) s = 1;
   return s;
 }
 
-// partial[s][c] = sum of rows of slab s in column c (fixed order)
+// partial[s][c] = sum of rows of slab s in column c (fixed order: row sub-group w takes rows
+// r0+w, r0+w+4, ...; the 4 sub-group sums are added in order)
+template <bool V4>
 __global__ __launch_bounds__(256) void colsum_partial_kernel(const float* __restrict__ M, TnetMatrixDim d,
                                                              float* __restrict__ partial, int slabs) {
-  __shared__ float red[CS_WAVES][CS_COLS];
+  constexpr int CW = V4 ? 4 : 1;                 // columns per lane
+  __shared__ float red[CS_WAVES][CS_COLS * CW];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int c = blockIdx.x * CS_COLS + lane;
+  const int c0 = (blockIdx.x * CS_COLS + lane) * CW;
   const int s = blockIdx.y;
   const int rows_per = (d.rows + slabs - 1) / slabs;
   const int r0 = s * rows_per, r1 = min(d.rows, r0 + rows_per);
-  float acc = 0.f;
-  if (c < d.cols)
-    for (int r = r0 + w; r < r1; r += CS_WAVES) acc += M[(long)r * d.stride + c];
-  red[w][lane] = acc;
-  __syncthreads();
-  if (w == 0 && c < d.cols) {
-    float t = red[0][lane];
+  float acc[CW];
 #pragma unroll
-    for (int k = 1; k < CS_WAVES; ++k) t += red[k][lane];
-    partial[(long)s * d.cols + c] = t;
+  for (int k = 0; k < CW; ++k) acc[k] = 0.f;
+  if (c0 < d.cols) {
+#pragma unroll 8
+    for (int r = r0 + w; r < r1; r += CS_WAVES) {
+      if (V4) {
+        const f32x4 v = *reinterpret_cast<const f32x4*>(M + (long)r * d.stride + c0);
+#pragma unroll
+        for (int k = 0; k < CW; ++k) acc[k] += v[k];
+      } else {
+        acc[0] += M[(long)r * d.stride + c0];
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < CW; ++k) red[w][lane * CW + k] = acc[k];
+  __syncthreads();
+  if (w == 0) {
+#pragma unroll
+    for (int k = 0; k < CW; ++k) {
+      const int c = c0 + k;
+      if (c < d.cols) {
+        float t = red[0][lane * CW + k];
+#pragma unroll
+        for (int q = 1; q < CS_WAVES; ++q) t += red[q][lane * CW + k];
+        partial[(long)s * d.cols + c] = t;
+      }
+    }
   }
 }
 
 // mode 0: v = alpha*sum + beta*v ; mode 1: bias update (c = sum + mmt*corr; b += scale*c; corr=c)
 // mode 2: grad_out = sum
-__global__ __launch_bounds__(256) void colsum_final_kernel(const float* __restrict__ partial, int slabs, int cols,
+__global__ __launch_bounds__(64) void colsum_final_kernel(const float* __restrict__ partial, int slabs, int cols,
                                                            int mode, float alpha, float beta, float* __restrict__ v,
                                                            float* __restrict__ corr, float scale, float mmt) {
   for (int c = blockIdx.x * blockDim.x + threadIdx.x; c < cols; c += gridDim.x * blockDim.x) {
     double s = 0.0;
+#pragma unroll 8
     for (int k = 0; k < slabs; ++k) s += (double)partial[(long)k * cols + c];
     if (mode == 0) {
       v[c] = (float)(alpha * s + (beta == 0.f ? 0.0 : (double)beta * v[c]));
@@ -88,12 +111,17 @@ static int colsum_run(const float* M, TnetMatrixDim d, void* workspace, hipStrea
   float* ws = workspace ? (float*)workspace : get_ws((long)slabs * d.cols * 4);
   if (!ws) return TNET_ERR_RUNTIME;
   if (d.rows > 0) {
-    colsum_partial_kernel<<<dim3(cdiv(d.cols, CS_COLS), slabs), 256, 0, st>>>(M, d, ws, slabs);
+    const bool v4 = (d.cols & 3) == 0 && (d.stride & 3) == 0 && ((uintptr_t)M & 15) == 0;
+    if (v4)
+      colsum_partial_kernel<true><<<dim3(cdiv(d.cols, CS_COLS * 4), slabs), 256, 0, st>>>(M, d, ws, slabs);
+    else
+      colsum_partial_kernel<false><<<dim3(cdiv(d.cols, CS_COLS), slabs), 256, 0, st>>>(M, d, ws, slabs);
     TNET_LAUNCH_CHECK();
   } else {
     if (hipMemsetAsync(ws, 0, (size_t)slabs * d.cols * 4, st) != hipSuccess) return TNET_ERR_RUNTIME;
   }
-  colsum_final_kernel<<<cdiv(d.cols, 256), 256, 0, st>>>(ws, slabs, d.cols, mode, alpha, beta, v, corr, scale, mmt);
+  // one 64-lane wave per 64 columns: enough workgroups to spread the slab reads over many CUs
+  colsum_final_kernel<<<cdiv(d.cols, 64), 64, 0, st>>>(ws, slabs, d.cols, mode, alpha, beta, v, corr, scale, mmt);
   TNET_LAUNCH_CHECK();
   return TNET_OK;
 }
@@ -129,9 +157,14 @@ __global__ __launch_bounds__(256) void softmax_xent_kernel(const float* __restri
                                                            float* __restrict__ Y, int strideY,
                                                            float* __restrict__ E, int strideE,
                                                            double* __restrict__ stats, int vec4) {
-  const int lane = threadIdx.x & 63;
+  __shared__ double red[2][4];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int row = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  if (row >= d.rows) return;
+  if (row >= d.rows) {
+    if (lane == 0) { red[0][wv] = 0.0; red[1][wv] = 0.0; }
+    __syncthreads();
+    return;
+  }
   const int N = d.cols;
   const float* src = Z ? Z + (long)row * d.stride : Y + (long)row * strideY;
   const bool cached = vec4 && N <= SX_MAXV4 * 256;
@@ -226,30 +259,41 @@ __global__ __launch_bounds__(256) void softmax_xent_kernel(const float* __restri
     des = ad.i;
   }
   if (KIND == 1) xent = wave_sum_d(xent);
-  if (lane == 0 && stats) {
+  if (lane == 0) {
     if (KIND == 0 && t >= 0) {
       const float yt = Z ? expf(src[t] - m) / sum : src[t];
       xent = -(double)logf(fmaxf(yt, FLT_MIN));
     }
-    atomicAdd(stats + 0, xent);
-    atomicAdd(stats + 1, (ay.i == des) ? 1.0 : 0.0);
+    red[0][wv] = xent;
+    red[1][wv] = (ay.i == des) ? 1.0 : 0.0;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0 && stats) {
+    const int slot = blockIdx.x % TNET_STATS_SLOTS;
+    atomicAdd(stats + 2 * slot, red[0][0] + red[0][1] + red[0][2] + red[0][3]);
+    atomicAdd(stats + 2 * slot + 1, red[1][0] + red[1][1] + red[1][2] + red[1][3]);
   }
 }
 
 __global__ __launch_bounds__(256) void mse_kernel(const float* __restrict__ Y, TnetMatrixDim d,
                                                   const float* __restrict__ D, int strideD, float* __restrict__ E,
                                                   int strideE, double* __restrict__ stats) {
-  const int lane = threadIdx.x & 63;
+  __shared__ double red[4];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int row = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  if (row >= d.rows) return;
   double s = 0.0;
-  for (int c = lane; c < d.cols; c += 64) {
-    const float e = Y[(long)row * d.stride + c] - D[(long)row * strideD + c];
-    if (E) E[(long)row * strideE + c] = e;
-    s += (double)(e * e);
+  if (row < d.rows) {
+    for (int c = lane; c < d.cols; c += 64) {
+      const float e = Y[(long)row * d.stride + c] - D[(long)row * strideD + c];
+      if (E) E[(long)row * strideE + c] = e;
+      s += (double)(e * e);
+    }
+    s = wave_sum_d(s);
   }
-  s = wave_sum_d(s);
-  if (lane == 0 && stats) atomicAdd(stats, s);
+  if (lane == 0) red[wv] = s;
+  __syncthreads();
+  if (threadIdx.x == 0 && stats)
+    atomicAdd(stats + 2 * (blockIdx.x % TNET_STATS_SLOTS), red[0] + red[1] + red[2] + red[3]);
 }
 
 __global__ __launch_bounds__(256) void check_class_kernel(const float* __restrict__ out,
@@ -337,6 +381,22 @@ extern "C" int tnet_mse(const float* Y, TnetMatrixDim dY, const float* D, int st
   if (!dY.rows) return TNET_OK;
   mse_kernel<<<cdiv((long)dY.rows * 64, 256), 256, 0, (hipStream_t)stream>>>(Y, dY, D, strideD, E, strideE, stats);
   TNET_LAUNCH_CHECK();
+  return TNET_OK;
+}
+
+extern "C" int tnet_stats_fetch(const double* stats, double* error, double* correct, void* stream) {
+  static double h[TNET_STATS_WORDS];
+  if (!stats) return TNET_ERR_ARG;
+  if (hipMemcpyAsync(h, stats, sizeof h, hipMemcpyDeviceToHost, (hipStream_t)stream) != hipSuccess)
+    return TNET_ERR_RUNTIME;
+  if (hipStreamSynchronize((hipStream_t)stream) != hipSuccess) return TNET_ERR_RUNTIME;
+  double e = 0.0, c = 0.0;
+  for (int i = 0; i < TNET_STATS_SLOTS; i++) {
+    e += h[2 * i];
+    c += h[2 * i + 1];
+  }
+  if (error) *error = e;
+  if (correct) *correct = c;
   return TNET_OK;
 }
 

@@ -56,8 +56,7 @@ class DeviceArray:
         a = np.asarray(a)
         if a.ndim == 1:
             a = a.reshape(1, -1) if a.dtype != np.int32 else a.reshape(-1, 1)
-        d = cls(a.shape[0], a.shape[1], a.dtype, stride=stride if stride is not None else
-                (pad_stride(a.shape[1]) if a.shape[1] > 1 else 1))
+        d = cls(a.shape[0], a.shape[1], a.dtype, stride=stride if stride is not None else pad_stride(a.shape[1]))
         d.upload(a)
         return d
 

@@ -57,6 +57,7 @@ _SIGS = {
     "tnetF_randomize": (i32, [vp, vp, vp, MatrixDim, MatrixDim, vp]),
     "tnet_gather_i32": (i32, [vp, vp, vp, i32, vp]),
     "tnet_sgemm": (i32, [C.c_char, C.c_char, i32, i32, i32, f32, vp, i32, vp, i32, f32, vp, i32, vp]),
+    "tnet_gemm_config": (i32, [C.c_char_p]),
     "tnet_affine_fwd": (i32, [vp, MatrixDim, vp, MatrixDim, vp, vp, MatrixDim, i32, vp]),
     "tnet_affine_bwd": (i32, [vp, MatrixDim, vp, MatrixDim, vp, i32, vp, MatrixDim, i32, vp]),
     "tnet_affine_update": (i32, [vp, MatrixDim, vp, MatrixDim, vp, MatrixDim, vp, i32, f32, f32, f32, vp]),
@@ -66,6 +67,7 @@ _SIGS = {
     "tnet_softmax_xent": (i32, [vp, MatrixDim, vp, vp, i32, vp, i32, vp, vp]),
     "tnet_softmax_xent_dense": (i32, [vp, MatrixDim, vp, i32, vp, i32, vp, i32, vp, vp]),
     "tnet_mse": (i32, [vp, MatrixDim, vp, i32, vp, i32, vp, vp]),
+    "tnet_stats_fetch": (i32, [vp, dp, dp, vp]),
     # tnet_train.h
     "tnet_last_error": (C.c_char_p, []),
     "tnet_device_count": (i32, [C.POINTER(i32)]),
@@ -80,6 +82,8 @@ _SIGS = {
     "tnet_memset": (i32, [vp, i32, C.c_size_t]),
     "tnet_set_profile": (i32, [i32]),
     "tnet_profile_report": (i32, [C.c_char_p, i32]),
+    "tnet_kernel_timing": (i32, [i32]),
+    "tnet_kernel_timing_report": (i32, [C.c_char_p, i32]),
     "tnet_timer_start": (i32, []),
     "tnet_timer_stop": (i32, [C.POINTER(f32)]),
     "tnet_net_read": (vp, [C.c_char_p]),
@@ -112,6 +116,7 @@ _SIGS = {
     "tnet_trainer_finish": (i32, [vp]),
     "tnet_trainer_steps": (i64, [vp]),
     "tnet_trainer_replay": (i32, [vp, i64]),
+    "tnet_trainer_prefill": (i64, [vp, vp, i32, i32, i32, vp]),
     "tnet_trainer_set_comm": (i32, [vp, vp]),
     "tnet_trainer_trace": (i32, [vp, i32]),
     "tnet_comm_unique_id": (i32, [C.c_char_p]),

@@ -38,6 +38,7 @@ def lib():
                                    C.c_int, C.c_float, C.c_float, C.c_float, C.c_int, C.c_int, f32p, f32p,
                                    C.POINTER(C.c_double), C.POINTER(C.c_long)]
         L.orc_mlp_forward.argtypes = [C.c_int, i32p, C.c_void_p, C.c_void_p, f32p, C.c_int, f32p]
+        L.orc_write_random_nnet.argtypes = [C.c_char_p, i32p, C.c_int, C.c_ulonglong]
         _LIB = L
     return _LIB
 
@@ -145,3 +146,9 @@ class MLP:
         Y = np.empty((X.shape[0], self.dims[-1]), np.float32)
         lib().orc_mlp_forward(len(self.W), self.dims, _ptrs(self.W), _ptrs(self.b), X, X.shape[0], Y)
         return Y
+
+
+def write_random_nnet(path, dims, seed=2):
+    d = np.ascontiguousarray(dims, np.int32)
+    if lib().orc_write_random_nnet(path.encode(), d, len(d), seed) != 0:
+        raise OSError(f"cannot write {path}")

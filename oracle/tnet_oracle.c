@@ -281,3 +281,35 @@ int orc_mlp_forward(int nl, const int* dims, float** W, float** b, const float* 
   free(buf);
   return 0;
 }
+
+/* ---------------------------------------------------------------------------------------
+ * Fast writer of a gen_mlp_init-style (--gauss --negbias) .nnet text file for the CPU baseline
+ * (tools/init/gen_mlp_init.py:36-68 layout: <biasedlinearity> nOut nIn / m nOut nIn / rows /
+ * v nOut ...).  Random weights matter for timing: an all-zero init drives the backpropagated
+ * errors of the lower layers into fp32 denormals, which makes x86 BLAS ~10x slower.
+ * Box-Muller on a 64-bit LCG; 6 significant digits like the reference writer.
+ * ------------------------------------------------------------------------------------- */
+#include <stdio.h>
+int orc_write_random_nnet(const char* path, const int* dims, int n, unsigned long long seed) {
+  FILE* f = fopen(path, "w");
+  if (!f) return -1;
+  unsigned long long s = seed * 6364136223846793005ull + 1442695040888963407ull;
+#define ORC_U01() ((s = s * 6364136223846793005ull + 1442695040888963407ull), ((double)(s >> 11) + 0.5) / 9007199254740992.0)
+  for (int l = 0; l + 1 < n; l++) {
+    int ni = dims[l], no = dims[l + 1];
+    fprintf(f, "<biasedlinearity> %d %d\nm %d %d\n", no, ni, no, ni);
+    for (int r = 0; r < no; r++) {
+      for (int c = 0; c < ni; c++) {
+        double u1 = ORC_U01(), u2 = ORC_U01();
+        double g = sqrt(-2.0 * log(u1)) * cos(6.283185307179586 * u2);
+        fprintf(f, "%g ", 0.1 * g);
+      }
+      fputc('\n', f);
+    }
+    fprintf(f, "v %d  ", no);
+    for (int c = 0; c < no; c++) fprintf(f, "%g ", (l + 2 == n) ? 0.0 : ORC_U01() / 5.0 - 4.1);
+    fprintf(f, "\n<%s> %d %d\n", (l + 2 == n) ? "softmax" : "sigmoid", no, no);
+  }
+#undef ORC_U01
+  return fclose(f) == 0 ? 0 : -1;
+}

@@ -32,13 +32,23 @@ def gemm_ref(ta, tb, A, B):
     return a @ b, np.abs(a) @ np.abs(b)
 
 
+GEMM_CFGS = ["auto", "128x64w4", "64x64w4", "128x64w8", "g128x64s3", "g64x64s3", "g64x64s4b"]
+
+
+@pytest.fixture(params=GEMM_CFGS)
+def gemm_cfg(request):
+    check(lib().tnet_gemm_config(request.param.encode()))
+    yield request.param
+    check(lib().tnet_gemm_config(b"auto"))
+
+
 GEMM_SHAPES = [(1, 1, 1), (7, 5, 3), (33, 65, 31), (64, 64, 32), (130, 70, 598), (200, 135, 1024),
                (256, 384, 440), (1024, 2048, 2048), (1024, 4000, 2048), (2048, 2048, 1024), (440, 2048, 1024)]
 
 
 @pytest.mark.parametrize("ta,tb", [("N", "N"), ("N", "T"), ("T", "N"), ("T", "T")])
 @pytest.mark.parametrize("M,N,K", GEMM_SHAPES)
-def test_sgemm(ta, tb, M, N, K):
+def test_sgemm(ta, tb, M, N, K, gemm_cfg):
     A = rnd((K, M) if ta == "T" else (M, K), 1)
     B = rnd((N, K) if tb == "T" else (K, N), 2)
     C0 = rnd((M, N), 3)
@@ -71,7 +81,7 @@ def test_sgemm_rejects_misaligned_stride():
 
 @pytest.mark.parametrize("act", [0, 1])
 @pytest.mark.parametrize("rows,n_in,n_out", [(16, 24, 32), (1024, 440, 2048), (960, 598, 1024), (33, 1024, 135)])
-def test_affine_fwd(act, rows, n_in, n_out):
+def test_affine_fwd(act, rows, n_in, n_out, gemm_cfg):
     X, W, b = rnd((rows, n_in), 6), rnd((n_in, n_out), 7, 0.1), rnd(n_out, 8)
     dX, dW, dY = DeviceArray.from_numpy(X), DeviceArray.from_numpy(W), DeviceArray(rows, n_out)
     db = DeviceArray.vector(b)
@@ -87,7 +97,7 @@ def test_affine_fwd(act, rows, n_in, n_out):
 
 
 @pytest.mark.parametrize("rows,n_in,n_out", [(16, 32, 10), (1024, 2048, 2048), (1024, 2048, 4000)])
-def test_affine_bwd_dsig(rows, n_in, n_out):
+def test_affine_bwd_dsig(rows, n_in, n_out, gemm_cfg):
     E, W = rnd((rows, n_out), 9), rnd((n_in, n_out), 10, 0.1)
     Yb = 1 / (1 + np.exp(-rnd((rows, n_in), 11)))
     dE, dW, dY, dO = (DeviceArray.from_numpy(E), DeviceArray.from_numpy(W), DeviceArray.from_numpy(Yb),
@@ -100,7 +110,7 @@ def test_affine_bwd_dsig(rows, n_in, n_out):
 
 @pytest.mark.parametrize("mmt", [0.0, 0.5])
 @pytest.mark.parametrize("rows,n_in,n_out", [(16, 24, 32), (1024, 2048, 2048), (1024, 440, 2048), (960, 1024, 135)])
-def test_affine_update(mmt, rows, n_in, n_out):
+def test_affine_update(mmt, rows, n_in, n_out, gemm_cfg):
     X, E = rnd((rows, n_in), 12), rnd((rows, n_out), 13, 0.01)
     W, corr = rnd((n_in, n_out), 14, 0.1), rnd((n_in, n_out), 15, 0.01)
     scale, l2 = -0.3 / rows, -1e-4
@@ -125,15 +135,15 @@ def test_softmax_xent_labels(rows, cols):
     lab[::7] = -1  # unlabeled frames: all-zero target rows
     dZ, dL = DeviceArray.from_numpy(Z), DeviceArray.vector(lab)
     dY, dE = DeviceArray(rows, cols), DeviceArray(rows, cols)
-    stats = DeviceArray(1, 4, np.float64, stride=4)
+    stats = DeviceArray(1, 1024, np.float64, stride=1024)
     check(lib().tnet_softmax_xent(dZ.ptr, dZ.dim, dL.ptr, dY.ptr, dY.stride, dE.ptr, dE.stride, stats.ptr, S()))
     Yref = orc.softmax(Z)
     Eref, xent, correct = orc.xent_eval(Yref, lab)
     np.testing.assert_allclose(dY.numpy(), Yref, rtol=2e-5, atol=1e-9)
     np.testing.assert_allclose(dE.numpy(), Eref, rtol=2e-5, atol=1e-8)
     s = stats.numpy()[0]
-    np.testing.assert_allclose(s[0], xent, rtol=1e-5, atol=1e-5)
-    assert int(round(s[1])) == correct
+    np.testing.assert_allclose(s[0::2].sum(), xent, rtol=1e-5, atol=1e-5)
+    assert int(round(s[1::2].sum())) == correct
 
 
 def test_softmax_xent_extreme_logits():
@@ -144,11 +154,12 @@ def test_softmax_xent_extreme_logits():
     lab = np.full(rows, 5, np.int32)
     dZ, dL = DeviceArray.from_numpy(Z), DeviceArray.vector(lab)
     dE = DeviceArray(rows, cols)
-    stats = DeviceArray(1, 4, np.float64, stride=4)
+    stats = DeviceArray(1, 1024, np.float64, stride=1024)
     check(lib().tnet_softmax_xent(dZ.ptr, dZ.dim, dL.ptr, None, 0, dE.ptr, dE.stride, stats.ptr, S()))
-    s = stats.numpy()[0]
-    np.testing.assert_allclose(s[0], -rows * np.log(np.float32(1.1754944e-38)), rtol=1e-6)
-    assert s[1] == 0
+    e, c = C.c_double(), C.c_double()
+    check(lib().tnet_stats_fetch(stats.ptr, C.byref(e), C.byref(c), S()))
+    np.testing.assert_allclose(e.value, -rows * np.log(np.float32(1.1754944e-38)), rtol=1e-6)
+    assert c.value == 0
 
 
 @pytest.mark.parametrize("rows,cols", [(1, 1), (1024, 2048), (960, 135), (3, 4000), (2049, 77)])

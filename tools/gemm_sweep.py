@@ -1,0 +1,78 @@
+#!/usr/bin/env python3
+"""Sweep the GEMM tile configurations (TNET_GEMM_CFG) over the SGD-step shapes on the GPU.
+
+Each configuration runs in its own process (the config is read once per process); every shape is
+timed with hipEvents on the library stream over `iters` back-to-back launches of the FUSED kernels
+the training step uses (affine fwd + sigmoid, affine bwd + diff-sigmoid, affine update + SGD)."""
+import json
+import os
+import subprocess
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CFGS = ["g128x64s3", "g64x64s3", "g64x64s4", "g128x64s3b", "g64x64s3b", "g64x64s4b", "g64x64s4+noload",
+        "g64x64s4b+noload"]
+# (kind, rows, n_in, n_out): fwd/bwd/upd of each layer of 440 -> 2048x4 -> 4000 at bunch 1024
+SHAPES = [("fwd", 1024, 2048, 2048), ("bwd", 1024, 2048, 2048), ("upd", 1024, 2048, 2048),
+          ("fwd", 1024, 2048, 4000), ("bwd", 1024, 2048, 4000), ("upd", 1024, 2048, 4000),
+          ("fwd", 1024, 440, 2048), ("upd", 1024, 440, 2048)]
+
+CHILD = r'''
+import sys, json, ctypes as C
+sys.path.insert(0, sys.argv[1] + "/nnet-asr_amd")
+import numpy as np
+from tnet_amd import DeviceArray
+from tnet_amd._lib import lib, check
+shapes = json.loads(sys.argv[2]); iters = int(sys.argv[3])
+S = lib().tnet_stream()
+out = []
+for kind, rows, ni, no in shapes:
+    rng = np.random.default_rng(0)
+    X = DeviceArray.from_numpy(rng.standard_normal((rows, ni)).astype(np.float32))
+    W = DeviceArray.from_numpy((0.05 * rng.standard_normal((ni, no))).astype(np.float32))
+    E = DeviceArray.from_numpy((0.01 * rng.standard_normal((rows, no))).astype(np.float32))
+    b = DeviceArray.vector(np.zeros(no, np.float32))
+    Y = DeviceArray(rows, no)
+    Eo = DeviceArray(rows, ni)
+    def run():
+        if kind == "fwd":
+            check(lib().tnet_affine_fwd(X.ptr, X.dim, W.ptr, W.dim, b.ptr, Y.ptr, Y.dim, 1, S))
+        elif kind == "bwd":
+            check(lib().tnet_affine_bwd(E.ptr, E.dim, W.ptr, W.dim, X.ptr, X.stride, Eo.ptr, Eo.dim, 1, S))
+        else:
+            check(lib().tnet_affine_update(X.ptr, X.dim, E.ptr, E.dim, W.ptr, W.dim, None, 0, -1e-6, 0.0, 0.0, S))
+    for _ in range(3): run()
+    ms = C.c_float()
+    check(lib().tnet_timer_start())
+    for _ in range(iters): run()
+    check(lib().tnet_timer_stop(C.byref(ms)))
+    us = 1000.0 * ms.value / iters
+    out.append([kind, rows, ni, no, us, 2.0 * rows * ni * no / (us * 1e-6) / 1e12])
+print("RESULT " + json.dumps(out))
+'''
+
+
+def main():
+    iters = int(sys.argv[1]) if len(sys.argv) > 1 else 20
+    cfgs = sys.argv[2].split(",") if len(sys.argv) > 2 else CFGS
+    res = {}
+    for cfg in cfgs:
+        env = dict(os.environ, TNET_GEMM_CFG=cfg.split("+")[0])
+        if cfg.endswith("+noload"):
+            env["TNET_GEMM_DIAG_NOLOAD"] = "1"
+        p = subprocess.run([sys.executable, "-c", CHILD, REPO, json.dumps(SHAPES), str(iters)], env=env,
+                           capture_output=True, text=True, timeout=300)
+        line = [l for l in p.stdout.splitlines() if l.startswith("RESULT ")]
+        if p.returncode != 0 or not line:
+            print(cfg, "FAILED", p.stderr[-500:], flush=True)
+            if p.returncode < 0 or p.returncode in (134, 139):
+                break
+            continue
+        res[cfg] = json.loads(line[0][7:])
+        for kind, rows, ni, no, us, tf in res[cfg]:
+            print(f"{cfg:12s} {kind} {rows}x{ni}x{no}: {us:8.1f} us {tf:6.1f} TF/s", flush=True)
+    print("SWEEP " + json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()
