@@ -106,6 +106,8 @@ int tnet_trainer_replay(TnetTrainer* t, long nsteps); /* benchmark: more steps o
 /* benchmark setup: load host frames into the cache without training; returns rows taken (<0 error) */
 long tnet_trainer_prefill(TnetTrainer* t, const float* feats, int rows, int cols, int ld, const int* labels);
 int tnet_trainer_set_comm(TnetTrainer* t, TnetComm* comm);
+/* data-parallel steps this rank joined without a bunch of its own (zero gradient) */
+long tnet_trainer_empty_steps(TnetTrainer* t);
 int tnet_trainer_trace(TnetTrainer* t, int trace);
 
 /* ---- data parallel (no reference counterpart: Platform.h:143-391 is the CPU analogue) ---- */
@@ -114,6 +116,22 @@ TnetComm* tnet_comm_create(int rank, int world, const char id[128]);
 int tnet_comm_free(TnetComm* comm);
 int tnet_comm_allreduce_host(TnetComm* comm, double* v, int n);
 int tnet_comm_allreduce_device(TnetComm* comm, float* dbuf, long n);
+/* Host-transport communicator: gradients are staged through host memory and summed in place by
+ * fn(user, buf, n, is_double) (float32 when is_double == 0); fn returns 0 on success.  For
+ * transports without RCCL (gloo, MPI) and multi-process tests on one device; PCIe-bound. */
+typedef int (*tnet_host_allreduce_fn)(void* user, void* buf, long n, int is_double);
+TnetComm* tnet_comm_create_host(int rank, int world, tnet_host_allreduce_fn fn, void* user);
+/* One round of the data-parallel step plan (collective over the communicator): this rank holds
+ * n bunches, final != 0 if it has reached the end of its utterances.  Returns the round's step
+ * count, the number of ranks holding a bunch at each step (ranks_at_step[cap]) and whether all
+ * ranks are final.  Pure host logic. */
+int tnet_dp_plan_round(TnetComm* comm, long n, int final, long* steps, int* ranks_at_step, long cap,
+                       int* all_final);
+/* Network-level data parallelism: tnet_net_train_bunch all-reduces the weight gradients over
+ * comm (NULL = local update); a rank without a bunch calls tnet_net_train_empty with the global
+ * row count of the step. */
+int tnet_net_set_comm(TnetNetwork* net, TnetComm* comm);
+int tnet_net_train_empty(TnetNetwork* net, TnetComm* comm, long global_rows);
 
 #ifdef __cplusplus
 }

@@ -30,6 +30,7 @@ struct TnetNetwork {
   CuNetwork net;
   CuMatrix<BaseFloat> in_view, out, err_view, tmp_view;
   CuVector<int> lab_view;
+  GradExchange* comm = nullptr;
 };
 struct TnetObjective {
   std::unique_ptr<CuObjectiveFunction> obj;
@@ -40,7 +41,9 @@ struct TnetTrainer {
   std::unique_ptr<CuTrainer> t;
 };
 struct TnetComm {
-  std::unique_ptr<RcclExchange> ex;
+  std::unique_ptr<GradExchange> ex;
+  RcclExchange* rccl = nullptr;  // one of these two is set
+  HostExchange* host = nullptr;
 };
 
 extern "C" {
@@ -252,7 +255,18 @@ int tnet_net_train_bunch(TnetNetwork* h, TnetObjective* o, const float* dX, int 
                          int train) {
   TRY_BEGIN CuMatrix<BaseFloat>::MakeView(h->in_view, const_cast<float*>(dX), rows, h->net.GetNInputs(), ldx);
   CuVector<int>::MakeView(h->lab_view, const_cast<int*>(dLabels), rows);
-  h->net.TrainBunch(h->in_view, h->lab_view, *o->obj, train != 0);
+  h->net.TrainBunch(h->in_view, h->lab_view, *o->obj, train != 0, train ? h->comm : nullptr);
+  TRY_END
+}
+int tnet_net_set_comm(TnetNetwork* h, TnetComm* c) {
+  TRY_BEGIN h->comm = c ? c->ex.get() : nullptr;
+  TRY_END
+}
+int tnet_net_train_empty(TnetNetwork* h, TnetComm* c, long global_rows) {
+  TRY_BEGIN if (!c) Error("tnet_net_train_empty: no communicator");
+  c->ex->SetStepRows((size_t)global_rows);
+  h->net.TrainEmpty(*c->ex);
+  c->ex->SetStepRows(0);
   TRY_END
 }
 int tnet_net_keep_output(TnetNetwork* h, int keep) {
@@ -361,6 +375,7 @@ int tnet_trainer_set_comm(TnetTrainer* t, TnetComm* c) {
   TRY_BEGIN t->t->SetExchange(c ? c->ex.get() : nullptr);
   TRY_END
 }
+long tnet_trainer_empty_steps(TnetTrainer* t) { return t ? t->t->EmptySteps() : -1; }
 int tnet_trainer_trace(TnetTrainer* t, int trace) {
   TRY_BEGIN t->t->Cache().Trace(trace);
   TRY_END
@@ -374,10 +389,29 @@ int tnet_comm_unique_id(char out[128]) {
 TnetComm* tnet_comm_create(int rank, int world, const char id[128]) {
   try {
     std::unique_ptr<TnetComm> h(new TnetComm);
-    h->ex.reset(new RcclExchange(rank, world, id));
+    h->rccl = new RcclExchange(rank, world, id);
+    h->ex.reset(h->rccl);
     return h.release();
   }
   TRY_END_PTR
+}
+TnetComm* tnet_comm_create_host(int rank, int world, tnet_host_allreduce_fn fn, void* user) {
+  try {
+    if (!fn || world < 1 || rank < 0 || rank >= world) Error("tnet_comm_create_host: bad arguments");
+    std::unique_ptr<TnetComm> h(new TnetComm);
+    h->host = new HostExchange(rank, world, fn, user);
+    h->ex.reset(h->host);
+    return h.release();
+  }
+  TRY_END_PTR
+}
+int tnet_dp_plan_round(TnetComm* c, long n, int final, long* steps, int* ranks_at_step, long cap, int* all_final) {
+  TRY_BEGIN DpRoundPlan plan = DpPlanRound(*c->ex, n, final != 0);
+  *steps = plan.steps;
+  *all_final = plan.all_final ? 1 : 0;
+  if (plan.steps > cap) Error("tnet_dp_plan_round: ranks_at_step capacity too small");
+  for (long j = 0; j < plan.steps; j++) ranks_at_step[j] = plan.ranks_at_step[(size_t)j];
+  TRY_END
 }
 int tnet_comm_free(TnetComm* c) {
   TRY_BEGIN delete c;
@@ -388,7 +422,8 @@ int tnet_comm_allreduce_host(TnetComm* c, double* v, int n) {
   TRY_END
 }
 int tnet_comm_allreduce_device(TnetComm* c, float* dbuf, long n) {
-  TRY_BEGIN c->ex->AllReduceDevice(dbuf, (size_t)n);
+  TRY_BEGIN if (c->rccl) c->rccl->AllReduceDevice(dbuf, (size_t)n);
+  else c->host->AllReduceDevice(dbuf, (size_t)n);
   TRY_END
 }
 

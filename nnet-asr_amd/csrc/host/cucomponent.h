@@ -136,6 +136,8 @@ class CuUpdatableComponent : public CuComponent {
   virtual void ApplyGradient(size_t frames) { Error(std::string(GetName()) + ": ApplyGradient not supported"); }
   /// Gradient buffers of this component (valid after ComputeGradient()).
   virtual std::vector<CuParamBlock> GradientBlocks() { return {}; }
+  /// Zero the gradient buffers (a data-parallel rank without a bunch contributes nothing).
+  void ZeroGradient();
 
   void LearnRate(BaseFloat rate) { mLearningRate = rate; }
   BaseFloat LearnRate() const { return mLearningRate; }

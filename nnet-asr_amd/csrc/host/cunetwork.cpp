@@ -186,6 +186,32 @@ void CuNetwork::TrainBunchGeneric(const CuMatrix<BaseFloat>& X, const CuVector<i
   if (train) Backpropagate(mGlobErr);
 }
 
+void CuNetwork::TrainEmpty(GradExchange& exchange) {
+  if (!IsFusableMLP()) Error("CuNetwork::TrainEmpty: data-parallel training needs the sigmoid-MLP topology");
+  const int nl = (int)mNetComponents.size() / 2;
+  // same layer order (top down to the stopper) as TrainBunch, so the collectives pair up
+  for (int l = nl - 1; l >= 0; l--) {
+    auto* lin = static_cast<CuBiasedLinearity*>(mNetComponents[2 * l]);
+    if (lin->LearnRate() > 0.0f) {
+      lin->ZeroGradient();
+      exchange.Submit(*lin);
+    }
+    if (lin == mpPropagErrorStopper) break;
+  }
+  exchange.WaitAll();
+  const size_t grows = exchange.GlobalRows(0);
+  for (int l = nl - 1; l >= 0; l--) {
+    auto* lin = static_cast<CuBiasedLinearity*>(mNetComponents[2 * l]);
+    if (lin->LearnRate() > 0.0f) lin->ApplyGradient(grows);
+    if (lin == mpPropagErrorStopper) break;
+  }
+}
+
+void CuUpdatableComponent::ZeroGradient() {
+  for (auto& b : GradientBlocks())
+    TNET_HIP_CALL(hipMemsetAsync(b.grad, 0, (size_t)b.n * sizeof(float), CuDevice::Instantiate().Stream()));
+}
+
 void CuNetwork::TrainBunch(const CuMatrix<BaseFloat>& X, const CuVector<int>& labels, CuObjectiveFunction& obj,
                            bool train, GradExchange* exchange) {
   if (!IsFusableMLP() || obj.GetTypeId() != CuObjectiveFunction::CROSS_ENTROPY) {

@@ -67,6 +67,9 @@ class CuNetwork {
   /// With `exchange` set, gradients are all-reduced over data-parallel ranks before the update
   /// and `global_rows` frames enter the GRADDIVFRM normalisation.
   /// `train` = false: cross-validation (forward + objective only).
+  /// Data-parallel step of a rank without a bunch: zero gradients into the exchange, then the
+  /// same update as the ranks that trained (GradExchange::GlobalRows).
+  void TrainEmpty(GradExchange& exchange);
   void TrainBunch(const CuMatrix<BaseFloat>& X, const CuVector<int>& labels, CuObjectiveFunction& obj,
                   bool train = true, GradExchange* exchange = nullptr);
   /// Keep the softmax output in the <softmax> component after TrainBunch (costs one extra

@@ -9,6 +9,8 @@
 #pragma once
 
 #include <cstddef>
+#include <functional>
+#include <vector>
 
 namespace TNet {
 
@@ -24,10 +26,35 @@ class GradExchange {
   virtual void Submit(CuUpdatableComponent& comp) = 0;
   /// Make the compute stream wait until every submitted reduction has finished.
   virtual void WaitAll() = 0;
-  /// Frames of the global bunch (sum over ranks) for the GRADDIVFRM normalisation.
-  virtual size_t GlobalRows(size_t local_rows) = 0;
-  /// Sum small host statistics over ranks (epoch-end MergeStats); blocking.
+  /// Sum small host statistics over ranks (epoch-end MergeStats, step planning); blocking.
   virtual void AllReduceHost(double* v, int n) = 0;
+
+  /// Frames of the global bunch (sum over ranks) for the GRADDIVFRM normalisation: the row
+  /// count planned for this step (SetStepRows), else every rank is assumed to hold local_rows.
+  size_t GlobalRows(size_t local_rows) const {
+    return mStepRows ? mStepRows : local_rows * (size_t)WorldSize();
+  }
+  void SetStepRows(size_t rows) { mStepRows = rows; }
+
+ private:
+  size_t mStepRows = 0;
 };
+
+/// One round of the data-parallel step plan (see DpPlanRound).
+struct DpRoundPlan {
+  long steps = 0;                 // max over ranks of the bunches of this round
+  std::vector<int> ranks_at_step; // [steps]: ranks that hold a bunch at step j
+  bool all_final = true;          // every rank has reached the end of its utterance list
+};
+
+/// Ranks fill their caches from different utterance shards, so at a cache drain they may hold
+/// different numbers of bunches (always at the last, partial drain; and a rank may run out of
+/// utterances whole drains earlier than another).  Every rank calls this once per drain with
+/// its bunch count and whether this is its final drain; all ranks get the same plan: the round
+/// lasts max(n_r) steps, a rank past its own n_r contributes a zero gradient, and step j
+/// normalises by the rows of the ranks_at_step[j] ranks that trained.  A rank that has finished
+/// keeps joining rounds with n = 0 until all_final.  (The reference's Platform slices one
+/// global bunch over threads instead and never sees unequal shards: Platform.h:206-236.)
+DpRoundPlan DpPlanRound(GradExchange& ex, long n, bool final);
 
 }  // namespace TNet

@@ -3,6 +3,7 @@
 
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <cstring>
 #include <sys/time.h>
 
@@ -38,10 +39,28 @@ void CuTrainer::Step() {
   mSteps++;
 }
 
-void CuTrainer::DrainCache() {
+bool CuTrainer::DrainCache(bool final) {
   if (mOpt.randomize) mCache.Randomize();
-  while (!mCache.Empty()) Step();
   mTrainedSinceFill = true;
+  if (DataParallel()) return DpRound((long)(mCache.IntakePos() / mCache.Bunchsize()), final);
+  while (!mCache.Empty()) Step();
+  return true;
+}
+
+bool CuTrainer::DpRound(long n, bool final) {
+  const DpRoundPlan plan = DpPlanRound(*mExchange, n, final);
+  const size_t B = mCache.Bunchsize();
+  for (long j = 0; j < plan.steps; j++) {
+    mExchange->SetStepRows((size_t)plan.ranks_at_step[j] * B);
+    if (j < n) {
+      Step();
+    } else {
+      mNet->TrainEmpty(*mExchange);
+      mEmptySteps++;
+    }
+  }
+  mExchange->SetStepRows(0);
+  return plan.all_final;
 }
 
 void CuTrainer::AddUtterance(const float* feats, size_t rows, size_t cols, size_t ld, const int* labels) {
@@ -53,20 +72,17 @@ void CuTrainer::AddUtterance(const float* feats, size_t rows, size_t cols, size_
   if (rows == 0) return;
   mCache.AddDataHost(feats, rows, cols, ld, labels);
   mTrainedSinceFill = false;
-  if (mCache.Full()) DrainCache();
+  if (mCache.Full()) DrainCache(false);
 }
 
 void CuTrainer::Finish() {
   // TNetCu.cc:376-441: after EndOfList the (partial) cache filled so far is drained once;
   // a leftover still pending after a full cache was drained is dropped.
-  if (!mTrainedSinceFill && mCache.IntakePos() > 0) DrainCache();
-  if (mExchange) {
-    double v[1] = {(double)mSteps};
-    double mx[1] = {v[0]};
-    mExchange->AllReduceHost(mx, 1);
-    if (mx[0] != v[0] * mExchange->WorldSize())
-      Error("CuTrainer: data-parallel ranks took different numbers of steps (unequal shards)");
-  }
+  bool all_final = true;
+  if (!mTrainedSinceFill && mCache.IntakePos() > 0) all_final = DrainCache(true);
+  else if (DataParallel()) all_final = DpRound(0, true);
+  // data-parallel: keep joining the other ranks' drains (zero gradients) until all are done
+  while (!all_final) all_final = DpRound(0, true);
 }
 
 size_t CuTrainer::Prefill(const float* feats, size_t rows, size_t cols, size_t ld, const int* labels) {
@@ -86,6 +102,51 @@ void CuTrainer::Replay(long n) {
     }
     Step();
   }
+}
+
+// ======================================================================================
+// data-parallel step plan
+// ======================================================================================
+DpRoundPlan DpPlanRound(GradExchange& ex, long n, bool final) {
+  const int world = ex.WorldSize(), rank = ex.Rank();
+  if (n < 0) Error("DpPlanRound: negative bunch count");
+  std::vector<double> info(2 * (size_t)world, 0.0);  // [n_r, final_r] per rank, summed = gathered
+  info[2 * rank] = (double)n;
+  info[2 * rank + 1] = final ? 1.0 : 0.0;
+  ex.AllReduceHost(info.data(), (int)info.size());
+  DpRoundPlan plan;
+  for (int r = 0; r < world; r++) {
+    plan.steps = std::max(plan.steps, (long)info[2 * r]);
+    plan.all_final = plan.all_final && info[2 * r + 1] != 0.0;
+  }
+  plan.ranks_at_step.assign((size_t)plan.steps, 0);
+  for (int r = 0; r < world; r++)
+    for (long j = 0; j < (long)info[2 * r]; j++) plan.ranks_at_step[(size_t)j]++;
+  return plan;
+}
+
+// ======================================================================================
+// host-transport exchange
+// ======================================================================================
+void HostExchange::Submit(CuUpdatableComponent& comp) {
+  CuDevice& dev = CuDevice::Instantiate();
+  TNET_HIP_CALL(hipStreamSynchronize(dev.Stream()));
+  for (auto& b : comp.GradientBlocks()) AllReduceDevice(b.grad, (size_t)b.n);
+}
+
+void HostExchange::AllReduceDevice(float* buf, size_t n) {
+  CuDevice& dev = CuDevice::Instantiate();
+  mStage.resize(n);
+  TNET_HIP_CALL(hipMemcpyAsync(mStage.data(), buf, n * sizeof(float), hipMemcpyDeviceToHost, dev.Stream()));
+  TNET_HIP_CALL(hipStreamSynchronize(dev.Stream()));
+  if (mFn(mUser, mStage.data(), (long)n, 0) != 0) Error("HostExchange: all-reduce callback failed");
+  TNET_HIP_CALL(hipMemcpyAsync(buf, mStage.data(), n * sizeof(float), hipMemcpyHostToDevice, dev.Stream()));
+  TNET_HIP_CALL(hipStreamSynchronize(dev.Stream()));
+}
+
+void HostExchange::AllReduceHost(double* v, int n) {
+  if (n <= 0) return;
+  if (mFn(mUser, v, (long)n, 1) != 0) Error("HostExchange: all-reduce callback failed");
 }
 
 // ======================================================================================

@@ -41,6 +41,8 @@ class CuTrainer {
   void Finish();
   /// Steps (bunches) trained so far.
   long Steps() const { return mSteps; }
+  /// Data-parallel steps this rank joined without a bunch of its own (zero gradient).
+  long EmptySteps() const { return mEmptySteps; }
   /// Fill the cache from host utterances WITHOUT training (benchmark setup); returns the
   /// number of rows taken.  The cache is shuffled once filled.
   size_t Prefill(const float* feats, size_t rows, size_t cols, size_t ld, const int* labels);
@@ -51,7 +53,11 @@ class CuTrainer {
   Rng48& Rng() { return mRng; }
 
  private:
-  void DrainCache();
+  /// Shuffle and train every bunch of the cache; in data-parallel mode one planned round
+  /// (DpPlanRound).  Returns whether every rank has reached its final drain.
+  bool DrainCache(bool final);
+  bool DpRound(long n, bool final);
+  bool DataParallel() const { return mExchange && !mOpt.crossval && mExchange->WorldSize() > 1; }
   void Step();
 
   CuNetwork* mNet;
@@ -63,7 +69,31 @@ class CuTrainer {
   CuMatrix<BaseFloat> mFeats;
   CuVector<int> mLabels;
   long mSteps = 0;
+  long mEmptySteps = 0;
   bool mTrainedSinceFill = false;
+};
+
+/// Host-transport exchange: gradients are staged to host memory and summed by a caller-supplied
+/// all-reduce (e.g. torch.distributed gloo, MPI).  Synchronous and PCIe-bound: for multi-node
+/// transports without RCCL and for exercising the data-parallel path with several processes on
+/// one device in tests.  fn(user, buf, n, is_double) must sum buf over ranks in place, return 0.
+typedef int (*HostAllReduceFn)(void* user, void* buf, long n, int is_double);
+class HostExchange : public GradExchange {
+ public:
+  HostExchange(int rank, int world, HostAllReduceFn fn, void* user)
+      : mRank(rank), mWorld(world), mFn(fn), mUser(user) {}
+  int Rank() const override { return mRank; }
+  int WorldSize() const override { return mWorld; }
+  void Submit(CuUpdatableComponent& comp) override;
+  void WaitAll() override {}
+  void AllReduceHost(double* v, int n) override;
+  void AllReduceDevice(float* buf, size_t n);
+
+ private:
+  int mRank, mWorld;
+  HostAllReduceFn mFn;
+  void* mUser;
+  std::vector<float> mStage;
 };
 
 /// RCCL all-reduce over xGMI, one communicator per rank (one process per GPU).
@@ -76,7 +106,6 @@ class RcclExchange : public GradExchange {
   int WorldSize() const override { return mWorld; }
   void Submit(CuUpdatableComponent& comp) override;
   void WaitAll() override;
-  size_t GlobalRows(size_t local_rows) override { return local_rows * (size_t)mWorld; }
   void AllReduceHost(double* v, int n) override;
   /// all-reduce (sum) of a device float buffer on the communication stream, synchronous
   void AllReduceDevice(float* buf, size_t n);

@@ -8,12 +8,12 @@ DeviceArray (hipMalloc through the library), never by a CPU fallback.
 from __future__ import annotations
 
 import ctypes as C
-from typing import Optional, Sequence
+from typing import Callable, Optional, Sequence
 
 import numpy as np
 
 from . import formats  # noqa: F401  (host formats; no device code)
-from ._lib import LIB_PATH, MatrixDim, TnetError, check, check_ptr, header_symbols, lib
+from ._lib import HOST_ALLREDUCE_FN, LIB_PATH, MatrixDim, TnetError, check, check_ptr, header_symbols, lib
 
 __all__ = ["DeviceArray", "Network", "Objective", "Trainer", "Comm", "TnetError", "synchronize", "pad_stride",
            "device_count", "version", "LIB_PATH", "header_symbols", "formats"]
@@ -170,6 +170,15 @@ class Network:
         check(lib().tnet_net_train_bunch(self.h, obj.h, X.ptr, X.rows, X.stride, labels.ptr, int(train)),
               "train_bunch")
 
+    def set_comm(self, comm: Optional["Comm"]) -> None:
+        """train_bunch all-reduces the weight gradients over `comm` (None: local update)."""
+        self._comm = comm
+        check(lib().tnet_net_set_comm(self.h, comm.h if comm else None), "set_comm")
+
+    def train_empty(self, comm: "Comm", global_rows: int) -> None:
+        """Data-parallel step of a rank without a bunch (zero gradient, same update)."""
+        check(lib().tnet_net_train_empty(self.h, comm.h, global_rows), "train_empty")
+
     def keep_output(self, keep: bool = True) -> None:
         check(lib().tnet_net_keep_output(self.h, int(keep)), "keep_output")
 
@@ -254,10 +263,15 @@ class Trainer:
     def steps(self) -> int:
         return lib().tnet_trainer_steps(self.h)
 
+    @property
+    def empty_steps(self) -> int:
+        return lib().tnet_trainer_empty_steps(self.h)
+
     def replay(self, n: int) -> None:
         check(lib().tnet_trainer_replay(self.h, n), "replay")
 
     def set_comm(self, comm: Optional["Comm"]) -> None:
+        self._comm = comm
         check(lib().tnet_trainer_set_comm(self.h, comm.h if comm else None), "set_comm")
 
     def __del__(self):
@@ -269,8 +283,17 @@ class Trainer:
             pass
 
 
+def shard_utterances(items: Sequence, rank: int, world: int) -> list:
+    """Utterance sharding of the data-parallel path: round-robin over ranks in list order, the
+    way the reference Platform deals utterances to its worker threads (Platform.h:206-236,
+    `thr = (thr+1) % num_thr_`)."""
+    if not 0 <= rank < world:
+        raise ValueError(f"rank {rank} outside world {world}")
+    return list(items)[rank::world]
+
+
 class Comm:
-    """RCCL communicator (one process per GPU)."""
+    """Data-parallel communicator: RCCL (one process per GPU), or a host transport (Comm.host)."""
 
     @staticmethod
     def unique_id() -> bytes:
@@ -280,6 +303,40 @@ class Comm:
 
     def __init__(self, rank: int, world: int, uid: bytes):
         self.h = check_ptr(lib().tnet_comm_create(rank, world, C.c_char_p(uid)), "tnet_comm_create")
+
+    @classmethod
+    def host(cls, rank: int, world: int, allreduce: Callable[[np.ndarray], None]) -> "Comm":
+        """Host-transport communicator: `allreduce(a)` must sum the numpy array `a` (float32 or
+        float64) over ranks in place, e.g. through torch.distributed with the gloo backend."""
+        self = cls.__new__(cls)
+
+        def _fn(user, buf, n, is_double):
+            try:
+                ct = C.c_double if is_double else C.c_float
+                a = np.ctypeslib.as_array(C.cast(buf, C.POINTER(ct)), shape=(n,))
+                allreduce(a)
+                return 0
+            except Exception:  # an exception cannot cross the C boundary
+                import traceback
+                traceback.print_exc()
+                return 1
+
+        self._fn = HOST_ALLREDUCE_FN(_fn)  # keep the trampoline alive as long as the communicator
+        self.h = check_ptr(lib().tnet_comm_create_host(rank, world, C.cast(self._fn, C.c_void_p), None),
+                           "tnet_comm_create_host")
+        return self
+
+    def plan_round(self, n: int, final: bool, cap: int = 1 << 16):
+        """One round of the data-parallel step plan (collective): (ranks_at_step, all_final)."""
+        steps = C.c_long(0)
+        allf = C.c_int(0)
+        buf = np.zeros(cap, np.int32)
+        check(lib().tnet_dp_plan_round(self.h, n, int(final), C.byref(steps), buf.ctypes.data_as(C.POINTER(C.c_int)),
+                                       cap, C.byref(allf)), "dp_plan_round")
+        return buf[: steps.value].copy(), bool(allf.value)
+
+    def allreduce_device(self, a: "DeviceArray") -> None:
+        check(lib().tnet_comm_allreduce_device(self.h, a.ptr, a.rows * a.stride), "allreduce_device")
 
     def allreduce_host(self, v: np.ndarray) -> np.ndarray:
         v = np.ascontiguousarray(v, np.float64).copy()

@@ -124,7 +124,15 @@ _SIGS = {
     "tnet_comm_free": (i32, [vp]),
     "tnet_comm_allreduce_host": (i32, [vp, dp, i32]),
     "tnet_comm_allreduce_device": (i32, [vp, vp, i64]),
+    "tnet_comm_create_host": (vp, [i32, i32, vp, vp]),
+    "tnet_dp_plan_round": (i32, [vp, i64, i32, C.POINTER(i64), C.POINTER(i32), i64, C.POINTER(i32)]),
+    "tnet_net_set_comm": (i32, [vp, vp]),
+    "tnet_net_train_empty": (i32, [vp, vp, i64]),
+    "tnet_trainer_empty_steps": (i64, [vp]),
 }
+
+# int fn(void* user, void* buf, long n, int is_double) -- tnet_host_allreduce_fn
+HOST_ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_long, C.c_int)
 
 
 def header_symbols():

@@ -83,6 +83,12 @@ def reference_cpu_baseline(dims, bunch=1024, threads=None, bunches=(6, 22), seed
         init = os.path.join(tmp, "init.nnet")
         import oracle as orc
         orc.write_random_nnet(init, dims, seed=2)
+        # untimed warm-up run: pages MKL and the binary in from a cold image (on a fresh box the
+        # first run is otherwise seconds slower, which corrupts the two-run slope)
+        d = os.path.join(tmp, "warm")
+        os.makedirs(d)
+        files = _write_corpus(d, bunch + cache, dims[0], dims[-1], seed)
+        _run_tnet(files, init, d, bunch, cache, threads)
         res = []
         for nb in bunches:
             d = os.path.join(tmp, f"run{nb}")
@@ -91,6 +97,8 @@ def reference_cpu_baseline(dims, bunch=1024, threads=None, bunches=(6, 22), seed
             files = _write_corpus(d, nb * bunch + cache, dims[0], dims[-1], seed)
             res.append(_run_tnet(files, init, d, bunch, cache, threads))
         (t1, fps1, f1, w1), (t2, fps2, f2, w2) = res
+        if t2 <= t1 or f2 <= f1:
+            raise RuntimeError(f"CPU baseline runs not monotone: {f1} frames {t1}s vs {f2} frames {t2}s")
         compute_fps = (f2 - f1) / (t2 - t1)
         return {"value": round(compute_fps, 1), "unit": "frames/s", "cores": threads, "kind": "reference",
                 "sample": (f"reference TNet (src/TNet.cc, TNetLib Platform --THREADS={threads}, MKL 1 thread/worker) "

@@ -1,0 +1,91 @@
+"""Data-parallel host logic on CPU, world_size 2 over gloo (no GPU).
+
+Runs the PRODUCT's step planner (trainer.cpp DpPlanRound through tnet_dp_plan_round) in two
+processes whose host-transport communicator sums over torch.distributed/gloo, and checks it
+against the pure-Python statement of the protocol in tests/dp_sim.py, plus utterance sharding.
+"""
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+import dp_sim  # noqa: E402
+
+# per rank: the (n, final) rounds it submits; rank 1 runs out of utterances two drains early
+SCENARIO = {0: [(4, False), (4, False), (4, False), (2, True)],
+            1: [(4, False), (3, True), (0, True), (0, True)]}
+
+WORKER = r'''
+import os, sys, json
+import numpy as np
+import torch, torch.distributed as dist
+sys.path.insert(0, os.path.join(sys.argv[1], "nnet-asr_amd"))
+import tnet_amd
+rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+dist.init_process_group("gloo", rank=rank, world_size=world)
+def allreduce(a):
+    t = torch.from_numpy(a)
+    dist.all_reduce(t)
+comm = tnet_amd.Comm.host(rank, world, allreduce)
+rounds = json.loads(sys.argv[2])[str(rank)]
+out = []
+for n, final in rounds:
+    steps, allf = comm.plan_round(n, final)
+    out.append([steps.tolist(), allf])
+    if allf:
+        break
+# device-free float32 + float64 sums through the same callback
+v = comm.allreduce_host(np.array([rank + 1.0, 2.0]))
+print(json.dumps({"rounds": out, "sum": v.tolist()}))
+dist.destroy_process_group()
+'''
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_shard_utterances_round_robin():
+    from tnet_amd import shard_utterances
+    assert shard_utterances(range(7), 0, 3) == [0, 3, 6]
+    assert shard_utterances(range(7), 2, 3) == [2, 5]
+    allr = sorted(sum((shard_utterances(range(11), r, 4) for r in range(4)), []))
+    assert allr == list(range(11))
+    with pytest.raises(ValueError):
+        shard_utterances(range(3), 2, 2)
+
+
+def test_rank_rounds_and_plan():
+    assert dp_sim.rank_rounds(10, 1024, 256) == [(4, False), (4, False), (2, True)]
+    assert dp_sim.rank_rounds(8, 1024, 256) == [(4, False), (4, False), (0, True)]
+    p = dp_sim.plan([[(4, False), (2, True)], [(3, True)]])
+    assert p == [[(0, 1), (0, 1), (0, 1), (0,)], [(0,), (0,)]]
+
+
+def test_dp_plan_gloo_world2():
+    import json
+    port = _free_port()
+    env_base = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE="2",
+                    OMP_NUM_THREADS="1")
+    repo = os.path.dirname(HERE)
+    procs = [subprocess.Popen([sys.executable, "-c", WORKER, repo, json.dumps(SCENARIO)],
+                              env=dict(env_base, RANK=str(r)), stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                              text=True) for r in range(2)]
+    outs = []
+    for p in procs:
+        o, e = p.communicate(timeout=240)
+        assert p.returncode == 0, e[-3000:]
+        outs.append(json.loads(o.strip().splitlines()[-1]))
+    expected = dp_sim.plan([SCENARIO[0], SCENARIO[1]])
+    for o in outs:
+        got = [[c for c in steps] for steps, _ in o["rounds"]]
+        assert got == [[len(s) for s in rnd] for rnd in expected]
+        assert [f for _, f in o["rounds"]] == [False] * (len(expected) - 1) + [True]
+        assert o["sum"] == [3.0, 4.0]

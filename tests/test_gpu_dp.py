@@ -1,0 +1,112 @@
+"""Data-parallel path on the GPU: two ranks (processes) on one device, weight gradients summed by
+the host-transport communicator over gloo (the RCCL communicator needs one GPU per rank; its
+world-1 case is covered below).  Expected results come from the CPU oracle on the global bunches
+(tests/dp_sim.py).  Tolerance: rtol 2e-4 / atol 1e-6 on parameters (fp32 GEMM order + the two
+partial gradient sums vs one)."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+import dp_cases  # noqa: E402
+import dp_sim  # noqa: E402
+import oracle as orc  # noqa: E402
+from tnet_amd import Comm, DeviceArray, Network, Objective, Trainer, formats  # noqa: E402
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _run_ranks(mode, tmp_path, world=2):
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), WORLD_SIZE=str(world),
+               OMP_NUM_THREADS="1")
+    outs = [str(tmp_path / f"{mode}_r{r}.npz") for r in range(world)]
+    procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "dp_worker.py"), mode, outs[r]],
+                              env=dict(env, RANK=str(r)), stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+             for r in range(world)]
+    for p in procs:
+        try:
+            _, e = p.communicate(timeout=300)
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise
+        assert p.returncode == 0, e[-4000:]
+    res = []
+    for o in outs:
+        z = np.load(o, allow_pickle=False)
+        res.append((json.loads(str(z["meta"])), {k: z[k] for k in z.files if k != "meta"}))
+    return res
+
+
+def _assert_params(got, net, rtol=2e-4, atol=1e-6):
+    for k in range(len(net.W)):
+        np.testing.assert_allclose(got[f"W{k}"], net.W[k], rtol=rtol, atol=atol)
+        np.testing.assert_allclose(got[f"b{k}"], net.b[k], rtol=rtol, atol=atol)
+
+
+def test_dp_network_two_ranks_matches_global_bunch(tmp_path):
+    c = dp_cases.NET
+    ranks = _run_ranks("net", tmp_path)
+    # every rank holds identical parameters
+    for k in ranks[0][1]:
+        np.testing.assert_array_equal(ranks[0][1][k], ranks[1][1][k])
+    net = orc.MLP.from_layers(formats.gen_mlp_init(c["dims"], seed=c["init_seed"]))
+    for X, L, _ in dp_cases.net_bunches(2):
+        net.step(X, L, c["lr"], graddivfrm=True)
+    _assert_params(ranks[0][1], net)
+    assert ranks[0][0]["frames"] == c["bunch"] * c["steps"]
+    assert ranks[1][0]["frames"] == c["bunch"] * (c["steps"] - 1)
+
+
+def test_dp_trainer_uneven_shards(tmp_path):
+    c = dp_cases.TRAINER
+    ranks = _run_ranks("trainer", tmp_path)
+    for k in ranks[0][1]:
+        np.testing.assert_array_equal(ranks[0][1][k], ranks[1][1][k])
+    corpus = dp_cases.trainer_corpus()
+    layers = formats.gen_mlp_init(c["dims"], seed=c["init_seed"])
+    net, nb, rounds = dp_sim.expected_dp_training(orc, layers, corpus, 2, c["bunch"], c["cache"],
+                                                  [c["seed"], c["seed"] + 1], c["lr"])
+    assert nb[0] > nb[1], "the case must exercise unequal shards"
+    total_steps = sum(len(r) for r in rounds)
+    for r in range(2):
+        assert ranks[r][0]["steps"] == nb[r]
+        assert ranks[r][0]["steps"] + ranks[r][0]["empty_steps"] == total_steps
+    _assert_params(ranks[0][1], net)
+    np.testing.assert_allclose(ranks[0][0]["xent"] + ranks[1][0]["xent"], net.xent, rtol=1e-4)
+    assert ranks[0][0]["frames"] + ranks[1][0]["frames"] == net.frames
+
+
+def test_dp_rccl_world1_equals_local_update():
+    """RCCL communicator at world 1: the split ComputeGradient -> all-reduce -> ApplyGradient path
+    gives the fused local update's result."""
+    c = dp_cases.NET
+    comm = Comm(0, 1, Comm.unique_id())
+    nets = []
+    for use_comm in (False, True):
+        net = Network.from_layers(formats.gen_mlp_init(c["dims"], seed=c["init_seed"]))
+        net.set_learn_rate(c["lr"])
+        net.set_momentum(0.5)
+        if use_comm:
+            net.set_comm(comm)
+        obj = Objective()
+        for X, L, active in dp_cases.net_bunches(1):
+            net.train_bunch(obj, DeviceArray.from_numpy(X), DeviceArray.vector(L))
+        nets.append(net.linear_params())
+    for (W0, b0), (W1, b1) in zip(*nets):
+        np.testing.assert_allclose(W1, W0, rtol=1e-5, atol=1e-7)
+        np.testing.assert_allclose(b1, b0, rtol=1e-5, atol=1e-7)
+    v = comm.allreduce_host(np.array([1.5, -2.0]))
+    assert v.tolist() == [1.5, -2.0]
