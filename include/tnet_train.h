@@ -131,6 +131,9 @@ int tnet_dp_plan_round(TnetComm* comm, long n, int final, long* steps, int* rank
  * comm (NULL = local update); a rank without a bunch calls tnet_net_train_empty with the global
  * row count of the step. */
 int tnet_net_set_comm(TnetNetwork* net, TnetComm* comm);
+/* Rows of the global bunch of the next steps (GRADDIVFRM normalisation) when the ranks' bunches
+ * differ in size; 0 restores the default local rows x world size. */
+int tnet_comm_set_step_rows(TnetComm* comm, long global_rows);
 int tnet_net_train_empty(TnetNetwork* net, TnetComm* comm, long global_rows);
 
 #ifdef __cplusplus

@@ -405,6 +405,11 @@ TnetComm* tnet_comm_create_host(int rank, int world, tnet_host_allreduce_fn fn, 
   }
   TRY_END_PTR
 }
+int tnet_comm_set_step_rows(TnetComm* c, long global_rows) {
+  TRY_BEGIN if (global_rows < 0) Error("tnet_comm_set_step_rows: negative row count");
+  c->ex->SetStepRows((size_t)global_rows);
+  TRY_END
+}
 int tnet_dp_plan_round(TnetComm* c, long n, int final, long* steps, int* ranks_at_step, long cap, int* all_final) {
   TRY_BEGIN DpRoundPlan plan = DpPlanRound(*c->ex, n, final != 0);
   *steps = plan.steps;

@@ -75,6 +75,11 @@ void CuCache::BeginIntake() {
     mIntakePos += leftover;
   }
   mLeftoverRows = 0;
+  // an utterance whose leftover alone fills the cache leaves no space for the next one: the
+  // reference asserts here (cuCache.cc:97 assert(cache_space > 0), Cache.cc:117 on the CPU)
+  if (mIntakePos >= mCachesize)
+    Error("CuCache: the previous segment's leftover fills the whole cache (cache smaller than the longest "
+          "utterance; the reference asserts cache_space > 0, cuCache.cc:97)");
 }
 
 void CuCache::AddData(const CuMatrix<BaseFloat>& rFeatures, const CuMatrix<BaseFloat>& rDesired) {

@@ -335,6 +335,10 @@ class Comm:
                                        cap, C.byref(allf)), "dp_plan_round")
         return buf[: steps.value].copy(), bool(allf.value)
 
+    def set_step_rows(self, global_rows: int) -> None:
+        """Rows of the global bunch for the next steps' GRADDIVFRM division (0 = rows x world)."""
+        check(lib().tnet_comm_set_step_rows(self.h, global_rows), "set_step_rows")
+
     def allreduce_device(self, a: "DeviceArray") -> None:
         check(lib().tnet_comm_allreduce_device(self.h, a.ptr, a.rows * a.stride), "allreduce_device")
 

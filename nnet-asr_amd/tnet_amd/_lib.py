@@ -127,6 +127,7 @@ _SIGS = {
     "tnet_comm_create_host": (vp, [i32, i32, vp, vp]),
     "tnet_dp_plan_round": (i32, [vp, i64, i32, C.POINTER(i64), C.POINTER(i32), i64, C.POINTER(i32)]),
     "tnet_net_set_comm": (i32, [vp, vp]),
+    "tnet_comm_set_step_rows": (i32, [vp, i64]),
     "tnet_net_train_empty": (i32, [vp, vp, i64]),
     "tnet_trainer_empty_steps": (i64, [vp]),
 }

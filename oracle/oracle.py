@@ -104,6 +104,8 @@ def epoch_schedule(lens, cachesize, bunch, seed, randomize=True):
     cap = int(lens.sum()) // bunch + 1
     out = np.zeros(cap * bunch, np.int32)
     nb = lib().orc_epoch_schedule(lens, len(lens), cachesize, bunch, seed, int(randomize), out, cap)
+    if nb < 0:
+        raise ValueError("utterance leftover fills the whole cache (the reference asserts cache_space > 0)")
     return out[: nb * bunch].reshape(nb, bunch)
 
 

@@ -64,6 +64,9 @@ long orc_epoch_schedule(const int* lens, int nutt, int cachesize, int bunch, lon
     int intake = 0;
     if (nleft > 0) {
       int l = nleft < cachesize ? nleft : cachesize;
+      /* a leftover that fills the whole cache leaves cache_space == 0 for the next utterance:
+       * the reference aborts (cuCache.cc:97 / Cache.cc:117 assert(cache_space > 0)) */
+      if (l == cachesize && u < nutt) { free(leftover); free(cache); free(perm); return -1; }
       memcpy(cache, leftover, sizeof(int) * (size_t)l);
       intake = l;
       free(leftover); leftover = NULL; nleft = 0;

@@ -9,7 +9,7 @@ NET = dict(dims=[40, 96, 96, 12], init_seed=5, lr=0.5, bunch=64, steps=4, solo_s
 # trainer level, uneven shards: 9 utterances round-robin -> rank 0 gets 5, rank 1 gets 4 (and fewer
 # frames), so rank 1 reaches its final drain first and joins the remaining steps empty
 TRAINER = dict(dims=[40, 96, 96, 12], init_seed=7, lr=0.004, gdf=False, bunch=64, cache=512, seed=123,
-               n_utts=9, corpus_seed=3, min_len=150, max_len=700)
+               n_utts=9, corpus_seed=3, min_len=100, max_len=450)
 
 
 def net_bunches(world):

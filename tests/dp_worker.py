@@ -44,8 +44,10 @@ def main():
             if rank in active:
                 k = active.index(rank)
                 B = c["bunch"]
+                comm.set_step_rows(len(active) * B)
                 net.train_bunch(obj, DeviceArray.from_numpy(X[k * B:(k + 1) * B]),
                                 DeviceArray.vector(L[k * B:(k + 1) * B]))
+                comm.set_step_rows(0)
             else:
                 net.train_empty(comm, len(active) * c["bunch"])
         res["frames"] = obj.stats()[1]

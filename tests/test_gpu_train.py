@@ -148,3 +148,16 @@ def test_epoch_matches_reference_report(golden_dir, name):
     assert abs(100.0 * correct / frames - cfg["correct_pct"]) <= 0.05
     rep = obj.report()
     assert rep.startswith("Xent:") and "correct[" in rep
+
+
+def test_cache_leftover_filling_cache_raises():
+    """cuCache.cc:97 assert(cache_space > 0): a leftover that fills the whole cache is an error."""
+    from tnet_amd import TnetError
+    layers = formats.gen_mlp_init([8, 16, 4], seed=1)
+    net = Network.from_layers(layers)
+    tr = Trainer(net, Objective(), bunchsize=64, cachesize=512, seed=1)
+    rng = np.random.default_rng(0)
+    lens = [500, 1100, 100]
+    with pytest.raises(TnetError):
+        for n in lens:
+            tr.add_utterance(rng.standard_normal((n, 8)).astype(np.float32), np.zeros(n, np.int32))

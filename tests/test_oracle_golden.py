@@ -102,3 +102,11 @@ def test_epoch_matches_reference_report(golden_dir, name):
     # the Report() line prints 6 significant digits
     np.testing.assert_allclose(net.xent, cfg["xent"], rtol=5e-6)
     np.testing.assert_allclose(100.0 * net.correct / net.frames, cfg["correct_pct"], atol=2e-5)
+
+
+def test_epoch_schedule_leftover_filling_cache_is_an_error():
+    # 500 rows, then 1100: 12 fill the cache, the 1088-row leftover is truncated to the whole
+    # 512-row cache, leaving no space for the third utterance -> reference assert(cache_space > 0)
+    with pytest.raises(ValueError):
+        orc.epoch_schedule([500, 1100, 100], 512, 64, 1)
+    assert orc.epoch_schedule([500, 1100], 512, 64, 1).shape == (8, 64)  # last leftover dropped
