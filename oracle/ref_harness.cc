@@ -8,6 +8,7 @@
 //             bunch loop (src/TNetLib/Platform.h:300-336): clone->Propagate,
 //             CrossEntropy::Evaluate, clone->Backpropagate (Gradient()), master
 //             AccuGradient/AccuBunchsize/Update(0,1)/ResetBunchsize.
+//   train   : the multi-threaded Platform training loop timed around RunTrain (CPU baseline).
 //   shuffle : the cache permutation produced by Cache::Init(seed)+AddData+Randomize
 //             (src/TNetLib/Cache.cc:23-192) -- lrand48 + libstdc++ random_shuffle.
 //
@@ -26,6 +27,9 @@
 #include "ObjFun.h"
 #include "Cache.h"
 #include "Matrix.h"
+#include "Platform.h"
+#include "Timer.h"
+#include "UserInterface.h"
 
 using namespace TNet;
 
@@ -122,11 +126,56 @@ static int cmd_shuffle(int argc, char** argv) {
   return 0;
 }
 
+// train <nnet> <scp> <mlf> <statemap> <lbl_dir> <threads> <bunch> <cache> <lr> <seed>
+// The reference's multi-threaded CPU training (Platform::RunTrain, src/TNetLib/Platform.h:143-198:
+// one HTK/MLF reader thread + <threads> SGD workers over row slices of each bunch), set up the way
+// src/TNet.cc:160-320 sets it up with default feature options, and timed around RunTrain ONLY
+// (TNet's own FPS line also counts reading and writing the model text: TNet.cc:321-362).
+// Prints "frames <n> seconds <t> xent <x> correct <c>".  Used as the CPU baseline of bench.py.
+static int cmd_train(int argc, char** argv) {
+  if (argc < 12) { std::cerr << "usage: train nnet scp mlf statemap lbl_dir threads bunch cache lr seed\n"; return 2; }
+  UserInterface ui;  // no options set: every feature parameter takes its default
+  int deriv_order = 0, start_ext = 0, end_ext = 0;
+  int* deriv_win = NULL;
+  char *cmn_path = NULL, *cmn_file = NULL, *cvn_path = NULL, *cvn_file = NULL;
+  const char *cmn_mask = NULL, *cvn_mask = NULL, *cvg_file = NULL;
+  int target_kind = ui.GetFeatureParams(&deriv_order, &deriv_win, &start_ext, &end_ext, &cmn_path, &cmn_file,
+                                        &cmn_mask, &cvn_path, &cvn_file, &cvn_mask, &cvg_file, "TNET:", 0);
+  Platform pl;
+  pl.feature_.Init(!TNet::IsBigEndian(), start_ext, end_ext, target_kind, deriv_order, deriv_win, cmn_path,
+                   cmn_mask, cvn_path, cvn_mask, cvg_file);
+  pl.feature_.AddFileList(argv[3]);
+  pl.label_.Init(argv[4], argv[5], argv[6], "lab");
+  pl.nnet_.ReadNetwork(argv[2]);
+  pl.nnet_.SetLearnRate((float)atof(argv[10]));
+  pl.nnet_.SetWeightcost(0.0f);
+  pl.obj_fun_ = ObjectiveFunction::Factory(ObjectiveFunction::CROSS_ENTROPY);
+  CrossEntropy* xent = dynamic_cast<CrossEntropy*>(pl.obj_fun_);
+  xent->SetConfusionMode(CrossEntropy::NO_CONF);
+  xent->SetOutputLabelMap(argv[5]);
+  pl.bunchsize_ = atoi(argv[8]);
+  pl.cachesize_ = atoi(argv[9]);
+  pl.randomize_ = true;
+  pl.start_frm_ext_ = start_ext;
+  pl.end_frm_ext_ = end_ext;
+  pl.trace_ = 0;
+  pl.crossval_ = false;
+  pl.seed_ = atol(argv[11]);
+  const int threads = atoi(argv[7]);
+  Timer timer;
+  timer.Start();
+  pl.RunTrain(threads);
+  timer.End();
+  std::cout << "frames " << pl.obj_fun_->GetFrames() << " seconds " << timer.Val() << "\n";
+  return 0;
+}
+
 int main(int argc, char** argv) try {
-  if (argc < 2) { std::cerr << "modes: step | shuffle\n"; return 2; }
+  if (argc < 2) { std::cerr << "modes: step | shuffle | train\n"; return 2; }
   std::string mode = argv[1];
   if (mode == "step") return cmd_step(argc, argv);
   if (mode == "shuffle") return cmd_shuffle(argc, argv);
+  if (mode == "train") return cmd_train(argc, argv);
   std::cerr << "unknown mode\n";
   return 2;
 } catch (std::exception& e) {

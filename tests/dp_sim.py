@@ -33,7 +33,7 @@ def plan(rounds_per_rank):
         k += 1
 
 
-def expected_dp_training(orc, layers, corpus, world, bunch, cachesize, seeds, lr):
+def expected_dp_training(orc, layers, corpus, world, bunch, cachesize, seeds, lr, graddivfrm=True):
     """Oracle MLP after one data-parallel epoch; also returns per-rank bunch counts."""
     from tnet_amd import shard_utterances
     shards = [shard_utterances(range(len(corpus.feats)), r, world) for r in range(world)]
@@ -52,6 +52,6 @@ def expected_dp_training(orc, layers, corpus, world, bunch, cachesize, seeds, lr
                 pos[r] += 1
                 xs.append(X[r][b])
                 ls.append(L[r][b])
-            net.step(np.concatenate(xs), np.concatenate(ls), lr)
+            net.step(np.concatenate(xs), np.concatenate(ls), lr, graddivfrm=graddivfrm)
     assert pos == [len(s) for s in sched]
     return net, [len(s) for s in sched], rounds

@@ -78,7 +78,7 @@ def test_dp_trainer_uneven_shards(tmp_path):
     corpus = dp_cases.trainer_corpus()
     layers = formats.gen_mlp_init(c["dims"], seed=c["init_seed"])
     net, nb, rounds = dp_sim.expected_dp_training(orc, layers, corpus, 2, c["bunch"], c["cache"],
-                                                  [c["seed"], c["seed"] + 1], c["lr"])
+                                                  [c["seed"], c["seed"] + 1], c["lr"], graddivfrm=c["gdf"])
     assert nb[0] > nb[1], "the case must exercise unequal shards"
     total_steps = sum(len(r) for r in rounds)
     for r in range(2):
