@@ -12,14 +12,17 @@
 //    m/n-contiguous operand feeds them with conflict-free ds_read_b32 -- so every operand layout
 //    (NN forward, NT backward, TN weight gradient) is staged straight from coalesced 16-B global
 //    loads, no transposes.
-//  * 256-thread workgroups (4 waves, one per SIMD), BK = 32, LDS double buffer filled from a
-//    register prefetch of the next k-tile issued before the MFMAs of the current one: one
-//    barrier per k-tile; the global latency hides under 16-32 MFMAs per wave.
-//  * k-contiguous tiles live in LDS as [rows][BK+4] (the +4 pad makes the 16-lane groups of
-//    ds_read_b128 hit 16 distinct 4-bank slots); row-contiguous tiles as [BK][cols].
-//  * tile shape chosen per GEMM shape so one launch has >= 256 workgroups where possible
-//    (256 CUs); blockIdx is remapped so that consecutive tiles (which share operand panels)
-//    run on one XCD (bijective remap, cdna_hip_programming.md T1).
+//  * operand k-tiles stream global -> LDS by LDS-DMA (global_load_lds_dwordx4, no VGPR staging)
+//    into an S-slot ring with S-1 tiles in flight and ONE raw s_barrier per k-tile behind a
+//    counted vmcnt (cdna_hip_programming.md section 5, "Pipelining across barriers");
+//  * k-contiguous operand images are [rows][BK] with the 16-B chunk index XOR-swizzled per row
+//    (the DMA image is lane-linear, so the swizzle goes on the per-lane SOURCE address and is
+//    undone on the ds_read_b128, rule 21): every 16-lane group of ds_read_b128 hits 16 distinct
+//    4-bank slots.  Row-contiguous images are plain [BK][cols] read with conflict-free b32;
+//  * blockIdx -> tile: bijective XCD-contiguous remap (T1) followed by a grouped order (GROUP
+//    tile-rows, column-major inside a group), so the ~64 workgroups resident on one XCD cover a
+//    square-ish block of C and its L2 holds few A and B panels;
+//  * the whole epilogue (bias, sigmoid, diff-sigmoid, momentum-SGD) is fused into the stores.
 #include <cstdlib>
 #include <cstring>
 
@@ -39,6 +42,7 @@ struct GemmP {
   const float* aux; long ldaux; // EPI_DSIG: y of the layer below [M x N]
   float* corr; long ldcorr;     // EPI_SGD: momentum buffer (nullable)
   float scale, mmt, l2;         // EPI_SGD
+  int group;                    // tile-rows per group of the blockIdx -> tile order
   int diag_noload;              // diagnostics only: skip the k-loop's global loads (wrong results)
 };
 
@@ -88,195 +92,12 @@ __device__ __forceinline__ void epilogue(const GemmP& p, f32x16 (&acc)[TM][TN], 
   }
 }
 
-// A tile of R rows x CF floats (row-major in global memory, leading dimension ld), held in
-// registers between its global load and its LDS store ([R][LDS_S] image).
-template <int R, int CF, int LDS_S, int NT>
-struct TileLoader {
-  static constexpr int C4 = CF / 4;
-  static constexpr int NV = R * C4 / NT;
-  static_assert(R * C4 % NT == 0, "tile must split evenly over the workgroup");
-  static_assert(NV <= 10, "3 validity bits per float4");
-  f32x4 v[NV];
-  unsigned valid;
-
-  // Branch-free bounded load: every lane issues its dwordx4 loads unconditionally (so hipcc keeps
-  // them all in flight and waits once, at the LDS store); out-of-range rows are clamped to the last
-  // valid row and out-of-range columns to column 0, then zeroed by select.  A column start
-  // gc < cmax <= ld (ld % 4 == 0) keeps the 16-byte read inside the row's allocation.
-  __device__ __forceinline__ void load(const float* __restrict__ g, long ld, int r0, int c0, int rmax, int cmax) {
-    const int t = threadIdx.x;
-    valid = 0;
-#pragma unroll
-    for (int p = 0; p < NV; ++p) {
-      const int idx = t + p * NT;
-      const int r = idx / C4, c = (idx % C4) * 4;
-      const int gr = r0 + r, gc = c0 + c;
-      const int grc = gr < rmax ? gr : rmax - 1;
-      const int gcc = gc < cmax ? gc : 0;
-      v[p] = *reinterpret_cast<const f32x4*>(g + (long)grc * ld + gcc);
-      // validity of the 4 elements, applied at store time so the loads stay in flight
-      const int nvalid = gr < rmax ? (cmax - gc < 0 ? 0 : (cmax - gc > 4 ? 4 : cmax - gc)) : 0;
-      valid |= (unsigned)nvalid << (3 * p);
-    }
-  }
-  __device__ __forceinline__ void store(float* s) const {
-    const int t = threadIdx.x;
-#pragma unroll
-    for (int p = 0; p < NV; ++p) {
-      const int idx = t + p * NT;
-      const int r = idx / C4, c = (idx % C4) * 4;
-      const int nv = (valid >> (3 * p)) & 7;
-      f32x4 x = v[p];
-#pragma unroll
-      for (int k = 0; k < 4; ++k) x[k] = (k < nv) ? x[k] : 0.f;
-      *reinterpret_cast<f32x4*>(s + r * LDS_S + c) = x;
-    }
-  }
-};
-
-template <int BM, int BN, int BK, int WM, int WN, int PF, bool A_KC, bool B_KC, int EPI>
-__global__ __launch_bounds__(WM * WN * 64) void gemm_f32_kernel(const GemmP p) {
-  constexpr int NT = WM * WN * 64;
-  constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
-  static_assert(TM >= 1 && TN >= 1 && BM == TM * WM * 32 && BN == TN * WN * 32, "32x32 MFMA blocks per wave");
-  static_assert(BK % 8 == 0, "k chunks of 8");
-  constexpr int A_S = A_KC ? (BK + 4) : BM;
-  constexpr int B_S = B_KC ? (BK + 4) : BN;
-  constexpr int A_SZ = A_KC ? BM * A_S : BK * A_S;
-  constexpr int B_SZ = B_KC ? BN * B_S : BK * B_S;
-  __shared__ __attribute__((aligned(16))) float smem[2 * (A_SZ + B_SZ)];
-
-  const int M = p.M, N = p.N, K = p.K;
-  const int nbn = (N + BN - 1) / BN, nbm = (M + BM - 1) / BM;
-  const int nwg = nbm * nbn;
-  // bijective XCD-aware remap: blocks b, b+8, ... (one XCD) take a contiguous range of tiles
-  const int bid = blockIdx.x, xcd = bid & 7, q = nwg >> 3, r8 = nwg & 7;
-  const int L = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + (bid >> 3);
-  const int bm = (L / nbn) * BM, bn = (L % nbn) * BN;
-
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int wm0 = (wid / WN) * (BM / WM), wn0 = (wid % WN) * (BN / WN);
-  const int li = lane & 31, lh = lane >> 5;
-
-  using LA = TileLoader<A_KC ? BM : BK, A_KC ? BK : BM, A_S, NT>;
-  using LB = TileLoader<B_KC ? BN : BK, B_KC ? BK : BN, B_S, NT>;
-  LA la[PF];
-  LB lb[PF];
-
-  f32x16 acc[TM][TN];
-#pragma unroll
-  for (int a = 0; a < TM; ++a)
-#pragma unroll
-    for (int b = 0; b < TN; ++b)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
-
-  auto load_stage = [&](LA& l_a, LB& l_b, int k0) {
-    if (p.diag_noload && k0 > 0) return;
-    if (A_KC) l_a.load(p.A, p.lda, bm, k0, M, K);
-    else      l_a.load(p.A, p.lda, k0, bm, K, M);
-    if (B_KC) l_b.load(p.B, p.ldb, bn, k0, N, K);
-    else      l_b.load(p.B, p.ldb, k0, bn, K, N);
-  };
-  auto store_stage = [&](const LA& l_a, const LB& l_b, int t) {
-    if (p.diag_noload) return;
-    float* An = smem + (t & 1) * (A_SZ + B_SZ);
-    l_a.store(An);
-    l_b.store(An + A_SZ);
-  };
-
-  // MFMAs over one LDS stage; fragments of k-chunk kk+8 are read while the MFMAs of chunk kk issue
-  auto compute = [&](int t) {
-    const float* As = smem + (t & 1) * (A_SZ + B_SZ);
-    const float* Bs = As + A_SZ;
-    float av[2][TM][4], bv[2][TN][4];
-    auto read_frags = [&](int kk, float (&a_)[TM][4], float (&b_)[TN][4]) {
-#pragma unroll
-      for (int a = 0; a < TM; ++a) {
-        const int row = wm0 + a * 32 + li;
-        if (A_KC) {
-          const f32x4 x = *reinterpret_cast<const f32x4*>(As + row * A_S + kk + 4 * lh);
-          a_[a][0] = x[0]; a_[a][1] = x[1]; a_[a][2] = x[2]; a_[a][3] = x[3];
-        } else {
-#pragma unroll
-          for (int s = 0; s < 4; ++s) a_[a][s] = As[(kk + 4 * lh + s) * A_S + row];
-        }
-      }
-#pragma unroll
-      for (int b = 0; b < TN; ++b) {
-        const int col = wn0 + b * 32 + li;
-        if (B_KC) {
-          const f32x4 x = *reinterpret_cast<const f32x4*>(Bs + col * B_S + kk + 4 * lh);
-          b_[b][0] = x[0]; b_[b][1] = x[1]; b_[b][2] = x[2]; b_[b][3] = x[3];
-        } else {
-#pragma unroll
-          for (int s = 0; s < 4; ++s) b_[b][s] = Bs[(kk + 4 * lh + s) * B_S + col];
-        }
-      }
-    };
-    read_frags(0, av[0], bv[0]);
-#pragma unroll
-    for (int kc = 0; kc < BK / 8; ++kc) {
-      const int cur = kc & 1;
-      if (kc + 1 < BK / 8) read_frags((kc + 1) * 8, av[cur ^ 1], bv[cur ^ 1]);
-#pragma unroll
-      for (int s = 0; s < 4; ++s)
-#pragma unroll
-        for (int a = 0; a < TM; ++a)
-#pragma unroll
-          for (int b = 0; b < TN; ++b)
-            acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[cur][a][s], bv[cur][b][s], acc[a][b], 0, 0, 0);
-    }
-  };
-
-  const int nk = (K + BK - 1) / BK;
-  if constexpr (PF == 1) {
-    // one k-tile in flight: load t+1 to registers under the MFMAs of t, store after them
-    load_stage(la[0], lb[0], 0);
-    la[0].store(smem);
-    lb[0].store(smem + A_SZ);
-    __syncthreads();
-    for (int t = 0; t < nk; ++t) {
-      if (t + 1 < nk) load_stage(la[0], lb[0], (t + 1) * BK);
-      compute(t);
-      if (t + 1 < nk) store_stage(la[0], lb[0], t + 1);
-      __syncthreads();
-    }
-  } else {
-    // two k-tiles in flight: register set (s % 2) holds k-tile s from its load (issued two
-    // tiles ahead) until its LDS store (one tile ahead); plain loads survive the barriers
-    load_stage(la[0], lb[0], 0);
-    if (nk > 1) load_stage(la[1], lb[1], BK);
-    la[0].store(smem);
-    lb[0].store(smem + A_SZ);
-    __syncthreads();
-    for (int t = 0; t < nk; t += 2) {
-      if (t + 2 < nk) load_stage(la[0], lb[0], (t + 2) * BK);
-      compute(t);
-      if (t + 1 < nk) store_stage(la[1], lb[1], t + 1);
-      __syncthreads();
-      if (t + 1 < nk) {
-        if (t + 3 < nk) load_stage(la[1], lb[1], (t + 3) * BK);
-        compute(t + 1);
-        if (t + 2 < nk) store_stage(la[0], lb[0], t + 2);
-        __syncthreads();
-      }
-    }
-  }
-
-  epilogue<TM, TN, EPI>(p, acc, bm, bn, wm0, wn0, li, lh);
-}
 
 // =============================================================================================
-// LDS-DMA pipelined variant: k-tiles of 32 are streamed global -> LDS by global_load_lds_dwordx4
-// (no VGPR staging) into an S-slot ring, S-1 tiles in flight, one raw s_barrier per k-tile behind
-// a COUNTED vmcnt (cdna_hip_programming.md section 5 "Pipelining across barriers").
-//   * k-contiguous operand images are [rows][32] with the 16-B chunk index XOR-swizzled by
-//     ((row >> 1) & 7): the DMA image is lane-linear, so the swizzle is applied to the per-lane
-//     SOURCE address and undone on the ds_read_b128 (rule 21); the 16-lane groups of ds_read_b128
-//     then hit 16 distinct 4-bank slots.  Row-contiguous images are plain [32][cols].
+// LDS-DMA pipelined GEMM.  BMxBN workgroup tile, BK k-depth per ring slot, WMxWN waves each
+// owning (BM/WM)x(BN/WN) = TMxTN blocks of 32x32 MFMA accumulators.
 //   * rows / columns beyond M / N are clamped to valid memory (their products only reach outputs
-//     that are never stored); a partial last k-tile (K % 32) goes through the masked register path.
+//     that are never stored); a partial last k-tile (K % BK) goes through a masked register path.
 // =============================================================================================
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
@@ -285,24 +106,38 @@ __device__ __forceinline__ void wait_vmcnt() {
   __builtin_amdgcn_s_waitcnt((N & 0xF) | (0x7 << 4) | (0xF << 8) | (((N >> 4) & 0x3) << 14));
 }
 
-__device__ __forceinline__ int swz8(int r) { return (r >> 1) & 7; }
+// XOR swizzle of the 16-B chunk index of row r of a k-contiguous [rows][BK] image.
+//   BK = 32: rows are 128 B, two per 256-B bank row -> ((r >> 1) & 7) over the 8 chunks;
+//   BK = 64: rows are 256 B, one per bank row        -> (r & 15) over the 16 chunks.
+template <int BK>
+__device__ __forceinline__ int swz(int r) {
+  return BK == 32 ? ((r >> 1) & 7) : (r & 15);
+}
 
-template <int BM, int BN, int WM, int WN, int S, bool SB, bool A_KC, bool B_KC, int EPI>
-__global__ __launch_bounds__(256) void gemm_f32_glds_kernel(const GemmP p) {
-  constexpr int BK = 32, NT = 256;
+template <int BM, int BN, int BK, int WM, int WN, int S, bool A_KC, bool B_KC, int EPI>
+__global__ __launch_bounds__(WM * WN * 64) void gemm_f32_glds_kernel(const GemmP p) {
+  constexpr int NT = WM * WN * 64, NW = WM * WN;
   constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
-  static_assert(WM * WN == 4 && TM >= 1 && TN >= 1, "4 waves of 32x32 MFMA blocks");
+  static_assert(TM >= 1 && TN >= 1 && BM == TM * WM * 32 && BN == TN * WN * 32, "32x32 MFMA blocks per wave");
+  static_assert(BK == 32 || BK == 64, "BK");
+  constexpr int CH = BK / 4;  // 16-B chunks per k-contiguous row
   constexpr int A_SZ = BM * BK, B_SZ = BN * BK, ST_SZ = A_SZ + B_SZ;
   constexpr int GA = A_SZ / 4 / NT, GB = B_SZ / 4 / NT, G = GA + GB;  // DMA instructions per thread per tile
   static_assert(A_SZ % (4 * NT) == 0 && B_SZ % (4 * NT) == 0, "tile splits into 1-KiB wave pieces");
+  static_assert(2 * G < 64, "vmcnt range");
   __shared__ __attribute__((aligned(16))) float smem[S * ST_SZ];
 
   const int M = p.M, N = p.N, K = p.K;
   const int nbn = (N + BN - 1) / BN, nbm = (M + BM - 1) / BM;
   const int nwg = nbm * nbn;
+  // bijective XCD remap: the blocks one XCD receives (bid % 8) take a contiguous range of L ...
   const int bid = blockIdx.x, xcd = bid & 7, q = nwg >> 3, r8 = nwg & 7;
   const int L = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + (bid >> 3);
-  const int bm = (L / nbn) * BM, bn = (L % nbn) * BN;
+  // ... and that range is walked in groups of `group` tile-rows, column-major inside a group
+  const int grp = p.group, per_group = grp * nbn;
+  const int first_m = (L / per_group) * grp;
+  const int gsz = min(nbm - first_m, grp);
+  const int bm = (first_m + (L % per_group) % gsz) * BM, bn = ((L % per_group) / gsz) * BN;
 
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int wm0 = (wid / WN) * (BM / WM), wn0 = (wid % WN) * (BN / WN);
@@ -312,11 +147,10 @@ __global__ __launch_bounds__(256) void gemm_f32_glds_kernel(const GemmP p) {
   long srcA[GA], srcB[GB];
 #pragma unroll
   for (int g = 0; g < GA; ++g) {
-    const int u = (g * 4 + wid) * 64 + lane;  // 16-B unit index inside the image
+    const int u = (g * NW + wid) * 64 + lane;  // 16-B unit index inside the image
     if (A_KC) {
-      const int r = u >> 3, j = u & 7;
-      const int gr = min(bm + r, M - 1);
-      srcA[g] = (long)gr * p.lda + 4 * (j ^ swz8(r));
+      const int r = u / CH, j = u % CH;
+      srcA[g] = (long)min(bm + r, M - 1) * p.lda + 4 * (j ^ swz<BK>(r));
     } else {
       const int k = u / (BM / 4), c = (u % (BM / 4)) * 4;
       srcA[g] = (long)k * p.lda + (bm + c < M ? bm + c : 0);
@@ -324,11 +158,10 @@ __global__ __launch_bounds__(256) void gemm_f32_glds_kernel(const GemmP p) {
   }
 #pragma unroll
   for (int g = 0; g < GB; ++g) {
-    const int u = (g * 4 + wid) * 64 + lane;
+    const int u = (g * NW + wid) * 64 + lane;
     if (B_KC) {
-      const int r = u >> 3, j = u & 7;
-      const int gr = min(bn + r, N - 1);
-      srcB[g] = (long)gr * p.ldb + 4 * (j ^ swz8(r));
+      const int r = u / CH, j = u % CH;
+      srcB[g] = (long)min(bn + r, N - 1) * p.ldb + 4 * (j ^ swz<BK>(r));
     } else {
       const int k = u / (BN / 4), c = (u % (BN / 4)) * 4;
       srcB[g] = (long)k * p.ldb + (bn + c < N ? bn + c : 0);
@@ -341,11 +174,12 @@ __global__ __launch_bounds__(256) void gemm_f32_glds_kernel(const GemmP p) {
     const long kb = B_KC ? (long)t * BK : (long)t * BK * p.ldb;
 #pragma unroll
     for (int g = 0; g < GA; ++g)
-      __builtin_amdgcn_global_load_lds((const void*)(p.A + ka + srcA[g]), (void*)(st + (g * 4 + wid) * 256), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(p.A + ka + srcA[g]), (void*)(st + (g * NW + wid) * 256), 16, 0,
+                                       0);
 #pragma unroll
     for (int g = 0; g < GB; ++g)
-      __builtin_amdgcn_global_load_lds((const void*)(p.B + kb + srcB[g]), (void*)(st + A_SZ + (g * 4 + wid) * 256), 16,
-                                       0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(p.B + kb + srcB[g]), (void*)(st + A_SZ + (g * NW + wid) * 256),
+                                       16, 0, 0);
   };
 
   f32x16 acc[TM][TN];
@@ -356,6 +190,8 @@ __global__ __launch_bounds__(256) void gemm_f32_glds_kernel(const GemmP p) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
 
+  // MFMAs over one ring slot.  k of MFMA step s (0..3) of 8-deep chunk kc is 8kc + 4*kh + s
+  // (kh = lane >> 5), so a k-contiguous operand feeds 4 MFMAs from one ds_read_b128.
   auto compute = [&](const float* st) {
     const float* As = st;
     const float* Bs = st + A_SZ;
@@ -365,7 +201,7 @@ __global__ __launch_bounds__(256) void gemm_f32_glds_kernel(const GemmP p) {
       for (int a = 0; a < TM; ++a) {
         const int row = wm0 + a * 32 + li;
         if (A_KC) {
-          const f32x4 x = *reinterpret_cast<const f32x4*>(As + row * BK + 4 * ((2 * kc + lh) ^ swz8(row)));
+          const f32x4 x = *reinterpret_cast<const f32x4*>(As + row * BK + 4 * ((2 * kc + lh) ^ swz<BK>(row)));
           a_[a][0] = x[0]; a_[a][1] = x[1]; a_[a][2] = x[2]; a_[a][3] = x[3];
         } else {
 #pragma unroll
@@ -376,7 +212,7 @@ __global__ __launch_bounds__(256) void gemm_f32_glds_kernel(const GemmP p) {
       for (int b = 0; b < TN; ++b) {
         const int col = wn0 + b * 32 + li;
         if (B_KC) {
-          const f32x4 x = *reinterpret_cast<const f32x4*>(Bs + col * BK + 4 * ((2 * kc + lh) ^ swz8(col)));
+          const f32x4 x = *reinterpret_cast<const f32x4*>(Bs + col * BK + 4 * ((2 * kc + lh) ^ swz<BK>(col)));
           b_[b][0] = x[0]; b_[b][1] = x[1]; b_[b][2] = x[2]; b_[b][3] = x[3];
         } else {
 #pragma unroll
@@ -389,7 +225,6 @@ __global__ __launch_bounds__(256) void gemm_f32_glds_kernel(const GemmP p) {
     for (int kc = 0; kc < BK / 8; ++kc) {
       const int cur = kc & 1;
       if (kc + 1 < BK / 8) read_frags(kc + 1, av[cur ^ 1], bv[cur ^ 1]);
-      if (SB) __builtin_amdgcn_sched_barrier(0);  // keep the next chunk's ds_reads ahead of these MFMAs
 #pragma unroll
       for (int s = 0; s < 4; ++s)
 #pragma unroll
@@ -421,10 +256,9 @@ __global__ __launch_bounds__(256) void gemm_f32_glds_kernel(const GemmP p) {
     float* st = smem + (nfull % S) * ST_SZ;
     const int k0 = nfull * BK;
     for (int u = threadIdx.x; u < A_SZ / 4; u += NT) {
-      int gr, gc, lds;
-      if (A_KC) { const int r = u >> 3, j = u & 7; gr = bm + r; gc = k0 + 4 * (j ^ swz8(r)); }
+      int gr, gc;
+      if (A_KC) { const int r = u / CH, j = u % CH; gr = bm + r; gc = k0 + 4 * (j ^ swz<BK>(r)); }
       else { const int k = u / (BM / 4); gr = k0 + k; gc = bm + (u % (BM / 4)) * 4; }
-      lds = u * 4;
       const int rmax = A_KC ? M : K, cmax = A_KC ? K : M;
       f32x4 x = {0.f, 0.f, 0.f, 0.f};
       if (gr < rmax) {
@@ -432,11 +266,11 @@ __global__ __launch_bounds__(256) void gemm_f32_glds_kernel(const GemmP p) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) x[e] = (gc + e < cmax) ? q[e] : 0.f;
       }
-      *reinterpret_cast<f32x4*>(st + lds) = x;
+      *reinterpret_cast<f32x4*>(st + u * 4) = x;
     }
     for (int u = threadIdx.x; u < B_SZ / 4; u += NT) {
       int gr, gc;
-      if (B_KC) { const int r = u >> 3, j = u & 7; gr = bn + r; gc = k0 + 4 * (j ^ swz8(r)); }
+      if (B_KC) { const int r = u / CH, j = u % CH; gr = bn + r; gc = k0 + 4 * (j ^ swz<BK>(r)); }
       else { const int k = u / (BN / 4); gr = k0 + k; gc = bn + (u % (BN / 4)) * 4; }
       const int rmax = B_KC ? N : K, cmax = B_KC ? K : N;
       f32x4 x = {0.f, 0.f, 0.f, 0.f};
@@ -456,14 +290,31 @@ __global__ __launch_bounds__(256) void gemm_f32_glds_kernel(const GemmP p) {
 // ---------------------------------------------------------------------------------------------
 // host-side dispatch
 // ---------------------------------------------------------------------------------------------
-// Tile configurations: BMxBN tile, BK k-depth per LDS stage, WMxWN waves (each wave owns a
-// (BM/WM)x(BN/WN) sub-tile of 32x32 MFMA blocks).
-enum GemmCfg { CFG_128x64_W4, CFG_64x64_W4, CFG_128x64_W8, CFG_G128x64_S3, CFG_G64x64_S3, CFG_G64x64_S4,
-               CFG_G128x64_S3B, CFG_G64x64_S3B, CFG_G64x64_S4B, CFG_COUNT };
-static const char* kCfgNames[CFG_COUNT] = {"128x64w4", "64x64w4", "128x64w8", "g128x64s3", "g64x64s3", "g64x64s4",
-                                           "g128x64s3b", "g64x64s3b", "g64x64s4b"};
+// name: g<BM>x<BN>k<BK>s<S>w<waves>  (waves laid out WMxWN)
+#define TNET_GEMM_CFGS(X)                   \
+  X(g64x64k32s4w4, 64, 64, 32, 2, 2, 4)     \
+  X(g64x64k64s2w4, 64, 64, 64, 2, 2, 2)     \
+  X(g64x64k32s4w2, 64, 64, 32, 2, 1, 4)     \
+  X(g64x64k64s2w2, 64, 64, 64, 2, 1, 2)     \
+  X(g128x64k32s3w4, 128, 64, 32, 2, 2, 3)   \
+  X(g64x128k32s3w4, 64, 128, 32, 2, 2, 3)   \
+  X(g128x128k32s2w4, 128, 128, 32, 2, 2, 2) \
+  X(g128x128k32s3w8, 128, 128, 32, 2, 4, 3)
+
+enum GemmCfg {
+#define X(name, ...) CFG_##name,
+  TNET_GEMM_CFGS(X)
+#undef X
+  CFG_COUNT
+};
+static const char* kCfgNames[CFG_COUNT] = {
+#define X(name, ...) #name,
+    TNET_GEMM_CFGS(X)
+#undef X
+};
 
 static int g_cfg = -2;  // -2: not initialised, -1: automatic
+static int g_group = -1;
 static int forced_cfg() {
   if (g_cfg == -2) {
     g_cfg = -1;
@@ -471,20 +322,16 @@ static int forced_cfg() {
     if (e)
       for (int i = 0; i < CFG_COUNT; i++)
         if (!strcmp(e, kCfgNames[i])) g_cfg = i;
+    const char* gg = getenv("TNET_GEMM_GROUP");
+    if (gg) g_group = atoi(gg);
   }
   return g_cfg;
 }
 
-template <int BM, int BN, int BK, int WM, int WN, int PF, bool A_KC, bool B_KC, int EPI>
-static void launch_cfg(const GemmP& p, hipStream_t st) {
-  const unsigned tiles = (unsigned)((long)cdiv(p.M, BM) * cdiv(p.N, BN));
-  gemm_f32_kernel<BM, BN, BK, WM, WN, PF, A_KC, B_KC, EPI><<<tiles, WM * WN * 64, 0, st>>>(p);
-}
-
-template <int BM, int BN, int WM, int WN, int S, bool SB, bool A_KC, bool B_KC, int EPI>
+template <int BM, int BN, int BK, int WM, int WN, int S, bool A_KC, bool B_KC, int EPI>
 static void launch_glds(const GemmP& p, hipStream_t st) {
   const unsigned tiles = (unsigned)((long)cdiv(p.M, BM) * cdiv(p.N, BN));
-  gemm_f32_glds_kernel<BM, BN, WM, WN, S, SB, A_KC, B_KC, EPI><<<tiles, 256, 0, st>>>(p);
+  gemm_f32_glds_kernel<BM, BN, BK, WM, WN, S, A_KC, B_KC, EPI><<<tiles, WM * WN * 64, 0, st>>>(p);
 }
 
 template <bool A_KC, bool B_KC, int EPI>
@@ -493,22 +340,14 @@ static int launch_gemm(const GemmP& p_in, hipStream_t st) {
   static const int noload = getenv("TNET_GEMM_DIAG_NOLOAD") ? 1 : 0;
   GemmP p = p_in;
   p.diag_noload = noload;
-  auto tiles = [&](int bm, int bn) { return (long)cdiv(p.M, bm) * cdiv(p.N, bn); };
   int cfg = forced_cfg();
-  if (cfg < 0) {
-    // the largest tile that still gives ~one workgroup per CU (256 CUs)
-    cfg = CFG_G64x64_S4;
-  }
+  if (cfg < 0) cfg = CFG_g64x64k32s4w4;
+  p.group = g_group > 0 ? g_group : 8;
   switch (cfg) {
-    case CFG_128x64_W4: launch_cfg<128, 64, 32, 2, 2, 1, A_KC, B_KC, EPI>(p, st); break;
-    case CFG_64x64_W4: launch_cfg<64, 64, 32, 2, 2, 1, A_KC, B_KC, EPI>(p, st); break;
-    case CFG_128x64_W8: launch_cfg<128, 64, 32, 4, 2, 1, A_KC, B_KC, EPI>(p, st); break;
-    case CFG_G128x64_S3: launch_glds<128, 64, 2, 2, 3, false, A_KC, B_KC, EPI>(p, st); break;
-    case CFG_G64x64_S3: launch_glds<64, 64, 2, 2, 3, false, A_KC, B_KC, EPI>(p, st); break;
-    case CFG_G64x64_S4: launch_glds<64, 64, 2, 2, 4, false, A_KC, B_KC, EPI>(p, st); break;
-    case CFG_G128x64_S3B: launch_glds<128, 64, 2, 2, 3, true, A_KC, B_KC, EPI>(p, st); break;
-    case CFG_G64x64_S3B: launch_glds<64, 64, 2, 2, 3, true, A_KC, B_KC, EPI>(p, st); break;
-    case CFG_G64x64_S4B: launch_glds<64, 64, 2, 2, 4, true, A_KC, B_KC, EPI>(p, st); break;
+#define X(name, BM, BN, BK, WM, WN, S) \
+  case CFG_##name: launch_glds<BM, BN, BK, WM, WN, S, A_KC, B_KC, EPI>(p, st); break;
+    TNET_GEMM_CFGS(X)
+#undef X
     default: return TNET_ERR_ARG;
   }
   TNET_LAUNCH_CHECK();
@@ -610,6 +449,7 @@ extern "C" int tnet_affine_grad(const float* X, TnetMatrixDim dX, const float* E
 }
 
 extern "C" int tnet_gemm_config(const char* name) {
+  forced_cfg();  // read the environment once, before it could override this call
   if (!name || !strcmp(name, "auto")) {
     g_cfg = -1;
     return TNET_OK;

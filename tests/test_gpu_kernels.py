@@ -32,7 +32,8 @@ def gemm_ref(ta, tb, A, B):
     return a @ b, np.abs(a) @ np.abs(b)
 
 
-GEMM_CFGS = ["auto", "128x64w4", "64x64w4", "128x64w8", "g128x64s3", "g64x64s3", "g64x64s4b"]
+GEMM_CFGS = ["auto", "g64x64k32s4w4", "g64x64k64s2w4", "g64x64k32s4w2", "g64x64k64s2w2", "g128x64k32s3w4",
+             "g64x128k32s3w4", "g128x128k32s2w4", "g128x128k32s3w8"]
 
 
 @pytest.fixture(params=GEMM_CFGS)

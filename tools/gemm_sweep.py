@@ -10,8 +10,8 @@ import subprocess
 import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-CFGS = ["g128x64s3", "g64x64s3", "g64x64s4", "g128x64s3b", "g64x64s3b", "g64x64s4b", "g64x64s4+noload",
-        "g64x64s4b+noload"]
+CFGS = ["g64x64k32s4w4", "g64x64k64s2w4", "g64x64k32s4w2", "g64x64k64s2w2", "g128x64k32s3w4", "g64x128k32s3w4",
+        "g128x128k32s2w4", "g128x128k32s3w8", "g64x64k32s4w4+g1", "g64x64k32s4w4+noload"]
 # (kind, rows, n_in, n_out): fwd/bwd/upd of each layer of 440 -> 2048x4 -> 4000 at bunch 1024
 SHAPES = [("fwd", 1024, 2048, 2048), ("bwd", 1024, 2048, 2048), ("upd", 1024, 2048, 2048),
           ("fwd", 1024, 2048, 4000), ("bwd", 1024, 2048, 4000), ("upd", 1024, 2048, 4000),
@@ -57,9 +57,13 @@ def main():
     cfgs = sys.argv[2].split(",") if len(sys.argv) > 2 else CFGS
     res = {}
     for cfg in cfgs:
-        env = dict(os.environ, TNET_GEMM_CFG=cfg.split("+")[0])
-        if cfg.endswith("+noload"):
-            env["TNET_GEMM_DIAG_NOLOAD"] = "1"
+        parts = cfg.split("+")
+        env = dict(os.environ, TNET_GEMM_CFG=parts[0])
+        for extra in parts[1:]:
+            if extra == "noload":
+                env["TNET_GEMM_DIAG_NOLOAD"] = "1"
+            elif extra.startswith("g") and extra[1:].isdigit():
+                env["TNET_GEMM_GROUP"] = extra[1:]
         p = subprocess.run([sys.executable, "-c", CHILD, REPO, json.dumps(SHAPES), str(iters)], env=env,
                            capture_output=True, text=True, timeout=300)
         line = [l for l in p.stdout.splitlines() if l.startswith("RESULT ")]
