@@ -106,6 +106,17 @@ __device__ __forceinline__ void wait_vmcnt() {
   __builtin_amdgcn_s_waitcnt((N & 0xF) | (0x7 << 4) | (0xF << 8) | (((N >> 4) & 0x3) << 14));
 }
 
+// s_waitcnt vmcnt(n) for a wave-uniform runtime n <= N (the immediate must be a constant)
+template <int N>
+__device__ __forceinline__ void wait_vmcnt_le(int n) {
+  if constexpr (N <= 0) {
+    wait_vmcnt<0>();
+  } else {
+    if (n >= N) wait_vmcnt<N>();
+    else wait_vmcnt_le<N - 1>(n);
+  }
+}
+
 // XOR swizzle of the 16-B chunk index of row r of a k-contiguous [rows][BK] image.
 //   BK = 32: rows are 128 B, two per 256-B bank row -> ((r >> 1) & 7) over the 8 chunks;
 //   BK = 64: rows are 256 B, one per bank row        -> (r & 15) over the 16 chunks.
@@ -114,7 +125,7 @@ __device__ __forceinline__ int swz(int r) {
   return BK == 32 ? ((r >> 1) & 7) : (r & 15);
 }
 
-template <int BM, int BN, int BK, int WM, int WN, int S, bool A_KC, bool B_KC, int EPI>
+template <int BM, int BN, int BK, int WM, int WN, int S, int IL, bool A_KC, bool B_KC, int EPI>
 __global__ __launch_bounds__(WM * WN * 64) void gemm_f32_glds_kernel(const GemmP p) {
   constexpr int NT = WM * WN * 64, NW = WM * WN;
   constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
@@ -168,6 +179,19 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_f32_glds_kernel(const GemmP
     }
   }
 
+  auto issue_piece = [&](int t, int g) {  // DMA piece g (A pieces first) of k-tile t into slot t % S
+    float* st = smem + (t % S) * ST_SZ;
+    if (g < GA) {
+      const long ka = A_KC ? (long)t * BK : (long)t * BK * p.lda;
+      __builtin_amdgcn_global_load_lds((const void*)(p.A + ka + srcA[g]), (void*)(st + (g * NW + wid) * 256), 16, 0,
+                                       0);
+    } else {
+      const int h = g - GA;
+      const long kb = B_KC ? (long)t * BK : (long)t * BK * p.ldb;
+      __builtin_amdgcn_global_load_lds((const void*)(p.B + kb + srcB[h]), (void*)(st + A_SZ + (h * NW + wid) * 256),
+                                       16, 0, 0);
+    }
+  };
   auto issue = [&](int t) {  // DMA of full k-tile t into ring slot t % S
     float* st = smem + (t % S) * ST_SZ;
     const long ka = A_KC ? (long)t * BK : (long)t * BK * p.lda;
@@ -190,65 +214,118 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_f32_glds_kernel(const GemmP
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
 
-  // MFMAs over one ring slot.  k of MFMA step s (0..3) of 8-deep chunk kc is 8kc + 4*kh + s
-  // (kh = lane >> 5), so a k-contiguous operand feeds 4 MFMAs from one ds_read_b128.
-  auto compute = [&](const float* st) {
+  // k of MFMA step s (0..3) of 8-deep chunk kc is 8kc + 4*kh + s (kh = lane >> 5), so a
+  // k-contiguous operand feeds 4 MFMAs from one ds_read_b128.  Fragments live in a 4-deep
+  // register ring (chunk c -> buffer c % 4) and are read TWO chunks ahead of their MFMAs --
+  // across k-tile boundaries too -- so an MFMA never waits on an LDS read issued just before it,
+  // even where the compiler's waitcnt is a conservative lgkmcnt(0).
+  constexpr int KC = BK / 8, NB = 4;
+  static_assert(KC % NB == 0, "chunk -> buffer mapping is per tile");
+  float av[NB][TM][4], bv[NB][TN][4];
+  auto read_frags = [&](const float* st, int kc, int buf) {  // chunk kc of the slot at st
     const float* As = st;
     const float* Bs = st + A_SZ;
-    float av[2][TM][4], bv[2][TN][4];
-    auto read_frags = [&](int kc, float (&a_)[TM][4], float (&b_)[TN][4]) {
 #pragma unroll
-      for (int a = 0; a < TM; ++a) {
-        const int row = wm0 + a * 32 + li;
-        if (A_KC) {
-          const f32x4 x = *reinterpret_cast<const f32x4*>(As + row * BK + 4 * ((2 * kc + lh) ^ swz<BK>(row)));
-          a_[a][0] = x[0]; a_[a][1] = x[1]; a_[a][2] = x[2]; a_[a][3] = x[3];
-        } else {
+    for (int a = 0; a < TM; ++a) {
+      const int row = wm0 + a * 32 + li;
+      if (A_KC) {
+        const f32x4 x = *reinterpret_cast<const f32x4*>(As + row * BK + 4 * ((2 * kc + lh) ^ swz<BK>(row)));
+        av[buf][a][0] = x[0]; av[buf][a][1] = x[1]; av[buf][a][2] = x[2]; av[buf][a][3] = x[3];
+      } else {
 #pragma unroll
-          for (int s = 0; s < 4; ++s) a_[a][s] = As[(8 * kc + 4 * lh + s) * BM + row];
-        }
+        for (int s = 0; s < 4; ++s) av[buf][a][s] = As[(8 * kc + 4 * lh + s) * BM + row];
       }
-#pragma unroll
-      for (int b = 0; b < TN; ++b) {
-        const int col = wn0 + b * 32 + li;
-        if (B_KC) {
-          const f32x4 x = *reinterpret_cast<const f32x4*>(Bs + col * BK + 4 * ((2 * kc + lh) ^ swz<BK>(col)));
-          b_[b][0] = x[0]; b_[b][1] = x[1]; b_[b][2] = x[2]; b_[b][3] = x[3];
-        } else {
-#pragma unroll
-          for (int s = 0; s < 4; ++s) b_[b][s] = Bs[(8 * kc + 4 * lh + s) * BN + col];
-        }
-      }
-    };
-    read_frags(0, av[0], bv[0]);
-#pragma unroll
-    for (int kc = 0; kc < BK / 8; ++kc) {
-      const int cur = kc & 1;
-      if (kc + 1 < BK / 8) read_frags(kc + 1, av[cur ^ 1], bv[cur ^ 1]);
-#pragma unroll
-      for (int s = 0; s < 4; ++s)
-#pragma unroll
-        for (int a = 0; a < TM; ++a)
-#pragma unroll
-          for (int b = 0; b < TN; ++b)
-            acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[cur][a][s], bv[cur][b][s], acc[a][b], 0, 0, 0);
     }
+#pragma unroll
+    for (int b = 0; b < TN; ++b) {
+      const int col = wn0 + b * 32 + li;
+      if (B_KC) {
+        const f32x4 x = *reinterpret_cast<const f32x4*>(Bs + col * BK + 4 * ((2 * kc + lh) ^ swz<BK>(col)));
+        bv[buf][b][0] = x[0]; bv[buf][b][1] = x[1]; bv[buf][b][2] = x[2]; bv[buf][b][3] = x[3];
+      } else {
+#pragma unroll
+        for (int s = 0; s < 4; ++s) bv[buf][b][s] = Bs[(8 * kc + 4 * lh + s) * BN + col];
+      }
+    }
+  };
+  auto mfmas = [&](int buf) {
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int a = 0; a < TM; ++a)
+#pragma unroll
+        for (int b = 0; b < TN; ++b)
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[buf][a][s], bv[buf][b][s], acc[a][b], 0, 0, 0);
+  };
+  // diagnostics only (wrong results): bit 0 no global loads in the k-loop, bit 1 no barriers,
+  // bit 2 no LDS fragment reads after the first
+  const bool noload = (p.diag_noload & 1) != 0, nobar = (p.diag_noload & 2) != 0,
+             noread = (p.diag_noload & 4) != 0;
+  auto slot = [&](int t) { return smem + ((noload ? 0 : t) % S) * ST_SZ; };
+  auto barrier = [&]() {
+    __builtin_amdgcn_sched_barrier(0);
+    if (!nobar) __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
   };
 
   const int nfull = K / BK;
-  // prologue: S-1 tiles in flight
+  // IL = 0: the DMA of k-tile t+S is issued in one burst right after the hand-over barrier.
+  // IL = 1: its G pieces are spread over the next KC chunks (piece group c = (kc + 2) % KC), one
+  //         group per MFMA chunk, so each wave's DMA issue hides under MFMAs (T3 interleave).
+  //         The prologue then issues tiles 0..S-2 plus the first half of tile S-1's pieces.
+  constexpr int GH = IL ? (2 * G) / KC : 0;  // pieces of the newest tile issued before its hand-over
+  auto pieces_of = [&](int c, int& g0, int& g1) { g0 = c * G / KC; g1 = (c + 1) * G / KC; };
 #pragma unroll
   for (int t = 0; t < S - 1; ++t)
     if (t < nfull) issue(t);
+  if (IL && S - 1 < nfull)
+#pragma unroll
+    for (int g = 0; g < GH; ++g) issue_piece(S - 1, g);
+  if (nfull > 0) {
+    // tile 0 must land; younger DMAs in flight: full tiles 1..S-2 (+ GH pieces of tile S-1)
+    int younger = (min(S - 2, nfull - 1)) * G + ((IL && S - 1 < nfull) ? GH : 0);
+    wait_vmcnt_le<3 * G + GH>(younger);
+    barrier();  // tile 0 landed in every wave's pieces
+    if (!IL && S - 1 < nfull && !noload) issue(S - 1);
+    read_frags(slot(0), 0, 0);
+    read_frags(slot(0), 1, 1);
+    if (noread) {
+      read_frags(slot(0), 2, 2);
+      read_frags(slot(0), 3, 3);
+    }
+  }
   for (int t = 0; t < nfull; ++t) {
-    // retire tile t: at most min(S-2, nfull-1-t) younger tiles may stay in flight
-    const int younger = min(S - 2, nfull - 1 - t);
-    if (younger >= 2) wait_vmcnt<2 * G>();
-    else if (younger == 1) wait_vmcnt<G>();
-    else wait_vmcnt<0>();
-    __builtin_amdgcn_s_barrier();  // every wave's pieces of tile t have landed; slot (t-1)%S is free
-    if (t + S - 1 < nfull && !p.diag_noload) issue(t + S - 1);
-    compute(smem + ((p.diag_noload ? 0 : t) % S) * ST_SZ);
+    const float* st = slot(t);
+#pragma unroll
+    for (int kc = 0; kc < KC; ++kc) {
+      const int nk = kc + 2;  // chunk whose fragments are read under this chunk's MFMAs
+      if (noread) {
+      } else if (nk < KC) {
+        read_frags(st, nk, nk % NB);
+      } else if (t + 1 < nfull) {
+        if (nk == KC) {
+          // hand over to tile t+1: this wave's reads of tile t are done (lgkmcnt 0), tile t+1
+          // has landed (vmcnt: only tiles t+2..t+S-1 may stay in flight), and after the barrier
+          // no wave reads tile t any more, so its slot takes the DMA of tile t+S
+          __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+          wait_vmcnt_le<3 * G + GH>(min(S - 2, nfull - 2 - t) * G);
+          barrier();
+          if (!IL && t + S < nfull && !noload) issue(t + S);
+        }
+        read_frags(slot(t + 1), nk - KC, nk % NB);
+      }
+      if (IL && !noload) {
+        const int T = (kc >= KC - 2) ? t + S : t + S - 1;  // tile whose pieces this chunk issues
+        if (T < nfull && (kc < KC - 2 || t + 1 < nfull)) {
+          int g0, g1;
+          pieces_of((kc + 2) % KC, g0, g1);
+#pragma unroll
+          for (int g = 0; g < G; ++g)
+            if (g >= g0 && g < g1) issue_piece(T, g);
+        }
+      }
+      mfmas(kc % NB);
+    }
   }
   if (K % BK) {
     // masked tail k-tile through registers, same swizzled image, in slot nfull % S
@@ -282,24 +359,345 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_f32_glds_kernel(const GemmP
       *reinterpret_cast<f32x4*>(st + A_SZ + u * 4) = x;
     }
     __syncthreads();
-    compute(st);
+#pragma unroll
+    for (int kc = 0; kc < KC; ++kc) {
+      read_frags(st, kc, kc % NB);
+      mfmas(kc % NB);
+    }
   }
   epilogue<TM, TN, EPI>(p, acc, bm, bn, wm0, wn0, li, lh);
+}
+
+
+// ---- element / 4-vector epilogues shared by the 16x16 kernel
+template <int EPI>
+__device__ __forceinline__ void epi_elem(const GemmP& p, int row, int col, float v) {
+  float* cp = p.C + (long)row * p.ldc + col;
+  if (EPI == EPI_STORE) {
+    *cp = (p.beta == 0.f) ? p.alpha * v : p.alpha * v + p.beta * *cp;
+  } else if (EPI == EPI_BIAS) {
+    *cp = v + p.bias[col];
+  } else if (EPI == EPI_BIAS_SIG) {
+    *cp = sigmoidf_ref(v + p.bias[col]);
+  } else if (EPI == EPI_DSIG) {
+    const float y = p.aux[(long)row * p.ldaux + col];
+    *cp = y * (1.f - y) * v;
+  } else {  // EPI_SGD
+    float c = v;
+    if (p.corr) {
+      float* qp = p.corr + (long)row * p.ldcorr + col;
+      c = v + p.mmt * *qp;
+      *qp = c;
+    }
+    float w = *cp;
+    w = w + p.scale * c;
+    w = w + p.l2 * w;
+    *cp = w;
+  }
+}
+
+// 4 consecutive columns col..col+3 (col % 4 == 0, every leading dimension % 4 == 0)
+template <int EPI>
+__device__ __forceinline__ void epi_vec4(const GemmP& p, int row, int col, f32x4 v) {
+  f32x4* cp = reinterpret_cast<f32x4*>(p.C + (long)row * p.ldc + col);
+  if (EPI == EPI_STORE) {
+    if (p.beta == 0.f) {
+      *cp = p.alpha * v;
+    } else {
+      *cp = p.alpha * v + p.beta * *cp;
+    }
+  } else if (EPI == EPI_BIAS || EPI == EPI_BIAS_SIG) {
+    f32x4 o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = EPI == EPI_BIAS ? v[e] + p.bias[col + e] : sigmoidf_ref(v[e] + p.bias[col + e]);
+    *cp = o;
+  } else if (EPI == EPI_DSIG) {
+    const f32x4 y = *reinterpret_cast<const f32x4*>(p.aux + (long)row * p.ldaux + col);
+    f32x4 o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = y[e] * (1.f - y[e]) * v[e];
+    *cp = o;
+  } else {  // EPI_SGD
+    f32x4 c = v;
+    if (p.corr) {
+      f32x4* qp = reinterpret_cast<f32x4*>(p.corr + (long)row * p.ldcorr + col);
+      c = v + p.mmt * *qp;
+      *qp = c;
+    }
+    f32x4 w = *cp;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      w[e] = w[e] + p.scale * c[e];
+      w[e] = w[e] + p.l2 * w[e];
+    }
+    *cp = w;
+  }
+}
+
+// =============================================================================================
+// 16x16x4 variant (v_mfma_f32_16x16x4_f32: 32 cycles per 1024 MACs; on this part it sustains a
+// higher clock than the 32x32x2 form -- tools/mfma_peak.hip: ~155 vs ~137-145 TFLOP/s).
+//   * lane l = 16*g + i supplies A[i][k] / B[k][i] with k = 16c + 4g + s for step s = 0..3 of a
+//     16-deep chunk c; D row = 4g + r (reg r), col = i.
+//   * k-contiguous operand: one ds_read_b128 per 16x16 tile per chunk = the 4 steps' k values
+//     (swizzled image as above).
+//   * m/n-contiguous operand: one ds_read_b128 per step per FOUR tiles -- the 4 consecutive floats
+//     feed 4 interleaved tiles (tile 4q+e holds rows/cols 64q + 4i + e), so every LDS read is a
+//     conflict-free b128 and, for an n-contiguous B, the epilogue stores 4 consecutive columns
+//     per lane as one 16-B store.
+// =============================================================================================
+template <int BM, int BN, int BK, int WM, int WN, int S, bool A_KC, bool B_KC, int EPI>
+__global__ __launch_bounds__(WM * WN * 64) void gemm16_kernel(const GemmP p) {
+  constexpr int NT = WM * WN * 64, NW = WM * WN;
+  constexpr int WTM = BM / WM, WTN = BN / WN;  // wave tile
+  constexpr int TM = WTM / 16, TN = WTN / 16;
+  static_assert(WTM % 16 == 0 && WTN % 16 == 0, "16x16 tiles per wave");
+  static_assert(A_KC || TM % 4 == 0, "m-contiguous A interleaves 4 tiles per read");
+  static_assert(B_KC || TN % 4 == 0, "n-contiguous B interleaves 4 tiles per read");
+  static_assert(BK == 32 || BK == 64, "BK");
+  constexpr int CH = BK / 4, KCH = BK / 16;
+  constexpr int A_SZ = BM * BK, B_SZ = BN * BK, ST_SZ = A_SZ + B_SZ;
+  constexpr int GA = A_SZ / 4 / NT, GB = B_SZ / 4 / NT, G = GA + GB;
+  static_assert(A_SZ % (4 * NT) == 0 && B_SZ % (4 * NT) == 0, "tile splits into 1-KiB wave pieces");
+  static_assert(3 * G < 64, "vmcnt range");
+  __shared__ __attribute__((aligned(16))) float smem[S * ST_SZ];
+
+  const int M = p.M, N = p.N, K = p.K;
+  const int nbn = (N + BN - 1) / BN, nbm = (M + BM - 1) / BM;
+  const int nwg = nbm * nbn;
+  const int bid = blockIdx.x, xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int L = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int grp = p.group, per_group = grp * nbn;
+  const int first_m = (L / per_group) * grp;
+  const int gsz = min(nbm - first_m, grp);
+  const int bm = (first_m + (L % per_group) % gsz) * BM, bn = ((L % per_group) / gsz) * BN;
+
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int wm0 = (wid / WN) * WTM, wn0 = (wid % WN) * WTN;
+  const int lg = lane >> 4, li = lane & 15;
+
+  long srcA[GA], srcB[GB];
+#pragma unroll
+  for (int g = 0; g < GA; ++g) {
+    const int u = (g * NW + wid) * 64 + lane;
+    if (A_KC) {
+      const int r = u / CH, j = u % CH;
+      srcA[g] = (long)min(bm + r, M - 1) * p.lda + 4 * (j ^ swz<BK>(r));
+    } else {
+      const int k = u / (BM / 4), c = (u % (BM / 4)) * 4;
+      srcA[g] = (long)k * p.lda + (bm + c < M ? bm + c : 0);
+    }
+  }
+#pragma unroll
+  for (int g = 0; g < GB; ++g) {
+    const int u = (g * NW + wid) * 64 + lane;
+    if (B_KC) {
+      const int r = u / CH, j = u % CH;
+      srcB[g] = (long)min(bn + r, N - 1) * p.ldb + 4 * (j ^ swz<BK>(r));
+    } else {
+      const int k = u / (BN / 4), c = (u % (BN / 4)) * 4;
+      srcB[g] = (long)k * p.ldb + (bn + c < N ? bn + c : 0);
+    }
+  }
+  auto issue = [&](int t) {
+    float* st = smem + (t % S) * ST_SZ;
+    const long ka = A_KC ? (long)t * BK : (long)t * BK * p.lda;
+    const long kb = B_KC ? (long)t * BK : (long)t * BK * p.ldb;
+#pragma unroll
+    for (int g = 0; g < GA; ++g)
+      __builtin_amdgcn_global_load_lds((const void*)(p.A + ka + srcA[g]), (void*)(st + (g * NW + wid) * 256), 16, 0,
+                                       0);
+#pragma unroll
+    for (int g = 0; g < GB; ++g)
+      __builtin_amdgcn_global_load_lds((const void*)(p.B + kb + srcB[g]), (void*)(st + A_SZ + (g * NW + wid) * 256),
+                                       16, 0, 0);
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int b = 0; b < TN; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  float av[2][TM][4], bv[2][TN][4];
+  auto read_frags = [&](const float* st, int c, int buf) {  // chunk c (16 k) of the slot at st
+    const float* As = st;
+    const float* Bs = st + A_SZ;
+    if (A_KC) {
+#pragma unroll
+      for (int a = 0; a < TM; ++a) {
+        const int row = wm0 + 16 * a + li;
+        const f32x4 x = *reinterpret_cast<const f32x4*>(As + row * BK + 4 * ((4 * c + lg) ^ swz<BK>(row)));
+#pragma unroll
+        for (int s = 0; s < 4; ++s) av[buf][a][s] = x[s];
+      }
+    } else {
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int q = 0; q < TM / 4; ++q) {
+          const f32x4 x = *reinterpret_cast<const f32x4*>(As + (16 * c + 4 * lg + s) * BM + wm0 + 64 * q + 4 * li);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) av[buf][4 * q + e][s] = x[e];
+        }
+    }
+    if (B_KC) {
+#pragma unroll
+      for (int b = 0; b < TN; ++b) {
+        const int col = wn0 + 16 * b + li;
+        const f32x4 x = *reinterpret_cast<const f32x4*>(Bs + col * BK + 4 * ((4 * c + lg) ^ swz<BK>(col)));
+#pragma unroll
+        for (int s = 0; s < 4; ++s) bv[buf][b][s] = x[s];
+      }
+    } else {
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int q = 0; q < TN / 4; ++q) {
+          const f32x4 x = *reinterpret_cast<const f32x4*>(Bs + (16 * c + 4 * lg + s) * BN + wn0 + 64 * q + 4 * li);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) bv[buf][4 * q + e][s] = x[e];
+        }
+    }
+  };
+  auto mfmas = [&](int buf) {
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int a = 0; a < TM; ++a)
+#pragma unroll
+        for (int b = 0; b < TN; ++b)
+          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[buf][a][s], bv[buf][b][s], acc[a][b], 0, 0, 0);
+  };
+  // diagnostics only (wrong results): bit 0 no global loads in the k-loop, bit 1 no barriers
+  const bool noload = (p.diag_noload & 1) != 0, nobar = (p.diag_noload & 2) != 0;
+  auto barrier = [&]() {
+    __builtin_amdgcn_sched_barrier(0);
+    if (!nobar) __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  auto slot = [&](int t) { return smem + ((noload ? 0 : t) % S) * ST_SZ; };
+
+  const int nfull = K / BK;
+#pragma unroll
+  for (int t = 0; t < S - 1; ++t)
+    if (t < nfull) issue(t);
+  if (nfull > 0) {
+    wait_vmcnt_le<3 * G>(min(S - 2, nfull - 1) * G);
+    barrier();  // tile 0 landed in every wave's pieces
+    if (S - 1 < nfull && !noload) issue(S - 1);
+    read_frags(slot(0), 0, 0);
+  }
+  for (int t = 0; t < nfull; ++t) {
+    const float* st = slot(t);
+#pragma unroll
+    for (int c = 0; c < KCH; ++c) {
+      const int buf = c & 1;  // KCH is even: chunk 0 of every tile uses buffer 0
+      if (c + 1 < KCH) {
+        read_frags(st, c + 1, buf ^ 1);
+      } else if (t + 1 < nfull) {
+        // hand over to tile t+1 under the last chunk's MFMAs (see gemm_f32_glds_kernel)
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+        wait_vmcnt_le<3 * G>(min(S - 2, nfull - 2 - t) * G);
+        barrier();
+        if (t + S < nfull && !noload) issue(t + S);
+        read_frags(slot(t + 1), 0, buf ^ 1);
+      }
+      mfmas(buf);
+    }
+  }
+  if (K % BK) {
+    // masked tail k-tile through registers, same images, in slot nfull % S
+    __builtin_amdgcn_s_barrier();
+    float* st = smem + (nfull % S) * ST_SZ;
+    const int k0 = nfull * BK;
+    for (int u = threadIdx.x; u < A_SZ / 4; u += NT) {
+      int gr, gc;
+      if (A_KC) { const int r = u / CH, j = u % CH; gr = bm + r; gc = k0 + 4 * (j ^ swz<BK>(r)); }
+      else { const int k = u / (BM / 4); gr = k0 + k; gc = bm + (u % (BM / 4)) * 4; }
+      const int rmax = A_KC ? M : K, cmax = A_KC ? K : M;
+      f32x4 x = {0.f, 0.f, 0.f, 0.f};
+      if (gr < rmax) {
+        const float* q = p.A + (long)gr * p.lda + gc;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) x[e] = (gc + e < cmax) ? q[e] : 0.f;
+      }
+      *reinterpret_cast<f32x4*>(st + u * 4) = x;
+    }
+    for (int u = threadIdx.x; u < B_SZ / 4; u += NT) {
+      int gr, gc;
+      if (B_KC) { const int r = u / CH, j = u % CH; gr = bn + r; gc = k0 + 4 * (j ^ swz<BK>(r)); }
+      else { const int k = u / (BN / 4); gr = k0 + k; gc = bn + (u % (BN / 4)) * 4; }
+      const int rmax = B_KC ? N : K, cmax = B_KC ? K : N;
+      f32x4 x = {0.f, 0.f, 0.f, 0.f};
+      if (gr < rmax) {
+        const float* q = p.B + (long)gr * p.ldb + gc;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) x[e] = (gc + e < cmax) ? q[e] : 0.f;
+      }
+      *reinterpret_cast<f32x4*>(st + A_SZ + u * 4) = x;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < KCH; ++c) {
+      read_frags(st, c, 0);
+      mfmas(0);
+    }
+  }
+
+  // ---- epilogue
+#pragma unroll
+  for (int a = 0; a < TM; ++a) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = A_KC ? bm + wm0 + 16 * a + 4 * lg + r : bm + wm0 + 64 * (a / 4) + 4 * (4 * lg + r) + (a % 4);
+      if (row >= M) continue;
+      if (!B_KC) {
+#pragma unroll
+        for (int q = 0; q < TN / 4; ++q) {
+          const int col = bn + wn0 + 64 * q + 4 * li;
+          f32x4 v;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = acc[a][4 * q + e][r];
+          if (col + 3 < N) epi_vec4<EPI>(p, row, col, v);
+          else
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              if (col + e < N) epi_elem<EPI>(p, row, col + e, v[e]);
+        }
+      } else {
+#pragma unroll
+        for (int b = 0; b < TN; ++b) {
+          const int col = bn + wn0 + 16 * b + li;
+          if (col < N) epi_elem<EPI>(p, row, col, acc[a][b][r]);
+        }
+      }
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------------------------
 // host-side dispatch
 // ---------------------------------------------------------------------------------------------
-// name: g<BM>x<BN>k<BK>s<S>w<waves>  (waves laid out WMxWN)
-#define TNET_GEMM_CFGS(X)                   \
-  X(g64x64k32s4w4, 64, 64, 32, 2, 2, 4)     \
-  X(g64x64k64s2w4, 64, 64, 64, 2, 2, 2)     \
-  X(g64x64k32s4w2, 64, 64, 32, 2, 1, 4)     \
-  X(g64x64k64s2w2, 64, 64, 64, 2, 1, 2)     \
-  X(g128x64k32s3w4, 128, 64, 32, 2, 2, 3)   \
-  X(g64x128k32s3w4, 64, 128, 32, 2, 2, 3)   \
-  X(g128x128k32s2w4, 128, 128, 32, 2, 2, 2) \
-  X(g128x128k32s3w8, 128, 128, 32, 2, 4, 3)
+// name: g<BM>x<BN>k<BK>s<S>w<waves>[i]: 32x32x2 kernel (waves laid out WMxWN; i = DMA pieces
+//       interleaved); m<BM>x<BN>k<BK>s<S>[w<WM><WN>]: 16x16x4 kernel (default 2x2 waves)
+#define TNET_GEMM_CFGS(X)                                 \
+  X(g64x64k32s4w4, 0, 64, 64, 32, 2, 2, 4, 0)            \
+  X(g64x64k32s4w4i, 0, 64, 64, 32, 2, 2, 4, 1)           \
+  X(g64x64k64s2w4, 0, 64, 64, 64, 2, 2, 2, 0)            \
+  X(g64x64k32s4w2, 0, 64, 64, 32, 2, 1, 4, 0)            \
+  X(g128x64k32s3w4, 0, 128, 64, 32, 2, 2, 3, 0)          \
+  X(g64x128k32s3w4, 0, 64, 128, 32, 2, 2, 3, 0)          \
+  X(g128x128k32s3w8, 0, 128, 128, 32, 2, 4, 3, 0)        \
+  X(m64x128k32s4, 1, 64, 128, 32, 2, 2, 4, 0)            \
+  X(m64x128k64s3, 1, 64, 128, 64, 2, 2, 3, 0)            \
+  X(m64x64k32s4w41, 1, 64, 64, 32, 4, 1, 4, 0)           \
+  X(m128x128k32s3, 1, 128, 128, 32, 2, 2, 3, 0)          \
+  X(m128x128k64s2, 1, 128, 128, 64, 2, 2, 2, 0)          \
+  X(m64x128k32s4w12, 1, 64, 128, 32, 1, 2, 4, 0)         \
+  X(m64x128k32s3, 1, 64, 128, 32, 2, 2, 3, 0)            \
+  X(m64x128k32s2, 1, 64, 128, 32, 2, 2, 2, 0)            \
+  X(m64x128k64s2, 1, 64, 128, 64, 2, 2, 2, 0)
 
 enum GemmCfg {
 #define X(name, ...) CFG_##name,
@@ -328,28 +726,49 @@ static int forced_cfg() {
   return g_cfg;
 }
 
-template <int BM, int BN, int BK, int WM, int WN, int S, bool A_KC, bool B_KC, int EPI>
-static void launch_glds(const GemmP& p, hipStream_t st) {
+template <int KIND, int BM, int BN, int BK, int WM, int WN, int S, int IL, bool A_KC, bool B_KC, int EPI>
+static bool launch_cfg(const GemmP& p, hipStream_t st) {
   const unsigned tiles = (unsigned)((long)cdiv(p.M, BM) * cdiv(p.N, BN));
-  gemm_f32_glds_kernel<BM, BN, BK, WM, WN, S, A_KC, B_KC, EPI><<<tiles, WM * WN * 64, 0, st>>>(p);
+  if constexpr (KIND == 0) {
+    gemm_f32_glds_kernel<BM, BN, BK, WM, WN, S, IL, A_KC, B_KC, EPI><<<tiles, WM * WN * 64, 0, st>>>(p);
+    return true;
+  } else {
+    constexpr int TM = BM / WM / 16, TN = BN / WN / 16;
+    if constexpr ((A_KC || TM % 4 == 0) && (B_KC || TN % 4 == 0)) {
+      gemm16_kernel<BM, BN, BK, WM, WN, S, A_KC, B_KC, EPI><<<tiles, WM * WN * 64, 0, st>>>(p);
+      return true;
+    } else {
+      return false;  // this tile cannot hold the operand layout
+    }
+  }
 }
 
 template <bool A_KC, bool B_KC, int EPI>
 static int launch_gemm(const GemmP& p_in, hipStream_t st) {
   if (p_in.M <= 0 || p_in.N <= 0) return TNET_OK;
-  static const int noload = getenv("TNET_GEMM_DIAG_NOLOAD") ? 1 : 0;
+  static const int noload = getenv("TNET_GEMM_DIAG") ? atoi(getenv("TNET_GEMM_DIAG")) : 0;
   GemmP p = p_in;
   p.diag_noload = noload;
   int cfg = forced_cfg();
-  if (cfg < 0) cfg = CFG_g64x64k32s4w4;
+  if (cfg < 0) {
+    // measured per-shape choice (tools/gemm_sweep.py on MI355X, round 1): the largest tile that
+    // still gives ~one workgroup per CU (256 CUs), the 16x16x4 kernel where the layout allows
+    const long t128 = (long)cdiv(p.M, 128) * cdiv(p.N, 128), t64x128 = (long)cdiv(p.M, 64) * cdiv(p.N, 128);
+    if (t128 >= 240) cfg = CFG_m128x128k64s2;
+    else if (A_KC && p.K < 1024) cfg = CFG_m64x64k32s4w41;
+    else if (A_KC && t64x128 >= 200) cfg = CFG_m64x128k64s2;
+    else cfg = CFG_g64x64k32s4w4;
+  }
   p.group = g_group > 0 ? g_group : 8;
+  bool ok = false;
   switch (cfg) {
-#define X(name, BM, BN, BK, WM, WN, S) \
-  case CFG_##name: launch_glds<BM, BN, BK, WM, WN, S, A_KC, B_KC, EPI>(p, st); break;
+#define X(name, KIND, BM, BN, BK, WM, WN, S, IL) \
+  case CFG_##name: ok = launch_cfg<KIND, BM, BN, BK, WM, WN, S, IL, A_KC, B_KC, EPI>(p, st); break;
     TNET_GEMM_CFGS(X)
 #undef X
     default: return TNET_ERR_ARG;
   }
+  if (!ok) launch_cfg<0, 64, 64, 32, 2, 2, 4, 0, A_KC, B_KC, EPI>(p, st);  // layout not supported by cfg
   TNET_LAUNCH_CHECK();
   return TNET_OK;
 }
@@ -430,6 +849,7 @@ extern "C" int tnet_affine_update(const float* X, TnetMatrixDim dX, const float*
   p.A = X; p.lda = dX.stride; p.B = E; p.ldb = dE.stride; p.C = W; p.ldc = dW.stride;
   p.corr = (mmt != 0.f || corrW) ? corrW : nullptr; p.ldcorr = strideCorr;
   if (mmt != 0.f && !corrW) return TNET_ERR_ARG;
+  if (p.corr && (p.ldcorr & 3)) return TNET_ERR_ARG;
   p.scale = scale; p.mmt = mmt; p.l2 = l2;
   int st = check_common(p);
   if (st) return st;

@@ -131,7 +131,7 @@ static int cmd_shuffle(int argc, char** argv) {
 // one HTK/MLF reader thread + <threads> SGD workers over row slices of each bunch), set up the way
 // src/TNet.cc:160-320 sets it up with default feature options, and timed around RunTrain ONLY
 // (TNet's own FPS line also counts reading and writing the model text: TNet.cc:321-362).
-// Prints "frames <n> seconds <t> xent <x> correct <c>".  Used as the CPU baseline of bench.py.
+// Prints "HARNESS_RESULT frames <n> seconds <t>" on stderr.  Used as the CPU baseline of bench.py.
 static int cmd_train(int argc, char** argv) {
   if (argc < 12) { std::cerr << "usage: train nnet scp mlf statemap lbl_dir threads bunch cache lr seed\n"; return 2; }
   UserInterface ui;  // no options set: every feature parameter takes its default
@@ -166,7 +166,8 @@ static int cmd_train(int argc, char** argv) {
   timer.Start();
   pl.RunTrain(threads);
   timer.End();
-  std::cout << "frames " << pl.obj_fun_->GetFrames() << " seconds " << timer.Val() << "\n";
+  // on stderr: the worker threads may still be printing to stdout
+  std::cerr << "HARNESS_RESULT frames " << pl.obj_fun_->GetFrames() << " seconds " << timer.Val() << std::endl;
   return 0;
 }
 

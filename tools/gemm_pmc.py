@@ -1,0 +1,33 @@
+"""Drive one GEMM shape repeatedly for rocprofv3 --pmc passes: our fused affine kernels
+(TNET_GEMM_CFG selects the tile config) and, for comparison, torch.mm (hipBLASLt) on the same
+shapes and data distribution.  usage: python tools/gemm_pmc.py [ours|torch] [iters]"""
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "nnet-asr_amd"))
+import numpy as np  # noqa: E402
+
+which = sys.argv[1] if len(sys.argv) > 1 else "ours"
+iters = int(sys.argv[2]) if len(sys.argv) > 2 else 20
+rows, ni, no = 1024, 2048, 2048
+if which == "ours":
+    from tnet_amd import DeviceArray
+    from tnet_amd._lib import check, lib
+    S = lib().tnet_stream()
+    rng = np.random.default_rng(0)
+    X = DeviceArray.from_numpy(rng.standard_normal((rows, ni)).astype(np.float32))
+    W = DeviceArray.from_numpy((0.05 * rng.standard_normal((ni, no))).astype(np.float32))
+    b = DeviceArray.vector(np.zeros(no, np.float32))
+    Y = DeviceArray(rows, no)
+    for _ in range(iters):
+        check(lib().tnet_affine_fwd(X.ptr, X.dim, W.ptr, W.dim, b.ptr, Y.ptr, Y.dim, 1, S))
+    check(lib().tnet_synchronize())
+else:
+    import torch
+    torch.backends.cuda.matmul.allow_tf32 = False
+    a = torch.randn(rows, ni, device="cuda")
+    w = 0.05 * torch.randn(ni, no, device="cuda")
+    for _ in range(iters):
+        c = a @ w
+    torch.cuda.synchronize()

@@ -55,16 +55,19 @@ print("RESULT " + json.dumps(out))
 def main():
     iters = int(sys.argv[1]) if len(sys.argv) > 1 else 20
     cfgs = sys.argv[2].split(",") if len(sys.argv) > 2 else CFGS
+    shapes = json.loads(sys.argv[3]) if len(sys.argv) > 3 else SHAPES
     res = {}
     for cfg in cfgs:
         parts = cfg.split("+")
         env = dict(os.environ, TNET_GEMM_CFG=parts[0])
         for extra in parts[1:]:
             if extra == "noload":
-                env["TNET_GEMM_DIAG_NOLOAD"] = "1"
+                env["TNET_GEMM_DIAG"] = "1"
+            elif extra.startswith("diag"):
+                env["TNET_GEMM_DIAG"] = extra[4:]
             elif extra.startswith("g") and extra[1:].isdigit():
                 env["TNET_GEMM_GROUP"] = extra[1:]
-        p = subprocess.run([sys.executable, "-c", CHILD, REPO, json.dumps(SHAPES), str(iters)], env=env,
+        p = subprocess.run([sys.executable, "-c", CHILD, REPO, json.dumps(shapes), str(iters)], env=env,
                            capture_output=True, text=True, timeout=300)
         line = [l for l in p.stdout.splitlines() if l.startswith("RESULT ")]
         if p.returncode != 0 or not line:
