@@ -133,12 +133,17 @@ int tnet_gemm_config(const char* name);
  * Fused kernels of the MI355X SGD path (no reference counterpart: each replaces a chain of
  * reference calls, cited per function).
  * ---------------------------------------------------------------------------------- */
-/* Y = act(X W + b), act = 0 none | 1 sigmoid.  X [rows x n_in], W [n_in x n_out] (memory layout
- * of CuBiasedLinearity::mLinearity), b [n_out].
+/* Y = act(X W + b), act = 0 none | 1 sigmoid | 2 negated (-(XW+b)) | 3 negated sigmoid.
+ * X [rows x n_in], W [n_in x n_out] (memory layout of CuBiasedLinearity::mLinearity), b [n_out].
  * Replaces AddScaledRow + Gemm('N','N') + CuMath::Sigmoid (cuBiasedLinearity.cc:11-16,
- * cuActivation.cc:11-14). */
+ * cuActivation.cc:11-14; CuRbm::PropagateFnc cuRbm.cc:15-23). The negated forms write the RBM
+ * negative-phase hidden statistics with the sign the fused update needs (tnet_rbm_update). */
 int tnet_affine_fwd(const float* X, TnetMatrixDim dX, const float* W, TnetMatrixDim dW, const float* b,
                     float* Y, TnetMatrixDim dY, int act, void* stream);
+/* Y = act(X W^T + b), act = 0 none | 1 sigmoid; X [rows x n_out], W [n_in x n_out], b [n_in].
+ * Replaces CuRbm::Reconstruct (cuRbm.cc:117-128: AddScaledRow + Gemm('N','T') + Sigmoid). */
+int tnet_affine_fwd_t(const float* X, TnetMatrixDim dX, const float* W, TnetMatrixDim dW, const float* b,
+                      float* Y, TnetMatrixDim dY, int act, void* stream);
 /* Eo = (E W^T) .* Ybelow (1 - Ybelow)  (dsig=1)  or  Eo = E W^T (dsig=0).
  * Replaces Gemm('N','T') + CuMath::DiffSigmoid (cuBiasedLinearity.cc:21-25, cuActivation.cc:19-22). */
 int tnet_affine_bwd(const float* E, TnetMatrixDim dE, const float* W, TnetMatrixDim dW, const float* Ybelow,
@@ -164,6 +169,38 @@ int tnet_sgd_update(float* p, const float* g, float* corr, long n, float scale, 
  * If grad_out != NULL the raw colsum is written there instead and b is not touched (DP path). */
 int tnet_bias_update(const float* E, TnetMatrixDim dE, float* b, float* corr_b, float* grad_out, float scale,
                      float mmt, void* workspace, void* stream);
+/* ---- RBM contrastive divergence (CuRbm::RbmUpdate, cuRbm.cc:133-174) ----------------------
+ * V [2B x n_vis] = [pos_vis ; neg_vis] and H [2B x n_hid] = [pos_hid ; -neg_hid] row-stacked:
+ *   corr = mmt*corr + scale*(V^T H) + l2*W ; W += corr
+ * with scale = lr/B and l2 = -lr*wc.  One GEMM over K = 2B replaces the reference's two
+ * Gemm('T','N') calls + AddScaled(-lr*wc) + AddScaled into W. */
+int tnet_rbm_update(const float* V, TnetMatrixDim dV, const float* H, TnetMatrixDim dH, float* W,
+                    TnetMatrixDim dW, float* corrW, int strideCorr, float scale, float mmt, float l2,
+                    void* stream);
+/* RBM bias update (cuRbm.cc:148-164): rows from neg_from on enter negated,
+ *   corr_b = mmt*corr_b + scale*(sum_{r<neg_from} M[r] - sum_{r>=neg_from} M[r]) ; b += corr_b. */
+int tnet_rbm_bias_update(const float* M, TnetMatrixDim d, int neg_from, float* b, float* corr_b, float scale,
+                         float mmt, void* workspace, void* stream);
+
+/* ---- per-element HybridTaus random numbers (CuRand, curand.tcc / curandkernels.cu) ----------
+ * z1..z4: four uint32 state arrays with the element layout of the target matrix (index =
+ * col + row*stride), seeded by the caller with lrand48() values > 128 (curand.tcc:36-45) and
+ * advanced in place. */
+/* mat = U(0,1) (cudaF_rand, curandkernels.cu:46-52) */
+int tnetF_rand(float* mat, TnetMatrixDim d, unsigned* z1, unsigned* z2, unsigned* z3, unsigned* z4, void* stream);
+/* mat = N(0,1) by Box-Muller (cudaF_gauss_rand, curandkernels.cu:69-77) */
+int tnetF_gauss_rand(float* mat, TnetMatrixDim d, unsigned* z1, unsigned* z2, unsigned* z3, unsigned* z4,
+                     void* stream);
+/* states = probs > rnd ? 1 : 0 (cudaF_binarize_probs, curandkernels.cu:80-88) */
+int tnetF_binarize_probs(float* states, const float* probs, const float* rnd, TnetMatrixDim d, void* stream);
+/* states = probs > U(0,1) ? 1 : 0 in one pass (CuRand::BinarizeProbs = Rand + binarize,
+ * curand.tcc:121-134); d describes probs and the state arrays. */
+int tnet_rand_binarize(float* states, int ld_states, const float* probs, TnetMatrixDim d, unsigned* z1,
+                       unsigned* z2, unsigned* z3, unsigned* z4, void* stream);
+/* mat += scale * N(0,1) (CuRand::AddGaussNoise, curand.tcc:55-60) */
+int tnet_add_gauss_noise(float* mat, TnetMatrixDim d, float scale, unsigned* z1, unsigned* z2, unsigned* z3,
+                         unsigned* z4, void* stream);
+
 /* Fused softmax + cross-entropy + error + accuracy for class-id targets
  * (CuSoftmax::PropagateFnc + CuCrossEntropy::Evaluate, cuActivation.cc:28-31,
  *  cuObjectiveFunction.cc:50-83; kernels _softmax, _add_scaled, _check_class, _log_elem,

@@ -26,6 +26,7 @@ typedef struct TnetNetwork TnetNetwork;
 typedef struct TnetObjective TnetObjective;
 typedef struct TnetTrainer TnetTrainer;
 typedef struct TnetComm TnetComm;
+typedef struct TnetRbmTrainer TnetRbmTrainer;
 
 const char* tnet_last_error(void);
 
@@ -109,6 +110,29 @@ int tnet_trainer_set_comm(TnetTrainer* t, TnetComm* comm);
 /* data-parallel steps this rank joined without a bunch of its own (zero gradient) */
 long tnet_trainer_empty_steps(TnetTrainer* t);
 int tnet_trainer_trace(TnetTrainer* t, int trace);
+
+/* ---- RBM pre-training (CuRbm, cuRbm.cc; the TRbmCu loop, TRbmCu.cc:291-357) ----------------
+ * <rbm> parameters: W [n_vis x n_hid] (host row-major), visible / hidden biases; types[0..1] =
+ * visible / hidden unit type (0 Bernoulli, 1 Gaussian; -1 in set = keep). */
+int tnet_net_rbm_get(TnetNetwork* net, int i, float* W, float* vis_bias, float* hid_bias, int* types);
+int tnet_net_rbm_set(TnetNetwork* net, int i, const float* W, const float* vis_bias, const float* hid_bias,
+                     int vis_type, int hid_type);
+/* CuRbm::RbmUpdate on four device matrices [rows x n_vis|n_hid] (cuRbm.cc:133-174) */
+int tnet_net_rbm_update(TnetNetwork* net, int i, const float* pos_vis, const float* pos_hid, const float* neg_vis,
+                        const float* neg_hid, int rows, int ld_vis, int ld_hid);
+/* CD-1 trainer over a one-<rbm> network (TRbmCu): per bunch positive phase, sample (Bernoulli)
+ * or Gaussian noise, reconstruct, negative phase, update, reconstruction MSE. seed as TRbmCu
+ * --SEED (CuRand state drawn first, then the cache shuffles, one lrand48 stream). */
+TnetRbmTrainer* tnet_rbm_trainer_create(TnetNetwork* net, int bunchsize, int cachesize, long seed, int randomize,
+                                        float learn_rate, float momentum, float weightcost);
+int tnet_rbm_trainer_free(TnetRbmTrainer* t);
+int tnet_rbm_trainer_add_utterance(TnetRbmTrainer* t, const float* feats, int rows, int cols, int ld);
+int tnet_rbm_trainer_finish(TnetRbmTrainer* t);
+long tnet_rbm_trainer_steps(TnetRbmTrainer* t);
+int tnet_rbm_trainer_stats(TnetRbmTrainer* t, double* mse, long* frames);
+int tnet_rbm_trainer_report(TnetRbmTrainer* t, char* buf, int cap); /* "Mse:... frames:... err/frm:..." */
+long tnet_rbm_trainer_prefill(TnetRbmTrainer* t, const float* feats, int rows, int cols, int ld);
+int tnet_rbm_trainer_replay(TnetRbmTrainer* t, long nsteps);
 
 /* ---- data parallel (no reference counterpart: Platform.h:143-391 is the CPU analogue) ---- */
 int tnet_comm_unique_id(char out[128]);        /* rank 0 creates, the launcher broadcasts it */

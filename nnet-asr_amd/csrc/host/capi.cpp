@@ -6,6 +6,7 @@
 #include <string>
 
 #include "tnet_train.h"
+#include "curbm.h"
 #include "trainer.h"
 
 using namespace TNet;
@@ -39,6 +40,9 @@ struct TnetObjective {
 };
 struct TnetTrainer {
   std::unique_ptr<CuTrainer> t;
+};
+struct TnetRbmTrainer {
+  std::unique_ptr<CuRbmTrainer> t;
 };
 struct TnetComm {
   std::unique_ptr<GradExchange> ex;
@@ -378,6 +382,106 @@ int tnet_trainer_set_comm(TnetTrainer* t, TnetComm* c) {
 long tnet_trainer_empty_steps(TnetTrainer* t) { return t ? t->t->EmptySteps() : -1; }
 int tnet_trainer_trace(TnetTrainer* t, int trace) {
   TRY_BEGIN t->t->Cache().Trace(trace);
+  TRY_END
+}
+
+// ------------------------------------------------------------------------------------ RBM
+static CuRbm& rbm_layer(TnetNetwork* h, int i) {
+  if (i < 0 || i >= h->net.Layers()) Error("component index out of range");
+  auto* p = dynamic_cast<CuRbm*>(&h->net.Layer(i));
+  if (!p) Error("component is not <rbm>");
+  return *p;
+}
+int tnet_net_rbm_get(TnetNetwork* h, int i, float* W, float* vb, float* hb, int* types) {
+  TRY_BEGIN CuRbm& R = rbm_layer(h, i);
+  if (W) R.VisHid().CopyToHost(W, R.VisHid().Cols());
+  if (vb) R.VisBias().CopyToHost(vb);
+  if (hb) R.HidBias().CopyToHost(hb);
+  if (types) {
+    types[0] = R.VisType() == CuRbm::BERNOULLI ? 0 : 1;
+    types[1] = R.HidType() == CuRbm::BERNOULLI ? 0 : 1;
+  }
+  TRY_END
+}
+int tnet_net_rbm_set(TnetNetwork* h, int i, const float* W, const float* vb, const float* hb, int vis_type,
+                     int hid_type) {
+  TRY_BEGIN CuRbm& R = rbm_layer(h, i);
+  if (W) R.VisHid().CopyFromHost(W, R.VisHid().Rows(), R.VisHid().Cols(), R.VisHid().Cols());
+  if (vb) R.VisBias().CopyFromHost(vb, R.VisBias().Dim());
+  if (hb) R.HidBias().CopyFromHost(hb, R.HidBias().Dim());
+  if (vis_type >= 0 && hid_type >= 0)
+    R.SetUnitTypes(vis_type == 0 ? CuRbm::BERNOULLI : CuRbm::GAUSSIAN, hid_type == 0 ? CuRbm::BERNOULLI : CuRbm::GAUSSIAN);
+  CuDevice::Instantiate().Synchronize();
+  TRY_END
+}
+int tnet_net_rbm_update(TnetNetwork* h, int i, const float* pos_vis, const float* pos_hid, const float* neg_vis,
+                        const float* neg_hid, int rows, int ldv, int ldh) {
+  TRY_BEGIN CuRbm& R = rbm_layer(h, i);
+  CuMatrix<BaseFloat> pv, ph, nv, nh;
+  const size_t V = R.GetNInputs(), H = R.GetNOutputs();
+  CuMatrix<BaseFloat>::MakeView(pv, const_cast<float*>(pos_vis), rows, V, ldv);
+  CuMatrix<BaseFloat>::MakeView(ph, const_cast<float*>(pos_hid), rows, H, ldh);
+  CuMatrix<BaseFloat>::MakeView(nv, const_cast<float*>(neg_vis), rows, V, ldv);
+  CuMatrix<BaseFloat>::MakeView(nh, const_cast<float*>(neg_hid), rows, H, ldh);
+  R.RbmUpdate(pv, ph, nv, nh);
+  TRY_END
+}
+TnetRbmTrainer* tnet_rbm_trainer_create(TnetNetwork* net, int bunchsize, int cachesize, long seed, int randomize,
+                                        float lr, float mmt, float wc) {
+  try {
+    // TRbmCu.cc:221-243: the network holds exactly one <rbm>; lr / momentum / weight cost set on it
+    if (net->net.Layers() != 1) Error("Number of layers must be 1");
+    CuRbm& R = rbm_layer(net, 0);
+    R.LearnRate(lr);
+    R.Momentum(mmt);
+    R.Weightcost(wc);
+    RbmTrainerOptions opt;
+    opt.bunchsize = (size_t)bunchsize;
+    opt.cachesize = (size_t)cachesize;
+    opt.seed = seed;
+    opt.randomize = randomize != 0;
+    std::unique_ptr<TnetRbmTrainer> h(new TnetRbmTrainer);
+    h->t.reset(new CuRbmTrainer(&R, opt));
+    return h.release();
+  }
+  TRY_END_PTR
+}
+int tnet_rbm_trainer_free(TnetRbmTrainer* t) {
+  TRY_BEGIN delete t;
+  TRY_END
+}
+int tnet_rbm_trainer_add_utterance(TnetRbmTrainer* t, const float* feats, int rows, int cols, int ld) {
+  TRY_BEGIN t->t->AddUtterance(feats, (size_t)rows, (size_t)cols, (size_t)ld);
+  TRY_END
+}
+int tnet_rbm_trainer_finish(TnetRbmTrainer* t) {
+  TRY_BEGIN t->t->Finish();
+  TRY_END
+}
+long tnet_rbm_trainer_steps(TnetRbmTrainer* t) { return t ? t->t->Steps() : -1; }
+int tnet_rbm_trainer_stats(TnetRbmTrainer* t, double* mse, long* frames) {
+  TRY_BEGIN if (mse) *mse = t->t->Mse().GetError();
+  if (frames) *frames = (long)t->t->Mse().GetFrames();
+  TRY_END
+}
+int tnet_rbm_trainer_report(TnetRbmTrainer* t, char* buf, int cap) {
+  TRY_BEGIN std::string s = t->t->Mse().Report();
+  if (cap > 0) {
+    std::strncpy(buf, s.c_str(), (size_t)cap - 1);
+    buf[cap - 1] = 0;
+  }
+  TRY_END
+}
+long tnet_rbm_trainer_prefill(TnetRbmTrainer* t, const float* feats, int rows, int cols, int ld) {
+  try {
+    return (long)t->t->Prefill(feats, (size_t)rows, (size_t)cols, (size_t)ld);
+  } catch (std::exception& e) {
+    g_last_error = e.what();
+    return -1;
+  }
+}
+int tnet_rbm_trainer_replay(TnetRbmTrainer* t, long n) {
+  TRY_BEGIN t->t->Replay(n);
   TRY_END
 }
 

@@ -1,6 +1,8 @@
 // cunetwork.cpp -- see cunetwork.h.
 #include "cunetwork.h"
 
+#include "curbm.h"
+
 #include <algorithm>
 #include <cctype>
 #include <fstream>
@@ -153,6 +155,7 @@ CuComponent* CuNetwork::ComponentFactory(std::istream& rIn) {
   if (tag == "<biasedlinearity>") pRet = new CuBiasedLinearity(nInputs, nOutputs, pPred);
   else if (tag == "<sigmoid>") pRet = new CuSigmoid(nInputs, nOutputs, pPred);
   else if (tag == "<softmax>") pRet = new CuSoftmax(nInputs, nOutputs, pPred);
+  else if (tag == "<rbm>") pRet = new CuRbm(nInputs, nOutputs, pPred);
   else Error(std::string("Unknown Component tag:") + tag);
   pRet->ReadFromStream(rIn);
   return pRet;

@@ -70,6 +70,12 @@ void CuMeanSquareError::Evaluate(const CuMatrix<BaseFloat>& out, const CuMatrix<
   mFrames += out.Rows();
 }
 
+void CuMeanSquareError::EvaluateStats(const CuMatrix<BaseFloat>& out, const CuMatrix<BaseFloat>& des) {
+  if (out.Rows() != des.Rows() || out.Cols() != des.Cols()) Error("CuMeanSquareError: non-matching dims");
+  TNET_SAFE_CALL(tnet_mse(out.pCUData(), out.Dim(), des.pCUData(), (int)des.Stride(), nullptr, 0, mDevStats, S));
+  mFrames += out.Rows();
+}
+
 std::string CuMeanSquareError::Report() {
   Sync();
   std::ostringstream ss;

@@ -55,6 +55,8 @@ class CuMeanSquareError : public CuObjectiveFunction {
   const char* GetTypeLabel() override { return "<mean_square_error>"; }
   void Evaluate(const CuMatrix<BaseFloat>& rNetOutput, const CuMatrix<BaseFloat>& rDesired,
                 CuMatrix<BaseFloat>& rNetError) override;
+  /// statistics only (the error matrix is not needed, e.g. the RBM reconstruction error)
+  void EvaluateStats(const CuMatrix<BaseFloat>& rNetOutput, const CuMatrix<BaseFloat>& rDesired);
   std::string Report() override;
 };
 

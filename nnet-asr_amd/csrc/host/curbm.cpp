@@ -1,0 +1,280 @@
+// curbm.cpp -- see curbm.h.
+#include "curbm.h"
+
+#include <sys/time.h>
+
+#include <algorithm>
+#include <cstring>
+
+namespace TNet {
+
+#define S ((void*)CuDevice::Instantiate().Stream())
+
+// ============================================================================== CuRbm
+void CuRbm::PropagateFnc(const CuMatrix<BaseFloat>& X, CuMatrix<BaseFloat>& Y) {
+  CuProfileScope p("CuRbm::Propagate");
+  // Y = hb + X W ; sigmoid for Bernoulli hidden units (cuRbm.cc:15-23)
+  TNET_SAFE_CALL(tnet_affine_fwd(X.pCUData(), X.Dim(), mLinearity.pCUData(), mLinearity.Dim(), mBias.pCUData(),
+                                 Y.pCUData(), Y.Dim(), mHidType == BERNOULLI ? 1 : 0, S));
+}
+
+void CuRbm::BackpropagateFnc(const CuMatrix<BaseFloat>& X, CuMatrix<BaseFloat>& Y) {
+  CuProfileScope p("CuRbm::Backpropagate");
+  // buf = X .* y(1-y) (Bernoulli) or X ; Y = buf W^T (cuRbm.cc:27-38)
+  const CuMatrix<BaseFloat>* e = &X;
+  if (mHidType == BERNOULLI) {
+    mBackpropErrBuf.Init(X.Rows(), X.Cols());
+    CuMath<BaseFloat>::DiffSigmoid(mBackpropErrBuf, X, GetOutput());
+    e = &mBackpropErrBuf;
+  }
+  TNET_SAFE_CALL(tnet_affine_bwd(e->pCUData(), e->Dim(), mLinearity.pCUData(), mLinearity.Dim(), nullptr, 0,
+                                 Y.pCUData(), Y.Dim(), 0, S));
+}
+
+void CuRbm::Update() {
+  // cuRbm.cc:42-97 ("new implementation"): the CuBiasedLinearity update with the hidden bias,
+  // on the error through the hidden nonlinearity (recomputed because of the backprop stopper)
+  const CuMatrix<BaseFloat>& E = GetErrorInput();
+  if (mHidType == BERNOULLI) {
+    mBackpropErrBuf.Init(E.Rows(), E.Cols());
+    CuMath<BaseFloat>::DiffSigmoid(mBackpropErrBuf, E, GetOutput());
+    UpdateFrom(GetInput(), mBackpropErrBuf);
+  } else {
+    UpdateFrom(GetInput(), E);
+  }
+}
+
+void CuRbm::Propagate(const CuMatrix<BaseFloat>& visProbs, CuMatrix<BaseFloat>& hidProbs) {
+  if (visProbs.Cols() != GetNInputs()) {
+    std::ostringstream os;
+    os << " Nonmatching input dim, needs:" << GetNInputs() << " got:" << visProbs.Cols() << "\n";
+    Error(os.str());
+  }
+  hidProbs.Init(visProbs.Rows(), GetNOutputs());
+  PropagateFnc(visProbs, hidProbs);
+}
+
+void CuRbm::Reconstruct(const CuMatrix<BaseFloat>& hidState, CuMatrix<BaseFloat>& visProbs) {
+  CuProfileScope p("CuRbm::Reconstruct");
+  // vis = vb + h W^T ; sigmoid for Bernoulli visible units (cuRbm.cc:117-128)
+  visProbs.Init(hidState.Rows(), GetNInputs());
+  TNET_SAFE_CALL(tnet_affine_fwd_t(hidState.pCUData(), hidState.Dim(), mLinearity.pCUData(), mLinearity.Dim(),
+                                   mVisBias.pCUData(), visProbs.pCUData(), visProbs.Dim(),
+                                   mVisType == BERNOULLI ? 1 : 0, S));
+}
+
+void CuRbm::RbmUpdate(const CuMatrix<BaseFloat>& pos_vis, const CuMatrix<BaseFloat>& pos_hid,
+                      const CuMatrix<BaseFloat>& neg_vis, const CuMatrix<BaseFloat>& neg_hid) {
+  CuProfileScope p("CuRbm::RbmUpdate");
+  // Generic (unstacked) form of cuRbm.cc:133-174, same operation order as the reference:
+  //   corr = -lr/N neg_v^T neg_h + mmt corr ; corr += lr/N pos_v^T pos_h ; corr += -lr wc W ;
+  //   W += corr ; biases likewise.  CuRbmTrainer uses the stacked one-GEMM form instead.
+  if (!(pos_vis.Rows() == pos_hid.Rows() && pos_vis.Rows() == neg_vis.Rows() && pos_vis.Rows() == neg_hid.Rows() &&
+        pos_vis.Cols() == neg_vis.Cols() && pos_hid.Cols() == neg_hid.Cols() && pos_vis.Cols() == GetNInputs() &&
+        pos_hid.Cols() == GetNOutputs()))
+    Error("CuRbm::RbmUpdate: non-matching dimensions");
+  const BaseFloat N = (BaseFloat)pos_vis.Rows();
+  const BaseFloat lr = mLearningRate;
+  mLinearityCorrection.Gemm('T', 'N', -lr / N, neg_vis, neg_hid, mMomentum);
+  mLinearityCorrection.Gemm('T', 'N', +lr / N, pos_vis, pos_hid, 1.0f);
+  mLinearityCorrection.AddScaled(-lr * mWeightcost, mLinearity, 1.0f);
+  mLinearity.AddScaled(1.0f, mLinearityCorrection, 1.0f);
+  mVisBiasCorrection.AddColSum(-lr / N, neg_vis, mMomentum);
+  mVisBiasCorrection.AddColSum(+lr / N, pos_vis, 1.0f);
+  mVisBias.AddScaled(1.0f, mVisBiasCorrection, 1.0f);
+  mBiasCorrection.AddColSum(-lr / N, neg_hid, mMomentum);
+  mBiasCorrection.AddColSum(+lr / N, pos_hid, 1.0f);
+  mBias.AddScaled(1.0f, mBiasCorrection, 1.0f);
+}
+
+void CuRbm::ReadFromStream(std::istream& rIn) {
+  // "bern|gauss bern|gauss" then W^T [n_hid x n_vis], visible bias, hidden bias (cuRbm.cc:179-213)
+  std::string str;
+  rIn >> std::ws >> str;
+  if (str == "bern") mVisType = BERNOULLI;
+  else if (str == "gauss") mVisType = GAUSSIAN;
+  else Error(std::string("Invalid unit type: ") + str);
+  rIn >> std::ws >> str;
+  if (str == "bern") mHidType = BERNOULLI;
+  else if (str == "gauss") mHidType = GAUSSIAN;
+  else Error(std::string("Invalid unit type: ") + str);
+  BfMatrix transpose;
+  ReadMatrixFast(rIn, transpose);
+  if (transpose.Rows() != GetNOutputs() || transpose.Cols() != GetNInputs())
+    Error("Wrong dimensionalities of the <rbm> matrix in network file");
+  mLinearity.CopyFrom(BfMatrix(transpose, TRANS));
+  BfVector bias;
+  ReadVectorFast(rIn, bias);
+  if (bias.Dim() != GetNInputs()) Error("Wrong dimensionality of the <rbm> visible bias");
+  mVisBias.CopyFrom(bias);
+  ReadVectorFast(rIn, bias);
+  if (bias.Dim() != GetNOutputs()) Error("Wrong dimensionality of the <rbm> hidden bias");
+  mBias.CopyFrom(bias);
+}
+
+void CuRbm::WriteToStream(std::ostream& rOut) {
+  rOut << (mVisType == BERNOULLI ? " bern " : " gauss ");
+  rOut << (mHidType == BERNOULLI ? " bern\n" : " gauss\n");
+  BfMatrix tmp;
+  mLinearity.CopyTo(tmp);
+  rOut << BfMatrix(tmp, TRANS);
+  BfVector vec;
+  mVisBias.CopyTo(vec);
+  rOut << vec << std::endl;
+  mBias.CopyTo(vec);
+  rOut << vec << std::endl;
+}
+
+// ============================================================================== CuRand
+void CuRand::SeedGpu(size_t rows, size_t cols, Rng48& rng) {
+  std::vector<unsigned> host(rows * cols);
+  for (int k = 0; k < 4; k++) {
+    for (size_t i = 0; i < rows * cols; i++) {
+      unsigned v = 0;
+      while (v <= 128) v = (unsigned)rng.Lrand48();  // curand.tcc:39-41
+      host[i] = v;
+    }
+    z[k].Init(rows, cols);
+    z[k].CopyFromHost(host.data(), rows, cols, cols);
+  }
+}
+
+void CuRand::Check(const CuMatrix<BaseFloat>& m) const {
+  if (m.Rows() != z[0].Rows() || m.Cols() != z[0].Cols() || m.Stride() != z[0].Stride())
+    Error("CuRand: Non matching dims!!");
+}
+
+void CuRand::Rand(CuMatrix<BaseFloat>& tgt) {
+  tgt.Init(z[0].Rows(), z[0].Cols());
+  Check(tgt);
+  TNET_SAFE_CALL(tnetF_rand(tgt.pCUData(), tgt.Dim(), z[0].pCUData(), z[1].pCUData(), z[2].pCUData(),
+                            z[3].pCUData(), S));
+}
+
+void CuRand::GaussRand(CuMatrix<BaseFloat>& tgt) {
+  tgt.Init(z[0].Rows(), z[0].Cols());
+  Check(tgt);
+  TNET_SAFE_CALL(tnetF_gauss_rand(tgt.pCUData(), tgt.Dim(), z[0].pCUData(), z[1].pCUData(), z[2].pCUData(),
+                                  z[3].pCUData(), S));
+}
+
+void CuRand::BinarizeProbs(const CuMatrix<BaseFloat>& probs, CuMatrix<BaseFloat>& states) {
+  Check(probs);
+  states.Init(z[0].Rows(), z[0].Cols());
+  TNET_SAFE_CALL(tnet_rand_binarize(states.pCUData(), (int)states.Stride(), probs.pCUData(), probs.Dim(),
+                                    z[0].pCUData(), z[1].pCUData(), z[2].pCUData(), z[3].pCUData(), S));
+}
+
+void CuRand::AddGaussNoise(CuMatrix<BaseFloat>& tgt, BaseFloat gscale) {
+  Check(tgt);
+  TNET_SAFE_CALL(tnet_add_gauss_noise(tgt.pCUData(), tgt.Dim(), gscale, z[0].pCUData(), z[1].pCUData(),
+                                      z[2].pCUData(), z[3].pCUData(), S));
+}
+
+// ======================================================================= CuRbmTrainer
+CuRbmTrainer::CuRbmTrainer(CuRbm* rbm, const RbmTrainerOptions& opt) : mRbm(rbm), mOpt(opt) {
+  if (mOpt.bunchsize == 0) Error("CuRbmTrainer: bunchsize must be > 0");
+  mOpt.cachesize = (mOpt.cachesize / mOpt.bunchsize) * mOpt.bunchsize;
+  if (mOpt.cachesize == 0) Error("CuRbmTrainer: cachesize smaller than bunchsize");
+  long seed = mOpt.seed;
+  if (seed == 0) {
+    struct timeval tv;
+    gettimeofday(&tv, 0);
+    seed = (int)(tv.tv_sec) + (int)tv.tv_usec;
+  }
+  // TRbmCu.cc:260-264: srand48(seed); CuRand(bunch, n_hid) draws its seeds first, the cache
+  // shuffles continue on the same stream
+  mRng.Seed(seed);
+  const size_t B = mOpt.bunchsize, V = mRbm->GetNInputs(), H = mRbm->GetNOutputs();
+  mRand.SeedGpu(B, H, mRng);
+  mCache.Init(mOpt.cachesize, B);
+  mCache.SetRng(&mRng);
+  mCache.Trace(mOpt.trace);
+  mV.Init(2 * B, V);
+  mH.Init(2 * B, H);
+  mStates.Init(B, H);
+  CuMatrix<BaseFloat>::MakeView(mPosVis, mV.pCUData(), B, V, mV.Stride());
+  CuMatrix<BaseFloat>::MakeView(mNegVis, mV.pCURowData(B), B, V, mV.Stride());
+  CuMatrix<BaseFloat>::MakeView(mPosHid, mH.pCUData(), B, H, mH.Stride());
+  CuMatrix<BaseFloat>::MakeView(mNegHid, mH.pCURowData(B), B, H, mH.Stride());
+}
+
+void CuRbmTrainer::Step() {
+  const size_t B = mOpt.bunchsize;
+  CuRbm& rbm = *mRbm;
+  const bool hid_bern = rbm.HidType() == CuRbm::BERNOULLI;
+  // positive phase: pos_vis (gathered from the shuffled cache), pos_hid = p(h | v)
+  mCache.GetBunchLabels(mPosVis, mDummyLabels);
+  TNET_SAFE_CALL(tnet_affine_fwd(mPosVis.pCUData(), mPosVis.Dim(), rbm.VisHid().pCUData(), rbm.VisHid().Dim(),
+                                 rbm.HidBias().pCUData(), mPosHid.pCUData(), mPosHid.Dim(), hid_bern ? 1 : 0, S));
+  // sample the hidden layer (TRbmCu.cc:336-341)
+  if (hid_bern) {
+    mRand.BinarizeProbs(mPosHid, mStates);
+  } else {
+    mStates.CopyFrom(mPosHid);
+    mRand.AddGaussNoise(mStates);
+  }
+  // reconstruction, then the negative phase stored negated in rows B..2B-1 of mH
+  TNET_SAFE_CALL(tnet_affine_fwd_t(mStates.pCUData(), mStates.Dim(), rbm.VisHid().pCUData(), rbm.VisHid().Dim(),
+                                   rbm.VisBias().pCUData(), mNegVis.pCUData(), mNegVis.Dim(),
+                                   rbm.VisType() == CuRbm::BERNOULLI ? 1 : 0, S));
+  TNET_SAFE_CALL(tnet_affine_fwd(mNegVis.pCUData(), mNegVis.Dim(), rbm.VisHid().pCUData(), rbm.VisHid().Dim(),
+                                 rbm.HidBias().pCUData(), mNegHid.pCUData(), mNegHid.Dim(), hid_bern ? 3 : 2, S));
+  // CD-1 update (cuRbm.cc:133-174): one GEMM over the stacked statistics + two signed colsums
+  const float lr = rbm.LearnRate(), scale = lr / (float)B;
+  TNET_SAFE_CALL(tnet_rbm_update(mV.pCUData(), mV.Dim(), mH.pCUData(), mH.Dim(), rbm.VisHid().pCUData(),
+                                 rbm.VisHid().Dim(), rbm.VisHidCorrection().pCUData(),
+                                 (int)rbm.VisHidCorrection().Stride(), scale, rbm.Momentum(), -lr * rbm.Weightcost(),
+                                 S));
+  void* ws = CuDevice::Instantiate().Workspace(
+      (size_t)std::max(tnet_col_sum_workspace(mV.Dim()), tnet_col_sum_workspace(mH.Dim())));
+  TNET_SAFE_CALL(tnet_rbm_bias_update(mV.pCUData(), mV.Dim(), (int)B, rbm.VisBias().pCUData(),
+                                      rbm.VisBiasCorrection().pCUData(), scale, rbm.Momentum(), ws, S));
+  TNET_SAFE_CALL(tnet_rbm_bias_update(mH.pCUData(), mH.Dim(), (int)(2 * B), rbm.HidBias().pCUData(),
+                                      rbm.HidBiasCorrection().pCUData(), scale, rbm.Momentum(), ws, S));
+  // reconstruction error (mse.Evaluate(neg_vis, pos_vis), TRbmCu.cc:350)
+  mMse.EvaluateStats(mNegVis, mPosVis);
+  if (mOpt.trace & 2) std::cout << "." << std::flush;
+  mSteps++;
+}
+
+void CuRbmTrainer::DrainCache() {
+  if (mOpt.randomize) mCache.Randomize();
+  while (!mCache.Empty()) Step();
+  mTrainedSinceFill = true;
+}
+
+void CuRbmTrainer::AddUtterance(const float* feats, size_t rows, size_t cols, size_t ld) {
+  if (cols != mRbm->GetNInputs()) Error("CuRbmTrainer::AddUtterance: feature dim != RBM visible dim");
+  if (rows == 0) return;
+  if (mZeroLabels.size() < rows) mZeroLabels.assign(rows, 0);  // "fake the labels" (TRbmCu.cc:311)
+  mCache.AddDataHost(feats, rows, cols, ld, mZeroLabels.data());
+  mTrainedSinceFill = false;
+  if (mCache.Full()) DrainCache();
+}
+
+void CuRbmTrainer::Finish() {
+  if (!mTrainedSinceFill && mCache.IntakePos() > 0) DrainCache();
+}
+
+size_t CuRbmTrainer::Prefill(const float* feats, size_t rows, size_t cols, size_t ld) {
+  if (mCache.Full()) return 0;
+  const size_t space = mOpt.cachesize - mCache.IntakePos();
+  const size_t take = rows < space ? rows : space;
+  if (mZeroLabels.size() < take) mZeroLabels.assign(take, 0);
+  mCache.AddDataHost(feats, take, cols, ld, mZeroLabels.data());
+  if (mCache.Full() && mOpt.randomize) mCache.Randomize();
+  return take;
+}
+
+void CuRbmTrainer::Replay(long n) {
+  for (long i = 0; i < n; i++) {
+    if (mCache.Empty()) {
+      mCache.Rewind();
+      if (mOpt.randomize) mCache.Randomize();
+    }
+    Step();
+  }
+}
+
+}  // namespace TNet

@@ -15,6 +15,9 @@ class Rng48 {
  public:
   explicit Rng48(long seed = 0) { Seed(seed); }
   void Seed(long seed) { mX = ((((uint64_t)(uint32_t)seed) << 16) | 0x330Eu) & kMask; }
+  /// raw 48-bit state (tests / checkpointing)
+  uint64_t State() const { return mX; }
+  void SetState(uint64_t x) { mX = x & kMask; }
   long Lrand48() {
     mX = (0x5DEECE66Dull * mX + 0xBull) & kMask;
     return (long)(mX >> 17);

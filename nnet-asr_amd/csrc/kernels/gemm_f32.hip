@@ -30,7 +30,11 @@
 
 namespace tnetk {
 
-enum { EPI_STORE = 0, EPI_BIAS = 1, EPI_BIAS_SIG = 2, EPI_DSIG = 3, EPI_SGD = 4 };
+// EPI_BIAS_NSIG / EPI_BIAS_NEG store the negated activation (the RBM negative phase enters the
+// stacked statistics with a minus sign); EPI_RBM is the CD-1 weight update of CuRbm::RbmUpdate
+// (cuRbm.cc:133-174): c = mmt*corr + scale*acc + l2*W ; corr = c ; W += c
+enum { EPI_STORE = 0, EPI_BIAS = 1, EPI_BIAS_SIG = 2, EPI_DSIG = 3, EPI_SGD = 4, EPI_BIAS_NSIG = 5,
+       EPI_BIAS_NEG = 6, EPI_RBM = 7 };
 
 struct GemmP {
   int M, N, K;
@@ -59,7 +63,7 @@ __device__ __forceinline__ void epilogue(const GemmP& p, f32x16 (&acc)[TM][TN], 
       const int col = bn + wn0 + b * 32 + li;
       if (col >= N) continue;
       float bias_v = 0.f;
-      if (EPI == EPI_BIAS || EPI == EPI_BIAS_SIG) bias_v = p.bias[col];
+      if (EPI == EPI_BIAS || EPI == EPI_BIAS_SIG || EPI == EPI_BIAS_NSIG || EPI == EPI_BIAS_NEG) bias_v = p.bias[col];
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int row = bm + wm0 + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
@@ -72,9 +76,19 @@ __device__ __forceinline__ void epilogue(const GemmP& p, f32x16 (&acc)[TM][TN], 
           *cp = v + bias_v;
         } else if (EPI == EPI_BIAS_SIG) {
           *cp = sigmoidf_ref(v + bias_v);
+        } else if (EPI == EPI_BIAS_NSIG) {
+          *cp = -sigmoidf_ref(v + bias_v);
+        } else if (EPI == EPI_BIAS_NEG) {
+          *cp = -(v + bias_v);
         } else if (EPI == EPI_DSIG) {
           const float y = p.aux[(long)row * p.ldaux + col];
           *cp = y * (1.f - y) * v;
+        } else if (EPI == EPI_RBM) {
+          float* qp = p.corr + (long)row * p.ldcorr + col;
+          const float w = *cp;
+          const float c = p.mmt * *qp + p.scale * v + p.l2 * w;
+          *qp = c;
+          *cp = w + c;
         } else {  // EPI_SGD
           float c = v;
           if (p.corr) {
@@ -379,9 +393,19 @@ __device__ __forceinline__ void epi_elem(const GemmP& p, int row, int col, float
     *cp = v + p.bias[col];
   } else if (EPI == EPI_BIAS_SIG) {
     *cp = sigmoidf_ref(v + p.bias[col]);
+  } else if (EPI == EPI_BIAS_NSIG) {
+    *cp = -sigmoidf_ref(v + p.bias[col]);
+  } else if (EPI == EPI_BIAS_NEG) {
+    *cp = -(v + p.bias[col]);
   } else if (EPI == EPI_DSIG) {
     const float y = p.aux[(long)row * p.ldaux + col];
     *cp = y * (1.f - y) * v;
+  } else if (EPI == EPI_RBM) {
+    float* qp = p.corr + (long)row * p.ldcorr + col;
+    const float w = *cp;
+    const float c = p.mmt * *qp + p.scale * v + p.l2 * w;
+    *qp = c;
+    *cp = w + c;
   } else {  // EPI_SGD
     float c = v;
     if (p.corr) {
@@ -406,10 +430,24 @@ __device__ __forceinline__ void epi_vec4(const GemmP& p, int row, int col, f32x4
     } else {
       *cp = p.alpha * v + p.beta * *cp;
     }
-  } else if (EPI == EPI_BIAS || EPI == EPI_BIAS_SIG) {
+  } else if (EPI == EPI_BIAS || EPI == EPI_BIAS_SIG || EPI == EPI_BIAS_NSIG || EPI == EPI_BIAS_NEG) {
     f32x4 o;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) o[e] = EPI == EPI_BIAS ? v[e] + p.bias[col + e] : sigmoidf_ref(v[e] + p.bias[col + e]);
+    for (int e = 0; e < 4; ++e) {
+      const float a = v[e] + p.bias[col + e];
+      o[e] = EPI == EPI_BIAS ? a : EPI == EPI_BIAS_SIG ? sigmoidf_ref(a) : EPI == EPI_BIAS_NSIG ? -sigmoidf_ref(a) : -a;
+    }
+    *cp = o;
+  } else if (EPI == EPI_RBM) {
+    f32x4* qp = reinterpret_cast<f32x4*>(p.corr + (long)row * p.ldcorr + col);
+    const f32x4 w = *cp, q = *qp;
+    f32x4 c, o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      c[e] = p.mmt * q[e] + p.scale * v[e] + p.l2 * w[e];
+      o[e] = w[e] + c[e];
+    }
+    *qp = c;
     *cp = o;
   } else if (EPI == EPI_DSIG) {
     const f32x4 y = *reinterpret_cast<const f32x4*>(p.aux + (long)row * p.ldaux + col);
@@ -809,15 +847,50 @@ extern "C" int tnet_sgemm(char transa, char transb, int m, int n, int k, float a
 
 extern "C" int tnet_affine_fwd(const float* X, TnetMatrixDim dX, const float* W, TnetMatrixDim dW, const float* b,
                                float* Y, TnetMatrixDim dY, int act, void* stream) {
-  if (dX.cols != dW.rows || dY.rows != dX.rows || dY.cols != dW.cols || !b) return TNET_ERR_ARG;
+  if (dX.cols != dW.rows || dY.rows != dX.rows || dY.cols != dW.cols || !b || act < 0 || act > 3) return TNET_ERR_ARG;
   GemmP p{};
   p.M = dX.rows; p.N = dW.cols; p.K = dX.cols;
   p.A = X; p.lda = dX.stride; p.B = W; p.ldb = dW.stride; p.C = Y; p.ldc = dY.stride;
   p.bias = b;
   int st = check_common(p);
   if (st) return st;
-  if (act == 1) return launch_gemm<true, false, EPI_BIAS_SIG>(p, (hipStream_t)stream);
-  return launch_gemm<true, false, EPI_BIAS>(p, (hipStream_t)stream);
+  switch (act) {
+    case 1: return launch_gemm<true, false, EPI_BIAS_SIG>(p, (hipStream_t)stream);
+    case 2: return launch_gemm<true, false, EPI_BIAS_NEG>(p, (hipStream_t)stream);
+    case 3: return launch_gemm<true, false, EPI_BIAS_NSIG>(p, (hipStream_t)stream);
+    default: return launch_gemm<true, false, EPI_BIAS>(p, (hipStream_t)stream);
+  }
+}
+
+extern "C" int tnet_affine_fwd_t(const float* X, TnetMatrixDim dX, const float* W, TnetMatrixDim dW, const float* b,
+                                 float* Y, TnetMatrixDim dY, int act, void* stream) {
+  // Y[rows x n_in] = act(X[rows x n_out] W^T + b) with W stored [n_in x n_out] (CuRbm::Reconstruct)
+  if (dX.cols != dW.cols || dY.rows != dX.rows || dY.cols != dW.rows || !b || act < 0 || act > 1) return TNET_ERR_ARG;
+  GemmP p{};
+  p.M = dX.rows; p.N = dW.rows; p.K = dX.cols;
+  p.A = X; p.lda = dX.stride; p.B = W; p.ldb = dW.stride; p.C = Y; p.ldc = dY.stride;
+  p.bias = b;
+  int st = check_common(p);
+  if (st) return st;
+  if (act == 1) return launch_gemm<true, true, EPI_BIAS_SIG>(p, (hipStream_t)stream);
+  return launch_gemm<true, true, EPI_BIAS>(p, (hipStream_t)stream);
+}
+
+extern "C" int tnet_rbm_update(const float* V, TnetMatrixDim dV, const float* H, TnetMatrixDim dH, float* W,
+                               TnetMatrixDim dW, float* corrW, int strideCorr, float scale, float mmt, float l2,
+                               void* stream) {
+  // corr = mmt*corr + scale*(V^T H) + l2*W ; W += corr, with V / H the row-stacked positive and
+  // (sign-flipped) negative phase statistics
+  if (dV.rows != dH.rows || dW.rows != dV.cols || dW.cols != dH.cols || !corrW || (strideCorr & 3))
+    return TNET_ERR_ARG;
+  GemmP p{};
+  p.M = dV.cols; p.N = dH.cols; p.K = dV.rows;
+  p.A = V; p.lda = dV.stride; p.B = H; p.ldb = dH.stride; p.C = W; p.ldc = dW.stride;
+  p.corr = corrW; p.ldcorr = strideCorr;
+  p.scale = scale; p.mmt = mmt; p.l2 = l2;
+  int st = check_common(p);
+  if (st) return st;
+  return launch_gemm<false, false, EPI_RBM>(p, (hipStream_t)stream);
 }
 
 extern "C" int tnet_affine_bwd(const float* E, TnetMatrixDim dE, const float* W, TnetMatrixDim dW,

@@ -27,7 +27,7 @@ static int cs_slabs(int rows) {
 // r0+w, r0+w+4, ...; the 4 sub-group sums are added in order)
 template <bool V4>
 __global__ __launch_bounds__(256) void colsum_partial_kernel(const float* __restrict__ M, TnetMatrixDim d,
-                                                             float* __restrict__ partial, int slabs) {
+                                                             float* __restrict__ partial, int slabs, int neg_from) {
   constexpr int CW = V4 ? 4 : 1;                 // columns per lane
   __shared__ float red[CS_WAVES][CS_COLS * CW];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -41,12 +41,14 @@ __global__ __launch_bounds__(256) void colsum_partial_kernel(const float* __rest
   if (c0 < d.cols) {
 #pragma unroll 8
     for (int r = r0 + w; r < r1; r += CS_WAVES) {
+      // rows from neg_from on enter negated (RBM: positive minus negative phase statistics)
+      const float sg = r < neg_from ? 1.f : -1.f;
       if (V4) {
         const f32x4 v = *reinterpret_cast<const f32x4*>(M + (long)r * d.stride + c0);
 #pragma unroll
-        for (int k = 0; k < CW; ++k) acc[k] += v[k];
+        for (int k = 0; k < CW; ++k) acc[k] += sg * v[k];
       } else {
-        acc[0] += M[(long)r * d.stride + c0];
+        acc[0] += sg * M[(long)r * d.stride + c0];
       }
     }
   }
@@ -68,7 +70,7 @@ __global__ __launch_bounds__(256) void colsum_partial_kernel(const float* __rest
 }
 
 // mode 0: v = alpha*sum + beta*v ; mode 1: bias update (c = sum + mmt*corr; b += scale*c; corr=c)
-// mode 2: grad_out = sum
+// mode 2: grad_out = sum ; mode 3: RBM bias update (c = mmt*corr + scale*sum; corr = c; b += c)
 __global__ __launch_bounds__(64) void colsum_final_kernel(const float* __restrict__ partial, int slabs, int cols,
                                                            int mode, float alpha, float beta, float* __restrict__ v,
                                                            float* __restrict__ corr, float scale, float mmt) {
@@ -85,6 +87,10 @@ __global__ __launch_bounds__(64) void colsum_final_kernel(const float* __restric
         corr[c] = g;
       }
       v[c] = v[c] + scale * g;
+    } else if (mode == 3) {
+      const float g = mmt * corr[c] + scale * (float)s;
+      corr[c] = g;
+      v[c] = v[c] + g;
     } else {
       v[c] = (float)s;
     }
@@ -104,7 +110,7 @@ static float* get_ws(long bytes) {
 }
 
 static int colsum_run(const float* M, TnetMatrixDim d, void* workspace, hipStream_t st, int mode, float alpha,
-                      float beta, float* v, float* corr, float scale, float mmt) {
+                      float beta, float* v, float* corr, float scale, float mmt, int neg_from = 0x7fffffff) {
   if (d.rows < 0 || d.cols < 0 || d.stride < d.cols) return TNET_ERR_ARG;
   if (d.cols == 0) return TNET_OK;
   const int slabs = cs_slabs(d.rows);
@@ -113,9 +119,10 @@ static int colsum_run(const float* M, TnetMatrixDim d, void* workspace, hipStrea
   if (d.rows > 0) {
     const bool v4 = (d.cols & 3) == 0 && (d.stride & 3) == 0 && ((uintptr_t)M & 15) == 0;
     if (v4)
-      colsum_partial_kernel<true><<<dim3(cdiv(d.cols, CS_COLS * 4), slabs), 256, 0, st>>>(M, d, ws, slabs);
+      colsum_partial_kernel<true><<<dim3(cdiv(d.cols, CS_COLS * 4), slabs), 256, 0, st>>>(M, d, ws, slabs,
+                                                                                         neg_from);
     else
-      colsum_partial_kernel<false><<<dim3(cdiv(d.cols, CS_COLS), slabs), 256, 0, st>>>(M, d, ws, slabs);
+      colsum_partial_kernel<false><<<dim3(cdiv(d.cols, CS_COLS), slabs), 256, 0, st>>>(M, d, ws, slabs, neg_from);
     TNET_LAUNCH_CHECK();
   } else {
     if (hipMemsetAsync(ws, 0, (size_t)slabs * d.cols * 4, st) != hipSuccess) return TNET_ERR_RUNTIME;
@@ -329,6 +336,12 @@ extern "C" int tnet_bias_update(const float* E, TnetMatrixDim dE, float* b, floa
   if (mmt != 0.f && !corr_b && !grad_out) return TNET_ERR_ARG;
   if (grad_out) return colsum_run(E, dE, workspace, (hipStream_t)stream, 2, 1.f, 0.f, grad_out, nullptr, 0.f, 0.f);
   return colsum_run(E, dE, workspace, (hipStream_t)stream, 1, 1.f, 0.f, b, corr_b, scale, mmt);
+}
+
+extern "C" int tnet_rbm_bias_update(const float* M, TnetMatrixDim d, int neg_from, float* b, float* corr_b,
+                                    float scale, float mmt, void* workspace, void* stream) {
+  if (!b || !corr_b || neg_from < 0) return TNET_ERR_ARG;
+  return colsum_run(M, d, workspace, (hipStream_t)stream, 3, 1.f, 0.f, b, corr_b, scale, mmt, neg_from);
 }
 
 static bool v4ok(const void* p, int stride) { return ((uintptr_t)p & 15) == 0 && (stride & 3) == 0; }

@@ -15,7 +15,8 @@ import numpy as np
 from . import formats  # noqa: F401  (host formats; no device code)
 from ._lib import HOST_ALLREDUCE_FN, LIB_PATH, MatrixDim, TnetError, check, check_ptr, header_symbols, lib
 
-__all__ = ["DeviceArray", "Network", "Objective", "Trainer", "Comm", "TnetError", "synchronize", "pad_stride",
+__all__ = ["DeviceArray", "Network", "Objective", "Trainer", "RbmTrainer", "Comm", "TnetError", "synchronize",
+           "pad_stride",
            "device_count", "version", "LIB_PATH", "header_symbols", "formats"]
 
 
@@ -170,6 +171,34 @@ class Network:
         check(lib().tnet_net_train_bunch(self.h, obj.h, X.ptr, X.rows, X.stride, labels.ptr, int(train)),
               "train_bunch")
 
+    def rbm_params(self, i: int = 0):
+        """(W [n_vis x n_hid], vis_bias, hid_bias, (vis_type, hid_type)) of an <rbm> component."""
+        _, ni, no = self.components()[i]
+        W = np.empty((ni, no), np.float32)
+        vb = np.empty(ni, np.float32)
+        hb = np.empty(no, np.float32)
+        t = np.zeros(2, np.int32)
+        check(lib().tnet_net_rbm_get(self.h, i, W.ctypes.data, vb.ctypes.data, hb.ctypes.data, t.ctypes.data),
+              "rbm_get")
+        names = ("bern", "gauss")
+        return W, vb, hb, (names[t[0]], names[t[1]])
+
+    def set_rbm_params(self, i: int, W=None, vis_bias=None, hid_bias=None, types=None) -> None:
+        keep = []
+        args = []
+        for a in (W, vis_bias, hid_bias):
+            a = None if a is None else np.ascontiguousarray(a, np.float32)
+            keep.append(a)
+            args.append(None if a is None else a.ctypes.data)
+        vt, ht = (-1, -1) if types is None else tuple(0 if x == "bern" else 1 for x in types)
+        check(lib().tnet_net_rbm_set(self.h, i, args[0], args[1], args[2], vt, ht), "rbm_set")
+
+    def rbm_update(self, i: int, pos_vis: "DeviceArray", pos_hid: "DeviceArray", neg_vis: "DeviceArray",
+                   neg_hid: "DeviceArray") -> None:
+        """CuRbm::RbmUpdate (generic, unstacked form)."""
+        check(lib().tnet_net_rbm_update(self.h, i, pos_vis.ptr, pos_hid.ptr, neg_vis.ptr, neg_hid.ptr, pos_vis.rows,
+                                        pos_vis.stride, pos_hid.stride), "rbm_update")
+
     def set_comm(self, comm: Optional["Comm"]) -> None:
         """train_bunch all-reduces the weight gradients over `comm` (None: local update)."""
         self._comm = comm
@@ -278,6 +307,63 @@ class Trainer:
         try:
             if getattr(self, "h", None):
                 lib().tnet_trainer_free(self.h)
+                self.h = None
+        except Exception:
+            pass
+
+
+class RbmTrainer:
+    """The TRbmCu CD-1 loop (src/TRbmCu.cc:291-357) over a one-<rbm> network."""
+
+    def __init__(self, net: Network, bunchsize=256, cachesize=12800, seed=0, randomize=True, learn_rate=0.1,
+                 momentum=0.5, weightcost=0.0002):
+        self.net = net
+        self.h = check_ptr(lib().tnet_rbm_trainer_create(net.h, bunchsize, cachesize, seed, int(randomize),
+                                                         learn_rate, momentum, weightcost), "tnet_rbm_trainer_create")
+
+    def add_utterance(self, feats: np.ndarray) -> None:
+        feats = np.ascontiguousarray(feats, np.float32)
+        check(lib().tnet_rbm_trainer_add_utterance(self.h, feats.ctypes.data, feats.shape[0], feats.shape[1],
+                                                   feats.shape[1]), "rbm add_utterance")
+
+    def finish(self) -> None:
+        check(lib().tnet_rbm_trainer_finish(self.h), "rbm finish")
+
+    def train_corpus(self, feats: Sequence[np.ndarray]) -> None:
+        for x in feats:
+            self.add_utterance(x)
+        self.finish()
+
+    @property
+    def steps(self) -> int:
+        return lib().tnet_rbm_trainer_steps(self.h)
+
+    def stats(self):
+        """(sum of squared reconstruction errors, frames)"""
+        e = C.c_double()
+        n = C.c_long()
+        check(lib().tnet_rbm_trainer_stats(self.h, C.byref(e), C.byref(n)), "rbm stats")
+        return e.value, n.value
+
+    def report(self) -> str:
+        buf = C.create_string_buffer(512)
+        check(lib().tnet_rbm_trainer_report(self.h, buf, 512), "rbm report")
+        return buf.value.decode()
+
+    def prefill(self, feats: np.ndarray) -> int:
+        feats = np.ascontiguousarray(feats, np.float32)
+        n = lib().tnet_rbm_trainer_prefill(self.h, feats.ctypes.data, feats.shape[0], feats.shape[1], feats.shape[1])
+        if n < 0:
+            check(-1, "rbm prefill")
+        return n
+
+    def replay(self, n: int) -> None:
+        check(lib().tnet_rbm_trainer_replay(self.h, n), "rbm replay")
+
+    def __del__(self):
+        try:
+            if getattr(self, "h", None):
+                lib().tnet_rbm_trainer_free(self.h)
                 self.h = None
         except Exception:
             pass

@@ -125,6 +125,26 @@ _SIGS = {
     "tnet_comm_allreduce_host": (i32, [vp, dp, i32]),
     "tnet_comm_allreduce_device": (i32, [vp, vp, i64]),
     "tnet_comm_create_host": (vp, [i32, i32, vp, vp]),
+    "tnet_net_rbm_get": (i32, [vp, i32, vp, vp, vp, vp]),
+    "tnet_net_rbm_set": (i32, [vp, i32, vp, vp, vp, i32, i32]),
+    "tnet_net_rbm_update": (i32, [vp, i32, vp, vp, vp, vp, i32, i32, i32]),
+    "tnet_rbm_trainer_create": (vp, [vp, i32, i32, i64, i32, f32, f32, f32]),
+    "tnet_rbm_trainer_free": (i32, [vp]),
+    "tnet_rbm_trainer_add_utterance": (i32, [vp, vp, i32, i32, i32]),
+    "tnet_rbm_trainer_finish": (i32, [vp]),
+    "tnet_rbm_trainer_steps": (i64, [vp]),
+    "tnet_rbm_trainer_stats": (i32, [vp, dp, C.POINTER(i64)]),
+    "tnet_rbm_trainer_report": (i32, [vp, C.c_char_p, i32]),
+    "tnet_rbm_trainer_prefill": (i64, [vp, vp, i32, i32, i32]),
+    "tnet_rbm_trainer_replay": (i32, [vp, i64]),
+    "tnet_affine_fwd_t": (i32, [vp, MatrixDim, vp, MatrixDim, vp, vp, MatrixDim, i32, vp]),
+    "tnet_rbm_update": (i32, [vp, MatrixDim, vp, MatrixDim, vp, MatrixDim, vp, i32, f32, f32, f32, vp]),
+    "tnet_rbm_bias_update": (i32, [vp, MatrixDim, i32, vp, vp, f32, f32, vp, vp]),
+    "tnetF_rand": (i32, [vp, MatrixDim, vp, vp, vp, vp, vp]),
+    "tnetF_gauss_rand": (i32, [vp, MatrixDim, vp, vp, vp, vp, vp]),
+    "tnetF_binarize_probs": (i32, [vp, vp, vp, MatrixDim, vp]),
+    "tnet_rand_binarize": (i32, [vp, i32, vp, MatrixDim, vp, vp, vp, vp, vp]),
+    "tnet_add_gauss_noise": (i32, [vp, MatrixDim, f32, vp, vp, vp, vp, vp]),
     "tnet_dp_plan_round": (i32, [vp, i64, i32, C.POINTER(i64), C.POINTER(i32), i64, C.POINTER(i32)]),
     "tnet_net_set_comm": (i32, [vp, vp]),
     "tnet_comm_set_step_rows": (i32, [vp, i64]),

@@ -149,6 +149,28 @@ def gen_mlp_init(dims: Sequence[int], seed: int, gauss: bool = True, negbias: bo
     return layers
 
 
+def gen_rbm_init(n_vis: int, n_hid: int, seed: int, vis_type: str = "gauss", hid_type: str = "bern",
+                 gauss: bool = True, negbias: bool = True) -> List[Layer]:
+    """Seeded restatement of tools/init/gen_rbm_init.py (one <rbm> layer): W^T ~ 0.1 N(0,1)
+    (--gauss) or U[-0.1, 0.1]; a Gaussian unit layer gets zero biases, a Bernoulli one
+    U[-4.1, -3.9] with --negbias (else 0)."""
+    rng = np.random.default_rng(seed)
+    if gauss:
+        Wt = (0.1 * rng.standard_normal((n_hid, n_vis))).astype(np.float32)
+    else:
+        Wt = (rng.random((n_hid, n_vis)) / 5.0 - 0.1).astype(np.float32)
+
+    def bias(n, kind):
+        if kind == "gauss" or not negbias:
+            return np.zeros(n, np.float32)
+        return (rng.random(n) / 5.0 - 4.1).astype(np.float32)
+
+    vb = bias(n_vis, vis_type)
+    hb = bias(n_hid, hid_type)
+    return [Layer("<rbm>", n_hid, n_vis, np.ascontiguousarray(Wt.T), hb,
+                  {"vis_type": vis_type, "hid_type": hid_type, "vis_bias": vb})]
+
+
 def round_trip_text(layers: Sequence[Layer], precision: int = 6) -> List[Layer]:
     """Weights exactly as a reader sees them after a text write at ``precision`` digits."""
     buf = io.StringIO()

@@ -34,6 +34,18 @@ def lib():
                                     C.POINTER(C.c_long)]
         L.orc_epoch_schedule.argtypes = [i32p, C.c_int, C.c_int, C.c_int, C.c_long, C.c_int, i32p, C.c_long]
         L.orc_epoch_schedule.restype = C.c_long
+        u32p = np.ctypeslib.ndpointer(np.uint32, flags="C_CONTIGUOUS")
+        L.orc_epoch_schedule_x.argtypes = [i32p, C.c_int, C.c_int, C.c_int, C.c_uint64, C.c_int, i32p, C.c_long,
+                                           C.POINTER(C.c_uint64)]
+        L.orc_epoch_schedule_x.restype = C.c_long
+        L.orc_rand_seed.argtypes = [C.c_long, C.c_long, u32p, u32p, u32p, u32p]
+        L.orc_rand_seed.restype = C.c_uint64
+        L.orc_rand_uniform.argtypes = [f32p, C.c_long, u32p, u32p, u32p, u32p]
+        L.orc_gauss_rand.argtypes = [f32p, C.c_long, u32p, u32p, u32p, u32p]
+        L.orc_rbm_step.argtypes = [C.c_int, C.c_int, f32p, f32p, f32p, f32p, f32p, f32p, f32p, C.c_int, C.c_int,
+                                   C.c_int, C.c_float, C.c_float, C.c_float, u32p, u32p, u32p, u32p, C.c_void_p,
+                                   C.POINTER(C.c_double)]
+        L.orc_rbm_step.restype = C.c_int
         L.orc_mlp_step.argtypes = [C.c_int, i32p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, f32p, i32p,
                                    C.c_int, C.c_float, C.c_float, C.c_float, C.c_int, C.c_int, f32p, f32p,
                                    C.POINTER(C.c_double), C.POINTER(C.c_long)]
@@ -154,3 +166,73 @@ def write_random_nnet(path, dims, seed=2):
     d = np.ascontiguousarray(dims, np.int32)
     if lib().orc_write_random_nnet(path.encode(), d, len(d), seed) != 0:
         raise OSError(f"cannot write {path}")
+
+
+# ---------------------------------------------------------------------------------------------
+# CuRand / CuRbm restatement (curand.tcc, curandkernels.cu, cuRbm.cc, TRbmCu.cc)
+# ---------------------------------------------------------------------------------------------
+class RandState:
+    """HybridTaus state of a rows x cols target, seeded as CuRand::SeedGpu after srand48(seed)."""
+
+    def __init__(self, seed, rows, cols):
+        n = rows * cols
+        self.rows, self.cols = rows, cols
+        self.z = [np.zeros(n, np.uint32) for _ in range(4)]
+        self.x_after = int(lib().orc_rand_seed(seed, n, *self.z))
+
+    def uniform(self):
+        out = np.empty(self.rows * self.cols, np.float32)
+        lib().orc_rand_uniform(out, out.size, *self.z)
+        return out.reshape(self.rows, self.cols)
+
+    def gauss(self):
+        out = np.empty(self.rows * self.cols, np.float32)
+        lib().orc_gauss_rand(out, out.size, *self.z)
+        return out.reshape(self.rows, self.cols)
+
+
+def epoch_schedule_x(lens, cachesize, bunch, x0, randomize=True):
+    """Epoch bunch schedule with the lrand48 stream starting at raw state x0."""
+    lens = np.ascontiguousarray(lens, np.int32)
+    cap = int(lens.sum()) // bunch + 1
+    out = np.zeros(cap * bunch, np.int32)
+    xe = C.c_uint64()
+    nb = lib().orc_epoch_schedule_x(lens, len(lens), cachesize, bunch, x0, int(randomize), out, cap, C.byref(xe))
+    if nb < 0:
+        raise ValueError("utterance leftover fills the whole cache (the reference asserts cache_space > 0)")
+    return out[: nb * bunch].reshape(nb, bunch)
+
+
+class RBM:
+    """Oracle RBM state: W [V x H], visible / hidden biases and their momentum buffers."""
+
+    def __init__(self, W, vb, hb, vis_type="gauss", hid_type="bern"):
+        self.W = np.ascontiguousarray(W, np.float32).copy()
+        self.vb = np.ascontiguousarray(vb, np.float32).copy()
+        self.hb = np.ascontiguousarray(hb, np.float32).copy()
+        self.cW = np.zeros_like(self.W)
+        self.cvb = np.zeros_like(self.vb)
+        self.chb = np.zeros_like(self.hb)
+        self.vis_gauss = vis_type == "gauss"
+        self.hid_gauss = hid_type == "gauss"
+        self.mse = 0.0
+        self.frames = 0
+
+    @classmethod
+    def from_layer(cls, L):
+        return cls(L.W, L.extra["vis_bias"], L.b, L.extra["vis_type"], L.extra["hid_type"])
+
+    def step(self, pos_vis, rand: RandState, lr, mmt, wc):
+        pos_vis = np.ascontiguousarray(pos_vis, np.float32)
+        B, V = pos_vis.shape
+        H = self.W.shape[1]
+        neg = np.empty((B, V), np.float32)
+        e2 = C.c_double(0.0)
+        st = lib().orc_rbm_step(V, H, self.W, self.vb, self.hb, self.cW, self.cvb, self.chb, pos_vis, B,
+                                int(self.vis_gauss), int(self.hid_gauss), lr, mmt, wc, *rand.z,
+                                neg.ctypes.data, C.byref(e2))
+        if st != 0:
+            raise MemoryError("orc_rbm_step")
+        self.mse += e2.value
+        self.frames += B
+        return neg

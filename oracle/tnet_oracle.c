@@ -52,9 +52,20 @@ void orc_random_shuffle(orc_rng48* r, int* p, int n) {
  * CuCache::AddData/Randomize/GetBunch (cuCache.cc:41-200) + the TNetCu fill loop
  * (TNetCu.cc:376-441).  Emits, for every trained bunch, `bunch` global frame indices
  * (utterance frames concatenated in scp order).  Returns number of bunches written. */
+long orc_epoch_schedule_x(const int* lens, int nutt, int cachesize, int bunch, uint64_t x0, int randomize,
+                          int* out, long out_cap_bunches, uint64_t* x_end);
+
 long orc_epoch_schedule(const int* lens, int nutt, int cachesize, int bunch, long seed, int randomize,
                         int* out, long out_cap_bunches) {
   orc_rng48 r; orc_srand48(&r, seed);
+  return orc_epoch_schedule_x(lens, nutt, cachesize, bunch, r.x, randomize, out, out_cap_bunches, NULL);
+}
+
+/* Same schedule with the lrand48 stream starting at raw state x0 (TRbmCu draws the CuRand seeds
+ * from the stream before the first shuffle, TRbmCu.cc:260-264); x_end receives the final state. */
+long orc_epoch_schedule_x(const int* lens, int nutt, int cachesize, int bunch, uint64_t x0, int randomize,
+                          int* out, long out_cap_bunches, uint64_t* x_end) {
+  orc_rng48 r; r.x = x0;
   int* cache = (int*)malloc(sizeof(int) * (size_t)cachesize);
   int* perm = (int*)malloc(sizeof(int) * (size_t)cachesize);
   int* leftover = NULL; int nleft = 0;
@@ -92,6 +103,7 @@ long orc_epoch_schedule(const int* lens, int nutt, int cachesize, int bunch, lon
     }
   }
   free(leftover); free(cache); free(perm);
+  if (x_end) *x_end = r.x;
   return nb;
 }
 
@@ -315,4 +327,108 @@ int orc_write_random_nnet(const char* path, const int* dims, int n, unsigned lon
   }
 #undef ORC_U01
   return fclose(f) == 0 ? 0 : -1;
+}
+
+
+/* ---------------------------------------------------------------------------------------
+ * CuRand (src/CuBaseLib/curand.tcc:13-154, curandkernels.cu:14-107): per-element HybridTaus
+ * state z1..z4, seeded row by row from lrand48 (values > 128), z1 first.  Arrays here are dense
+ * [n] in element order.
+ * ------------------------------------------------------------------------------------- */
+static unsigned orc_taus(unsigned* z, int s1, int s2, int s3, unsigned m) {
+  unsigned b = ((*z << s1) ^ *z) >> s2;
+  return *z = ((*z & m) << s3) ^ b;
+}
+
+static float orc_hybrid_taus(unsigned* z1, unsigned* z2, unsigned* z3, unsigned* z4) {
+  float r;
+  do {
+    unsigned x = orc_taus(z1, 13, 19, 12, 4294967294u) ^ orc_taus(z2, 2, 25, 4, 4294967288u) ^
+                 orc_taus(z3, 3, 11, 17, 4294967280u) ^ (*z4 = 1664525u * *z4 + 1013904223u);
+    r = (float)(2.3283064365387e-10 * (double)x);
+  } while (!(r > 0.0f && r < 1.0f));
+  return r;
+}
+
+static float orc_box_muller(unsigned* z1, unsigned* z2, unsigned* z3, unsigned* z4) {
+  const float two_pi = 6.283185307179586476925286766558f;
+  float u0 = orc_hybrid_taus(z1, z2, z3, z4), u1 = orc_hybrid_taus(z1, z2, z3, z4);
+  float r = (float)sqrt(-2.0 * (double)logf(u0));
+  float th = two_pi * u1;
+  return r * sinf(th);
+}
+
+/* srand48(seed), then SeedGpu(rows, cols) draws; returns the lrand48 state afterwards */
+uint64_t orc_rand_seed(long seed, long n, unsigned* z1, unsigned* z2, unsigned* z3, unsigned* z4) {
+  orc_rng48 r; orc_srand48(&r, seed);
+  unsigned* zs[4] = {z1, z2, z3, z4};
+  for (int k = 0; k < 4; k++)
+    for (long i = 0; i < n; i++) {
+      unsigned v = 0;
+      while (v <= 128) v = (unsigned)orc_lrand48(&r);
+      zs[k][i] = v;
+    }
+  return r.x;
+}
+
+void orc_rand_uniform(float* out, long n, unsigned* z1, unsigned* z2, unsigned* z3, unsigned* z4) {
+  for (long i = 0; i < n; i++) out[i] = orc_hybrid_taus(z1 + i, z2 + i, z3 + i, z4 + i);
+}
+
+void orc_gauss_rand(float* out, long n, unsigned* z1, unsigned* z2, unsigned* z3, unsigned* z4) {
+  for (long i = 0; i < n; i++) out[i] = orc_box_muller(z1 + i, z2 + i, z3 + i, z4 + i);
+}
+
+/* One CD-1 step of the TRbmCu loop (TRbmCu.cc:329-350) with CuRbm's formulas and operation
+ * order (cuRbm.cc:15-23 Propagate, :117-128 Reconstruct, :133-174 RbmUpdate):
+ *   pos_hid = act(hb + pos_vis W)
+ *   states  = pos_hid > U (Bernoulli hidden) | pos_hid + N(0,1) (Gaussian hidden)
+ *   neg_vis = act(vb + states W^T) ; neg_hid = act(hb + neg_vis W)
+ *   cW = -lr/B neg_vis^T neg_hid + mmt cW ; cW += lr/B pos_vis^T pos_hid ; cW += -lr wc W ; W += cW
+ *   cvb, chb likewise from column sums ; vb += cvb ; hb += chb
+ *   mse += sum (neg_vis - pos_vis)^2
+ * W [V x H]; z arrays dense [B x H]; neg_vis_out [B x V] (may be NULL). */
+int orc_rbm_step(int V, int H, float* W, float* vb, float* hb, float* cW, float* cvb, float* chb,
+                 const float* pos_vis, int B, int vis_gauss, int hid_gauss, float lr, float mmt, float wc,
+                 unsigned* z1, unsigned* z2, unsigned* z3, unsigned* z4, float* neg_vis_out, double* mse) {
+  const long nh = (long)B * H, nv = (long)B * V;
+  float* pos_hid = (float*)malloc(sizeof(float) * nh);
+  float* states = (float*)malloc(sizeof(float) * nh);
+  float* neg_vis = (float*)malloc(sizeof(float) * nv);
+  float* neg_hid = (float*)malloc(sizeof(float) * nh);
+  if (!pos_hid || !states || !neg_vis || !neg_hid) return -1;
+  orc_affine(pos_vis, B, V, W, hb, H, pos_hid);
+  if (!hid_gauss) orc_sigmoid(pos_hid, pos_hid, nh);
+  if (!hid_gauss) {
+    for (long i = 0; i < nh; i++) states[i] = pos_hid[i] > orc_hybrid_taus(z1 + i, z2 + i, z3 + i, z4 + i) ? 1.0f : 0.0f;
+  } else {
+    for (long i = 0; i < nh; i++) states[i] = 1.0f * orc_box_muller(z1 + i, z2 + i, z3 + i, z4 + i) + 1.0f * pos_hid[i];
+  }
+  /* neg_vis = vb + states W^T */
+  for (int r = 0; r < B; r++)
+    for (int c = 0; c < V; c++) neg_vis[(size_t)r * V + c] = vb[c];
+  orc_sgemm('N', 'T', B, V, H, 1.0f, states, H, W, H, 1.0f, neg_vis, V);
+  if (!vis_gauss) orc_sigmoid(neg_vis, neg_vis, nv);
+  orc_affine(neg_vis, B, V, W, hb, H, neg_hid);
+  if (!hid_gauss) orc_sigmoid(neg_hid, neg_hid, nh);
+  const float N = (float)B;
+  orc_sgemm('T', 'N', V, H, B, -lr / N, neg_vis, V, neg_hid, H, mmt, cW, H);
+  orc_sgemm('T', 'N', V, H, B, +lr / N, pos_vis, V, pos_hid, H, 1.0f, cW, H);
+  for (long i = 0; i < (long)V * H; i++) cW[i] = (-lr * wc) * W[i] + 1.0f * cW[i];
+  for (long i = 0; i < (long)V * H; i++) W[i] = 1.0f * cW[i] + 1.0f * W[i];
+  orc_add_col_sum(-lr / N, neg_vis, B, V, mmt, cvb);
+  orc_add_col_sum(+lr / N, pos_vis, B, V, 1.0f, cvb);
+  for (int i = 0; i < V; i++) vb[i] = 1.0f * cvb[i] + 1.0f * vb[i];
+  orc_add_col_sum(-lr / N, neg_hid, B, H, mmt, chb);
+  orc_add_col_sum(+lr / N, pos_hid, B, H, 1.0f, chb);
+  for (int i = 0; i < H; i++) hb[i] = 1.0f * chb[i] + 1.0f * hb[i];
+  double e2 = 0.0;
+  for (long i = 0; i < nv; i++) {
+    float e = neg_vis[i] - pos_vis[i];
+    e2 += (double)(e * e);
+  }
+  if (mse) *mse += e2;
+  if (neg_vis_out) memcpy(neg_vis_out, neg_vis, sizeof(float) * nv);
+  free(pos_hid); free(states); free(neg_vis); free(neg_hid);
+  return 0;
 }

@@ -1,0 +1,196 @@
+"""RBM pre-training path (BASELINE config 4: Gauss-Bernoulli RBM, CD-1) on the GPU vs the oracle's
+restatement of CuRand / CuRbm / TRbmCu.
+
+The reference RBM code is CUDA-only (no CPU counterpart in TNetLib), so parity is against the
+restatement (oracle/tnet_oracle.c: orc_rand_*, orc_rbm_step) -- "parity restated", not
+reference-run.  Tolerances:
+  uniforms, binarised states, generator state: bit-exact (integer recurrences + one double->float
+  rounding, identical by construction);
+  Box-Muller normals: abs 2e-5 (logf/sinf ulp differences between libm and the device);
+  per-step / per-epoch parameters: rtol 2e-4, atol 2e-6 (fp32 GEMM order; the fused update sums
+  positive and negative statistics in one GEMM where the reference runs two);
+  reconstruction MSE over an epoch: rtol 1e-4.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+import oracle as orc  # noqa: E402
+from tnet_amd import DeviceArray, Network, RbmTrainer, formats  # noqa: E402
+from tnet_amd._lib import check, lib  # noqa: E402
+
+
+def S():
+    return lib().tnet_stream()
+
+
+def _state_dev(rs, rows, cols):
+    return [DeviceArray.from_numpy(z.reshape(rows, cols)) for z in rs.z]
+
+
+@pytest.mark.parametrize("rows,cols", [(1, 1), (3, 70), (64, 128), (17, 300)])
+def test_rand_uniform_bitexact(rows, cols):
+    rs = orc.RandState(1234, rows, cols)
+    z = _state_dev(rs, rows, cols)
+    out = DeviceArray(rows, cols)
+    for _ in range(3):
+        check(lib().tnetF_rand(out.ptr, out.dim, *[a.ptr for a in z], S()))
+        np.testing.assert_array_equal(out.numpy(), rs.uniform())
+    for a, b in zip(z, rs.z):
+        np.testing.assert_array_equal(a.numpy().reshape(-1), b)
+
+
+def test_gauss_rand_and_noise():
+    rows, cols = 32, 96
+    rs = orc.RandState(77, rows, cols)
+    z = _state_dev(rs, rows, cols)
+    out = DeviceArray(rows, cols)
+    check(lib().tnetF_gauss_rand(out.ptr, out.dim, *[a.ptr for a in z], S()))
+    np.testing.assert_allclose(out.numpy(), rs.gauss(), rtol=0, atol=2e-5)
+    base = np.random.default_rng(0).standard_normal((rows, cols)).astype(np.float32)
+    tgt = DeviceArray.from_numpy(base)
+    check(lib().tnet_add_gauss_noise(tgt.ptr, tgt.dim, 0.5, *[a.ptr for a in z], S()))
+    np.testing.assert_allclose(tgt.numpy(), base + 0.5 * rs.gauss(), rtol=0, atol=2e-5)
+    for a, b in zip(z, rs.z):
+        np.testing.assert_array_equal(a.numpy().reshape(-1), b)
+
+
+def test_rand_binarize_bitexact():
+    rows, cols = 48, 200
+    rs = orc.RandState(9, rows, cols)
+    z = _state_dev(rs, rows, cols)
+    P = np.random.default_rng(3).random((rows, cols)).astype(np.float32)
+    dP = DeviceArray.from_numpy(P)
+    st = DeviceArray(rows, cols)
+    check(lib().tnet_rand_binarize(st.ptr, st.stride, dP.ptr, dP.dim, *[a.ptr for a in z], S()))
+    np.testing.assert_array_equal(st.numpy(), (P > rs.uniform()).astype(np.float32))
+    # the unfused reference form: uniforms then _binarize_probs
+    U = DeviceArray(rows, cols)
+    check(lib().tnetF_rand(U.ptr, U.dim, *[a.ptr for a in z], S()))
+    st2 = DeviceArray(rows, cols)
+    check(lib().tnetF_binarize_probs(st2.ptr, dP.ptr, U.ptr, dP.dim, S()))
+    np.testing.assert_array_equal(st2.numpy(), (P > rs.uniform()).astype(np.float32))
+
+
+@pytest.mark.parametrize("act", [0, 1, 2, 3])
+def test_affine_fwd_negated_and_transposed(act):
+    rng = np.random.default_rng(act)
+    X = rng.standard_normal((70, 40)).astype(np.float32)
+    W = (0.1 * rng.standard_normal((40, 90))).astype(np.float32)
+    b = rng.standard_normal(90).astype(np.float32)
+    dX, dW, db = DeviceArray.from_numpy(X), DeviceArray.from_numpy(W), DeviceArray.vector(b)
+    Y = DeviceArray(70, 90)
+    check(lib().tnet_affine_fwd(dX.ptr, dX.dim, dW.ptr, dW.dim, db.ptr, Y.ptr, Y.dim, act, S()))
+    a = X.astype(np.float64) @ W + b
+    ref = {0: a, 1: 1 / (1 + np.exp(-a)), 2: -a, 3: -1 / (1 + np.exp(-a))}[act]
+    np.testing.assert_allclose(Y.numpy(), ref, rtol=1e-5, atol=1e-5)
+    if act < 2:  # reconstruction: X2 [70 x 90] W^T + vb
+        X2 = rng.standard_normal((70, 90)).astype(np.float32)
+        vb = rng.standard_normal(40).astype(np.float32)
+        dX2, dvb = DeviceArray.from_numpy(X2), DeviceArray.vector(vb)
+        Y2 = DeviceArray(70, 40)
+        check(lib().tnet_affine_fwd_t(dX2.ptr, dX2.dim, dW.ptr, dW.dim, dvb.ptr, Y2.ptr, Y2.dim, act, S()))
+        a2 = X2.astype(np.float64) @ W.T + vb
+        np.testing.assert_allclose(Y2.numpy(), a2 if act == 0 else 1 / (1 + np.exp(-a2)), rtol=1e-5, atol=1e-5)
+
+
+def _cd1_reference(W, vb, hb, cW, cvb, chb, pv, ph, nv, nh, lr, mmt, wc):
+    N = pv.shape[0]
+    cW = (-lr / N) * (nv.T.astype(np.float64) @ nh) + mmt * cW
+    cW = (lr / N) * (pv.T.astype(np.float64) @ ph) + cW
+    cW = (-lr * wc) * W + cW
+    W = W + cW
+    cvb = (-lr / N) * nv.sum(0, dtype=np.float64) + mmt * cvb + (lr / N) * pv.sum(0, dtype=np.float64)
+    chb = (-lr / N) * nh.sum(0, dtype=np.float64) + mmt * chb + (lr / N) * ph.sum(0, dtype=np.float64)
+    return W, vb + cvb, hb + chb, cW, cvb, chb
+
+
+@pytest.mark.parametrize("V,H,B", [(40, 64, 32), (440, 256, 64), (33, 70, 17)])
+def test_rbm_update_generic_and_stacked(V, H, B):
+    rng = np.random.default_rng(V + H)
+    L = formats.gen_rbm_init(V, H, seed=4)[0]
+    pv, nv = (rng.standard_normal((B, V)).astype(np.float32) for _ in range(2))
+    ph, nh = (rng.random((B, H)).astype(np.float32) for _ in range(2))
+    lr, mmt, wc = 0.1, 0.5, 0.0002
+    cW0 = (0.01 * rng.standard_normal((V, H))).astype(np.float32)
+    cvb0 = (0.01 * rng.standard_normal(V)).astype(np.float32)
+    chb0 = (0.01 * rng.standard_normal(H)).astype(np.float32)
+    ref = _cd1_reference(L.W, L.extra["vis_bias"], L.b, cW0, cvb0, chb0, pv, ph, nv, nh, lr, mmt, wc)
+    # generic CuRbm::RbmUpdate (two GEMMs + AddScaled, the reference's sequence), from zero momentum
+    net = Network.from_layers([L])
+    net.set_learn_rate(lr)
+    net.set_momentum(mmt)
+    net.set_weightcost(wc)
+    ref0 = _cd1_reference(L.W, L.extra["vis_bias"], L.b, 0 * cW0, 0 * cvb0, 0 * chb0, pv, ph, nv, nh, lr, mmt, wc)
+    net.rbm_update(0, *(DeviceArray.from_numpy(a) for a in (pv, ph, nv, nh)))
+    W, vb, hb, _ = net.rbm_params(0)
+    for got, want in zip((W, vb, hb), ref0[:3]):
+        np.testing.assert_allclose(got, want, rtol=2e-4, atol=2e-6)
+    # stacked one-GEMM form with momentum state
+    dV = DeviceArray.from_numpy(np.concatenate([pv, nv]))
+    dH = DeviceArray.from_numpy(np.concatenate([ph, -nh]))
+    dW = DeviceArray.from_numpy(L.W)
+    dc = DeviceArray.from_numpy(cW0)
+    dvb, dhb = DeviceArray.vector(L.extra["vis_bias"]), DeviceArray.vector(L.b)
+    dcvb, dchb = DeviceArray.vector(cvb0), DeviceArray.vector(chb0)
+    check(lib().tnet_rbm_update(dV.ptr, dV.dim, dH.ptr, dH.dim, dW.ptr, dW.dim, dc.ptr, dc.stride, lr / B, mmt,
+                                -lr * wc, S()))
+    check(lib().tnet_rbm_bias_update(dV.ptr, dV.dim, B, dvb.ptr, dcvb.ptr, lr / B, mmt, None, S()))
+    check(lib().tnet_rbm_bias_update(dH.ptr, dH.dim, 2 * B, dhb.ptr, dchb.ptr, lr / B, mmt, None, S()))
+    for got, want in zip((dW.numpy(), dvb.numpy().reshape(-1), dhb.numpy().reshape(-1), dc.numpy()),
+                         (ref[0], ref[1], ref[2], ref[3])):
+        np.testing.assert_allclose(got, want, rtol=2e-4, atol=2e-6)
+
+
+def test_rbm_text_round_trip(tmp_path):
+    layers = formats.gen_rbm_init(24, 40, seed=2, vis_type="gauss", hid_type="bern")
+    net = Network.from_layers(layers)
+    assert net.components() == [("<rbm>", 24, 40)]
+    W, vb, hb, types = net.rbm_params(0)
+    assert types == ("gauss", "bern")
+    np.testing.assert_array_equal(W, layers[0].W)
+    np.testing.assert_array_equal(vb, layers[0].extra["vis_bias"])
+    np.testing.assert_array_equal(hb, layers[0].b)
+    p = str(tmp_path / "rbm.nnet")
+    net.write(p)
+    back = formats.read_nnet(p)
+    assert back[0].tag == "<rbm>" and back[0].extra["vis_type"] == "gauss" and back[0].extra["hid_type"] == "bern"
+    np.testing.assert_allclose(back[0].W, layers[0].W, rtol=1e-5, atol=1e-7)
+
+
+def _rbm_epoch_expected(layer, corpus_feats, bunch, cache, seed, lr, mmt, wc):
+    rs = orc.RandState(seed, bunch, layer.n_out)
+    X = np.concatenate(corpus_feats)
+    sched = orc.epoch_schedule_x([len(f) for f in corpus_feats], cache, bunch, rs.x_after)
+    m = orc.RBM.from_layer(layer)
+    for b in sched:
+        m.step(X[b], rs, lr, mmt, wc)
+    return m, len(sched)
+
+
+@pytest.mark.parametrize("vis,hid", [("gauss", "bern"), ("bern", "bern"), ("gauss", "gauss")])
+def test_rbm_trainer_epoch_matches_oracle(vis, hid):
+    """TRbmCu epoch: cache fill/shuffle (after the CuRand seeds on the same lrand48 stream),
+    CD-1 per bunch, reconstruction MSE -- config 4 in miniature (Gauss-Bernoulli first)."""
+    V, H, B, cache, seed = 40, 64, 32, 256, 321
+    lr, mmt, wc = 0.01, 0.5, 0.0002
+    rng = np.random.default_rng(5)
+    feats = [rng.standard_normal((int(n), V)).astype(np.float32) for n in rng.integers(40, 200, size=12)]
+    if vis == "bern":
+        feats = [1 / (1 + np.exp(-f)) for f in feats]
+    layer = formats.round_trip_text(formats.gen_rbm_init(V, H, seed=6, vis_type=vis, hid_type=hid), 9)[0]
+    net = Network.from_layers([layer])
+    tr = RbmTrainer(net, bunchsize=B, cachesize=cache, seed=seed, learn_rate=lr, momentum=mmt, weightcost=wc)
+    tr.train_corpus(feats)
+    exp, nb = _rbm_epoch_expected(layer, feats, B, cache, seed, lr, mmt, wc)
+    assert tr.steps == nb
+    mse, frames = tr.stats()
+    assert frames == exp.frames
+    np.testing.assert_allclose(mse, exp.mse, rtol=1e-4)
+    W, vb, hb, _ = net.rbm_params(0)
+    np.testing.assert_allclose(W, exp.W, rtol=2e-4, atol=2e-6)
+    np.testing.assert_allclose(vb, exp.vb, rtol=2e-4, atol=2e-6)
+    np.testing.assert_allclose(hb, exp.hb, rtol=2e-4, atol=2e-6)
+    rep = tr.report()
+    assert rep.startswith("Mse:") and f"frames:{frames}" in rep
