@@ -182,6 +182,25 @@ int tnet_rbm_update(const float* V, TnetMatrixDim dV, const float* H, TnetMatrix
 int tnet_rbm_bias_update(const float* M, TnetMatrixDim d, int neg_from, float* b, float* corr_b, float scale,
                          float mmt, void* workspace, void* stream);
 
+/* ---- single-frame kernels (TRecurrentCu: CuMath::OffsetGemv / BlasGer, cumath.cc:292-362) ---- */
+/* workspace bytes for tnet_gemv_rowvec */
+long tnet_gemv_workspace(int K, int N);
+/* y[0:N] = act(b + v[0:K] W), W [K x N] row-major (ld ldw), act 0 none | 1 sigmoid; b may be NULL.
+ * Split-K over many workgroups, fixed-order partials in `workspace`. */
+int tnet_gemv_rowvec(const float* v, int K, const float* W, int ldw, const float* b, float* y, int N, int act,
+                     void* workspace, void* stream);
+/* y[r] = beta*y[r] + W[r0 + r, 0:n] . x  for r < nrows, then y[r] *= s[r](1 - s[r]) if s != NULL
+ * (OffsetGemv('N') with the row offset, and the fused diff-sigmoid of the BPTT step). */
+int tnet_gemv_rows(const float* W, int ldw, int r0, int nrows, int n, const float* x, float* y, float beta,
+                   const float* s, void* stream);
+/* CuRecurrent::Update weight/bias step (cuRecurrent.cc:88-153) in one pass over W [rows x nout]:
+ *   corr = sum_{i<steps} (-lr h_i) (x) d_i ; corr += -lr*wc*W ; W += corr
+ *   cb = -lr d_0 + mmt*cb ; cb = -lr d_i + cb (i >= 1) ; b += cb
+ * h_i = row (head + i) % R of the history ring hist [R x rows], d_i = row i of D. */
+int tnet_rnn_update(float* W, int ldw, int rows, int nout, const float* hist, int ldh, int head, int R,
+                    const float* D, int ldd, int steps, float* b, float* corr_b, float lr, float mmt, float wc,
+                    void* stream);
+
 /* ---- per-element HybridTaus random numbers (CuRand, curand.tcc / curandkernels.cu) ----------
  * z1..z4: four uint32 state arrays with the element layout of the target matrix (index =
  * col + row*stride), seeded by the caller with lrand48() values > 128 (curand.tcc:36-45) and

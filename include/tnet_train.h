@@ -27,6 +27,7 @@ typedef struct TnetObjective TnetObjective;
 typedef struct TnetTrainer TnetTrainer;
 typedef struct TnetComm TnetComm;
 typedef struct TnetRbmTrainer TnetRbmTrainer;
+typedef struct TnetRnnTrainer TnetRnnTrainer;
 
 const char* tnet_last_error(void);
 
@@ -133,6 +134,17 @@ int tnet_rbm_trainer_stats(TnetRbmTrainer* t, double* mse, long* frames);
 int tnet_rbm_trainer_report(TnetRbmTrainer* t, char* buf, int cap); /* "Mse:... frames:... err/frm:..." */
 long tnet_rbm_trainer_prefill(TnetRbmTrainer* t, const float* feats, int rows, int cols, int ld);
 int tnet_rbm_trainer_replay(TnetRbmTrainer* t, long nsteps);
+
+/* ---- recurrent training (CuRecurrent, cuRecurrent.cc; the TRecurrentCu loop, TRecurrentCu.cc:319-375) --
+ * <recurrent> parameters: W [(n_in + n_out) x n_out] (host row-major), bias [n_out]. */
+int tnet_net_recurrent_get(TnetNetwork* net, int i, float* W, float* b);
+int tnet_net_recurrent_set(TnetNetwork* net, int i, const float* W, const float* b);
+/* Frame-by-frame trainer: sets the BPTT order of every <recurrent> layer (--BPTT); per utterance
+ * clears the history, then per frame propagate / objective / backpropagate+update. */
+TnetRnnTrainer* tnet_rnn_trainer_create(TnetNetwork* net, TnetObjective* obj, int bptt, int crossval);
+int tnet_rnn_trainer_free(TnetRnnTrainer* t);
+int tnet_rnn_trainer_utterance(TnetRnnTrainer* t, const float* feats, int rows, int cols, int ld, const int* labels);
+long tnet_rnn_trainer_frames(TnetRnnTrainer* t);
 
 /* ---- data parallel (no reference counterpart: Platform.h:143-391 is the CPU analogue) ---- */
 int tnet_comm_unique_id(char out[128]);        /* rank 0 creates, the launcher broadcasts it */

@@ -7,6 +7,7 @@
 
 #include "tnet_train.h"
 #include "curbm.h"
+#include "curecurrent.h"
 #include "trainer.h"
 
 using namespace TNet;
@@ -43,6 +44,9 @@ struct TnetTrainer {
 };
 struct TnetRbmTrainer {
   std::unique_ptr<CuRbmTrainer> t;
+};
+struct TnetRnnTrainer {
+  std::unique_ptr<CuRecurrentTrainer> t;
 };
 struct TnetComm {
   std::unique_ptr<GradExchange> ex;
@@ -484,6 +488,44 @@ int tnet_rbm_trainer_replay(TnetRbmTrainer* t, long n) {
   TRY_BEGIN t->t->Replay(n);
   TRY_END
 }
+
+// ------------------------------------------------------------------------------ recurrent
+static CuRecurrent& rnn_layer(TnetNetwork* h, int i) {
+  if (i < 0 || i >= h->net.Layers()) Error("component index out of range");
+  auto* p = dynamic_cast<CuRecurrent*>(&h->net.Layer(i));
+  if (!p) Error("component is not <recurrent>");
+  return *p;
+}
+int tnet_net_recurrent_get(TnetNetwork* h, int i, float* W, float* b) {
+  TRY_BEGIN CuRecurrent& R = rnn_layer(h, i);
+  if (W) R.Linearity().CopyToHost(W, R.Linearity().Cols());
+  if (b) R.Bias().CopyToHost(b);
+  TRY_END
+}
+int tnet_net_recurrent_set(TnetNetwork* h, int i, const float* W, const float* b) {
+  TRY_BEGIN CuRecurrent& R = rnn_layer(h, i);
+  if (W) R.Linearity().CopyFromHost(W, R.Linearity().Rows(), R.Linearity().Cols(), R.Linearity().Cols());
+  if (b) R.Bias().CopyFromHost(b, R.Bias().Dim());
+  CuDevice::Instantiate().Synchronize();
+  TRY_END
+}
+TnetRnnTrainer* tnet_rnn_trainer_create(TnetNetwork* net, TnetObjective* obj, int bptt, int crossval) {
+  try {
+    std::unique_ptr<TnetRnnTrainer> h(new TnetRnnTrainer);
+    h->t.reset(new CuRecurrentTrainer(&net->net, obj->obj.get(), bptt, crossval != 0));
+    return h.release();
+  }
+  TRY_END_PTR
+}
+int tnet_rnn_trainer_free(TnetRnnTrainer* t) {
+  TRY_BEGIN delete t;
+  TRY_END
+}
+int tnet_rnn_trainer_utterance(TnetRnnTrainer* t, const float* feats, int rows, int cols, int ld, const int* labels) {
+  TRY_BEGIN t->t->TrainUtterance(feats, (size_t)rows, (size_t)cols, (size_t)ld, labels);
+  TRY_END
+}
+long tnet_rnn_trainer_frames(TnetRnnTrainer* t) { return t ? t->t->Frames() : -1; }
 
 // -------------------------------------------------------------------------------------- DP
 int tnet_comm_unique_id(char out[128]) {

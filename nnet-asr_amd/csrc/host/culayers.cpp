@@ -63,6 +63,12 @@ void ReadVectorFast(std::istream& in, Vector<BaseFloat>& v) {
 void CuBiasedLinearity::PropagateFnc(const CuMatrix<BaseFloat>& X, CuMatrix<BaseFloat>& Y) {
   CuProfileScope p("CuBiasedLinearity::Propagate");
   // Y = b + X W  (AddScaledRow + Gemm('N','N',1,X,W,1), cuBiasedLinearity.cc:11-16) in one kernel
+  if (X.Rows() == 1) {  // single frame (TRecurrentCu): split-K row-vector kernel
+    void* ws = CuDevice::Instantiate().Workspace((size_t)tnet_gemv_workspace((int)GetNInputs(), (int)GetNOutputs()));
+    TNET_SAFE_CALL(tnet_gemv_rowvec(X.pCUData(), (int)GetNInputs(), mLinearity.pCUData(), (int)mLinearity.Stride(),
+                                    mBias.pCUData(), Y.pCUData(), (int)GetNOutputs(), 0, ws, S));
+    return;
+  }
   TNET_SAFE_CALL(tnet_affine_fwd(X.pCUData(), X.Dim(), mLinearity.pCUData(), mLinearity.Dim(), mBias.pCUData(),
                                  Y.pCUData(), Y.Dim(), 0, S));
 }
@@ -70,6 +76,11 @@ void CuBiasedLinearity::PropagateFnc(const CuMatrix<BaseFloat>& X, CuMatrix<Base
 void CuBiasedLinearity::BackpropagateFnc(const CuMatrix<BaseFloat>& X, CuMatrix<BaseFloat>& Y) {
   CuProfileScope p("CuBiasedLinearity::Backpropagate");
   // Y = X W^T  (Gemm('N','T',1,E,W,0), cuBiasedLinearity.cc:21-25)
+  if (X.Rows() == 1) {  // single frame: one wavefront per row of W
+    TNET_SAFE_CALL(tnet_gemv_rows(mLinearity.pCUData(), (int)mLinearity.Stride(), 0, (int)GetNInputs(),
+                                  (int)GetNOutputs(), X.pCUData(), Y.pCUData(), 0.0f, nullptr, S));
+    return;
+  }
   TNET_SAFE_CALL(tnet_affine_bwd(X.pCUData(), X.Dim(), mLinearity.pCUData(), mLinearity.Dim(), nullptr, 0,
                                  Y.pCUData(), Y.Dim(), 0, S));
 }

@@ -2,6 +2,7 @@
 #include "cunetwork.h"
 
 #include "curbm.h"
+#include "curecurrent.h"
 
 #include <algorithm>
 #include <cctype>
@@ -156,6 +157,7 @@ CuComponent* CuNetwork::ComponentFactory(std::istream& rIn) {
   else if (tag == "<sigmoid>") pRet = new CuSigmoid(nInputs, nOutputs, pPred);
   else if (tag == "<softmax>") pRet = new CuSoftmax(nInputs, nOutputs, pPred);
   else if (tag == "<rbm>") pRet = new CuRbm(nInputs, nOutputs, pPred);
+  else if (tag == "<recurrent>") pRet = new CuRecurrent(nInputs, nOutputs, pPred);
   else Error(std::string("Unknown Component tag:") + tag);
   pRet->ReadFromStream(rIn);
   return pRet;

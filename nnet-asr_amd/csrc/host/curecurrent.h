@@ -1,0 +1,78 @@
+// curecurrent.h -- Elman recurrent layer trained frame by frame with truncated BPTT, and the
+// TRecurrentCu loop (BASELINE config 5).
+//
+//   CuRecurrent        : src/CuTNetLib/cuRecurrent.h:15-57, cuRecurrent.cc:16-183 -- input row
+//                        [x_t, y_{t-1}] pushed into a (bptt+1)-row history, y_t = sigmoid(b + row W),
+//                        per-frame update from the present row plus bptt back-propagated rows
+//   CuRecurrentTrainer : src/TRecurrentCu.cc:319-375 -- per utterance: clear the history, then for
+//                        every frame propagate, cross-entropy, backpropagate + update
+//
+// MI355X: the history is a ring (no row shifting), every one-row GEMM/GEMV runs on the single-
+// frame kernels of gemv.hip (split-K row-vector x matrix, wave-per-row matrix x vector), and the
+// whole recurrent weight update -- all bptt+1 outer products, weight decay and the write of W --
+// is one pass over W.
+#pragma once
+
+#include "cuobjective.h"
+#include "culayers.h"
+
+namespace TNet {
+
+class CuNetwork;
+
+class CuRecurrent : public CuUpdatableComponent {
+ public:
+  CuRecurrent(size_t nInputs, size_t nOutputs, CuComponent* pPred)
+      : CuUpdatableComponent(nInputs, nOutputs, pPred), mLinearity(nInputs + nOutputs, nOutputs), mBias(nOutputs),
+        mBiasCorrection(nOutputs) {}
+
+  ComponentType GetType() const override { return RECURRENT; }
+  const char* GetName() const override { return "<recurrent>"; }
+
+  void PropagateFnc(const CuMatrix<BaseFloat>& X, CuMatrix<BaseFloat>& Y) override;
+  void BackpropagateFnc(const CuMatrix<BaseFloat>& X, CuMatrix<BaseFloat>& Y) override;
+  void Update() override;
+
+  /// BPTT order; allocates the (ord+1)-row input history (cuRecurrent.h:30-33)
+  void BpttOrder(int ord);
+  int GetBpttOrder() const { return mBpttOrder; }
+  /// zero the history and the previous output (cuRecurrent.h:34-39)
+  void ClearHistory();
+
+  void ReadFromStream(std::istream& rIn) override;
+  void WriteToStream(std::ostream& rOut) override;
+
+  CuMatrix<BaseFloat>& Linearity() { return mLinearity; }  ///< [(nIn + nOut) x nOut]
+  CuVector<BaseFloat>& Bias() { return mBias; }
+
+ private:
+  const float* HistRow(int i) const {  // logical history row i (0 = present)
+    return mInputHistory.pCURowData((size_t)((mHead + i) % (int)mInputHistory.Rows()));
+  }
+  CuMatrix<BaseFloat> mLinearity;
+  CuVector<BaseFloat> mBias, mBiasCorrection;
+  CuMatrix<BaseFloat> mInputHistory;  // ring of bptt+1 rows [x, y_prev]
+  CuMatrix<BaseFloat> mDiff;          // [bptt+1 x nOut] back-propagated errors of the present update
+  CuMatrix<BaseFloat> mDiffTmp;       // [1 x nOut]
+  int mBpttOrder = -1;
+  int mHead = 0;
+};
+
+/// The TRecurrentCu loop over a network containing <recurrent> layers.
+class CuRecurrentTrainer {
+ public:
+  CuRecurrentTrainer(CuNetwork* net, CuObjectiveFunction* obj, int bptt, bool crossval);
+  /// One utterance: features [rows x cols] (host, leading dim ld) and class ids.
+  void TrainUtterance(const float* feats, size_t rows, size_t cols, size_t ld, const int* labels);
+  long Frames() const { return mFrames; }
+
+ private:
+  CuNetwork* mNet;
+  CuObjectiveFunction* mObj;
+  bool mCrossval;
+  CuMatrix<BaseFloat> mFeats, mOut, mErr, mRow;
+  CuVector<int> mLabels, mLabelRow;
+  long mFrames = 0;
+};
+
+}  // namespace TNet

@@ -15,7 +15,7 @@ import numpy as np
 from . import formats  # noqa: F401  (host formats; no device code)
 from ._lib import HOST_ALLREDUCE_FN, LIB_PATH, MatrixDim, TnetError, check, check_ptr, header_symbols, lib
 
-__all__ = ["DeviceArray", "Network", "Objective", "Trainer", "RbmTrainer", "Comm", "TnetError", "synchronize",
+__all__ = ["DeviceArray", "Network", "Objective", "Trainer", "RbmTrainer", "RnnTrainer", "Comm", "TnetError", "synchronize",
            "pad_stride",
            "device_count", "version", "LIB_PATH", "header_symbols", "formats"]
 
@@ -170,6 +170,14 @@ class Network:
     def train_bunch(self, obj: "Objective", X: DeviceArray, labels: DeviceArray, train: bool = True) -> None:
         check(lib().tnet_net_train_bunch(self.h, obj.h, X.ptr, X.rows, X.stride, labels.ptr, int(train)),
               "train_bunch")
+
+    def recurrent_params(self, i: int = 0):
+        """(W [(n_in + n_out) x n_out], bias) of a <recurrent> component."""
+        _, ni, no = self.components()[i]
+        W = np.empty((ni + no, no), np.float32)
+        b = np.empty(no, np.float32)
+        check(lib().tnet_net_recurrent_get(self.h, i, W.ctypes.data, b.ctypes.data), "recurrent_get")
+        return W, b
 
     def rbm_params(self, i: int = 0):
         """(W [n_vis x n_hid], vis_bias, hid_bias, (vis_type, hid_type)) of an <rbm> component."""
@@ -364,6 +372,36 @@ class RbmTrainer:
         try:
             if getattr(self, "h", None):
                 lib().tnet_rbm_trainer_free(self.h)
+                self.h = None
+        except Exception:
+            pass
+
+
+class RnnTrainer:
+    """The TRecurrentCu frame-by-frame loop (src/TRecurrentCu.cc:319-375)."""
+
+    def __init__(self, net: Network, obj: Objective, bptt: int = 4, crossval: bool = False):
+        self.net, self.obj = net, obj
+        self.h = check_ptr(lib().tnet_rnn_trainer_create(net.h, obj.h, bptt, int(crossval)), "tnet_rnn_trainer_create")
+
+    def train_utterance(self, feats: np.ndarray, labels: np.ndarray) -> None:
+        feats = np.ascontiguousarray(feats, np.float32)
+        labels = np.ascontiguousarray(labels, np.int32)
+        check(lib().tnet_rnn_trainer_utterance(self.h, feats.ctypes.data, feats.shape[0], feats.shape[1],
+                                               feats.shape[1], labels.ctypes.data), "rnn utterance")
+
+    def train_corpus(self, feats, labels) -> None:
+        for x, l in zip(feats, labels):
+            self.train_utterance(x, l)
+
+    @property
+    def frames(self) -> int:
+        return lib().tnet_rnn_trainer_frames(self.h)
+
+    def __del__(self):
+        try:
+            if getattr(self, "h", None):
+                lib().tnet_rnn_trainer_free(self.h)
                 self.h = None
         except Exception:
             pass

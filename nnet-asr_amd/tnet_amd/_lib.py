@@ -137,6 +137,16 @@ _SIGS = {
     "tnet_rbm_trainer_report": (i32, [vp, C.c_char_p, i32]),
     "tnet_rbm_trainer_prefill": (i64, [vp, vp, i32, i32, i32]),
     "tnet_rbm_trainer_replay": (i32, [vp, i64]),
+    "tnet_net_recurrent_get": (i32, [vp, i32, vp, vp]),
+    "tnet_net_recurrent_set": (i32, [vp, i32, vp, vp]),
+    "tnet_rnn_trainer_create": (vp, [vp, vp, i32, i32]),
+    "tnet_rnn_trainer_free": (i32, [vp]),
+    "tnet_rnn_trainer_utterance": (i32, [vp, vp, i32, i32, i32, vp]),
+    "tnet_rnn_trainer_frames": (i64, [vp]),
+    "tnet_gemv_workspace": (i64, [i32, i32]),
+    "tnet_gemv_rowvec": (i32, [vp, i32, vp, i32, vp, vp, i32, i32, vp, vp]),
+    "tnet_gemv_rows": (i32, [vp, i32, i32, i32, i32, vp, vp, f32, vp, vp]),
+    "tnet_rnn_update": (i32, [vp, i32, i32, i32, vp, i32, i32, i32, vp, i32, i32, vp, vp, f32, f32, f32, vp]),
     "tnet_affine_fwd_t": (i32, [vp, MatrixDim, vp, MatrixDim, vp, vp, MatrixDim, i32, vp]),
     "tnet_rbm_update": (i32, [vp, MatrixDim, vp, MatrixDim, vp, MatrixDim, vp, i32, f32, f32, f32, vp]),
     "tnet_rbm_bias_update": (i32, [vp, MatrixDim, i32, vp, vp, f32, f32, vp, vp]),

@@ -171,6 +171,19 @@ def gen_rbm_init(n_vis: int, n_hid: int, seed: int, vis_type: str = "gauss", hid
                   {"vis_type": vis_type, "hid_type": hid_type, "vis_bias": vb})]
 
 
+def gen_recurrent_init(n_in: int, n_hid: int, n_out: int, seed: int, gauss: bool = True,
+                       negbias: bool = False) -> List[Layer]:
+    """Seeded restatement of tools/init/gen_recurrent_init.py (<recurrent> n_in -> n_hid, matrix
+    [n_hid x (n_in + n_hid)] in the file) followed by a gen_mlp_init-style <biasedlinearity>
+    n_hid -> n_out + <softmax> (the TRecurrentCu network of BASELINE config 5)."""
+    rng = np.random.default_rng(seed)
+    k = n_in + n_hid
+    Wt = (0.1 * rng.standard_normal((n_hid, k)) if gauss else rng.random((n_hid, k)) / 5.0 - 0.1).astype(np.float32)
+    b = ((rng.random(n_hid) / 5.0 - 4.1) if negbias else np.zeros(n_hid)).astype(np.float32)
+    out = gen_mlp_init([n_hid, n_out], seed=seed + 1)
+    return [Layer("<recurrent>", n_hid, n_in, np.ascontiguousarray(Wt.T), b)] + out
+
+
 def round_trip_text(layers: Sequence[Layer], precision: int = 6) -> List[Layer]:
     """Weights exactly as a reader sees them after a text write at ``precision`` digits."""
     buf = io.StringIO()

@@ -46,6 +46,10 @@ def lib():
                                    C.c_int, C.c_float, C.c_float, C.c_float, u32p, u32p, u32p, u32p, C.c_void_p,
                                    C.POINTER(C.c_double)]
         L.orc_rbm_step.restype = C.c_int
+        L.orc_rnn_utterance.argtypes = [C.c_int, C.c_int, C.c_int, f32p, f32p, f32p, f32p, f32p, f32p, f32p, f32p,
+                                        i32p, C.c_int, C.c_int, C.c_float, C.c_float, C.c_float, C.c_int,
+                                        C.POINTER(C.c_double), C.POINTER(C.c_long)]
+        L.orc_rnn_utterance.restype = C.c_int
         L.orc_mlp_step.argtypes = [C.c_int, i32p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, f32p, i32p,
                                    C.c_int, C.c_float, C.c_float, C.c_float, C.c_int, C.c_int, f32p, f32p,
                                    C.POINTER(C.c_double), C.POINTER(C.c_long)]
@@ -236,3 +240,34 @@ class RBM:
         self.mse += e2.value
         self.frames += B
         return neg
+
+
+class RNN:
+    """Oracle state of [<recurrent> nIn->H, <biasedlinearity> H->S, <softmax>] (TRecurrentCu)."""
+
+    def __init__(self, Wr, br, W2, b2):
+        self.Wr = np.ascontiguousarray(Wr, np.float32).copy()
+        self.br = np.ascontiguousarray(br, np.float32).copy()
+        self.W2 = np.ascontiguousarray(W2, np.float32).copy()
+        self.b2 = np.ascontiguousarray(b2, np.float32).copy()
+        self.cbr = np.zeros_like(self.br)
+        self.cW2 = np.zeros_like(self.W2)
+        self.cb2 = np.zeros_like(self.b2)
+        self.xent = 0.0
+        self.correct = 0
+        self.frames = 0
+
+    def utterance(self, feats, labels, bptt, lr, mmt=0.0, wc=0.0, gdf=True):
+        feats = np.ascontiguousarray(feats, np.float32)
+        labels = np.ascontiguousarray(labels, np.int32)
+        T, nIn = feats.shape
+        H, S = self.W2.shape
+        xe = C.c_double(0.0)
+        cor = C.c_long(0)
+        st = lib().orc_rnn_utterance(nIn, H, S, self.Wr, self.br, self.cbr, self.W2, self.b2, self.cW2, self.cb2,
+                                     feats, labels, T, bptt, lr, mmt, wc, int(gdf), C.byref(xe), C.byref(cor))
+        if st != 0:
+            raise MemoryError("orc_rnn_utterance")
+        self.xent += xe.value
+        self.correct += cor.value
+        self.frames += T

@@ -432,3 +432,101 @@ int orc_rbm_step(int V, int H, float* W, float* vb, float* hb, float* cW, float*
   free(pos_hid); free(states); free(neg_vis); free(neg_hid);
   return 0;
 }
+
+/* ---------------------------------------------------------------------------------------
+ * TRecurrentCu (TRecurrentCu.cc:319-375) over [<recurrent> nIn->H, <biasedlinearity> H->S,
+ * <softmax>] with cross-entropy, one utterance, frame by frame:
+ *   CuRecurrent::PropagateFnc (cuRecurrent.cc:16-53): history ring push of [x_t, y_{t-1}],
+ *     y_t = sigmoid(br + row Wr)
+ *   CuBiasedLinearity forward + softmax; objective err = out - onehot
+ *   CuNetwork::Backpropagate: <biasedlinearity> error e = err W2^T (old W2), its GPU update
+ *     (cuBiasedLinearity.cc:46-64, rows = 1); <recurrent> is the stopper: Update only
+ *     (cuRecurrent.cc:88-153: d_0 = e y(1-y); d_i = (Wr[nIn:] d_{i-1}) y_{t-i}(1-y_{t-i});
+ *     corr = sum_i -lr h_i (x) d_i ; corr += -lr wc Wr ; Wr += corr ; bias with momentum)
+ * State arrays are updated in place; hist [(bptt+1) x (nIn+H)] and y_prev [H] are zeroed here
+ * (ClearHistory at the utterance start).  Returns 0.
+ * ------------------------------------------------------------------------------------- */
+int orc_rnn_utterance(int nIn, int H, int S, float* Wr, float* br, float* cbr, float* W2, float* b2, float* cW2,
+                      float* cb2, const float* feats, const int* labels, int T, int bptt, float lr, float mmt,
+                      float wc, int gdf, double* xent, long* correct) {
+  const int K = nIn + H, R = bptt + 1;
+  float* hist = (float*)calloc((size_t)R * K, sizeof(float));
+  float* y = (float*)calloc((size_t)H, sizeof(float));
+  float* out = (float*)malloc(sizeof(float) * S);
+  float* err = (float*)malloc(sizeof(float) * S);
+  float* e = (float*)malloc(sizeof(float) * H);
+  float* D = (float*)malloc(sizeof(float) * (size_t)R * H);
+  if (!hist || !y || !out || !err || !e || !D) return -1;
+  int head = 0;
+  for (int t = 0; t < T; t++) {
+    /* forward: recurrent layer */
+    head = (head + R - 1) % R;
+    float* row = hist + (size_t)head * K;
+    memcpy(row, feats + (size_t)t * nIn, sizeof(float) * nIn);
+    memcpy(row + nIn, y, sizeof(float) * H);
+    for (int c = 0; c < H; c++) {
+      double s = br[c];
+      for (int k = 0; k < K; k++) s += (double)row[k] * Wr[(size_t)k * H + c];
+      y[c] = (float)(1.0 / (1.0 + exp(-(double)(float)s)));
+    }
+    /* output layer + softmax + objective */
+    float* a = out;
+    for (int c = 0; c < S; c++) {
+      double s = b2[c];
+      for (int k = 0; k < H; k++) s += (double)y[k] * W2[(size_t)k * S + c];
+      a[c] = (float)s;
+    }
+    orc_softmax(out, a, 1, S);
+    orc_xent_eval(out, labels + t, 1, S, err, xent, correct);
+    /* <biasedlinearity>: backpropagate with the old weights, then its GPU update (rows = 1) */
+    for (int k = 0; k < H; k++) {
+      double s = 0.0;
+      for (int c = 0; c < S; c++) s += (double)err[c] * W2[(size_t)k * S + c];
+      e[k] = (float)s;
+    }
+    {
+      float N = 1.0f;  /* GRADDIVFRM: rows = 1 either way */
+      (void)gdf;
+      N *= (float)(1.0 / (1.0 - mmt));
+      const float scale = -lr / N, l2 = -lr * wc;
+      for (int k = 0; k < H; k++)
+        for (int c = 0; c < S; c++) {
+          float* cp = cW2 + (size_t)k * S + c;
+          float* wp = W2 + (size_t)k * S + c;
+          *cp = y[k] * err[c] + mmt * *cp;
+          float w = *wp + scale * *cp;
+          *wp = w + l2 * w;
+        }
+      for (int c = 0; c < S; c++) {
+        cb2[c] = err[c] + mmt * cb2[c];
+        b2[c] = b2[c] + scale * cb2[c];
+      }
+    }
+    /* <recurrent> update with BPTT */
+    for (int c = 0; c < H; c++) D[c] = (float)((double)y[c] * (1.0 - (double)y[c]) * (double)e[c]);
+    for (int i = 1; i <= bptt; i++) {
+      const float* hy = hist + (size_t)((head + i - 1) % R) * K + nIn;
+      for (int r = 0; r < H; r++) {
+        double s = 0.0;
+        for (int c = 0; c < H; c++) s += (double)Wr[(size_t)(nIn + r) * H + c] * D[(size_t)(i - 1) * H + c];
+        D[(size_t)i * H + r] = (float)((float)s * (hy[r] * (1.0f - hy[r])));
+      }
+    }
+    for (int k = 0; k < K; k++)
+      for (int c = 0; c < H; c++) {
+        float acc = 0.f;
+        for (int i = 0; i < R; i++) acc += (-lr * hist[(size_t)((head + i) % R) * K + k]) * D[(size_t)i * H + c];
+        float* wp = Wr + (size_t)k * H + c;
+        const float w = *wp;
+        *wp = ((-lr * wc) * w + acc) + w;
+      }
+    for (int c = 0; c < H; c++) {
+      float g = -lr * D[c] + mmt * cbr[c];
+      for (int i = 1; i < R; i++) g = -lr * D[(size_t)i * H + c] + g;
+      cbr[c] = g;
+      br[c] = g + br[c];
+    }
+  }
+  free(hist); free(y); free(out); free(err); free(e); free(D);
+  return 0;
+}
