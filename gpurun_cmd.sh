@@ -1,4 +1,4 @@
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 600 python -m pytest tests/test_gpu_rnn.py tests/test_gpu_rbm.py -x -q > gpurun_out/gpu_tests.log 2>&1
+timeout -k 10 600 python -m pytest tests/test_gpu_dropin.py -x -q > gpurun_out/gpu_tests.log 2>&1
 echo "done $?"

@@ -7,6 +7,10 @@ namespace TNet {
 
 Rng48& GlobalRng() {
   static Rng48 rng(0);
+#ifdef TNET_HOST_KALDILIB
+  static bool libc = (rng.UseLibc(true), true);  // the reference drivers seed libc's srand48
+  (void)libc;
+#endif
   return rng;
 }
 void SeedRandom(long seed) { GlobalRng().Seed(seed); }

@@ -32,12 +32,14 @@ void ReadMatrixFast(std::istream& in, Matrix<BaseFloat>& m) {
   m.Init((size_t)r, (size_t)c);
   std::streambuf* sb = in.rdbuf();
   char tok[128];
-  float* p = m.pData();
-  for (long long i = 0; i < r * c; i++) {
-    if (!next_token(sb, tok, sizeof tok)) Error("Failed to read matrix from stream: truncated");
-    char* end = nullptr;
-    p[i] = std::strtof(tok, &end);
-    if (end == tok) Error(std::string("Failed to read matrix from stream: bad token ") + tok);
+  for (long long i = 0; i < r; i++) {
+    float* p = m.pRowData((size_t)i);  // rows may be padded (KaldiLib Matrix stride)
+    for (long long j = 0; j < c; j++) {
+      if (!next_token(sb, tok, sizeof tok)) Error("Failed to read matrix from stream: truncated");
+      char* end = nullptr;
+      p[j] = std::strtof(tok, &end);
+      if (end == tok) Error(std::string("Failed to read matrix from stream: bad token ") + tok);
+    }
   }
 }
 

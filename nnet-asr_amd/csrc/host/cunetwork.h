@@ -59,6 +59,9 @@ class CuNetwork {
   void SetWeightcost(BaseFloat weightcost);
   void SetL1(BaseFloat l1);
   void SetGradDivFrm(bool div);
+  /// Directory for the cluster-transform bases of the TROY components (TNetCu.cc:245-248); no
+  /// component of this build uses it, the value is only kept.
+  void SetTempBasisDir(const char* dir) { mTempBasisDir = dir ? dir : ""; }
 
   // ---- MI355X fused training path -------------------------------------------------------
   /// true if the topology is the plain sigmoid MLP with a softmax output
@@ -83,6 +86,7 @@ class CuNetwork {
                          bool train);
 
   LayeredType mNetComponents;
+  std::string mTempBasisDir;
   CuComponent* mpPropagErrorStopper = nullptr;
   BaseFloat mGlobLearnRate = 0.0f;
   std::string mLearnRateFactors;

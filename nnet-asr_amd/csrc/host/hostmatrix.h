@@ -12,6 +12,12 @@
 
 #include "tnet_common.h"
 
+#ifdef TNET_HOST_KALDILIB
+// drop-in build: the reference's host containers and their text I/O (src/KaldiLib/Matrix.h,
+// Vector.h, Matrix.tcc:521-600, Vector.tcc:525-571)
+#include "Matrix.h"
+#include "Vector.h"
+#else
 namespace TNet {
 
 enum MatrixTrasposeType { NO_TRANS = 'N', TRANS = 'T' };
@@ -40,8 +46,8 @@ class Matrix {
   size_t Stride() const { return mCols; }
   T* pData() { return mData.data(); }
   const T* pData() const { return mData.data(); }
-  T* operator[](size_t r) { return mData.data() + r * mCols; }
-  const T* operator[](size_t r) const { return mData.data() + r * mCols; }
+  T* pRowData(size_t r) { return mData.data() + r * mCols; }
+  const T* pRowData(size_t r) const { return mData.data() + r * mCols; }
   T& operator()(size_t r, size_t c) { return mData[r * mCols + c]; }
   const T& operator()(size_t r, size_t c) const { return mData[r * mCols + c]; }
   void Zero() { std::fill(mData.begin(), mData.end(), T(0)); }
@@ -134,3 +140,4 @@ typedef Matrix<BaseFloat> BfMatrix;
 typedef Vector<BaseFloat> BfVector;
 
 }  // namespace TNet
+#endif  // TNET_HOST_KALDILIB

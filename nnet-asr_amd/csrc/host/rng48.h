@@ -7,6 +7,7 @@
 #pragma once
 
 #include <cstdint>
+#include <cstdlib>
 #include <vector>
 
 namespace TNet {
@@ -19,9 +20,13 @@ class Rng48 {
   uint64_t State() const { return mX; }
   void SetState(uint64_t x) { mX = x & kMask; }
   long Lrand48() {
+    if (mLibc) return ::lrand48();
     mX = (0x5DEECE66Dull * mX + 0xBull) & kMask;
     return (long)(mX >> 17);
   }
+  /// Draw from the C library's srand48/lrand48 stream instead (drop-in build: the reference
+  /// drivers seed it with srand48(SEED), TNetCu.cc:330-338, and CuCache shuffles with lrand48)
+  void UseLibc(bool on) { mLibc = on; }
   /// libstdc++ std::random_shuffle(first, last, gen) with gen(k) = lrand48() % k
   /// (bits/stl_algo.h:4603-4620)
   void RandomShuffle(int* p, size_t n) {
@@ -38,6 +43,7 @@ class Rng48 {
  private:
   static constexpr uint64_t kMask = 0xFFFFFFFFFFFFull;
   uint64_t mX = 0;
+  bool mLibc = false;
 };
 
 /// Process-wide stream, the counterpart of libc's srand48/lrand48 state.

@@ -5,7 +5,7 @@
 // (src/CuBaseLib/cucommon.h:13-22) -- but WITHOUT the device synchronisation after each call.
 #pragma once
 
-#include <hip/hip_runtime.h>
+#include <hip/hip_runtime_api.h>
 
 #include <sstream>
 #include <stdexcept>
@@ -13,6 +13,13 @@
 
 #include "tnet_kernels.h"
 
+#ifdef TNET_HOST_KALDILIB
+// Drop-in build: the library is compiled against the reference's own KaldiLib
+// (src/KaldiLib/Error.h, Types.h), so drivers such as TNetCu.cc exchange its Matrix / Vector /
+// MyException types with the CuTNetLib API unchanged.
+#include "Error.h"
+#include "Types.h"
+#else
 namespace TNet {
 
 typedef float BaseFloat;  // src/KaldiLib/Types.h:15-18 (DOUBLEPRECISION off)
@@ -27,6 +34,7 @@ class MyException : public std::runtime_error {
 inline void Warning(const std::string& msg);
 
 }  // namespace TNet
+#endif
 
 #define TNET_SAFE_CALL(fun)                                                                       \
   do {                                                                                            \
@@ -50,5 +58,7 @@ inline void Warning(const std::string& msg);
     }                                                                                             \
   } while (0)
 
+#ifndef TNET_HOST_KALDILIB
 #include <iostream>
 inline void TNet::Warning(const std::string& msg) { std::cerr << "WARNING " << msg << std::endl; }
+#endif
