@@ -126,7 +126,7 @@ void CuRbm::WriteToStream(std::ostream& rOut) {
 }
 
 // ============================================================================== CuRand
-void CuRand::SeedGpu(size_t rows, size_t cols, Rng48& rng) {
+void CuRandState::SeedGpu(size_t rows, size_t cols, Rng48& rng) {
   std::vector<unsigned> host(rows * cols);
   for (int k = 0; k < 4; k++) {
     for (size_t i = 0; i < rows * cols; i++) {
@@ -139,33 +139,33 @@ void CuRand::SeedGpu(size_t rows, size_t cols, Rng48& rng) {
   }
 }
 
-void CuRand::Check(const CuMatrix<BaseFloat>& m) const {
+void CuRandState::Check(const CuMatrix<BaseFloat>& m) const {
   if (m.Rows() != z[0].Rows() || m.Cols() != z[0].Cols() || m.Stride() != z[0].Stride())
     Error("CuRand: Non matching dims!!");
 }
 
-void CuRand::Rand(CuMatrix<BaseFloat>& tgt) {
+void CuRandState::Rand(CuMatrix<BaseFloat>& tgt) {
   tgt.Init(z[0].Rows(), z[0].Cols());
   Check(tgt);
   TNET_SAFE_CALL(tnetF_rand(tgt.pCUData(), tgt.Dim(), z[0].pCUData(), z[1].pCUData(), z[2].pCUData(),
                             z[3].pCUData(), S));
 }
 
-void CuRand::GaussRand(CuMatrix<BaseFloat>& tgt) {
+void CuRandState::GaussRand(CuMatrix<BaseFloat>& tgt) {
   tgt.Init(z[0].Rows(), z[0].Cols());
   Check(tgt);
   TNET_SAFE_CALL(tnetF_gauss_rand(tgt.pCUData(), tgt.Dim(), z[0].pCUData(), z[1].pCUData(), z[2].pCUData(),
                                   z[3].pCUData(), S));
 }
 
-void CuRand::BinarizeProbs(const CuMatrix<BaseFloat>& probs, CuMatrix<BaseFloat>& states) {
+void CuRandState::BinarizeProbs(const CuMatrix<BaseFloat>& probs, CuMatrix<BaseFloat>& states) {
   Check(probs);
   states.Init(z[0].Rows(), z[0].Cols());
   TNET_SAFE_CALL(tnet_rand_binarize(states.pCUData(), (int)states.Stride(), probs.pCUData(), probs.Dim(),
                                     z[0].pCUData(), z[1].pCUData(), z[2].pCUData(), z[3].pCUData(), S));
 }
 
-void CuRand::AddGaussNoise(CuMatrix<BaseFloat>& tgt, BaseFloat gscale) {
+void CuRandState::AddGaussNoise(CuMatrix<BaseFloat>& tgt, BaseFloat gscale) {
   Check(tgt);
   TNET_SAFE_CALL(tnet_add_gauss_noise(tgt.pCUData(), tgt.Dim(), gscale, z[0].pCUData(), z[1].pCUData(),
                                       z[2].pCUData(), z[3].pCUData(), S));

@@ -22,12 +22,24 @@
 
 namespace TNet {
 
-class CuRbm : public CuBiasedLinearity {
+/// The RBM training interface the drivers program against (cuRbm.h:15-45).
+class CuRbmBase : public CuBiasedLinearity {
  public:
   typedef enum { BERNOULLI, GAUSSIAN } RbmUnitType;
+  CuRbmBase(size_t nInputs, size_t nOutputs, CuComponent* pPred) : CuBiasedLinearity(nInputs, nOutputs, pPred) {}
+  virtual void Propagate(const CuMatrix<BaseFloat>& visProbs, CuMatrix<BaseFloat>& hidProbs) = 0;
+  virtual void Reconstruct(const CuMatrix<BaseFloat>& hidState, CuMatrix<BaseFloat>& visProbs) = 0;
+  virtual void RbmUpdate(const CuMatrix<BaseFloat>& pos_vis, const CuMatrix<BaseFloat>& pos_hid,
+                         const CuMatrix<BaseFloat>& neg_vis, const CuMatrix<BaseFloat>& neg_hid) = 0;
+  virtual RbmUnitType VisType() const = 0;
+  virtual RbmUnitType HidType() const = 0;
+  using CuComponent::Propagate;
+};
 
+class CuRbm : public CuRbmBase {
+ public:
   CuRbm(size_t nInputs, size_t nOutputs, CuComponent* pPred)
-      : CuBiasedLinearity(nInputs, nOutputs, pPred), mVisBias(nInputs), mVisBiasCorrection(nInputs) {}
+      : CuRbmBase(nInputs, nOutputs, pPred), mVisBias(nInputs), mVisBiasCorrection(nInputs) {}
 
   ComponentType GetType() const override { return RBM; }
   const char* GetName() const override { return "<rbm>"; }
@@ -38,12 +50,13 @@ class CuRbm : public CuBiasedLinearity {
   void Update() override;
 
   // RBM training API (cuRbm.h:27-45)
-  void Propagate(const CuMatrix<BaseFloat>& visProbs, CuMatrix<BaseFloat>& hidProbs);
-  void Reconstruct(const CuMatrix<BaseFloat>& hidState, CuMatrix<BaseFloat>& visProbs);
+  void Propagate(const CuMatrix<BaseFloat>& visProbs, CuMatrix<BaseFloat>& hidProbs) override;
+  void Reconstruct(const CuMatrix<BaseFloat>& hidState, CuMatrix<BaseFloat>& visProbs) override;
   void RbmUpdate(const CuMatrix<BaseFloat>& pos_vis, const CuMatrix<BaseFloat>& pos_hid,
-                 const CuMatrix<BaseFloat>& neg_vis, const CuMatrix<BaseFloat>& neg_hid);
-  RbmUnitType VisType() const { return mVisType; }
-  RbmUnitType HidType() const { return mHidType; }
+                 const CuMatrix<BaseFloat>& neg_vis, const CuMatrix<BaseFloat>& neg_hid) override;
+  RbmUnitType VisType() const override { return mVisType; }
+  RbmUnitType HidType() const override { return mHidType; }
+  using CuComponent::Propagate;
   void SetUnitTypes(RbmUnitType vis, RbmUnitType hid) { mVisType = vis; mHidType = hid; }
 
   void ReadFromStream(std::istream& rIn) override;
@@ -63,10 +76,10 @@ class CuRbm : public CuBiasedLinearity {
 };
 
 /// Per-element HybridTaus generator state for a rows x cols target (curand.h:11-32).
-class CuRand {
+class CuRandState {
  public:
-  CuRand() {}
-  CuRand(size_t rows, size_t cols, Rng48& rng) { SeedGpu(rows, cols, rng); }
+  CuRandState() {}
+  CuRandState(size_t rows, size_t cols, Rng48& rng) { SeedGpu(rows, cols, rng); }
   /// Four state matrices filled row by row with lrand48() values > 128, z1 first
   /// (curand.tcc:13-45: the draws come from the process lrand48 stream, here `rng`).
   void SeedGpu(size_t rows, size_t cols, Rng48& rng);
@@ -81,6 +94,16 @@ class CuRand {
  private:
   void Check(const CuMatrix<BaseFloat>& m) const;
   CuMatrix<unsigned> z[4];
+};
+
+/// The reference's CuRand<T>(rows, cols) (curand.h:11-32): seeded from the process lrand48
+/// stream (GlobalRng: libc's srand48/lrand48 in the drop-in build).
+template <typename T>
+class CuRand : public CuRandState {
+  static_assert(std::is_same<T, BaseFloat>::value, "CuRand: BaseFloat only");
+
+ public:
+  CuRand(size_t rows, size_t cols) : CuRandState(rows, cols, GlobalRng()) {}
 };
 
 struct RbmTrainerOptions {
@@ -109,7 +132,7 @@ class CuRbmTrainer {
   CuRbm* mRbm;
   RbmTrainerOptions mOpt;
   Rng48 mRng;
-  CuRand mRand;
+  CuRandState mRand;
   CuCache mCache;
   CuMeanSquareError mMse;
   CuMatrix<BaseFloat> mV, mH, mStates;               // [2B x vis], [2B x hid], [B x hid]
