@@ -111,6 +111,11 @@ int tnetF_expand(float* y, const float* x, const int* off, TnetMatrixDim dout, T
 /* y[i,j] = x[i, copy_from[j]] (out of range -> +inf)            -- cudaF_rearrange (cukernels.cu:364-379) */
 int tnetF_rearrange(float* y, const float* x, const int* copy_from, TnetMatrixDim dout, TnetMatrixDim din,
                     void* stream);
+/* y[:, b*bo:(b+1)*bo] = x[:, b*bi:(b+1)*bi] . t for every block b, t = [bi x bo], one launch
+ * -- CuMath::BlockLinearity (cumath.cc:76-113: one cublasSgemm per block), <blocklinearity>
+ * (cuCRBEDctFeat.h:146-197); any strides/offsets */
+int tnet_block_linearity(float* y, TnetMatrixDim dy, const float* x, TnetMatrixDim dx, const float* t,
+                         TnetMatrixDim dt, void* stream);
 /* y[i,:] = x[copy_from[i], :]                                    -- cudaF_randomize (cukernels.cu:382-393) */
 int tnetF_randomize(float* y, const float* x, const int* copy_from, TnetMatrixDim dout, TnetMatrixDim din,
                     void* stream);

@@ -111,6 +111,10 @@ int tnet_trainer_set_comm(TnetTrainer* t, TnetComm* comm);
 /* data-parallel steps this rank joined without a bunch of its own (zero gradient) */
 long tnet_trainer_empty_steps(TnetTrainer* t);
 int tnet_trainer_trace(TnetTrainer* t, int trace);
+/* --FEATURETRANSFORM / --STARTFRMEXT / --ENDFRMEXT (TNetCu.cc:274-278, 384-393): each utterance
+ * passed to add_utterance is edge-extended, propagated through `transform` (a front-end network,
+ * borrowed, may be NULL = off) and trimmed before the cache; labels stay one per input frame */
+int tnet_trainer_set_transform(TnetTrainer* t, TnetNetwork* transform, int start_ext, int end_ext);
 
 /* ---- RBM pre-training (CuRbm, cuRbm.cc; the TRbmCu loop, TRbmCu.cc:291-357) ----------------
  * <rbm> parameters: W [n_vis x n_hid] (host row-major), visible / hidden biases; types[0..1] =

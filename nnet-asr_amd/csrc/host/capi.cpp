@@ -383,6 +383,11 @@ int tnet_trainer_set_comm(TnetTrainer* t, TnetComm* c) {
   TRY_BEGIN t->t->SetExchange(c ? c->ex.get() : nullptr);
   TRY_END
 }
+int tnet_trainer_set_transform(TnetTrainer* t, TnetNetwork* transform, int start_ext, int end_ext) {
+  TRY_BEGIN if (start_ext < 0 || end_ext < 0) Error("tnet_trainer_set_transform: negative frame extension");
+  t->t->SetTransform(transform ? &transform->net : nullptr, (size_t)start_ext, (size_t)end_ext);
+  TRY_END
+}
 long tnet_trainer_empty_steps(TnetTrainer* t) { return t ? t->t->EmptySteps() : -1; }
 int tnet_trainer_trace(TnetTrainer* t, int trace) {
   TRY_BEGIN t->t->Cache().Trace(trace);

@@ -120,13 +120,9 @@ void CuMath<BaseFloat>::BlockLinearity(CuMatrix<BaseFloat>& Y, const CuMatrix<Ba
   const size_t bi = block_transf.Rows(), bo = block_transf.Cols();
   if (X.Cols() % bi != 0 || Y.Cols() != X.Cols() / bi * bo || X.Rows() != Y.Rows())
     Error("CuMath::BlockLinearity: non matching dimensions");
-  const size_t nb = X.Cols() / bi;
-  for (size_t b = 0; b < nb; b++) {
-    // sub-matrix views need 16-B alignment of the column offsets for the MFMA path
-    TNET_SAFE_CALL(tnet_sgemm('N', 'N', (int)X.Rows(), (int)bo, (int)bi, 1.f, X.pCUData() + b * bi, (int)X.Stride(),
-                              block_transf.pCUData(), (int)block_transf.Stride(), 0.f, Y.pCUData() + b * bo,
-                              (int)Y.Stride(), S));
-  }
+  // all blocks in one launch (the reference: one cublasSgemm per block)
+  TNET_SAFE_CALL(tnet_block_linearity(Y.pCUData(), Y.Dim(), X.pCUData(), X.Dim(), block_transf.pCUData(),
+                                      block_transf.Dim(), S));
 }
 void CuMath<BaseFloat>::Expand(CuMatrix<BaseFloat>& Y, const CuMatrix<BaseFloat>& X,
                                const CuVector<int>& frameOffsets) {

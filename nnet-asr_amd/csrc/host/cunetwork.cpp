@@ -1,6 +1,7 @@
 // cunetwork.cpp -- see cunetwork.h.
 #include "cunetwork.h"
 
+#include "cufeat.h"
 #include "curbm.h"
 #include "curecurrent.h"
 
@@ -158,6 +159,14 @@ CuComponent* CuNetwork::ComponentFactory(std::istream& rIn) {
   else if (tag == "<softmax>") pRet = new CuSoftmax(nInputs, nOutputs, pPred);
   else if (tag == "<rbm>") pRet = new CuRbm(nInputs, nOutputs, pPred);
   else if (tag == "<recurrent>") pRet = new CuRecurrent(nInputs, nOutputs, pPred);
+  // feature front end (cuNetwork.cc:263-268, cuCRBEDctFeat.h)
+  else if (tag == "<expand>") pRet = new CuExpand(nInputs, nOutputs, pPred);
+  else if (tag == "<copy>") pRet = new CuCopy(nInputs, nOutputs, pPred);
+  else if (tag == "<transpose>") pRet = new CuTranspose(nInputs, nOutputs, pPred);
+  else if (tag == "<blocklinearity>") pRet = new CuBlockLinearity(nInputs, nOutputs, pPred);
+  else if (tag == "<bias>") pRet = new CuBias(nInputs, nOutputs, pPred);
+  else if (tag == "<window>") pRet = new CuWindow(nInputs, nOutputs, pPred);
+  else if (tag == "<log>") pRet = new CuLog(nInputs, nOutputs, pPred);
   else Error(std::string("Unknown Component tag:") + tag);
   pRet->ReadFromStream(rIn);
   return pRet;

@@ -63,7 +63,38 @@ bool CuTrainer::DpRound(long n, bool final) {
   return plan.all_final;
 }
 
+void CuTrainer::SetTransform(CuNetwork* transform, size_t start_ext, size_t end_ext) {
+  mTransform = transform;
+  mStartExt = transform ? start_ext : 0;
+  mEndExt = transform ? end_ext : 0;
+}
+
 void CuTrainer::AddUtterance(const float* feats, size_t rows, size_t cols, size_t ld, const int* labels) {
+  if (mTransform && rows > 0) {
+    // frame extension on the host (the reader's job in the reference), one upload, the transform
+    // network on the device, trim, then the cache takes the device rows
+    const size_t R = rows + mStartExt + mEndExt;
+    mExtHost.resize(R * cols);
+    for (size_t r = 0; r < R; r++) {
+      const size_t src = r < mStartExt ? 0 : (r - mStartExt >= rows ? rows - 1 : r - mStartExt);
+      std::memcpy(&mExtHost[r * cols], feats + src * ld, cols * sizeof(float));
+    }
+    mRaw.CopyFromHost(mExtHost.data(), R, cols, cols);
+    mTransform->Propagate(mRaw, mTransformed);
+    if (mTransformed.Cols() != mNet->GetNInputs()) {
+      std::ostringstream os;
+      os << "CuTrainer::AddUtterance: transformed feature dim " << mTransformed.Cols() << " != network input dim "
+         << mNet->GetNInputs();
+      Error(os.str());
+    }
+    mTrimmed.Init(rows, mTransformed.Cols());
+    mTrimmed.CopyRows(rows, mStartExt, mTransformed, 0);
+    mUttLabels.CopyFromHost(labels, rows);
+    mCache.AddDataLabels(mTrimmed, mUttLabels);
+    mTrainedSinceFill = false;
+    if (mCache.Full()) DrainCache(false);
+    return;
+  }
   if (cols != mNet->GetNInputs()) {
     std::ostringstream os;
     os << "CuTrainer::AddUtterance: feature dim " << cols << " != network input dim " << mNet->GetNInputs();

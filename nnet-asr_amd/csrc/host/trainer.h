@@ -35,6 +35,12 @@ class CuTrainer {
   /// number of steps).
   void SetExchange(GradExchange* ex) { mExchange = ex; }
 
+  /// --FEATURETRANSFORM + --STARTFRMEXT/--ENDFRMEXT (TNetCu.cc:274-278, 384-393): every utterance
+  /// is extended by repeating its first/last frame (the KaldiLib reader, Features.cc:776-850),
+  /// pushed through `transform` on the device and trimmed before it enters the cache.  The
+  /// transform network is borrowed (not owned); nullptr switches it off.
+  void SetTransform(CuNetwork* transform, size_t start_ext, size_t end_ext);
+
   /// Append one utterance (host memory): features [rows x cols] with leading dim ld, class ids.
   void AddUtterance(const float* feats, size_t rows, size_t cols, size_t ld, const int* labels);
   /// End of the utterance list.
@@ -68,6 +74,11 @@ class CuTrainer {
   Rng48 mRng;
   CuMatrix<BaseFloat> mFeats;
   CuVector<int> mLabels;
+  CuNetwork* mTransform = nullptr;
+  size_t mStartExt = 0, mEndExt = 0;
+  std::vector<float> mExtHost;
+  CuMatrix<BaseFloat> mRaw, mTransformed, mTrimmed;
+  CuVector<int> mUttLabels;
   long mSteps = 0;
   long mEmptySteps = 0;
   bool mTrainedSinceFill = false;

@@ -307,6 +307,12 @@ class Trainer:
     def replay(self, n: int) -> None:
         check(lib().tnet_trainer_replay(self.h, n), "replay")
 
+    def set_transform(self, transform: Optional["Network"], start_ext: int = 0, end_ext: int = 0) -> None:
+        """--FEATURETRANSFORM network + --STARTFRMEXT/--ENDFRMEXT (TNetCu.cc:384-393)."""
+        self._transform = transform   # borrowed by the C++ trainer: keep it alive
+        check(lib().tnet_trainer_set_transform(self.h, transform.h if transform else None, start_ext, end_ext),
+              "set_transform")
+
     def set_comm(self, comm: Optional["Comm"]) -> None:
         self._comm = comm
         check(lib().tnet_trainer_set_comm(self.h, comm.h if comm else None), "set_comm")

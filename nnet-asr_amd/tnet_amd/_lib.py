@@ -55,6 +55,7 @@ _SIGS = {
     "tnetF_expand": (i32, [vp, vp, vp, MatrixDim, MatrixDim, vp]),
     "tnetF_rearrange": (i32, [vp, vp, vp, MatrixDim, MatrixDim, vp]),
     "tnetF_randomize": (i32, [vp, vp, vp, MatrixDim, MatrixDim, vp]),
+    "tnet_block_linearity": (i32, [vp, MatrixDim, vp, MatrixDim, vp, MatrixDim, vp]),
     "tnet_gather_i32": (i32, [vp, vp, vp, i32, vp]),
     "tnet_sgemm": (i32, [C.c_char, C.c_char, i32, i32, i32, f32, vp, i32, vp, i32, f32, vp, i32, vp]),
     "tnet_gemm_config": (i32, [C.c_char_p]),
@@ -119,6 +120,7 @@ _SIGS = {
     "tnet_trainer_prefill": (i64, [vp, vp, i32, i32, i32, vp]),
     "tnet_trainer_set_comm": (i32, [vp, vp]),
     "tnet_trainer_trace": (i32, [vp, i32]),
+    "tnet_trainer_set_transform": (i32, [vp, vp, i32, i32]),
     "tnet_comm_unique_id": (i32, [C.c_char_p]),
     "tnet_comm_create": (vp, [i32, i32, C.c_char_p]),
     "tnet_comm_free": (i32, [vp]),

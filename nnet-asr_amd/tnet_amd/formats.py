@@ -13,9 +13,9 @@
 * deterministic synthetic corpora (features ~ N(0,1), teacher-MLP or uniform labels) used by the
   tests and by bench.py.
 
-The C++ product library has its own reader/writer for the same format
-(nnet-asr_amd/csrc/host/nnet_io.cpp); this module exists so tests and the bench can build
-inputs without touching the device.
+The C++ product library has its own reader/writer for the same format (CuNetwork::ReadNetwork /
+WriteNetwork and each component's ReadFromStream / WriteToStream, nnet-asr_amd/csrc/host/); this
+module exists so tests and the bench can build inputs without touching the device.
 """
 from __future__ import annotations
 
@@ -66,12 +66,42 @@ def write_nnet(layers: Sequence[Layer], path_or_buf, precision: int = 6) -> None
             b = np.asarray(L.b, dtype=np.float32)
             out.write(f"v {b.shape[0]}  " + " ".join(_fmt(v, precision) for v in b) + " ")
             out.write("\n\n")
+        else:
+            _write_frontend(out, L, precision)
     text = out.getvalue()
     if hasattr(path_or_buf, "write"):
         path_or_buf.write(text)
     else:
         with open(path_or_buf, "w") as f:
             f.write(text)
+
+
+def _write_frontend(out, L: Layer, precision: int) -> None:
+    """Payload of the front-end components (cuCRBEDctFeat.h:16-304 ReadFromStream/WriteToStream)."""
+    def ivec(v):
+        v = np.asarray(v, dtype=np.int64)
+        out.write(f"v {v.shape[0]}  " + " ".join(str(int(x)) for x in v) + " \n")
+
+    def fvec(v):
+        v = np.asarray(v, dtype=np.float32)
+        out.write(f"v {v.shape[0]}  " + " ".join(_fmt(x, precision) for x in v) + " \n")
+
+    if L.tag == "<expand>":
+        ivec(L.extra["offsets"])
+    elif L.tag == "<copy>":
+        ivec(np.asarray(L.extra["indices"]) + 1)          # the file is 1-based
+    elif L.tag == "<transpose>":
+        out.write(f" {int(L.extra['context'])}\n")
+    elif L.tag == "<blocklinearity>":
+        Bt = np.asarray(L.W, dtype=np.float32).T           # file holds the [bo x bi] transpose
+        out.write(f"m {Bt.shape[0]} {Bt.shape[1]}\n")
+        for row in Bt:
+            out.write(" ".join(_fmt(v, precision) for v in row) + " \n")
+    elif L.tag == "<bias>":
+        fvec(L.b)
+    elif L.tag == "<window>":
+        fvec(L.extra["window"])
+    # <sigmoid>, <softmax>, <log>: no payload
 
 
 def _tokens(text: str):
@@ -125,6 +155,19 @@ def read_nnet(path_or_text: str) -> List[Layer]:
             L.W = np.ascontiguousarray(read_matrix().T)
             L.extra["vis_bias"] = read_vector()
             L.b = read_vector()
+        elif tag == "<expand>":
+            L.extra["offsets"] = read_vector().astype(np.int64)
+        elif tag == "<copy>":
+            L.extra["indices"] = read_vector().astype(np.int64) - 1
+        elif tag == "<transpose>":
+            L.extra["context"] = int(toks[i])
+            i += 1
+        elif tag == "<blocklinearity>":
+            L.W = np.ascontiguousarray(read_matrix().T)
+        elif tag == "<bias>":
+            L.b = read_vector()
+        elif tag == "<window>":
+            L.extra["window"] = read_vector()
         layers.append(L)
     return layers
 
@@ -182,6 +225,37 @@ def gen_recurrent_init(n_in: int, n_hid: int, n_out: int, seed: int, gauss: bool
     b = ((rng.random(n_hid) / 5.0 - 4.1) if negbias else np.zeros(n_hid)).astype(np.float32)
     out = gen_mlp_init([n_hid, n_out], seed=seed + 1)
     return [Layer("<recurrent>", n_hid, n_in, np.ascontiguousarray(Wt.T), b)] + out
+
+
+def gen_frontend_transform(dim: int = 23, context: int = 25, n_dct: int = 26, seed: int = 0,
+                           normalise: bool = True) -> List[Layer]:
+    """A --FEATURETRANSFORM network of the examples/01 "Hamm_dct_norm" structure, built from
+    formulas: <expand> to 2*context+1 frames, <transpose> to band-major, a Hamming <window> per
+    band, a per-band DCT-II <blocklinearity> (2*context+1 -> n_dct; row k = cos(pi k (j+1/2) / L)),
+    then (normalise) a seeded <bias> / <window> pair standing in for the global mean/variance
+    normalisation.  Output dim = dim * n_dct."""
+    L = 2 * context + 1
+    n_sp = dim * L
+    n_out = dim * n_dct
+    j = np.arange(L)
+    hamming = (0.54 - 0.46 * np.cos(2.0 * np.pi * j / (L - 1))).astype(np.float32)
+    dct = np.cos(np.pi * np.outer(np.arange(n_dct), j + 0.5) / L).astype(np.float32)   # [n_dct x L]
+    layers = [Layer("<expand>", n_sp, dim, extra={"offsets": np.arange(-context, context + 1)}),
+              Layer("<transpose>", n_sp, n_sp, extra={"context": L}),
+              Layer("<window>", n_sp, n_sp, extra={"window": np.tile(hamming, dim)}),
+              Layer("<blocklinearity>", n_out, n_sp, W=np.ascontiguousarray(dct.T))]
+    if normalise:
+        rng = np.random.default_rng(seed)
+        layers.append(Layer("<bias>", n_out, n_out, b=(-rng.standard_normal(n_out)).astype(np.float32)))
+        layers.append(Layer("<window>", n_out, n_out,
+                            extra={"window": (0.05 + 0.3 * rng.random(n_out)).astype(np.float32)}))
+    return layers
+
+
+def extend_frames(x: np.ndarray, start: int, end: int) -> np.ndarray:
+    """--STARTFRMEXT / --ENDFRMEXT: repeat the first / last frame (src/KaldiLib/Features.cc:776-850)."""
+    x = np.asarray(x, dtype=np.float32)
+    return np.concatenate([np.repeat(x[:1], start, 0), x, np.repeat(x[-1:], end, 0)], axis=0)
 
 
 def round_trip_text(layers: Sequence[Layer], precision: int = 6) -> List[Layer]:

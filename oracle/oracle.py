@@ -271,3 +271,54 @@ class RNN:
         self.xent += xe.value
         self.correct += cor.value
         self.frames += T
+
+
+# --------------------------------------------------------------------------------------
+# feature front end (--FEATURETRANSFORM networks): numpy restatement
+# --------------------------------------------------------------------------------------
+
+def frontend_component(L, x):
+    """One front-end component forward, restating src/CuTNetLib/cuCRBEDctFeat.h:16-304 (and the
+    CUDA kernels it calls, src/CuBaseLib/cukernels.cu:347-379, cumath.cc:76-113).  Returns float32;
+    the block product accumulates in float64."""
+    x = np.asarray(x, dtype=np.float32)
+    T = x.shape[0]
+    if L.tag == "<expand>":                                     # _expand: edge-clamped row offsets
+        off = np.asarray(L.extra["offsets"], dtype=np.int64)
+        rows = np.clip(np.arange(T)[:, None] + off[None, :], 0, T - 1)   # [T x k]
+        return x[rows].reshape(T, -1)
+    if L.tag in ("<copy>", "<transpose>"):                      # _rearrange: out of range -> +inf
+        if L.tag == "<copy>":
+            idx = np.asarray(L.extra["indices"], dtype=np.int64)
+        else:                                                   # cuCRBEDctFeat.h:109-123
+            n, ctx = L.n_in, int(L.extra["context"])
+            ch = n // ctx
+            idx = np.array([c + f * ch for c in range(ch) for f in range(ctx)], dtype=np.int64)
+        ok = (idx >= 0) & (idx < x.shape[1])
+        y = np.full((T, idx.shape[0]), np.inf, dtype=np.float32)
+        y[:, ok] = x[:, idx[ok]]
+        return y
+    if L.tag == "<blocklinearity>":
+        B = np.asarray(L.W, dtype=np.float64)                   # [bi x bo]
+        bi, bo = B.shape
+        nb = x.shape[1] // bi
+        xb = x.astype(np.float64).reshape(T, nb, bi)
+        return np.einsum("tbi,io->tbo", xb, B).reshape(T, nb * bo).astype(np.float32)
+    if L.tag == "<bias>":
+        return (x + np.asarray(L.b, dtype=np.float32)[None, :]).astype(np.float32)
+    if L.tag == "<window>":
+        return (x * np.asarray(L.extra["window"], dtype=np.float32)[None, :]).astype(np.float32)
+    if L.tag == "<log>":
+        with np.errstate(divide="ignore", invalid="ignore"):
+            return np.log(x).astype(np.float32)
+    raise ValueError("not a front-end component: " + L.tag)
+
+
+def frontend_forward(layers, x, start_ext=0, end_ext=0):
+    """TNetCu's per-utterance front end (TNetCu.cc:384-393): frame extension by edge repetition
+    (src/KaldiLib/Features.cc:776-850), transform network, trim start_ext/end_ext rows."""
+    x = np.asarray(x, dtype=np.float32)
+    y = np.concatenate([np.repeat(x[:1], start_ext, 0), x, np.repeat(x[-1:], end_ext, 0)], axis=0)
+    for L in layers:
+        y = frontend_component(L, y)
+    return y[start_ext:y.shape[0] - end_ext]

@@ -110,3 +110,73 @@ def test_epoch_schedule_leftover_filling_cache_is_an_error():
     with pytest.raises(ValueError):
         orc.epoch_schedule([500, 1100, 100], 512, 64, 1)
     assert orc.epoch_schedule([500, 1100], 512, 64, 1).shape == (8, 64)  # last leftover dropped
+
+
+# ---------------------------------------------------------------------------------------------
+# feature front end: the numpy restatement vs the reference CPU TFeaCat (tests/golden/make_frontend.py)
+# ---------------------------------------------------------------------------------------------
+
+def _frontend_inputs():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location(
+        "make_frontend", os.path.join(os.path.dirname(__file__), "golden", "make_frontend.py"))
+    mf = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mf)
+    from tnet_amd import formats
+    corpus = formats.synth_corpus(**mf.CORPUS)
+    layers = formats.round_trip_text(formats.gen_frontend_transform(**mf.TRANSFORM), 9)
+    return mf, corpus, layers
+
+
+def test_frontend_oracle_vs_reference_tfeacat(golden_dir):
+    """Hamm_dct_norm-structured transform, frame extension 25/25: full output of two utterances
+    (abs 1e-5; values up to ~10) and float64 sum / sum of squares of all 40 (rel 1e-6)."""
+    mf, corpus, layers = _frontend_inputs()
+    g = _load(golden_dir, "frontend_feacat.npz")
+    for k, x in enumerate(corpus.feats):
+        y = orc.frontend_forward(layers, x, 25, 25)
+        assert y.shape == (int(g["rows"][k]), 598)
+        if k in mf.FULL:
+            np.testing.assert_allclose(y, g[f"Y_{k}"], rtol=0, atol=1e-5)
+        y = y.astype(np.float64)
+        assert abs(y.sum() - g["sum"][k]) <= 1e-6 * np.abs(y).sum()
+        assert abs((y ** 2).sum() - g["sumsq"][k]) <= 1e-6 * g["sumsq"][k]
+
+
+def test_frontend_decode_oracle_vs_reference_tfeacat(golden_dir):
+    """decode.sh's TFeaCat call (transform + MLP + GMMBYPASS sqrt(-2 ln p), TFeaCat.cc:236-243)."""
+    from tnet_amd import formats
+    mf, corpus, layers = _frontend_inputs()
+    g = _load(golden_dir, "frontend_decode.npz")
+    mlp = formats.round_trip_text(formats.gen_mlp_init(mf.EPOCH["dims"], seed=mf.EPOCH["init_seed"]), 6)
+    net = orc.MLP.from_layers(mlp)
+    for k in (mf.DECODE, 0, 5):
+        p = net.forward(orc.frontend_forward(layers, corpus.feats[k], 25, 25)).astype(np.float64)
+        y = np.sqrt(-2.0 * np.log(p))
+        if k == mf.DECODE:
+            np.testing.assert_allclose(y, g[f"Y_{k}"], rtol=1e-4, atol=1e-5)
+        assert abs(y.sum() - g["sum"][k]) <= 1e-5 * np.abs(y).sum()
+
+
+def test_frontend_component_restatement_edges():
+    """<copy> (1-based in the file, out-of-range -> +inf as _rearrange), <expand> clamping with
+    asymmetric offsets, <log>, and the .nnet text round trip of every front-end tag."""
+    from tnet_amd import formats
+    rng = np.random.default_rng(3)
+    x = rng.random((7, 5)).astype(np.float32) + 0.1
+    cp = formats.Layer("<copy>", 4, 5, extra={"indices": np.array([4, 0, 0, 9])})
+    y = orc.frontend_component(cp, x)
+    np.testing.assert_array_equal(y[:, :3], x[:, [4, 0, 0]])
+    assert np.isinf(y[:, 3]).all()
+    ex = formats.Layer("<expand>", 15, 5, extra={"offsets": np.array([-3, 0, 2])})
+    y = orc.frontend_component(ex, x)
+    np.testing.assert_array_equal(y[0, :5], x[0])
+    np.testing.assert_array_equal(y[1, :5], x[0])
+    np.testing.assert_array_equal(y[6, 10:], x[6])
+    np.testing.assert_array_equal(y[4, 10:], x[6])
+    np.testing.assert_allclose(orc.frontend_component(formats.Layer("<log>", 5, 5), x), np.log(x), rtol=1e-6)
+    layers = formats.gen_frontend_transform(dim=5, context=2, n_dct=3, seed=1) + [cp, formats.Layer("<log>", 4, 4)]
+    back = formats.round_trip_text(layers, 9)
+    assert [L.tag for L in back] == [L.tag for L in layers]
+    np.testing.assert_array_equal(back[-2].extra["indices"], cp.extra["indices"])
+    np.testing.assert_allclose(back[3].W, layers[3].W, rtol=1e-7)
