@@ -69,6 +69,19 @@ def synth_frames(n, dim, n_cls, seed):
     return rng.standard_normal((n, dim)).astype(np.float32), rng.integers(0, n_cls, n).astype(np.int32)
 
 
+def pmc_traffic():
+    """roofline.traffic: HBM bytes per launch of the roofline kernel set, from the newest committed
+    PMC summary (profiles/r*_pmc_gemm2048.json, tools/profile_round.sh + tools/roofline_evidence.py:
+    FETCH_SIZE x2 + WRITE_SIZE of the same kernels, measured in separate rocprofv3 --pmc passes --
+    counters cannot be read inside this process)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "r*_pmc_gemm2048.json")))
+    if not files:
+        return None, None
+    d = json.load(open(files[-1]))
+    return d["traffic_MB_per_launch"] * 1e6, os.path.relpath(files[-1], REPO)
+
+
 def parse_kernel_report(text):
     out = {}
     for line in text.strip().splitlines():
@@ -156,9 +169,13 @@ def main():
         ms = sum(v["ms"] for v in hid)
         flops = sum(v["work"] for v in hid)
         achieved = flops / (ms * 1e-3) / 1e12
+        traffic, traffic_src = pmc_traffic()
         roof = {"bound": "mfma", "kernel": "gemm_f32 2048x2048 (fwd/bwd/update)", "achieved": round(achieved, 2),
                 "peak": PEAK_FP32_MFMA, "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_MFMA, 4),
-                "traffic": None, "launches": launches, "avg_launch_us": round(1000.0 * ms / launches, 2),
+                "traffic": traffic, "traffic_unit": "bytes/launch", "traffic_source": traffic_src,
+                "algorithmic_bytes_per_launch": 4.0 * ((2 * B * 2048 + 2048 ** 2) + (3 * B * 2048 + 2048 ** 2) +
+                                                       (2 * B * 2048 + 2 * 2048 ** 2)) / 3,  # fwd, bwd, upd
+                "launches": launches, "avg_launch_us": round(1000.0 * ms / launches, 2),
                 "flops_per_launch": flops / launches}
     all_gemm_ms = sum(v["ms"] for k, v in kern.items() if k.startswith("gemm_"))
     all_ms = sum(v["ms"] for v in kern.values())

@@ -1,6 +1,14 @@
 """Drive one GEMM shape repeatedly for rocprofv3 --pmc passes: our fused affine kernels
 (TNET_GEMM_CFG selects the tile config) and, for comparison, torch.mm (hipBLASLt) on the same
-shapes and data distribution.  usage: python tools/gemm_pmc.py [ours|torch] [iters]"""
+shapes and data distribution.
+
+  ours   fwd only (1024 x 2048 x 2048, bias + sigmoid)
+  layer  the bench's roofline kernel set: one 2048x2048 <biasedlinearity> layer's fwd (bias +
+         sigmoid), bwd (diff-sigmoid) and fused SGD update per iteration, bunch 1024, exactly the
+         launches bench.py times (momentum 0, weight cost 0 -> no momentum buffer)
+  torch  torch.mm on the fwd shape
+
+usage: python tools/gemm_pmc.py [ours|layer|torch] [iters]"""
 import os
 import sys
 
@@ -22,6 +30,22 @@ if which == "ours":
     Y = DeviceArray(rows, no)
     for _ in range(iters):
         check(lib().tnet_affine_fwd(X.ptr, X.dim, W.ptr, W.dim, b.ptr, Y.ptr, Y.dim, 1, S))
+    check(lib().tnet_synchronize())
+elif which == "layer":
+    from tnet_amd import DeviceArray
+    from tnet_amd._lib import check, lib
+    S = lib().tnet_stream()
+    rng = np.random.default_rng(0)
+    X = DeviceArray.from_numpy((1.0 / (1.0 + np.exp(-rng.standard_normal((rows, ni))))).astype(np.float32))
+    W = DeviceArray.from_numpy((0.05 * rng.standard_normal((ni, no))).astype(np.float32))
+    b = DeviceArray.vector(np.zeros(no, np.float32))
+    Y = DeviceArray(rows, no)
+    E = DeviceArray.from_numpy((1e-3 * rng.standard_normal((rows, no))).astype(np.float32))
+    Eo = DeviceArray(rows, ni)
+    for _ in range(iters):
+        check(lib().tnet_affine_fwd(X.ptr, X.dim, W.ptr, W.dim, b.ptr, Y.ptr, Y.dim, 1, S))
+        check(lib().tnet_affine_bwd(E.ptr, E.dim, W.ptr, W.dim, X.ptr, X.stride, Eo.ptr, Eo.dim, 1, S))
+        check(lib().tnet_affine_update(X.ptr, X.dim, E.ptr, E.dim, W.ptr, W.dim, None, 0, -1e-6, 0.0, 0.0, S))
     check(lib().tnet_synchronize())
 else:
     import torch

@@ -1,0 +1,100 @@
+"""Turn one tools/profile_round.sh run into the round's committed evidence under profiles/.
+
+usage: python tools/roofline_evidence.py gpurun_out rNN
+
+  profiles/<rNN>_bench_dnn4.json              the bench line of that run
+  profiles/<rNN>_bench_dnn4_kernel_stats.csv  rocprofv3 --kernel-trace --stats summary (same command)
+  profiles/<rNN>_rocprof_roofline.json        per-dispatch durations of the roofline kernel set (the
+                                              2048x2048 fwd / bwd / update GEMMs) from the kernel
+                                              trace, next to the bench's live hipEvent average
+  profiles/<rNN>_pmc_gemm2048.json            HBM traffic per launch of the same kernel set from the
+                                              FETCH_SIZE and WRITE_SIZE passes (tools/gemm_pmc.py
+                                              layer), FETCH_SIZE doubled on gfx950 (MI355X_MICROARCH.md)
+bench.py reads the newest profiles/r*_pmc_gemm2048.json for roofline.traffic.
+
+The 2048x2048 launches are found in the trace by dispatch order inside each step (split at the
+cache gather): forward = the three 64x128 BIAS_SIG launches after the K=440 layer; backward = the
+diff-sigmoid launches except the first after softmax_xent (that one has K=4000); update = the
+64-tile-row SGD launches with grid 65536 (the 4000-wide update has a larger grid).
+"""
+import csv
+import json
+import os
+import shutil
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import pmc_summary  # noqa: E402
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def classify_trace(path):
+    rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
+    cls = {"fwd": [], "bwd": [], "upd": []}
+    after_softmax = False
+    for r in rows:
+        name = r["Kernel_Name"]
+        dur = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+        grid = int(r["Grid_Size_X"])
+        if "softmax_xent" in name:
+            after_softmax = True
+            continue
+        if "gemm16_kernel<64, 128, 64, 2, 2, 2, true, false, 2>" in name:
+            cls["fwd"].append(dur)
+        elif "gemm16_kernel<64, 128, 64, 2, 2, 2, true, true, 3>" in name:
+            if after_softmax:          # K = 4000 (error into the last hidden layer)
+                after_softmax = False
+            else:
+                cls["bwd"].append(dur)
+        elif "gemm16_kernel<128, 128, 64, 2, 2, 2, false, false, 4>" in name and grid == 65536:
+            cls["upd"].append(dur)
+    return cls
+
+
+def main():
+    src, tag = sys.argv[1], sys.argv[2]
+    prof = os.path.join(REPO, "profiles")
+    os.makedirs(prof, exist_ok=True)
+    bench = json.loads(open(os.path.join(src, "bench.json")).read().strip().splitlines()[-1])
+    with open(os.path.join(prof, f"{tag}_bench_dnn4.json"), "w") as f:
+        json.dump(bench, f, indent=1)
+    shutil.copyfile(os.path.join(src, "prof_stats", "bench_kernel_stats.csv"),
+                    os.path.join(prof, f"{tag}_bench_dnn4_kernel_stats.csv"))
+    cls = classify_trace(os.path.join(src, "prof_stats", "bench_kernel_trace.csv"))
+    allv = cls["fwd"] + cls["bwd"] + cls["upd"]
+    prof_bench = json.loads(open(os.path.join(src, "bench_prof.json")).read().strip().splitlines()[-1])
+    tr = {"source": "rocprofv3 --kernel-trace --stats -- python3 bench.py --no-cpu-baseline",
+          "per_class_avg_us": {k: round(sum(v) / len(v), 2) for k, v in cls.items() if v},
+          "per_class_launches": {k: len(v) for k, v in cls.items()},
+          "roofline_set_avg_us_rocprof": round(sum(allv) / len(allv), 2),
+          "roofline_set_avg_us_hipevent_same_run": prof_bench["roofline"]["avg_launch_us"],
+          "roofline_set_avg_us_hipevent_bench_run": bench["roofline"]["avg_launch_us"],
+          "note": "warmup launches included in the rocprof average (the trace covers the whole process)"}
+    with open(os.path.join(prof, f"{tag}_rocprof_roofline.json"), "w") as f:
+        json.dump(tr, f, indent=1)
+    fetch = pmc_summary.summarise(os.path.join(src, "pmc_fetch"))
+    write = pmc_summary.summarise(os.path.join(src, "pmc_write"))
+    kern = {}
+    for d in (fetch, write):
+        for k, r in d.items():
+            if "gemm" in k:
+                kern.setdefault(k, {}).update({kk: v for kk, v in r.items() if kk in ("kernel", "grid", "dispatches",
+                                                                                       "fetch_MB_x2", "write_MB")})
+    per = [r["fetch_MB_x2"] + r["write_MB"] for r in kern.values()]
+    algo = {"fwd": (1024 * 2048 + 2048 * 2048 + 1024 * 2048) * 4 / 1e6,     # X, W read; Y written
+            "bwd": (1024 * 2048 * 3 + 2048 * 2048) * 4 / 1e6,               # E, W, Ybelow read; Eo written
+            "upd": (1024 * 2048 * 2 + 2048 * 2048 * 2) * 4 / 1e6}           # X, E read; W read + written
+    pmc = {"source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes) -- python3 "
+                     "tools/gemm_pmc.py layer 20; FETCH_SIZE x2 (gfx950), KiB -> MB",
+           "kernels": kern, "traffic_MB_per_launch": round(sum(per) / len(per), 3),
+           "algorithmic_MB_per_launch": {k: round(v, 3) for k, v in algo.items()},
+           "algorithmic_MB_per_launch_avg": round(sum(algo.values()) / 3, 3)}
+    with open(os.path.join(prof, f"{tag}_pmc_gemm2048.json"), "w") as f:
+        json.dump(pmc, f, indent=1)
+    print(json.dumps(tr, indent=1))
+    print(json.dumps(pmc, indent=1))
+
+
+if __name__ == "__main__":
+    main()
