@@ -14,8 +14,9 @@ barrier / max-reduce of the timings; it is imported after the HIP library so one
 loaded.
 
 Extra JSON fields: roofline (dominant kernel = the 2048x2048 affine-layer GEMMs, timed with hipEvents
-on the library stream inside the timed region), kernels (per-kernel breakdown), cpu_baseline
-(the reference CPU TNet on this host, rank 0 at N=1).
+on the library stream over K further steps of the same workload right after the timed region -- only
+those launches carry events, and the value region none, since every event pair adds stream time), kernels (per-kernel breakdown from extra all-events steps after the timed
+region), cpu_baseline (the reference CPU TNet on this host, rank 0 at N=1).
 """
 import argparse
 import json
@@ -101,7 +102,11 @@ def main():
     ap.add_argument("--lr", type=float, default=1.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0)
-    ap.add_argument("--kernel-timing", type=int, default=1, help="hipEvent per-kernel timing in the timed region")
+    ap.add_argument("--kernel-timing", type=int, default=1,
+                    help="hipEvent timing in the roofline region (K steps after the timed region): 0 off, 1 the "
+                         "roofline kernels only (2048x2048 GEMMs; each event pair costs stream time), 2 every launch")
+    ap.add_argument("--breakdown-steps", type=int, default=20,
+                    help="extra steps after the timed region with every launch event-timed (kernels field)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -140,17 +145,32 @@ def main():
 
     trainer.replay(args.warmup)
     barrier()
-    check(lib().tnet_kernel_timing(int(bool(args.kernel_timing))), "kernel_timing")
-    barrier()
+    # timed region: K steps, no events on the stream (value, ms_per_step)
     t0 = time.perf_counter()
     trainer.replay(args.steps)
     barrier()
     dt = time.perf_counter() - t0
-    check(lib().tnet_kernel_timing(0), "kernel_timing")
+    # roofline region: the next K steps of the same workload with hipEvent pairs around the
+    # roofline kernels only (each pair adds ~3 us of stream time, so not inside the value region)
     import ctypes
     buf = ctypes.create_string_buffer(1 << 16)
-    check(lib().tnet_kernel_timing_report(buf, len(buf)), "kernel_timing_report")
-    kern = parse_kernel_report(buf.value.decode())
+    kern = {}
+    if args.kernel_timing:
+        check(lib().tnet_kernel_timing_filter(b":2048x2048" if args.kernel_timing == 1 else b""), "timing_filter")
+        check(lib().tnet_kernel_timing(1), "kernel_timing")
+        trainer.replay(args.steps)
+        check(lib().tnet_kernel_timing(0), "kernel_timing")
+        check(lib().tnet_kernel_timing_report(buf, len(buf)), "kernel_timing_report")
+        kern = parse_kernel_report(buf.value.decode())
+    # per-kernel breakdown (every launch event-timed) in extra steps outside the timed region
+    breakdown = {}
+    if args.breakdown_steps > 0:
+        check(lib().tnet_kernel_timing_filter(b""), "timing_filter")
+        check(lib().tnet_kernel_timing(1), "kernel_timing")
+        trainer.replay(args.breakdown_steps)
+        check(lib().tnet_kernel_timing(0), "kernel_timing")
+        check(lib().tnet_kernel_timing_report(buf, len(buf)), "kernel_timing_report")
+        breakdown = parse_kernel_report(buf.value.decode())
     if dist is not None:
         import torch
         t = torch.tensor([dt], dtype=torch.float64)
@@ -176,12 +196,14 @@ def main():
                 "algorithmic_bytes_per_launch": 4.0 * ((2 * B * 2048 + 2048 ** 2) + (3 * B * 2048 + 2048 ** 2) +
                                                        (2 * B * 2048 + 2 * 2048 ** 2)) / 3,  # fwd, bwd, upd
                 "launches": launches, "avg_launch_us": round(1000.0 * ms / launches, 2),
+                "timing": f"hipEvent pairs on the library stream around each roofline launch, {args.steps} steps "
+                          "right after the value region",
                 "flops_per_launch": flops / launches}
-    all_gemm_ms = sum(v["ms"] for k, v in kern.items() if k.startswith("gemm_"))
-    all_ms = sum(v["ms"] for v in kern.values())
+    all_gemm_ms = sum(v["ms"] for k, v in breakdown.items() if k.startswith("gemm_"))
+    all_ms = sum(v["ms"] for v in breakdown.values())
     kernels = {k: {"launches": v["launches"], "avg_us": round(1000 * v["ms"] / v["launches"], 2),
                    "rate": round(v["work"] / (v["ms"] * 1e-3) / (1e12 if k.startswith("gemm") else 1e9), 2),
-                   "rate_unit": "TFLOP/s" if k.startswith("gemm") else "GB/s"} for k, v in sorted(kern.items())}
+                   "rate_unit": "TFLOP/s" if k.startswith("gemm") else "GB/s"} for k, v in sorted(breakdown.items())}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -208,6 +230,9 @@ def main():
             "roofline": roof,
             "cpu_baseline": cpu,
             "kernels": kernels,
+            "kernels_note": f"every launch event-timed, {args.breakdown_steps} extra steps after the timed region "
+                            "(event pairs add stream time: the value region has none, the roofline region times "
+                            "only the roofline kernels)",
         }
         print(json.dumps(line), flush=True)
     if dist is not None:

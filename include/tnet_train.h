@@ -48,6 +48,8 @@ int tnet_profile_report(char* buf, int cap);
  * library stream).  The report lists "tag count total_ms total_work" lines (work = algorithmic
  * FLOPs for GEMMs, bytes for HBM-bound kernels) accumulated since the last report. */
 int tnet_kernel_timing(int on);
+/* time only launches whose tag contains `filter` ("" or NULL = all), e.g. ":2048x2048" */
+int tnet_kernel_timing_filter(const char* filter);
 int tnet_kernel_timing_report(char* buf, int cap);
 /* Device-side timing of the enqueued work: start/stop return elapsed ms between two marks. */
 int tnet_timer_start(void);

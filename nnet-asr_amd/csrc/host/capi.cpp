@@ -145,6 +145,10 @@ int tnet_kernel_timing(int on) {
   TRY_BEGIN CuDevice::Instantiate().KernelTiming(on != 0);
   TRY_END
 }
+int tnet_kernel_timing_filter(const char* filter) {
+  TRY_BEGIN CuDevice::Instantiate().KernelTimingFilter(filter ? filter : "");
+  TRY_END
+}
 int tnet_kernel_timing_report(char* buf, int cap) {
   TRY_BEGIN std::string s = CuDevice::Instantiate().KTCollect();
   if ((int)s.size() >= cap) Error("tnet_kernel_timing_report: buffer too small");

@@ -143,7 +143,7 @@ std::string CuDevice::KTCollect() {
 
 KTScope::KTScope(const std::string& tag, double work) : mTag(tag), mWork(work) {
   CuDevice& d = CuDevice::Instantiate();
-  if (!d.KernelTiming()) return;
+  if (!d.KernelTimed(tag)) return;
   mA = d.KTEvent();
   TNET_HIP_CALL(hipEventRecord(mA, d.Stream()));
 }

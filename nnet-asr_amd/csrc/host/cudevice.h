@@ -42,6 +42,12 @@ class CuDevice {
   // ---- per-kernel device timing (hipEvent pairs around launches; off by default)
   void KernelTiming(bool on) { mKTOn = on; }
   bool KernelTiming() const { return mKTOn; }
+  /// time only the launches whose tag contains `filter` (empty = all): each event pair costs
+  /// a few microseconds of stream time, so a benchmark times only the kernel it reports
+  void KernelTimingFilter(const std::string& filter) { mKTFilter = filter; }
+  bool KernelTimed(const std::string& tag) const {
+    return mKTOn && (mKTFilter.empty() || tag.find(mKTFilter) != std::string::npos);
+  }
   void KTRecord(const std::string& tag, double work, hipEvent_t a, hipEvent_t b);
   hipEvent_t KTEvent();
   /// sync, aggregate "tag count total_ms total_work" lines, reset
@@ -72,6 +78,7 @@ class CuDevice {
   void* mWs = nullptr;
   size_t mWsBytes = 0;
   bool mKTOn = false;
+  std::string mKTFilter;
   struct KTRec {
     std::string tag;
     double work;

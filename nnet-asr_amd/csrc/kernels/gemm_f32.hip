@@ -484,9 +484,15 @@ __device__ __forceinline__ void epi_vec4(const GemmP& p, int row, int col, f32x4
 //     conflict-free b128 and, for an n-contiguous B, the epilogue stores 4 consecutive columns
 //     per lane as one 16-B store.
 // =============================================================================================
-template <int BM, int BN, int BK, int WM, int WN, int S, bool A_KC, bool B_KC, int EPI>
-__global__ __launch_bounds__(WM * WN * 64) void gemm16_kernel(const GemmP p) {
+//   * SP = 1 (S >= 3): the G LDS-DMA pieces of tile t+S-1 are issued spread over tile t's chunks
+//     (about G/KCH per chunk, between the fragment reads and the chunk's MFMAs) instead of all at
+//     the tile seam, and the MFMA block runs at s_setprio 1 (an 8-wave workgroup's partner wave
+//     then fills the other wave's seams).
+template <int BM, int BN, int BK, int WM, int WN, int S, int SP, bool A_KC, bool B_KC, int EPI>
+__global__ __launch_bounds__(WM * WN * 64) __attribute__((amdgpu_waves_per_eu((WM * WN + 3) / 4, (WM * WN + 3) / 4)))
+void gemm16_kernel(const GemmP p) {
   constexpr int NT = WM * WN * 64, NW = WM * WN;
+  static_assert(SP == 0 || S >= 3, "spread DMA needs a 3-slot ring");
   constexpr int WTM = BM / WM, WTN = BN / WN;  // wave tile
   constexpr int TM = WTM / 16, TN = WTN / 16;
   static_assert(WTM % 16 == 0 && WTN % 16 == 0, "16x16 tiles per wave");
@@ -510,20 +516,23 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm16_kernel(const GemmP p) {
   const int gsz = min(nbm - first_m, grp);
   const int bm = (first_m + (L % per_group) % gsz) * BM, bn = ((L % per_group) / gsz) * BN;
 
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  // wave index in an SGPR: every LDS-DMA destination (M0) is then scalar arithmetic
+  const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm0 = (wid / WN) * WTM, wn0 = (wid % WN) * WTN;
   const int lg = lane >> 4, li = lane & 15;
 
-  long srcA[GA], srcB[GB];
+  // per-lane BYTE offsets from the tile's base (32-bit: the launcher checks the operand extent), so
+  // each DMA is global_load_lds with a scalar base (advanced per tile) + one VGPR offset
+  unsigned srcA[GA], srcB[GB];
 #pragma unroll
   for (int g = 0; g < GA; ++g) {
     const int u = (g * NW + wid) * 64 + lane;
     if (A_KC) {
       const int r = u / CH, j = u % CH;
-      srcA[g] = (long)min(bm + r, M - 1) * p.lda + 4 * (j ^ swz<BK>(r));
+      srcA[g] = 4u * (unsigned)(min(bm + r, M - 1) * p.lda + 4 * (j ^ swz<BK>(r)));
     } else {
       const int k = u / (BM / 4), c = (u % (BM / 4)) * 4;
-      srcA[g] = (long)k * p.lda + (bm + c < M ? bm + c : 0);
+      srcA[g] = 4u * (unsigned)(k * p.lda + (bm + c < M ? bm + c : 0));
     }
   }
 #pragma unroll
@@ -531,24 +540,39 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm16_kernel(const GemmP p) {
     const int u = (g * NW + wid) * 64 + lane;
     if (B_KC) {
       const int r = u / CH, j = u % CH;
-      srcB[g] = (long)min(bn + r, N - 1) * p.ldb + 4 * (j ^ swz<BK>(r));
+      srcB[g] = 4u * (unsigned)(min(bn + r, N - 1) * p.ldb + 4 * (j ^ swz<BK>(r)));
     } else {
       const int k = u / (BN / 4), c = (u % (BN / 4)) * 4;
-      srcB[g] = (long)k * p.ldb + (bn + c < N ? bn + c : 0);
+      srcB[g] = 4u * (unsigned)(k * p.ldb + (bn + c < N ? bn + c : 0));
     }
   }
-  auto issue = [&](int t) {
-    float* st = smem + (t % S) * ST_SZ;
-    const long ka = A_KC ? (long)t * BK : (long)t * BK * p.lda;
-    const long kb = B_KC ? (long)t * BK : (long)t * BK * p.ldb;
+  // DMA of k-tile t into ring slot sl (t may be a clamped repeat of the last tile: see the loop)
+  auto issue = [&](int t, int sl) {
+    float* st = smem + sl * ST_SZ;
+    const char* ab = (const char*)(p.A + (A_KC ? (long)t * BK : (long)t * BK * p.lda));
+    const char* bb = (const char*)(p.B + (B_KC ? (long)t * BK : (long)t * BK * p.ldb));
 #pragma unroll
     for (int g = 0; g < GA; ++g)
-      __builtin_amdgcn_global_load_lds((const void*)(p.A + ka + srcA[g]), (void*)(st + (g * NW + wid) * 256), 16, 0,
-                                       0);
+      __builtin_amdgcn_global_load_lds((const void*)(ab + srcA[g]), (void*)(st + (g * NW + wid) * 256), 16, 0, 0);
 #pragma unroll
     for (int g = 0; g < GB; ++g)
-      __builtin_amdgcn_global_load_lds((const void*)(p.B + kb + srcB[g]), (void*)(st + A_SZ + (g * NW + wid) * 256),
-                                       16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(bb + srcB[g]), (void*)(st + A_SZ + (g * NW + wid) * 256), 16, 0,
+                                       0);
+  };
+  // pieces [g0, g1) of tile t (piece g < GA: A piece g, else B piece g - GA)
+  constexpr int PPC = (G + KCH - 1) / KCH;
+  auto issue_part = [&](int t, int sl, int c) {
+    float* st = smem + sl * ST_SZ;
+    const char* ab = (const char*)(p.A + (A_KC ? (long)t * BK : (long)t * BK * p.lda));
+    const char* bb = (const char*)(p.B + (B_KC ? (long)t * BK : (long)t * BK * p.ldb));
+#pragma unroll
+    for (int g = c * PPC; g < (c + 1) * PPC && g < G; ++g) {
+      if (g < GA)
+        __builtin_amdgcn_global_load_lds((const void*)(ab + srcA[g]), (void*)(st + (g * NW + wid) * 256), 16, 0, 0);
+      else
+        __builtin_amdgcn_global_load_lds((const void*)(bb + srcB[g - GA]),
+                                         (void*)(st + A_SZ + ((g - GA) * NW + wid) * 256), 16, 0, 0);
+    }
   };
 
   f32x4 acc[TM][TN];
@@ -607,45 +631,140 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm16_kernel(const GemmP p) {
         for (int b = 0; b < TN; ++b)
           acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[buf][a][s], bv[buf][b][s], acc[a][b], 0, 0, 0);
   };
-  // diagnostics only (wrong results): bit 0 no global loads in the k-loop, bit 1 no barriers
-  const bool noload = (p.diag_noload & 1) != 0, nobar = (p.diag_noload & 2) != 0;
   auto barrier = [&]() {
     __builtin_amdgcn_sched_barrier(0);
-    if (!nobar) __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
   };
-  auto slot = [&](int t) { return smem + ((noload ? 0 : t) % S) * ST_SZ; };
+  constexpr int NRD = TM + TN;      // ds_read_b128 per chunk (both operand layouts)
+  constexpr int NMF = 4 * TM * TN;  // MFMAs per chunk
+  static_assert(NMF >= NRD + (SP ? PPC : G), "interleave pattern");
+  static_assert(PPC * KCH >= G, "pieces per chunk");
+  // vmcnt at a seam: everything younger than tile t+1 may stay in flight -- tiles t+2..t+S-1 without
+  // SP; with SP tiles t+2..t+S-2 plus the pieces of tile t+S-1 issued in the chunks before the seam
+  // (the seam chunk issues its share after the wait)
+  constexpr int SEAM_VM = SP ? (S - 3) * G + (G < (KCH - 1) * PPC ? G : (KCH - 1) * PPC) : (S - 2) * G;
 
+  // Branch-free main loop: every tile ends with the seam (wait for tile t+1, barrier, first
+  // fragments of t+1) and every tile issues exactly G pieces, so the counted vmcnt is the constant
+  // (S-2)*G.  Tiles past the end are re-loads of the last tile into a slot no later tile reads
+  // (harmless); the fragments read at the final seam are discarded.  Straight-line code lets the
+  // compiler count lgkmcnt exactly instead of draining at every block join.
   const int nfull = K / BK;
-#pragma unroll
-  for (int t = 0; t < S - 1; ++t)
-    if (t < nfull) issue(t);
+  const int tlast = max(nfull - 1, 0);
   if (nfull > 0) {
-    wait_vmcnt_le<3 * G>(min(S - 2, nfull - 1) * G);
+#pragma unroll
+    for (int t = 0; t < S - 1; ++t) issue(min(t, tlast), t);
+    wait_vmcnt<(S - 2) * G>();
     barrier();  // tile 0 landed in every wave's pieces
-    if (S - 1 < nfull && !noload) issue(S - 1);
-    read_frags(slot(0), 0, 0);
+    if (!SP) issue(min(S - 1, tlast), S - 1);
+    read_frags(smem, 0, 0);
   }
+  // one fragment read (r < TM: operand A, else B) of chunk c of the slot at st into buffer buf
+  auto read_one = [&](const float* st, int c, int buf, int r) {
+    const float* As = st;
+    const float* Bs = st + A_SZ;
+    if (r < TM) {
+      if (A_KC) {
+        const int a = r, row = wm0 + 16 * a + li;
+        const f32x4 x = *reinterpret_cast<const f32x4*>(As + row * BK + 4 * ((4 * c + lg) ^ swz<BK>(row)));
+#pragma unroll
+        for (int s2 = 0; s2 < 4; ++s2) av[buf][a][s2] = x[s2];
+      } else {
+        const int s2 = r % 4, q = r / 4;
+        const f32x4 x = *reinterpret_cast<const f32x4*>(As + (16 * c + 4 * lg + s2) * BM + wm0 + 64 * q + 4 * li);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) av[buf][4 * q + e][s2] = x[e];
+      }
+    } else {
+      const int rb = r - TM;
+      if (B_KC) {
+        const int b = rb, col = wn0 + 16 * b + li;
+        const f32x4 x = *reinterpret_cast<const f32x4*>(Bs + col * BK + 4 * ((4 * c + lg) ^ swz<BK>(col)));
+#pragma unroll
+        for (int s2 = 0; s2 < 4; ++s2) bv[buf][b][s2] = x[s2];
+      } else {
+        const int s2 = rb % 4, q = rb / 4;
+        const f32x4 x = *reinterpret_cast<const f32x4*>(Bs + (16 * c + 4 * lg + s2) * BN + wn0 + 64 * q + 4 * li);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) bv[buf][4 * q + e][s2] = x[e];
+      }
+    }
+  };
+  // one DMA piece g of tile t into slot sl
+  auto issue_one = [&](int t, int sl, int g) {
+    float* st = smem + sl * ST_SZ;
+    if (g < GA) {
+      const char* ab = (const char*)(p.A + (A_KC ? (long)t * BK : (long)t * BK * p.lda));
+      __builtin_amdgcn_global_load_lds((const void*)(ab + srcA[g]), (void*)(st + (g * NW + wid) * 256), 16, 0, 0);
+    } else {
+      const char* bb = (const char*)(p.B + (B_KC ? (long)t * BK : (long)t * BK * p.ldb));
+      __builtin_amdgcn_global_load_lds((const void*)(bb + srcB[g - GA]),
+                                       (void*)(st + A_SZ + ((g - GA) * NW + wid) * 256), 16, 0, 0);
+    }
+  };
+
+  // Each chunk is written out as its MFMA sequence with one filler instruction pinned after each
+  // of the first MFMAs (sched_barrier fences): first the NRD fragment reads of the next chunk,
+  // then the chunk's DMA pieces (SP: PPC of tile t+S-1; seam without SP: all G of tile t+S).
+  // Left to itself the scheduler sinks every read to just before its first use and waits
+  // lgkmcnt(0) there, and bunches the DMA pieces behind the barrier with the MFMA pipe idle.
+  int sl = 0;  // slot of tile t
   for (int t = 0; t < nfull; ++t) {
-    const float* st = slot(t);
+    const float* st = smem + sl * ST_SZ;
+    const int sl1 = sl + 1 == S ? 0 : sl + 1;          // slot of tile t+1
+    const int slp = sl == 0 ? S - 1 : sl - 1;          // slot of tile t+S-1 (= t-1, released at the last seam)
+    const int tsp = min(t + S - 1, tlast), tns = min(t + S, tlast);
 #pragma unroll
     for (int c = 0; c < KCH; ++c) {
       const int buf = c & 1;  // KCH is even: chunk 0 of every tile uses buffer 0
-      if (c + 1 < KCH) {
-        read_frags(st, c + 1, buf ^ 1);
-      } else if (t + 1 < nfull) {
-        // hand over to tile t+1 under the last chunk's MFMAs (see gemm_f32_glds_kernel)
+      const bool seam = c + 1 == KCH;
+      const float* rst = seam ? smem + sl1 * ST_SZ : st;
+      const int rc = seam ? 0 : c + 1;
+      if (seam) {
+        // hand over to tile t+1: own reads of tile t retired, tile t+1 landed, everyone past
+        __builtin_amdgcn_sched_barrier(0);
         __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
-        wait_vmcnt_le<3 * G>(min(S - 2, nfull - 2 - t) * G);
+        wait_vmcnt<SEAM_VM>();
         barrier();
-        if (t + S < nfull && !noload) issue(t + S);
-        read_frags(slot(t + 1), 0, buf ^ 1);
       }
-      mfmas(buf);
+      if (SP) __builtin_amdgcn_s_setprio(1);
+      constexpr int NP = SP ? PPC : G;
+      int idx = 0;
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int a = 0; a < TM; ++a)
+#pragma unroll
+          for (int b = 0; b < TN; ++b) {
+            acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[buf][a][s], bv[buf][b][s], acc[a][b], 0, 0, 0);
+            if (idx < NRD) {
+              __builtin_amdgcn_sched_barrier(0);
+              read_one(rst, rc, buf ^ 1, idx);
+              __builtin_amdgcn_sched_barrier(0);
+            } else if (idx < NRD + NP) {
+              const int g = SP ? c * PPC + (idx - NRD) : idx - NRD;
+              if (SP && g < G) {
+                __builtin_amdgcn_sched_barrier(0);
+                issue_one(tsp, slp, g);
+                __builtin_amdgcn_sched_barrier(0);
+              } else if (!SP && seam) {
+                __builtin_amdgcn_sched_barrier(0);
+                issue_one(tns, sl, g);
+                __builtin_amdgcn_sched_barrier(0);
+              }
+            }
+            ++idx;
+          }
+      if (SP) __builtin_amdgcn_s_setprio(0);
     }
+    sl = sl1;
   }
+  wait_vmcnt<0>();  // repeat loads of the last tile still land in LDS
   if (K % BK) {
-    // masked tail k-tile through registers, same images, in slot nfull % S
+    // masked tail k-tile through registers, same images, in slot nfull % S (the final seam read
+    // it: every wave's reads retire before the barrier)
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
     __builtin_amdgcn_s_barrier();
     float* st = smem + (nfull % S) * ST_SZ;
     const int k0 = nfull * BK;
@@ -718,7 +837,8 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm16_kernel(const GemmP p) {
 // host-side dispatch
 // ---------------------------------------------------------------------------------------------
 // name: g<BM>x<BN>k<BK>s<S>w<waves>[i]: 32x32x2 kernel (waves laid out WMxWN; i = DMA pieces
-//       interleaved); m<BM>x<BN>k<BK>s<S>[w<WM><WN>]: 16x16x4 kernel (default 2x2 waves)
+//       interleaved); m<BM>x<BN>k<BK>s<S>[w<WM><WN>][p]: 16x16x4 kernel (default 2x2 waves; p = DMA
+//       pieces spread over the chunks + MFMA at setprio 1)
 #define TNET_GEMM_CFGS(X)                                 \
   X(g64x64k32s4w4, 0, 64, 64, 32, 2, 2, 4, 0)            \
   X(g64x64k32s4w4i, 0, 64, 64, 32, 2, 2, 4, 1)           \
@@ -735,7 +855,20 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm16_kernel(const GemmP p) {
   X(m64x128k32s4w12, 1, 64, 128, 32, 1, 2, 4, 0)         \
   X(m64x128k32s3, 1, 64, 128, 32, 2, 2, 3, 0)            \
   X(m64x128k32s2, 1, 64, 128, 32, 2, 2, 2, 0)            \
-  X(m64x128k64s2, 1, 64, 128, 64, 2, 2, 2, 0)
+  X(m64x128k64s2, 1, 64, 128, 64, 2, 2, 2, 0)           \
+  X(m64x128k64s2w42, 1, 64, 128, 64, 4, 2, 2, 0)         \
+  X(m64x128k32s3w42, 1, 64, 128, 32, 4, 2, 3, 0)         \
+  X(m64x128k32s4w42, 1, 64, 128, 32, 4, 2, 4, 0)         \
+  X(m64x64k32s4w21, 1, 64, 64, 32, 2, 1, 4, 0)           \
+  X(m64x64k64s2w21, 1, 64, 64, 64, 2, 1, 2, 0)           \
+  X(m64x128k32s2w12, 1, 64, 128, 32, 1, 2, 2, 0)         \
+  X(m64x128k32s3w12, 1, 64, 128, 32, 1, 2, 3, 0)         \
+  X(m64x128k64s3p, 1, 64, 128, 64, 2, 2, 3, 1)           \
+  X(m64x128k64s3w42p, 1, 64, 128, 64, 4, 2, 3, 1)        \
+  X(m64x128k32s4p, 1, 64, 128, 32, 2, 2, 4, 1)           \
+  X(m64x128k32s4w42p, 1, 64, 128, 32, 4, 2, 4, 1)        \
+  X(m128x128k32s3p, 1, 128, 128, 32, 2, 2, 3, 1)         \
+  X(m128x128k32s4p, 1, 128, 128, 32, 2, 2, 4, 1)
 
 enum GemmCfg {
 #define X(name, ...) CFG_##name,
@@ -772,8 +905,12 @@ static bool launch_cfg(const GemmP& p, hipStream_t st) {
     return true;
   } else {
     constexpr int TM = BM / WM / 16, TN = BN / WN / 16;
+    // the 16x16 kernel addresses a k-tile with 32-bit byte offsets from a per-tile base
+    const long extA = A_KC ? (long)p.M * p.lda : (long)BK * p.lda + p.M;
+    const long extB = B_KC ? (long)p.N * p.ldb : (long)BK * p.ldb + p.N;
+    if (4 * extA >= (1L << 32) || 4 * extB >= (1L << 32)) return false;
     if constexpr ((A_KC || TM % 4 == 0) && (B_KC || TN % 4 == 0)) {
-      gemm16_kernel<BM, BN, BK, WM, WN, S, A_KC, B_KC, EPI><<<tiles, WM * WN * 64, 0, st>>>(p);
+      gemm16_kernel<BM, BN, BK, WM, WN, S, IL, A_KC, B_KC, EPI><<<tiles, WM * WN * 64, 0, st>>>(p);
       return true;
     } else {
       return false;  // this tile cannot hold the operand layout

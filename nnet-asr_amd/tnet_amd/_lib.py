@@ -84,6 +84,7 @@ _SIGS = {
     "tnet_set_profile": (i32, [i32]),
     "tnet_profile_report": (i32, [C.c_char_p, i32]),
     "tnet_kernel_timing": (i32, [i32]),
+    "tnet_kernel_timing_filter": (i32, [C.c_char_p]),
     "tnet_kernel_timing_report": (i32, [C.c_char_p, i32]),
     "tnet_timer_start": (i32, []),
     "tnet_timer_stop": (i32, [C.POINTER(f32)]),
