@@ -162,6 +162,23 @@ int tnet_affine_bwd(const float* E, TnetMatrixDim dE, const float* W, TnetMatrix
 int tnet_affine_update(const float* X, TnetMatrixDim dX, const float* E, TnetMatrixDim dE, float* W,
                        TnetMatrixDim dW, float* corrW, int strideCorr, float scale, float mmt, float l2,
                        void* stream);
+/* ---- bias gradient fused into the GEMMs (removes the AddColSum pass over E and its two launches)
+ * The error E_l of a hidden layer is produced by the backward GEMM of the layer above; that GEMM also
+ * writes the column sums of E_l per 32-row slab.  The update GEMM of layer l then applies the bias SGD
+ * of tnet_bias_update from those slab sums (fp32 within a slab, fp64 across slabs) in its prologue. */
+/* number of 32-row slabs of a [rows x n] error matrix (rows of the colpart buffer) */
+int tnet_colsum_slabs(int rows);
+/* tnet_affine_bwd(..., dsig=1) plus colpart[s * ldcolpart + c] = sum_{r in slab s} Eo[r][c]
+ * (cuBiasedLinearity.cc:21-25 + cuActivation.cc:19-22 + the AddColSum half of cuBiasedLinearity.cc:56). */
+int tnet_affine_bwd_colsum(const float* E, TnetMatrixDim dE, const float* W, TnetMatrixDim dW,
+                           const float* Ybelow, int strideYbelow, float* Eo, TnetMatrixDim dEo, float* colpart,
+                           int ldcolpart, void* stream);
+/* tnet_affine_update + tnet_bias_update(E, b, corr_b, scale, mmt) in one launch, colsum(E) taken from
+ * colpart (written for E by tnet_affine_bwd_colsum); corr_b is required when mmt != 0
+ * (cuBiasedLinearity.cc:46-64). */
+int tnet_affine_update_bias(const float* X, TnetMatrixDim dX, const float* E, TnetMatrixDim dE, float* W,
+                            TnetMatrixDim dW, float* corrW, int strideCorr, float scale, float mmt, float l2,
+                            const float* colpart, int ldcolpart, float* b, float* corr_b, void* stream);
 /* G = X^T E into a gradient buffer (data-parallel path: all-reduced before tnet_sgd_update). */
 int tnet_affine_grad(const float* X, TnetMatrixDim dX, const float* E, TnetMatrixDim dE, float* G,
                      TnetMatrixDim dG, void* stream);

@@ -120,6 +120,21 @@ void CuBiasedLinearity::UpdateFrom(const CuMatrix<BaseFloat>& X, const CuMatrix<
                                     (int)mLinearityCorrection.Stride(), scale, mMomentum, l2, S));
 }
 
+void CuBiasedLinearity::UpdateFromColsum(const CuMatrix<BaseFloat>& X, const CuMatrix<BaseFloat>& E,
+                                         const CuMatrix<BaseFloat>& colpart) {
+  CuProfileScope p("CuBiasedLinearity::Update");
+  float scale, l2;
+  UpdateConstants(X.Rows(), &scale, &l2);
+  const bool mmt = mMomentum != 0.0f;
+  KTScope kt("gemm_upd:" + std::to_string(GetNInputs()) + "x" + std::to_string(GetNOutputs()),
+             2.0 * X.Rows() * GetNInputs() * GetNOutputs());
+  TNET_SAFE_CALL(tnet_affine_update_bias(X.pCUData(), X.Dim(), E.pCUData(), E.Dim(), mLinearity.pCUData(),
+                                         mLinearity.Dim(), mmt ? mLinearityCorrection.pCUData() : nullptr,
+                                         (int)mLinearityCorrection.Stride(), scale, mMomentum, l2, colpart.pCUData(),
+                                         (int)colpart.Stride(), mBias.pCUData(),
+                                         mmt ? mBiasCorrection.pCUData() : nullptr, S));
+}
+
 void CuBiasedLinearity::Update() { UpdateFrom(GetInput(), GetErrorInput()); }
 
 void CuBiasedLinearity::ComputeGradient() {

@@ -239,7 +239,11 @@ void CuNetwork::TrainBunch(const CuMatrix<BaseFloat>& X, const CuVector<int>& la
   const int nl = (int)mNetComponents.size() / 2;
   if (mErr.size() != (size_t)nl) {
     mErr.clear();
-    for (int l = 0; l < nl; l++) mErr.emplace_back(new CuMatrix<BaseFloat>());
+    mColPart.clear();
+    for (int l = 0; l < nl; l++) {
+      mErr.emplace_back(new CuMatrix<BaseFloat>());
+      mColPart.emplace_back(new CuMatrix<BaseFloat>());
+    }
   }
   mNetComponents.front()->SetInput(X);
 
@@ -282,18 +286,35 @@ void CuNetwork::TrainBunch(const CuMatrix<BaseFloat>& X, const CuVector<int>& la
 
   // ---- backward + update, top to bottom (error uses the pre-update weights of the layer)
   const CuMatrix<BaseFloat>* err = &mGlobErr;
+  bool err_colsum = false;  // slab column sums of *err are in mColPart[l] (bias gradient fused, no exchange)
   for (int l = nl - 1; l >= 0; l--) {
     auto* lin = static_cast<CuBiasedLinearity*>(mNetComponents[2 * l]);
     const bool stopper = (lin == mpPropagErrorStopper);
     CuMatrix<BaseFloat>* eo = nullptr;
+    bool eo_colsum = false;
     if (!stopper && l > 0) {
       eo = mErr[l].get();
       eo->Init(rows, lin->GetNInputs());
       KTScope kt("gemm_bwd:" + std::to_string(lin->GetNInputs()) + "x" + std::to_string(lin->GetNOutputs()),
                  2.0 * rows * lin->GetNInputs() * lin->GetNOutputs());
-      // E_l = (E_{l+1} W_l^T) .* y_l (1 - y_l)   (backprop through <biasedlinearity> and the <sigmoid> below)
-      TNET_SAFE_CALL(tnet_affine_bwd(err->pCUData(), err->Dim(), lin->Linearity().pCUData(), lin->Linearity().Dim(),
-                                     acts[l]->pCUData(), (int)acts[l]->Stride(), eo->pCUData(), eo->Dim(), 1, S));
+      // E_l = (E_{l+1} W_l^T) .* y_l (1 - y_l)   (backprop through <biasedlinearity> and the <sigmoid> below);
+      // when the layer below is trained here, the same launch writes the bias gradient of E_l as slab sums
+      auto* below = static_cast<CuBiasedLinearity*>(mNetComponents[2 * (l - 1)]);
+      if (!exchange && below->LearnRate() > 0.0f) {
+        CuMatrix<BaseFloat>& cp = *mColPart[l - 1];
+        cp.Init(tnet_colsum_slabs((int)rows), lin->GetNInputs());
+        const int st = tnet_affine_bwd_colsum(err->pCUData(), err->Dim(), lin->Linearity().pCUData(),
+                                              lin->Linearity().Dim(), acts[l]->pCUData(), (int)acts[l]->Stride(),
+                                              eo->pCUData(), eo->Dim(), cp.pCUData(), (int)cp.Stride(), S);
+        if (st != TNET_ERR_UNSUPPORTED) {
+          TNET_SAFE_CALL(st);
+          eo_colsum = true;
+        }
+      }
+      if (!eo_colsum)
+        TNET_SAFE_CALL(tnet_affine_bwd(err->pCUData(), err->Dim(), lin->Linearity().pCUData(),
+                                       lin->Linearity().Dim(), acts[l]->pCUData(), (int)acts[l]->Stride(),
+                                       eo->pCUData(), eo->Dim(), 1, S));
     }
     if (lin->LearnRate() > 0.0f) {
       if (exchange) {
@@ -301,12 +322,15 @@ void CuNetwork::TrainBunch(const CuMatrix<BaseFloat>& X, const CuVector<int>& la
         lin->SetErrorInput(*err);
         lin->ComputeGradient();
         exchange->Submit(*lin);
+      } else if (err_colsum) {
+        lin->UpdateFromColsum(*acts[l], *err, *mColPart[l]);
       } else {
         lin->UpdateFrom(*acts[l], *err);
       }
     }
     if (stopper || l == 0) break;
     err = eo;
+    err_colsum = eo_colsum;
   }
   if (exchange) {
     exchange->WaitAll();

@@ -94,6 +94,7 @@ class CuNetwork {
   // fused-path buffers: activations of sigmoid layers are the components' own outputs;
   // errors live here (one per affine layer input)
   std::vector<std::unique_ptr<CuMatrix<BaseFloat>>> mErr;
+  std::vector<std::unique_ptr<CuMatrix<BaseFloat>>> mColPart;  // per layer: 32-row slab column sums of its error
   CuMatrix<BaseFloat> mGlobErr;
 };
 

@@ -34,7 +34,14 @@ namespace tnetk {
 // stacked statistics with a minus sign); EPI_RBM is the CD-1 weight update of CuRbm::RbmUpdate
 // (cuRbm.cc:133-174): c = mmt*corr + scale*acc + l2*W ; corr = c ; W += c
 enum { EPI_STORE = 0, EPI_BIAS = 1, EPI_BIAS_SIG = 2, EPI_DSIG = 3, EPI_SGD = 4, EPI_BIAS_NSIG = 5,
-       EPI_BIAS_NEG = 6, EPI_RBM = 7 };
+       EPI_BIAS_NEG = 6, EPI_RBM = 7,
+       // fused bias gradient (16x16 kernel): EPI_DSIG_CS = EPI_DSIG + per-32-row-slab column sums of the
+       // output (the bias gradient of the layer below); EPI_SGD_B = EPI_SGD + that layer's bias SGD from
+       // the slab sums, done by the first tile-row's workgroups in the prologue
+       EPI_DSIG_CS = 8, EPI_SGD_B = 9 };
+constexpr int kColsumSlabRows = 32;
+// base epilogue of a fused one
+constexpr int epi_base(int e) { return e == EPI_DSIG_CS ? EPI_DSIG : e == EPI_SGD_B ? EPI_SGD : e; }
 
 struct GemmP {
   int M, N, K;
@@ -46,6 +53,10 @@ struct GemmP {
   const float* aux; long ldaux; // EPI_DSIG: y of the layer below [M x N]
   float* corr; long ldcorr;     // EPI_SGD: momentum buffer (nullable)
   float scale, mmt, l2;         // EPI_SGD
+  float* cpart; long ldcpart;   // EPI_DSIG_CS: [cdiv(M,32)][N] column sums of the output per 32-row slab
+  const float* bpart; long ldbpart; int bslabs;  // EPI_SGD_B: bias-gradient slab sums [bslabs][N]
+  float* bvec; float* bcorr;    // EPI_SGD_B: bias [N] and its momentum buffer (nullable)
+  float bscale, bmmt;           // EPI_SGD_B
   int group;                    // tile-rows per group of the blockIdx -> tile order
   int diag_noload;              // diagnostics only: skip the k-loop's global loads (wrong results)
 };
@@ -106,6 +117,42 @@ __device__ __forceinline__ void epilogue(const GemmP& p, f32x16 (&acc)[TM][TN], 
   }
 }
 
+
+// ---- EPI_SGD_B: the workgroups of the first tile-row (bm == 0) also update the bias of their BN
+// columns.  g = the fp32 slab sums added in fp64, in slab order (the reference accumulates the column
+// sum in double, _add_col_sum cukernels.cu:147-164); then corr = g + mmt*corr ; b += scale*corr
+// (cuBiasedLinearity.cc:46-64).  The first 32 slab sums, b and corr are loaded into registers right
+// after the prologue (bias_pre_load) so their latency hides under the main loop; the sum and the
+// stores happen at the epilogue (bias_pre_finish).  Column c of the WG is thread c (BN <= NT).
+constexpr int kBiasPreSlabs = 32;
+struct BiasPre {
+  float v[kBiasPreSlabs];
+  float b, q;
+};
+template <int BN>
+__device__ __forceinline__ void bias_pre_load(const GemmP& p, int bn, BiasPre& bp) {
+  const int col = bn + (int)threadIdx.x;
+  if ((int)threadIdx.x >= BN || col >= p.N) return;
+#pragma unroll
+  for (int k = 0; k < kBiasPreSlabs; ++k) bp.v[k] = k < p.bslabs ? p.bpart[(long)k * p.ldbpart + col] : 0.f;
+  bp.b = p.bvec[col];
+  bp.q = p.bcorr ? p.bcorr[col] : 0.f;
+}
+template <int BN>
+__device__ __forceinline__ void bias_pre_finish(const GemmP& p, int bn, const BiasPre& bp) {
+  const int col = bn + (int)threadIdx.x;
+  if ((int)threadIdx.x >= BN || col >= p.N) return;
+  double s = 0.0;
+#pragma unroll
+  for (int k = 0; k < kBiasPreSlabs; ++k) s += (double)bp.v[k];
+  for (int k = kBiasPreSlabs; k < p.bslabs; ++k) s += (double)p.bpart[(long)k * p.ldbpart + col];
+  float g = (float)s;
+  if (p.bcorr) {
+    g = g + p.bmmt * bp.q;
+    p.bcorr[col] = g;
+  }
+  p.bvec[col] = bp.b + p.bscale * g;
+}
 
 // =============================================================================================
 // LDS-DMA pipelined GEMM.  BMxBN workgroup tile, BK k-depth per ring slot, WMxWN waves each
@@ -295,6 +342,11 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_f32_glds_kernel(const GemmP
   if (IL && S - 1 < nfull)
 #pragma unroll
     for (int g = 0; g < GH; ++g) issue_piece(S - 1, g);
+  static_assert(EPI != EPI_DSIG_CS, "column sums: 16x16 kernel only");
+  static_assert(EPI != EPI_SGD_B || BN <= NT, "one thread per bias column");
+  BiasPre bpre;
+  if constexpr (EPI == EPI_SGD_B)
+    if (bm == 0) bias_pre_load<BN>(p, bn, bpre);
   if (nfull > 0) {
     // tile 0 must land; younger DMAs in flight: full tiles 1..S-2 (+ GH pieces of tile S-1)
     int younger = (min(S - 2, nfull - 1)) * G + ((IL && S - 1 < nfull) ? GH : 0);
@@ -379,98 +431,33 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_f32_glds_kernel(const GemmP
       mfmas(kc % NB);
     }
   }
-  epilogue<TM, TN, EPI>(p, acc, bm, bn, wm0, wn0, li, lh);
+  if constexpr (EPI == EPI_SGD_B)
+    if (bm == 0) bias_pre_finish<BN>(p, bn, bpre);
+  epilogue<TM, TN, epi_base(EPI)>(p, acc, bm, bn, wm0, wn0, li, lh);
 }
 
 
-// ---- element / 4-vector epilogues shared by the 16x16 kernel
-template <int EPI>
-__device__ __forceinline__ void epi_elem(const GemmP& p, int row, int col, float v) {
-  float* cp = p.C + (long)row * p.ldc + col;
-  if (EPI == EPI_STORE) {
-    *cp = (p.beta == 0.f) ? p.alpha * v : p.alpha * v + p.beta * *cp;
-  } else if (EPI == EPI_BIAS) {
-    *cp = v + p.bias[col];
-  } else if (EPI == EPI_BIAS_SIG) {
-    *cp = sigmoidf_ref(v + p.bias[col]);
-  } else if (EPI == EPI_BIAS_NSIG) {
-    *cp = -sigmoidf_ref(v + p.bias[col]);
-  } else if (EPI == EPI_BIAS_NEG) {
-    *cp = -(v + p.bias[col]);
-  } else if (EPI == EPI_DSIG) {
-    const float y = p.aux[(long)row * p.ldaux + col];
-    *cp = y * (1.f - y) * v;
-  } else if (EPI == EPI_RBM) {
-    float* qp = p.corr + (long)row * p.ldcorr + col;
-    const float w = *cp;
-    const float c = p.mmt * *qp + p.scale * v + p.l2 * w;
-    *qp = c;
-    *cp = w + c;
-  } else {  // EPI_SGD
-    float c = v;
-    if (p.corr) {
-      float* qp = p.corr + (long)row * p.ldcorr + col;
-      c = v + p.mmt * *qp;
-      *qp = c;
-    }
-    float w = *cp;
-    w = w + p.scale * c;
-    w = w + p.l2 * w;
-    *cp = w;
-  }
-}
-
-// 4 consecutive columns col..col+3 (col % 4 == 0, every leading dimension % 4 == 0)
-template <int EPI>
-__device__ __forceinline__ void epi_vec4(const GemmP& p, int row, int col, f32x4 v) {
-  f32x4* cp = reinterpret_cast<f32x4*>(p.C + (long)row * p.ldc + col);
-  if (EPI == EPI_STORE) {
-    if (p.beta == 0.f) {
-      *cp = p.alpha * v;
-    } else {
-      *cp = p.alpha * v + p.beta * *cp;
-    }
-  } else if (EPI == EPI_BIAS || EPI == EPI_BIAS_SIG || EPI == EPI_BIAS_NSIG || EPI == EPI_BIAS_NEG) {
-    f32x4 o;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const float a = v[e] + p.bias[col + e];
-      o[e] = EPI == EPI_BIAS ? a : EPI == EPI_BIAS_SIG ? sigmoidf_ref(a) : EPI == EPI_BIAS_NSIG ? -sigmoidf_ref(a) : -a;
-    }
-    *cp = o;
-  } else if (EPI == EPI_RBM) {
-    f32x4* qp = reinterpret_cast<f32x4*>(p.corr + (long)row * p.ldcorr + col);
-    const f32x4 w = *cp, q = *qp;
-    f32x4 c, o;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      c[e] = p.mmt * q[e] + p.scale * v[e] + p.l2 * w[e];
-      o[e] = w[e] + c[e];
-    }
-    *qp = c;
-    *cp = o;
-  } else if (EPI == EPI_DSIG) {
-    const f32x4 y = *reinterpret_cast<const f32x4*>(p.aux + (long)row * p.ldaux + col);
-    f32x4 o;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) o[e] = y[e] * (1.f - y[e]) * v[e];
-    *cp = o;
-  } else {  // EPI_SGD
-    f32x4 c = v;
-    if (p.corr) {
-      f32x4* qp = reinterpret_cast<f32x4*>(p.corr + (long)row * p.ldcorr + col);
-      c = v + p.mmt * *qp;
-      *qp = c;
-    }
-    f32x4 w = *cp;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      w[e] = w[e] + p.scale * c[e];
-      w[e] = w[e] + p.l2 * w[e];
-    }
-    *cp = w;
-  }
-}
+// ---- diagnostic clock stamps (separate build: make stamp -> lib/libtnet_amd_stamp.so; the product
+// library has none; the stamp build's ablations TNET_GEMM_DIAG_NODMA / _NOREAD / _NOBAR drop the
+// main loop's LDS-DMA pieces / fragment reads / seam barriers -- wrong results, timing only).  Wave 0 of every workgroup records s_memtime (shader clock) at kernel entry,
+// after the prologue, after the main loop and after the epilogue, and s_memrealtime (100 MHz) at
+// entry and exit, into a buffer no other code reads (MI355X_MICROARCH.md 'DVFS give-back' item 6).
+#ifdef TNET_GEMM_STAMP
+__device__ unsigned long long g_tnet_stamps[8192 * 6];
+#define TNET_STAMP(i)                                                                   \
+  do {                                                                                  \
+    const unsigned long long tt_ = __builtin_amdgcn_s_memtime();                        \
+    if (threadIdx.x == 0 && blockIdx.x < 8192) g_tnet_stamps[blockIdx.x * 6 + (i)] = tt_; \
+  } while (0)
+#define TNET_STAMP_RT(i)                                                                \
+  do {                                                                                  \
+    const unsigned long long tt_ = __builtin_amdgcn_s_memrealtime();                    \
+    if (threadIdx.x == 0 && blockIdx.x < 8192) g_tnet_stamps[blockIdx.x * 6 + (i)] = tt_; \
+  } while (0)
+#else
+#define TNET_STAMP(i) do { } while (0)
+#define TNET_STAMP_RT(i) do { } while (0)
+#endif
 
 // =============================================================================================
 // 16x16x4 variant (v_mfma_f32_16x16x4_f32: 32 cycles per 1024 MACs; on this part it sustains a
@@ -488,11 +475,24 @@ __device__ __forceinline__ void epi_vec4(const GemmP& p, int row, int col, f32x4
 //     (about G/KCH per chunk, between the fragment reads and the chunk's MFMAs) instead of all at
 //     the tile seam, and the MFMA block runs at s_setprio 1 (an 8-wave workgroup's partner wave
 //     then fills the other wave's seams).
+//   * SP = 2: one extra LOADER wave issues every LDS-DMA piece; the WMxWN compute waves only read
+//     fragments and issue MFMAs.  An LDS-DMA instruction holds its issuing wave for ~20-30 cycles
+//     (tools/gemm_clock.py ablation: dropping the compute waves' pieces cut the 2048^2 main loop by
+//     8 %), which the loader now absorbs on its own wave slot.  Same ring protocol: the loader waits
+//     for tile t+1 (counted vmcnt), meets the compute waves at the seam barrier, then refills the
+//     slot of tile t.  MEASURED SLOWER (2048^2 main loop 185k vs 149k cycles): the issue cost is paid
+//     by the loader's SIMD, whose compute wave then trails the other three at every seam barrier --
+//     kept as one config (m64x128k64s2L) for the record, not chosen by the heuristic.
 template <int BM, int BN, int BK, int WM, int WN, int S, int SP, bool A_KC, bool B_KC, int EPI>
-__global__ __launch_bounds__(WM * WN * 64) __attribute__((amdgpu_waves_per_eu((WM * WN + 3) / 4, (WM * WN + 3) / 4)))
+__global__ __launch_bounds__((WM * WN + (SP == 2)) * 64)
+__attribute__((amdgpu_waves_per_eu((WM * WN + (SP == 2) + 3) / 4, (WM * WN + (SP == 2) + 3) / 4)))
 void gemm16_kernel(const GemmP p) {
   constexpr int NT = WM * WN * 64, NW = WM * WN;
-  static_assert(SP == 0 || S >= 3, "spread DMA needs a 3-slot ring");
+  constexpr bool LDR = SP == 2;
+  static_assert(SP != 1 || S >= 3, "spread DMA needs a 3-slot ring");
+#ifdef TNET_GEMM_DIAG_NOBAR
+  static_assert(!LDR, "the loader wave meets the compute waves at every seam barrier");
+#endif
   constexpr int WTM = BM / WM, WTN = BN / WN;  // wave tile
   constexpr int TM = WTM / 16, TN = WTN / 16;
   static_assert(WTM % 16 == 0 && WTN % 16 == 0, "16x16 tiles per wave");
@@ -505,6 +505,8 @@ void gemm16_kernel(const GemmP p) {
   static_assert(A_SZ % (4 * NT) == 0 && B_SZ % (4 * NT) == 0, "tile splits into 1-KiB wave pieces");
   static_assert(3 * G < 64, "vmcnt range");
   __shared__ __attribute__((aligned(16))) float smem[S * ST_SZ];
+  TNET_STAMP_RT(4);
+  TNET_STAMP(0);
 
   const int M = p.M, N = p.N, K = p.K;
   const int nbn = (N + BN - 1) / BN, nbm = (M + BM - 1) / BM;
@@ -520,6 +522,74 @@ void gemm16_kernel(const GemmP p) {
   const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm0 = (wid / WN) * WTM, wn0 = (wid % WN) * WTN;
   const int lg = lane >> 4, li = lane & 15;
+
+  if constexpr (LDR) {
+    if (wid == NW) {  // ---- loader wave: all G_L pieces of every k-tile, nothing else
+      constexpr int GAL = A_SZ / 256, GBL = B_SZ / 256, GL = GAL + GBL;
+      static_assert((S - 2) * GL < 64, "loader vmcnt range");
+      unsigned offA[GAL], offB[GBL];
+#pragma unroll
+      for (int g = 0; g < GAL; ++g) {
+        const int u = g * 64 + lane;
+        if (A_KC) {
+          const int r = u / CH, j = u % CH;
+          offA[g] = 4u * (unsigned)(min(bm + r, M - 1) * p.lda + 4 * (j ^ swz<BK>(r)));
+        } else {
+          const int k = u / (BM / 4), c = (u % (BM / 4)) * 4;
+          offA[g] = 4u * (unsigned)(k * p.lda + (bm + c < M ? bm + c : 0));
+        }
+      }
+#pragma unroll
+      for (int g = 0; g < GBL; ++g) {
+        const int u = g * 64 + lane;
+        if (B_KC) {
+          const int r = u / CH, j = u % CH;
+          offB[g] = 4u * (unsigned)(min(bn + r, N - 1) * p.ldb + 4 * (j ^ swz<BK>(r)));
+        } else {
+          const int k = u / (BN / 4), c = (u % (BN / 4)) * 4;
+          offB[g] = 4u * (unsigned)(k * p.ldb + (bn + c < N ? bn + c : 0));
+        }
+      }
+      auto issue_l = [&](int t, int sl) {
+        float* st = smem + sl * ST_SZ;
+        const char* ab = (const char*)(p.A + (A_KC ? (long)t * BK : (long)t * BK * p.lda));
+        const char* bb = (const char*)(p.B + (B_KC ? (long)t * BK : (long)t * BK * p.ldb));
+#pragma unroll
+        for (int g = 0; g < GAL; ++g) {
+          unsigned o = offA[g];
+          asm volatile("" : "+v"(o));
+          __builtin_amdgcn_global_load_lds((const void*)(ab + o), (void*)(st + g * 256), 16, 0, 0);
+        }
+#pragma unroll
+        for (int g = 0; g < GBL; ++g) {
+          unsigned o = offB[g];
+          asm volatile("" : "+v"(o));
+          __builtin_amdgcn_global_load_lds((const void*)(bb + o), (void*)(st + A_SZ + g * 256), 16, 0, 0);
+        }
+      };
+      const int nfull = K / BK, tlast = max(nfull - 1, 0);
+      if (nfull > 0) {
+#pragma unroll
+        for (int t = 0; t < S - 1; ++t) issue_l(min(t, tlast), t);
+        wait_vmcnt<(S - 2) * GL>();
+        __builtin_amdgcn_s_barrier();  // tile 0 landed
+        issue_l(min(S - 1, tlast), S - 1);
+      }
+      int sl = 0;
+      for (int t = 0; t < nfull; ++t) {
+        wait_vmcnt<(S - 2) * GL>();    // tile t+1 landed
+        __builtin_amdgcn_s_barrier();  // seam t: every compute wave is done with tile t's slot
+        issue_l(min(t + S, tlast), sl);
+        sl = sl + 1 == S ? 0 : sl + 1;
+      }
+      wait_vmcnt<0>();  // no DMA may outlive the workgroup's LDS
+      if (K % BK) {     // the masked tail's two barriers
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_s_barrier();
+      }
+      return;
+    }
+  }
 
   // per-lane BYTE offsets from the tile's base (32-bit: the launcher checks the operand extent), so
   // each DMA is global_load_lds with a scalar base (advanced per tile) + one VGPR offset
@@ -638,12 +708,12 @@ void gemm16_kernel(const GemmP p) {
   };
   constexpr int NRD = TM + TN;      // ds_read_b128 per chunk (both operand layouts)
   constexpr int NMF = 4 * TM * TN;  // MFMAs per chunk
-  static_assert(NMF >= NRD + (SP ? PPC : G), "interleave pattern");
+  static_assert(NMF >= NRD + (SP == 1 ? PPC : LDR ? 0 : G), "interleave pattern");
   static_assert(PPC * KCH >= G, "pieces per chunk");
   // vmcnt at a seam: everything younger than tile t+1 may stay in flight -- tiles t+2..t+S-1 without
   // SP; with SP tiles t+2..t+S-2 plus the pieces of tile t+S-1 issued in the chunks before the seam
   // (the seam chunk issues its share after the wait)
-  constexpr int SEAM_VM = SP ? (S - 3) * G + (G < (KCH - 1) * PPC ? G : (KCH - 1) * PPC) : (S - 2) * G;
+  constexpr int SEAM_VM = SP == 1 ? (S - 3) * G + (G < (KCH - 1) * PPC ? G : (KCH - 1) * PPC) : (S - 2) * G;
 
   // Branch-free main loop: every tile ends with the seam (wait for tile t+1, barrier, first
   // fragments of t+1) and every tile issues exactly G pieces, so the counted vmcnt is the constant
@@ -652,14 +722,89 @@ void gemm16_kernel(const GemmP p) {
   // compiler count lgkmcnt exactly instead of draining at every block join.
   const int nfull = K / BK;
   const int tlast = max(nfull - 1, 0);
-  if (nfull > 0) {
+  if constexpr (!LDR) {
+    if (nfull > 0)
 #pragma unroll
-    for (int t = 0; t < S - 1; ++t) issue(min(t, tlast), t);
-    wait_vmcnt<(S - 2) * G>();
+      for (int t = 0; t < S - 1; ++t) issue(min(t, tlast), t);
+  }
+  if (nfull > 0) {
+    if constexpr (!LDR) wait_vmcnt<(S - 2) * G>();
     barrier();  // tile 0 landed in every wave's pieces
     if (!SP) issue(min(S - 1, tlast), S - 1);
     read_frags(smem, 0, 0);
   }
+  // Epilogue operands (bias / y of the layer below / W and the momentum buffer) are loaded into
+  // registers HERE, right after the prologue: the main loop hides their latency (a seam's counted
+  // vmcnt wait may also wait for them: they are older than every DMA piece still in flight -- safe)
+  // and the epilogue is pure arithmetic + stores.  (Loaded at the end, each load waits behind the
+  // stores issued before it -- vmcnt is in order -- one full round trip per row of the tile.)
+  constexpr int EB = epi_base(EPI);
+  constexpr bool EV = !B_KC;  // output columns in 4-vectors (n-contiguous B) or scalars (k-contiguous B)
+  constexpr int NJ = EV ? TN / 4 : TN;
+  constexpr bool PRE_BIAS = EB == EPI_BIAS || EB == EPI_BIAS_SIG || EB == EPI_BIAS_NSIG || EB == EPI_BIAS_NEG;
+  constexpr bool PRE_C = EB == EPI_SGD || EB == EPI_RBM;
+  constexpr bool PRE_AUX = EB == EPI_DSIG;
+  constexpr bool PRE_Q = EB == EPI_SGD || EB == EPI_RBM;
+  auto erow = [&](int a, int r) {
+    return A_KC ? bm + wm0 + 16 * a + 4 * lg + r : bm + wm0 + 64 * (a / 4) + 4 * (4 * lg + r) + (a % 4);
+  };
+  auto ecol = [&](int j) { return EV ? bn + wn0 + 64 * j + 4 * li : bn + wn0 + 16 * j + li; };
+  auto ld_tile = [&](const float* base, long ld, int row, int col) {
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    if (row < M) {
+      const float* q = base + (long)row * ld + col;
+      if (EV) {
+        if (col + 3 < N) v = *reinterpret_cast<const f32x4*>(q);
+        else
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = col + e < N ? q[e] : 0.f;
+      } else if (col < N) {
+        v[0] = *q;
+      }
+    }
+    return v;
+  };
+  f32x4 pre_bias[PRE_BIAS ? NJ : 1];
+  f32x4 pre_a[PRE_C || PRE_AUX ? TM : 1][4][PRE_C || PRE_AUX ? NJ : 1];
+  f32x4 pre_q[PRE_Q ? TM : 1][4][PRE_Q ? NJ : 1];
+  const bool has_q = PRE_Q && p.corr != nullptr;
+  if constexpr (PRE_BIAS) {
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int col = ecol(j);
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int e = 0; e < (EV ? 4 : 1); ++e) v[e] = col + e < N ? p.bias[col + e] : 0.f;
+      pre_bias[j] = v;
+    }
+  }
+  if constexpr (PRE_C || PRE_AUX) {
+    const float* base = PRE_AUX ? p.aux : p.C;
+    const long ld = PRE_AUX ? p.ldaux : p.ldc;
+#pragma unroll
+    for (int a = 0; a < TM; ++a)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) pre_a[a][r][j] = ld_tile(base, ld, erow(a, r), ecol(j));
+  }
+  if constexpr (PRE_Q) {
+    if (has_q) {
+#pragma unroll
+      for (int a = 0; a < TM; ++a)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int j = 0; j < NJ; ++j) pre_q[a][r][j] = ld_tile(p.corr, p.ldcorr, erow(a, r), ecol(j));
+    }
+  }
+
+  static_assert(EPI != EPI_SGD_B || BN <= NT, "one thread per bias column");
+  BiasPre bpre;
+  if constexpr (EPI == EPI_SGD_B)
+    if (bm == 0) bias_pre_load<BN>(p, bn, bpre);
+
+  TNET_STAMP(1);
   // one fragment read (r < TM: operand A, else B) of chunk c of the slot at st into buffer buf
   auto read_one = [&](const float* st, int c, int buf, int r) {
     const float* As = st;
@@ -692,15 +837,21 @@ void gemm16_kernel(const GemmP p) {
     }
   };
   // one DMA piece g of tile t into slot sl
+  // (the 32-bit offset is made opaque per use so its zero-extension stays next to the load and the
+  // instruction selects the SGPR-base + 32-bit VGPR-offset form: no 64-bit VALU add per piece)
   auto issue_one = [&](int t, int sl, int g) {
     float* st = smem + sl * ST_SZ;
     if (g < GA) {
       const char* ab = (const char*)(p.A + (A_KC ? (long)t * BK : (long)t * BK * p.lda));
-      __builtin_amdgcn_global_load_lds((const void*)(ab + srcA[g]), (void*)(st + (g * NW + wid) * 256), 16, 0, 0);
+      unsigned o = srcA[g];
+      asm volatile("" : "+v"(o));
+      __builtin_amdgcn_global_load_lds((const void*)(ab + o), (void*)(st + (g * NW + wid) * 256), 16, 0, 0);
     } else {
       const char* bb = (const char*)(p.B + (B_KC ? (long)t * BK : (long)t * BK * p.ldb));
-      __builtin_amdgcn_global_load_lds((const void*)(bb + srcB[g - GA]),
-                                       (void*)(st + A_SZ + ((g - GA) * NW + wid) * 256), 16, 0, 0);
+      unsigned o = srcB[g - GA];
+      asm volatile("" : "+v"(o));
+      __builtin_amdgcn_global_load_lds((const void*)(bb + o), (void*)(st + A_SZ + ((g - GA) * NW + wid) * 256), 16,
+                                       0, 0);
     }
   };
 
@@ -725,11 +876,13 @@ void gemm16_kernel(const GemmP p) {
         // hand over to tile t+1: own reads of tile t retired, tile t+1 landed, everyone past
         __builtin_amdgcn_sched_barrier(0);
         __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
-        wait_vmcnt<SEAM_VM>();
+        if constexpr (!LDR) wait_vmcnt<SEAM_VM>();
+#ifndef TNET_GEMM_DIAG_NOBAR
         barrier();
+#endif
       }
-      if (SP) __builtin_amdgcn_s_setprio(1);
-      constexpr int NP = SP ? PPC : G;
+      if (SP == 1) __builtin_amdgcn_s_setprio(1);
+      constexpr int NP = SP == 1 ? PPC : LDR ? 0 : G;
       int idx = 0;
 #pragma unroll
       for (int s = 0; s < 4; ++s)
@@ -740,27 +893,34 @@ void gemm16_kernel(const GemmP p) {
             acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[buf][a][s], bv[buf][b][s], acc[a][b], 0, 0, 0);
             if (idx < NRD) {
               __builtin_amdgcn_sched_barrier(0);
+#ifndef TNET_GEMM_DIAG_NOREAD
               read_one(rst, rc, buf ^ 1, idx);
+#endif
               __builtin_amdgcn_sched_barrier(0);
             } else if (idx < NRD + NP) {
-              const int g = SP ? c * PPC + (idx - NRD) : idx - NRD;
-              if (SP && g < G) {
+              const int g = SP == 1 ? c * PPC + (idx - NRD) : idx - NRD;
+              if (SP == 1 && g < G) {
                 __builtin_amdgcn_sched_barrier(0);
+#ifndef TNET_GEMM_DIAG_NODMA
                 issue_one(tsp, slp, g);
+#endif
                 __builtin_amdgcn_sched_barrier(0);
-              } else if (!SP && seam) {
+              } else if (SP == 0 && seam) {
                 __builtin_amdgcn_sched_barrier(0);
+#ifndef TNET_GEMM_DIAG_NODMA
                 issue_one(tns, sl, g);
+#endif
                 __builtin_amdgcn_sched_barrier(0);
               }
             }
             ++idx;
           }
-      if (SP) __builtin_amdgcn_s_setprio(0);
+      if (SP == 1) __builtin_amdgcn_s_setprio(0);
     }
     sl = sl1;
   }
   wait_vmcnt<0>();  // repeat loads of the last tile still land in LDS
+  TNET_STAMP(2);
   if (K % BK) {
     // masked tail k-tile through registers, same images, in slot nfull % S (the final seam read
     // it: every wave's reads retire before the barrier)
@@ -802,43 +962,114 @@ void gemm16_kernel(const GemmP p) {
     }
   }
 
-  // ---- epilogue
+  if constexpr (EPI == EPI_SGD_B)
+    if (bm == 0) bias_pre_finish<BN>(p, bn, bpre);
+
+  // ---- epilogue: arithmetic on the prefetched operands, then 16-B (n-contiguous) or 4-B stores
+  // EPI_DSIG_CS: each wave owns 32 output rows (one slab) x its columns; a lane sums its 8 rows of
+  // a column in order, the 4 lane groups of a column meet by two xor-shuffles
+  constexpr bool CS = EPI == EPI_DSIG_CS;
+  static_assert(!CS || (A_KC && B_KC && WTM == kColsumSlabRows), "column sums: bwd layout, 32-row wave tiles");
+  float csum[CS ? TN : 1];
+#pragma unroll
+  for (int j = 0; j < (CS ? TN : 1); ++j) csum[j] = 0.f;
 #pragma unroll
   for (int a = 0; a < TM; ++a) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int row = A_KC ? bm + wm0 + 16 * a + 4 * lg + r : bm + wm0 + 64 * (a / 4) + 4 * (4 * lg + r) + (a % 4);
+      const int row = erow(a, r);
       if (row >= M) continue;
-      if (!B_KC) {
 #pragma unroll
-        for (int q = 0; q < TN / 4; ++q) {
-          const int col = bn + wn0 + 64 * q + 4 * li;
-          f32x4 v;
+      for (int j = 0; j < NJ; ++j) {
+        const int col = ecol(j);
+        constexpr int NE = EV ? 4 : 1;
+        f32x4 v;
 #pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = acc[a][4 * q + e][r];
-          if (col + 3 < N) epi_vec4<EPI>(p, row, col, v);
-          else
+        for (int e = 0; e < NE; ++e) v[e] = EV ? acc[a][4 * j + e][r] : acc[a][j][r];
+        f32x4 o = v, qn = v;
+        if constexpr (EB == EPI_STORE) {
+          if (p.beta == 0.f) {
 #pragma unroll
-            for (int e = 0; e < 4; ++e)
-              if (col + e < N) epi_elem<EPI>(p, row, col + e, v[e]);
+            for (int e = 0; e < NE; ++e) o[e] = p.alpha * v[e];
+          } else {
+            const f32x4 c0 = ld_tile(p.C, p.ldc, row, col);
+#pragma unroll
+            for (int e = 0; e < NE; ++e) o[e] = p.alpha * v[e] + p.beta * c0[e];
+          }
+        } else if constexpr (PRE_BIAS) {
+#pragma unroll
+          for (int e = 0; e < NE; ++e) {
+            const float x = v[e] + pre_bias[j][e];
+            o[e] = EB == EPI_BIAS ? x : EB == EPI_BIAS_SIG ? sigmoidf_ref(x)
+                 : EB == EPI_BIAS_NSIG ? -sigmoidf_ref(x) : -x;
+          }
+        } else if constexpr (EB == EPI_DSIG) {
+#pragma unroll
+          for (int e = 0; e < NE; ++e) {
+            const float y = pre_a[a][r][j][e];
+            o[e] = y * (1.f - y) * v[e];
+          }
+          if constexpr (CS) csum[j] += o[0];
+        } else if constexpr (EB == EPI_RBM) {
+          // c = mmt*corr + scale*acc + l2*W ; corr = c ; W += c   (cuRbm.cc:133-174)
+#pragma unroll
+          for (int e = 0; e < NE; ++e) {
+            const float w = pre_a[a][r][j][e];
+            const float c = p.mmt * pre_q[a][r][j][e] + p.scale * v[e] + p.l2 * w;
+            qn[e] = c;
+            o[e] = w + c;
+          }
+        } else {  // EPI_SGD: corr = acc + mmt*corr ; W += scale*corr ; W += l2*W   (cuBiasedLinearity.cc:46-64)
+#pragma unroll
+          for (int e = 0; e < NE; ++e) {
+            const float c = has_q ? v[e] + p.mmt * pre_q[a][r][j][e] : v[e];
+            qn[e] = c;
+            float w = pre_a[a][r][j][e];
+            w = w + p.scale * c;
+            w = w + p.l2 * w;
+            o[e] = w;
+          }
         }
-      } else {
+        float* cp = p.C + (long)row * p.ldc + col;
+        float* qp = has_q ? p.corr + (long)row * p.ldcorr + col : nullptr;
+        if (EV && col + 3 < N) {
+          *reinterpret_cast<f32x4*>(cp) = o;
+          if (has_q) *reinterpret_cast<f32x4*>(qp) = qn;
+        } else {
 #pragma unroll
-        for (int b = 0; b < TN; ++b) {
-          const int col = bn + wn0 + 16 * b + li;
-          if (col < N) epi_elem<EPI>(p, row, col, acc[a][b][r]);
+          for (int e = 0; e < NE; ++e)
+            if (col + e < N) {
+              cp[e] = o[e];
+              if (has_q) qp[e] = qn[e];
+            }
         }
       }
     }
   }
+  if constexpr (CS) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      csum[j] += __shfl_xor(csum[j], 16, 64);
+      csum[j] += __shfl_xor(csum[j], 32, 64);
+    }
+    const int slab_row = bm + wm0, col0 = bn + wn0 + li;
+    if (lg == 0 && slab_row < M) {
+      float* cp = p.cpart + (long)(slab_row / kColsumSlabRows) * p.ldcpart;
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        if (col0 + 16 * j < N) cp[col0 + 16 * j] = csum[j];
+    }
+  }
+  TNET_STAMP(3);
+  TNET_STAMP_RT(5);
 }
 
 // ---------------------------------------------------------------------------------------------
 // host-side dispatch
 // ---------------------------------------------------------------------------------------------
 // name: g<BM>x<BN>k<BK>s<S>w<waves>[i]: 32x32x2 kernel (waves laid out WMxWN; i = DMA pieces
-//       interleaved); m<BM>x<BN>k<BK>s<S>[w<WM><WN>][p]: 16x16x4 kernel (default 2x2 waves; p = DMA
-//       pieces spread over the chunks + MFMA at setprio 1)
+//       interleaved); m<BM>x<BN>k<BK>s<S>[w<WM><WN>][p|L]: 16x16x4 kernel (default 2x2 waves; p = DMA
+//       pieces spread over the chunks + MFMA at setprio 1; L = one extra loader wave issues all DMA)
 #define TNET_GEMM_CFGS(X)                                 \
   X(g64x64k32s4w4, 0, 64, 64, 32, 2, 2, 4, 0)            \
   X(g64x64k32s4w4i, 0, 64, 64, 32, 2, 2, 4, 1)           \
@@ -868,7 +1099,8 @@ void gemm16_kernel(const GemmP p) {
   X(m64x128k32s4p, 1, 64, 128, 32, 2, 2, 4, 1)           \
   X(m64x128k32s4w42p, 1, 64, 128, 32, 4, 2, 4, 1)        \
   X(m128x128k32s3p, 1, 128, 128, 32, 2, 2, 3, 1)         \
-  X(m128x128k32s4p, 1, 128, 128, 32, 2, 2, 4, 1)
+  X(m128x128k32s4p, 1, 128, 128, 32, 2, 2, 4, 1)         \
+  X(m64x128k64s2L, 1, 64, 128, 64, 2, 2, 2, 2)
 
 enum GemmCfg {
 #define X(name, ...) CFG_##name,
@@ -910,7 +1142,7 @@ static bool launch_cfg(const GemmP& p, hipStream_t st) {
     const long extB = B_KC ? (long)p.N * p.ldb : (long)BK * p.ldb + p.N;
     if (4 * extA >= (1L << 32) || 4 * extB >= (1L << 32)) return false;
     if constexpr ((A_KC || TM % 4 == 0) && (B_KC || TN % 4 == 0)) {
-      gemm16_kernel<BM, BN, BK, WM, WN, S, IL, A_KC, B_KC, EPI><<<tiles, WM * WN * 64, 0, st>>>(p);
+      gemm16_kernel<BM, BN, BK, WM, WN, S, IL, A_KC, B_KC, EPI><<<tiles, (WM * WN + (IL == 2)) * 64, 0, st>>>(p);
       return true;
     } else {
       return false;  // this tile cannot hold the operand layout
@@ -918,8 +1150,22 @@ static bool launch_cfg(const GemmP& p, hipStream_t st) {
   }
 }
 
+// bwd GEMM + diff-sigmoid + column sums: one fixed 64x128 16x16 config (32-row wave tiles = slabs)
+static int launch_colsum_bwd(const GemmP& p_in, hipStream_t st) {
+  if (p_in.M <= 0 || p_in.N <= 0) return TNET_OK;
+  forced_cfg();
+  GemmP p = p_in;
+  p.group = g_group > 0 ? g_group : 8;
+  if (!launch_cfg<1, 64, 128, 64, 2, 2, 2, 0, true, true, EPI_DSIG_CS>(p, st)) return TNET_ERR_UNSUPPORTED;
+  TNET_LAUNCH_CHECK();
+  return TNET_OK;
+}
+
 template <bool A_KC, bool B_KC, int EPI>
 static int launch_gemm(const GemmP& p_in, hipStream_t st) {
+  if constexpr (EPI == EPI_DSIG_CS) {
+    return launch_colsum_bwd(p_in, st);
+  } else {
   if (p_in.M <= 0 || p_in.N <= 0) return TNET_OK;
   static const int noload = getenv("TNET_GEMM_DIAG") ? atoi(getenv("TNET_GEMM_DIAG")) : 0;
   GemmP p = p_in;
@@ -946,6 +1192,7 @@ static int launch_gemm(const GemmP& p_in, hipStream_t st) {
   if (!ok) launch_cfg<0, 64, 64, 32, 2, 2, 4, 0, A_KC, B_KC, EPI>(p, st);  // layout not supported by cfg
   TNET_LAUNCH_CHECK();
   return TNET_OK;
+  }
 }
 
 static bool aligned16(const void* q) { return ((uintptr_t)q & 15) == 0; }
@@ -1066,6 +1313,49 @@ extern "C" int tnet_affine_update(const float* X, TnetMatrixDim dX, const float*
   return launch_gemm<false, false, EPI_SGD>(p, (hipStream_t)stream);
 }
 
+extern "C" int tnet_colsum_slabs(int rows) { return rows > 0 ? (rows + kColsumSlabRows - 1) / kColsumSlabRows : 0; }
+
+extern "C" int tnet_affine_bwd_colsum(const float* E, TnetMatrixDim dE, const float* W, TnetMatrixDim dW,
+                                      const float* Ybelow, int strideYbelow, float* Eo, TnetMatrixDim dEo,
+                                      float* colpart, int ldcolpart, void* stream) {
+  // tnet_affine_bwd with dsig, plus colpart[s][c] = sum of Eo[r][c] over the 32-row slab s (fp32, in row order)
+  if (dE.cols != dW.cols || dEo.rows != dE.rows || dEo.cols != dW.rows || !Ybelow || !colpart ||
+      ldcolpart < dEo.cols)
+    return TNET_ERR_ARG;
+  GemmP p{};
+  p.M = dE.rows; p.N = dW.rows; p.K = dE.cols;
+  p.A = E; p.lda = dE.stride; p.B = W; p.ldb = dW.stride; p.C = Eo; p.ldc = dEo.stride;
+  p.alpha = 1.f; p.beta = 0.f;
+  p.aux = Ybelow; p.ldaux = strideYbelow;
+  p.cpart = colpart; p.ldcpart = ldcolpart;
+  int st = check_common(p);
+  if (st) return st;
+  return launch_gemm<true, true, EPI_DSIG_CS>(p, (hipStream_t)stream);
+}
+
+extern "C" int tnet_affine_update_bias(const float* X, TnetMatrixDim dX, const float* E, TnetMatrixDim dE, float* W,
+                                       TnetMatrixDim dW, float* corrW, int strideCorr, float scale, float mmt,
+                                       float l2, const float* colpart, int ldcolpart, float* b, float* corr_b,
+                                       void* stream) {
+  // tnet_affine_update + the bias SGD of tnet_bias_update(E, b, corr_b, scale, mmt), the column sum of E
+  // taken from the slab sums tnet_affine_bwd_colsum wrote for E
+  if (dX.rows != dE.rows || dW.rows != dX.cols || dW.cols != dE.cols || !colpart || !b || ldcolpart < dE.cols)
+    return TNET_ERR_ARG;
+  if (mmt != 0.f && (!corrW || !corr_b)) return TNET_ERR_ARG;
+  GemmP p{};
+  p.M = dX.cols; p.N = dE.cols; p.K = dX.rows;
+  p.A = X; p.lda = dX.stride; p.B = E; p.ldb = dE.stride; p.C = W; p.ldc = dW.stride;
+  p.corr = (mmt != 0.f || corrW) ? corrW : nullptr; p.ldcorr = strideCorr;
+  if (p.corr && (p.ldcorr & 3)) return TNET_ERR_ARG;
+  p.scale = scale; p.mmt = mmt; p.l2 = l2;
+  p.bpart = colpart; p.ldbpart = ldcolpart; p.bslabs = tnet_colsum_slabs(dE.rows);
+  p.bvec = b; p.bcorr = mmt != 0.f ? corr_b : nullptr; p.bscale = scale; p.bmmt = mmt;
+  int st = check_common(p);
+  if (st) return st;
+  if (p.M <= 0 || p.N <= 0) return TNET_OK;
+  return launch_gemm<false, false, EPI_SGD_B>(p, (hipStream_t)stream);
+}
+
 extern "C" int tnet_affine_grad(const float* X, TnetMatrixDim dX, const float* E, TnetMatrixDim dE, float* G,
                                 TnetMatrixDim dG, void* stream) {
   if (dX.rows != dE.rows || dG.rows != dX.cols || dG.cols != dE.cols) return TNET_ERR_ARG;
@@ -1091,3 +1381,16 @@ extern "C" int tnet_gemm_config(const char* name) {
     }
   return TNET_ERR_ARG;
 }
+
+#ifdef TNET_GEMM_STAMP
+extern "C" int tnet_diag_stamps(unsigned long long* host, int n_wg) {
+  if (n_wg > 8192) n_wg = 8192;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_tnet_stamps), sizeof(unsigned long long) * 6 * n_wg, 0,
+                             hipMemcpyDeviceToHost) == hipSuccess ? TNET_OK : TNET_ERR_LAUNCH;
+}
+extern "C" int tnet_diag_stamps_clear() {
+  void* a = nullptr;
+  if (hipGetSymbolAddress(&a, HIP_SYMBOL(g_tnet_stamps)) != hipSuccess) return TNET_ERR_RUNTIME;
+  return hipMemset(a, 0, sizeof(g_tnet_stamps)) == hipSuccess ? TNET_OK : TNET_ERR_RUNTIME;
+}
+#endif

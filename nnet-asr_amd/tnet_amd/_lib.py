@@ -12,6 +12,9 @@ import re
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "libtnet_amd.so")
+if os.environ.get("TNET_DIAG_STAMP_LIB"):  # diagnostics only (tools/gemm_clock.py): clock-stamped GEMM build
+    _v = os.environ["TNET_DIAG_STAMP_LIB"]
+    LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "libtnet_amd_stamp" + ("" if _v == "1" else "_" + _v) + ".so")
 INCLUDE_DIR = os.path.join(os.path.dirname(os.path.dirname(_HERE)), "include")
 
 _lib = None
@@ -62,6 +65,10 @@ _SIGS = {
     "tnet_affine_fwd": (i32, [vp, MatrixDim, vp, MatrixDim, vp, vp, MatrixDim, i32, vp]),
     "tnet_affine_bwd": (i32, [vp, MatrixDim, vp, MatrixDim, vp, i32, vp, MatrixDim, i32, vp]),
     "tnet_affine_update": (i32, [vp, MatrixDim, vp, MatrixDim, vp, MatrixDim, vp, i32, f32, f32, f32, vp]),
+    "tnet_colsum_slabs": (i32, [i32]),
+    "tnet_affine_bwd_colsum": (i32, [vp, MatrixDim, vp, MatrixDim, vp, i32, vp, MatrixDim, vp, i32, vp]),
+    "tnet_affine_update_bias": (i32, [vp, MatrixDim, vp, MatrixDim, vp, MatrixDim, vp, i32, f32, f32, f32, vp, i32,
+                                      vp, vp, vp]),
     "tnet_affine_grad": (i32, [vp, MatrixDim, vp, MatrixDim, vp, MatrixDim, vp]),
     "tnet_sgd_update": (i32, [vp, vp, vp, i64, f32, f32, f32, vp]),
     "tnet_bias_update": (i32, [vp, MatrixDim, vp, vp, vp, f32, f32, vp, vp]),

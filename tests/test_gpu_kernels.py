@@ -35,7 +35,8 @@ def gemm_ref(ta, tb, A, B):
 GEMM_CFGS = ["auto", "g64x64k32s4w4", "g64x64k32s4w4i", "g64x64k64s2w4", "g64x64k32s4w2", "g128x64k32s3w4",
              "g64x128k32s3w4", "g128x128k32s3w8", "m64x128k32s4", "m64x128k64s3", "m64x64k32s4w41", "m128x128k32s3",
              "m128x128k64s2", "m64x128k32s4w12", "m64x128k64s2w42", "m64x64k32s4w21", "m64x128k64s3p",
-             "m64x128k64s3w42p", "m64x128k32s4p", "m64x128k32s4w42p", "m128x128k32s3p", "m128x128k32s4p"]
+             "m64x128k64s3w42p", "m64x128k32s4p", "m64x128k32s4w42p", "m128x128k32s3p", "m128x128k32s4p",
+             "m64x128k64s2L"]
 
 
 @pytest.fixture(params=GEMM_CFGS)
@@ -129,6 +130,69 @@ def test_affine_update(mmt, rows, n_in, n_out, gemm_cfg):
     assert np.all(np.abs(dW.numpy() - w) <= tol)
     if mmt:
         assert np.all(np.abs(dC.numpy() - c) <= 2e-5 * mag + 1e-6)
+
+
+def slab_sums(M, slab=32):
+    """column sums of M per 32-row slab (fp64)"""
+    n = -(-M.shape[0] // slab)
+    return np.stack([M[s * slab:(s + 1) * slab].astype(np.float64).sum(0) for s in range(n)])
+
+
+@pytest.mark.parametrize("rows,n_in,n_out", [(16, 32, 10), (33, 64, 40), (1024, 2048, 2048), (1000, 440, 2048),
+                                             (1024, 2048, 4000)])
+def test_affine_bwd_colsum(rows, n_in, n_out):
+    """bwd + diff-sigmoid with the bias gradient of the layer below as 32-row slab column sums"""
+    E, W = rnd((rows, n_out), 9), rnd((n_in, n_out), 10, 0.1)
+    Yb = 1 / (1 + np.exp(-rnd((rows, n_in), 11)))
+    dE, dW, dY, dO = (DeviceArray.from_numpy(E), DeviceArray.from_numpy(W), DeviceArray.from_numpy(Yb),
+                      DeviceArray(rows, n_in))
+    slabs = lib().tnet_colsum_slabs(rows)
+    assert slabs == -(-rows // 32)
+    dP = DeviceArray.from_numpy(np.full((slabs, n_in), np.nan, np.float32))
+    check(lib().tnet_affine_bwd_colsum(dE.ptr, dE.dim, dW.ptr, dW.dim, dY.ptr, dY.stride, dO.ptr, dO.dim, dP.ptr,
+                                       dP.stride, S()))
+    z, mag = gemm_ref("N", "T", E, W)
+    s = Yb * (1 - Yb)
+    got = dO.numpy()
+    assert np.all(np.abs(got - z * s) <= 2e-5 * mag * s + 1e-7)
+    # slab sums: each is the fp32 sum (in row order) of the kernel's own outputs
+    P = dP.numpy()
+    ref = slab_sums(z * s)
+    tol = slab_sums(2e-5 * mag * s + 1e-7) + 32 * 6e-8 * slab_sums(np.abs(got))
+    assert np.all(np.abs(P - ref) <= tol)
+    assert np.all(np.abs(P - slab_sums(got)) <= 32 * 1.2e-7 * slab_sums(np.abs(got)) + 1e-7)
+
+
+@pytest.mark.parametrize("mmt", [0.0, 0.5])
+@pytest.mark.parametrize("rows,n_in,n_out", [(16, 24, 32), (1024, 2048, 2048), (1024, 440, 2048), (960, 1024, 135),
+                                             (1024, 2048, 4000)])
+def test_affine_update_bias(mmt, rows, n_in, n_out, gemm_cfg):
+    """weight SGD + bias SGD (bias gradient from slab sums) in one launch"""
+    X, E = rnd((rows, n_in), 12), rnd((rows, n_out), 13, 0.01)
+    W, corr = rnd((n_in, n_out), 14, 0.1), rnd((n_in, n_out), 15, 0.01)
+    b, corr_b = rnd(n_out, 18), rnd(n_out, 19, 0.01)
+    P = slab_sums(E).astype(np.float32)
+    scale, l2 = -0.3 / rows, -1e-4
+    dX, dE, dW = DeviceArray.from_numpy(X), DeviceArray.from_numpy(E), DeviceArray.from_numpy(W)
+    dP, db = DeviceArray.from_numpy(P), DeviceArray.vector(b)
+    dC = DeviceArray.from_numpy(corr) if mmt else None
+    dCb = DeviceArray.vector(corr_b) if mmt else None
+    check(lib().tnet_affine_update_bias(dX.ptr, dX.dim, dE.ptr, dE.dim, dW.ptr, dW.dim, dC.ptr if dC else None,
+                                        dC.stride if dC else 0, scale, mmt, l2, dP.ptr, dP.stride, db.ptr,
+                                        dCb.ptr if dCb else None, S()))
+    g, mag = gemm_ref("T", "N", X, E)
+    c = g + mmt * corr
+    w = W + scale * c
+    w = w + l2 * w
+    tol = 2e-5 * abs(scale) * mag + 2e-7 * np.abs(W) + 1e-7
+    assert np.all(np.abs(dW.numpy() - w) <= tol)
+    if mmt:
+        assert np.all(np.abs(dC.numpy() - c) <= 2e-5 * mag + 1e-6)
+    gb = P.astype(np.float64).sum(0).astype(np.float32).astype(np.float64)
+    cb = gb + mmt * corr_b
+    np.testing.assert_allclose(db.numpy().ravel(), b + scale * cb, rtol=1e-6, atol=1e-7)
+    if mmt:
+        np.testing.assert_allclose(dCb.numpy().ravel(), cb, rtol=1e-6, atol=1e-9)
 
 
 @pytest.mark.parametrize("rows,cols", [(1, 1), (16, 10), (1024, 135), (1024, 4000), (300, 4099), (64, 5000)])
