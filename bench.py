@@ -14,9 +14,11 @@ barrier / max-reduce of the timings; it is imported after the HIP library so one
 loaded.
 
 Extra JSON fields: roofline (dominant kernel = the 2048x2048 affine-layer GEMMs, timed with hipEvents
-on the library stream over K further steps of the same workload right after the timed region -- only
-those launches carry events, and the value region none, since every event pair adds stream time), kernels (per-kernel breakdown from extra all-events steps after the timed
-region), cpu_baseline (the reference CPU TNet on this host, rank 0 at N=1).
+on the library stream over K further steps of the same workload right after the timed region: one
+event pair per run of back-to-back roofline launches -- the 3 hidden forward GEMMs, and the 6 hidden
+backward + update GEMMs -- and none in the value region, since every event pair adds stream time),
+kernels (per-kernel breakdown from extra all-events steps after the timed region), cpu_baseline (the
+reference CPU TNet on this host, rank 0 at N=1).
 """
 import argparse
 import json
@@ -87,6 +89,9 @@ def parse_kernel_report(text):
     out = {}
     for line in text.strip().splitlines():
         tag, n, ms, work = line.split()
+        if tag.startswith("@runs:"):
+            out["@runs"] = {"runs": int(tag[6:]), "launches": int(n), "ms": float(ms), "work": float(work)}
+            continue
         out[tag] = {"launches": int(n), "ms": float(ms), "work": float(work)}
     return out
 
@@ -104,7 +109,8 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--kernel-timing", type=int, default=1,
                     help="hipEvent timing in the roofline region (K steps after the timed region): 0 off, 1 the "
-                         "roofline kernels only (2048x2048 GEMMs; each event pair costs stream time), 2 every launch")
+                         "roofline kernels (2048x2048 GEMMs), one event pair per RUN of back-to-back roofline "
+                         "launches (each pair costs stream time), 2 a pair around every roofline launch")
     ap.add_argument("--breakdown-steps", type=int, default=20,
                     help="extra steps after the timed region with every launch event-timed (kernels field)")
     args = ap.parse_args()
@@ -150,14 +156,14 @@ def main():
     trainer.replay(args.steps)
     barrier()
     dt = time.perf_counter() - t0
-    # roofline region: the next K steps of the same workload with hipEvent pairs around the
-    # roofline kernels only (each pair adds ~3 us of stream time, so not inside the value region)
+    # roofline region: the next K steps of the same workload with one hipEvent pair around each run of
+    # back-to-back roofline kernels (each pair adds ~3 us of stream time, so not inside the value region)
     import ctypes
     buf = ctypes.create_string_buffer(1 << 16)
     kern = {}
     if args.kernel_timing:
-        check(lib().tnet_kernel_timing_filter(b":2048x2048" if args.kernel_timing == 1 else b""), "timing_filter")
-        check(lib().tnet_kernel_timing(1), "kernel_timing")
+        check(lib().tnet_kernel_timing_filter(b":2048x2048"), "timing_filter")
+        check(lib().tnet_kernel_timing(2 if args.kernel_timing == 1 else 1), "kernel_timing")
         trainer.replay(args.steps)
         check(lib().tnet_kernel_timing(0), "kernel_timing")
         check(lib().tnet_kernel_timing_report(buf, len(buf)), "kernel_timing_report")
@@ -185,9 +191,10 @@ def main():
     hid = [v for k, v in kern.items() if k.startswith("gemm_") and k.endswith(":2048x2048")]
     roof = None
     if hid:
-        launches = sum(v["launches"] for v in hid)
-        ms = sum(v["ms"] for v in hid)
-        flops = sum(v["work"] for v in hid)
+        # run mode: exact totals of the event-bracketed runs (every launch in a run is a roofline GEMM)
+        tot = kern.get("@runs") or {"launches": sum(v["launches"] for v in hid), "ms": sum(v["ms"] for v in hid),
+                                    "work": sum(v["work"] for v in hid)}
+        launches, ms, flops = tot["launches"], tot["ms"], tot["work"]
         achieved = flops / (ms * 1e-3) / 1e12
         traffic, traffic_src = pmc_traffic()
         roof = {"bound": "mfma", "kernel": "gemm_f32 2048x2048 (fwd/bwd/update)", "achieved": round(achieved, 2),
@@ -196,9 +203,13 @@ def main():
                 "algorithmic_bytes_per_launch": 4.0 * ((2 * B * 2048 + 2048 ** 2) + (3 * B * 2048 + 2048 ** 2) +
                                                        (2 * B * 2048 + 2 * 2048 ** 2)) / 3,  # fwd, bwd, upd
                 "launches": launches, "avg_launch_us": round(1000.0 * ms / launches, 2),
-                "timing": f"hipEvent pairs on the library stream around each roofline launch, {args.steps} steps "
-                          "right after the value region",
+                "timing": (f"hipEvent pairs on the library stream around each run of back-to-back roofline launches "
+                           f"({kern['@runs']['runs']} runs), {args.steps} steps right after the value region"
+                           if "@runs" in kern else
+                           f"hipEvent pairs on the library stream around each roofline launch, {args.steps} steps "
+                           "right after the value region"),
                 "flops_per_launch": flops / launches}
+    breakdown.pop("@runs", None)
     all_gemm_ms = sum(v["ms"] for k, v in breakdown.items() if k.startswith("gemm_"))
     all_ms = sum(v["ms"] for v in breakdown.values())
     kernels = {k: {"launches": v["launches"], "avg_us": round(1000 * v["ms"] / v["launches"], 2),

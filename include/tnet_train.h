@@ -44,9 +44,11 @@ int tnet_memcpy_d2d(void* dst, const void* src, size_t bytes);
 int tnet_memset(void* dst, int value, size_t bytes);
 int tnet_set_profile(int on);                  /* CuDevice::Verbose + AccuProfile map */
 int tnet_profile_report(char* buf, int cap);
-/* Per-kernel device timing (hipEvent pairs around each launch of the fused SGD step, on the
- * library stream).  The report lists "tag count total_ms total_work" lines (work = algorithmic
- * FLOPs for GEMMs, bytes for HBM-bound kernels) accumulated since the last report. */
+/* Per-kernel device timing (hipEvent pairs on the library stream).  on = 1: a pair around each timed
+ * launch; on = 2: one pair per RUN of consecutive timed launches (a launch whose tag fails the filter
+ * ends the run), the run's time split over its tags by work share and the exact run totals on a
+ * "@runs:<n> launches total_ms total_work" line.  The report lists "tag count total_ms total_work"
+ * lines (work = algorithmic FLOPs for GEMMs, bytes for HBM-bound kernels) since the last report. */
 int tnet_kernel_timing(int on);
 /* time only launches whose tag contains `filter` ("" or NULL = all), e.g. ":2048x2048" */
 int tnet_kernel_timing_filter(const char* filter);

@@ -142,7 +142,7 @@ int tnet_profile_report(char* buf, int cap) {
 }
 
 int tnet_kernel_timing(int on) {
-  TRY_BEGIN CuDevice::Instantiate().KernelTiming(on != 0);
+  TRY_BEGIN CuDevice::Instantiate().KernelTiming(on == 2 ? 2 : on != 0 ? 1 : 0);
   TRY_END
 }
 int tnet_kernel_timing_filter(const char* filter) {

@@ -118,7 +118,31 @@ void CuDevice::KTRecord(const std::string& tag, double work, hipEvent_t a, hipEv
   mKT.push_back(KTRec{tag, work, a, b});
 }
 
+void CuDevice::KTRunBegin() {
+  if (mKTRunOpen) return;
+  KTRun r;
+  r.a = KTEvent();
+  TNET_HIP_CALL(hipEventRecord(r.a, mStream));
+  mKTRunList.push_back(r);
+  mKTRunOpen = true;
+}
+
+void CuDevice::KTRunAdd(const std::string& tag, double work) {
+  if (!mKTRunOpen) return;
+  auto& t = mKTRunList.back().tags[tag];
+  t.first++;
+  t.second += work;
+}
+
+void CuDevice::KTCloseRun() {
+  if (!mKTRunOpen) return;
+  mKTRunList.back().b = KTEvent();
+  TNET_HIP_CALL(hipEventRecord(mKTRunList.back().b, mStream));
+  mKTRunOpen = false;
+}
+
 std::string CuDevice::KTCollect() {
+  KTCloseRun();
   TNET_HIP_CALL(hipStreamSynchronize(mStream));
   struct Agg {
     long n = 0;
@@ -133,24 +157,58 @@ std::string CuDevice::KTCollect() {
     g.ms += ms;
     g.work += r.work;
   }
+  Agg runs;
+  long nruns = 0;
+  for (auto& r : mKTRunList) {
+    float ms = 0.f;
+    TNET_HIP_CALL(hipEventElapsedTime(&ms, r.a, r.b));
+    double work = 0;
+    for (auto& t : r.tags) work += t.second.second;
+    for (auto& t : r.tags) {
+      Agg& g = agg[t.first];
+      g.n += t.second.first;
+      g.ms += work > 0 ? ms * t.second.second / work : 0.0;
+      g.work += t.second.second;
+      runs.n += t.second.first;
+    }
+    runs.ms += ms;
+    runs.work += work;
+    nruns++;
+  }
   mKT.clear();
+  mKTRunList.clear();
   mKTNext = 0;
   std::ostringstream os;
   os.precision(10);
   for (auto& kv : agg) os << kv.first << " " << kv.second.n << " " << kv.second.ms << " " << kv.second.work << "\n";
+  if (nruns) os << "@runs:" << nruns << " " << runs.n << " " << runs.ms << " " << runs.work << "\n";
   return os.str();
 }
 
 KTScope::KTScope(const std::string& tag, double work) : mTag(tag), mWork(work) {
   CuDevice& d = CuDevice::Instantiate();
+  if (!d.KernelTiming()) return;
+  if (d.KernelTimingRuns()) {
+    if (d.KernelTimed(tag)) {
+      d.KTRunBegin();
+      mRun = true;
+    } else {
+      d.KTCloseRun();
+    }
+    return;
+  }
   if (!d.KernelTimed(tag)) return;
   mA = d.KTEvent();
   TNET_HIP_CALL(hipEventRecord(mA, d.Stream()));
 }
 
 KTScope::~KTScope() {
-  if (!mA) return;
   CuDevice& d = CuDevice::Instantiate();
+  if (mRun) {
+    d.KTRunAdd(mTag, mWork);
+    return;
+  }
+  if (!mA) return;
   hipEvent_t b = d.KTEvent();
   (void)hipEventRecord(b, d.Stream());
   d.KTRecord(mTag, mWork, mA, b);

@@ -40,8 +40,23 @@ class CuDevice {
   const std::map<std::string, double>& ProfileMap() const { return mProfileMap; }
 
   // ---- per-kernel device timing (hipEvent pairs around launches; off by default)
-  void KernelTiming(bool on) { mKTOn = on; }
+  /// mode 0 off; 1 an event pair around every timed launch; 2 RUNS: consecutive timed launches share
+  /// one event pair (a scope whose tag fails the filter, or the report, closes the run), so a chain of
+  /// back-to-back timed kernels carries one pair instead of one per launch.  A run's time is split over
+  /// its tags by work share; the exact run totals are reported on a "@runs" line.
+  void KernelTiming(int mode) {
+    if (mode == 0) KTCloseRun();
+    mKTOn = mode != 0;
+    mKTRuns = mode == 2;
+  }
   bool KernelTiming() const { return mKTOn; }
+  bool KernelTimingRuns() const { return mKTRuns; }
+  /// run mode: a timed launch begins (opens a run unless one is open)
+  void KTRunBegin();
+  /// run mode: a timed launch ended (its work joins the open run)
+  void KTRunAdd(const std::string& tag, double work);
+  /// run mode: an untimed launch begins / the report is taken: close the open run
+  void KTCloseRun();
   /// time only the launches whose tag contains `filter` (empty = all): each event pair costs
   /// a few microseconds of stream time, so a benchmark times only the kernel it reports
   void KernelTimingFilter(const std::string& filter) { mKTFilter = filter; }
@@ -78,7 +93,14 @@ class CuDevice {
   void* mWs = nullptr;
   size_t mWsBytes = 0;
   bool mKTOn = false;
+  bool mKTRuns = false;
   std::string mKTFilter;
+  struct KTRun {
+    std::map<std::string, std::pair<long, double>> tags;  // tag -> (launches, work)
+    hipEvent_t a = nullptr, b = nullptr;
+  };
+  std::vector<KTRun> mKTRunList;
+  bool mKTRunOpen = false;
   struct KTRec {
     std::string tag;
     double work;
@@ -99,6 +121,7 @@ class KTScope {
   std::string mTag;
   double mWork;
   hipEvent_t mA = nullptr;
+  bool mRun = false;
 };
 
 /// RAII profile scope: times the enqueued work of one op when profiling is on.

@@ -921,9 +921,60 @@ void gemm16_kernel(const GemmP p) {
   }
   wait_vmcnt<0>();  // repeat loads of the last tile still land in LDS
   TNET_STAMP(2);
-  if (K % BK) {
-    // masked tail k-tile through registers, same images, in slot nfull % S (the final seam read
-    // it: every wave's reads retire before the barrier)
+  if (!LDR && K % BK && K % 4 == 0) {
+    // partial last k-tile (Kt = K % BK deep) through the same LDS-DMA images, in slot nfull % S (the
+    // final seam read it: every wave's reads retire before the barrier).  Sources past K are clamped
+    // to valid memory (last k column / row) and the fragments with k >= Kt are zeroed in registers.
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+    __builtin_amdgcn_s_barrier();
+    float* st = smem + (nfull % S) * ST_SZ;
+    const int k0 = nfull * BK, Kt = K - k0;
+#pragma unroll
+    for (int g = 0; g < GA; ++g) {
+      const int u = (g * NW + wid) * 64 + lane;
+      long off;
+      if (A_KC) {
+        const int r = u / CH, j = u % CH, kc = k0 + 4 * (j ^ swz<BK>(r));
+        off = (long)min(bm + r, M - 1) * p.lda + (kc < K ? kc : K - 4);
+      } else {
+        const int k = u / (BM / 4), c = (u % (BM / 4)) * 4;
+        off = (long)min(k0 + k, K - 1) * p.lda + (bm + c < M ? bm + c : 0);
+      }
+      __builtin_amdgcn_global_load_lds((const void*)(p.A + off), (void*)(st + (g * NW + wid) * 256), 16, 0, 0);
+    }
+#pragma unroll
+    for (int g = 0; g < GB; ++g) {
+      const int u = (g * NW + wid) * 64 + lane;
+      long off;
+      if (B_KC) {
+        const int r = u / CH, j = u % CH, kc = k0 + 4 * (j ^ swz<BK>(r));
+        off = (long)min(bn + r, N - 1) * p.ldb + (kc < K ? kc : K - 4);
+      } else {
+        const int k = u / (BN / 4), c = (u % (BN / 4)) * 4;
+        off = (long)min(k0 + k, K - 1) * p.ldb + (bn + c < N ? bn + c : 0);
+      }
+      __builtin_amdgcn_global_load_lds((const void*)(p.B + off), (void*)(st + A_SZ + (g * NW + wid) * 256), 16, 0,
+                                       0);
+    }
+    wait_vmcnt<0>();
+    barrier();
+#pragma unroll
+    for (int c = 0; c < KCH; ++c) {
+      if (16 * c >= Kt) break;
+      read_frags(st, c, 0);
+#pragma unroll
+      for (int s2 = 0; s2 < 4; ++s2) {
+        const bool ok = 16 * c + 4 * lg + s2 < Kt;  // k of this lane's operand elements in MFMA step s2
+#pragma unroll
+        for (int a = 0; a < TM; ++a) av[0][a][s2] = ok ? av[0][a][s2] : 0.f;
+#pragma unroll
+        for (int b = 0; b < TN; ++b) bv[0][b][s2] = ok ? bv[0][b][s2] : 0.f;
+      }
+      mfmas(0);
+    }
+  } else if (K % BK) {
+    // K not a multiple of 4 (or the loader-wave variant): masked tail k-tile through registers,
+    // same images, in slot nfull % S
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
     __builtin_amdgcn_s_barrier();
     float* st = smem + (nfull % S) * ST_SZ;
@@ -1176,8 +1227,8 @@ static int launch_gemm(const GemmP& p_in, hipStream_t st) {
     // still gives ~one workgroup per CU (256 CUs), the 16x16x4 kernel where the layout allows
     const long t128 = (long)cdiv(p.M, 128) * cdiv(p.N, 128), t64x128 = (long)cdiv(p.M, 64) * cdiv(p.N, 128);
     if (t128 >= 240) cfg = CFG_m128x128k64s2;
+    else if (A_KC && t64x128 >= 200) cfg = CFG_m64x128k64s2;  // incl. the K = 440 first layer (one round)
     else if (A_KC && p.K < 1024) cfg = CFG_m64x64k32s4w41;
-    else if (A_KC && t64x128 >= 200) cfg = CFG_m64x128k64s2;
     else cfg = CFG_g64x64k32s4w4;
   }
   p.group = g_group > 0 ? g_group : 8;

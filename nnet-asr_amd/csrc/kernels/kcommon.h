@@ -28,8 +28,14 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
-// sigmoid with the reference's double constants (cukernels.cu:192-206): 1.0/(1.0+exp(-x))
-__device__ __forceinline__ float sigmoidf_ref(float x) { return 1.0f / (1.0f + expf(-x)); }
+// sigmoid 1/(1+exp(-x)) (cukernels.cu:192-206) on the hardware transcendentals: v_exp_f32 of
+// -x*log2(e) and v_rcp_f32 -- 3 VALU instead of ocml expf + an IEEE division (~25), which made the
+// sigmoid the largest part of the fused forward GEMM's epilogue.  Error <= ~3e-7 absolute for
+// |x| <= 16 (the scaled exponent's rounding, damped by sigma(1-sigma) <= 1/4), well inside the
+// kernel tests' 2e-6; exp overflow / underflow give exactly 0 / 1.
+__device__ __forceinline__ float sigmoidf_ref(float x) {
+  return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-1.44269504088896341f * x));
+}
 
 inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }
 

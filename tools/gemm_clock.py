@@ -8,7 +8,7 @@ Per workgroup (wave 0): s_memtime at entry / after the prologue / after the main
 epilogue, s_memrealtime (100 MHz) at entry and exit.  Reports the median in-kernel clock, the cycle
 split, the MFMA-issue floor of the main loop (MFMAs of one wave x 32 cycles) and the launch spread.
 
-usage: python tools/gemm_clock.py [warm_s] [reps] [cfg]"""
+usage: python tools/gemm_clock.py [warm_s] [reps] [cfg|auto] [rows,n_in,n_out] [kinds]"""
 import ctypes as C
 import json
 import os
@@ -16,7 +16,7 @@ import sys
 import time
 
 os.environ.setdefault("TNET_DIAG_STAMP_LIB", "1")  # or nodma / noread / nobar (ablation builds)
-if len(sys.argv) > 3:
+if len(sys.argv) > 3 and sys.argv[3] != "auto":
     os.environ["TNET_GEMM_CFG"] = sys.argv[3]
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "nnet-asr_amd"))
@@ -26,7 +26,8 @@ from tnet_amd._lib import check, lib  # noqa: E402
 
 warm_s = float(sys.argv[1]) if len(sys.argv) > 1 else 1.5
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 5
-rows, ni, no = 1024, 2048, 2048
+rows, ni, no = (int(x) for x in sys.argv[4].split(",")) if len(sys.argv) > 4 else (1024, 2048, 2048)
+KINDS = sys.argv[5].split(",") if len(sys.argv) > 5 else ["fwd", "bwd", "upd"]
 L = lib()
 L.tnet_diag_stamps.restype = C.c_int
 L.tnet_diag_stamps.argtypes = [C.c_void_p, C.c_int]
@@ -53,7 +54,7 @@ def warm():
     t0 = time.time()
     while time.time() - t0 < warm_s:
         for _ in range(30):
-            for k in ("fwd", "bwd", "upd"):
+            for k in KINDS:
                 run(k)
         check(L.tnet_synchronize())
 
@@ -61,7 +62,7 @@ def warm():
 out = {}
 nwg = 256  # 64x128 / 128x128 tiles of the 2048x2048 layer at bunch 1024
 buf = (C.c_ulonglong * (6 * 8192))()
-for kind in ("fwd", "bwd", "upd"):
+for kind in KINDS:
     recs = []
     for _ in range(reps):
         warm()
