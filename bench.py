@@ -107,6 +107,9 @@ def main():
     ap.add_argument("--lr", type=float, default=1.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--force-dp", action="store_true",
+                    help="diagnostic: run the data-parallel path (gradient GEMMs + RCCL all-reduce + SGD apply) "
+                         "even at N=1, on a one-rank RCCL communicator")
     ap.add_argument("--kernel-timing", type=int, default=1,
                     help="hipEvent timing in the roofline region (K steps after the timed region): 0 off, 1 the "
                          "roofline kernels (2048x2048 GEMMs), one event pair per RUN of back-to-back roofline "
@@ -130,6 +133,8 @@ def main():
         uid = [Comm.unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
         comm = Comm(rank, world, uid[0])
+    elif args.force_dp:
+        comm = Comm(0, 1, Comm.unique_id())
 
     net = build_network(dims)
     net.set_learn_rate(args.lr)
@@ -234,7 +239,7 @@ def main():
             "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
             "config": {"workload": f"TNet SGD step, {'x'.join(map(str, dims))} sigmoid MLP + softmax xent",
                        "bunch_per_gpu": B, "global_bunch": B * world, "frames_resident_per_gpu": args.cache,
-                       "parallelism": f"dp{world}" + (" (RCCL all-reduce)" if world > 1 else ""),
+                       "parallelism": f"dp{world}" + (" (RCCL all-reduce)" if world > 1 or args.force_dp else ""),
                        "flops_per_frame": flops_per_frame(dims),
                        "achieved_tflops_whole_step": round(value * flops_per_frame(dims) / 1e12 / world, 2),
                        "gemm_share_of_kernel_time": round(all_gemm_ms / all_ms, 4) if all_ms else None},

@@ -778,26 +778,33 @@ void gemm16_kernel(const GemmP p) {
       pre_bias[j] = v;
     }
   }
-  if constexpr (PRE_C || PRE_AUX) {
-    const float* base = PRE_AUX ? p.aux : p.C;
-    const long ld = PRE_AUX ? p.ldaux : p.ldc;
-#pragma unroll
-    for (int a = 0; a < TM; ++a)
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) pre_a[a][r][j] = ld_tile(base, ld, erow(a, r), ecol(j));
-  }
-  if constexpr (PRE_Q) {
-    if (has_q) {
+  // tiles of more than 128 prefetched floats per lane (128x256 tiles) are loaded at the epilogue
+  // instead, all at once (one round trip): held across the main loop they would spill
+  constexpr int PRE_TILE = TM * 4 * NJ * (EV ? 4 : 1);
+  constexpr bool EARLY = ((PRE_C || PRE_AUX) ? PRE_TILE : 0) + (PRE_Q ? PRE_TILE : 0) <= 128;
+  auto prefetch_tiles = [&]() {
+    if constexpr (PRE_C || PRE_AUX) {
+      const float* base = PRE_AUX ? p.aux : p.C;
+      const long ld = PRE_AUX ? p.ldaux : p.ldc;
 #pragma unroll
       for (int a = 0; a < TM; ++a)
 #pragma unroll
         for (int r = 0; r < 4; ++r)
 #pragma unroll
-          for (int j = 0; j < NJ; ++j) pre_q[a][r][j] = ld_tile(p.corr, p.ldcorr, erow(a, r), ecol(j));
+          for (int j = 0; j < NJ; ++j) pre_a[a][r][j] = ld_tile(base, ld, erow(a, r), ecol(j));
     }
-  }
+    if constexpr (PRE_Q) {
+      if (has_q) {
+#pragma unroll
+        for (int a = 0; a < TM; ++a)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) pre_q[a][r][j] = ld_tile(p.corr, p.ldcorr, erow(a, r), ecol(j));
+      }
+    }
+  };
+  if constexpr (EARLY) prefetch_tiles();
 
   static_assert(EPI != EPI_SGD_B || BN <= NT, "one thread per bias column");
   BiasPre bpre;
@@ -1016,6 +1023,7 @@ void gemm16_kernel(const GemmP p) {
   if constexpr (EPI == EPI_SGD_B)
     if (bm == 0) bias_pre_finish<BN>(p, bn, bpre);
 
+  if constexpr (!EARLY) prefetch_tiles();
   // ---- epilogue: arithmetic on the prefetched operands, then 16-B (n-contiguous) or 4-B stores
   // EPI_DSIG_CS: each wave owns 32 output rows (one slab) x its columns; a lane sums its 8 rows of
   // a column in order, the 4 lane groups of a column meet by two xor-shuffles
@@ -1151,7 +1159,9 @@ void gemm16_kernel(const GemmP p) {
   X(m64x128k32s4w42p, 1, 64, 128, 32, 4, 2, 4, 1)        \
   X(m128x128k32s3p, 1, 128, 128, 32, 2, 2, 3, 1)         \
   X(m128x128k32s4p, 1, 128, 128, 32, 2, 2, 4, 1)         \
-  X(m64x128k64s2L, 1, 64, 128, 64, 2, 2, 2, 2)
+  X(m64x128k64s2L, 1, 64, 128, 64, 2, 2, 2, 2)           \
+  X(m128x256k32s3, 1, 128, 256, 32, 2, 2, 3, 0)          \
+  X(m128x256k32s2, 1, 128, 256, 32, 2, 2, 2, 0)
 
 enum GemmCfg {
 #define X(name, ...) CFG_##name,
@@ -1226,7 +1236,9 @@ static int launch_gemm(const GemmP& p_in, hipStream_t st) {
     // measured per-shape choice (tools/gemm_sweep.py on MI355X, round 1): the largest tile that
     // still gives ~one workgroup per CU (256 CUs), the 16x16x4 kernel where the layout allows
     const long t128 = (long)cdiv(p.M, 128) * cdiv(p.N, 128), t64x128 = (long)cdiv(p.M, 64) * cdiv(p.N, 128);
-    if (t128 >= 240) cfg = CFG_m128x128k64s2;
+    const long t128x256 = (long)cdiv(p.M, 128) * cdiv(p.N, 256);
+    if (!A_KC && t128x256 >= 240) cfg = CFG_m128x256k32s3;  // one round where 128x128 needs two
+    else if (t128 >= 240) cfg = CFG_m128x128k64s2;
     else if (A_KC && t64x128 >= 200) cfg = CFG_m64x128k64s2;  // incl. the K = 440 first layer (one round)
     else if (A_KC && p.K < 1024) cfg = CFG_m64x64k32s4w41;
     else cfg = CFG_g64x64k32s4w4;
