@@ -182,10 +182,24 @@ int tnet_affine_update_bias(const float* X, TnetMatrixDim dX, const float* E, Tn
 /* G = X^T E into a gradient buffer (data-parallel path: all-reduced before tnet_sgd_update). */
 int tnet_affine_grad(const float* X, TnetMatrixDim dX, const float* E, TnetMatrixDim dE, float* G,
                      TnetMatrixDim dG, void* stream);
+/* tnet_affine_grad + gradB = colsum(E) from the 32-row slab sums tnet_affine_bwd_colsum wrote for E
+ * (data-parallel path: both gradients are all-reduced, then applied by tnet_sgd_update_multi). */
+int tnet_affine_grad_bias(const float* X, TnetMatrixDim dX, const float* E, TnetMatrixDim dE, float* G,
+                          TnetMatrixDim dG, const float* colpart, int ldcolpart, float* gradB, void* stream);
 /* Element-wise SGD of the same formula on flat arrays:  c = g + mmt*corr; p += scale*c; p += l2*p;
  * corr = c (corr may be NULL when mmt == 0). */
 int tnet_sgd_update(float* p, const float* g, float* corr, long n, float scale, float mmt, float l2,
                     void* stream);
+/* The same SGD over several flat segments in ONE launch (a layer's W and b after the all-reduce):
+ * per segment k: c = g + mmt*corr; p += scale*c; p += l2_k*p; corr = c. */
+typedef struct TnetSgdSeg_ {
+  float* p;
+  const float* g;
+  float* corr; /* NULL when mmt == 0 */
+  long n;
+  float l2;
+} TnetSgdSeg;
+int tnet_sgd_update_multi(const TnetSgdSeg* segs, int nseg, float scale, float mmt, void* stream);
 /* Bias update from the error matrix E (CuVector::AddColSum + AddScaled, cuBiasedLinearity.cc:56-59):
  *   c = colsum(E) + mmt*corr_b ; b += scale * c ; corr_b = c   (corr_b may be NULL if mmt == 0)
  * If grad_out != NULL the raw colsum is written there instead and b is not touched (DP path). */

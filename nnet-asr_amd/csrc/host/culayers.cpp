@@ -151,6 +151,18 @@ void CuBiasedLinearity::ComputeGradient() {
   TNET_SAFE_CALL(tnet_bias_update(E.pCUData(), dE, nullptr, nullptr, mGradB.pCUData(), 0.f, 0.f, ws, S));
 }
 
+void CuBiasedLinearity::ComputeGradientColsum(const CuMatrix<BaseFloat>& colpart) {
+  CuProfileScope p("CuBiasedLinearity::ComputeGradient");
+  const CuMatrix<BaseFloat>& X = GetInput();
+  const CuMatrix<BaseFloat>& E = GetErrorInput();
+  mGradW.Init(mLinearity.Rows(), mLinearity.Cols());
+  mGradB.Init(mBias.Dim());
+  KTScope kt("gemm_grad:" + std::to_string(GetNInputs()) + "x" + std::to_string(GetNOutputs()),
+             2.0 * X.Rows() * GetNInputs() * GetNOutputs());
+  TNET_SAFE_CALL(tnet_affine_grad_bias(X.pCUData(), X.Dim(), E.pCUData(), E.Dim(), mGradW.pCUData(), mGradW.Dim(),
+                                       colpart.pCUData(), (int)colpart.Stride(), mGradB.pCUData(), S));
+}
+
 std::vector<CuParamBlock> CuBiasedLinearity::GradientBlocks() {
   mGradW.Init(mLinearity.Rows(), mLinearity.Cols());
   mGradB.Init(mBias.Dim());
@@ -163,11 +175,15 @@ void CuBiasedLinearity::ApplyGradient(size_t frames) {
   float scale, l2;
   UpdateConstants(frames, &scale, &l2);
   const bool mmt = mMomentum != 0.0f;
-  // padding columns of W and of the gradient are zero, so the flat update keeps them zero
-  TNET_SAFE_CALL(tnet_sgd_update(mLinearity.pCUData(), mGradW.pCUData(), mmt ? mLinearityCorrection.pCUData() : nullptr,
-                                 (long)(mLinearity.Rows() * mLinearity.Stride()), scale, mMomentum, l2, S));
-  TNET_SAFE_CALL(tnet_sgd_update(mBias.pCUData(), mGradB.pCUData(), mmt ? mBiasCorrection.pCUData() : nullptr,
-                                 (long)mBias.Dim(), scale, mMomentum, 0.f, S));
+  // padding columns of W and of the gradient are zero, so the flat update keeps them zero; W and b
+  // in one launch
+  TnetSgdSeg seg[2] = {
+      {mLinearity.pCUData(), mGradW.pCUData(), mmt ? mLinearityCorrection.pCUData() : nullptr,
+       (long)(mLinearity.Rows() * mLinearity.Stride()), l2},
+      {mBias.pCUData(), mGradB.pCUData(), mmt ? mBiasCorrection.pCUData() : nullptr, (long)mBias.Dim(), 0.f}};
+  KTScope kt("sgd_apply:" + std::to_string(GetNInputs()) + "x" + std::to_string(GetNOutputs()),
+             12.0 * (double)(mLinearity.Rows() * mLinearity.Stride() + mBias.Dim()));
+  TNET_SAFE_CALL(tnet_sgd_update_multi(seg, 2, scale, mMomentum, S));
 }
 
 void CuBiasedLinearity::ReadFromStream(std::istream& rIn) {

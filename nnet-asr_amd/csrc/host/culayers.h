@@ -23,6 +23,8 @@ class CuBiasedLinearity : public CuUpdatableComponent {
   void BackpropagateFnc(const CuMatrix<BaseFloat>& X, CuMatrix<BaseFloat>& Y) override;
   void Update() override;
   void ComputeGradient() override;
+  // ComputeGradient with the bias gradient from the slab column sums of E (tnet_affine_grad_bias)
+  void ComputeGradientColsum(const CuMatrix<BaseFloat>& colpart);
   void ApplyGradient(size_t frames) override;
   std::vector<CuParamBlock> GradientBlocks() override;
 

@@ -286,6 +286,7 @@ void CuNetwork::TrainBunch(const CuMatrix<BaseFloat>& X, const CuVector<int>& la
 
   // ---- backward + update, top to bottom (error uses the pre-update weights of the layer)
   const CuMatrix<BaseFloat>* err = &mGlobErr;
+  std::vector<CuBiasedLinearity*> submitted;  // data-parallel: layers in reduction order
   bool err_colsum = false;  // slab column sums of *err are in mColPart[l] (bias gradient fused, no exchange)
   for (int l = nl - 1; l >= 0; l--) {
     auto* lin = static_cast<CuBiasedLinearity*>(mNetComponents[2 * l]);
@@ -300,7 +301,7 @@ void CuNetwork::TrainBunch(const CuMatrix<BaseFloat>& X, const CuVector<int>& la
       // E_l = (E_{l+1} W_l^T) .* y_l (1 - y_l)   (backprop through <biasedlinearity> and the <sigmoid> below);
       // when the layer below is trained here, the same launch writes the bias gradient of E_l as slab sums
       auto* below = static_cast<CuBiasedLinearity*>(mNetComponents[2 * (l - 1)]);
-      if (!exchange && below->LearnRate() > 0.0f) {
+      if (below->LearnRate() > 0.0f) {
         CuMatrix<BaseFloat>& cp = *mColPart[l - 1];
         cp.Init(tnet_colsum_slabs((int)rows), lin->GetNInputs());
         const int st = tnet_affine_bwd_colsum(err->pCUData(), err->Dim(), lin->Linearity().pCUData(),
@@ -320,8 +321,12 @@ void CuNetwork::TrainBunch(const CuMatrix<BaseFloat>& X, const CuVector<int>& la
       if (exchange) {
         lin->SetInput(*acts[l]);
         lin->SetErrorInput(*err);
-        lin->ComputeGradient();
+        if (err_colsum)
+          lin->ComputeGradientColsum(*mColPart[l]);
+        else
+          lin->ComputeGradient();
         exchange->Submit(*lin);
+        submitted.push_back(lin);
       } else if (err_colsum) {
         lin->UpdateFromColsum(*acts[l], *err, *mColPart[l]);
       } else {
@@ -333,13 +338,14 @@ void CuNetwork::TrainBunch(const CuMatrix<BaseFloat>& X, const CuVector<int>& la
     err_colsum = eo_colsum;
   }
   if (exchange) {
-    exchange->WaitAll();
+    // apply each layer as soon as its own reduction is done (top layer first): the applies overlap
+    // the reductions of the layers below
     const size_t grows = exchange->GlobalRows(rows);
-    for (int l = nl - 1; l >= 0; l--) {
-      auto* lin = static_cast<CuBiasedLinearity*>(mNetComponents[2 * l]);
-      if (lin->LearnRate() > 0.0f) lin->ApplyGradient(grows);
-      if (lin == mpPropagErrorStopper) break;
+    for (size_t i = 0; i < submitted.size(); i++) {
+      exchange->WaitFor((int)i);
+      submitted[i]->ApplyGradient(grows);
     }
+    exchange->WaitAll();
   }
   // restore the component wiring the generic path relies on
   for (int l = 0; l < nl; l++) {

@@ -26,6 +26,12 @@ class GradExchange {
   virtual void Submit(CuUpdatableComponent& comp) = 0;
   /// Make the compute stream wait until every submitted reduction has finished.
   virtual void WaitAll() = 0;
+  /// Make the compute stream wait for the i-th reduction submitted since the last WaitAll() (the
+  /// apply of that layer can then overlap the reductions still running); default: WaitAll().
+  virtual void WaitFor(int i) {
+    (void)i;
+    WaitAll();
+  }
   /// Sum small host statistics over ranks (epoch-end MergeStats, step planning); blocking.
   virtual void AllReduceHost(double* v, int n) = 0;
 

@@ -196,7 +196,8 @@ void HostExchange::AllReduceHost(double* v, int n) {
 struct RcclExchange::Impl {
   ncclComm_t comm = nullptr;
   hipStream_t comm_stream = nullptr;
-  std::vector<hipEvent_t> events;
+  std::vector<hipEvent_t> events;     // compute stream -> comm stream (gradient ready), per submit
+  std::vector<hipEvent_t> ar_done;    // comm stream -> compute stream (reduction done), per submit
   size_t next_event = 0;
   hipEvent_t done = nullptr;
   double* dscratch = nullptr;
@@ -224,6 +225,7 @@ RcclExchange::~RcclExchange() {
   if (!mImpl) return;
   (void)hipStreamSynchronize(mImpl->comm_stream);
   for (auto e : mImpl->events) (void)hipEventDestroy(e);
+  for (auto e : mImpl->ar_done) (void)hipEventDestroy(e);
   if (mImpl->done) (void)hipEventDestroy(mImpl->done);
   if (mImpl->dscratch) (void)hipFree(mImpl->dscratch);
   if (mImpl->comm) (void)ncclCommDestroy(mImpl->comm);
@@ -233,11 +235,14 @@ RcclExchange::~RcclExchange() {
 void RcclExchange::Submit(CuUpdatableComponent& comp) {
   CuDevice& dev = CuDevice::Instantiate();
   if (mImpl->next_event >= mImpl->events.size()) {
-    hipEvent_t e;
+    hipEvent_t e, d;
     TNET_HIP_CALL(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    TNET_HIP_CALL(hipEventCreateWithFlags(&d, hipEventDisableTiming));
     mImpl->events.push_back(e);
+    mImpl->ar_done.push_back(d);
   }
-  hipEvent_t ev = mImpl->events[mImpl->next_event++];
+  const size_t idx = mImpl->next_event++;
+  hipEvent_t ev = mImpl->events[idx];
   // the gradient kernels were enqueued on the compute stream: order the reduction after them
   TNET_HIP_CALL(hipEventRecord(ev, dev.Stream()));
   TNET_HIP_CALL(hipStreamWaitEvent(mImpl->comm_stream, ev, 0));
@@ -246,6 +251,12 @@ void RcclExchange::Submit(CuUpdatableComponent& comp) {
   for (auto& b : blocks)
     NCCL_CALL(ncclAllReduce(b.grad, b.grad, (size_t)b.n, ncclFloat, ncclSum, mImpl->comm, mImpl->comm_stream));
   NCCL_CALL(ncclGroupEnd());
+  TNET_HIP_CALL(hipEventRecord(mImpl->ar_done[idx], mImpl->comm_stream));
+}
+
+void RcclExchange::WaitFor(int i) {
+  if (i < 0 || (size_t)i >= mImpl->next_event) Error("RcclExchange::WaitFor: no such reduction");
+  TNET_HIP_CALL(hipStreamWaitEvent(CuDevice::Instantiate().Stream(), mImpl->ar_done[(size_t)i], 0));
 }
 
 void RcclExchange::WaitAll() {

@@ -7,6 +7,8 @@
 // stride and width allow it, and a scalar tail otherwise; no sync, caller's stream.
 #include <float.h>
 
+#include <algorithm>
+
 #include "kcommon.h"
 
 namespace tnetk {
@@ -123,6 +125,54 @@ __global__ __launch_bounds__(EW_THREADS) void sgd_kernel(float* __restrict__ p, 
     w = w + scale * c;
     w = w + l2 * w;
     p[i] = w;
+  }
+}
+
+// several SGD segments (a layer's W and b, ...) in one launch: block b serves the segment whose
+// [first, first + nblk) block range holds it (uniform per block), 16-B accesses where aligned
+constexpr int SGD_MAXSEG = 8;
+struct SgdSegs {
+  TnetSgdSeg s[SGD_MAXSEG];
+  int first[SGD_MAXSEG + 1];
+  int nseg;
+};
+__global__ __launch_bounds__(EW_THREADS) void sgd_multi_kernel(const SgdSegs segs, float scale, float mmt) {
+  int k = 0;
+  while (k + 1 < segs.nseg && (int)blockIdx.x >= segs.first[k + 1]) ++k;
+  const TnetSgdSeg sg = segs.s[k];
+  const long nb = segs.first[k + 1] - segs.first[k];
+  const long t0 = (long)(blockIdx.x - segs.first[k]) * blockDim.x + threadIdx.x, step = nb * blockDim.x;
+  const bool v4 = ((sg.n & 3) == 0) && (((uintptr_t)sg.p | (uintptr_t)sg.g | (uintptr_t)sg.corr) & 15) == 0;
+  if (v4) {
+    f32x4* p = reinterpret_cast<f32x4*>(sg.p);
+    const f32x4* g = reinterpret_cast<const f32x4*>(sg.g);
+    f32x4* q = reinterpret_cast<f32x4*>(sg.corr);
+    for (long i = t0; i < sg.n / 4; i += step) {
+      f32x4 c = g[i];
+      if (q) {
+        c = c + mmt * q[i];
+        q[i] = c;
+      }
+      f32x4 w = p[i];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        w[e] = w[e] + scale * c[e];
+        w[e] = w[e] + sg.l2 * w[e];
+      }
+      p[i] = w;
+    }
+  } else {
+    for (long i = t0; i < sg.n; i += step) {
+      float c = sg.g[i];
+      if (sg.corr) {
+        c = c + mmt * sg.corr[i];
+        sg.corr[i] = c;
+      }
+      float w = sg.p[i];
+      w = w + scale * c;
+      w = w + sg.l2 * w;
+      sg.p[i] = w;
+    }
   }
 }
 
@@ -265,5 +315,34 @@ extern "C" int tnet_sgd_update(float* p, const float* g, float* corr, long n, fl
   if (!n) return TNET_OK;
   sgd_kernel<<<ew_grid(n), EW_THREADS, 0, STREAM>>>(p, g, corr, n, scale, mmt, l2);
   TNET_LAUNCH_CHECK();
+  return TNET_OK;
+}
+
+extern "C" int tnet_sgd_update_multi(const TnetSgdSeg* segs, int nseg, float scale, float mmt, void* stream) {
+  if (nseg < 0 || (nseg && !segs)) return TNET_ERR_ARG;
+  for (int k0 = 0; k0 < nseg; k0 += SGD_MAXSEG) {
+    SgdSegs a{};
+    long total = 0;
+    int blocks = 0;
+    a.nseg = 0;
+    for (int k = k0; k < nseg && k < k0 + SGD_MAXSEG; ++k) {
+      const TnetSgdSeg& sg = segs[k];
+      if (sg.n < 0 || (sg.n && (!sg.p || !sg.g)) || (mmt != 0.f && sg.n && !sg.corr)) return TNET_ERR_ARG;
+      if (!sg.n) continue;
+      total += sg.n;
+      a.s[a.nseg++] = sg;
+    }
+    if (!a.nseg) continue;
+    // blocks proportional to the segment sizes (at least one each): one 16-B vector per thread per
+    // pass, the whole launch capped at 8192 blocks (grid-stride beyond)
+    const long want = std::min(8192L, (total / 4 + EW_THREADS - 1) / EW_THREADS);
+    for (int k = 0; k < a.nseg; ++k) {
+      a.first[k] = blocks;
+      blocks += (int)std::max(1L, (long)((double)want * a.s[k].n / total + 0.5));
+    }
+    a.first[a.nseg] = blocks;
+    sgd_multi_kernel<<<blocks, EW_THREADS, 0, STREAM>>>(a, scale, mmt);
+    TNET_LAUNCH_CHECK();
+  }
   return TNET_OK;
 }

@@ -38,10 +38,16 @@ enum { EPI_STORE = 0, EPI_BIAS = 1, EPI_BIAS_SIG = 2, EPI_DSIG = 3, EPI_SGD = 4,
        // fused bias gradient (16x16 kernel): EPI_DSIG_CS = EPI_DSIG + per-32-row-slab column sums of the
        // output (the bias gradient of the layer below); EPI_SGD_B = EPI_SGD + that layer's bias SGD from
        // the slab sums, done by the first tile-row's workgroups in the prologue
-       EPI_DSIG_CS = 8, EPI_SGD_B = 9 };
+       EPI_DSIG_CS = 8, EPI_SGD_B = 9,
+       // data-parallel gradient: EPI_STORE of X^T E plus the raw bias gradient from the slab sums
+       EPI_STORE_BG = 10 };
 constexpr int kColsumSlabRows = 32;
 // base epilogue of a fused one
-constexpr int epi_base(int e) { return e == EPI_DSIG_CS ? EPI_DSIG : e == EPI_SGD_B ? EPI_SGD : e; }
+constexpr int epi_base(int e) {
+  return e == EPI_DSIG_CS ? EPI_DSIG : e == EPI_SGD_B ? EPI_SGD : e == EPI_STORE_BG ? EPI_STORE : e;
+}
+// epilogues that also produce the bias (SGD update or raw gradient) from slab sums
+constexpr bool epi_bias_slabs(int e) { return e == EPI_SGD_B || e == EPI_STORE_BG; }
 
 struct GemmP {
   int M, N, K;
@@ -55,7 +61,7 @@ struct GemmP {
   float scale, mmt, l2;         // EPI_SGD
   float* cpart; long ldcpart;   // EPI_DSIG_CS: [cdiv(M,32)][N] column sums of the output per 32-row slab
   const float* bpart; long ldbpart; int bslabs;  // EPI_SGD_B: bias-gradient slab sums [bslabs][N]
-  float* bvec; float* bcorr;    // EPI_SGD_B: bias [N] and its momentum buffer (nullable)
+  float* bvec; float* bcorr;    // EPI_SGD_B: bias [N] and its momentum buffer (nullable); EPI_STORE_BG: gradient out
   float bscale, bmmt;           // EPI_SGD_B
   int group;                    // tile-rows per group of the blockIdx -> tile order
   int diag_noload;              // diagnostics only: skip the k-loop's global loads (wrong results)
@@ -129,16 +135,17 @@ struct BiasPre {
   float v[kBiasPreSlabs];
   float b, q;
 };
-template <int BN>
+template <int BN, bool GRAD>
 __device__ __forceinline__ void bias_pre_load(const GemmP& p, int bn, BiasPre& bp) {
   const int col = bn + (int)threadIdx.x;
   if ((int)threadIdx.x >= BN || col >= p.N) return;
 #pragma unroll
   for (int k = 0; k < kBiasPreSlabs; ++k) bp.v[k] = k < p.bslabs ? p.bpart[(long)k * p.ldbpart + col] : 0.f;
+  if (GRAD) return;  // EPI_STORE_BG: the raw gradient, no bias read
   bp.b = p.bvec[col];
   bp.q = p.bcorr ? p.bcorr[col] : 0.f;
 }
-template <int BN>
+template <int BN, bool GRAD>
 __device__ __forceinline__ void bias_pre_finish(const GemmP& p, int bn, const BiasPre& bp) {
   const int col = bn + (int)threadIdx.x;
   if ((int)threadIdx.x >= BN || col >= p.N) return;
@@ -147,6 +154,10 @@ __device__ __forceinline__ void bias_pre_finish(const GemmP& p, int bn, const Bi
   for (int k = 0; k < kBiasPreSlabs; ++k) s += (double)bp.v[k];
   for (int k = kBiasPreSlabs; k < p.bslabs; ++k) s += (double)p.bpart[(long)k * p.ldbpart + col];
   float g = (float)s;
+  if (GRAD) {
+    p.bvec[col] = g;
+    return;
+  }
   if (p.bcorr) {
     g = g + p.bmmt * bp.q;
     p.bcorr[col] = g;
@@ -343,10 +354,10 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_f32_glds_kernel(const GemmP
 #pragma unroll
     for (int g = 0; g < GH; ++g) issue_piece(S - 1, g);
   static_assert(EPI != EPI_DSIG_CS, "column sums: 16x16 kernel only");
-  static_assert(EPI != EPI_SGD_B || BN <= NT, "one thread per bias column");
+  static_assert(!epi_bias_slabs(EPI) || BN <= NT, "one thread per bias column");
   BiasPre bpre;
-  if constexpr (EPI == EPI_SGD_B)
-    if (bm == 0) bias_pre_load<BN>(p, bn, bpre);
+  if constexpr (epi_bias_slabs(EPI))
+    if (bm == 0) bias_pre_load<BN, EPI == EPI_STORE_BG>(p, bn, bpre);
   if (nfull > 0) {
     // tile 0 must land; younger DMAs in flight: full tiles 1..S-2 (+ GH pieces of tile S-1)
     int younger = (min(S - 2, nfull - 1)) * G + ((IL && S - 1 < nfull) ? GH : 0);
@@ -431,8 +442,8 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_f32_glds_kernel(const GemmP
       mfmas(kc % NB);
     }
   }
-  if constexpr (EPI == EPI_SGD_B)
-    if (bm == 0) bias_pre_finish<BN>(p, bn, bpre);
+  if constexpr (epi_bias_slabs(EPI))
+    if (bm == 0) bias_pre_finish<BN, EPI == EPI_STORE_BG>(p, bn, bpre);
   epilogue<TM, TN, epi_base(EPI)>(p, acc, bm, bn, wm0, wn0, li, lh);
 }
 
@@ -806,10 +817,10 @@ void gemm16_kernel(const GemmP p) {
   };
   if constexpr (EARLY) prefetch_tiles();
 
-  static_assert(EPI != EPI_SGD_B || BN <= NT, "one thread per bias column");
+  static_assert(!epi_bias_slabs(EPI) || BN <= NT, "one thread per bias column");
   BiasPre bpre;
-  if constexpr (EPI == EPI_SGD_B)
-    if (bm == 0) bias_pre_load<BN>(p, bn, bpre);
+  if constexpr (epi_bias_slabs(EPI))
+    if (bm == 0) bias_pre_load<BN, EPI == EPI_STORE_BG>(p, bn, bpre);
 
   TNET_STAMP(1);
   // one fragment read (r < TM: operand A, else B) of chunk c of the slot at st into buffer buf
@@ -1020,8 +1031,8 @@ void gemm16_kernel(const GemmP p) {
     }
   }
 
-  if constexpr (EPI == EPI_SGD_B)
-    if (bm == 0) bias_pre_finish<BN>(p, bn, bpre);
+  if constexpr (epi_bias_slabs(EPI))
+    if (bm == 0) bias_pre_finish<BN, EPI == EPI_STORE_BG>(p, bn, bpre);
 
   if constexpr (!EARLY) prefetch_tiles();
   // ---- epilogue: arithmetic on the prefetched operands, then 16-B (n-contiguous) or 4-B stores
@@ -1417,6 +1428,24 @@ extern "C" int tnet_affine_update_bias(const float* X, TnetMatrixDim dX, const f
   if (st) return st;
   if (p.M <= 0 || p.N <= 0) return TNET_OK;
   return launch_gemm<false, false, EPI_SGD_B>(p, (hipStream_t)stream);
+}
+
+extern "C" int tnet_affine_grad_bias(const float* X, TnetMatrixDim dX, const float* E, TnetMatrixDim dE, float* G,
+                                     TnetMatrixDim dG, const float* colpart, int ldcolpart, float* gradB,
+                                     void* stream) {
+  // tnet_affine_grad + gradB = colsum(E) from the slab sums tnet_affine_bwd_colsum wrote for E
+  if (dX.rows != dE.rows || dG.rows != dX.cols || dG.cols != dE.cols || !colpart || !gradB || ldcolpart < dE.cols)
+    return TNET_ERR_ARG;
+  GemmP p{};
+  p.M = dX.cols; p.N = dE.cols; p.K = dX.rows;
+  p.A = X; p.lda = dX.stride; p.B = E; p.ldb = dE.stride; p.C = G; p.ldc = dG.stride;
+  p.alpha = 1.f; p.beta = 0.f;
+  p.bpart = colpart; p.ldbpart = ldcolpart; p.bslabs = tnet_colsum_slabs(dE.rows);
+  p.bvec = gradB;
+  int st = check_common(p);
+  if (st) return st;
+  if (p.M <= 0 || p.N <= 0) return TNET_OK;
+  return launch_gemm<false, false, EPI_STORE_BG>(p, (hipStream_t)stream);
 }
 
 extern "C" int tnet_affine_grad(const float* X, TnetMatrixDim dX, const float* E, TnetMatrixDim dE, float* G,

@@ -195,6 +195,48 @@ def test_affine_update_bias(mmt, rows, n_in, n_out, gemm_cfg):
         np.testing.assert_allclose(dCb.numpy().ravel(), cb, rtol=1e-6, atol=1e-9)
 
 
+@pytest.mark.parametrize("rows,n_in,n_out", [(16, 24, 32), (1024, 2048, 2048), (1024, 440, 2048), (1000, 2048, 4000)])
+def test_affine_grad_bias(rows, n_in, n_out, gemm_cfg):
+    """data-parallel gradient: G = X^T E and gradB = colsum(E) from slab sums, one launch"""
+    X, E = rnd((rows, n_in), 12), rnd((rows, n_out), 13, 0.01)
+    P = slab_sums(E).astype(np.float32)
+    dX, dE, dG = DeviceArray.from_numpy(X), DeviceArray.from_numpy(E), DeviceArray(n_in, n_out)
+    dP, dgb = DeviceArray.from_numpy(P), DeviceArray.vector(np.full(n_out, np.nan, np.float32))
+    check(lib().tnet_affine_grad_bias(dX.ptr, dX.dim, dE.ptr, dE.dim, dG.ptr, dG.dim, dP.ptr, dP.stride, dgb.ptr, S()))
+    g, mag = gemm_ref("T", "N", X, E)
+    assert np.all(np.abs(dG.numpy() - g) <= 2e-5 * mag + 1e-7)
+    np.testing.assert_array_equal(dgb.numpy().ravel(), P.astype(np.float64).sum(0).astype(np.float32))
+
+
+class SgdSeg(C.Structure):
+    _fields_ = [("p", C.c_void_p), ("g", C.c_void_p), ("corr", C.c_void_p), ("n", C.c_long), ("l2", C.c_float)]
+
+
+@pytest.mark.parametrize("mmt", [0.0, 0.9])
+@pytest.mark.parametrize("sizes", [[1], [4194304, 2048], [7, 13, 4096, 1, 5, 3, 1000, 9, 17, 4]])
+def test_sgd_update_multi(mmt, sizes):
+    """several SGD segments in one launch (more than 8 split over launches), ragged and unaligned sizes"""
+    scale = -0.01
+    segs, refs = [], []
+    keep = []
+    for k, n in enumerate(sizes):
+        p, g, c = rnd(n, 30 + k), rnd(n, 50 + k), rnd(n, 70 + k, 0.1)
+        l2 = -1e-4 * (k % 3)
+        dp_, dg, dc = DeviceArray.vector(p), DeviceArray.vector(g), DeviceArray.vector(c)
+        keep += [dp_, dg, dc]
+        segs.append(SgdSeg(dp_.ptr, dg.ptr, dc.ptr if mmt else None, n, l2))
+        cc = g.astype(np.float64) + mmt * c if mmt else g.astype(np.float64)
+        w = p + scale * cc
+        w = w + l2 * w
+        refs.append((dp_, dc, w, cc))
+    arr = (SgdSeg * len(segs))(*segs)
+    check(lib().tnet_sgd_update_multi(C.cast(arr, C.c_void_p), len(segs), scale, mmt, S()))
+    for dp_, dc, w, cc in refs:
+        np.testing.assert_allclose(dp_.numpy().ravel(), w, rtol=1e-6, atol=1e-7)
+        if mmt:
+            np.testing.assert_allclose(dc.numpy().ravel(), cc, rtol=1e-6, atol=1e-7)
+
+
 @pytest.mark.parametrize("rows,cols", [(1, 1), (16, 10), (1024, 135), (1024, 4000), (300, 4099), (64, 5000)])
 def test_softmax_xent_labels(rows, cols):
     Z = rnd((rows, cols), 16, 3.0)
