@@ -121,6 +121,10 @@ int tnetF_randomize(float* y, const float* x, const int* copy_from, TnetMatrixDi
                     void* stream);
 /* labels_out[i] = labels_in[copy_from[i]]  (class-id twin of randomize for one-hot targets) */
 int tnet_gather_i32(int* out, const int* in, const int* copy_from, int n, void* stream);
+/* both in one launch: y = rows copy_from[] of x, labels_out[i] = labels_in[copy_from[i]]
+ * (CuCache::GetBunch's two _randomize calls, cuCache.cc:155-200, for a class-id target cache) */
+int tnet_gather_bunch(float* y, const float* x, int* labels_out, const int* labels_in, const int* copy_from,
+                      TnetMatrixDim dout, TnetMatrixDim din, void* stream);
 
 /* ------------------------------------------------------------------------------------
  * GEMM (replaces cublasSgemm at cumatrix.tcc:336-370, row-major semantics)
@@ -173,6 +177,10 @@ int tnet_colsum_slabs(int rows);
 int tnet_affine_bwd_colsum(const float* E, TnetMatrixDim dE, const float* W, TnetMatrixDim dW,
                            const float* Ybelow, int strideYbelow, float* Eo, TnetMatrixDim dEo, float* colpart,
                            int ldcolpart, void* stream);
+/* slab sums for an E that no backward GEMM produced (the top layer's softmax error): the same slab
+ * count; the slabs are disjoint row ranges (32 rows when rows % 32 == 0) whose sum is colsum(E), which
+ * is all tnet_affine_update_bias / tnet_affine_grad_bias use.  TNET_ERR_UNSUPPORTED above 8192 rows. */
+int tnet_colsum_slab_sums(const float* E, TnetMatrixDim dE, float* colpart, int ldcolpart, void* stream);
 /* tnet_affine_update + tnet_bias_update(E, b, corr_b, scale, mmt) in one launch, colsum(E) taken from
  * colpart (written for E by tnet_affine_bwd_colsum); corr_b is required when mmt != 0
  * (cuBiasedLinearity.cc:46-64). */

@@ -224,10 +224,8 @@ void CuCache::GetBunchLabels(CuMatrix<BaseFloat>& rFeatures, CuVector<int>& rLab
   rLabels.Init(mBunchsize);
   if (mRandomized) {
     KTScope kt("gather", 2.0 * mBunchsize * mFeatures.Cols() * 4.0);
-    TNET_SAFE_CALL(tnetF_randomize(rFeatures.pCUData(), mFeatures.pCUData(), mPerm.pCUData() + mExhaustPos,
-                                   rFeatures.Dim(), mFeatures.Dim(), S));
-    TNET_SAFE_CALL(tnet_gather_i32(rLabels.pCUData(), mLabels.pCUData(), mPerm.pCUData() + mExhaustPos,
-                                   (int)mBunchsize, S));
+    TNET_SAFE_CALL(tnet_gather_bunch(rFeatures.pCUData(), mFeatures.pCUData(), rLabels.pCUData(), mLabels.pCUData(),
+                                     mPerm.pCUData() + mExhaustPos, rFeatures.Dim(), mFeatures.Dim(), S));
   } else {
     rFeatures.CopyRows(mBunchsize, mExhaustPos, mFeatures, 0);
     TNET_HIP_CALL(hipMemcpyAsync(rLabels.pCUData(), mLabels.pCUData() + mExhaustPos, mBunchsize * sizeof(int),

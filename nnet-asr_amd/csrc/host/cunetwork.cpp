@@ -287,7 +287,21 @@ void CuNetwork::TrainBunch(const CuMatrix<BaseFloat>& X, const CuVector<int>& la
   // ---- backward + update, top to bottom (error uses the pre-update weights of the layer)
   const CuMatrix<BaseFloat>* err = &mGlobErr;
   std::vector<CuBiasedLinearity*> submitted;  // data-parallel: layers in reduction order
-  bool err_colsum = false;  // slab column sums of *err are in mColPart[l] (bias gradient fused, no exchange)
+  bool err_colsum = false;
+  {
+    // the top layer's bias gradient as slab sums too (one launch; the update GEMM applies it)
+    auto* top = static_cast<CuBiasedLinearity*>(mNetComponents[2 * (nl - 1)]);
+    if (top->LearnRate() > 0.0f) {
+      CuMatrix<BaseFloat>& cp = *mColPart[nl - 1];
+      cp.Init(tnet_colsum_slabs((int)rows), GetNOutputs());
+      KTScope kt("colsum:" + std::to_string(GetNOutputs()), 4.0 * rows * GetNOutputs());
+      const int st = tnet_colsum_slab_sums(mGlobErr.pCUData(), mGlobErr.Dim(), cp.pCUData(), (int)cp.Stride(), S);
+      if (st != TNET_ERR_UNSUPPORTED) {
+        TNET_SAFE_CALL(st);
+        err_colsum = true;
+      }
+    }
+  }  // slab column sums of *err are in mColPart[l] (bias gradient fused, no exchange)
   for (int l = nl - 1; l >= 0; l--) {
     auto* lin = static_cast<CuBiasedLinearity*>(mNetComponents[2 * l]);
     const bool stopper = (lin == mpPropagErrorStopper);

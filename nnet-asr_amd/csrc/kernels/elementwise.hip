@@ -90,12 +90,16 @@ __global__ __launch_bounds__(EW_THREADS) void diff_sigmoid_kernel(float* __restr
 // Row gather: y[i,:] = x[idx[i],:]   (cache shuffle / bunch fetch; one wave per row, float4)
 __global__ __launch_bounds__(EW_THREADS) void gather_rows_kernel(float* __restrict__ y, const float* __restrict__ x,
                                                                  const int* __restrict__ idx, TnetMatrixDim dout,
-                                                                 TnetMatrixDim din, int vec4) {
+                                                                 TnetMatrixDim din, int vec4,
+                                                                 int* __restrict__ lab_out = nullptr,
+                                                                 const int* __restrict__ lab_in = nullptr) {
   const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int lane = threadIdx.x & 63;
   const int nwaves = (gridDim.x * blockDim.x) >> 6;
   for (int r = wave; r < dout.rows; r += nwaves) {
-    const long src = (long)idx[r] * din.stride;
+    const int ir = idx[r];
+    if (lab_out && lane == 0) lab_out[r] = lab_in[ir];  // the bunch's class ids ride along
+    const long src = (long)ir * din.stride;
     const long dst = (long)r * dout.stride;
     if (vec4) {
       for (int c = lane * 4; c < dout.cols; c += 256)
@@ -297,6 +301,18 @@ extern "C" int tnetF_randomize(float* y, const float* x, const int* copy_from, T
   unsigned grid = (unsigned)((waves * 64 + EW_THREADS - 1) / EW_THREADS);
   if (grid > 4096) grid = 4096;
   gather_rows_kernel<<<grid, EW_THREADS, 0, STREAM>>>(y, x, copy_from, dout, din, v4);
+  TNET_LAUNCH_CHECK();
+  return TNET_OK;
+}
+
+extern "C" int tnet_gather_bunch(float* y, const float* x, int* labels_out, const int* labels_in,
+                                 const int* copy_from, TnetMatrixDim dout, TnetMatrixDim din, void* stream) {
+  if (dout.cols != din.cols || dout.rows < 0 || !labels_out || !labels_in) return TNET_ERR_ARG;
+  if (!dout.rows) return TNET_OK;
+  const int v4 = vec4_ok(x, din) && vec4_ok(y, dout);
+  unsigned grid = (unsigned)(((long)dout.rows * 64 + EW_THREADS - 1) / EW_THREADS);
+  if (grid > 4096) grid = 4096;
+  gather_rows_kernel<<<grid, EW_THREADS, 0, STREAM>>>(y, x, copy_from, dout, din, v4, labels_out, labels_in);
   TNET_LAUNCH_CHECK();
   return TNET_OK;
 }

@@ -27,7 +27,8 @@ static int cs_slabs(int rows) {
 // r0+w, r0+w+4, ...; the 4 sub-group sums are added in order)
 template <bool V4>
 __global__ __launch_bounds__(256) void colsum_partial_kernel(const float* __restrict__ M, TnetMatrixDim d,
-                                                             float* __restrict__ partial, int slabs, int neg_from) {
+                                                             float* __restrict__ partial, int slabs, int neg_from,
+                                                             long ldp) {
   constexpr int CW = V4 ? 4 : 1;                 // columns per lane
   __shared__ float red[CS_WAVES][CS_COLS * CW];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -63,7 +64,7 @@ __global__ __launch_bounds__(256) void colsum_partial_kernel(const float* __rest
         float t = red[0][lane * CW + k];
 #pragma unroll
         for (int q = 1; q < CS_WAVES; ++q) t += red[q][lane * CW + k];
-        partial[(long)s * d.cols + c] = t;
+        partial[(long)s * ldp + c] = t;
       }
     }
   }
@@ -120,9 +121,10 @@ static int colsum_run(const float* M, TnetMatrixDim d, void* workspace, hipStrea
     const bool v4 = (d.cols & 3) == 0 && (d.stride & 3) == 0 && ((uintptr_t)M & 15) == 0;
     if (v4)
       colsum_partial_kernel<true><<<dim3(cdiv(d.cols, CS_COLS * 4), slabs), 256, 0, st>>>(M, d, ws, slabs,
-                                                                                         neg_from);
+                                                                                         neg_from, d.cols);
     else
-      colsum_partial_kernel<false><<<dim3(cdiv(d.cols, CS_COLS), slabs), 256, 0, st>>>(M, d, ws, slabs, neg_from);
+      colsum_partial_kernel<false><<<dim3(cdiv(d.cols, CS_COLS), slabs), 256, 0, st>>>(M, d, ws, slabs, neg_from,
+                                                                                      d.cols);
     TNET_LAUNCH_CHECK();
   } else {
     if (hipMemsetAsync(ws, 0, (size_t)slabs * d.cols * 4, st) != hipSuccess) return TNET_ERR_RUNTIME;
@@ -329,6 +331,24 @@ extern "C" long tnet_col_sum_workspace(TnetMatrixDim d) { return (long)cs_slabs(
 extern "C" int tnetF_add_col_sum(float alpha, const float* mat, float beta, float* vec, TnetMatrixDim d,
                                  void* workspace, void* stream) {
   return colsum_run(mat, d, workspace, (hipStream_t)stream, 0, alpha, beta, vec, nullptr, 0.f, 0.f);
+}
+
+extern "C" int tnet_colsum_slab_sums(const float* E, TnetMatrixDim dE, float* colpart, int ldcolpart, void* stream) {
+  // the 32-row slab sums tnet_affine_bwd_colsum writes, for an E no backward GEMM produced (the top
+  // layer's error from the softmax): same slab count (tnet_colsum_slabs), fp32 sums in row order
+  if (dE.rows < 0 || dE.cols < 0 || dE.stride < dE.cols || !colpart || ldcolpart < dE.cols) return TNET_ERR_ARG;
+  if (!dE.rows || !dE.cols) return TNET_OK;
+  const int slabs = cs_slabs(dE.rows);
+  if (slabs != cdiv(dE.rows, CS_ROWS)) return TNET_ERR_UNSUPPORTED;  // > 8192 rows: capped slab count
+  const bool v4 = (dE.cols & 3) == 0 && (dE.stride & 3) == 0 && ((uintptr_t)E & 15) == 0;
+  if (v4)
+    colsum_partial_kernel<true><<<dim3(cdiv(dE.cols, CS_COLS * 4), slabs), 256, 0, (hipStream_t)stream>>>(
+        E, dE, colpart, slabs, 0x7fffffff, ldcolpart);
+  else
+    colsum_partial_kernel<false><<<dim3(cdiv(dE.cols, CS_COLS), slabs), 256, 0, (hipStream_t)stream>>>(
+        E, dE, colpart, slabs, 0x7fffffff, ldcolpart);
+  TNET_LAUNCH_CHECK();
+  return TNET_OK;
 }
 
 extern "C" int tnet_bias_update(const float* E, TnetMatrixDim dE, float* b, float* corr_b, float* grad_out,

@@ -60,12 +60,14 @@ _SIGS = {
     "tnetF_randomize": (i32, [vp, vp, vp, MatrixDim, MatrixDim, vp]),
     "tnet_block_linearity": (i32, [vp, MatrixDim, vp, MatrixDim, vp, MatrixDim, vp]),
     "tnet_gather_i32": (i32, [vp, vp, vp, i32, vp]),
+    "tnet_gather_bunch": (i32, [vp, vp, vp, vp, vp, MatrixDim, MatrixDim, vp]),
     "tnet_sgemm": (i32, [C.c_char, C.c_char, i32, i32, i32, f32, vp, i32, vp, i32, f32, vp, i32, vp]),
     "tnet_gemm_config": (i32, [C.c_char_p]),
     "tnet_affine_fwd": (i32, [vp, MatrixDim, vp, MatrixDim, vp, vp, MatrixDim, i32, vp]),
     "tnet_affine_bwd": (i32, [vp, MatrixDim, vp, MatrixDim, vp, i32, vp, MatrixDim, i32, vp]),
     "tnet_affine_update": (i32, [vp, MatrixDim, vp, MatrixDim, vp, MatrixDim, vp, i32, f32, f32, f32, vp]),
     "tnet_colsum_slabs": (i32, [i32]),
+    "tnet_colsum_slab_sums": (i32, [vp, MatrixDim, vp, i32, vp]),
     "tnet_affine_grad_bias": (i32, [vp, MatrixDim, vp, MatrixDim, vp, MatrixDim, vp, i32, vp, vp]),
     "tnet_sgd_update_multi": (i32, [vp, i32, f32, f32, vp]),
     "tnet_affine_bwd_colsum": (i32, [vp, MatrixDim, vp, MatrixDim, vp, i32, vp, MatrixDim, vp, i32, vp]),

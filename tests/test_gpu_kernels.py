@@ -324,6 +324,28 @@ def test_randomize_and_gather():
     check(lib().tnet_gather_i32(dLo.ptr, dL.ptr, dP.ptr, 256, S()))
     np.testing.assert_array_equal(dY.numpy(), X[perm])
     np.testing.assert_array_equal(dLo.numpy()[:, 0], lab[perm])
+    # both in one launch (the cache's GetBunchLabels)
+    dY2, dLo2 = DeviceArray(256, cols), DeviceArray.vector(np.zeros(256, np.int32))
+    check(lib().tnet_gather_bunch(dY2.ptr, dX.ptr, dLo2.ptr, dL.ptr, dP.ptr, dY2.dim, dX.dim, S()))
+    np.testing.assert_array_equal(dY2.numpy(), X[perm])
+    np.testing.assert_array_equal(dLo2.numpy()[:, 0], lab[perm])
+
+
+@pytest.mark.parametrize("rows,cols", [(16, 10), (1000, 4000), (1024, 135), (33, 7)])
+def test_colsum_slab_sums(rows, cols):
+    E = rnd((rows, cols), 40)
+    dE = DeviceArray.from_numpy(E)
+    slabs = lib().tnet_colsum_slabs(rows)
+    dP = DeviceArray.from_numpy(np.full((slabs, cols), np.nan, np.float32))
+    check(lib().tnet_colsum_slab_sums(dE.ptr, dE.dim, dP.ptr, dP.stride, S()))
+    P = dP.numpy()
+    assert not np.isnan(P).any()
+    # contract: tnet_colsum_slabs(rows) slabs of disjoint row ranges (the kernel's own boundaries when
+    # rows is not a multiple of 32) whose sum is the column sum
+    tot = np.abs(E).astype(np.float64).sum(0)
+    assert np.all(np.abs(P.astype(np.float64).sum(0) - E.astype(np.float64).sum(0)) <= 32 * 1.2e-7 * tot + 1e-7)
+    if rows % 32 == 0:
+        assert np.all(np.abs(P - slab_sums(E)) <= 32 * 1.2e-7 * slab_sums(np.abs(E)) + 1e-7)
 
 
 def test_check_class_first_max_wins():
