@@ -39,15 +39,19 @@ b = DeviceArray.vector(np.zeros(no, np.float32))
 Y = DeviceArray(rows, no)
 E = DeviceArray.from_numpy((1e-3 * rng.standard_normal((rows, no))).astype(np.float32))
 Eo = DeviceArray(rows, ni)
+Po = DeviceArray(L.tnet_colsum_slabs(rows), ni)
+Pi = DeviceArray.from_numpy(np.zeros((L.tnet_colsum_slabs(rows), no), np.float32))
 
 
 def run(kind):
     if kind == "fwd":
         check(L.tnet_affine_fwd(X.ptr, X.dim, W.ptr, W.dim, b.ptr, Y.ptr, Y.dim, 1, S))
-    elif kind == "bwd":
-        check(L.tnet_affine_bwd(E.ptr, E.dim, W.ptr, W.dim, X.ptr, X.stride, Eo.ptr, Eo.dim, 1, S))
+    elif kind == "bwd":  # the training step's fused forms (bias gradient as slab sums)
+        check(L.tnet_affine_bwd_colsum(E.ptr, E.dim, W.ptr, W.dim, X.ptr, X.stride, Eo.ptr, Eo.dim, Po.ptr,
+                                       Po.stride, S))
     else:
-        check(L.tnet_affine_update(X.ptr, X.dim, E.ptr, E.dim, W.ptr, W.dim, None, 0, -1e-9, 0.0, 0.0, S))
+        check(L.tnet_affine_update_bias(X.ptr, X.dim, E.ptr, E.dim, W.ptr, W.dim, None, 0, -1e-9, 0.0, 0.0, Pi.ptr,
+                                        Pi.stride, b.ptr, None, S))
 
 
 def warm():

@@ -42,10 +42,17 @@ elif which == "layer":
     Y = DeviceArray(rows, no)
     E = DeviceArray.from_numpy((1e-3 * rng.standard_normal((rows, no))).astype(np.float32))
     Eo = DeviceArray(rows, ni)
+    # the training step's fused forms: bwd writes the bias gradient of the layer below as slab sums,
+    # the update applies the bias SGD from slab sums
+    slabs = lib().tnet_colsum_slabs(rows)
+    Po = DeviceArray(slabs, ni)
+    Pi = DeviceArray.from_numpy(np.zeros((slabs, no), np.float32))
     for _ in range(iters):
         check(lib().tnet_affine_fwd(X.ptr, X.dim, W.ptr, W.dim, b.ptr, Y.ptr, Y.dim, 1, S))
-        check(lib().tnet_affine_bwd(E.ptr, E.dim, W.ptr, W.dim, X.ptr, X.stride, Eo.ptr, Eo.dim, 1, S))
-        check(lib().tnet_affine_update(X.ptr, X.dim, E.ptr, E.dim, W.ptr, W.dim, None, 0, -1e-6, 0.0, 0.0, S))
+        check(lib().tnet_affine_bwd_colsum(E.ptr, E.dim, W.ptr, W.dim, X.ptr, X.stride, Eo.ptr, Eo.dim, Po.ptr,
+                                           Po.stride, S))
+        check(lib().tnet_affine_update_bias(X.ptr, X.dim, E.ptr, E.dim, W.ptr, W.dim, None, 0, -1e-6, 0.0, 0.0,
+                                            Pi.ptr, Pi.stride, b.ptr, None, S))
     check(lib().tnet_synchronize())
 else:
     import torch

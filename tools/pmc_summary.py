@@ -6,7 +6,7 @@ Units / corrections (MI355X_MICROARCH.md, HBM/rocprofv3 section):
   FETCH_SIZE, WRITE_SIZE are KiB per dispatch; on gfx950 FETCH_SIZE counts half the bytes of wide
   16-B/lane streaming reads (global_load_dwordx4 and LDS-DMA alike), so it is doubled here.
   GRBM_GUI_ACTIVE is summed over the 8 XCDs: effective clock = GRBM_GUI_ACTIVE / 8 / duration.
-  SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE/8 * 256 CUs) = fraction of CU-cycles with an MFMA busy.
+  SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE/8 * 1024 SIMDs) = fraction of SIMD-cycles with an MFMA busy.
 """
 import csv
 import glob
@@ -50,7 +50,10 @@ def summarise(d):
             # duration of the SQ pass dispatches only (the counter pass that holds GRBM)
             r["eff_clock_GHz"] = mean["GRBM_GUI_ACTIVE"] / 8 / avg_ns
             if "SQ_VALU_MFMA_BUSY_CYCLES" in mean:
-                r["mfma_busy_frac"] = mean["SQ_VALU_MFMA_BUSY_CYCLES"] / (mean["GRBM_GUI_ACTIVE"] / 8 * 256)
+                # rocprofv3's MfmaUtil: busy cycles summed over the SIMDs / (GRBM cycles x SIMD count)
+                r["mfma_busy_frac"] = mean["SQ_VALU_MFMA_BUSY_CYCLES"] / (mean["GRBM_GUI_ACTIVE"] / 8 * 1024)
+            if "SQ_INSTS_VALU_MFMA_MOPS_F32" in mean:
+                r["mfma_flops_f32"] = mean["SQ_INSTS_VALU_MFMA_MOPS_F32"] * 512
         for c in ("SQ_BUSY_CU_CYCLES", "SQ_WAVES"):
             if c in mean:
                 r[c] = mean[c]

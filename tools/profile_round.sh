@@ -16,7 +16,12 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof_stats"
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d "$R/gpurun_out/pmc_fetch" -o pmc --output-format csv \
   -- python3 "$R/tools/gemm_pmc.py" layer 20 > "$R/gpurun_out/pmc_fetch.log" 2>&1 &&
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d "$R/gpurun_out/pmc_write" -o pmc --output-format csv \
-  -- python3 "$R/tools/gemm_pmc.py" layer 20 > "$R/gpurun_out/pmc_write.log" 2>&1
+  -- python3 "$R/tools/gemm_pmc.py" layer 20 > "$R/gpurun_out/pmc_write.log" 2>&1 &&
+timeout -k 10 300 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_BUSY_CYCLES \
+  -d "$R/gpurun_out/pmc_mfma" -o pmc --output-format csv \
+  -- python3 "$R/tools/gemm_pmc.py" layer 300 > "$R/gpurun_out/pmc_mfma.log" 2>&1 &&
+cd "$R" &&
+timeout -k 10 200 python3 tools/gemm_clock.py 1.5 5 > gpurun_out/clock.log 2>&1
 rc=$?
 echo "profile_round rc=$rc"
 exit $rc

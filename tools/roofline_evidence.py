@@ -29,10 +29,16 @@ import pmc_summary  # noqa: E402
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
+FWD = "gemm16_kernel<64, 128, 64, 2, 2, 2, 0, true, false, 2>"    # bias + sigmoid
+BWD = "gemm16_kernel<64, 128, 64, 2, 2, 2, 0, true, true, 8>"     # diff-sigmoid + slab column sums
+UPD = "gemm16_kernel<128, 128, 64, 2, 2, 2, 0, false, false, 9>"  # SGD + bias SGD
+
+
 def classify_trace(path):
     rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
     cls = {"fwd": [], "bwd": [], "upd": []}
     after_softmax = False
+    after_gather = False
     for r in rows:
         name = r["Kernel_Name"]
         dur = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
@@ -40,14 +46,20 @@ def classify_trace(path):
         if "softmax_xent" in name:
             after_softmax = True
             continue
-        if "gemm16_kernel<64, 128, 64, 2, 2, 2, true, false, 2>" in name:
-            cls["fwd"].append(dur)
-        elif "gemm16_kernel<64, 128, 64, 2, 2, 2, true, true, 3>" in name:
+        if "gather_rows" in name:
+            after_gather = True
+            continue
+        if FWD in name:
+            if after_gather:           # K = 440 (the first layer, same tile config)
+                after_gather = False
+            else:
+                cls["fwd"].append(dur)
+        elif BWD in name:
             if after_softmax:          # K = 4000 (error into the last hidden layer)
                 after_softmax = False
             else:
                 cls["bwd"].append(dur)
-        elif "gemm16_kernel<128, 128, 64, 2, 2, 2, false, false, 4>" in name and grid == 65536:
+        elif UPD in name and grid == 65536:
             cls["upd"].append(dur)
     return cls
 
@@ -90,6 +102,17 @@ def main():
            "kernels": kern, "traffic_MB_per_launch": round(sum(per) / len(per), 3),
            "algorithmic_MB_per_launch": {k: round(v, 3) for k, v in algo.items()},
            "algorithmic_MB_per_launch_avg": round(sum(algo.values()) / 3, 3)}
+    # MFMA utilisation pass (GRBM_GUI_ACTIVE, SQ_VALU_MFMA_BUSY_CYCLES, SQ_INSTS_VALU_MFMA_MOPS_F32) and
+    # the in-kernel clock stamps (tools/gemm_clock.py, separate stamped build)
+    mf = pmc_summary.summarise(os.path.join(src, "pmc_mfma"))
+    pmc["mfma_pass"] = {k: r for k, r in mf.items() if "gemm" in k}
+    pmc["mfma_pass_note"] = ("mfma_busy_frac = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE/8 * 1024 SIMDs); "
+                             "GRBM_GUI_ACTIVE/8/duration reads above the real clock on sub-0.3-ms dispatches "
+                             "(MI355X_MICROARCH.md 'DVFS give-back'), so the in-kernel stamps below are the "
+                             "clock and cycle reference")
+    clk = [l for l in open(os.path.join(src, "clock.log")) if l.startswith("CLOCK ")]
+    if clk:
+        pmc["clock_stamps"] = json.loads(clk[-1][6:])
     with open(os.path.join(prof, f"{tag}_pmc_gemm2048.json"), "w") as f:
         json.dump(pmc, f, indent=1)
     print(json.dumps(tr, indent=1))
