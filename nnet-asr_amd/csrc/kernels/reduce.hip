@@ -158,6 +158,10 @@ __device__ __forceinline__ ArgMax wave_argmax(ArgMax a) {
   return a;
 }
 
+// exp(x) for x <= 0 on v_exp_f32: exp2(x*log2 e); relative error ~|x|*6e-8 (the rounding of the
+// scaled argument), i.e. <= 1e-6 over the 16 nats that carry any probability mass
+__device__ __forceinline__ float fast_exp(float x) { return __builtin_amdgcn_exp2f(1.44269504088896341f * x); }
+
 // KIND 0: class-id labels; KIND 1: dense targets D.  Z == nullptr: Y already holds softmax output.
 template <int KIND>
 __global__ __launch_bounds__(256) void softmax_xent_kernel(const float* __restrict__ Z, TnetMatrixDim d,
@@ -207,18 +211,19 @@ __global__ __launch_bounds__(256) void softmax_xent_kernel(const float* __restri
         if (c < N) {
 #pragma unroll
           for (int k = 0; k < 4; ++k) {
-            const float e = expf(rv[j][k] - m);
+            const float e = fast_exp(rv[j][k] - m);
             rv[j][k] = e;
             s += e;
           }
         }
       }
     } else {
-      for (int c = lane; c < N; c += 64) s += expf(src[c] - m);
+      for (int c = lane; c < N; c += 64) s += fast_exp(src[c] - m);
     }
     dsum = wave_sum_d((double)s);
   }
   const float sum = (float)dsum;
+  const float rsum = 1.f / sum;  // one division per row; y = e * (1/sum)
 
   // ---- pass 3: y, error, argmax, xent
   ArgMax ay{-1e20f, 0x7fffffff}, ad{-1e20f, 0x7fffffff};
@@ -244,7 +249,7 @@ __global__ __launch_bounds__(256) void softmax_xent_kernel(const float* __restri
         f32x4 y, e;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-          y[k] = Z ? rv[j][k] / sum : rv[j][k];
+          y[k] = Z ? rv[j][k] * rsum : rv[j][k];
           e[k] = y[k] - visit(c + k, y[k]);
         }
         if (yrow && Z) *reinterpret_cast<f32x4*>(yrow + c) = y;
@@ -253,7 +258,7 @@ __global__ __launch_bounds__(256) void softmax_xent_kernel(const float* __restri
     }
   } else {
     for (int c = lane; c < N; c += 64) {
-      const float y = Z ? expf(src[c] - m) / sum : src[c];
+      const float y = Z ? fast_exp(src[c] - m) * rsum : src[c];
       const float dv = visit(c, y);
       if (yrow && Z) yrow[c] = y;
       if (erow) erow[c] = y - dv;
@@ -270,7 +275,7 @@ __global__ __launch_bounds__(256) void softmax_xent_kernel(const float* __restri
   if (KIND == 1) xent = wave_sum_d(xent);
   if (lane == 0) {
     if (KIND == 0 && t >= 0) {
-      const float yt = Z ? expf(src[t] - m) / sum : src[t];
+      const float yt = Z ? fast_exp(src[t] - m) * rsum : src[t];  // the y written for column t
       xent = -(double)logf(fmaxf(yt, FLT_MIN));
     }
     red[0][wv] = xent;
@@ -364,6 +369,94 @@ extern "C" int tnet_rbm_bias_update(const float* M, TnetMatrixDim d, int neg_fro
   return colsum_run(M, d, workspace, (hipStream_t)stream, 3, 1.f, 0.f, b, corr_b, scale, mmt, neg_from);
 }
 
+// Wide rows (1025..4096 columns, 16-B aligned), class-id targets, logits in Z: one 256-thread block
+// per ROW, wave w holding 256-column chunks w, w+4, w+8, w+12 in registers; the row max / sum /
+// argmax meet through LDS.  Four waves per row keep four times the loads in flight per row and a
+// quarter of the exp / compare work per wave of the one-wave-per-row kernel (latency-bound there).
+__global__ __launch_bounds__(256) void softmax_xent_row4_kernel(const float* __restrict__ Z, TnetMatrixDim d,
+                                                                const int* __restrict__ labels,
+                                                                float* __restrict__ Y, int strideY,
+                                                                float* __restrict__ E, int strideE,
+                                                                double* __restrict__ stats) {
+  constexpr int CPW = SX_MAXV4 / 4;  // chunks per wave
+  __shared__ float smax[4];
+  __shared__ double ssum[4];
+  __shared__ ArgMax sarg[4];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int row = blockIdx.x, N = d.cols;
+  const float* src = Z + (long)row * d.stride;
+  f32x4 rv[CPW];
+  float m = -1e20f;
+#pragma unroll
+  for (int q = 0; q < CPW; ++q) {
+    const int c = (wv + 4 * q) * 256 + lane * 4;
+    f32x4 x = {-1e30f, -1e30f, -1e30f, -1e30f};
+    if (c < N) x = *reinterpret_cast<const f32x4*>(src + c);
+    rv[q] = x;
+    m = fmaxf(m, fmaxf(fmaxf(x[0], x[1]), fmaxf(x[2], x[3])));
+  }
+  m = wave_max(m);
+  if (lane == 0) smax[wv] = m;
+  __syncthreads();
+  m = fmaxf(fmaxf(smax[0], smax[1]), fmaxf(smax[2], smax[3]));
+  float s = 0.f;
+#pragma unroll
+  for (int q = 0; q < CPW; ++q) {
+    const int c = (wv + 4 * q) * 256 + lane * 4;
+    if (c < N) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float e = fast_exp(rv[q][k] - m);
+        rv[q][k] = e;
+        s += e;
+      }
+    }
+  }
+  const double ws = wave_sum_d((double)s);
+  if (lane == 0) ssum[wv] = ws;
+  __syncthreads();
+  const float sum = (float)(ssum[0] + ssum[1] + ssum[2] + ssum[3]);
+  const float rsum = 1.f / sum;
+  const int t = labels[row];
+  float* yrow = Y ? Y + (long)row * strideY : nullptr;
+  float* erow = E ? E + (long)row * strideE : nullptr;
+  ArgMax ay{-1e20f, 0x7fffffff};
+#pragma unroll
+  for (int q = 0; q < CPW; ++q) {
+    const int c = (wv + 4 * q) * 256 + lane * 4;
+    if (c < N) {
+      f32x4 y, e;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        y[k] = rv[q][k] * rsum;
+        if (y[k] > ay.v) { ay.v = y[k]; ay.i = c + k; }
+        e[k] = y[k] - ((c + k == t) ? 1.f : 0.f);
+      }
+      if (yrow) *reinterpret_cast<f32x4*>(yrow + c) = y;
+      if (erow) *reinterpret_cast<f32x4*>(erow + c) = e;
+    }
+  }
+  ay = wave_argmax(ay);
+  if (lane == 0) sarg[wv] = ay;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    ArgMax a = sarg[0];
+#pragma unroll
+    for (int w = 1; w < 4; ++w) a = argmax_merge(a, sarg[w]);
+    const int des = t >= 0 ? t : 0;  // all-zero target row: first max of zeros is column 0
+    double xent = 0.0;
+    if (t >= 0) {
+      const float yt = fast_exp(src[t] - m) * rsum;  // the y written for column t
+      xent = -(double)logf(fmaxf(yt, FLT_MIN));
+    }
+    if (stats) {
+      const int slot = blockIdx.x % TNET_STATS_SLOTS;
+      atomicAdd(stats + 2 * slot, xent);
+      atomicAdd(stats + 2 * slot + 1, (a.i == des) ? 1.0 : 0.0);
+    }
+  }
+}
+
 static bool v4ok(const void* p, int stride) { return ((uintptr_t)p & 15) == 0 && (stride & 3) == 0; }
 
 extern "C" int tnet_softmax_xent(const float* Z, TnetMatrixDim dZ, const int* labels, float* Y, int strideY, float* E,
@@ -375,8 +468,11 @@ extern "C" int tnet_softmax_xent(const float* Z, TnetMatrixDim dZ, const int* la
   // when Z == NULL, Y already holds the softmax output (read through strideY)
   TnetMatrixDim dd = dZ;
   if (!Z) dd.stride = strideY;
-  softmax_xent_kernel<0><<<cdiv((long)dZ.rows * 64, 256), 256, 0, (hipStream_t)stream>>>(
-      Z, dd, labels, nullptr, 0, Y, strideY, E, strideE, stats, v4);
+  if (Z && v4 && dZ.cols > 1024 && dZ.cols <= SX_MAXV4 * 256)
+    softmax_xent_row4_kernel<<<dZ.rows, 256, 0, (hipStream_t)stream>>>(Z, dd, labels, Y, strideY, E, strideE, stats);
+  else
+    softmax_xent_kernel<0><<<cdiv((long)dZ.rows * 64, 256), 256, 0, (hipStream_t)stream>>>(
+        Z, dd, labels, nullptr, 0, Y, strideY, E, strideE, stats, v4);
   TNET_LAUNCH_CHECK();
   return TNET_OK;
 }
