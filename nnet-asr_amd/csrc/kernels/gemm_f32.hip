@@ -470,6 +470,20 @@ __device__ unsigned long long g_tnet_stamps[8192 * 6];
 #define TNET_STAMP_RT(i) do { } while (0)
 #endif
 
+// V consecutive floats from LDS (ds_read_b128 / b64 / b32) into x[0..V)
+template <int V>
+__device__ __forceinline__ void lds_vec(const float* p, float (&x)[4]) {
+  if constexpr (V == 4) {
+    const f32x4 v = *reinterpret_cast<const f32x4*>(p);
+    x[0] = v[0]; x[1] = v[1]; x[2] = v[2]; x[3] = v[3];
+  } else if constexpr (V == 2) {
+    const float2 v = *reinterpret_cast<const float2*>(p);
+    x[0] = v.x; x[1] = v.y;
+  } else {
+    x[0] = *p;
+  }
+}
+
 // =============================================================================================
 // 16x16x4 variant (v_mfma_f32_16x16x4_f32: 32 cycles per 1024 MACs; on this part it sustains a
 // higher clock than the 32x32x2 form -- tools/mfma_peak.hip: ~155 vs ~137-145 TFLOP/s).
@@ -507,8 +521,11 @@ void gemm16_kernel(const GemmP p) {
   constexpr int WTM = BM / WM, WTN = BN / WN;  // wave tile
   constexpr int TM = WTM / 16, TN = WTN / 16;
   static_assert(WTM % 16 == 0 && WTN % 16 == 0, "16x16 tiles per wave");
-  static_assert(A_KC || TM % 4 == 0, "m-contiguous A interleaves 4 tiles per read");
-  static_assert(B_KC || TN % 4 == 0, "n-contiguous B interleaves 4 tiles per read");
+  // an m/n-contiguous operand is read VM/VN consecutive floats per lane (ds_read_b128/b64/b32), which
+  // feed VM/VN interleaved 16x16 tiles: tile V*q + e holds rows (cols) 16*V*q + V*i + e
+  constexpr int VM = A_KC ? 1 : (TM % 4 == 0 ? 4 : TM % 2 == 0 ? 2 : 1);
+  constexpr int VN = B_KC ? 1 : (TN % 4 == 0 ? 4 : TN % 2 == 0 ? 2 : 1);
+  constexpr int NRA = A_KC ? TM : 4 * TM / VM, NRB = B_KC ? TN : 4 * TN / VN;  // fragment reads per chunk
   static_assert(BK == 32 || BK == 64, "BK");
   constexpr int CH = BK / 4, KCH = BK / 16;
   constexpr int A_SZ = BM * BK, B_SZ = BN * BK, ST_SZ = A_SZ + B_SZ;
@@ -678,10 +695,11 @@ void gemm16_kernel(const GemmP p) {
 #pragma unroll
       for (int s = 0; s < 4; ++s)
 #pragma unroll
-        for (int q = 0; q < TM / 4; ++q) {
-          const f32x4 x = *reinterpret_cast<const f32x4*>(As + (16 * c + 4 * lg + s) * BM + wm0 + 64 * q + 4 * li);
+        for (int q = 0; q < TM / VM; ++q) {
+          float x[4];
+          lds_vec<VM>(As + (16 * c + 4 * lg + s) * BM + wm0 + 16 * VM * q + VM * li, x);
 #pragma unroll
-          for (int e = 0; e < 4; ++e) av[buf][4 * q + e][s] = x[e];
+          for (int e = 0; e < VM; ++e) av[buf][VM * q + e][s] = x[e];
         }
     }
     if (B_KC) {
@@ -696,10 +714,11 @@ void gemm16_kernel(const GemmP p) {
 #pragma unroll
       for (int s = 0; s < 4; ++s)
 #pragma unroll
-        for (int q = 0; q < TN / 4; ++q) {
-          const f32x4 x = *reinterpret_cast<const f32x4*>(Bs + (16 * c + 4 * lg + s) * BN + wn0 + 64 * q + 4 * li);
+        for (int q = 0; q < TN / VN; ++q) {
+          float x[4];
+          lds_vec<VN>(Bs + (16 * c + 4 * lg + s) * BN + wn0 + 16 * VN * q + VN * li, x);
 #pragma unroll
-          for (int e = 0; e < 4; ++e) bv[buf][4 * q + e][s] = x[e];
+          for (int e = 0; e < VN; ++e) bv[buf][VN * q + e][s] = x[e];
         }
     }
   };
@@ -717,9 +736,10 @@ void gemm16_kernel(const GemmP p) {
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
   };
-  constexpr int NRD = TM + TN;      // ds_read_b128 per chunk (both operand layouts)
+  constexpr int NRD = NRA + NRB;    // fragment reads per chunk
   constexpr int NMF = 4 * TM * TN;  // MFMAs per chunk
-  static_assert(NMF >= NRD + (SP == 1 ? PPC : LDR ? 0 : G), "interleave pattern");
+  // fillers (fragment reads, DMA pieces) pinned after each MFMA: one, or more on small wave tiles
+  constexpr int FPM = (NRD + (SP == 1 ? PPC : LDR ? 0 : G) + NMF - 1) / NMF;
   static_assert(PPC * KCH >= G, "pieces per chunk");
   // vmcnt at a seam: everything younger than tile t+1 may stay in flight -- tiles t+2..t+S-1 without
   // SP; with SP tiles t+2..t+S-2 plus the pieces of tile t+S-1 issued in the chunks before the seam
@@ -750,27 +770,30 @@ void gemm16_kernel(const GemmP p) {
   // and the epilogue is pure arithmetic + stores.  (Loaded at the end, each load waits behind the
   // stores issued before it -- vmcnt is in order -- one full round trip per row of the tile.)
   constexpr int EB = epi_base(EPI);
-  constexpr bool EV = !B_KC;  // output columns in 4-vectors (n-contiguous B) or scalars (k-contiguous B)
-  constexpr int NJ = EV ? TN / 4 : TN;
+  constexpr bool EV = !B_KC;  // output columns in VN-vectors (n-contiguous B) or scalars (k-contiguous B)
+  constexpr int NE = EV ? VN : 1;
+  constexpr int NJ = TN / NE;
   constexpr bool PRE_BIAS = EB == EPI_BIAS || EB == EPI_BIAS_SIG || EB == EPI_BIAS_NSIG || EB == EPI_BIAS_NEG;
   constexpr bool PRE_C = EB == EPI_SGD || EB == EPI_RBM;
   constexpr bool PRE_AUX = EB == EPI_DSIG;
   constexpr bool PRE_Q = EB == EPI_SGD || EB == EPI_RBM;
   auto erow = [&](int a, int r) {
-    return A_KC ? bm + wm0 + 16 * a + 4 * lg + r : bm + wm0 + 64 * (a / 4) + 4 * (4 * lg + r) + (a % 4);
+    return A_KC ? bm + wm0 + 16 * a + 4 * lg + r : bm + wm0 + 16 * VM * (a / VM) + VM * (4 * lg + r) + (a % VM);
   };
-  auto ecol = [&](int j) { return EV ? bn + wn0 + 64 * j + 4 * li : bn + wn0 + 16 * j + li; };
+  auto ecol = [&](int j) { return bn + wn0 + 16 * NE * j + NE * li; };
   auto ld_tile = [&](const float* base, long ld, int row, int col) {
     f32x4 v = {0.f, 0.f, 0.f, 0.f};
     if (row < M) {
       const float* q = base + (long)row * ld + col;
-      if (EV) {
-        if (col + 3 < N) v = *reinterpret_cast<const f32x4*>(q);
-        else
+      if (NE == 4 && col + 3 < N) {
+        v = *reinterpret_cast<const f32x4*>(q);
+      } else if (NE == 2 && col + 1 < N) {
+        const float2 t = *reinterpret_cast<const float2*>(q);
+        v[0] = t.x;
+        v[1] = t.y;
+      } else {
 #pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = col + e < N ? q[e] : 0.f;
-      } else if (col < N) {
-        v[0] = *q;
+        for (int e = 0; e < NE; ++e) v[e] = col + e < N ? q[e] : 0.f;
       }
     }
     return v;
@@ -785,13 +808,13 @@ void gemm16_kernel(const GemmP p) {
       const int col = ecol(j);
       f32x4 v = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int e = 0; e < (EV ? 4 : 1); ++e) v[e] = col + e < N ? p.bias[col + e] : 0.f;
+      for (int e = 0; e < NE; ++e) v[e] = col + e < N ? p.bias[col + e] : 0.f;
       pre_bias[j] = v;
     }
   }
   // tiles of more than 128 prefetched floats per lane (128x256 tiles) are loaded at the epilogue
   // instead, all at once (one round trip): held across the main loop they would spill
-  constexpr int PRE_TILE = TM * 4 * NJ * (EV ? 4 : 1);
+  constexpr int PRE_TILE = TM * 4 * NJ * NE;
   constexpr bool EARLY = ((PRE_C || PRE_AUX) ? PRE_TILE : 0) + (PRE_Q ? PRE_TILE : 0) <= 128;
   auto prefetch_tiles = [&]() {
     if constexpr (PRE_C || PRE_AUX) {
@@ -827,7 +850,7 @@ void gemm16_kernel(const GemmP p) {
   auto read_one = [&](const float* st, int c, int buf, int r) {
     const float* As = st;
     const float* Bs = st + A_SZ;
-    if (r < TM) {
+    if (r < NRA) {
       if (A_KC) {
         const int a = r, row = wm0 + 16 * a + li;
         const f32x4 x = *reinterpret_cast<const f32x4*>(As + row * BK + 4 * ((4 * c + lg) ^ swz<BK>(row)));
@@ -835,12 +858,13 @@ void gemm16_kernel(const GemmP p) {
         for (int s2 = 0; s2 < 4; ++s2) av[buf][a][s2] = x[s2];
       } else {
         const int s2 = r % 4, q = r / 4;
-        const f32x4 x = *reinterpret_cast<const f32x4*>(As + (16 * c + 4 * lg + s2) * BM + wm0 + 64 * q + 4 * li);
+        float x[4];
+        lds_vec<VM>(As + (16 * c + 4 * lg + s2) * BM + wm0 + 16 * VM * q + VM * li, x);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) av[buf][4 * q + e][s2] = x[e];
+        for (int e = 0; e < VM; ++e) av[buf][VM * q + e][s2] = x[e];
       }
     } else {
-      const int rb = r - TM;
+      const int rb = r - NRA;
       if (B_KC) {
         const int b = rb, col = wn0 + 16 * b + li;
         const f32x4 x = *reinterpret_cast<const f32x4*>(Bs + col * BK + 4 * ((4 * c + lg) ^ swz<BK>(col)));
@@ -848,9 +872,10 @@ void gemm16_kernel(const GemmP p) {
         for (int s2 = 0; s2 < 4; ++s2) bv[buf][b][s2] = x[s2];
       } else {
         const int s2 = rb % 4, q = rb / 4;
-        const f32x4 x = *reinterpret_cast<const f32x4*>(Bs + (16 * c + 4 * lg + s2) * BN + wn0 + 64 * q + 4 * li);
+        float x[4];
+        lds_vec<VN>(Bs + (16 * c + 4 * lg + s2) * BN + wn0 + 16 * VN * q + VN * li, x);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) bv[buf][4 * q + e][s2] = x[e];
+        for (int e = 0; e < VN; ++e) bv[buf][VN * q + e][s2] = x[e];
       }
     }
   };
@@ -901,7 +926,7 @@ void gemm16_kernel(const GemmP p) {
       }
       if (SP == 1) __builtin_amdgcn_s_setprio(1);
       constexpr int NP = SP == 1 ? PPC : LDR ? 0 : G;
-      int idx = 0;
+      int mi = 0;
 #pragma unroll
       for (int s = 0; s < 4; ++s)
 #pragma unroll
@@ -909,6 +934,9 @@ void gemm16_kernel(const GemmP p) {
 #pragma unroll
           for (int b = 0; b < TN; ++b) {
             acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[buf][a][s], bv[buf][b][s], acc[a][b], 0, 0, 0);
+#pragma unroll
+            for (int f = 0; f < FPM; ++f) {
+            const int idx = mi * FPM + f;
             if (idx < NRD) {
               __builtin_amdgcn_sched_barrier(0);
 #ifndef TNET_GEMM_DIAG_NOREAD
@@ -931,7 +959,8 @@ void gemm16_kernel(const GemmP p) {
                 __builtin_amdgcn_sched_barrier(0);
               }
             }
-            ++idx;
+            }
+            ++mi;
           }
       if (SP == 1) __builtin_amdgcn_s_setprio(0);
     }
@@ -1052,10 +1081,9 @@ void gemm16_kernel(const GemmP p) {
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
         const int col = ecol(j);
-        constexpr int NE = EV ? 4 : 1;
         f32x4 v;
 #pragma unroll
-        for (int e = 0; e < NE; ++e) v[e] = EV ? acc[a][4 * j + e][r] : acc[a][j][r];
+        for (int e = 0; e < NE; ++e) v[e] = acc[a][NE * j + e][r];
         f32x4 o = v, qn = v;
         if constexpr (EB == EPI_STORE) {
           if (p.beta == 0.f) {
@@ -1102,9 +1130,12 @@ void gemm16_kernel(const GemmP p) {
         }
         float* cp = p.C + (long)row * p.ldc + col;
         float* qp = has_q ? p.corr + (long)row * p.ldcorr + col : nullptr;
-        if (EV && col + 3 < N) {
+        if (NE == 4 && col + 3 < N) {
           *reinterpret_cast<f32x4*>(cp) = o;
           if (has_q) *reinterpret_cast<f32x4*>(qp) = qn;
+        } else if (NE == 2 && col + 1 < N) {
+          *reinterpret_cast<float2*>(cp) = float2{o[0], o[1]};
+          if (has_q) *reinterpret_cast<float2*>(qp) = float2{qn[0], qn[1]};
         } else {
 #pragma unroll
           for (int e = 0; e < NE; ++e)
@@ -1140,39 +1171,21 @@ void gemm16_kernel(const GemmP p) {
 // name: g<BM>x<BN>k<BK>s<S>w<waves>[i]: 32x32x2 kernel (waves laid out WMxWN; i = DMA pieces
 //       interleaved); m<BM>x<BN>k<BK>s<S>[w<WM><WN>][p|L]: 16x16x4 kernel (default 2x2 waves; p = DMA
 //       pieces spread over the chunks + MFMA at setprio 1; L = one extra loader wave issues all DMA)
-#define TNET_GEMM_CFGS(X)                                 \
-  X(g64x64k32s4w4, 0, 64, 64, 32, 2, 2, 4, 0)            \
-  X(g64x64k32s4w4i, 0, 64, 64, 32, 2, 2, 4, 1)           \
-  X(g64x64k64s2w4, 0, 64, 64, 64, 2, 2, 2, 0)            \
-  X(g64x64k32s4w2, 0, 64, 64, 32, 2, 1, 4, 0)            \
-  X(g128x64k32s3w4, 0, 128, 64, 32, 2, 2, 3, 0)          \
-  X(g64x128k32s3w4, 0, 64, 128, 32, 2, 2, 3, 0)          \
-  X(g128x128k32s3w8, 0, 128, 128, 32, 2, 4, 3, 0)        \
-  X(m64x128k32s4, 1, 64, 128, 32, 2, 2, 4, 0)            \
-  X(m64x128k64s3, 1, 64, 128, 64, 2, 2, 3, 0)            \
-  X(m64x64k32s4w41, 1, 64, 64, 32, 4, 1, 4, 0)           \
-  X(m128x128k32s3, 1, 128, 128, 32, 2, 2, 3, 0)          \
-  X(m128x128k64s2, 1, 128, 128, 64, 2, 2, 2, 0)          \
-  X(m64x128k32s4w12, 1, 64, 128, 32, 1, 2, 4, 0)         \
-  X(m64x128k32s3, 1, 64, 128, 32, 2, 2, 3, 0)            \
-  X(m64x128k32s2, 1, 64, 128, 32, 2, 2, 2, 0)            \
+#define TNET_GEMM_CFGS(X)                         \
+  X(g64x64k32s4w4, 0, 64, 64, 32, 2, 2, 4, 0)           \
+  X(m64x128k32s4, 1, 64, 128, 32, 2, 2, 4, 0)           \
+  X(m64x128k64s3, 1, 64, 128, 64, 2, 2, 3, 0)           \
+  X(m64x64k32s4w41, 1, 64, 64, 32, 4, 1, 4, 0)          \
+  X(m128x128k32s3, 1, 128, 128, 32, 2, 2, 3, 0)         \
+  X(m128x128k64s2, 1, 128, 128, 64, 2, 2, 2, 0)         \
   X(m64x128k64s2, 1, 64, 128, 64, 2, 2, 2, 0)           \
-  X(m64x128k64s2w42, 1, 64, 128, 64, 4, 2, 2, 0)         \
-  X(m64x128k32s3w42, 1, 64, 128, 32, 4, 2, 3, 0)         \
-  X(m64x128k32s4w42, 1, 64, 128, 32, 4, 2, 4, 0)         \
-  X(m64x64k32s4w21, 1, 64, 64, 32, 2, 1, 4, 0)           \
-  X(m64x64k64s2w21, 1, 64, 64, 64, 2, 1, 2, 0)           \
-  X(m64x128k32s2w12, 1, 64, 128, 32, 1, 2, 2, 0)         \
-  X(m64x128k32s3w12, 1, 64, 128, 32, 1, 2, 3, 0)         \
-  X(m64x128k64s3p, 1, 64, 128, 64, 2, 2, 3, 1)           \
-  X(m64x128k64s3w42p, 1, 64, 128, 64, 4, 2, 3, 1)        \
-  X(m64x128k32s4p, 1, 64, 128, 32, 2, 2, 4, 1)           \
-  X(m64x128k32s4w42p, 1, 64, 128, 32, 4, 2, 4, 1)        \
-  X(m128x128k32s3p, 1, 128, 128, 32, 2, 2, 3, 1)         \
-  X(m128x128k32s4p, 1, 128, 128, 32, 2, 2, 4, 1)         \
-  X(m64x128k64s2L, 1, 64, 128, 64, 2, 2, 2, 2)           \
-  X(m128x256k32s3, 1, 128, 256, 32, 2, 2, 3, 0)          \
-  X(m128x256k32s2, 1, 128, 256, 32, 2, 2, 2, 0)
+  X(m64x128k64s2w42, 1, 64, 128, 64, 4, 2, 2, 0)        \
+  X(m64x128k64s3p, 1, 64, 128, 64, 2, 2, 3, 1)          \
+  X(m64x128k64s2L, 1, 64, 128, 64, 2, 2, 2, 2)          \
+  X(m128x256k32s3, 1, 128, 256, 32, 2, 2, 3, 0)         \
+  X(m64x64k64s2, 1, 64, 64, 64, 2, 2, 2, 0)             \
+  X(m64x64k32s4, 1, 64, 64, 32, 2, 2, 4, 0)             \
+  X(m32x64k64s2, 1, 32, 64, 64, 2, 2, 2, 0)
 
 enum GemmCfg {
 #define X(name, ...) CFG_##name,
@@ -1213,12 +1226,8 @@ static bool launch_cfg(const GemmP& p, hipStream_t st) {
     const long extA = A_KC ? (long)p.M * p.lda : (long)BK * p.lda + p.M;
     const long extB = B_KC ? (long)p.N * p.ldb : (long)BK * p.ldb + p.N;
     if (4 * extA >= (1L << 32) || 4 * extB >= (1L << 32)) return false;
-    if constexpr ((A_KC || TM % 4 == 0) && (B_KC || TN % 4 == 0)) {
-      gemm16_kernel<BM, BN, BK, WM, WN, S, IL, A_KC, B_KC, EPI><<<tiles, (WM * WN + (IL == 2)) * 64, 0, st>>>(p);
-      return true;
-    } else {
-      return false;  // this tile cannot hold the operand layout
-    }
+    gemm16_kernel<BM, BN, BK, WM, WN, S, IL, A_KC, B_KC, EPI><<<tiles, (WM * WN + (IL == 2)) * 64, 0, st>>>(p);
+    return true;
   }
 }
 
@@ -1252,6 +1261,7 @@ static int launch_gemm(const GemmP& p_in, hipStream_t st) {
     else if (t128 >= 240) cfg = CFG_m128x128k64s2;
     else if (A_KC && t64x128 >= 200) cfg = CFG_m64x128k64s2;  // incl. the K = 440 first layer (one round)
     else if (A_KC && p.K < 1024) cfg = CFG_m64x64k32s4w41;
+    else if ((long)cdiv(p.M, 64) * cdiv(p.N, 64) >= 200) cfg = CFG_m64x64k32s4;  // e.g. the 440-row update
     else cfg = CFG_g64x64k32s4w4;
   }
   p.group = g_group > 0 ? g_group : 8;

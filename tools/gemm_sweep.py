@@ -10,8 +10,8 @@ import subprocess
 import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-CFGS = ["g64x64k32s4w4", "g64x64k64s2w4", "g64x64k32s4w2", "g64x64k64s2w2", "g128x64k32s3w4", "g64x128k32s3w4",
-        "g128x128k32s2w4", "g128x128k32s3w8", "g64x64k32s4w4+g1", "g64x64k32s4w4+noload"]
+CFGS = ["g64x64k32s4w4", "m64x128k64s2", "m64x128k32s4", "m64x128k64s3", "m128x128k64s2", "m128x128k32s3",
+        "m128x256k32s3", "m64x64k64s2", "m64x64k32s4", "m32x64k64s2", "m64x64k32s4w41"]
 # (kind, rows, n_in, n_out): fwd/bwd/upd of each layer of 440 -> 2048x4 -> 4000 at bunch 1024
 SHAPES = [("fwd", 1024, 2048, 2048), ("bwd", 1024, 2048, 2048), ("upd", 1024, 2048, 2048),
           ("fwd", 1024, 2048, 4000), ("bwd", 1024, 2048, 4000), ("upd", 1024, 2048, 4000),
