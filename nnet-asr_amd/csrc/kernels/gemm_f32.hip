@@ -765,7 +765,8 @@ void gemm16_kernel(const GemmP p) {
     read_frags(smem, 0, 0);
   }
   // Epilogue operands (bias / y of the layer below / W and the momentum buffer) are loaded into
-  // registers HERE, right after the prologue: the main loop hides their latency (a seam's counted
+  // registers HERE, right after the prologue (issued inside the main loop at tile 1 instead, they
+  // shortened the prologue by 3-4k cycles but stretched the main loop by 4-7k): the main loop hides their latency (a seam's counted
   // vmcnt wait may also wait for them: they are older than every DMA piece still in flight -- safe)
   // and the epilogue is pure arithmetic + stores.  (Loaded at the end, each load waits behind the
   // stores issued before it -- vmcnt is in order -- one full round trip per row of the tile.)
