@@ -1,6 +1,4 @@
 set -o pipefail
-mkdir -p gpurun_out
-for v in 1 pfloop 1 pfloop; do
-  TNET_DIAG_STAMP_LIB=$v timeout -k 10 120 python3 tools/gemm_clock.py 1.0 3 >> gpurun_out/pf_$v.log 2>&1 || exit 1
-done
+bash tools/profile_round.sh &&
+timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
 echo "done $?"
