@@ -1,4 +1,6 @@
 set -o pipefail
-bash tools/profile_round.sh &&
-timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
+mkdir -p gpurun_out
+timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 &&
+timeout -k 10 200 python3 bench.py --no-cpu-baseline --steps 100 > gpurun_out/b.json 2> gpurun_out/b.err &&
+timeout -k 10 120 python3 tools/gemm_clock.py 1.0 3 > gpurun_out/clock.log 2>&1
 echo "done $?"

@@ -153,7 +153,8 @@ int tnet_affine_fwd(const float* X, TnetMatrixDim dX, const float* W, TnetMatrix
  * Replaces CuRbm::Reconstruct (cuRbm.cc:117-128: AddScaledRow + Gemm('N','T') + Sigmoid). */
 int tnet_affine_fwd_t(const float* X, TnetMatrixDim dX, const float* W, TnetMatrixDim dW, const float* b,
                       float* Y, TnetMatrixDim dY, int act, void* stream);
-/* Eo = (E W^T) .* Ybelow (1 - Ybelow)  (dsig=1)  or  Eo = E W^T (dsig=0).
+/* Eo = (E W^T) .* Ybelow (1 - Ybelow)  (dsig=1)  or  Eo = E W^T (dsig=0); Ybelow 16-byte aligned with a
+ * stride that is a multiple of 4 (as the other operands).
  * Replaces Gemm('N','T') + CuMath::DiffSigmoid (cuBiasedLinearity.cc:21-25, cuActivation.cc:19-22). */
 int tnet_affine_bwd(const float* E, TnetMatrixDim dE, const float* W, TnetMatrixDim dW, const float* Ybelow,
                     int strideYbelow, float* Eo, TnetMatrixDim dEo, int dsig, void* stream);

@@ -774,6 +774,15 @@ void gemm16_kernel(const GemmP p) {
   constexpr bool EV = !B_KC;  // output columns in VN-vectors (n-contiguous B) or scalars (k-contiguous B)
   constexpr int NE = EV ? VN : 1;
   constexpr int NJ = TN / NE;
+  // TRE: k-contiguous A and B (NT: the backward GEMM) leave each lane 4 ROWS of one column per tile;
+  // the epilogue then goes through LDS (the ring is free after the main loop) so that every lane
+  // holds 4 consecutive COLUMNS of a row: 16-B loads of the diff-sigmoid operand and 16-B stores
+  // instead of one 4-B access per element
+  constexpr bool TRE = A_KC && B_KC && !LDR && (epi_base(EPI) == EPI_DSIG || epi_base(EPI) == EPI_STORE);
+  constexpr int LDT = WTN + 4, QPR = WTN / 4, RPP = 64 / QPR, TP = WTM / RPP;
+  static_assert(!TRE || (QPR <= 64 && 64 % QPR == 0 && WTM % RPP == 0 && NW * WTM * LDT <= S * ST_SZ),
+                "transposed epilogue");
+  const int tcq = lane % QPR, tr0 = lane / QPR;
   constexpr bool PRE_BIAS = EB == EPI_BIAS || EB == EPI_BIAS_SIG || EB == EPI_BIAS_NSIG || EB == EPI_BIAS_NEG;
   constexpr bool PRE_C = EB == EPI_SGD || EB == EPI_RBM;
   constexpr bool PRE_AUX = EB == EPI_DSIG;
@@ -802,6 +811,18 @@ void gemm16_kernel(const GemmP p) {
   f32x4 pre_bias[PRE_BIAS ? NJ : 1];
   f32x4 pre_a[PRE_C || PRE_AUX ? TM : 1][4][PRE_C || PRE_AUX ? NJ : 1];
   f32x4 pre_q[PRE_Q ? TM : 1][4][PRE_Q ? NJ : 1];
+  f32x4 pre_t[TRE ? TP : 1];
+  auto ld_row4 = [&](const float* base, long ld, int row, int col) {  // 4 columns of one row, masked
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    if (row < M) {
+      const float* q = base + (long)row * ld + col;
+      if (col + 3 < N) v = *reinterpret_cast<const f32x4*>(q);
+      else
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = col + e < N ? q[e] : 0.f;
+    }
+    return v;
+  };
   const bool has_q = PRE_Q && p.corr != nullptr;
   if constexpr (PRE_BIAS) {
 #pragma unroll
@@ -818,7 +839,11 @@ void gemm16_kernel(const GemmP p) {
   constexpr int PRE_TILE = TM * 4 * NJ * NE;
   constexpr bool EARLY = ((PRE_C || PRE_AUX) ? PRE_TILE : 0) + (PRE_Q ? PRE_TILE : 0) <= 128;
   auto prefetch_tiles = [&]() {
-    if constexpr (PRE_C || PRE_AUX) {
+    if constexpr (TRE) {
+      if constexpr (PRE_AUX)
+#pragma unroll
+        for (int q = 0; q < TP; ++q) pre_t[q] = ld_row4(p.aux, p.ldaux, bm + wm0 + tr0 + RPP * q, bn + wn0 + 4 * tcq);
+    } else if constexpr (PRE_C || PRE_AUX) {
       const float* base = PRE_AUX ? p.aux : p.C;
       const long ld = PRE_AUX ? p.ldaux : p.ldc;
 #pragma unroll
@@ -1065,11 +1090,68 @@ void gemm16_kernel(const GemmP p) {
     if (bm == 0) bias_pre_finish<BN, EPI == EPI_STORE_BG>(p, bn, bpre);
 
   if constexpr (!EARLY) prefetch_tiles();
+  constexpr bool CS = EPI == EPI_DSIG_CS;
+  static_assert(!CS || (A_KC && B_KC && WTM == kColsumSlabRows), "column sums: bwd layout, 32-row wave tiles");
+  if constexpr (TRE) {
+    // ---- transposed epilogue (see TRE)
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's last fragment reads retired
+    __builtin_amdgcn_s_barrier();         // every wave is done with the ring
+    float* wl = smem + wid * WTM * LDT;
+#pragma unroll
+    for (int a = 0; a < TM; ++a)
+#pragma unroll
+      for (int b = 0; b < TN; ++b)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) wl[(16 * a + 4 * lg + r) * LDT + 16 * b + li] = acc[a][b][r];
+    // EPI_DSIG_CS: the wave's 32 rows are one slab; a lane sums its rows of 4 columns in order, the
+    // lanes of a column quad meet by xor-shuffles
+    float cs4[4] = {0.f, 0.f, 0.f, 0.f};
+    const int col = bn + wn0 + 4 * tcq;
+#pragma unroll
+    for (int q = 0; q < TP; ++q) {
+      const int rl = tr0 + RPP * q, row = bm + wm0 + rl;
+      const f32x4 v = *reinterpret_cast<const f32x4*>(wl + rl * LDT + 4 * tcq);
+      if (row >= M) continue;
+      f32x4 o;
+      if constexpr (EB == EPI_STORE) {
+        if (p.beta == 0.f) {
+          o = p.alpha * v;
+        } else {
+          o = p.alpha * v + p.beta * ld_row4(p.C, p.ldc, row, col);
+        }
+      } else {  // EPI_DSIG
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] = pre_t[q][e] * (1.f - pre_t[q][e]) * v[e];
+      }
+      float* cp = p.C + (long)row * p.ldc + col;
+      if (col + 3 < N) {
+        *reinterpret_cast<f32x4*>(cp) = o;
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (col + e < N) cp[e] = o[e];
+      }
+      if constexpr (CS)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) cs4[e] += o[e];
+    }
+    if constexpr (CS) {
+#pragma unroll
+      for (int k = QPR; k < 64; k <<= 1)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) cs4[e] += __shfl_xor(cs4[e], k, 64);
+      const int slab_row = bm + wm0;
+      if (tr0 == 0 && slab_row < M) {
+        float* cp = p.cpart + (long)(slab_row / kColsumSlabRows) * p.ldcpart + col;
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (col + e < N) cp[e] = cs4[e];
+      }
+    }
+  } else {
   // ---- epilogue: arithmetic on the prefetched operands, then 16-B (n-contiguous) or 4-B stores
   // EPI_DSIG_CS: each wave owns 32 output rows (one slab) x its columns; a lane sums its 8 rows of
   // a column in order, the 4 lane groups of a column meet by two xor-shuffles
-  constexpr bool CS = EPI == EPI_DSIG_CS;
-  static_assert(!CS || (A_KC && B_KC && WTM == kColsumSlabRows), "column sums: bwd layout, 32-row wave tiles");
   float csum[CS ? TN : 1];
 #pragma unroll
   for (int j = 0; j < (CS ? TN : 1); ++j) csum[j] = 0.f;
@@ -1161,6 +1243,7 @@ void gemm16_kernel(const GemmP p) {
       for (int j = 0; j < TN; ++j)
         if (col0 + 16 * j < N) cp[col0 + 16 * j] = csum[j];
     }
+  }
   }
   TNET_STAMP(3);
   TNET_STAMP_RT(5);
@@ -1375,7 +1458,7 @@ extern "C" int tnet_affine_bwd(const float* E, TnetMatrixDim dE, const float* W,
   int st = check_common(p);
   if (st) return st;
   if (dsig) {
-    if (!Ybelow) return TNET_ERR_ARG;
+    if (!Ybelow || !aligned16(Ybelow) || (strideYbelow & 3)) return TNET_ERR_ARG;
     return launch_gemm<true, true, EPI_DSIG>(p, (hipStream_t)stream);
   }
   return launch_gemm<true, true, EPI_STORE>(p, (hipStream_t)stream);
@@ -1405,7 +1488,7 @@ extern "C" int tnet_affine_bwd_colsum(const float* E, TnetMatrixDim dE, const fl
                                       float* colpart, int ldcolpart, void* stream) {
   // tnet_affine_bwd with dsig, plus colpart[s][c] = sum of Eo[r][c] over the 32-row slab s (fp32, in row order)
   if (dE.cols != dW.cols || dEo.rows != dE.rows || dEo.cols != dW.rows || !Ybelow || !colpart ||
-      ldcolpart < dEo.cols)
+      ldcolpart < dEo.cols || !aligned16(Ybelow) || (strideYbelow & 3))
     return TNET_ERR_ARG;
   GemmP p{};
   p.M = dE.rows; p.N = dW.rows; p.K = dE.cols;
