@@ -1,6 +1,7 @@
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 &&
-timeout -k 10 200 python3 bench.py --no-cpu-baseline --steps 100 > gpurun_out/b.json 2> gpurun_out/b.err &&
-timeout -k 10 120 python3 tools/gemm_clock.py 1.0 3 > gpurun_out/clock.log 2>&1
+rm -f gpurun_out/doff_*.log
+for v in 1 dmaoff6 dmaoff14 1 dmaoff6 dmaoff14; do
+  TNET_DIAG_STAMP_LIB=$v timeout -k 10 120 python3 tools/gemm_clock.py 1.0 3 >> gpurun_out/doff_$v.log 2>&1 || exit 1
+done
 echo "done $?"
