@@ -10,8 +10,7 @@ TNetCu per-bunch loop (src/TNetCu.cc:427-441).
 Multi-GPU (launched by torch.distributed.run): one process per GPU, utterance-sharded caches
 (weak scaling: 1024 frames per GPU per step), per-layer RCCL all-reduce of the gradients over
 xGMI, global-bunch GRADDIVFRM normalisation.  torch is used only for the gloo rendezvous /
-barrier / max-reduce of the timings; it is imported after the HIP library so one HIP runtime is
-loaded.
+barrier / max-reduce of the timings; at N>1 it is imported before the HIP library (one ROCm runtime, clean exit).
 
 Extra JSON fields: roofline (dominant kernel = the 2048x2048 affine-layer GEMMs, timed with hipEvents
 on the library stream over K further steps of the same workload right after the timed region: one
@@ -32,7 +31,12 @@ sys.path.insert(0, os.path.join(REPO, "oracle"))
 
 import numpy as np  # noqa: E402
 
-import tnet_amd  # noqa: E402  (loads libtnet_amd.so before torch: one HIP runtime in the process)
+if int(os.environ.get("WORLD_SIZE", "1")) > 1 or os.environ.get("TNET_BENCH_TORCH_FIRST"):
+    # multi-rank: torch (rendezvous / barrier / max over ranks) is loaded BEFORE the HIP library, so its
+    # bundled ROCm runtime serves both -- the order of tests/dp_worker.py.  Loaded after, the process
+    # aborted in runtime teardown at exit ("double free or corruption") once the JSON line was out.
+    import torch  # noqa: E402,F401
+import tnet_amd  # noqa: E402
 from tnet_amd import Comm, Network, Objective, Trainer, formats  # noqa: E402
 from tnet_amd._lib import check, lib  # noqa: E402
 
@@ -107,6 +111,11 @@ def main():
     ap.add_argument("--lr", type=float, default=1.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--comm", default="rccl", choices=["rccl", "host"],
+                    help="N>1 gradient transport: RCCL over xGMI (the measured path), or 'host' (gloo through "
+                         "host memory) to rehearse the multi-process launch on a one-GPU box")
+    ap.add_argument("--same-device", action="store_true",
+                    help="rehearsal only: every rank on GPU 0 (with --comm host)")
     ap.add_argument("--force-dp", action="store_true",
                     help="diagnostic: run the data-parallel path (gradient GEMMs + RCCL all-reduce + SGD apply) "
                          "even at N=1, on a one-rank RCCL communicator")
@@ -124,15 +133,24 @@ def main():
     dims = CONFIGS[args.config]
     B = args.bunch
 
-    check(lib().tnet_select_gpu(local_rank), "select_gpu")
+    check(lib().tnet_select_gpu(0 if args.same_device else local_rank), "select_gpu")
     dist = None
     comm = None
     if world > 1:
         import torch.distributed as dist  # noqa: F811  (gloo only: rendezvous, barrier, max)
         dist.init_process_group("gloo")
-        uid = [Comm.unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(uid, src=0)
-        comm = Comm(rank, world, uid[0])
+        if args.comm == "host":
+            import torch
+
+            def allreduce(a):
+                t = torch.from_numpy(a)
+                dist.all_reduce(t)
+
+            comm = Comm.host(rank, world, allreduce)
+        else:
+            uid = [Comm.unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(uid, src=0)
+            comm = Comm(rank, world, uid[0])
     elif args.force_dp:
         comm = Comm(0, 1, Comm.unique_id())
 
@@ -239,7 +257,9 @@ def main():
             "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
             "config": {"workload": f"TNet SGD step, {'x'.join(map(str, dims))} sigmoid MLP + softmax xent",
                        "bunch_per_gpu": B, "global_bunch": B * world, "frames_resident_per_gpu": args.cache,
-                       "parallelism": f"dp{world}" + (" (RCCL all-reduce)" if world > 1 or args.force_dp else ""),
+                       "parallelism": f"dp{world}" + ((" (RCCL all-reduce)" if args.comm == "rccl" else
+                                                       " (host all-reduce rehearsal)")
+                                                      if world > 1 or args.force_dp else ""),
                        "flops_per_frame": flops_per_frame(dims),
                        "achieved_tflops_whole_step": round(value * flops_per_frame(dims) / 1e12 / world, 2),
                        "gemm_share_of_kernel_time": round(all_gemm_ms / all_ms, 4) if all_ms else None},
@@ -251,9 +271,21 @@ def main():
                             "only the roofline kernels)",
         }
         print(json.dumps(line), flush=True)
+    # release the library objects in dependency order (trainer -> objective / network -> communicator)
+    # while the HIP runtime and the process group are still up
+    tnet_amd.synchronize()
+    for name in ("trainer", "obj", "net", "comm"):
+        if os.environ.get("TNET_BENCH_TRACE_TEARDOWN"):
+            print(f"teardown {name}", file=sys.stderr, flush=True)
+        locals_ = {"trainer": trainer, "obj": obj, "net": net, "comm": comm}
+        o = locals_[name]
+        if o is not None:
+            o.__del__()
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
+    if os.environ.get("TNET_BENCH_TRACE_TEARDOWN"):
+        print("teardown done", file=sys.stderr, flush=True)
 
 
 if __name__ == "__main__":
