@@ -1,4 +1,4 @@
 set -o pipefail
-mkdir -p gpurun_out
-TNET_BENCH_TORCH_FIRST=1 timeout -k 10 300 python3 bench.py --force-dp --no-cpu-baseline --steps 30 > gpurun_out/b_dpt.json 2> gpurun_out/b_dpt.err
+bash tools/profile_round.sh &&
+timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
 echo "done $?"
