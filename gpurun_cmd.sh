@@ -1,4 +1,4 @@
 set -o pipefail
-bash tools/profile_round.sh &&
-timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
+mkdir -p gpurun_out
+timeout -k 10 600 python3 -u -m pytest tests/test_gpu_kernels.py -x -q --timeout 120 --timeout-method thread -k "bwd" > gpurun_out/kt.log 2>&1
 echo "done $?"

@@ -98,7 +98,7 @@ def test_affine_fwd(act, rows, n_in, n_out, gemm_cfg):
         assert np.all(np.abs(got - z) <= 2e-5 * mag + 1e-6)
 
 
-@pytest.mark.parametrize("rows,n_in,n_out", [(16, 32, 10), (1024, 2048, 2048), (1024, 2048, 4000)])
+@pytest.mark.parametrize("rows,n_in,n_out", [(16, 32, 10), (45, 37, 50), (1024, 2048, 2048), (1024, 2048, 4000)])
 def test_affine_bwd_dsig(rows, n_in, n_out, gemm_cfg):
     E, W = rnd((rows, n_out), 9), rnd((n_in, n_out), 10, 0.1)
     Yb = 1 / (1 + np.exp(-rnd((rows, n_in), 11)))
@@ -136,8 +136,8 @@ def slab_sums(M, slab=32):
     return np.stack([M[s * slab:(s + 1) * slab].astype(np.float64).sum(0) for s in range(n)])
 
 
-@pytest.mark.parametrize("rows,n_in,n_out", [(16, 32, 10), (33, 64, 40), (1024, 2048, 2048), (1000, 440, 2048),
-                                             (1024, 2048, 4000)])
+@pytest.mark.parametrize("rows,n_in,n_out", [(16, 32, 10), (33, 64, 40), (45, 37, 50), (1024, 2048, 2048),
+                                             (1000, 440, 2048), (1024, 2048, 4000)])
 def test_affine_bwd_colsum(rows, n_in, n_out):
     """bwd + diff-sigmoid with the bias gradient of the layer below as 32-row slab column sums"""
     E, W = rnd((rows, n_out), 9), rnd((n_in, n_out), 10, 0.1)
