@@ -18,7 +18,35 @@ void SeedRandom(long seed) { GlobalRng().Seed(seed); }
 #define S ((void*)CuDevice::Instantiate().Stream())
 
 CuCache::CuCache() {}
-CuCache::~CuCache() {}
+CuCache::~CuCache() {
+  if (mCopy) (void)hipStreamSynchronize(mCopy);
+  (void)hipStreamSynchronize(CuDevice::Instantiate().Stream());
+  for (hipEvent_t e : {mRel[0], mRel[1], mFilled, mSync, mPermEv[0], mPermEv[1]})
+    if (e) (void)hipEventDestroy(e);
+  for (int* p : mPermPinned)
+    if (p) (void)hipHostFree(p);
+  if (mCopy) (void)hipStreamDestroy(mCopy);
+}
+
+// the copy stream waits for everything enqueued on the compute stream so far
+void CuCache::CopyAfterCompute() {
+  TNET_HIP_CALL(hipEventRecord(mSync, CuDevice::Instantiate().Stream()));
+  TNET_HIP_CALL(hipStreamWaitEvent(mCopy, mSync, 0));
+}
+
+// the compute stream waits for everything enqueued on the copy stream so far
+static void compute_after_copy(hipStream_t copy, hipEvent_t ev) {
+  TNET_HIP_CALL(hipEventRecord(ev, copy));
+  TNET_HIP_CALL(hipStreamWaitEvent(CuDevice::Instantiate().Stream(), ev, 0));
+}
+
+// first bunch of a fill: the compute stream waits for the fill's intake copies
+void CuCache::EnterExhaust() {
+  mState = EXHAUST;
+  mExhaustPos = 0;
+  TNET_HIP_CALL(hipEventRecord(mFilled, mCopy));
+  TNET_HIP_CALL(hipStreamWaitEvent(CuDevice::Instantiate().Stream(), mFilled, 0));
+}
 
 void CuCache::Init(size_t cachesize, size_t bunchsize) {
   if (bunchsize == 0 || (cachesize % bunchsize) != 0) Error("Non divisible cachesize by bunchsize");
@@ -44,12 +72,47 @@ void CuCache::WarnLong(size_t rows) {
 }
 
 void CuCache::Alloc(size_t cols, size_t tcols) {
-  if (mFeatures.Rows() != mCachesize || mFeatures.Cols() != cols) mFeatures.Init(mCachesize, cols);
-  if (mMode == DENSE) {
-    if (mDesired.Rows() != mCachesize || mDesired.Cols() != tcols) mDesired.Init(mCachesize, tcols);
-  } else {
-    mLabels.Init(mCachesize);
+  if (!mCopy) {
+    TNET_HIP_CALL(hipStreamCreateWithFlags(&mCopy, hipStreamNonBlocking));
+    for (hipEvent_t* e : {&mRel[0], &mRel[1], &mFilled, &mSync, &mPermEv[0], &mPermEv[1]})
+      TNET_HIP_CALL(hipEventCreateWithFlags(e, hipEventDisableTiming));
   }
+  if (mPerm.Dim() != mCachesize) {
+    // sized once: a reallocation could hand memory that queued gathers still read to someone else
+    (void)hipStreamSynchronize(CuDevice::Instantiate().Stream());
+    mPerm.Init(mCachesize);
+    for (int k = 0; k < 2; ++k) {
+      if (mPermPinned[k]) TNET_HIP_CALL(hipHostFree(mPermPinned[k]));
+      TNET_HIP_CALL(hipHostMalloc((void**)&mPermPinned[k], mCachesize * sizeof(int), hipHostMallocDefault));
+      mPermEvSet[k] = false;
+    }
+  }
+  bool fresh = false;
+  auto mat = [&](CuMatrix<BaseFloat>& m, size_t c) {
+    if (m.Rows() != mCachesize || m.Cols() != c) {
+      m.Init(mCachesize, c);
+      fresh = true;
+    }
+  };
+  auto vec = [&](CuVector<int>& v) {
+    if (v.Dim() != mCachesize) {
+      v.Init(mCachesize);
+      fresh = true;
+    }
+  };
+  mat(mFeatures, cols);
+  mat(mFeaturesAlt, cols);
+  mat(mFeaturesLeftover, cols);
+  if (mMode == DENSE) {
+    mat(mDesired, tcols);
+    mat(mDesiredAlt, tcols);
+    mat(mDesiredLeftover, tcols);
+  } else {
+    vec(mLabels);
+    vec(mLabelsAlt);
+    vec(mLabelsLeftover);
+  }
+  if (fresh) CopyAfterCompute();  // the allocations' zero-fills (compute stream) precede any copy
 }
 
 void CuCache::BeginIntake() {
@@ -57,6 +120,16 @@ void CuCache::BeginIntake() {
   if (mTrace & 3) std::cout << "/" << std::flush;
   mState = INTAKE;
   mIntakePos = 0;
+  // flip the double buffer: the fill just exhausted (its gathers are all enqueued) becomes the
+  // alternate; the new fill goes into the buffer the fill before last used, once its gathers ran
+  hipStream_t cs = CuDevice::Instantiate().Stream();
+  TNET_HIP_CALL(hipEventRecord(mRel[mCurId], cs));
+  mHasRel[mCurId] = true;
+  mFeatures.Swap(mFeaturesAlt);
+  mDesired.Swap(mDesiredAlt);
+  mLabels.Swap(mLabelsAlt);
+  mCurId ^= 1;
+  if (mHasRel[mCurId]) TNET_HIP_CALL(hipStreamWaitEvent(mCopy, mRel[mCurId], 0));
   size_t leftover = mLeftoverRows;
   if (leftover > mCachesize) {
     std::ostringstream os;
@@ -66,16 +139,19 @@ void CuCache::BeginIntake() {
     leftover = mCachesize;
   }
   if (leftover > 0) {
-    mFeatures.CopyRows(leftover, 0, mFeaturesLeftover, 0);
+    // on the copy stream; leftover rows a device intake wrote on the compute stream are waited for
+    if (!mLeftoverOnCopy) CopyAfterCompute();
+    TNET_HIP_CALL(hipMemcpy2DAsync(mFeatures.pCUData(), mFeatures.Stride() * sizeof(float), mFeaturesLeftover.pCUData(),
+                                   mFeaturesLeftover.Stride() * sizeof(float), mFeatures.Cols() * sizeof(float),
+                                   leftover, hipMemcpyDeviceToDevice, mCopy));
     if (mMode == DENSE) {
-      mDesired.CopyRows(leftover, 0, mDesiredLeftover, 0);
+      TNET_HIP_CALL(hipMemcpy2DAsync(mDesired.pCUData(), mDesired.Stride() * sizeof(float), mDesiredLeftover.pCUData(),
+                                     mDesiredLeftover.Stride() * sizeof(float), mDesired.Cols() * sizeof(float),
+                                     leftover, hipMemcpyDeviceToDevice, mCopy));
     } else {
       TNET_HIP_CALL(hipMemcpyAsync(mLabels.pCUData(), mLabelsLeftover.pCUData(), leftover * sizeof(int),
-                                   hipMemcpyDeviceToDevice, CuDevice::Instantiate().Stream()));
+                                   hipMemcpyDeviceToDevice, mCopy));
     }
-    mFeaturesLeftover.Destroy();
-    mDesiredLeftover.Destroy();
-    mLabelsLeftover.Destroy();
     mIntakePos += leftover;
   }
   mLeftoverRows = 0;
@@ -99,11 +175,14 @@ void CuCache::AddData(const CuMatrix<BaseFloat>& rFeatures, const CuMatrix<BaseF
   mFeatures.CopyRows(fill, 0, rFeatures, mIntakePos);
   mDesired.CopyRows(fill, 0, rDesired, mIntakePos);
   if (leftover > 0) {
-    mFeaturesLeftover.Init(leftover, mFeatures.Cols());
-    mDesiredLeftover.Init(leftover, mDesired.Cols());
-    mFeaturesLeftover.CopyRows(leftover, fill, rFeatures, 0);
-    mDesiredLeftover.CopyRows(leftover, fill, rDesired, 0);
+    // the leftover buffers hold the cache size (the reference truncates a longer leftover); the copy
+    // stream may still be reading the previous leftover
+    const size_t keep = leftover < mCachesize ? leftover : mCachesize;
+    compute_after_copy(mCopy, mSync);
+    mFeaturesLeftover.CopyRows(keep, fill, rFeatures, 0);
+    mDesiredLeftover.CopyRows(keep, fill, rDesired, 0);
     mLeftoverRows = leftover;
+    mLeftoverOnCopy = false;
   }
   mIntakePos += fill;
   if (mIntakePos == mCachesize) {
@@ -126,12 +205,13 @@ void CuCache::AddDataLabels(const CuMatrix<BaseFloat>& rFeatures, const CuVector
   TNET_HIP_CALL(hipMemcpyAsync(mLabels.pCUData() + mIntakePos, rLabels.pCUData(), fill * sizeof(int),
                                hipMemcpyDeviceToDevice, st));
   if (leftover > 0) {
-    mFeaturesLeftover.Init(leftover, mFeatures.Cols());
-    mFeaturesLeftover.CopyRows(leftover, fill, rFeatures, 0);
-    mLabelsLeftover.Init(leftover);
-    TNET_HIP_CALL(hipMemcpyAsync(mLabelsLeftover.pCUData(), rLabels.pCUData() + fill, leftover * sizeof(int),
+    const size_t keep = leftover < mCachesize ? leftover : mCachesize;
+    compute_after_copy(mCopy, mSync);
+    mFeaturesLeftover.CopyRows(keep, fill, rFeatures, 0);
+    TNET_HIP_CALL(hipMemcpyAsync(mLabelsLeftover.pCUData(), rLabels.pCUData() + fill, keep * sizeof(int),
                                  hipMemcpyDeviceToDevice, st));
     mLeftoverRows = leftover;
+    mLeftoverOnCopy = false;
   }
   mIntakePos += fill;
   if (mIntakePos == mCachesize) mState = FULL;
@@ -145,23 +225,24 @@ void CuCache::AddDataHost(const float* feats, size_t rows, size_t cols, size_t l
   if (mState != INTAKE) Error("CuCache::AddDataHost: cache not in INTAKE state");
   const size_t space = mCachesize - mIntakePos;
   const size_t fill = space < rows ? space : rows, leftover = rows - fill;
-  hipStream_t st = CuDevice::Instantiate().Stream();
+  hipStream_t st = mCopy;  // overlaps the training queued on the compute stream
   if (fill) {
     TNET_HIP_CALL(hipMemcpy2DAsync(mFeatures.pCURowData(mIntakePos), mFeatures.Stride() * sizeof(float), feats,
                                    ld * sizeof(float), cols * sizeof(float), fill, hipMemcpyHostToDevice, st));
     TNET_HIP_CALL(hipMemcpyAsync(mLabels.pCUData() + mIntakePos, labels, fill * sizeof(int), hipMemcpyHostToDevice, st));
   }
   if (leftover > 0) {
-    mFeaturesLeftover.Init(leftover, cols);
+    const size_t keep = leftover < mCachesize ? leftover : mCachesize;
     TNET_HIP_CALL(hipMemcpy2DAsync(mFeaturesLeftover.pCUData(), mFeaturesLeftover.Stride() * sizeof(float),
-                                   feats + fill * ld, ld * sizeof(float), cols * sizeof(float), leftover,
+                                   feats + fill * ld, ld * sizeof(float), cols * sizeof(float), keep,
                                    hipMemcpyHostToDevice, st));
-    mLabelsLeftover.Init(leftover);
-    TNET_HIP_CALL(hipMemcpyAsync(mLabelsLeftover.pCUData(), labels + fill, leftover * sizeof(int),
+    TNET_HIP_CALL(hipMemcpyAsync(mLabelsLeftover.pCUData(), labels + fill, keep * sizeof(int),
                                  hipMemcpyHostToDevice, st));
     mLeftoverRows = leftover;
+    mLeftoverOnCopy = true;
   }
-  TNET_HIP_CALL(hipStreamSynchronize(st));  // caller's host buffers may be reused
+  // the caller's host buffers may be reused: wait for the copies (not for the queued training)
+  TNET_HIP_CALL(hipStreamSynchronize(st));
   mIntakePos += fill;
   if (mIntakePos == mCachesize) mState = FULL;
 }
@@ -173,7 +254,16 @@ void CuCache::Randomize() {
   std::iota(mPermHost.begin(), mPermHost.end(), 0);
   Rng48& rng = mRng ? *mRng : GlobalRng();
   rng.RandomShuffle(mPermHost.data(), mIntakePos);
-  mPerm.CopyFromHost(mPermHost.data(), mIntakePos, /*sync=*/true);
+  // upload from a pinned slot on the compute stream (ordered after the gathers that read the
+  // previous permutation); the slot's previous upload finished long ago (two shuffles back)
+  const int k = mPermSlot;
+  if (mPermEvSet[k]) TNET_HIP_CALL(hipEventSynchronize(mPermEv[k]));
+  std::copy(mPermHost.begin(), mPermHost.end(), mPermPinned[k]);
+  hipStream_t cs = CuDevice::Instantiate().Stream();
+  TNET_HIP_CALL(hipMemcpyAsync(mPerm.pCUData(), mPermPinned[k], mIntakePos * sizeof(int), hipMemcpyHostToDevice, cs));
+  TNET_HIP_CALL(hipEventRecord(mPermEv[k], cs));
+  mPermEvSet[k] = true;
+  mPermSlot ^= 1;
   mRandomized = true;
 }
 
@@ -194,10 +284,7 @@ void CuCache::AdvanceAfterBunch() {
 void CuCache::GetBunch(CuMatrix<BaseFloat>& rFeatures, CuMatrix<BaseFloat>& rDesired) {
   if (mState == EMPTY) Error("GetBunch on empty cache!!!");
   if (mMode != DENSE) Error("CuCache::GetBunch: cache holds class ids, use GetBunchLabels");
-  if (mState == FULL || mState == INTAKE) {
-    mState = EXHAUST;
-    mExhaustPos = 0;
-  }
+  if (mState == FULL || mState == INTAKE) EnterExhaust();
   rFeatures.Init(mBunchsize, mFeatures.Cols());
   rDesired.Init(mBunchsize, mDesired.Cols());
   if (mRandomized) {
@@ -216,10 +303,7 @@ void CuCache::GetBunch(CuMatrix<BaseFloat>& rFeatures, CuMatrix<BaseFloat>& rDes
 void CuCache::GetBunchLabels(CuMatrix<BaseFloat>& rFeatures, CuVector<int>& rLabels) {
   if (mState == EMPTY) Error("GetBunch on empty cache!!!");
   if (mMode != LABELS) Error("CuCache::GetBunchLabels: cache holds dense targets, use GetBunch");
-  if (mState == FULL || mState == INTAKE) {
-    mState = EXHAUST;
-    mExhaustPos = 0;
-  }
+  if (mState == FULL || mState == INTAKE) EnterExhaust();
   rFeatures.Init(mBunchsize, mFeatures.Cols());
   rLabels.Init(mBunchsize);
   if (mRandomized) {

@@ -11,7 +11,12 @@
 //     row-gather kernel) instead of materialising a shuffled copy of the whole cache -- same
 //     rows, half the HBM traffic;
 //   * one-hot targets are held as class ids (4 B/frame; a 4000-senone one-hot cache row is
-//     16 KB); a dense-target mode keeps the reference's AddData(features, desired) API.
+//     16 KB); a dense-target mode keeps the reference's AddData(features, desired) API;
+//   * the cache is double-buffered and a host intake (AddDataHost) copies on its own copy stream:
+//     the next fill streams in over PCIe while the GPU still trains on the previous one (the
+//     compute stream waits for the copies once, when the new fill starts being exhausted; the copy
+//     stream waits, before writing a buffer, for the gathers of the fill that last used it).
+//     Leftover buffers are allocated once at the cache size (no allocation between the streams).
 #pragma once
 
 #include "cumatrix.h"
@@ -61,6 +66,8 @@ class CuCache {
   void CheckMode(Mode m);
   void WarnLong(size_t rows);
   void AdvanceAfterBunch();
+  void EnterExhaust();
+  void CopyAfterCompute();
 
   State mState = EMPTY;
   Mode mMode = UNSET;
@@ -73,6 +80,22 @@ class CuCache {
   CuMatrix<BaseFloat> mFeatures, mDesired, mFeaturesLeftover, mDesiredLeftover;
   CuVector<int> mLabels, mLabelsLeftover;
   size_t mLeftoverRows = 0;
+  bool mLeftoverOnCopy = false;  // the leftover rows were written on the copy stream (host intake)
+  // double buffer: the fill being taken in / exhausted is mFeatures/mLabels/mDesired; the other one
+  // holds the previous fill, which queued gathers may still read
+  CuMatrix<BaseFloat> mFeaturesAlt, mDesiredAlt;
+  CuVector<int> mLabelsAlt;
+  int mCurId = 0;                    // physical buffer behind mFeatures (0/1)
+  hipStream_t mCopy = nullptr;
+  hipEvent_t mRel[2] = {nullptr, nullptr};  // compute stream: last gathers of buffer 0/1 enqueued
+  bool mHasRel[2] = {false, false};
+  hipEvent_t mFilled = nullptr;      // copy stream: intake copies of the current fill enqueued
+  hipEvent_t mSync = nullptr;
+  // permutation upload from pinned host memory (two slots: the host never waits for the GPU)
+  int* mPermPinned[2] = {nullptr, nullptr};
+  hipEvent_t mPermEv[2] = {nullptr, nullptr};
+  bool mPermEvSet[2] = {false, false};
+  int mPermSlot = 0;
   CuVector<int> mPerm;          // device permutation of intake rows
   std::vector<int> mPermHost;
 };

@@ -180,6 +180,17 @@ class CuMatrix {
   size_t mRows = 0, mCols = 0, mStride = 0, mBytes = 0;
   T* mpCUData = nullptr;
   bool mView = false;
+
+ public:
+  /// exchange the storage of two matrices (double buffers)
+  void Swap(CuMatrix& o) {
+    std::swap(mRows, o.mRows);
+    std::swap(mCols, o.mCols);
+    std::swap(mStride, o.mStride);
+    std::swap(mBytes, o.mBytes);
+    std::swap(mpCUData, o.mpCUData);
+    std::swap(mView, o.mView);
+  }
 };
 
 template <typename T>
@@ -261,6 +272,14 @@ class CuVector {
   size_t mDim = 0, mBytes = 0;
   T* mpCUData = nullptr;
   bool mView = false;
+
+ public:
+  void Swap(CuVector& o) {
+    std::swap(mDim, o.mDim);
+    std::swap(mBytes, o.mBytes);
+    std::swap(mpCUData, o.mpCUData);
+    std::swap(mView, o.mView);
+  }
 };
 
 }  // namespace TNet

@@ -515,9 +515,6 @@ void gemm16_kernel(const GemmP p) {
   constexpr int NT = WM * WN * 64, NW = WM * WN;
   constexpr bool LDR = SP == 2;
   static_assert(SP != 1 || S >= 3, "spread DMA needs a 3-slot ring");
-#ifdef TNET_GEMM_DIAG_NOBAR
-  static_assert(!LDR, "the loader wave meets the compute waves at every seam barrier");
-#endif
   constexpr int WTM = BM / WM, WTN = BN / WN;  // wave tile
   constexpr int TM = WTM / 16, TN = WTN / 16;
   static_assert(WTM % 16 == 0 && WTN % 16 == 0, "16x16 tiles per wave");
@@ -946,7 +943,9 @@ void gemm16_kernel(const GemmP p) {
         __builtin_amdgcn_sched_barrier(0);
         __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
         if constexpr (!LDR) wait_vmcnt<SEAM_VM>();
-#ifndef TNET_GEMM_DIAG_NOBAR
+#ifdef TNET_GEMM_DIAG_NOBAR
+        if constexpr (LDR) barrier();  // the loader wave meets the compute waves at every seam barrier
+#else
         barrier();
 #endif
       }
