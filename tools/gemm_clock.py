@@ -82,6 +82,9 @@ for kind in KINDS:
         recs.append(dict(n_wg=n, clock_GHz=float(np.median(clk)), prologue_cyc=float(np.median(t1 - t0)),
                          main_cyc=float(np.median(t2 - t1)), epilogue_cyc=float(np.median(t3 - t2)),
                          total_cyc=float(np.median(t3 - t0)),
+                         total_cyc_max=float(np.max(t3 - t0)),
+                         n_wg_slow=float(np.sum((t3 - t0) > np.median(t3 - t0) + 2000)),
+                         end_rt_spread_us=float((np.percentile(r1, 100) - np.percentile(r1, 50)) / 100.0),
                          start_spread_us=float((r0.max() - r0.min()) / 100.0),
                          end_spread_us=float((r1.max() - r1.min()) / 100.0),
                          span_us=float((r1.max() - r0.min()) / 100.0)))

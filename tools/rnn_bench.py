@@ -1,0 +1,45 @@
+#!/usr/bin/env python3
+"""BASELINE config 5 (TRecurrentCu: 440 -> 512-unit Elman RNN -> softmax, 1000-frame utterances,
+BPTT order 4, frame-by-frame SGD) on the GPU, next to the oracle's C restatement of the same loop on
+one host core (oracle/tnet_oracle.c orc_rnn_utterance: the reference's CuRecurrent arithmetic in
+plain C -- a CPU stand-in, not the reference binary, which is CUDA-only).
+
+usage: python tools/rnn_bench.py [utterances] [senones]"""
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "nnet-asr_amd"))
+sys.path.insert(0, os.path.join(REPO, "oracle"))
+import numpy as np  # noqa: E402
+
+import oracle as orc  # noqa: E402
+import tnet_amd  # noqa: E402
+from tnet_amd import Network, Objective, RnnTrainer, formats  # noqa: E402
+
+n_utt = int(sys.argv[1]) if len(sys.argv) > 1 else 4
+S = int(sys.argv[2]) if len(sys.argv) > 2 else 135
+nIn, H, T, bptt, lr = 440, 512, 1000, 4, 0.01
+rng = np.random.default_rng(0)
+layers = formats.gen_recurrent_init(nIn, H, S, seed=7)
+feats = [rng.standard_normal((T, nIn)).astype(np.float32) for _ in range(n_utt)]
+labels = [rng.integers(0, S, T).astype(np.int32) for _ in range(n_utt)]
+
+net = Network.from_layers(layers)
+net.set_learn_rate(lr)
+obj = Objective()
+tr = RnnTrainer(net, obj, bptt=bptt)
+tr.train_utterance(feats[0][:50], labels[0][:50])  # warm-up
+tnet_amd.synchronize()
+t0 = time.perf_counter()
+tr.train_corpus(feats, labels)
+tnet_amd.synchronize()
+gpu = n_utt * T / (time.perf_counter() - t0)
+
+m = orc.RNN(layers[0].W, layers[0].b, layers[1].W, layers[1].b)
+t0 = time.perf_counter()
+m.utterance(feats[0], labels[0], bptt, lr, 0.0, 0.0)
+cpu = T / (time.perf_counter() - t0)
+print(f"RNN {nIn}->{H}(recurrent, bptt {bptt})->{S}, {T}-frame utterances: GPU {gpu:.0f} frames/s, "
+      f"oracle C restatement (1 core) {cpu:.0f} frames/s", flush=True)
