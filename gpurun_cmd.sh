@@ -1,5 +1,4 @@
 set -o pipefail
-mkdir -p gpurun_out
-timeout -k 10 300 python3 tools/rnn_bench.py 4 135 > gpurun_out/rnn.log 2>&1 &&
-timeout -k 10 300 python3 tools/rnn_bench.py 2 4000 >> gpurun_out/rnn.log 2>&1
+bash tools/profile_round.sh &&
+timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
 echo "done $?"
