@@ -228,6 +228,29 @@ int tnet_rbm_bias_update(const float* M, TnetMatrixDim d, int neg_from, float* b
                          float mmt, void* workspace, void* stream);
 
 /* ---- single-frame kernels (TRecurrentCu: CuMath::OffsetGemv / BlasGer, cumath.cc:292-362) ---- */
+/* single-frame forward of the recurrent layer: y = act(b + [v0, v1] W) for the row [v0 (K0), v1 (K1)]
+ * read in place, also stored to vout (K0+K1 floats, NULL: not stored) -- CuRecurrent::Propagate's
+ * history push + OffsetGemv (cuRecurrent.cc:26-47) in two launches; v1 may alias y. */
+int tnet_gemv_rowvec_cat(const float* v0, int K0, const float* v1, int K1, float* vout, const float* W, int ldw,
+                         const float* b, float* y, int N, int act, void* workspace, void* stream);
+/* single-frame output layer + softmax + cross-entropy (CuBiasedLinearity::Propagate, CuSoftmax::
+ * Propagate, CuCrossEntropy::EvaluateLabels for one row; TRecurrentCu.cc:360-368): z = b + v W,
+ * y = softmax(z), e = y - onehot(*label), xent / correct added to stats slot 0.  z / y / e may be NULL.
+ * N <= 4096 (else TNET_ERR_UNSUPPORTED); workspace: tnet_gemv_workspace(K, N) bytes. */
+int tnet_gemv_rowvec_softmax_xent(const float* v, int K, const float* W, int ldw, const float* b, float* z, float* y,
+                                  float* e, int N, const int* label, double* stats, void* workspace, void* stream);
+/* single-frame CuBiasedLinearity::Backpropagate + Update (cuBiasedLinearity.cc:32-64) in one pass
+ * over W: e_out = W e (with the weights before the update), then the update of
+ * tnet_affine_update_row; with s != NULL also d_out = e_out .* s (1 - s) (the diff-sigmoid of a
+ * recurrent layer below).  e_out / d_out may be NULL. */
+int tnet_affine_bwd_update_row(const float* x, int n_in, const float* e, int n_out, float* W, int ldw, float* corrW,
+                               int ldc, float* b, float* corr_b, float scale, float mmt, float l2, float* e_out,
+                               const float* s, float* d_out, void* stream);
+/* one frame's tnet_affine_update + tnet_bias_update in one launch (the output layer of TRecurrentCu,
+ * cuBiasedLinearity.cc:46-64 with one row): c = x_i e_j (+ mmt corrW); W += scale c; W += l2 W;
+ * b += scale (e_j + mmt corr_b). corrW / corr_b may be NULL when mmt == 0. */
+int tnet_affine_update_row(const float* x, int n_in, const float* e, int n_out, float* W, int ldw, float* corrW,
+                           int ldc, float* b, float* corr_b, float scale, float mmt, float l2, void* stream);
 /* workspace bytes for tnet_gemv_rowvec */
 long tnet_gemv_workspace(int K, int N);
 /* y[0:N] = act(b + v[0:K] W), W [K x N] row-major (ld ldw), act 0 none | 1 sigmoid; b may be NULL.

@@ -102,6 +102,14 @@ void CuBiasedLinearity::UpdateFrom(const CuMatrix<BaseFloat>& X, const CuMatrix<
   float scale, l2;
   UpdateConstants(X.Rows(), &scale, &l2);
   const bool mmt = mMomentum != 0.0f;
+  if (X.Rows() == 1) {  // single frame (TRecurrentCu's output layer): one rank-1 launch
+    TNET_SAFE_CALL(tnet_affine_update_row(X.pCUData(), (int)GetNInputs(), E.pCUData(), (int)GetNOutputs(),
+                                          mLinearity.pCUData(), (int)mLinearity.Stride(),
+                                          mmt ? mLinearityCorrection.pCUData() : nullptr,
+                                          (int)mLinearityCorrection.Stride(), mBias.pCUData(),
+                                          mmt ? mBiasCorrection.pCUData() : nullptr, scale, mMomentum, l2, S));
+    return;
+  }
   // bias first: it reads only E (the weight kernel rewrites W in place)
   TnetMatrixDim dE = E.Dim();
   void* ws = CuDevice::Instantiate().Workspace((size_t)tnet_col_sum_workspace(dE));
@@ -118,6 +126,22 @@ void CuBiasedLinearity::UpdateFrom(const CuMatrix<BaseFloat>& X, const CuMatrix<
   TNET_SAFE_CALL(tnet_affine_update(X.pCUData(), X.Dim(), E.pCUData(), dE, mLinearity.pCUData(), mLinearity.Dim(),
                                     mmt ? mLinearityCorrection.pCUData() : nullptr,
                                     (int)mLinearityCorrection.Stride(), scale, mMomentum, l2, S));
+}
+
+void CuBiasedLinearity::BackpropUpdateRow(const CuMatrix<BaseFloat>& X, const CuMatrix<BaseFloat>& E,
+                                          CuMatrix<BaseFloat>& Eout, const float* s, float* d) {
+  CuProfileScope p("CuBiasedLinearity::BackpropUpdate");
+  if (X.Rows() != 1 || E.Rows() != 1) Error("CuBiasedLinearity::BackpropUpdateRow: one frame only");
+  float scale, l2;
+  UpdateConstants(1, &scale, &l2);
+  const bool mmt = mMomentum != 0.0f;
+  Eout.Init(1, GetNInputs());
+  TNET_SAFE_CALL(tnet_affine_bwd_update_row(X.pCUData(), (int)GetNInputs(), E.pCUData(), (int)GetNOutputs(),
+                                            mLinearity.pCUData(), (int)mLinearity.Stride(),
+                                            mmt ? mLinearityCorrection.pCUData() : nullptr,
+                                            (int)mLinearityCorrection.Stride(), mBias.pCUData(),
+                                            mmt ? mBiasCorrection.pCUData() : nullptr, scale, mMomentum, l2,
+                                            Eout.pCUData(), s, d, S));
 }
 
 void CuBiasedLinearity::UpdateFromColsum(const CuMatrix<BaseFloat>& X, const CuMatrix<BaseFloat>& E,

@@ -40,6 +40,10 @@ class CuBiasedLinearity : public CuUpdatableComponent {
   void UpdateConstants(size_t rows, float* scale, float* l2) const;
   /// Update from explicit input/error matrices (fused GEMM + SGD epilogue, + bias kernel)
   void UpdateFrom(const CuMatrix<BaseFloat>& X, const CuMatrix<BaseFloat>& E);
+  /// single frame: Backpropagate (E -> Eout, old weights) + Update in one pass over W; with s != NULL
+  /// also d = Eout .* s (1 - s) (tnet_affine_bwd_update_row)
+  void BackpropUpdateRow(const CuMatrix<BaseFloat>& X, const CuMatrix<BaseFloat>& E, CuMatrix<BaseFloat>& Eout,
+                         const float* s, float* d);
   // same update with the bias gradient taken from the 32-row slab column sums of E that the backward
   // GEMM of the layer above wrote (tnet_affine_bwd_colsum): one launch instead of three
   void UpdateFromColsum(const CuMatrix<BaseFloat>& X, const CuMatrix<BaseFloat>& E, const CuMatrix<BaseFloat>& colpart);

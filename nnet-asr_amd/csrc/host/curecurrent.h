@@ -32,6 +32,9 @@ class CuRecurrent : public CuUpdatableComponent {
   void PropagateFnc(const CuMatrix<BaseFloat>& X, CuMatrix<BaseFloat>& Y) override;
   void BackpropagateFnc(const CuMatrix<BaseFloat>& X, CuMatrix<BaseFloat>& Y) override;
   void Update() override;
+  /// Update with d_0 = e .* y(1-y) already in DiffRow0() (written by the fused output-layer kernel)
+  void UpdateFromDiff0();
+  float* DiffRow0() { return mDiff.pCURowData(0); }
 
   /// BPTT order; allocates the (ord+1)-row input history (cuRecurrent.h:30-33)
   void BpttOrder(int ord);
@@ -70,6 +73,10 @@ class CuRecurrentTrainer {
   CuNetwork* mNet;
   CuObjectiveFunction* mObj;
   bool mCrossval;
+  // [<recurrent>, <biasedlinearity>, <softmax>] + cross-entropy: the per-frame chain on the fused
+  // single-frame kernels (8 launches a frame instead of 18)
+  bool FusedFrameOk() const;
+  void TrainFrameFused(size_t f);
   CuMatrix<BaseFloat> mFeats, mOut, mErr, mRow;
   CuVector<int> mLabels, mLabelRow;
   long mFrames = 0;

@@ -10,24 +10,32 @@
 //     one wavefront per row, float4 loads, butterfly reduction;
 //   * recurrent weight update: all BPTT outer products + weight decay + the weight write in ONE
 //     pass over W (the reference: bptt+1 cublasSger calls, AddScaled, AddScaled).
+#include <float.h>
+
 #include "kcommon.h"
 
 namespace tnetk {
 
 constexpr int GV_KSLICE = 64;  // k rows per split-K slice
 
-// partial[s][c] = sum_{k in slice s} v[k] * W[k][c]
-__global__ __launch_bounds__(256) void gemv_rowvec_partial(const float* __restrict__ v, int K,
+// partial[s][c] = sum_{k in slice s} v[k] * W[k][c], v = [v0[0:K0], v1[0:K-K0]] (the recurrent
+// layer's [x_t, y_{t-1}], read in place); the column-block-0 workgroups also store v to vout (the
+// history row, cuRecurrent.cc:31-35), so the two row copies need no launches of their own
+__global__ __launch_bounds__(256) void gemv_rowvec_partial(const float* __restrict__ v0, int K0,
+                                                           const float* __restrict__ v1, int K,
                                                            const float* __restrict__ W, long ldw, int N,
-                                                           float* __restrict__ partial) {
+                                                           float* __restrict__ partial, float* __restrict__ vout) {
   __shared__ float red[4][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + lane;
   const int k0 = blockIdx.y * GV_KSLICE, k1 = min(K, k0 + GV_KSLICE);
+  auto vk = [&](int k) { return k < K0 ? v0[k] : v1[k - K0]; };
+  if (vout && blockIdx.x == 0)
+    for (int k = k0 + threadIdx.x; k < k1; k += blockDim.x) vout[k] = vk(k);
   float acc = 0.f;
   if (c < N) {
 #pragma unroll 4
-    for (int k = k0 + w; k < k1; k += 4) acc += v[k] * W[(long)k * ldw + c];
+    for (int k = k0 + w; k < k1; k += 4) acc += vk(k) * W[(long)k * ldw + c];
   }
   red[w][lane] = acc;
   __syncthreads();
@@ -43,6 +51,79 @@ __global__ __launch_bounds__(256) void gemv_rowvec_final(const float* __restrict
   for (int k = 0; k < slices; ++k) s += partial[(long)k * N + c];
   const float a = (b ? b[c] : 0.f) + s;
   y[c] = act == 1 ? sigmoidf_ref(a) : a;
+}
+
+// the output layer + <softmax> + cross-entropy of one frame (TRecurrentCu's
+// CuBiasedLinearity::Propagate -> CuSoftmax::Propagate -> CuCrossEntropy::EvaluateLabels, with the
+// network-output and error copies): z = b + sum_s partial[s] (the order of gemv_rowvec_final),
+// y = softmax(z), e = y - onehot(t), xent / argmax-correct into the stats slots.  One workgroup,
+// N <= GV_SMX_MAX columns held in registers (16 per thread).
+constexpr int GV_SMX_PER = 16, GV_SMX_MAX = 256 * GV_SMX_PER;
+__global__ __launch_bounds__(256) void gemv_softmax_xent_final(const float* __restrict__ partial, int slices, int N,
+                                                               const float* __restrict__ b, float* __restrict__ z,
+                                                               float* __restrict__ y, float* __restrict__ e,
+                                                               const int* __restrict__ label,
+                                                               double* __restrict__ stats) {
+  __shared__ float smax[4];
+  __shared__ double ssum[4];
+  __shared__ ArgMax sarg[4];
+  __shared__ float syt;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  float rv[GV_SMX_PER];
+  float m = -1e20f;
+#pragma unroll
+  for (int q = 0; q < GV_SMX_PER; ++q) {
+    const int c = threadIdx.x + 256 * q;
+    float a = -1e30f;
+    if (c < N) {
+      float s = 0.f;
+      for (int k = 0; k < slices; ++k) s += partial[(long)k * N + c];
+      a = (b ? b[c] : 0.f) + s;
+      if (z) z[c] = a;
+    }
+    rv[q] = a;
+    m = fmaxf(m, a);
+  }
+  m = wave_max(m);
+  if (lane == 0) smax[wv] = m;
+  __syncthreads();
+  m = fmaxf(fmaxf(smax[0], smax[1]), fmaxf(smax[2], smax[3]));
+  float s = 0.f;
+#pragma unroll
+  for (int q = 0; q < GV_SMX_PER; ++q) {
+    if (threadIdx.x + 256 * q < N) {
+      rv[q] = fast_exp(rv[q] - m);
+      s += rv[q];
+    }
+  }
+  const double ws = wave_sum_d((double)s);
+  if (lane == 0) ssum[wv] = ws;
+  __syncthreads();
+  const float rsum = 1.f / (float)(ssum[0] + ssum[1] + ssum[2] + ssum[3]);
+  const int t = label[0];
+  ArgMax ay{-1e20f, 0x7fffffff};
+#pragma unroll
+  for (int q = 0; q < GV_SMX_PER; ++q) {
+    const int c = threadIdx.x + 256 * q;
+    if (c < N) {
+      const float yc = rv[q] * rsum;
+      if (yc > ay.v) { ay.v = yc; ay.i = c; }
+      if (y) y[c] = yc;
+      if (e) e[c] = yc - (c == t ? 1.f : 0.f);
+      if (c == t) syt = yc;
+    }
+  }
+  ay = wave_argmax(ay);
+  if (lane == 0) sarg[wv] = ay;
+  __syncthreads();
+  if (threadIdx.x == 0 && stats) {
+    ArgMax a = sarg[0];
+#pragma unroll
+    for (int w = 1; w < 4; ++w) a = argmax_merge(a, sarg[w]);
+    const double xent = (t >= 0 && t < N) ? -(double)logf(fmaxf(syt, FLT_MIN)) : 0.0;
+    atomicAdd(stats, xent);
+    atomicAdd(stats + 1, (a.i == (t >= 0 ? t : 0)) ? 1.0 : 0.0);
+  }
 }
 
 // y[r] = beta*y[r] + dot(W[r0 + r, 0:n], x) ; then if s != NULL: y[r] *= s[r] (1 - s[r])
@@ -101,21 +182,170 @@ __global__ __launch_bounds__(256) void rnn_update_kernel(float* __restrict__ W, 
   *wp = corr + w;
 }
 
+// single-frame CuBiasedLinearity::Backpropagate + Update (cuBiasedLinearity.cc:32-64) in one pass
+// over W, one wavefront per weight row i: eo[i] = W[i,:] . e with the OLD row (the order of
+// gemv_rows_kernel), then the row's SGD exactly as affine_update_row_kernel; with s: d[i] =
+// eo[i] s_i (1 - s_i) -- the diff-sigmoid of the recurrent layer below (cuRecurrent.cc:88-92).
+// Workgroups past the weight rows update the bias.
+__global__ __launch_bounds__(256) void affine_bwd_update_row_kernel(
+    const float* __restrict__ x, int n_in, const float* __restrict__ e, int n_out, float* __restrict__ W, long ldw,
+    float* __restrict__ corrW, long ldc, float* __restrict__ b, float* __restrict__ cb, float scale, float mmt,
+    float l2, float* __restrict__ eo, const float* __restrict__ s, float* __restrict__ d, int row_blocks) {
+  if ((int)blockIdx.x >= row_blocks) {  // bias
+    const int j = (blockIdx.x - row_blocks) * blockDim.x + threadIdx.x;
+    if (j >= n_out) return;
+    float g = e[j];
+    if (cb) {
+      g = g + mmt * cb[j];
+      cb[j] = g;
+    }
+    b[j] = b[j] + scale * g;
+    return;
+  }
+  const int lane = threadIdx.x & 63;
+  const int i = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  if (i >= n_in) return;
+  const float xi = x[i];
+  float* row = W + (long)i * ldw;
+  float* qrow = corrW ? corrW + (long)i * ldc : nullptr;
+  auto upd = [&](float w, float ej, float* q) {
+    float c = xi * ej;
+    if (qrow) {
+      c = c + mmt * *q;
+      *q = c;
+    }
+    w = w + scale * c;
+    return w + l2 * w;
+  };
+  float acc = 0.f;
+  if ((n_out & 3) == 0 && (ldw & 3) == 0 && (!qrow || (ldc & 3) == 0) &&
+      (((uintptr_t)row | (uintptr_t)e | (uintptr_t)qrow) & 15) == 0) {
+    for (int c = lane * 4; c < n_out; c += 256) {
+      f32x4 a = *reinterpret_cast<const f32x4*>(row + c);
+      const f32x4 ev = *reinterpret_cast<const f32x4*>(e + c);
+      acc += a[0] * ev[0] + a[1] * ev[1] + a[2] * ev[2] + a[3] * ev[3];
+      f32x4 qv = qrow ? *reinterpret_cast<const f32x4*>(qrow + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+      float q[4] = {qv[0], qv[1], qv[2], qv[3]};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) a[k] = upd(a[k], ev[k], &q[k]);
+      *reinterpret_cast<f32x4*>(row + c) = a;
+      if (qrow) *reinterpret_cast<f32x4*>(qrow + c) = f32x4{q[0], q[1], q[2], q[3]};
+    }
+  } else {
+    for (int c = lane; c < n_out; c += 64) {
+      const float w = row[c], ej = e[c];
+      acc += w * ej;
+      row[c] = upd(w, ej, qrow ? qrow + c : nullptr);
+    }
+  }
+  acc = wave_sum(acc);
+  if (lane == 0) {
+    if (eo) eo[i] = acc;
+    if (d) d[i] = acc * (s[i] * (1.f - s[i]));
+  }
+}
+
+// single-frame CuBiasedLinearity::Update (cuBiasedLinearity.cc:46-64) as one rank-1 kernel: the
+// GEMM's acc = x_i e_j (one exact fp32 product), the SGD epilogue of tnet_affine_update and the bias
+// SGD of tnet_bias_update (the column sum of one row is the row) -- three launches in one
+__global__ __launch_bounds__(256) void affine_update_row_kernel(const float* __restrict__ x, int n_in,
+                                                                const float* __restrict__ e, int n_out,
+                                                                float* __restrict__ W, long ldw,
+                                                                float* __restrict__ corrW, long ldc,
+                                                                float* __restrict__ b, float* __restrict__ cb,
+                                                                float scale, float mmt, float l2) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  const int i = blockIdx.y;
+  if (j >= n_out) return;
+  const float ej = e[j];
+  if (i == n_in) {  // bias
+    float g = ej;
+    if (cb) {
+      g = g + mmt * cb[j];
+      cb[j] = g;
+    }
+    b[j] = b[j] + scale * g;
+    return;
+  }
+  float c = x[i] * ej;
+  if (corrW) {
+    float* qp = corrW + (long)i * ldc + j;
+    c = c + mmt * *qp;
+    *qp = c;
+  }
+  float* wp = W + (long)i * ldw + j;
+  float w = *wp;
+  w = w + scale * c;
+  w = w + l2 * w;
+  *wp = w;
+}
+
 }  // namespace tnetk
 
 using namespace tnetk;
+
+extern "C" int tnet_affine_update_row(const float* x, int n_in, const float* e, int n_out, float* W, int ldw,
+                                      float* corrW, int ldc, float* b, float* corr_b, float scale, float mmt,
+                                      float l2, void* stream) {
+  if (n_in <= 0 || n_out <= 0 || !x || !e || !W || !b || ldw < n_out || (corrW && ldc < n_out) ||
+      (mmt != 0.f && (!corrW || !corr_b)))
+    return TNET_ERR_ARG;
+  affine_update_row_kernel<<<dim3(cdiv(n_out, 256), n_in + 1), 256, 0, (hipStream_t)stream>>>(
+      x, n_in, e, n_out, W, ldw, corrW, ldc, b, mmt != 0.f ? corr_b : nullptr, scale, mmt, l2);
+  TNET_LAUNCH_CHECK();
+  return TNET_OK;
+}
+
+extern "C" int tnet_affine_bwd_update_row(const float* x, int n_in, const float* e, int n_out, float* W, int ldw,
+                                          float* corrW, int ldc, float* b, float* corr_b, float scale, float mmt,
+                                          float l2, float* e_out, const float* s, float* d_out, void* stream) {
+  if (n_in <= 0 || n_out <= 0 || !x || !e || !W || !b || ldw < n_out || (corrW && ldc < n_out) ||
+      (mmt != 0.f && (!corrW || !corr_b)) || (d_out && !s))
+    return TNET_ERR_ARG;
+  const int row_blocks = cdiv((long)n_in * 64, 256);
+  affine_bwd_update_row_kernel<<<row_blocks + cdiv(n_out, 256), 256, 0, (hipStream_t)stream>>>(
+      x, n_in, e, n_out, W, ldw, mmt != 0.f ? corrW : nullptr, ldc, b, mmt != 0.f ? corr_b : nullptr, scale, mmt,
+      l2, e_out, s, d_out, row_blocks);
+  TNET_LAUNCH_CHECK();
+  return TNET_OK;
+}
 
 extern "C" long tnet_gemv_workspace(int K, int N) { return (long)cdiv(K, GV_KSLICE) * (N > 0 ? N : 1) * 4; }
 
 extern "C" int tnet_gemv_rowvec(const float* v, int K, const float* W, int ldw, const float* b, float* y, int N,
                                 int act, void* workspace, void* stream) {
   if (K <= 0 || N <= 0 || ldw < N || !v || !W || !y || !workspace || act < 0 || act > 1) return TNET_ERR_ARG;
+  return tnet_gemv_rowvec_cat(v, K, nullptr, 0, nullptr, W, ldw, b, y, N, act, workspace, stream);
+}
+
+extern "C" int tnet_gemv_rowvec_cat(const float* v0, int K0, const float* v1, int K1, float* vout, const float* W,
+                                    int ldw, const float* b, float* y, int N, int act, void* workspace,
+                                    void* stream) {
+  const int K = K0 + K1;
+  if (K0 < 0 || K1 < 0 || K <= 0 || N <= 0 || ldw < N || (K0 && !v0) || (K1 && !v1) || !W || !y || !workspace ||
+      act < 0 || act > 1)
+    return TNET_ERR_ARG;
   const int slices = cdiv(K, GV_KSLICE);
   float* part = (float*)workspace;
   hipStream_t st = (hipStream_t)stream;
-  gemv_rowvec_partial<<<dim3(cdiv(N, 64), slices), 256, 0, st>>>(v, K, W, ldw, N, part);
+  gemv_rowvec_partial<<<dim3(cdiv(N, 64), slices), 256, 0, st>>>(v0, K0, v1, K, W, ldw, N, part, vout);
   TNET_LAUNCH_CHECK();
   gemv_rowvec_final<<<cdiv(N, 256), 256, 0, st>>>(part, slices, N, b, y, act);
+  TNET_LAUNCH_CHECK();
+  return TNET_OK;
+}
+
+extern "C" int tnet_gemv_rowvec_softmax_xent(const float* v, int K, const float* W, int ldw, const float* b,
+                                             float* z, float* y, float* e, int N, const int* label, double* stats,
+                                             void* workspace, void* stream) {
+  if (K <= 0 || N <= 0 || ldw < N || !v || !W || !label || !workspace) return TNET_ERR_ARG;
+  if (N > GV_SMX_MAX) return TNET_ERR_UNSUPPORTED;
+  const int slices = cdiv(K, GV_KSLICE);
+  float* part = (float*)workspace;
+  hipStream_t st = (hipStream_t)stream;
+  gemv_rowvec_partial<<<dim3(cdiv(N, 64), slices), 256, 0, st>>>(v, K, nullptr, K, W, ldw, N, part, nullptr);
+  TNET_LAUNCH_CHECK();
+  gemv_softmax_xent_final<<<1, 256, 0, st>>>(part, slices, N, b, z, y, e, label, stats);
   TNET_LAUNCH_CHECK();
   return TNET_OK;
 }

@@ -37,6 +37,28 @@ __device__ __forceinline__ float sigmoidf_ref(float x) {
   return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-1.44269504088896341f * x));
 }
 
+struct ArgMax {
+  float v;
+  int i;
+};
+__device__ __forceinline__ ArgMax argmax_merge(ArgMax a, ArgMax b) {
+  // first maximum wins: larger value, or equal value with smaller index
+  if (b.v > a.v || (b.v == a.v && b.i < a.i)) return b;
+  return a;
+}
+__device__ __forceinline__ ArgMax wave_argmax(ArgMax a) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    ArgMax b{__shfl_xor(a.v, o, 64), __shfl_xor(a.i, o, 64)};
+    a = argmax_merge(a, b);
+  }
+  return a;
+}
+
+// exp(x) for x <= 0 on v_exp_f32: exp2(x*log2 e); relative error ~|x|*6e-8 (the rounding of the
+// scaled argument), i.e. <= 1e-6 over the 16 nats that carry any probability mass
+__device__ __forceinline__ float fast_exp(float x) { return __builtin_amdgcn_exp2f(1.44269504088896341f * x); }
+
 inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }
 
 }  // namespace tnetk

@@ -140,27 +140,7 @@ static int colsum_run(const float* M, TnetMatrixDim d, void* workspace, hipStrea
 // ---------------------------------------------------------------------------------------------
 constexpr int SX_MAXV4 = 16;  // row held in registers up to 16 float4 per lane = 4096 columns
 
-struct ArgMax {
-  float v;
-  int i;
-};
-__device__ __forceinline__ ArgMax argmax_merge(ArgMax a, ArgMax b) {
-  // first maximum wins: larger value, or equal value with smaller index
-  if (b.v > a.v || (b.v == a.v && b.i < a.i)) return b;
-  return a;
-}
-__device__ __forceinline__ ArgMax wave_argmax(ArgMax a) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    ArgMax b{__shfl_xor(a.v, o, 64), __shfl_xor(a.i, o, 64)};
-    a = argmax_merge(a, b);
-  }
-  return a;
-}
 
-// exp(x) for x <= 0 on v_exp_f32: exp2(x*log2 e); relative error ~|x|*6e-8 (the rounding of the
-// scaled argument), i.e. <= 1e-6 over the 16 nats that carry any probability mass
-__device__ __forceinline__ float fast_exp(float x) { return __builtin_amdgcn_exp2f(1.44269504088896341f * x); }
 
 // KIND 0: class-id labels; KIND 1: dense targets D.  Z == nullptr: Y already holds softmax output.
 template <int KIND>

@@ -206,6 +206,47 @@ def test_affine_grad_bias(rows, n_in, n_out, gemm_cfg):
     np.testing.assert_array_equal(dgb.numpy().ravel(), P.astype(np.float64).sum(0).astype(np.float32))
 
 
+@pytest.mark.parametrize("mmt", [0.0, 0.9])
+@pytest.mark.parametrize("n_in,n_out", [(1, 1), (512, 135), (440, 2048), (37, 4001)])
+def test_affine_update_row(mmt, n_in, n_out):
+    """one-frame weight + bias SGD in one launch (TRecurrentCu's output layer) agrees with the
+    GEMM-epilogue update + column-sum bias update it replaces"""
+    x, e = rnd((1, n_in), 40), rnd((1, n_out), 41, 0.01)
+    W, corr, b, corr_b = rnd((n_in, n_out), 42, 0.1), rnd((n_in, n_out), 43, 0.01), rnd(n_out, 44), rnd(n_out, 45)
+    scale, l2 = -0.02, -1e-4
+    out = []
+    for fused in (True, False):
+        dX, dE, dW, db = (DeviceArray.from_numpy(x), DeviceArray.from_numpy(e), DeviceArray.from_numpy(W),
+                          DeviceArray.vector(b))
+        dC = DeviceArray.from_numpy(corr) if mmt else None
+        dCb = DeviceArray.vector(corr_b) if mmt else None
+        if fused:
+            check(lib().tnet_affine_update_row(dX.ptr, n_in, dE.ptr, n_out, dW.ptr, dW.stride,
+                                               dC.ptr if dC else None, dC.stride if dC else 0, db.ptr,
+                                               dCb.ptr if dCb else None, scale, mmt, l2, S()))
+        else:
+            ws = DeviceArray(1, max(1, lib().tnet_col_sum_workspace(dE.dim) // 4 + 64))
+            check(lib().tnet_bias_update(dE.ptr, dE.dim, db.ptr, dCb.ptr if dCb else None, None, scale, mmt,
+                                         ws.ptr, S()))
+            check(lib().tnet_affine_update(dX.ptr, dX.dim, dE.ptr, dE.dim, dW.ptr, dW.dim, dC.ptr if dC else None,
+                                           dC.stride if dC else 0, scale, mmt, l2, S()))
+        synchronize()
+        out.append([a.numpy() for a in (dW, db, dC, dCb) if a is not None])
+    c = x.T.astype(np.float64) * e + mmt * corr
+    w = W + scale * c
+    w = w + l2 * w
+    np.testing.assert_allclose(out[0][0], w, rtol=1e-6, atol=1e-7)
+    np.testing.assert_allclose(out[0][1].ravel(), b + scale * (e[0] + mmt * corr_b), rtol=1e-6, atol=1e-7)
+    for a, r in zip(out[0], out[1]):
+        np.testing.assert_allclose(a, r, rtol=2.5e-7, atol=1e-9)
+
+
+def test_affine_update_row_rejects_missing_momentum_buffer():
+    d = DeviceArray(1, 8)
+    assert lib().tnet_affine_update_row(d.ptr, 8, d.ptr, 8, d.ptr, 8, None, 0, d.ptr, None, 0.1, 0.5, 0.0,
+                                        S()) == -1  # TNET_ERR_ARG
+
+
 class SgdSeg(C.Structure):
     _fields_ = [("p", C.c_void_p), ("g", C.c_void_p), ("corr", C.c_void_p), ("n", C.c_long), ("l2", C.c_float)]
 

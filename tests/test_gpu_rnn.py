@@ -7,6 +7,8 @@ Tolerances: single-frame kernels rtol 1e-5; after whole utterances (hundreds of 
 per-frame SGD updates, each amplifying fp32 rounding differences) parameters rtol 2e-3 /
 atol 2e-5 and summed cross-entropy rtol 1e-4.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -86,9 +88,136 @@ def test_rnn_trainer_matches_oracle(bptt, mmt, wc):
     err, frames, correct = obj.stats()
     assert frames == m.frames == tr.frames
     np.testing.assert_allclose(err, m.xent, rtol=1e-4)
+    assert abs(correct - m.correct) <= 1  # argmax near-ties may flip on fp32 rounding
     Wr, br = net.recurrent_params(0)
     np.testing.assert_allclose(Wr, m.Wr, rtol=2e-3, atol=2e-5)
     np.testing.assert_allclose(br, m.br, rtol=2e-3, atol=2e-5)
     W2, b2 = net.linear_params()[0]
     np.testing.assert_allclose(W2, m.W2, rtol=2e-3, atol=2e-5)
     np.testing.assert_allclose(b2, m.b2, rtol=2e-3, atol=2e-5)
+
+
+def _train_rnn(layers, feats, labels, bptt, lr, mmt, wc, generic, crossval=False):
+    os.environ["TNET_RNN_GENERIC"] = "1" if generic else "0"
+    try:
+        net = Network.from_layers(layers)
+        net.set_learn_rate(lr)
+        net.set_momentum(mmt)
+        net.set_weightcost(wc)
+        obj = Objective()
+        RnnTrainer(net, obj, bptt=bptt, crossval=crossval).train_corpus(feats, labels)
+        return obj.stats(), net.recurrent_params(0), net.linear_params()[0]
+    finally:
+        os.environ.pop("TNET_RNN_GENERIC", None)
+
+
+@pytest.mark.parametrize("S,bptt,mmt,wc", [(10, 4, 0.0, 0.0), (135, 2, 0.5, 1e-4), (4000, 4, 0.9, 0.0),
+                                           (37, 0, 0.0, 1e-3)])
+def test_rnn_fused_frame_matches_component_chain(S, bptt, mmt, wc):
+    """the fused single-frame chain (8 launches) vs the component-by-component chain (Propagate,
+    EvaluateLabels, Backpropagate + Update per layer) on the same utterances"""
+    nIn, H, lr = 40, 64, 0.02
+    rng = np.random.default_rng(S)
+    layers = formats.gen_recurrent_init(nIn, H, S, seed=11)
+    feats = [rng.standard_normal((T, nIn)).astype(np.float32) for T in (50, 33)]
+    labels = [rng.integers(0, S, len(f)).astype(np.int32) for f in feats]
+    labels[1][::9] = -1  # unlabeled frames: zero target
+    a = _train_rnn(layers, feats, labels, bptt, lr, mmt, wc, generic=False)
+    b = _train_rnn(layers, feats, labels, bptt, lr, mmt, wc, generic=True)
+    (ea, fa, ca), (eb, fb, cb) = a[0], b[0]
+    assert fa == fb == 83
+    np.testing.assert_allclose(ea, eb, rtol=1e-5)
+    assert abs(ca - cb) <= 1
+    for x, y in zip(a[1] + a[2], b[1] + b[2]):
+        np.testing.assert_allclose(x, y, rtol=1e-4, atol=1e-6)
+
+
+def test_rnn_fused_crossval_leaves_weights():
+    nIn, H, S = 24, 32, 10
+    rng = np.random.default_rng(5)
+    layers = formats.gen_recurrent_init(nIn, H, S, seed=3)
+    feats = [rng.standard_normal((40, nIn)).astype(np.float32)]
+    labels = [rng.integers(0, S, 40).astype(np.int32)]
+    (e, f, c), (Wr, br), (W2, b2) = _train_rnn(layers, feats, labels, 4, 0.05, 0.0, 0.0, False, crossval=True)
+    (e2, f2, c2), _, _ = _train_rnn(layers, feats, labels, 4, 0.05, 0.0, 0.0, True, crossval=True)
+    assert f == f2 == 40 and c == c2
+    np.testing.assert_allclose(e, e2, rtol=1e-5)
+    np.testing.assert_array_equal(Wr, layers[0].W)
+    np.testing.assert_array_equal(W2, layers[1].W)
+
+
+@pytest.mark.parametrize("K0,K1,N", [(440, 512, 512), (7, 0, 5), (0, 33, 70)])
+def test_gemv_rowvec_cat_pushes_history_row(K0, K1, N):
+    rng = np.random.default_rng(K0 + K1)
+    v0, v1 = rng.standard_normal(max(K0, 1)).astype(np.float32), rng.standard_normal(max(K1, 1)).astype(np.float32)
+    W = (0.05 * rng.standard_normal((K0 + K1, N))).astype(np.float32)
+    b = rng.standard_normal(N).astype(np.float32)
+    d0, d1 = DeviceArray.vector(v0), DeviceArray.vector(v1)
+    dW, db, y, hist = DeviceArray.from_numpy(W), DeviceArray.vector(b), DeviceArray(1, N), DeviceArray(1, K0 + K1)
+    ws = DeviceArray(1, max(1, lib().tnet_gemv_workspace(K0 + K1, N) // 4))
+    check(lib().tnet_gemv_rowvec_cat(d0.ptr, K0, d1.ptr, K1, hist.ptr, dW.ptr, dW.stride, db.ptr, y.ptr, N, 1,
+                                     ws.ptr, S()))
+    row = np.concatenate([v0[:K0], v1[:K1]])
+    np.testing.assert_array_equal(hist.numpy().ravel(), row)
+    a = b + row.astype(np.float64) @ W
+    np.testing.assert_allclose(y.numpy().ravel(), 1 / (1 + np.exp(-a)), rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("K,N,t", [(512, 135, 7), (512, 4000, 3999), (64, 1, 0), (100, 300, -1)])
+def test_gemv_rowvec_softmax_xent(K, N, t):
+    rng = np.random.default_rng(N)
+    v = rng.standard_normal(K).astype(np.float32)
+    W = (0.1 * rng.standard_normal((K, N))).astype(np.float32)
+    b = rng.standard_normal(N).astype(np.float32)
+    dv, dW, db = DeviceArray.vector(v), DeviceArray.from_numpy(W), DeviceArray.vector(b)
+    z, y, e = DeviceArray(1, N), DeviceArray(1, N), DeviceArray(1, N)
+    lab = DeviceArray.vector(np.array([t], np.int32))
+    stats = DeviceArray(1, 1024, np.float64, stride=1024)
+    ws = DeviceArray(1, max(1, lib().tnet_gemv_workspace(K, N) // 4))
+    check(lib().tnet_gemv_rowvec_softmax_xent(dv.ptr, K, dW.ptr, dW.stride, db.ptr, z.ptr, y.ptr, e.ptr, N, lab.ptr,
+                                              stats.ptr, ws.ptr, S()))
+    zr = b + v.astype(np.float64) @ W
+    np.testing.assert_allclose(z.numpy().ravel(), zr, rtol=1e-5, atol=1e-5)
+    Yr = orc.softmax(zr.reshape(1, -1).astype(np.float32))
+    Er, xent, correct = orc.xent_eval(Yr, np.array([t], np.int32))
+    np.testing.assert_allclose(y.numpy(), Yr, rtol=2e-5, atol=1e-9)
+    np.testing.assert_allclose(e.numpy(), Er, rtol=2e-5, atol=1e-8)
+    s = stats.numpy()[0]
+    np.testing.assert_allclose(s[0::2].sum(), xent, rtol=1e-5, atol=1e-6)
+    assert int(round(s[1::2].sum())) == correct
+    ok = DeviceArray(1, 4097)
+    assert lib().tnet_gemv_rowvec_softmax_xent(dv.ptr, K, ok.ptr, 4097, None, None, None, None, 4097, lab.ptr,
+                                               None, ws.ptr, S()) == -4  # TNET_ERR_UNSUPPORTED: N > 4096
+
+
+@pytest.mark.parametrize("mmt", [0.0, 0.9])
+@pytest.mark.parametrize("n_in,n_out", [(512, 135), (512, 4000), (13, 7)])
+def test_affine_bwd_update_row(mmt, n_in, n_out):
+    """e_out = W e with the weights before the update, the update of tnet_affine_update_row, and the
+    diff-sigmoid d = e_out s (1 - s)"""
+    rng = np.random.default_rng(n_out)
+    x, s = rng.random(n_in).astype(np.float32), rng.random(n_in).astype(np.float32)
+    e = (0.1 * rng.standard_normal(n_out)).astype(np.float32)
+    W, corr = (0.1 * rng.standard_normal((n_in, n_out))).astype(np.float32), rng.standard_normal((n_in, n_out)).astype(np.float32)
+    b, cb = rng.standard_normal(n_out).astype(np.float32), rng.standard_normal(n_out).astype(np.float32)
+    dx, ds, de, dW, db = (DeviceArray.vector(x), DeviceArray.vector(s), DeviceArray.vector(e),
+                          DeviceArray.from_numpy(W), DeviceArray.vector(b))
+    dC, dCb = DeviceArray.from_numpy(corr), DeviceArray.vector(cb)
+    eo, d = DeviceArray(1, n_in), DeviceArray(1, n_in)
+    scale, l2 = -0.02, -1e-4
+    check(lib().tnet_affine_bwd_update_row(dx.ptr, n_in, de.ptr, n_out, dW.ptr, dW.stride, dC.ptr, dC.stride, db.ptr,
+                                           dCb.ptr, scale, mmt, l2, eo.ptr, ds.ptr, d.ptr, S()))
+    er = W.astype(np.float64) @ e
+    np.testing.assert_allclose(eo.numpy().ravel(), er, rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(d.numpy().ravel(), er * s * (1 - s), rtol=1e-5, atol=1e-6)
+    c = np.outer(x, e).astype(np.float64) + (mmt * corr if mmt else 0)
+    w = W + scale * c
+    w = w + l2 * w
+    np.testing.assert_allclose(dW.numpy(), w, rtol=1e-6, atol=1e-7)
+    gb = e + mmt * cb if mmt else e.astype(np.float64)
+    np.testing.assert_allclose(db.numpy().ravel(), b + scale * gb, rtol=1e-6, atol=1e-7)
+    if mmt:
+        np.testing.assert_allclose(dC.numpy(), c, rtol=1e-6, atol=1e-7)
+        np.testing.assert_allclose(dCb.numpy().ravel(), gb, rtol=1e-6, atol=1e-7)
+    else:  # momentum 0: the correction buffers are not touched
+        np.testing.assert_array_equal(dC.numpy(), corr)
