@@ -87,6 +87,17 @@ void CuCache::Alloc(size_t cols, size_t tcols) {
       mPermEvSet[k] = false;
     }
   }
+  // a shape change re-Inits buffers that gathers (compute stream) or intake copies (copy stream)
+  // of the previous fill may still use; the blocks go back to CuDevice's pool, which assumes all
+  // work on them is ordered on the compute stream -- drain both streams first
+  const bool resize = (mFeatures.Rows() > 0 && (mFeatures.Rows() != mCachesize || mFeatures.Cols() != cols)) ||
+                      (mMode == DENSE && mDesired.Rows() > 0 &&
+                       (mDesired.Rows() != mCachesize || mDesired.Cols() != tcols)) ||
+                      (mMode != DENSE && mLabels.Dim() > 0 && mLabels.Dim() != mCachesize);
+  if (resize) {
+    TNET_HIP_CALL(hipStreamSynchronize(mCopy));
+    TNET_HIP_CALL(hipStreamSynchronize(CuDevice::Instantiate().Stream()));
+  }
   bool fresh = false;
   auto mat = [&](CuMatrix<BaseFloat>& m, size_t c) {
     if (m.Rows() != mCachesize || m.Cols() != c) {

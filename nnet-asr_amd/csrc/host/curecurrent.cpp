@@ -110,6 +110,7 @@ void CuRecurrentTrainer::TrainUtterance(const float* feats, size_t rows, size_t 
                                         const int* labels) {
   if (cols != mNet->GetNInputs()) Error("CuRecurrentTrainer: feature dim != network input dim");
   if (rows == 0) return;
+  CheckLabels(labels, rows, mNet->GetNOutputs(), "CuRecurrentTrainer::TrainUtterance");
   mFeats.Init(rows, cols);
   mFeats.CopyFromHost(feats, rows, cols, ld);
   mLabels.Init(rows);

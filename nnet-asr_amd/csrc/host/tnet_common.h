@@ -62,3 +62,20 @@ inline void Warning(const std::string& msg);
 #include <iostream>
 inline void TNet::Warning(const std::string& msg) { std::cerr << "WARNING " << msg << std::endl; }
 #endif
+
+namespace TNet {
+// Class-id targets at intake: each label names an output column, or is < 0 (an unlabeled row, the
+// all-zero target row of the reference's one-hot matrix).  The reference cannot hold an
+// out-of-range id (LabelRepository::GenDesiredMatrix builds [T x n_out] one-hot rows,
+// src/KaldiLib/Labels.cc:44-187); here a label >= n_out would index past the softmax row.
+inline void CheckLabels(const int* labels, size_t rows, size_t n_out, const char* who) {
+  if (rows && !labels) Error(std::string(who) + ": labels pointer is null");
+  for (size_t r = 0; r < rows; r++) {
+    if (labels[r] >= 0 && (size_t)labels[r] >= n_out) {
+      std::ostringstream os;
+      os << who << ": label " << labels[r] << " of frame " << r << " is outside [0, " << n_out << ")";
+      Error(os.str());
+    }
+  }
+}
+}  // namespace TNet

@@ -70,6 +70,7 @@ void CuTrainer::SetTransform(CuNetwork* transform, size_t start_ext, size_t end_
 }
 
 void CuTrainer::AddUtterance(const float* feats, size_t rows, size_t cols, size_t ld, const int* labels) {
+  CheckLabels(labels, rows, mNet->GetNOutputs(), "CuTrainer::AddUtterance");
   if (mTransform && rows > 0) {
     // frame extension on the host (the reader's job in the reference), one upload, the transform
     // network on the device, trim, then the cache takes the device rows
@@ -120,6 +121,7 @@ size_t CuTrainer::Prefill(const float* feats, size_t rows, size_t cols, size_t l
   if (mCache.Full()) return 0;
   const size_t space = mOpt.cachesize - mCache.IntakePos();
   const size_t take = rows < space ? rows : space;
+  CheckLabels(labels, take, mNet->GetNOutputs(), "CuTrainer::Prefill");
   mCache.AddDataHost(feats, take, cols, ld, labels);
   if (mCache.Full() && mOpt.randomize) mCache.Randomize();
   return take;

@@ -115,7 +115,7 @@ __global__ __launch_bounds__(256) void gemv_softmax_xent_final(const float* __re
   if (lane == 0) ssum[wv] = ws;
   __syncthreads();
   const float rsum = 1.f / (float)(ssum[0] + ssum[1] + ssum[2] + ssum[3]);
-  const int t = label[0];
+  const int t = label[0] < N ? label[0] : -1;  // out of range: an unlabeled frame, as the batched kernels
   ArgMax ay{-1e20f, 0x7fffffff};
 #pragma unroll
   for (int q = 0; q < GV_SMX_PER; ++q) {

@@ -208,7 +208,9 @@ __global__ __launch_bounds__(256) void softmax_xent_kernel(const float* __restri
   // ---- pass 3: y, error, argmax, xent
   ArgMax ay{-1e20f, 0x7fffffff}, ad{-1e20f, 0x7fffffff};
   double xent = 0.0;
-  const int t = (KIND == 0) ? labels[row] : -1;
+  // a class id outside [0, N) is treated as an unlabeled row (the host intake rejects one, CheckLabels)
+  int t = (KIND == 0) ? labels[row] : -1;
+  if (t >= N) t = -1;
   float* yrow = Y ? Y + (long)row * strideY : nullptr;
   float* erow = E ? E + (long)row * strideE : nullptr;
   const float* drow = (KIND == 1) ? D + (long)row * strideD : nullptr;
@@ -397,7 +399,8 @@ __global__ __launch_bounds__(256) void softmax_xent_row4_kernel(const float* __r
   __syncthreads();
   const float sum = (float)(ssum[0] + ssum[1] + ssum[2] + ssum[3]);
   const float rsum = 1.f / sum;
-  const int t = labels[row];
+  int t = labels[row];
+  if (t >= N) t = -1;  // out of range: an unlabeled row (the host intake rejects one, CheckLabels)
   float* yrow = Y ? Y + (long)row * strideY : nullptr;
   float* erow = E ? E + (long)row * strideE : nullptr;
   ArgMax ay{-1e20f, 0x7fffffff};

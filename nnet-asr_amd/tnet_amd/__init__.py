@@ -38,6 +38,21 @@ def synchronize() -> None:
     check(lib().tnet_synchronize(), "synchronize")
 
 
+def _utterance(feats, labels=None, who: str = "utterance"):
+    """Host-side shape check of one utterance before its pointers reach the C ABI: the library
+    copies feats.shape[0] rows and as many labels, so a short labels array would be read past."""
+    feats = np.ascontiguousarray(feats, np.float32)
+    if feats.ndim != 2:
+        raise ValueError(f"{who}: feats must be 2-D [frames x dim], got shape {feats.shape}")
+    if labels is None:
+        return feats, None
+    labels = np.ascontiguousarray(labels, np.int32)
+    if labels.ndim != 1 or labels.shape[0] != feats.shape[0]:
+        raise ValueError(f"{who}: labels must be 1-D with one class id per frame "
+                         f"({feats.shape[0]} frames), got shape {labels.shape}")
+    return feats, labels
+
+
 class DeviceArray:
     """Row-major device matrix (rows x cols) with a padded stride (multiple of 64 elements)."""
 
@@ -283,8 +298,7 @@ class Trainer:
                                                      int(crossval)), "tnet_trainer_create")
 
     def add_utterance(self, feats: np.ndarray, labels: np.ndarray) -> None:
-        feats = np.ascontiguousarray(feats, np.float32)
-        labels = np.ascontiguousarray(labels, np.int32)
+        feats, labels = _utterance(feats, labels, "Trainer.add_utterance")
         check(lib().tnet_trainer_add_utterance(self.h, feats.ctypes.data, feats.shape[0], feats.shape[1],
                                                feats.shape[1], labels.ctypes.data), "add_utterance")
 
@@ -336,7 +350,7 @@ class RbmTrainer:
                                                          learn_rate, momentum, weightcost), "tnet_rbm_trainer_create")
 
     def add_utterance(self, feats: np.ndarray) -> None:
-        feats = np.ascontiguousarray(feats, np.float32)
+        feats, _ = _utterance(feats, None, "RbmTrainer.add_utterance")
         check(lib().tnet_rbm_trainer_add_utterance(self.h, feats.ctypes.data, feats.shape[0], feats.shape[1],
                                                    feats.shape[1]), "rbm add_utterance")
 
@@ -365,7 +379,7 @@ class RbmTrainer:
         return buf.value.decode()
 
     def prefill(self, feats: np.ndarray) -> int:
-        feats = np.ascontiguousarray(feats, np.float32)
+        feats, _ = _utterance(feats, None, "RbmTrainer.prefill")
         n = lib().tnet_rbm_trainer_prefill(self.h, feats.ctypes.data, feats.shape[0], feats.shape[1], feats.shape[1])
         if n < 0:
             check(-1, "rbm prefill")
@@ -391,8 +405,7 @@ class RnnTrainer:
         self.h = check_ptr(lib().tnet_rnn_trainer_create(net.h, obj.h, bptt, int(crossval)), "tnet_rnn_trainer_create")
 
     def train_utterance(self, feats: np.ndarray, labels: np.ndarray) -> None:
-        feats = np.ascontiguousarray(feats, np.float32)
-        labels = np.ascontiguousarray(labels, np.int32)
+        feats, labels = _utterance(feats, labels, "RnnTrainer.train_utterance")
         check(lib().tnet_rnn_trainer_utterance(self.h, feats.ctypes.data, feats.shape[0], feats.shape[1],
                                                feats.shape[1], labels.ctypes.data), "rnn utterance")
 

@@ -42,3 +42,21 @@ def test_version_and_status_strings_without_gpu():
     L = _lib.lib()
     assert b"gfx950" in L.tnet_version()
     assert L.tnet_status_str(-1) == b"invalid argument"
+
+
+def test_utterance_shape_checks_before_the_abi():
+    """The binding rejects mis-shaped utterances before their pointers reach the C ABI, which copies
+    feats.shape[0] rows and as many labels (a short labels array would be read past its end)."""
+    import numpy as np
+
+    from tnet_amd import _utterance
+    f, l = _utterance(np.zeros((5, 3)), np.arange(5))
+    assert f.dtype == np.float32 and l.dtype == np.int32 and f.flags.c_contiguous
+    with pytest.raises(ValueError):
+        _utterance(np.zeros((5, 3)), np.arange(4))
+    with pytest.raises(ValueError):
+        _utterance(np.zeros(15), np.arange(15))
+    with pytest.raises(ValueError):
+        _utterance(np.zeros((5, 3)), np.zeros((5, 1)))
+    f, l = _utterance(np.zeros((2, 3)), None)
+    assert l is None

@@ -294,6 +294,28 @@ def test_softmax_xent_labels(rows, cols):
     assert int(round(s[1::2].sum())) == correct
 
 
+@pytest.mark.parametrize("rows,cols", [(64, 135), (64, 4000)])
+def test_softmax_xent_label_out_of_range_is_unlabeled(rows, cols):
+    """a class id >= N never indexes past the row: the kernels (both the one-wave-per-row and the
+    four-waves-per-row form) treat it as an unlabeled row, like -1 (the host intake rejects it)"""
+    Z = rnd((rows, cols), 21, 3.0)
+    lab = np.random.default_rng(22).integers(0, cols, size=rows).astype(np.int32)
+    bad = lab.copy()
+    bad[::3] = cols
+    bad[1::5] = cols + 1000
+    ref = lab.copy()
+    ref[bad >= cols] = -1
+    out = []
+    for L in (bad, ref):
+        dZ, dL = DeviceArray.from_numpy(Z), DeviceArray.vector(L)
+        dE = DeviceArray(rows, cols)
+        stats = DeviceArray(1, 1024, np.float64, stride=1024)
+        check(lib().tnet_softmax_xent(dZ.ptr, dZ.dim, dL.ptr, None, 0, dE.ptr, dE.stride, stats.ptr, S()))
+        out.append((dE.numpy(), stats.numpy()[0]))
+    np.testing.assert_array_equal(out[0][0], out[1][0])
+    np.testing.assert_array_equal(out[0][1], out[1][1])
+
+
 def test_softmax_xent_extreme_logits():
     """underflowing probabilities hit the FLT_MIN clamp of _log_elem (cukernels.cu:131-141)"""
     rows, cols = 8, 300

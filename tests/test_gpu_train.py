@@ -161,3 +161,29 @@ def test_cache_leftover_filling_cache_raises():
     with pytest.raises(TnetError):
         for n in lens:
             tr.add_utterance(rng.standard_normal((n, 8)).astype(np.float32), np.zeros(n, np.int32))
+
+
+def test_out_of_range_label_rejected_at_intake():
+    """a class id >= the number of network outputs is an error at intake (the reference's one-hot
+    target matrix cannot hold one); negative ids stay allowed (all-zero target rows)"""
+    from tnet_amd import RnnTrainer, TnetError
+    layers = formats.gen_mlp_init([8, 16, 4], seed=1)
+    net = Network.from_layers(layers)
+    tr = Trainer(net, Objective(), bunchsize=16, cachesize=64, seed=1)
+    rng = np.random.default_rng(0)
+    X = rng.standard_normal((20, 8)).astype(np.float32)
+    ok = rng.integers(0, 4, 20).astype(np.int32)
+    ok[3] = -1
+    tr.add_utterance(X, ok)
+    bad = ok.copy()
+    bad[7] = 4
+    with pytest.raises(TnetError, match="outside"):
+        tr.add_utterance(X, bad)
+    with pytest.raises(ValueError):
+        tr.add_utterance(X, ok[:10])
+    rnn = Network.from_layers(formats.gen_recurrent_init(8, 16, 4, seed=3))
+    rnn.set_learn_rate(0.1)
+    rt = RnnTrainer(rnn, Objective(), bptt=2)
+    with pytest.raises(TnetError, match="outside"):
+        rt.train_utterance(X, bad)
+
