@@ -129,13 +129,16 @@ int tnet_gather_bunch(float* y, const float* x, int* labels_out, const int* labe
 /* ------------------------------------------------------------------------------------
  * GEMM (replaces cublasSgemm at cumatrix.tcc:336-370, row-major semantics)
  *   C[m x n] = alpha * op(A) * op(B) + beta * C,  op(X) = X or X^T ('N' / 'T')
- * fp32 in / fp32 accumulate on v_mfma_f32_32x32x2_f32 (exact f32 FMA chain per k).
+ * fp32 in / fp32 accumulate on the f32 MFMA (v_mfma_f32_16x16x4_f32; exact f32 FMA chain per k).
+ * Shapes with few output tiles and a long K (fewer than ~100 tiles, K >= 1024) are split over K:
+ * the slices' partial products are added in slice order (deterministic) before the epilogue.
  * Requirements: lda/ldb/ldc multiples of 4 elements, pointers 16-byte aligned.
  * ---------------------------------------------------------------------------------- */
 int tnet_sgemm(char transa, char transb, int m, int n, int k, float alpha, const float* A, int lda,
                const float* B, int ldb, float beta, float* C, int ldc, void* stream);
 /* Tuning knob: force one GEMM tile configuration for every later launch in this process
- * ("auto" = per-shape heuristic; names as in gemm_f32.hip, e.g. "g128x64s4").  Not thread-safe. */
+ * ("auto" = per-shape heuristic; names as in gemm_f32.hip, e.g. "m64x128k64s2"), optionally with a
+ * forced split-K count ("m64x64k32s4w41+sk8").  Not thread-safe. */
 int tnet_gemm_config(const char* name);
 
 /* ------------------------------------------------------------------------------------
@@ -226,6 +229,15 @@ int tnet_rbm_update(const float* V, TnetMatrixDim dV, const float* H, TnetMatrix
  *   corr_b = mmt*corr_b + scale*(sum_{r<neg_from} M[r] - sum_{r>=neg_from} M[r]) ; b += corr_b. */
 int tnet_rbm_bias_update(const float* M, TnetMatrixDim d, int neg_from, float* b, float* corr_b, float scale,
                          float mmt, void* workspace, void* stream);
+/* The CD-1 bias updates and reconstruction error of one RBM step in one launch (replaces the
+ * AddColSum / AddScaled pairs of cuRbm.cc:148-164 and CuMeanSquareError::Evaluate of TRbmCu.cc:350):
+ * Vs = [pos_vis; neg_vis] (2B x V), Hs = [pos_hid; -neg_hid] (2B x H, negative phase stored negated);
+ *   c_v = mmt*c_v + scale*(sum pos_vis - sum neg_vis) ; vb += c_v
+ *   c_h = mmt*c_h + scale*(sum of all rows of Hs)      ; hb += c_h
+ *   mse_stats (nullable, stats layout as tnet_mse) += sum (neg_vis - pos_vis)^2.
+ * Column sums bit-identical to tnet_rbm_bias_update; no workspace.  TNET_ERR_UNSUPPORTED for B > 4096. */
+int tnet_rbm_stats_update(const float* Vs, TnetMatrixDim dV, const float* Hs, TnetMatrixDim dH, int B, float* vb,
+                          float* cvb, float* hb, float* chb, float scale, float mmt, double* mse_stats, void* stream);
 
 /* ---- single-frame kernels (TRecurrentCu: CuMath::OffsetGemv / BlasGer, cumath.cc:292-362) ---- */
 /* single-frame forward of the recurrent layer: y = act(b + [v0, v1] W) for the row [v0 (K0), v1 (K1)]

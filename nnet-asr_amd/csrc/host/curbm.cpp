@@ -226,14 +226,24 @@ void CuRbmTrainer::Step() {
                                  rbm.VisHid().Dim(), rbm.VisHidCorrection().pCUData(),
                                  (int)rbm.VisHidCorrection().Stride(), scale, rbm.Momentum(), -lr * rbm.Weightcost(),
                                  S));
-  void* ws = CuDevice::Instantiate().Workspace(
-      (size_t)std::max(tnet_col_sum_workspace(mV.Dim()), tnet_col_sum_workspace(mH.Dim())));
-  TNET_SAFE_CALL(tnet_rbm_bias_update(mV.pCUData(), mV.Dim(), (int)B, rbm.VisBias().pCUData(),
-                                      rbm.VisBiasCorrection().pCUData(), scale, rbm.Momentum(), ws, S));
-  TNET_SAFE_CALL(tnet_rbm_bias_update(mH.pCUData(), mH.Dim(), (int)(2 * B), rbm.HidBias().pCUData(),
-                                      rbm.HidBiasCorrection().pCUData(), scale, rbm.Momentum(), ws, S));
-  // reconstruction error (mse.Evaluate(neg_vis, pos_vis), TRbmCu.cc:350)
-  mMse.EvaluateStats(mNegVis, mPosVis);
+  // both bias updates and the reconstruction error (mse.Evaluate(neg_vis, pos_vis), TRbmCu.cc:350) in
+  // one launch over the stacked statistics
+  const int st = tnet_rbm_stats_update(mV.pCUData(), mV.Dim(), mH.pCUData(), mH.Dim(), (int)B,
+                                       rbm.VisBias().pCUData(), rbm.VisBiasCorrection().pCUData(),
+                                       rbm.HidBias().pCUData(), rbm.HidBiasCorrection().pCUData(), scale,
+                                       rbm.Momentum(), mMse.DeviceStats(), S);
+  if (st == TNET_ERR_UNSUPPORTED) {  // bunches above 4096 frames: the two column sums + the MSE kernel
+    void* ws = CuDevice::Instantiate().Workspace(
+        (size_t)std::max(tnet_col_sum_workspace(mV.Dim()), tnet_col_sum_workspace(mH.Dim())));
+    TNET_SAFE_CALL(tnet_rbm_bias_update(mV.pCUData(), mV.Dim(), (int)B, rbm.VisBias().pCUData(),
+                                        rbm.VisBiasCorrection().pCUData(), scale, rbm.Momentum(), ws, S));
+    TNET_SAFE_CALL(tnet_rbm_bias_update(mH.pCUData(), mH.Dim(), (int)(2 * B), rbm.HidBias().pCUData(),
+                                        rbm.HidBiasCorrection().pCUData(), scale, rbm.Momentum(), ws, S));
+    mMse.EvaluateStats(mNegVis, mPosVis);
+  } else {
+    TNET_SAFE_CALL(st);
+    mMse.AddFrames(B);
+  }
   if (mOpt.trace & 2) std::cout << "." << std::flush;
   mSteps++;
 }

@@ -25,6 +25,8 @@
 //  * the whole epilogue (bias, sigmoid, diff-sigmoid, momentum-SGD) is fused into the stores.
 #include <cstdlib>
 #include <cstring>
+#include <map>
+#include <mutex>
 
 #include "kcommon.h"
 
@@ -65,6 +67,10 @@ struct GemmP {
   float bscale, bmmt;           // EPI_SGD_B
   int group;                    // tile-rows per group of the blockIdx -> tile order
   int diag_noload;              // diagnostics only: skip the k-loop's global loads (wrong results)
+  // split-K (gemm16_kernel, blockIdx.y = split z): the split reads A + z*kstepA, B + z*kstepB over
+  // K = its own depth and stores its partial product to C + z*slabC (EPI_STORE, alpha 1, beta 0)
+  int ksplit;
+  long kstepA, kstepB, slabC;
 };
 
 
@@ -511,7 +517,14 @@ __device__ __forceinline__ void lds_vec(const float* p, float (&x)[4]) {
 template <int BM, int BN, int BK, int WM, int WN, int S, int SP, bool A_KC, bool B_KC, int EPI>
 __global__ __launch_bounds__((WM * WN + (SP == 2)) * 64)
 __attribute__((amdgpu_waves_per_eu((WM * WN + (SP == 2) + 3) / 4, (WM * WN + (SP == 2) + 3) / 4)))
-void gemm16_kernel(const GemmP p) {
+void gemm16_kernel(const GemmP p_in) {
+  GemmP p = p_in;
+  if (p.ksplit > 1) {
+    const long z = blockIdx.y;
+    p.A += z * p.kstepA;
+    p.B += z * p.kstepB;
+    p.C += z * p.slabC;
+  }
   constexpr int NT = WM * WN * 64, NW = WM * WN;
   constexpr bool LDR = SP == 2;
   static_assert(SP != 1 || S >= 3, "spread DMA needs a 3-slot ring");
@@ -1249,6 +1262,86 @@ void gemm16_kernel(const GemmP p) {
 }
 
 // ---------------------------------------------------------------------------------------------
+// split-K combine: C = epilogue(P[0] + P[1] + ... + P[splits-1]) summed in split order (fixed, so the
+// result is deterministic), then the same epilogue arithmetic as gemm16_kernel; 4 columns / thread
+// ---------------------------------------------------------------------------------------------
+constexpr bool epi_splittable(int e) { return e != EPI_DSIG_CS && !epi_bias_slabs(e); }
+constexpr int kMaxSplit = 8;
+
+template <int EPI>
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(const GemmP p, const float* __restrict__ P, long slab,
+                                                            int splits, int ldp) {
+  const int N4 = (p.N + 3) >> 2;
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long)p.M * N4) return;
+  const int row = (int)(i / N4), col = (int)(i % N4) * 4;
+  const float* q = P + (long)row * ldp + col;
+  // every slice's load in flight before the first add (splits <= kMaxSplit)
+  f32x4 t[kMaxSplit];
+#pragma unroll
+  for (int z = 0; z < kMaxSplit; ++z)
+    if (z < splits) t[z] = *reinterpret_cast<const f32x4*>(q + z * slab);
+  f32x4 v = t[0];
+#pragma unroll
+  for (int z = 1; z < kMaxSplit; ++z)
+    if (z < splits)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = v[e] + t[z][e];
+  float* cp = p.C + (long)row * p.ldc + col;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    if (col + e >= p.N) break;
+    const float x = v[e];
+    if constexpr (EPI == EPI_STORE) {
+      cp[e] = (p.beta == 0.f) ? p.alpha * x : p.alpha * x + p.beta * cp[e];
+    } else if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_SIG || EPI == EPI_BIAS_NSIG || EPI == EPI_BIAS_NEG) {
+      const float y = x + p.bias[col + e];
+      cp[e] = EPI == EPI_BIAS ? y : EPI == EPI_BIAS_SIG ? sigmoidf_ref(y) : EPI == EPI_BIAS_NSIG ? -sigmoidf_ref(y) : -y;
+    } else if constexpr (EPI == EPI_DSIG) {
+      const float y = p.aux[(long)row * p.ldaux + col + e];
+      cp[e] = y * (1.f - y) * x;
+    } else if constexpr (EPI == EPI_RBM) {
+      float* qp = p.corr + (long)row * p.ldcorr + col + e;
+      const float w = cp[e];
+      const float c = p.mmt * *qp + p.scale * x + p.l2 * w;
+      *qp = c;
+      cp[e] = w + c;
+    } else if constexpr (EPI == EPI_SGD) {
+      float c = x;
+      if (p.corr) {
+        float* qp = p.corr + (long)row * p.ldcorr + col + e;
+        c = x + p.mmt * *qp;
+        *qp = c;
+      }
+      float w = cp[e];
+      w = w + p.scale * c;
+      w = w + p.l2 * w;
+      cp[e] = w;
+    }
+  }
+}
+
+// per-stream partial-product workspace of the split-K path (grown on demand; the library enqueues
+// a stream's GEMMs in order, so one buffer per stream is reused launch after launch)
+static std::mutex g_skws_mu;
+static std::map<hipStream_t, std::pair<void*, size_t>> g_skws;
+static float* splitk_workspace(size_t bytes, hipStream_t st) {
+  std::lock_guard<std::mutex> lk(g_skws_mu);
+  auto& w = g_skws[st];
+  if (bytes > w.second) {
+    if (w.first) {
+      if (hipStreamSynchronize(st) != hipSuccess) return nullptr;
+      (void)hipFree(w.first);
+      w = {nullptr, 0};
+    }
+    void* q = nullptr;
+    if (hipMalloc(&q, bytes) != hipSuccess) return nullptr;
+    w = {q, bytes};
+  }
+  return (float*)w.first;
+}
+
+// ---------------------------------------------------------------------------------------------
 // host-side dispatch
 // ---------------------------------------------------------------------------------------------
 // name: g<BM>x<BN>k<BK>s<S>w<waves>[i]: 32x32x2 kernel (waves laid out WMxWN; i = DMA pieces
@@ -1284,6 +1377,7 @@ static const char* kCfgNames[CFG_COUNT] = {
 
 static int g_cfg = -2;  // -2: not initialised, -1: automatic
 static int g_group = -1;
+static int g_split = -1;  // TNET_GEMM_SPLITK: forced split-K count (diagnostics / sweeps), -1 automatic
 static int forced_cfg() {
   if (g_cfg == -2) {
     g_cfg = -1;
@@ -1293,6 +1387,8 @@ static int forced_cfg() {
         if (!strcmp(e, kCfgNames[i])) g_cfg = i;
     const char* gg = getenv("TNET_GEMM_GROUP");
     if (gg) g_group = atoi(gg);
+    const char* sk = getenv("TNET_GEMM_SPLITK");
+    if (sk) g_split = atoi(sk);
   }
   return g_cfg;
 }
@@ -1309,9 +1405,54 @@ static bool launch_cfg(const GemmP& p, hipStream_t st) {
     const long extA = A_KC ? (long)p.M * p.lda : (long)BK * p.lda + p.M;
     const long extB = B_KC ? (long)p.N * p.ldb : (long)BK * p.ldb + p.N;
     if (4 * extA >= (1L << 32) || 4 * extB >= (1L << 32)) return false;
-    gemm16_kernel<BM, BN, BK, WM, WN, S, IL, A_KC, B_KC, EPI><<<tiles, (WM * WN + (IL == 2)) * 64, 0, st>>>(p);
+    const dim3 grid(tiles, p.ksplit > 1 ? p.ksplit : 1);
+    gemm16_kernel<BM, BN, BK, WM, WN, S, IL, A_KC, B_KC, EPI><<<grid, (WM * WN + (IL == 2)) * 64, 0, st>>>(p);
     return true;
   }
+}
+
+static void cfg_shape(int cfg, int* bm, int* bn, int* kind) {
+  switch (cfg) {
+#define X(name, KIND, BM, BN, BK, WM, WN, S, IL) \
+  case CFG_##name: *bm = BM; *bn = BN; *kind = KIND; return;
+    TNET_GEMM_CFGS(X)
+#undef X
+    default: *bm = 64; *bn = 64; *kind = 0;
+  }
+}
+
+// split-K: the K range is cut into ks slices (blockIdx.y) whose partial products go to the stream's
+// workspace; splitk_reduce_kernel adds them in slice order and applies the epilogue
+template <bool A_KC, bool B_KC, int EPI>
+static int launch_splitk(const GemmP& p, int cfg, int ks, hipStream_t st) {
+  const int ldp = (p.N + 3) & ~3;
+  const long slab = (long)p.M * ldp;
+  float* ws = splitk_workspace(sizeof(float) * (size_t)slab * ks, st);
+  if (!ws) return TNET_ERR_RUNTIME;
+  GemmP q = p;
+  q.K = p.K / ks;
+  q.ksplit = ks;
+  q.kstepA = A_KC ? (long)q.K : (long)q.K * p.lda;
+  q.kstepB = B_KC ? (long)q.K : (long)q.K * p.ldb;
+  q.C = ws;
+  q.ldc = ldp;
+  q.slabC = slab;
+  q.alpha = 1.f;
+  q.beta = 0.f;
+  bool ok = false;
+  switch (cfg) {
+#define X(name, KIND, BM, BN, BK, WM, WN, S, IL) \
+  case CFG_##name: if (KIND == 1) ok = launch_cfg<KIND, BM, BN, BK, WM, WN, S, IL, A_KC, B_KC, EPI_STORE>(q, st); break;
+    TNET_GEMM_CFGS(X)
+#undef X
+    default: break;
+  }
+  if (!ok) return TNET_ERR_UNSUPPORTED;
+  TNET_LAUNCH_CHECK();
+  const long n = (long)p.M * ((p.N + 3) >> 2);
+  splitk_reduce_kernel<EPI><<<(unsigned)cdiv(n, 256), 256, 0, st>>>(p, ws, slab, ks, ldp);
+  TNET_LAUNCH_CHECK();
+  return TNET_OK;
 }
 
 // bwd GEMM + diff-sigmoid + column sums: one fixed 64x128 16x16 config (32-row wave tiles = slabs)
@@ -1340,14 +1481,40 @@ static int launch_gemm(const GemmP& p_in, hipStream_t st) {
     // still gives ~one workgroup per CU (256 CUs), the 16x16x4 kernel where the layout allows
     const long t128 = (long)cdiv(p.M, 128) * cdiv(p.N, 128), t64x128 = (long)cdiv(p.M, 64) * cdiv(p.N, 128);
     const long t128x256 = (long)cdiv(p.M, 128) * cdiv(p.N, 256);
+    // round 2 (tools/gemm_sweep.py): 16x64 wave tiles (w41) for 64x64 tiles in every layout (the
+    // 440-row update 24.4 -> 23.4 us), 32x64 tiles where 64x64 leaves most CUs idle (RBM phases,
+    // 256 x 2048 over K = 440: 11.8 -> 9.7 us); fewer tiles than that: split-K below
+    const long t64 = (long)cdiv(p.M, 64) * cdiv(p.N, 64), t32x64 = (long)cdiv(p.M, 32) * cdiv(p.N, 64);
     if (!A_KC && t128x256 >= 240) cfg = CFG_m128x256k32s3;  // one round where 128x128 needs two
     else if (t128 >= 240) cfg = CFG_m128x128k64s2;
     else if (A_KC && t64x128 >= 200) cfg = CFG_m64x128k64s2;  // incl. the K = 440 first layer (one round)
-    else if (A_KC && p.K < 1024) cfg = CFG_m64x64k32s4w41;
-    else if ((long)cdiv(p.M, 64) * cdiv(p.N, 64) >= 200) cfg = CFG_m64x64k32s4;  // e.g. the 440-row update
-    else cfg = CFG_g64x64k32s4w4;
+    else if (t64 >= 200) cfg = CFG_m64x64k32s4w41;
+    else if (t32x64 >= 128) cfg = CFG_m32x64k64s2;
+    else cfg = CFG_m64x64k32s4w41;
   }
   p.group = g_group > 0 ? g_group : 8;
+  if constexpr (epi_splittable(EPI)) {
+    // split-K where few output tiles meet a long K (the RBM reconstruction 256 x 440 over K = 2048:
+    // 28 tiles of 64x64 for 256 CUs)
+    int tbm, tbn, kind;
+    cfg_shape(cfg, &tbm, &tbn, &kind);
+    const long tiles = (long)cdiv(p.M, tbm) * cdiv(p.N, tbn);
+    int ks = 1;
+    if (g_split > 0) {
+      ks = g_split < kMaxSplit ? g_split : kMaxSplit;
+    } else if (tiles < 100 && p.K >= 1024) {
+      while (ks < kMaxSplit && tiles * ks * 2 <= 288) ks *= 2;
+      // 32x64 tiles need half the slices of 64x64 ones for the same workgroup count: less combine traffic
+      const long t32 = (long)cdiv(p.M, 32) * cdiv(p.N, 64);
+      if (cfg == CFG_m64x64k32s4w41 && ks >= 4 && t32 * (ks / 2) <= 288) {
+        cfg = CFG_m32x64k64s2;
+        kind = 1;
+        ks /= 2;
+      }
+    }
+    while (ks > 1 && (p.K % (4 * ks) != 0 || p.K / ks < 64)) ks /= 2;
+    if (ks > 1) return launch_splitk<A_KC, B_KC, EPI>(p, kind == 1 ? cfg : CFG_m64x64k32s4w41, ks, st);
+  }
   bool ok = false;
   switch (cfg) {
 #define X(name, KIND, BM, BN, BK, WM, WN, S, IL) \
@@ -1555,16 +1722,28 @@ extern "C" int tnet_affine_grad(const float* X, TnetMatrixDim dX, const float* E
 
 extern "C" int tnet_gemm_config(const char* name) {
   forced_cfg();  // read the environment once, before it could override this call
-  if (!name || !strcmp(name, "auto")) {
-    g_cfg = -1;
-    return TNET_OK;
-  }
-  for (int i = 0; i < CFG_COUNT; i++)
-    if (!strcmp(name, kCfgNames[i])) {
-      g_cfg = i;
-      return TNET_OK;
+  // "<cfg>[+sk<n>]": a tile configuration (or "auto") and optionally a forced split-K count
+  char base[64] = "auto";
+  int split = -1;
+  if (name) {
+    const char* plus = strchr(name, '+');
+    const size_t n = plus ? (size_t)(plus - name) : strlen(name);
+    if (n >= sizeof(base)) return TNET_ERR_ARG;
+    memcpy(base, name, n);
+    base[n] = 0;
+    if (plus) {
+      if (strncmp(plus, "+sk", 3) != 0 || atoi(plus + 3) < 1) return TNET_ERR_ARG;
+      split = atoi(plus + 3);
     }
-  return TNET_ERR_ARG;
+  }
+  int cfg = -2;
+  if (!strcmp(base, "auto")) cfg = -1;
+  for (int i = 0; i < CFG_COUNT; i++)
+    if (!strcmp(base, kCfgNames[i])) cfg = i;
+  if (cfg == -2) return TNET_ERR_ARG;
+  g_cfg = cfg;
+  g_split = split;
+  return TNET_OK;
 }
 
 #ifdef TNET_GEMM_STAMP

@@ -168,6 +168,7 @@ _SIGS = {
     "tnet_affine_fwd_t": (i32, [vp, MatrixDim, vp, MatrixDim, vp, vp, MatrixDim, i32, vp]),
     "tnet_rbm_update": (i32, [vp, MatrixDim, vp, MatrixDim, vp, MatrixDim, vp, i32, f32, f32, f32, vp]),
     "tnet_rbm_bias_update": (i32, [vp, MatrixDim, i32, vp, vp, f32, f32, vp, vp]),
+    "tnet_rbm_stats_update": (i32, [vp, MatrixDim, vp, MatrixDim, i32, vp, vp, vp, vp, f32, f32, vp, vp]),
     "tnetF_rand": (i32, [vp, MatrixDim, vp, vp, vp, vp, vp]),
     "tnetF_gauss_rand": (i32, [vp, MatrixDim, vp, vp, vp, vp, vp]),
     "tnetF_binarize_probs": (i32, [vp, vp, vp, MatrixDim, vp]),

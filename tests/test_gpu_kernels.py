@@ -34,7 +34,10 @@ def gemm_ref(ta, tb, A, B):
 
 GEMM_CFGS = ["auto", "g64x64k32s4w4", "m64x128k32s4", "m64x128k64s3", "m64x64k32s4w41", "m128x128k32s3",
              "m128x128k64s2", "m64x128k64s2", "m64x128k64s2w42", "m64x128k64s3p", "m64x128k64s2L", "m128x256k32s3",
-             "m64x64k64s2", "m64x64k32s4", "m32x64k64s2"]
+             "m64x64k64s2", "m64x64k32s4", "m32x64k64s2",
+             # split-K (K cut into slices + an in-order combine with the epilogue); counts that do not
+             # divide K fall back to fewer slices
+             "auto+sk4", "m64x64k32s4w41+sk8", "m32x64k64s2+sk2", "m64x128k64s2+sk3"]
 
 
 @pytest.fixture(params=GEMM_CFGS)

@@ -143,6 +143,39 @@ def test_rbm_update_generic_and_stacked(V, H, B):
         np.testing.assert_allclose(got, want, rtol=2e-4, atol=2e-6)
 
 
+@pytest.mark.parametrize("V,H,B", [(440, 2048, 256), (33, 70, 17), (64, 130, 600), (440, 200, 1024), (8, 40, 4096)])
+def test_rbm_stats_update_matches_two_colsums_and_mse(V, H, B):
+    """the one-launch bias updates + reconstruction MSE == two tnet_rbm_bias_update launches (bit
+    for bit: same slab sums, same fp64 combine) + tnet_mse (fp64 sums, rtol 1e-12)"""
+    rng = np.random.default_rng(V + B)
+    Vs = rng.standard_normal((2 * B, V)).astype(np.float32)
+    Hs = rng.random((2 * B, H)).astype(np.float32)
+    Hs[B:] *= -1
+    vb, hb = (rng.standard_normal(n).astype(np.float32) for n in (V, H))
+    cvb, chb = (0.01 * rng.standard_normal(n).astype(np.float32) for n in (V, H))
+    lr, mmt = 0.1, 0.5
+    dV, dH = DeviceArray.from_numpy(Vs), DeviceArray.from_numpy(Hs)
+    out = []
+    for fused in (True, False):
+        d = [DeviceArray.vector(a) for a in (vb, cvb, hb, chb)]
+        st = DeviceArray(1, 1024, np.float64, stride=1024)
+        if fused:
+            check(lib().tnet_rbm_stats_update(dV.ptr, dV.dim, dH.ptr, dH.dim, B, d[0].ptr, d[1].ptr, d[2].ptr, d[3].ptr,
+                                              lr / B, mmt, st.ptr, S()))
+        else:
+            check(lib().tnet_rbm_bias_update(dV.ptr, dV.dim, B, d[0].ptr, d[1].ptr, lr / B, mmt, None, S()))
+            check(lib().tnet_rbm_bias_update(dH.ptr, dH.dim, 2 * B, d[2].ptr, d[3].ptr, lr / B, mmt, None, S()))
+            neg = DeviceArray.from_numpy(Vs[B:])
+            pos = DeviceArray.from_numpy(Vs[:B])
+            check(lib().tnet_mse(neg.ptr, neg.dim, pos.ptr, pos.stride, None, 0, st.ptr, S()))
+        out.append(([a.numpy().reshape(-1) for a in d], st.numpy()[0][0::2].sum()))
+    for a, b in zip(out[0][0], out[1][0]):
+        np.testing.assert_array_equal(a, b)
+    np.testing.assert_allclose(out[0][1], out[1][1], rtol=1e-12)
+    e = (Vs[B:] - Vs[:B]).astype(np.float64)
+    np.testing.assert_allclose(out[0][1], (e * e).sum(), rtol=1e-6)
+
+
 def test_rbm_text_round_trip(tmp_path):
     layers = formats.gen_rbm_init(24, 40, seed=2, vis_type="gauss", hid_type="bern")
     net = Network.from_layers(layers)

@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""Sweep the GEMM tile configurations (TNET_GEMM_CFG) over the SGD-step shapes on the GPU.
+"""Sweep the GEMM tile configurations (TNET_GEMM_CFG; "auto" = the library's own choice; a "+sk<n>"
+suffix forces a split-K count, TNET_GEMM_SPLITK) over the SGD-step shapes on the GPU.
 
 Each configuration runs in its own process (the config is read once per process); every shape is
 timed with hipEvents on the library stream over `iters` back-to-back launches of the FUSED kernels
@@ -67,6 +68,8 @@ def main():
                 env["TNET_GEMM_DIAG"] = extra[4:]
             elif extra.startswith("g") and extra[1:].isdigit():
                 env["TNET_GEMM_GROUP"] = extra[1:]
+            elif extra.startswith("sk") and extra[2:].isdigit():
+                env["TNET_GEMM_SPLITK"] = extra[2:]
         p = subprocess.run([sys.executable, "-c", CHILD, REPO, json.dumps(shapes), str(iters)], env=env,
                            capture_output=True, text=True, timeout=300)
         line = [l for l in p.stdout.splitlines() if l.startswith("RESULT ")]
