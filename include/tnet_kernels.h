@@ -251,6 +251,33 @@ int tnet_gemv_rowvec_cat(const float* v0, int K0, const float* v1, int K1, float
  * N <= 4096 (else TNET_ERR_UNSUPPORTED); workspace: tnet_gemv_workspace(K, N) bytes. */
 int tnet_gemv_rowvec_softmax_xent(const float* v, int K, const float* W, int ldw, const float* b, float* z, float* y,
                                   float* e, int N, const int* label, double* stats, void* workspace, void* stream);
+/* ---- the TRecurrentCu frame chain in five launches + the BPTT (CuRecurrentTrainer's fused path) ----
+ * [<recurrent> nIn->H, <biasedlinearity> H->N, <softmax>] + cross-entropy, one frame
+ * (TRecurrentCu.cc:360-368 over cuRecurrent.cc:16-53 and cuBiasedLinearity.cc:11-64):
+ *   tnet_gemv_rowvec_partial : split-K partials of [v0, v1] W (ceil(K/64) x N floats; vout: the
+ *                              history row [v0, v1], NULL: not stored) -- CuRecurrent's forward,
+ *                              without the sigmoid finish
+ *   tnet_rnn_out_partial     : h = sigmoid(hb + sum of the hslices partials [hslices x H]) stored to h,
+ *                              and the split-K partials of h Wo (ceil(H/64) x N floats)
+ *   tnet_rnn_out_stats       : z = bo + sum of those partials (z may be NULL: not stored) and per 256
+ *                              columns the pair {max z, sum exp(z - max)} into smx (2*ceil(N/256) doubles)
+ *   tnet_rnn_out_bwd_update  : e = softmax(z) - onehot(*label) formed in place from z and smx; with
+ *                              train: the output layer's backprop + SGD of tnet_affine_bwd_update_row
+ *                              (e_out = Wo e, d = e_out .* h (1 - h)); cross-entropy into stats slot 0;
+ *                              the frame's argmax folded into *argkey (zero it first) by atomicMax of
+ *                              {y bits << 32 | ~column}; y / e / e_out / d may be NULL
+ *   tnet_argmax_correct      : frame accuracy of T frames from their argmax keys into stats slot 0 */
+int tnet_gemv_rowvec_partial(const float* v0, int K0, const float* v1, int K1, float* vout, const float* W, int ldw,
+                             int N, float* partial, void* stream);
+int tnet_rnn_out_partial(const float* hpart, int hslices, const float* hb, float* h, int H, const float* Wo, int ldwo,
+                         int N, float* opart, void* stream);
+int tnet_rnn_out_stats(const float* opart, int H, int N, const float* bo, float* z, double* smx, void* stream);
+int tnet_rnn_out_bwd_update(const float* z, const double* smx, int N, const int* label, const float* h, int H,
+                            float* Wo, int ldwo, float* corrWo, int ldc, float* bo, float* corr_bo, float scale,
+                            float mmt, float l2, float* y, float* e, float* e_out, float* d, double* stats,
+                            unsigned long long* argkey, int train, void* stream);
+int tnet_argmax_correct(const unsigned long long* keys, const int* labels, int T, int N, double* stats,
+                        void* stream);
 /* single-frame CuBiasedLinearity::Backpropagate + Update (cuBiasedLinearity.cc:32-64) in one pass
  * over W: e_out = W e (with the weights before the update), then the update of
  * tnet_affine_update_row; with s != NULL also d_out = e_out .* s (1 - s) (the diff-sigmoid of a

@@ -42,6 +42,17 @@ void CuRecurrent::PropagateFnc(const CuMatrix<BaseFloat>& X, CuMatrix<BaseFloat>
                                       N, 1, ws, S));
 }
 
+void CuRecurrent::PropagatePartial(const CuMatrix<BaseFloat>& X, float* part) {
+  if (X.Rows() != 1 || X.Cols() != GetNInputs()) Error("CuRecurrent::PropagatePartial: one input row");
+  if (mInputHistory.Rows() == 0) Error("Bptt order was not set");
+  mOutput.Init(1, GetNOutputs());  // y_{t-1}: kept across frames (no-op when allocated, cumatrix.tcc:20-23)
+  const int R = (int)mInputHistory.Rows();
+  mHead = (mHead + R - 1) % R;
+  TNET_SAFE_CALL(tnet_gemv_rowvec_partial(X.pCUData(), (int)X.Cols(), mOutput.pCUData(), (int)mOutput.Cols(),
+                                          mInputHistory.pCURowData((size_t)mHead), mLinearity.pCUData(),
+                                          (int)mLinearity.Stride(), (int)GetNOutputs(), part, S));
+}
+
 void CuRecurrent::BackpropagateFnc(const CuMatrix<BaseFloat>& X, CuMatrix<BaseFloat>& Y) {
   CuProfileScope p("CuRecurrent::Backpropagate");
   // diff = e .* y(1-y) ; Y += W[0:nIn] diff  (OffsetGemv('N', beta = 1.0), cuRecurrent.cc:58-83:
@@ -106,6 +117,26 @@ CuRecurrentTrainer::CuRecurrentTrainer(CuNetwork* net, CuObjectiveFunction* obj,
     if (net->Layer(i).GetType() == CuComponent::RECURRENT) dynamic_cast<CuRecurrent&>(net->Layer(i)).BpttOrder(bptt);
 }
 
+CuRecurrentTrainer::~CuRecurrentTrainer() {
+  (void)hipStreamSynchronize(CuDevice::Instantiate().Stream());
+  if (mSmx) (void)hipFree(mSmx);
+  if (mArgKey) (void)hipFree(mArgKey);
+}
+
+void* CuRecurrentTrainer::Scratch(void*& p, size_t& have, size_t bytes) {
+  if (bytes > have) {
+    if (p) {
+      TNET_HIP_CALL(hipStreamSynchronize(CuDevice::Instantiate().Stream()));
+      TNET_HIP_CALL(hipFree(p));
+      p = nullptr;
+      have = 0;
+    }
+    TNET_HIP_CALL(hipMalloc(&p, bytes));
+    have = bytes;
+  }
+  return p;
+}
+
 void CuRecurrentTrainer::TrainUtterance(const float* feats, size_t rows, size_t cols, size_t ld,
                                         const int* labels) {
   if (cols != mNet->GetNInputs()) Error("CuRecurrentTrainer: feature dim != network input dim");
@@ -119,6 +150,10 @@ void CuRecurrentTrainer::TrainUtterance(const float* feats, size_t rows, size_t 
   for (int i = 0; i < mNet->Layers(); i++)
     if (mNet->Layer(i).GetType() == CuComponent::RECURRENT) dynamic_cast<CuRecurrent&>(mNet->Layer(i)).ClearHistory();
   const bool fused = FusedFrameOk();
+  if (fused) {  // per-frame argmax keys of this utterance, read by tnet_argmax_correct at its end
+    Scratch(mArgKey, mArgKeyBytes, rows * sizeof(unsigned long long));
+    TNET_HIP_CALL(hipMemsetAsync(mArgKey, 0, rows * sizeof(unsigned long long), CuDevice::Instantiate().Stream()));
+  }
   for (size_t f = 0; f < rows; f++) {
     CuMatrix<BaseFloat>::MakeView(mRow, mFeats.pCURowData(f), 1, cols, mFeats.Stride());
     if (fused) {
@@ -130,6 +165,9 @@ void CuRecurrentTrainer::TrainUtterance(const float* feats, size_t rows, size_t 
     mObj->EvaluateLabels(mOut, mLabelRow, mErr);
     if (!mCrossval) mNet->Backpropagate(mErr);
   }
+  if (fused)
+    TNET_SAFE_CALL(tnet_argmax_correct((const unsigned long long*)mArgKey, mLabels.pCUData(), (int)rows,
+                                       (int)mNet->GetNOutputs(), mObj->DeviceStats(), S));
   mFrames += (long)rows;
 }
 
@@ -147,31 +185,39 @@ bool CuRecurrentTrainer::FusedFrameOk() const {
   return rec.LearnRate() > 0.0f && lin.LearnRate() > 0.0f;
 }
 
-// One frame of TRecurrentCu.cc:360-368 on the fused kernels, the same arithmetic as the generic
-// Propagate / EvaluateLabels / Backpropagate chain: the recurrent forward (2 launches: split-K
-// partials that also push the history row, + the sigmoid finish), output layer + softmax +
-// cross-entropy (2), output-layer backprop + update + the recurrent diff-sigmoid (1), the BPTT
-// GEMVs (bptt) and the recurrent update (1).  The network-output / softmax-error copies of the
-// generic chain have no reader here and are not made.
+// One frame of TRecurrentCu.cc:360-368 on the fused kernels, the arithmetic of the generic
+// Propagate / EvaluateLabels / Backpropagate chain: the recurrent split-K partials (+ the history
+// push), the sigmoid finish fused with the output layer's split-K partials, z + the softmax pairs,
+// the output layer's softmax error + backprop + update + the recurrent diff-sigmoid (+ xent and the
+// frame's argmax key), then the BPTT GEMVs (bptt) and the recurrent update (1).  The network-output
+// / softmax copies of the generic chain have no reader here and are not made.
 void CuRecurrentTrainer::TrainFrameFused(size_t f) {
   auto& rec = dynamic_cast<CuRecurrent&>(mNet->Layer(0));
   auto& lin = dynamic_cast<CuBiasedLinearity&>(mNet->Layer(1));
-  CuComponent& sm = mNet->Layer(2);
-  rec.SetInput(mRow);
-  rec.Propagate();
-  const int H = (int)lin.GetNInputs(), N = (int)lin.GetNOutputs();
+  const int nIn = (int)rec.GetNInputs(), H = (int)lin.GetNInputs(), N = (int)lin.GetNOutputs();
+  const int hs = (nIn + H + 63) / 64, os = (H + 63) / 64, G = (N + 255) / 256;
+  mRecPart.Init((size_t)hs, (size_t)H);
+  mOutPart.Init((size_t)os, (size_t)N);
+  double* smx = (double*)Scratch(mSmx, mSmxBytes, sizeof(double) * 2 * (size_t)G);
+  rec.PropagatePartial(mRow, mRecPart.pCUData());
+  // (the partial kernels address [slices x cols] densely inside these allocations)
   lin.Output().Init(1, (size_t)N);
-  sm.Output().Init(1, (size_t)N);
-  mErr.Init(1, (size_t)N);
-  void* ws = CuDevice::Instantiate().Workspace((size_t)tnet_gemv_workspace(H, N));
-  TNET_SAFE_CALL(tnet_gemv_rowvec_softmax_xent(rec.GetOutput().pCUData(), H, lin.Linearity().pCUData(),
-                                               (int)lin.Linearity().Stride(), lin.Bias().pCUData(),
-                                               lin.Output().pCUData(), sm.Output().pCUData(),
-                                               mCrossval ? nullptr : mErr.pCUData(), N, mLabels.pCUData() + f,
-                                               mObj->DeviceStats(), ws, S));
+  TNET_SAFE_CALL(tnet_rnn_out_partial(mRecPart.pCUData(), hs, rec.Bias().pCUData(), rec.Output().pCUData(), H,
+                                      lin.Linearity().pCUData(), (int)lin.Linearity().Stride(), N,
+                                      mOutPart.pCUData(), S));
+  TNET_SAFE_CALL(tnet_rnn_out_stats(mOutPart.pCUData(), H, N, lin.Bias().pCUData(), lin.Output().pCUData(), smx, S));
+  float scale, l2;
+  lin.UpdateConstants(1, &scale, &l2);
+  const bool mmt = lin.Momentum() != 0.0f;
+  lin.ErrorOutput().Init(1, (size_t)H);
+  TNET_SAFE_CALL(tnet_rnn_out_bwd_update(
+      lin.Output().pCUData(), smx, N, mLabels.pCUData() + f, rec.Output().pCUData(), H, lin.Linearity().pCUData(),
+      (int)lin.Linearity().Stride(), mmt ? lin.LinearityCorrection().pCUData() : nullptr,
+      (int)lin.LinearityCorrection().Stride(), lin.Bias().pCUData(), mmt ? lin.BiasCorrection().pCUData() : nullptr,
+      scale, lin.Momentum(), l2, nullptr, nullptr, lin.ErrorOutput().pCUData(), rec.DiffRow0(), mObj->DeviceStats(),
+      (unsigned long long*)mArgKey + f, mCrossval ? 0 : 1, S));
   mObj->AddFrames(1);
   if (mCrossval) return;
-  lin.BackpropUpdateRow(rec.GetOutput(), mErr, lin.ErrorOutput(), rec.GetOutput().pCUData(), rec.DiffRow0());
   rec.UpdateFromDiff0();
 }
 

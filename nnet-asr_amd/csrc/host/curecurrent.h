@@ -34,6 +34,10 @@ class CuRecurrent : public CuUpdatableComponent {
   void Update() override;
   /// Update with d_0 = e .* y(1-y) already in DiffRow0() (written by the fused output-layer kernel)
   void UpdateFromDiff0();
+  /// Fused-chain forward, first half: push the history row [x_t, y_{t-1}] and write the split-K
+  /// partials of row W to `part` (tnet_gemv_rowvec_partial); the bias + sigmoid finish is done by
+  /// the output layer's kernel, which stores y_t into GetOutput().
+  void PropagatePartial(const CuMatrix<BaseFloat>& X, float* part);
   float* DiffRow0() { return mDiff.pCURowData(0); }
 
   /// BPTT order; allocates the (ord+1)-row input history (cuRecurrent.h:30-33)
@@ -74,12 +78,22 @@ class CuRecurrentTrainer {
   CuObjectiveFunction* mObj;
   bool mCrossval;
   // [<recurrent>, <biasedlinearity>, <softmax>] + cross-entropy: the per-frame chain on the fused
-  // single-frame kernels (8 launches a frame instead of 18)
+  // single-frame kernels (4 launches + the BPTT a frame instead of 18)
   bool FusedFrameOk() const;
   void TrainFrameFused(size_t f);
   CuMatrix<BaseFloat> mFeats, mOut, mErr, mRow;
   CuVector<int> mLabels, mLabelRow;
   long mFrames = 0;
+  // fused-chain scratch: recurrent / output split-K partials, softmax pairs, per-frame argmax keys
+  CuMatrix<BaseFloat> mRecPart, mOutPart;
+  void* mSmx = nullptr;
+  size_t mSmxBytes = 0;
+  void* mArgKey = nullptr;
+  size_t mArgKeyBytes = 0;
+  void* Scratch(void*& p, size_t& have, size_t bytes);
+
+ public:
+  ~CuRecurrentTrainer();
 };
 
 }  // namespace TNet

@@ -71,6 +71,7 @@ struct GemmP {
   // K = its own depth and stores its partial product to C + z*slabC (EPI_STORE, alpha 1, beta 0)
   int ksplit;
   long kstepA, kstepB, slabC;
+  int early_issue;  // gemm16_kernel prologue: issue all S ring slots before the first wait (TNET_GEMM_EARLY)
 };
 
 
@@ -763,15 +764,23 @@ void gemm16_kernel(const GemmP p_in) {
   // compiler count lgkmcnt exactly instead of draining at every block join.
   const int nfull = K / BK;
   const int tlast = max(nfull - 1, 0);
+  // Prologue.  early: every slot's tile is issued before the first wait (tile S-1 lands while tile 0
+  // computes) -- else tile S-1 goes out only after tile 0 has landed (SP spreads it over tile 0)
+  const bool early = !SP && !LDR && p.early_issue;
   if constexpr (!LDR) {
-    if (nfull > 0)
+    if (nfull > 0) {
 #pragma unroll
       for (int t = 0; t < S - 1; ++t) issue(min(t, tlast), t);
+      if (early) issue(min(S - 1, tlast), S - 1);
+    }
   }
   if (nfull > 0) {
-    if constexpr (!LDR) wait_vmcnt<(S - 2) * G>();
+    if constexpr (!LDR) {
+      if (early) wait_vmcnt<(S - 1) * G>();
+      else wait_vmcnt<(S - 2) * G>();
+    }
     barrier();  // tile 0 landed in every wave's pieces
-    if (!SP) issue(min(S - 1, tlast), S - 1);
+    if (!SP && !early) issue(min(S - 1, tlast), S - 1);
     read_frags(smem, 0, 0);
   }
   // Epilogue operands (bias / y of the layer below / W and the momentum buffer) are loaded into
@@ -1378,6 +1387,7 @@ static const char* kCfgNames[CFG_COUNT] = {
 static int g_cfg = -2;  // -2: not initialised, -1: automatic
 static int g_group = -1;
 static int g_split = -1;  // TNET_GEMM_SPLITK: forced split-K count (diagnostics / sweeps), -1 automatic
+static int g_early = 1;   // TNET_GEMM_EARLY=0: prologue issues S-1 slots before the first wait (round-1 form)
 static int forced_cfg() {
   if (g_cfg == -2) {
     g_cfg = -1;
@@ -1389,6 +1399,8 @@ static int forced_cfg() {
     if (gg) g_group = atoi(gg);
     const char* sk = getenv("TNET_GEMM_SPLITK");
     if (sk) g_split = atoi(sk);
+    const char* ea = getenv("TNET_GEMM_EARLY");
+    if (ea) g_early = atoi(ea);
   }
   return g_cfg;
 }
@@ -1406,7 +1418,9 @@ static bool launch_cfg(const GemmP& p, hipStream_t st) {
     const long extB = B_KC ? (long)p.N * p.ldb : (long)BK * p.ldb + p.N;
     if (4 * extA >= (1L << 32) || 4 * extB >= (1L << 32)) return false;
     const dim3 grid(tiles, p.ksplit > 1 ? p.ksplit : 1);
-    gemm16_kernel<BM, BN, BK, WM, WN, S, IL, A_KC, B_KC, EPI><<<grid, (WM * WN + (IL == 2)) * 64, 0, st>>>(p);
+    GemmP q = p;
+    q.early_issue = g_early;
+    gemm16_kernel<BM, BN, BK, WM, WN, S, IL, A_KC, B_KC, EPI><<<grid, (WM * WN + (IL == 2)) * 64, 0, st>>>(q);
     return true;
   }
 }

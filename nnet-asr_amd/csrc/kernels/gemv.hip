@@ -187,12 +187,20 @@ __global__ __launch_bounds__(256) void rnn_update_kernel(float* __restrict__ W, 
     return;
   }
   float acc = 0.f;
-  for (int i = 0; i < steps; ++i) {
-    const float h = hist[(long)((head + i) % R) * ldh + k];
-    acc += (-lr * h) * D[(long)i * ldd + c];
-  }
   float* wp = W + (long)k * ldw + c;
   const float w = *wp;
+  for (int i0 = 0; i0 < steps; i0 += 8) {  // up to 8 steps' loads in flight, accumulated in step order
+    float hv[8], dv[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int i = i0 + q;
+      hv[q] = i < steps ? hist[(long)((head + i) % R) * ldh + k] : 0.f;
+      dv[q] = i < steps ? D[(long)i * ldd + c] : 0.f;
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+      if (i0 + q < steps) acc += (-lr * hv[q]) * dv[q];
+  }
   const float corr = (-lr * wc) * w + acc;
   *wp = corr + w;
 }
@@ -295,9 +303,289 @@ __global__ __launch_bounds__(256) void affine_update_row_kernel(const float* __r
   *wp = w;
 }
 
+// ---------------------------------------------------------------------------------------------
+// TRecurrentCu frame chain, output side, in three launches instead of four (the recurrent layer's
+// sigmoid finish, the output GEMV, the one-workgroup softmax and the output-layer backprop + update):
+//   rnn_out_partial_kernel : h = sigmoid(b + sum of the recurrent split-K partials) for the
+//                            workgroup's 64-row slice (gemv_rowvec_final's order, computed where it is
+//                            consumed; column block 0 stores it), then the output split-K partials
+//                            (gemv_rowvec_partial's order)
+//   rnn_out_stats_kernel   : z = b + sum of the output partials (gemv_softmax_xent_final's order) for
+//                            256 columns per workgroup, the workgroup's max m_g and sum of exp(z - m_g)
+//   rnn_out_bwd_kernel     : every workgroup combines the (m_g, s_g) pairs into the softmax normaliser,
+//                            forms e = softmax(z) - onehot(t) where it reads it, and runs
+//                            affine_bwd_update_row_kernel's arithmetic; the bias workgroups add the
+//                            cross-entropy and fold their argmax into the frame's 64-bit argmax key
+//                            (atomicMax of {y bits, ~column}: largest y, first column on ties)
+//   argmax_correct_kernel  : at the end of the utterance, frame accuracy from the keys
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void rnn_out_partial_kernel(const float* __restrict__ hpart, int hslices,
+                                                              const float* __restrict__ hb, float* __restrict__ h,
+                                                              int H, const float* __restrict__ Wo, long ldw, int N,
+                                                              float* __restrict__ opart) {
+  __shared__ float red[4][64];
+  __shared__ float hs[GV_KSLICE];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
+  const int k0 = blockIdx.y * GV_KSLICE, k1 = min(H, k0 + GV_KSLICE);
+  if ((int)threadIdx.x < k1 - k0) {
+    const int k = k0 + threadIdx.x;
+    float sacc = 0.f;
+    for (int q0 = 0; q0 < hslices; q0 += 16) {  // 16 slices' loads in flight, added in slice order
+      float p[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) p[q] = q0 + q < hslices ? hpart[(long)(q0 + q) * H + k] : 0.f;
+#pragma unroll
+      for (int q = 0; q < 16; ++q)
+        if (q0 + q < hslices) sacc += p[q];
+    }
+    const float hv = sigmoidf_ref((hb ? hb[k] : 0.f) + sacc);
+    hs[threadIdx.x] = hv;
+    if (blockIdx.x == 0) h[k] = hv;
+  }
+  __syncthreads();
+  float acc = 0.f;
+  if (c < N) {
+#pragma unroll 4
+    for (int k = k0 + w; k < k1; k += 4) acc += hs[k - k0] * Wo[(long)k * ldw + c];
+  }
+  red[w][lane] = acc;
+  __syncthreads();
+  if (w == 0 && c < N) opart[(long)blockIdx.y * N + c] = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
+}
+
+__global__ __launch_bounds__(256) void rnn_out_stats_kernel(const float* __restrict__ opart, int slices, int N,
+                                                            const float* __restrict__ b, float* __restrict__ z,
+                                                            double* __restrict__ smx) {
+  __shared__ float smax[4];
+  __shared__ double ssum[4];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  const int cc = min(c, N - 1);
+  float p[8];
+  float sacc = 0.f;
+  for (int k0 = 0; k0 < slices; k0 += 8) {  // 8 slices' loads in flight, added in slice order
+#pragma unroll
+    for (int q = 0; q < 8; ++q) p[q] = k0 + q < slices ? opart[(long)(k0 + q) * N + cc] : 0.f;
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+      if (k0 + q < slices) sacc += p[q];
+  }
+  const float a = c < N ? (b ? b[c] : 0.f) + sacc : -1e30f;
+  if (z && c < N) z[c] = a;
+  float m = wave_max(a);
+  if (lane == 0) smax[wv] = m;
+  __syncthreads();
+  m = fmaxf(fmaxf(smax[0], smax[1]), fmaxf(smax[2], smax[3]));
+  const double ws = wave_sum_d(c < N ? (double)fast_exp(a - m) : 0.0);
+  if (lane == 0) ssum[wv] = ws;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    smx[2 * blockIdx.x] = (double)m;
+    smx[2 * blockIdx.x + 1] = ssum[0] + ssum[1] + ssum[2] + ssum[3];
+  }
+}
+
+// the softmax normaliser from the stats workgroups' pairs: M = max m_g, S = sum s_g exp(m_g - M);
+// every wave loads the G <= 64 pairs in one pass (lane g) and reduces them itself
+__device__ __forceinline__ void rnn_softmax_norm(const double* __restrict__ smx, int G, float* M, float* rsum) {
+  const int lane = threadIdx.x & 63;
+  const float mg = lane < G ? (float)smx[2 * lane] : -1e30f;
+  const double sg = lane < G ? smx[2 * lane + 1] : 0.0;
+  const float m = wave_max(mg);
+  const double s = wave_sum_d(lane < G ? sg * (double)fast_exp(mg - m) : 0.0);
+  *M = m;
+  *rsum = 1.f / (float)s;
+}
+
+// WPR waves per weight row (1: rows of <= 1024 columns, a wave each; 4: a workgroup per row, so a
+// 4000-column row has its 16 KB of W in flight at once and the row sums meet in LDS in wave order)
+template <int WPR>
+__global__ __launch_bounds__(256) void rnn_out_bwd_kernel(
+    const float* __restrict__ z, const double* __restrict__ smx, int G, const int* __restrict__ label,
+    const float* __restrict__ h, int n_in, int n_out, float* __restrict__ W, long ldw, float* __restrict__ corrW,
+    long ldc, float* __restrict__ b, float* __restrict__ cb, float scale, float mmt, float l2,
+    float* __restrict__ yout, float* __restrict__ eout, float* __restrict__ eo, float* __restrict__ d,
+    double* __restrict__ stats, unsigned long long* __restrict__ argkey, int row_blocks, int train) {
+  __shared__ ArgMax sarg[4];
+  __shared__ float racc[4];
+  float M, rsum;
+  rnn_softmax_norm(smx, G, &M, &rsum);
+  const int t0 = label[0];
+  const int t = t0 < n_out ? t0 : -1;  // out of range: an unlabeled frame, as the batched kernels
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if ((int)blockIdx.x >= row_blocks) {  // bias / statistics workgroups: 256 columns each
+    const int j = (blockIdx.x - row_blocks) * blockDim.x + threadIdx.x;
+    ArgMax ay{-1e20f, 0x7fffffff};
+    if (j < n_out) {
+      const float yj = fast_exp(z[j] - M) * rsum;
+      const float ej = yj - (j == t ? 1.f : 0.f);
+      ay.v = yj;
+      ay.i = j;
+      if (yout) yout[j] = yj;
+      if (eout) eout[j] = ej;
+      if (j == t && stats) atomicAdd(stats, -(double)logf(fmaxf(yj, FLT_MIN)));
+      if (train) {
+        float g = ej;
+        if (cb) {
+          g = g + mmt * cb[j];
+          cb[j] = g;
+        }
+        b[j] = b[j] + scale * g;
+      }
+    }
+    ay = wave_argmax(ay);
+    if (lane == 0) sarg[wv] = ay;
+    __syncthreads();
+    if (threadIdx.x == 0 && argkey) {
+      ArgMax a = sarg[0];
+#pragma unroll
+      for (int q = 1; q < 4; ++q) a = argmax_merge(a, sarg[q]);
+      if (a.i < n_out) {
+        const unsigned long long key =
+            ((unsigned long long)__float_as_uint(fmaxf(a.v, 0.f)) << 32) | (unsigned long long)(0xffffffffu - (unsigned)a.i);
+        atomicMax(argkey, key);
+      }
+    }
+    return;
+  }
+  if (!train) return;
+  constexpr int RPB = 4 / WPR;  // rows per workgroup
+  const int i = blockIdx.x * RPB + wv / WPR, sub = wv % WPR;
+  const bool live = i < n_in;
+  const float xi = live ? h[i] : 0.f;
+  float* row = W + (long)(live ? i : 0) * ldw;
+  float* qrow = corrW ? corrW + (long)(live ? i : 0) * ldc : nullptr;
+  auto upd = [&](float w, float ej, float* q) {
+    float c = xi * ej;
+    if (qrow) {
+      c = c + mmt * *q;
+      *q = c;
+    }
+    w = w + scale * c;
+    return w + l2 * w;
+  };
+  auto err = [&](int c, float zc) { return fast_exp(zc - M) * rsum - (c == t ? 1.f : 0.f); };
+  float acc = 0.f;
+  if (live) {
+    if ((n_out & 3) == 0 && (ldw & 3) == 0 && (!qrow || (ldc & 3) == 0) &&
+        (((uintptr_t)row | (uintptr_t)z | (uintptr_t)qrow) & 15) == 0) {
+      constexpr int STEP = 256 * WPR;  // floats per pass of the row's waves
+#pragma unroll 2
+      for (int c = (sub * 64 + lane) * 4; c < n_out; c += STEP) {
+        f32x4 a = *reinterpret_cast<const f32x4*>(row + c);
+        const f32x4 zv = *reinterpret_cast<const f32x4*>(z + c);
+        f32x4 qv = qrow ? *reinterpret_cast<const f32x4*>(qrow + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+        float ev[4], q[4] = {qv[0], qv[1], qv[2], qv[3]};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) ev[k] = err(c + k, zv[k]);
+        acc += a[0] * ev[0] + a[1] * ev[1] + a[2] * ev[2] + a[3] * ev[3];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) a[k] = upd(a[k], ev[k], &q[k]);
+        *reinterpret_cast<f32x4*>(row + c) = a;
+        if (qrow) *reinterpret_cast<f32x4*>(qrow + c) = f32x4{q[0], q[1], q[2], q[3]};
+      }
+    } else {
+      for (int c = sub * 64 + lane; c < n_out; c += 64 * WPR) {
+        const float w = row[c], ej = err(c, z[c]);
+        acc += w * ej;
+        row[c] = upd(w, ej, qrow ? qrow + c : nullptr);
+      }
+    }
+  }
+  acc = wave_sum(acc);
+  if constexpr (WPR > 1) {
+    if (lane == 0) racc[wv] = acc;
+    __syncthreads();
+    acc = ((racc[0] + racc[1]) + racc[2]) + racc[3];
+  }
+  if (live && sub == 0 && lane == 0) {
+    if (eo) eo[i] = acc;
+    if (d) d[i] = acc * (xi * (1.f - xi));
+  }
+}
+
+__global__ __launch_bounds__(256) void argmax_correct_kernel(const unsigned long long* __restrict__ keys,
+                                                             const int* __restrict__ labels, int T, int N,
+                                                             double* __restrict__ stats) {
+  __shared__ double red[4];
+  double n = 0.0;
+  for (int f = threadIdx.x; f < T; f += 256) {
+    const int t = labels[f];
+    const int des = (t >= 0 && t < N) ? t : 0;
+    const unsigned idx = 0xffffffffu - (unsigned)(keys[f] & 0xffffffffull);
+    n += (keys[f] != 0ull && idx == (unsigned)des) ? 1.0 : 0.0;
+  }
+  n = wave_sum_d(n);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = n;
+  __syncthreads();
+  if (threadIdx.x == 0) atomicAdd(stats + 1, red[0] + red[1] + red[2] + red[3]);
+}
+
 }  // namespace tnetk
 
 using namespace tnetk;
+
+extern "C" int tnet_gemv_rowvec_partial(const float* v0, int K0, const float* v1, int K1, float* vout,
+                                        const float* W, int ldw, int N, float* partial, void* stream) {
+  const int K = K0 + K1;
+  if (K0 < 0 || K1 < 0 || K <= 0 || N <= 0 || ldw < N || (K0 && !v0) || (K1 && !v1) || !W || !partial)
+    return TNET_ERR_ARG;
+  gemv_rowvec_partial<<<dim3(cdiv(N, 64), cdiv(K, GV_KSLICE)), 256, 0, (hipStream_t)stream>>>(v0, K0, v1, K, W, ldw,
+                                                                                                N, partial, vout);
+  TNET_LAUNCH_CHECK();
+  return TNET_OK;
+}
+
+extern "C" int tnet_rnn_out_partial(const float* hpart, int hslices, const float* hb, float* h, int H,
+                                    const float* Wo, int ldwo, int N, float* opart, void* stream) {
+  if (hslices <= 0 || H <= 0 || N <= 0 || ldwo < N || !hpart || !h || !Wo || !opart) return TNET_ERR_ARG;
+  rnn_out_partial_kernel<<<dim3(cdiv(N, 64), cdiv(H, GV_KSLICE)), 256, 0, (hipStream_t)stream>>>(
+      hpart, hslices, hb, h, H, Wo, ldwo, N, opart);
+  TNET_LAUNCH_CHECK();
+  return TNET_OK;
+}
+
+extern "C" int tnet_rnn_out_stats(const float* opart, int H, int N, const float* bo, float* z, double* smx,
+                                  void* stream) {
+  if (H <= 0 || N <= 0 || !opart || !smx) return TNET_ERR_ARG;
+  rnn_out_stats_kernel<<<cdiv(N, 256), 256, 0, (hipStream_t)stream>>>(opart, cdiv(H, GV_KSLICE), N, bo, z, smx);
+  TNET_LAUNCH_CHECK();
+  return TNET_OK;
+}
+
+extern "C" int tnet_rnn_out_bwd_update(const float* z, const double* smx, int N, const int* label, const float* h,
+                                       int H, float* Wo, int ldwo, float* corrWo, int ldc, float* bo, float* corr_bo,
+                                       float scale, float mmt, float l2, float* y, float* e, float* eo, float* d,
+                                       double* stats, unsigned long long* argkey, int train, void* stream) {
+  if (N <= 0 || H <= 0 || !z || !smx || !label || !h || (train && (!Wo || !bo || ldwo < N)) ||
+      (train && mmt != 0.f && (!corrWo || !corr_bo || ldc < N)))
+    return TNET_ERR_ARG;
+  if (cdiv(N, 256) > 64) return TNET_ERR_UNSUPPORTED;  // N <= 16384: one pair per lane in rnn_softmax_norm
+  const bool wide = N > 1024;  // a workgroup per weight row
+  const int row_blocks = train ? (wide ? H : cdiv(H, 4)) : 0;
+  const dim3 grid(row_blocks + cdiv(N, 256));
+  hipStream_t st = (hipStream_t)stream;
+  if (wide)
+    rnn_out_bwd_kernel<4><<<grid, 256, 0, st>>>(z, smx, cdiv(N, 256), label, h, H, N, Wo, ldwo,
+                                                mmt != 0.f ? corrWo : nullptr, ldc, bo, mmt != 0.f ? corr_bo : nullptr,
+                                                scale, mmt, l2, y, e, eo, d, stats, argkey, row_blocks, train);
+  else
+    rnn_out_bwd_kernel<1><<<grid, 256, 0, st>>>(z, smx, cdiv(N, 256), label, h, H, N, Wo, ldwo,
+                                                mmt != 0.f ? corrWo : nullptr, ldc, bo, mmt != 0.f ? corr_bo : nullptr,
+                                                scale, mmt, l2, y, e, eo, d, stats, argkey, row_blocks, train);
+  TNET_LAUNCH_CHECK();
+  return TNET_OK;
+}
+
+extern "C" int tnet_argmax_correct(const unsigned long long* keys, const int* labels, int T, int N, double* stats,
+                                   void* stream) {
+  if (T < 0 || N <= 0 || (T && (!keys || !labels || !stats))) return TNET_ERR_ARG;
+  if (!T) return TNET_OK;
+  argmax_correct_kernel<<<1, 256, 0, (hipStream_t)stream>>>(keys, labels, T, N, stats);
+  TNET_LAUNCH_CHECK();
+  return TNET_OK;
+}
 
 extern "C" int tnet_affine_update_row(const float* x, int n_in, const float* e, int n_out, float* W, int ldw,
                                       float* corrW, int ldc, float* b, float* corr_b, float scale, float mmt,

@@ -169,6 +169,12 @@ _SIGS = {
     "tnet_rbm_update": (i32, [vp, MatrixDim, vp, MatrixDim, vp, MatrixDim, vp, i32, f32, f32, f32, vp]),
     "tnet_rbm_bias_update": (i32, [vp, MatrixDim, i32, vp, vp, f32, f32, vp, vp]),
     "tnet_rbm_stats_update": (i32, [vp, MatrixDim, vp, MatrixDim, i32, vp, vp, vp, vp, f32, f32, vp, vp]),
+    "tnet_gemv_rowvec_partial": (i32, [vp, i32, vp, i32, vp, vp, i32, i32, vp, vp]),
+    "tnet_rnn_out_partial": (i32, [vp, i32, vp, vp, i32, vp, i32, i32, vp, vp]),
+    "tnet_rnn_out_stats": (i32, [vp, i32, i32, vp, vp, vp, vp]),
+    "tnet_rnn_out_bwd_update": (i32, [vp, vp, i32, vp, vp, i32, vp, i32, vp, i32, vp, vp, f32, f32, f32, vp, vp, vp,
+                                      vp, vp, vp, i32, vp]),
+    "tnet_argmax_correct": (i32, [vp, vp, i32, i32, vp, vp]),
     "tnetF_rand": (i32, [vp, MatrixDim, vp, vp, vp, vp, vp]),
     "tnetF_gauss_rand": (i32, [vp, MatrixDim, vp, vp, vp, vp, vp]),
     "tnetF_binarize_probs": (i32, [vp, vp, vp, MatrixDim, vp]),

@@ -221,3 +221,62 @@ def test_affine_bwd_update_row(mmt, n_in, n_out):
         np.testing.assert_allclose(dCb.numpy().ravel(), gb, rtol=1e-6, atol=1e-7)
     else:  # momentum 0: the correction buffers are not touched
         np.testing.assert_array_equal(dC.numpy(), corr)
+
+
+@pytest.mark.parametrize("nIn,H,N,t", [(440, 512, 4000, 17), (440, 512, 135, 3), (30, 70, 300, -1), (8, 64, 5, 9)])
+def test_rnn_output_chain_kernels(nIn, H, N, t):
+    """tnet_gemv_rowvec_partial -> tnet_rnn_out_partial -> tnet_rnn_out_stats -> tnet_rnn_out_bwd_update
+    (the fused frame's output side) vs numpy in fp64: h, z, the softmax error inside the SGD of Wo / bo,
+    e_out = Wo e (old Wo), d = e_out h (1 - h), cross-entropy and the argmax key (rtol 1e-5)"""
+    rng = np.random.default_rng(N + H)
+    x = rng.standard_normal(nIn).astype(np.float32)
+    yp = rng.random(H).astype(np.float32)
+    W = (0.05 * rng.standard_normal((nIn + H, H))).astype(np.float32)
+    b = rng.standard_normal(H).astype(np.float32)
+    Wo = (0.05 * rng.standard_normal((H, N))).astype(np.float32)
+    bo = rng.standard_normal(N).astype(np.float32)
+    scale, l2 = -0.03, -1e-5
+    d = {k: DeviceArray.from_numpy(v.reshape(1, -1) if v.ndim == 1 else v) for k, v in
+         dict(x=x, yp=yp, W=W, b=b, Wo=Wo, bo=bo).items()}
+    hs, os_, G = -(-(nIn + H) // 64), -(-H // 64), -(-N // 256)
+    hpart, opart = DeviceArray(hs, H), DeviceArray(os_, N)
+    hist, h, z = DeviceArray(1, nIn + H), DeviceArray(1, H), DeviceArray(1, N)
+    smx = DeviceArray(1, 2 * G, np.float64, stride=2 * G)
+    lab = DeviceArray.vector(np.array([t], np.int32))
+    eo, dd, e, y = DeviceArray(1, H), DeviceArray(1, H), DeviceArray(1, N), DeviceArray(1, N)
+    stats = DeviceArray(1, 1024, np.float64, stride=1024)
+    key = DeviceArray.vector(np.zeros(2, np.int32))  # one 64-bit key
+    check(lib().tnet_gemv_rowvec_partial(d["x"].ptr, nIn, d["yp"].ptr, H, hist.ptr, d["W"].ptr, d["W"].stride, H,
+                                         hpart.ptr, S()))
+    check(lib().tnet_rnn_out_partial(hpart.ptr, hs, d["b"].ptr, h.ptr, H, d["Wo"].ptr, d["Wo"].stride, N, opart.ptr,
+                                     S()))
+    check(lib().tnet_rnn_out_stats(opart.ptr, H, N, d["bo"].ptr, z.ptr, smx.ptr, S()))
+    check(lib().tnet_rnn_out_bwd_update(z.ptr, smx.ptr, N, lab.ptr, h.ptr, H, d["Wo"].ptr, d["Wo"].stride, None, 0,
+                                        d["bo"].ptr, None, scale, 0.0, l2, y.ptr, e.ptr, eo.ptr, dd.ptr, stats.ptr,
+                                        key.ptr, 1, S()))
+    v = np.concatenate([x, yp]).astype(np.float64)
+    np.testing.assert_array_equal(hist.numpy().ravel(), np.concatenate([x, yp]))
+    hr = 1 / (1 + np.exp(-(b + v @ W)))
+    np.testing.assert_allclose(h.numpy().ravel(), hr, rtol=1e-5, atol=1e-6)
+    zr = bo + hr @ Wo
+    np.testing.assert_allclose(z.numpy().ravel(), zr, rtol=1e-5, atol=1e-5)
+    yr = np.exp(zr - zr.max())
+    yr /= yr.sum()
+    tt = t if 0 <= t < N else -1
+    er = yr - (np.arange(N) == tt)
+    np.testing.assert_allclose(y.numpy().ravel(), yr, rtol=2e-5, atol=1e-9)
+    np.testing.assert_allclose(e.numpy().ravel(), er, rtol=2e-5, atol=1e-8)
+    eor = Wo.astype(np.float64) @ er
+    np.testing.assert_allclose(eo.numpy().ravel(), eor, rtol=1e-4, atol=1e-6)
+    np.testing.assert_allclose(dd.numpy().ravel(), eor * hr * (1 - hr), rtol=1e-4, atol=1e-6)
+    Wn = Wo + scale * np.outer(hr, er)
+    np.testing.assert_allclose(d["Wo"].numpy(), Wn + l2 * Wn, rtol=1e-5, atol=1e-7)
+    np.testing.assert_allclose(d["bo"].numpy().ravel(), bo + scale * er, rtol=1e-5, atol=1e-7)
+    xent = -np.log(max(yr[tt], 1.1754944e-38)) if tt >= 0 else 0.0
+    np.testing.assert_allclose(stats.numpy()[0][0::2].sum(), xent, rtol=1e-5, atol=1e-6)
+    k = int(key.numpy().ravel().view(np.uint64)[0])
+    assert 0xFFFFFFFF - (k & 0xFFFFFFFF) == int(np.argmax(y.numpy().ravel()))
+    # frame accuracy from the key
+    st2 = DeviceArray(1, 1024, np.float64, stride=1024)
+    check(lib().tnet_argmax_correct(key.ptr, lab.ptr, 1, N, st2.ptr, S()))
+    assert st2.numpy()[0][1] == float(int(np.argmax(y.numpy().ravel())) == (tt if tt >= 0 else 0))
