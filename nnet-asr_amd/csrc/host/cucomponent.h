@@ -133,7 +133,12 @@ class CuUpdatableComponent : public CuComponent {
   /// Compute the local gradient into the component's gradient buffers (no parameter change).
   virtual void ComputeGradient() { Error(std::string(GetName()) + ": ComputeGradient not supported"); }
   /// Apply the (already all-reduced) gradient; `frames` = global rows contributing.
-  virtual void ApplyGradient(size_t frames) { Error(std::string(GetName()) + ": ApplyGradient not supported"); }
+  /// stream: where to enqueue the update (nullptr: the library stream)
+  virtual void ApplyGradient(size_t frames, void* stream = nullptr) {
+    (void)frames;
+    (void)stream;
+    Error(std::string(GetName()) + ": ApplyGradient not supported");
+  }
   /// Gradient buffers of this component (valid after ComputeGradient()).
   virtual std::vector<CuParamBlock> GradientBlocks() { return {}; }
   /// Zero the gradient buffers (a data-parallel rank without a bunch contributes nothing).

@@ -194,7 +194,7 @@ std::vector<CuParamBlock> CuBiasedLinearity::GradientBlocks() {
           CuParamBlock{mGradB.pCUData(), (long)mGradB.Dim()}};
 }
 
-void CuBiasedLinearity::ApplyGradient(size_t frames) {
+void CuBiasedLinearity::ApplyGradient(size_t frames, void* stream) {
   CuProfileScope p("CuBiasedLinearity::ApplyGradient");
   float scale, l2;
   UpdateConstants(frames, &scale, &l2);
@@ -205,6 +205,10 @@ void CuBiasedLinearity::ApplyGradient(size_t frames) {
       {mLinearity.pCUData(), mGradW.pCUData(), mmt ? mLinearityCorrection.pCUData() : nullptr,
        (long)(mLinearity.Rows() * mLinearity.Stride()), l2},
       {mBias.pCUData(), mGradB.pCUData(), mmt ? mBiasCorrection.pCUData() : nullptr, (long)mBias.Dim(), 0.f}};
+  if (stream) {  // beside the compute stream (GradExchange::ApplyStream): no library-stream timing
+    TNET_SAFE_CALL(tnet_sgd_update_multi(seg, 2, scale, mMomentum, stream));
+    return;
+  }
   KTScope kt("sgd_apply:" + std::to_string(GetNInputs()) + "x" + std::to_string(GetNOutputs()),
              12.0 * (double)(mLinearity.Rows() * mLinearity.Stride() + mBias.Dim()));
   TNET_SAFE_CALL(tnet_sgd_update_multi(seg, 2, scale, mMomentum, S));

@@ -212,8 +212,23 @@ void CuNetwork::TrainEmpty(GradExchange& exchange) {
     }
     if (lin == mpPropagErrorStopper) break;
   }
-  exchange.WaitAll();
   const size_t grows = exchange.GlobalRows(0);
+  int i = 0;
+  bool inline_apply = true;
+  for (int l = nl - 1; l >= 0; l--) {  // applies beside the reductions where the transport allows
+    auto* lin = static_cast<CuBiasedLinearity*>(mNetComponents[2 * l]);
+    if (lin->LearnRate() > 0.0f) {
+      void* as = exchange.ApplyStream(i++);
+      if (!as) {
+        inline_apply = false;
+        break;
+      }
+      lin->ApplyGradient(grows, as);
+    }
+    if (lin == mpPropagErrorStopper) break;
+  }
+  exchange.WaitAll();
+  if (inline_apply) return;
   for (int l = nl - 1; l >= 0; l--) {
     auto* lin = static_cast<CuBiasedLinearity*>(mNetComponents[2 * l]);
     if (lin->LearnRate() > 0.0f) lin->ApplyGradient(grows);
@@ -286,7 +301,9 @@ void CuNetwork::TrainBunch(const CuMatrix<BaseFloat>& X, const CuVector<int>& la
 
   // ---- backward + update, top to bottom (error uses the pre-update weights of the layer)
   const CuMatrix<BaseFloat>* err = &mGlobErr;
-  std::vector<CuBiasedLinearity*> submitted;  // data-parallel: layers in reduction order
+  std::vector<CuBiasedLinearity*> submitted;  // data-parallel: layers in reduction order, not yet applied
+  const size_t grows = exchange ? exchange->GlobalRows(rows) : rows;
+  int n_submitted = 0;
   bool err_colsum = false;
   {
     // the top layer's bias gradient as slab sums too (one launch; the update GEMM applies it)
@@ -340,7 +357,12 @@ void CuNetwork::TrainBunch(const CuMatrix<BaseFloat>& X, const CuVector<int>& la
         else
           lin->ComputeGradient();
         exchange->Submit(*lin);
-        submitted.push_back(lin);
+        // the layer's SGD update right behind its reduction, beside the backward GEMMs below (W_l is
+        // read for the last time by this layer's backward GEMM, already enqueued)
+        void* as = submitted.empty() ? exchange->ApplyStream(n_submitted) : nullptr;
+        if (as) lin->ApplyGradient(grows, as);
+        else submitted.push_back(lin);
+        n_submitted++;
       } else if (err_colsum) {
         lin->UpdateFromColsum(*acts[l], *err, *mColPart[l]);
       } else {
@@ -352,11 +374,11 @@ void CuNetwork::TrainBunch(const CuMatrix<BaseFloat>& X, const CuVector<int>& la
     err_colsum = eo_colsum;
   }
   if (exchange) {
-    // apply each layer as soon as its own reduction is done (top layer first): the applies overlap
-    // the reductions of the layers below
-    const size_t grows = exchange->GlobalRows(rows);
+    // transports without an apply stream: apply each layer on the compute stream as soon as its own
+    // reduction is done (top layer first), overlapping the reductions of the layers below
+    const int first = n_submitted - (int)submitted.size();
     for (size_t i = 0; i < submitted.size(); i++) {
-      exchange->WaitFor((int)i);
+      exchange->WaitFor(first + (int)i);
       submitted[i]->ApplyGradient(grows);
     }
     exchange->WaitAll();

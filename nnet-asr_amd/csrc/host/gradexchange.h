@@ -32,6 +32,14 @@ class GradExchange {
     (void)i;
     WaitAll();
   }
+  /// Stream on which the apply (SGD update) of the i-th submitted layer may be enqueued so that it
+  /// runs as soon as that layer's reduction is done, beside the backward GEMMs still running on the
+  /// compute stream; WaitAll() then also joins the applies.  nullptr: apply on the compute stream
+  /// after WaitFor(i) (host transports, whose Submit is synchronous).
+  virtual void* ApplyStream(int i) {
+    (void)i;
+    return nullptr;
+  }
   /// Sum small host statistics over ranks (epoch-end MergeStats, step planning); blocking.
   virtual void AllReduceHost(double* v, int n) = 0;
 

@@ -202,6 +202,10 @@ struct RcclExchange::Impl {
   std::vector<hipEvent_t> ar_done;    // comm stream -> compute stream (reduction done), per submit
   size_t next_event = 0;
   hipEvent_t done = nullptr;
+  // applies of reduced layers: their own stream, so the comm stream only carries the reductions
+  hipStream_t apply_stream = nullptr;
+  hipEvent_t apply_done = nullptr;
+  bool applied = false;
   double* dscratch = nullptr;
 };
 
@@ -218,7 +222,9 @@ RcclExchange::RcclExchange(int rank, int world, const char id[128]) : mImpl(new 
   std::memcpy(&uid, id, 128);
   NCCL_CALL(ncclCommInitRank(&mImpl->comm, world, uid, rank));
   TNET_HIP_CALL(hipStreamCreateWithFlags(&mImpl->comm_stream, hipStreamNonBlocking));
+  TNET_HIP_CALL(hipStreamCreateWithFlags(&mImpl->apply_stream, hipStreamNonBlocking));
   TNET_HIP_CALL(hipEventCreateWithFlags(&mImpl->done, hipEventDisableTiming));
+  TNET_HIP_CALL(hipEventCreateWithFlags(&mImpl->apply_done, hipEventDisableTiming));
   TNET_HIP_CALL(hipMalloc(&mImpl->dscratch, 4096));
   (void)dev;
 }
@@ -226,9 +232,12 @@ RcclExchange::RcclExchange(int rank, int world, const char id[128]) : mImpl(new 
 RcclExchange::~RcclExchange() {
   if (!mImpl) return;
   (void)hipStreamSynchronize(mImpl->comm_stream);
+  if (mImpl->apply_stream) (void)hipStreamSynchronize(mImpl->apply_stream);
   for (auto e : mImpl->events) (void)hipEventDestroy(e);
   for (auto e : mImpl->ar_done) (void)hipEventDestroy(e);
   if (mImpl->done) (void)hipEventDestroy(mImpl->done);
+  if (mImpl->apply_done) (void)hipEventDestroy(mImpl->apply_done);
+  if (mImpl->apply_stream) (void)hipStreamDestroy(mImpl->apply_stream);
   if (mImpl->dscratch) (void)hipFree(mImpl->dscratch);
   if (mImpl->comm) (void)ncclCommDestroy(mImpl->comm);
   if (mImpl->comm_stream) (void)hipStreamDestroy(mImpl->comm_stream);
@@ -261,10 +270,24 @@ void RcclExchange::WaitFor(int i) {
   TNET_HIP_CALL(hipStreamWaitEvent(CuDevice::Instantiate().Stream(), mImpl->ar_done[(size_t)i], 0));
 }
 
+void* RcclExchange::ApplyStream(int i) {
+  static const bool off = getenv("TNET_DP_APPLY_STREAM") && getenv("TNET_DP_APPLY_STREAM")[0] == '0';
+  if (off) return nullptr;  // A/B: the applies on the compute stream after WaitFor (round-1 form)
+  if (i < 0 || (size_t)i >= mImpl->next_event) Error("RcclExchange::ApplyStream: no such reduction");
+  TNET_HIP_CALL(hipStreamWaitEvent(mImpl->apply_stream, mImpl->ar_done[(size_t)i], 0));
+  mImpl->applied = true;
+  return (void*)mImpl->apply_stream;
+}
+
 void RcclExchange::WaitAll() {
   CuDevice& dev = CuDevice::Instantiate();
   TNET_HIP_CALL(hipEventRecord(mImpl->done, mImpl->comm_stream));
   TNET_HIP_CALL(hipStreamWaitEvent(dev.Stream(), mImpl->done, 0));
+  if (mImpl->applied) {
+    TNET_HIP_CALL(hipEventRecord(mImpl->apply_done, mImpl->apply_stream));
+    TNET_HIP_CALL(hipStreamWaitEvent(dev.Stream(), mImpl->apply_done, 0));
+    mImpl->applied = false;
+  }
   mImpl->next_event = 0;
 }
 

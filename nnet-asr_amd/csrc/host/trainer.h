@@ -118,6 +118,7 @@ class RcclExchange : public GradExchange {
   void Submit(CuUpdatableComponent& comp) override;
   void WaitAll() override;
   void WaitFor(int i) override;
+  void* ApplyStream(int i) override;
   void AllReduceHost(double* v, int n) override;
   /// all-reduce (sum) of a device float buffer on the communication stream, synchronous
   void AllReduceDevice(float* buf, size_t n);
