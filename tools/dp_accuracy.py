@@ -1,0 +1,151 @@
+#!/usr/bin/env python3
+"""Frame accuracy of data-parallel training at 1, 2, 4 and 8 ranks (the
+weak-scaling mode needs "matched frame accuracy" shown on a teacher-labelled set).
+
+Every rank is a process on ONE GPU here (the 8-GPU node is the driver's), the gradients summed by
+the host-transport communicator over gloo -- the same exchange protocol as the RCCL path
+(GradExchange: per-layer sum, GRADDIVFRM over the global bunch, zero-gradient joins for uneven
+shards), so the trajectory is the one an N-GPU run takes.  Network: BASELINE config 2's MLP3
+(598:1024:135 sigmoid + softmax); data: a synthetic 598-dim N(0,1) corpus labelled by a fixed
+random teacher MLP (learnable, tools/../formats.synth_corpus), utterances dealt round-robin to the
+ranks (Platform.h:206-236), bunch 1024 frames PER RANK (global 1024 N), learning rate scaled
+linearly with N (lr_N = N lr_1: the same step per epoch of frames; --scale sqrt: sqrt(N) lr_1).  After every epoch (one
+TNetCu-style pass, fresh cache / shuffle seed per epoch, TNetCu.cc:330-441) rank 0 evaluates a
+held-out set in cross-validation mode (TNetCu -c).
+
+usage: python tools/dp_accuracy.py [--worlds 1,2,4,8] [--epochs 4] [--utts 800] [--lr 1.0]
+       (worker mode is internal)"""
+import argparse
+import json
+import os
+import socket
+import subprocess
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "nnet-asr_amd"))
+import numpy as np  # noqa: E402
+
+DIMS = [598, 1024, 135]
+SEED = 7
+
+
+def teacher(dim, n_cls, hidden=64):
+    trng = np.random.default_rng(SEED + 1)
+    return [trng.standard_normal((dim, hidden)).astype(np.float32) / np.sqrt(dim),
+            trng.standard_normal((hidden, n_cls)).astype(np.float32) / np.sqrt(hidden) * 4.0]
+
+
+def utterance(i, T, split):
+    """utterance i of a split (0 train, 1 held-out), generated on its own seed (a rank makes only
+    its shard)"""
+    rng = np.random.default_rng(1000003 * (split + 1) + i)
+    n = int(rng.integers(200, 1501))
+    x = rng.standard_normal((n, DIMS[0])).astype(np.float32)
+    h = np.tanh(x @ T[0]) @ T[1]
+    return x, np.argmax(h, axis=1).astype(np.int32)
+
+
+def worker(a):
+    import torch
+    import torch.distributed as dist
+
+    import tnet_amd
+    from tnet_amd import Network, Objective, Trainer, formats
+
+    rank, world = int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1"))
+    comm = None
+    if world > 1:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+
+        def allreduce(v):
+            dist.all_reduce(torch.from_numpy(v))
+
+        comm = tnet_amd.Comm.host(rank, world, allreduce)
+    T = teacher(DIMS[0], DIMS[-1])
+    mine = tnet_amd.shard_utterances(list(range(a.utts)), rank, world)
+    train = [utterance(i, T, 0) for i in mine]
+    held = [utterance(i, T, 1) for i in range(a.cv_utts)] if rank == 0 else []
+    net = Network.from_layers(formats.gen_mlp_init(DIMS, seed=SEED))
+    lr = a.lr * (world if a.scale == "linear" else world ** 0.5)
+    net.set_learn_rate(lr)
+    net.set_grad_div_frm(True)
+    log = []
+    t0 = time.time()
+    for ep in range(a.epochs):
+        obj = Objective()
+        tr = Trainer(net, obj, bunchsize=a.bunch, cachesize=a.cache, seed=1 + 1000 * ep + rank)
+        if comm is not None:
+            tr.set_comm(comm)
+        tr.train_corpus([x for x, _ in train], [y for _, y in train])
+        err, frames, correct = obj.stats()
+        st = np.array([err, frames, correct], np.float64)
+        if comm is not None:
+            st = comm.allreduce_host(st)
+        rec = {"epoch": ep + 1, "train_xent_per_frame": st[0] / st[1], "train_acc": 100.0 * st[2] / st[1],
+               "train_frames": int(st[1]), "steps_rank0": tr.steps}
+        if rank == 0:
+            cobj = Objective()
+            cv = Trainer(net, cobj, bunchsize=a.bunch, cachesize=a.cache, seed=0, randomize=False, crossval=True)
+            cv.train_corpus([x for x, _ in held], [y for _, y in held])
+            ce, cf, cc = cobj.stats()
+            rec.update(cv_xent_per_frame=ce / cf, cv_acc=100.0 * cc / cf, cv_frames=int(cf))
+        log.append(rec)
+        del tr
+    if rank == 0:
+        print("RESULT " + json.dumps({"world": world, "lr": lr, "lr_scaling": a.scale, "bunch_per_rank": a.bunch,
+                                      "global_bunch": a.bunch * world, "epochs": log,
+                                      "wall_s": round(time.time() - t0, 1)}), flush=True)
+    if comm is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("mode", nargs="?", default="launch", choices=["launch", "worker"])
+    ap.add_argument("--worlds", default="1,2,4,8")
+    ap.add_argument("--epochs", type=int, default=4)
+    ap.add_argument("--utts", type=int, default=800)
+    ap.add_argument("--cv-utts", type=int, default=40)
+    ap.add_argument("--bunch", type=int, default=1024)
+    ap.add_argument("--cache", type=int, default=16384)
+    ap.add_argument("--lr", type=float, default=1.0)
+    ap.add_argument("--scale", default="linear", choices=["linear", "sqrt"], help="lr_N = lr_1 N or lr_1 sqrt(N)")
+    a = ap.parse_args()
+    if a.mode == "worker":
+        worker(a)
+        return
+    out = []
+    for world in [int(w) for w in a.worlds.split(",")]:
+        env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(free_port()), WORLD_SIZE=str(world),
+                   OMP_NUM_THREADS="2")
+        args = [sys.executable, os.path.abspath(__file__), "worker", "--epochs", str(a.epochs), "--utts",
+                str(a.utts), "--cv-utts", str(a.cv_utts), "--bunch", str(a.bunch), "--cache", str(a.cache), "--lr",
+                str(a.lr), "--scale", a.scale]
+        procs = [subprocess.Popen(args, env=dict(env, RANK=str(r)), stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                                  text=True) for r in range(world)]
+        res = None
+        for r, p in enumerate(procs):
+            o, e = p.communicate(timeout=1500)
+            if p.returncode != 0:
+                raise SystemExit(f"world {world} rank {r} failed:\n{e[-3000:]}")
+            for line in o.splitlines():
+                if line.startswith("RESULT "):
+                    res = json.loads(line[7:])
+        print(json.dumps(res), flush=True)
+        out.append(res)
+    print("SUMMARY " + json.dumps([{"world": r["world"], "lr": r["lr"], "cv_acc": [round(e["cv_acc"], 2) for e in r["epochs"]],
+                                     "train_acc": [round(e["train_acc"], 2) for e in r["epochs"]]} for r in out]),
+          flush=True)
+
+
+if __name__ == "__main__":
+    main()
