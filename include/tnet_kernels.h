@@ -278,6 +278,26 @@ int tnet_rnn_out_bwd_update(const float* z, const double* smx, int N, const int*
                             unsigned long long* argkey, int train, void* stream);
 int tnet_argmax_correct(const unsigned long long* keys, const int* labels, int T, int N, double* stats,
                         void* stream);
+/* ---- a whole TRecurrentCu utterance in ONE launch (TRecurrentCu.cc:346-371, the frames' chain above
+ * plus the BPTT GEMVs and the recurrent update): co-resident workgroups keep W (the recurrent
+ * [(nIn + H) x H]) and Wo ([H x N]) in LDS, column slices each, and hand the per-frame vectors to
+ * each other as write-through {tag, value} granules (rnn_persistent.hip).  X [T x nIn] (ld ldx),
+ * labels [T]; W / b / corr_b: the <recurrent> layer (CuRecurrent::Update's lr / mmt / wc); Wo / bo and
+ * their momentum buffers (NULL when ommt == 0): the output <biasedlinearity> (oscale / ol2 of its
+ * UpdateConstants(1)); y [H]: y_{-1} in, y_{T-1} out; stats: cross-entropy into slot 0; argkey [T]
+ * zeroed by the caller (tnet_argmax_correct afterwards); workspace: tnet_rnn_utterance_workspace
+ * bytes, zeroed once; epoch0: grows by >= 16 T + 16 between calls on one workspace; train = 0:
+ * forward + statistics only; *err = 1 if a hand-off wait timed out (2 s).  bptt <= 8;
+ * TNET_ERR_UNSUPPORTED when the weight slices do not fit the LDS of 256 workgroups. */
+long tnet_rnn_utterance_workspace(int H, int N, int G);
+/* diagnostics: later tnet_rnn_utterance launches store workgroup 0's s_memrealtime (100 MHz) at 8
+ * phase points per frame into buf[8 t + k] (NULL: off) */
+int tnet_rnn_utterance_stamps(long long* buf);
+int tnet_rnn_utterance(const float* X, int T, int nIn, int ldx, const int* labels, float* W, int ldw, float* b,
+                       float* corr_b, int H, float* Wo, int ldwo, float* bo, float* corr_Wo, int ldwoc,
+                       float* corr_bo, int N, int bptt, float lr, float mmt, float wc, float oscale, float ommt,
+                       float ol2, float* y, double* stats, unsigned long long* argkey, void* workspace,
+                       unsigned epoch0, int train, int* err, void* stream);
 /* single-frame CuBiasedLinearity::Backpropagate + Update (cuBiasedLinearity.cc:32-64) in one pass
  * over W: e_out = W e (with the weights before the update), then the update of
  * tnet_affine_update_row; with s != NULL also d_out = e_out .* s (1 - s) (the diff-sigmoid of a

@@ -121,6 +121,8 @@ CuRecurrentTrainer::~CuRecurrentTrainer() {
   (void)hipStreamSynchronize(CuDevice::Instantiate().Stream());
   if (mSmx) (void)hipFree(mSmx);
   if (mArgKey) (void)hipFree(mArgKey);
+  if (mXbuf) (void)hipFree(mXbuf);
+  if (mErrFlag) (void)hipFree(mErrFlag);
 }
 
 void* CuRecurrentTrainer::Scratch(void*& p, size_t& have, size_t bytes) {
@@ -150,6 +152,10 @@ void CuRecurrentTrainer::TrainUtterance(const float* feats, size_t rows, size_t 
   for (int i = 0; i < mNet->Layers(); i++)
     if (mNet->Layer(i).GetType() == CuComponent::RECURRENT) dynamic_cast<CuRecurrent&>(mNet->Layer(i)).ClearHistory();
   const bool fused = FusedFrameOk();
+  if (fused && TrainUtterancePersistent(rows)) {
+    mFrames += (long)rows;
+    return;
+  }
   if (fused) {  // per-frame argmax keys of this utterance, read by tnet_argmax_correct at its end
     Scratch(mArgKey, mArgKeyBytes, rows * sizeof(unsigned long long));
     TNET_HIP_CALL(hipMemsetAsync(mArgKey, 0, rows * sizeof(unsigned long long), CuDevice::Instantiate().Stream()));
@@ -169,6 +175,55 @@ void CuRecurrentTrainer::TrainUtterance(const float* feats, size_t rows, size_t 
     TNET_SAFE_CALL(tnet_argmax_correct((const unsigned long long*)mArgKey, mLabels.pCUData(), (int)rows,
                                        (int)mNet->GetNOutputs(), mObj->DeviceStats(), S));
   mFrames += (long)rows;
+}
+
+// TRecurrentCu.cc:346-371 for one utterance in one launch: the frames' forward, cross-entropy,
+// output-layer backprop + SGD, BPTT and recurrent update on workgroups that keep the weights in LDS
+// (rnn_persistent.hip).  Opt-in (TNET_RNN_PERSIST=1): MEASURED SLOWER than the per-frame launch
+// chain (TrainFrameFused) -- 61-62 us a frame vs ~35 us: the seven in-launch hand-offs a frame cost
+// 2.5-6.6 us each (write-through granules polled across XCDs), as much as the launch boundaries they
+// replace (tools/rnn_stamps.py).
+bool CuRecurrentTrainer::TrainUtterancePersistent(size_t rows) {
+  const char* e = getenv("TNET_RNN_PERSIST");
+  if (!e || e[0] != '1') return false;
+  auto& rec = dynamic_cast<CuRecurrent&>(mNet->Layer(0));
+  auto& lin = dynamic_cast<CuBiasedLinearity&>(mNet->Layer(1));
+  const int nIn = (int)rec.GetNInputs(), H = (int)lin.GetNInputs(), N = (int)lin.GetNOutputs();
+  const int bptt = rec.GetBpttOrder();
+  if (bptt < 0 || bptt > 8) return false;
+  hipStream_t st = CuDevice::Instantiate().Stream();
+  Scratch(mArgKey, mArgKeyBytes, rows * sizeof(unsigned long long));
+  TNET_HIP_CALL(hipMemsetAsync(mArgKey, 0, rows * sizeof(unsigned long long), st));
+  const size_t xb = (size_t)tnet_rnn_utterance_workspace(H, N, 256);
+  if (xb > mXbufBytes) {
+    Scratch(mXbuf, mXbufBytes, xb);
+    TNET_HIP_CALL(hipMemsetAsync(mXbuf, 0, xb, st));  // no stale tag can match (tags only grow)
+  }
+  if (!mErrFlag) TNET_HIP_CALL(hipMalloc((void**)&mErrFlag, sizeof(int)));
+  TNET_HIP_CALL(hipMemsetAsync(mErrFlag, 0, sizeof(int), st));
+  rec.Output().Init(1, (size_t)H);  // y_{-1}: zero after ClearHistory
+  float oscale, ol2;
+  lin.UpdateConstants(1, &oscale, &ol2);
+  const bool ommt = lin.Momentum() != 0.0f;
+  const int stt = tnet_rnn_utterance(
+      mFeats.pCUData(), (int)rows, nIn, (int)mFeats.Stride(), mLabels.pCUData(), rec.Linearity().pCUData(),
+      (int)rec.Linearity().Stride(), rec.Bias().pCUData(), rec.BiasCorrection().pCUData(), H,
+      lin.Linearity().pCUData(), (int)lin.Linearity().Stride(), lin.Bias().pCUData(),
+      ommt ? lin.LinearityCorrection().pCUData() : nullptr, (int)lin.LinearityCorrection().Stride(),
+      ommt ? lin.BiasCorrection().pCUData() : nullptr, N, bptt, rec.LearnRate(), rec.Momentum(), rec.Weightcost(),
+      oscale, lin.Momentum(), ol2, rec.Output().pCUData(), mObj->DeviceStats(), (unsigned long long*)mArgKey,
+      mXbuf, mEpoch, mCrossval ? 0 : 1, mErrFlag, st);
+  if (stt == TNET_ERR_UNSUPPORTED) return false;
+  TNET_SAFE_CALL(stt);
+  mEpoch += 16u * (unsigned)rows + 16u;
+  TNET_SAFE_CALL(tnet_argmax_correct((const unsigned long long*)mArgKey, mLabels.pCUData(), (int)rows, N,
+                                     mObj->DeviceStats(), st));
+  mObj->AddFrames(rows);
+  int err = 0;
+  TNET_HIP_CALL(hipMemcpyAsync(&err, mErrFlag, sizeof(int), hipMemcpyDeviceToHost, st));
+  TNET_HIP_CALL(hipStreamSynchronize(st));
+  if (err) Error("CuRecurrentTrainer: persistent utterance kernel timed out waiting for a workgroup hand-off");
+  return true;
 }
 
 bool CuRecurrentTrainer::FusedFrameOk() const {

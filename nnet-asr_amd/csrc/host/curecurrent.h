@@ -51,6 +51,7 @@ class CuRecurrent : public CuUpdatableComponent {
 
   CuMatrix<BaseFloat>& Linearity() { return mLinearity; }  ///< [(nIn + nOut) x nOut]
   CuVector<BaseFloat>& Bias() { return mBias; }
+  CuVector<BaseFloat>& BiasCorrection() { return mBiasCorrection; }
 
  private:
   const float* HistRow(int i) const {  // logical history row i (0 = present)
@@ -91,6 +92,12 @@ class CuRecurrentTrainer {
   void* mArgKey = nullptr;
   size_t mArgKeyBytes = 0;
   void* Scratch(void*& p, size_t& have, size_t bytes);
+  // the whole utterance as one persistent launch (tnet_rnn_utterance); false: not applicable
+  bool TrainUtterancePersistent(size_t rows);
+  void* mXbuf = nullptr;
+  size_t mXbufBytes = 0;
+  int* mErrFlag = nullptr;
+  unsigned mEpoch = 0;
 
  public:
   ~CuRecurrentTrainer();

@@ -175,6 +175,10 @@ _SIGS = {
     "tnet_rnn_out_bwd_update": (i32, [vp, vp, i32, vp, vp, i32, vp, i32, vp, i32, vp, vp, f32, f32, f32, vp, vp, vp,
                                       vp, vp, vp, i32, vp]),
     "tnet_argmax_correct": (i32, [vp, vp, i32, i32, vp, vp]),
+    "tnet_rnn_utterance_workspace": (C.c_long, [i32, i32, i32]),
+    "tnet_rnn_utterance_stamps": (i32, [vp]),
+    "tnet_rnn_utterance": (i32, [vp, i32, i32, i32, vp, vp, i32, vp, vp, i32, vp, i32, vp, vp, i32, vp, i32, i32, f32,
+                                 f32, f32, f32, f32, f32, vp, vp, vp, vp, C.c_uint, i32, vp, vp]),
     "tnetF_rand": (i32, [vp, MatrixDim, vp, vp, vp, vp, vp]),
     "tnetF_gauss_rand": (i32, [vp, MatrixDim, vp, vp, vp, vp, vp]),
     "tnetF_binarize_probs": (i32, [vp, vp, vp, MatrixDim, vp]),

@@ -67,9 +67,12 @@ def test_recurrent_text_round_trip(tmp_path):
     np.testing.assert_allclose(back[0].W, layers[0].W, rtol=1e-5, atol=1e-7)
 
 
+@pytest.mark.parametrize("persistent", ["0", "1"])
 @pytest.mark.parametrize("bptt,mmt,wc", [(4, 0.0, 0.0), (2, 0.5, 1e-4), (0, 0.0, 0.0)])
-def test_rnn_trainer_matches_oracle(bptt, mmt, wc):
-    """Two utterances through TRecurrentCu semantics (history reset per utterance)."""
+def test_rnn_trainer_matches_oracle(bptt, mmt, wc, persistent, monkeypatch):
+    """Two utterances through TRecurrentCu semantics (history reset per utterance); the per-frame
+    launch chain and the opt-in one-launch utterance kernel (TNET_RNN_PERSIST=1)."""
+    monkeypatch.setenv("TNET_RNN_PERSIST", persistent)
     nIn, H, Sd, lr = 24, 32, 10, 0.05
     rng = np.random.default_rng(bptt)
     layers = formats.round_trip_text(formats.gen_recurrent_init(nIn, H, Sd, seed=7), 9)
@@ -97,8 +100,9 @@ def test_rnn_trainer_matches_oracle(bptt, mmt, wc):
     np.testing.assert_allclose(b2, m.b2, rtol=2e-3, atol=2e-5)
 
 
-def _train_rnn(layers, feats, labels, bptt, lr, mmt, wc, generic, crossval=False):
+def _train_rnn(layers, feats, labels, bptt, lr, mmt, wc, generic, crossval=False, persistent=False):
     os.environ["TNET_RNN_GENERIC"] = "1" if generic else "0"
+    os.environ["TNET_RNN_PERSIST"] = "1" if persistent else "0"
     try:
         net = Network.from_layers(layers)
         net.set_learn_rate(lr)
@@ -109,20 +113,23 @@ def _train_rnn(layers, feats, labels, bptt, lr, mmt, wc, generic, crossval=False
         return obj.stats(), net.recurrent_params(0), net.linear_params()[0]
     finally:
         os.environ.pop("TNET_RNN_GENERIC", None)
+        os.environ.pop("TNET_RNN_PERSIST", None)
 
 
+@pytest.mark.parametrize("persistent", [True, False])
 @pytest.mark.parametrize("S,bptt,mmt,wc", [(10, 4, 0.0, 0.0), (135, 2, 0.5, 1e-4), (4000, 4, 0.9, 0.0),
-                                           (37, 0, 0.0, 1e-3)])
-def test_rnn_fused_frame_matches_component_chain(S, bptt, mmt, wc):
-    """the fused single-frame chain (8 launches) vs the component-by-component chain (Propagate,
-    EvaluateLabels, Backpropagate + Update per layer) on the same utterances"""
+                                           (37, 0, 0.0, 1e-3), (135, 8, 0.0, 0.0)])
+def test_rnn_fused_frame_matches_component_chain(S, bptt, mmt, wc, persistent):
+    """the fused paths -- the whole utterance as one persistent launch (tnet_rnn_utterance) or the
+    per-frame launch chain -- vs the component-by-component chain (Propagate, EvaluateLabels,
+    Backpropagate + Update per layer) on the same utterances"""
     nIn, H, lr = 40, 64, 0.02
     rng = np.random.default_rng(S)
     layers = formats.gen_recurrent_init(nIn, H, S, seed=11)
     feats = [rng.standard_normal((T, nIn)).astype(np.float32) for T in (50, 33)]
     labels = [rng.integers(0, S, len(f)).astype(np.int32) for f in feats]
     labels[1][::9] = -1  # unlabeled frames: zero target
-    a = _train_rnn(layers, feats, labels, bptt, lr, mmt, wc, generic=False)
+    a = _train_rnn(layers, feats, labels, bptt, lr, mmt, wc, generic=False, persistent=persistent)
     b = _train_rnn(layers, feats, labels, bptt, lr, mmt, wc, generic=True)
     (ea, fa, ca), (eb, fb, cb) = a[0], b[0]
     assert fa == fb == 83
@@ -132,13 +139,15 @@ def test_rnn_fused_frame_matches_component_chain(S, bptt, mmt, wc):
         np.testing.assert_allclose(x, y, rtol=1e-4, atol=1e-6)
 
 
-def test_rnn_fused_crossval_leaves_weights():
+@pytest.mark.parametrize("persistent", [False, True])
+def test_rnn_fused_crossval_leaves_weights(persistent):
     nIn, H, S = 24, 32, 10
     rng = np.random.default_rng(5)
     layers = formats.gen_recurrent_init(nIn, H, S, seed=3)
     feats = [rng.standard_normal((40, nIn)).astype(np.float32)]
     labels = [rng.integers(0, S, 40).astype(np.int32)]
-    (e, f, c), (Wr, br), (W2, b2) = _train_rnn(layers, feats, labels, 4, 0.05, 0.0, 0.0, False, crossval=True)
+    (e, f, c), (Wr, br), (W2, b2) = _train_rnn(layers, feats, labels, 4, 0.05, 0.0, 0.0, False, crossval=True,
+                                                  persistent=persistent)
     (e2, f2, c2), _, _ = _train_rnn(layers, feats, labels, 4, 0.05, 0.0, 0.0, True, crossval=True)
     assert f == f2 == 40 and c == c2
     np.testing.assert_allclose(e, e2, rtol=1e-5)
