@@ -185,6 +185,17 @@ int tnet_affine_bwd_colsum(const float* E, TnetMatrixDim dE, const float* W, Tne
  * count; the slabs are disjoint row ranges (32 rows when rows % 32 == 0) whose sum is colsum(E), which
  * is all tnet_affine_update_bias / tnet_affine_grad_bias use.  TNET_ERR_UNSUPPORTED above 8192 rows. */
 int tnet_colsum_slab_sums(const float* E, TnetMatrixDim dE, float* colpart, int ldcolpart, void* stream);
+/* The top layer for n_out <= TNET_AFFINE_SOFTMAX_MAX_N classes in two launches (the GEMM's K slices, then one workgroup per
+ * 32-row slab): Z = X W + b (written when Z != NULL), Y = softmax(Z) (when Y != NULL), E = Y - onehot,
+ * the statistics of tnet_softmax_xent, and (colpart != NULL) E's slab column sums for
+ * tnet_affine_update_bias -- tnet_affine_fwd(act 0) + tnet_softmax_xent + tnet_colsum_slab_sums with
+ * the same Z, Y, E per element (CuBiasedLinearity::PropagateFnc + CuSoftmax::PropagateFnc +
+ * CuCrossEntropy::Evaluate, cuBiasedLinearity.cc:11-16, cuActivation.cc:28-31,
+ * cuObjectiveFunction.cc:50-83).  TNET_ERR_UNSUPPORTED for more classes (use the three calls). */
+#define TNET_AFFINE_SOFTMAX_MAX_N 256
+int tnet_affine_softmax_xent(const float* X, TnetMatrixDim dX, const float* W, TnetMatrixDim dW, const float* b,
+                             const int* labels, float* Z, int strideZ, float* Y, int strideY, float* E, int strideE,
+                             double* stats, float* colpart, int ldcolpart, void* stream);
 /* tnet_affine_update + tnet_bias_update(E, b, corr_b, scale, mmt) in one launch, colsum(E) taken from
  * colpart (written for E by tnet_affine_bwd_colsum); corr_b is required when mmt != 0
  * (cuBiasedLinearity.cc:46-64). */

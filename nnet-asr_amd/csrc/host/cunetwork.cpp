@@ -262,25 +262,7 @@ void CuNetwork::TrainBunch(const CuMatrix<BaseFloat>& X, const CuVector<int>& la
   }
   mNetComponents.front()->SetInput(X);
 
-  // ---- forward: act_{l+1} = sigmoid(act_l W_l + b_l) straight into the <sigmoid>'s output
-  const CuMatrix<BaseFloat>* act = &X;
-  std::vector<const CuMatrix<BaseFloat>*> acts(nl + 1);
-  acts[0] = &X;
-  for (int l = 0; l < nl; l++) {
-    auto* lin = static_cast<CuBiasedLinearity*>(mNetComponents[2 * l]);
-    CuComponent* actc = mNetComponents[2 * l + 1];
-    const bool last = (l == nl - 1);
-    CuMatrix<BaseFloat>& dst = last ? lin->Output() : actc->Output();
-    dst.Init(rows, lin->GetNOutputs());
-    const std::string shape = std::to_string(lin->GetNInputs()) + "x" + std::to_string(lin->GetNOutputs());
-    KTScope kt("gemm_fwd:" + shape, 2.0 * rows * lin->GetNInputs() * lin->GetNOutputs());
-    TNET_SAFE_CALL(tnet_affine_fwd(act->pCUData(), act->Dim(), lin->Linearity().pCUData(), lin->Linearity().Dim(),
-                                   lin->Bias().pCUData(), dst.pCUData(), dst.Dim(), last ? 0 : 1, S));
-    act = &dst;
-    acts[l + 1] = &dst;
-  }
-  // ---- objective: softmax + xent + error (+ optional softmax output)
-  CuMatrix<BaseFloat>& logits = mNetComponents[2 * (nl - 1)]->Output();
+  // objective outputs: the error (+ the softmax output when kept)
   CuComponent* smx = mNetComponents.back();
   float* yout = nullptr;
   int ystride = 0;
@@ -290,7 +272,56 @@ void CuNetwork::TrainBunch(const CuMatrix<BaseFloat>& X, const CuVector<int>& la
     ystride = (int)smx->Output().Stride();
   }
   mGlobErr.Init(rows, GetNOutputs());
-  {
+  // the top layer's bias gradient as slab sums (the update GEMM applies it)
+  auto* top = static_cast<CuBiasedLinearity*>(mNetComponents[2 * (nl - 1)]);
+  const bool top_colsum = train && top->LearnRate() > 0.0f;
+  bool err_colsum = false;
+
+  // ---- forward: act_{l+1} = sigmoid(act_l W_l + b_l) straight into the <sigmoid>'s output
+  const CuMatrix<BaseFloat>* act = &X;
+  std::vector<const CuMatrix<BaseFloat>*> acts(nl + 1);
+  acts[0] = &X;
+  bool fused_top = false;
+  for (int l = 0; l < nl; l++) {
+    auto* lin = static_cast<CuBiasedLinearity*>(mNetComponents[2 * l]);
+    CuComponent* actc = mNetComponents[2 * l + 1];
+    const bool last = (l == nl - 1);
+    CuMatrix<BaseFloat>& dst = last ? lin->Output() : actc->Output();
+    dst.Init(rows, lin->GetNOutputs());
+    const std::string shape = std::to_string(lin->GetNInputs()) + "x" + std::to_string(lin->GetNOutputs());
+    // TNET_FUSED_TOP=0: the three-call form (A/B measurements)
+    static const bool fuse_top = !(getenv("TNET_FUSED_TOP") && getenv("TNET_FUSED_TOP")[0] == '0');
+    if (last && fuse_top && lin->GetNOutputs() <= TNET_AFFINE_SOFTMAX_MAX_N) {
+      // up to 256 classes: logits, softmax, xent, error and the error's slab sums in one pass
+      float* cp = nullptr;
+      int ldcp = 0;
+      if (top_colsum) {
+        mColPart[l]->Init(tnet_colsum_slabs((int)rows), lin->GetNOutputs());
+        cp = mColPart[l]->pCUData();
+        ldcp = (int)mColPart[l]->Stride();
+      }
+      KTScope kt("gemm_fwd+softmax:" + shape, 2.0 * rows * lin->GetNInputs() * lin->GetNOutputs());
+      const int st = tnet_affine_softmax_xent(act->pCUData(), act->Dim(), lin->Linearity().pCUData(),
+                                              lin->Linearity().Dim(), lin->Bias().pCUData(), labels.pCUData(),
+                                              dst.pCUData(), (int)dst.Stride(), yout, ystride, mGlobErr.pCUData(),
+                                              (int)mGlobErr.Stride(), obj.DeviceStats(), cp, ldcp, S);
+      if (st != TNET_ERR_UNSUPPORTED) {
+        TNET_SAFE_CALL(st);
+        fused_top = true;
+        err_colsum = top_colsum;
+        acts[l + 1] = &dst;
+        break;
+      }
+    }
+    KTScope kt("gemm_fwd:" + shape, 2.0 * rows * lin->GetNInputs() * lin->GetNOutputs());
+    TNET_SAFE_CALL(tnet_affine_fwd(act->pCUData(), act->Dim(), lin->Linearity().pCUData(), lin->Linearity().Dim(),
+                                   lin->Bias().pCUData(), dst.pCUData(), dst.Dim(), last ? 0 : 1, S));
+    act = &dst;
+    acts[l + 1] = &dst;
+  }
+  // ---- objective: softmax + xent + error (+ optional softmax output)
+  if (!fused_top) {
+    CuMatrix<BaseFloat>& logits = mNetComponents[2 * (nl - 1)]->Output();
     KTScope kts("softmax_xent:" + std::to_string(GetNOutputs()),
                 (double)rows * GetNOutputs() * 4.0 * (mKeepOutput ? 3 : 2) + rows * 4.0);
     TNET_SAFE_CALL(tnet_softmax_xent(logits.pCUData(), logits.Dim(), labels.pCUData(), yout, ystride,
@@ -304,19 +335,14 @@ void CuNetwork::TrainBunch(const CuMatrix<BaseFloat>& X, const CuVector<int>& la
   std::vector<CuBiasedLinearity*> submitted;  // data-parallel: layers in reduction order, not yet applied
   const size_t grows = exchange ? exchange->GlobalRows(rows) : rows;
   int n_submitted = 0;
-  bool err_colsum = false;
-  {
-    // the top layer's bias gradient as slab sums too (one launch; the update GEMM applies it)
-    auto* top = static_cast<CuBiasedLinearity*>(mNetComponents[2 * (nl - 1)]);
-    if (top->LearnRate() > 0.0f) {
-      CuMatrix<BaseFloat>& cp = *mColPart[nl - 1];
-      cp.Init(tnet_colsum_slabs((int)rows), GetNOutputs());
-      KTScope kt("colsum:" + std::to_string(GetNOutputs()), 4.0 * rows * GetNOutputs());
-      const int st = tnet_colsum_slab_sums(mGlobErr.pCUData(), mGlobErr.Dim(), cp.pCUData(), (int)cp.Stride(), S);
-      if (st != TNET_ERR_UNSUPPORTED) {
-        TNET_SAFE_CALL(st);
-        err_colsum = true;
-      }
+  if (top_colsum && !fused_top) {
+    CuMatrix<BaseFloat>& cp = *mColPart[nl - 1];
+    cp.Init(tnet_colsum_slabs((int)rows), GetNOutputs());
+    KTScope kt("colsum:" + std::to_string(GetNOutputs()), 4.0 * rows * GetNOutputs());
+    const int st = tnet_colsum_slab_sums(mGlobErr.pCUData(), mGlobErr.Dim(), cp.pCUData(), (int)cp.Stride(), S);
+    if (st != TNET_ERR_UNSUPPORTED) {
+      TNET_SAFE_CALL(st);
+      err_colsum = true;
     }
   }  // slab column sums of *err are in mColPart[l] (bias gradient fused, no exchange)
   for (int l = nl - 1; l >= 0; l--) {

@@ -23,6 +23,8 @@
 //    tile-rows, column-major inside a group), so the ~64 workgroups resident on one XCD cover a
 //    square-ish block of C and its L2 holds few A and B panels;
 //  * the whole epilogue (bias, sigmoid, diff-sigmoid, momentum-SGD) is fused into the stores.
+#include <float.h>
+
 #include <cstdlib>
 #include <cstring>
 #include <map>
@@ -1274,12 +1276,25 @@ void gemm16_kernel(const GemmP p_in) {
 // split-K combine: C = epilogue(P[0] + P[1] + ... + P[splits-1]) summed in split order (fixed, so the
 // result is deterministic), then the same epilogue arithmetic as gemm16_kernel; 4 columns / thread
 // ---------------------------------------------------------------------------------------------
-constexpr bool epi_splittable(int e) { return e != EPI_DSIG_CS && !epi_bias_slabs(e); }
+constexpr bool epi_splittable(int e) { return e != EPI_DSIG_CS; }
 constexpr int kMaxSplit = 8;
 
-template <int EPI>
+template <int EPI_FULL>
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(const GemmP p, const float* __restrict__ P, long slab,
-                                                            int splits, int ldp) {
+                                                            int splits, int ldp, unsigned main_blocks) {
+  if constexpr (epi_bias_slabs(EPI_FULL)) {
+    // EPI_SGD_B / EPI_STORE_BG: the trailing workgroups update (or store) the bias, a column per
+    // thread, with the fused epilogue's own arithmetic (bias_pre_load / bias_pre_finish)
+    if (blockIdx.x >= main_blocks) {
+      constexpr bool GRAD = EPI_FULL == EPI_STORE_BG;
+      const int bn = (int)(blockIdx.x - main_blocks) * 256;
+      BiasPre bp;
+      bias_pre_load<256, GRAD>(p, bn, bp);
+      bias_pre_finish<256, GRAD>(p, bn, bp);
+      return;
+    }
+  }
+  constexpr int EPI = epi_base(EPI_FULL);
   const int N4 = (p.N + 3) >> 2;
   const long i = (long)blockIdx.x * 256 + threadIdx.x;
   if (i >= (long)p.M * N4) return;
@@ -1328,6 +1343,137 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const GemmP p, const
       cp[e] = w;
     }
   }
+}
+
+// ---------------------------------------------------------------------------------------------
+// The top layer of a TNet MLP for at most 256 classes (BASELINE config 2's 135 senones): the
+// GEMM's slices combined with the bias into the logits, softmax + cross-entropy + error + frame
+// accuracy per row, and the error's 32-row slab column sums (the top layer's bias gradient), in ONE
+// workgroup per slab -- replacing splitk_reduce_kernel<EPI_BIAS> + softmax_xent_kernel +
+// colsum_partial_kernel (tnet_affine_fwd, tnet_softmax_xent, tnet_colsum_slab_sums).
+//   * logits: the slices added in slice order, then + bias (splitk_reduce_kernel's arithmetic);
+//   * softmax row: softmax_xent_kernel's arithmetic and lane-to-column map (4 contiguous columns a
+//     lane when v4, else columns lane + 64 j), so Y / E / the statistics per row are its values;
+//   * slab sums: fp32 over the slab's rows in row order (a thread per column).
+// ---------------------------------------------------------------------------------------------
+constexpr int kSxMaxN = TNET_AFFINE_SOFTMAX_MAX_N;
+constexpr int kSxThreads = 1024;  // 16 waves, 2 rows each
+constexpr int kSxPer = kColsumSlabRows * (kSxMaxN / 4) / kSxThreads;  // float4 logits per thread
+__global__ __launch_bounds__(kSxThreads) void affine_softmax_xent_kernel(
+    const GemmP p, const float* __restrict__ P, long slab, int splits, int ldp, const int* __restrict__ labels,
+    float* __restrict__ Z, long ldz, float* __restrict__ Y, long ldy, float* __restrict__ E, long lde,
+    double* __restrict__ stats, float* __restrict__ cpart, long ldcpart, int v4) {
+  constexpr int NW = kSxThreads / 64;
+  __shared__ __attribute__((aligned(16))) float zs[kColsumSlabRows * kSxMaxN];
+  __shared__ int s_lab[kColsumSlabRows];
+  __shared__ double red[2][NW];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int N = p.N, r0 = blockIdx.x * kColsumSlabRows, nr = min(kColsumSlabRows, p.M - r0);
+  if (tid < nr) s_lab[tid] = labels[r0 + tid];
+  // ---- logits of the slab into LDS (and Z): every slice's loads of a thread in flight together
+  const int N4 = (N + 3) >> 2, n = nr * N4;
+  f32x4 v[kSxPer], bv[kSxPer];
+#pragma unroll
+  for (int k = 0; k < kSxPer; ++k) {
+    const int i = min(tid + kSxThreads * k, n - 1), r = i / N4, c = (i % N4) * 4;
+    v[k] = *reinterpret_cast<const f32x4*>(P + (long)(r0 + r) * ldp + c);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) bv[k][e] = c + e < N ? p.bias[c + e] : 0.f;
+  }
+  for (int z = 1; z < splits; ++z) {
+    f32x4 t[kSxPer];
+#pragma unroll
+    for (int k = 0; k < kSxPer; ++k) {
+      const int i = min(tid + kSxThreads * k, n - 1), r = i / N4, c = (i % N4) * 4;
+      t[k] = *reinterpret_cast<const f32x4*>(P + (long)z * slab + (long)(r0 + r) * ldp + c);
+    }
+#pragma unroll
+    for (int k = 0; k < kSxPer; ++k)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[k][e] = v[k][e] + t[k][e];
+  }
+#pragma unroll
+  for (int k = 0; k < kSxPer; ++k) {
+    const int i = tid + kSxThreads * k;
+    if (i >= n) break;
+    const int r = i / N4, c = (i % N4) * 4;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      if (c + e >= N) break;
+      const float y = v[k][e] + bv[k][e];
+      zs[r * kSxMaxN + c + e] = y;
+      if (Z) Z[(long)(r0 + r) * ldz + c + e] = y;
+    }
+  }
+  __syncthreads();
+  // ---- softmax / xent / error, a wave per row (rows wv, wv + NW, ...)
+  double wx = 0.0, wc = 0.0;
+  for (int r = wv; r < nr; r += NW) {
+    float* zr = zs + r * kSxMaxN;
+    const long row = r0 + r;
+    int t = s_lab[r];
+    if (t >= N) t = -1;  // unlabeled (the host intake rejects such a label, CheckLabels)
+    float x[4];
+    int cl[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      cl[j] = v4 ? 4 * lane + j : lane + 64 * j;
+      x[j] = cl[j] < N ? zr[cl[j]] : -1e30f;
+    }
+    const float zt = t >= 0 ? zr[t] : 0.f;
+    float m = -1e20f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (cl[j] < N) m = fmaxf(m, x[j]);
+    m = wave_max(m);
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (cl[j] < N) {
+        x[j] = fast_exp(x[j] - m);
+        s += x[j];
+      }
+    const float rsum = 1.f / (float)wave_sum_d((double)s);
+    ArgMax ay{-1e20f, 0x7fffffff};
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (cl[j] < N) {
+        const float y = x[j] * rsum;
+        if (y > ay.v) { ay.v = y; ay.i = cl[j]; }
+        const float e = y - (cl[j] == t ? 1.f : 0.f);
+        if (Y) Y[row * ldy + cl[j]] = y;
+        E[row * lde + cl[j]] = e;
+        zr[cl[j]] = e;  // every lane has read its logits and zt above
+      }
+    ay = wave_argmax(ay);
+    if (lane == 0) {
+      if (t >= 0) wx += -(double)logf(fmaxf(fast_exp(zt - m) * rsum, FLT_MIN));
+      wc += ay.i == (t >= 0 ? t : 0) ? 1.0 : 0.0;
+    }
+  }
+  if (lane == 0) {
+    red[0][wv] = wx;
+    red[1][wv] = wc;
+  }
+  __syncthreads();
+  if (tid == 0 && stats) {
+    double sx = 0.0, sc = 0.0;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+      sx += red[0][w];
+      sc += red[1][w];
+    }
+    const int slot = blockIdx.x % TNET_STATS_SLOTS;
+    atomicAdd(stats + 2 * slot, sx);
+    atomicAdd(stats + 2 * slot + 1, sc);
+  }
+  // ---- the slab's column sums of the error
+  if (cpart)
+    for (int c = tid; c < N; c += kSxThreads) {
+      float a = 0.f;
+      for (int r = 0; r < nr; ++r) a += zs[r * kSxMaxN + c];
+      cpart[(long)blockIdx.x * ldcpart + c] = a;
+    }
 }
 
 // per-stream partial-product workspace of the split-K path (grown on demand; the library enqueues
@@ -1437,8 +1583,15 @@ static void cfg_shape(int cfg, int* bm, int* bn, int* kind) {
 
 // split-K: the K range is cut into ks slices (blockIdx.y) whose partial products go to the stream's
 // workspace; splitk_reduce_kernel adds them in slice order and applies the epilogue
-template <bool A_KC, bool B_KC, int EPI>
-static int launch_splitk(const GemmP& p, int cfg, int ks, hipStream_t st) {
+// the ks slices' raw products A B (no epilogue) into the stream's workspace: slice z at ws + z * slab,
+// rows of ldp = N rounded up to 4 floats
+struct Partials {
+  float* ws;
+  long slab;
+  int ldp;
+};
+template <bool A_KC, bool B_KC>
+static int launch_partials(const GemmP& p, int cfg, int ks, hipStream_t st, Partials* out) {
   const int ldp = (p.N + 3) & ~3;
   const long slab = (long)p.M * ldp;
   float* ws = splitk_workspace(sizeof(float) * (size_t)slab * ks, st);
@@ -1463,32 +1616,51 @@ static int launch_splitk(const GemmP& p, int cfg, int ks, hipStream_t st) {
   }
   if (!ok) return TNET_ERR_UNSUPPORTED;
   TNET_LAUNCH_CHECK();
-  const long n = (long)p.M * ((p.N + 3) >> 2);
-  splitk_reduce_kernel<EPI><<<(unsigned)cdiv(n, 256), 256, 0, st>>>(p, ws, slab, ks, ldp);
-  TNET_LAUNCH_CHECK();
-  return TNET_OK;
-}
-
-// bwd GEMM + diff-sigmoid + column sums: one fixed 64x128 16x16 config (32-row wave tiles = slabs)
-static int launch_colsum_bwd(const GemmP& p_in, hipStream_t st) {
-  if (p_in.M <= 0 || p_in.N <= 0) return TNET_OK;
-  forced_cfg();
-  GemmP p = p_in;
-  p.group = g_group > 0 ? g_group : 8;
-  if (!launch_cfg<1, 64, 128, 64, 2, 2, 2, 0, true, true, EPI_DSIG_CS>(p, st)) return TNET_ERR_UNSUPPORTED;
-  TNET_LAUNCH_CHECK();
+  *out = Partials{ws, slab, ldp};
   return TNET_OK;
 }
 
 template <bool A_KC, bool B_KC, int EPI>
-static int launch_gemm(const GemmP& p_in, hipStream_t st) {
-  if constexpr (EPI == EPI_DSIG_CS) {
-    return launch_colsum_bwd(p_in, st);
-  } else {
+static int launch_splitk(const GemmP& p, int cfg, int ks, hipStream_t st) {
+  Partials pt;
+  const int rc = launch_partials<A_KC, B_KC>(p, cfg, ks, st, &pt);
+  if (rc) return rc;
+  float* ws = pt.ws;
+  const long slab = pt.slab;
+  const int ldp = pt.ldp;
+  const long n = (long)p.M * ((p.N + 3) >> 2);
+  const unsigned main_blocks = (unsigned)cdiv(n, 256);
+  const unsigned bias_blocks = epi_bias_slabs(EPI) ? (unsigned)cdiv(p.N, 256) : 0u;
+  splitk_reduce_kernel<EPI><<<main_blocks + bias_blocks, 256, 0, st>>>(p, ws, slab, ks, ldp, main_blocks);
+  TNET_LAUNCH_CHECK();
+  return TNET_OK;
+}
+
+// bwd GEMM + diff-sigmoid + column sums: 16x16 configs with 32-row wave tiles (= slabs); 64x128 where
+// that gives ~one workgroup per CU, else 64x64 (MLP3's 1024 x 1024 over K = 135: 128 tiles of 64x128)
+static int launch_colsum_bwd(const GemmP& p_in, hipStream_t st) {
   if (p_in.M <= 0 || p_in.N <= 0) return TNET_OK;
-  static const int noload = getenv("TNET_GEMM_DIAG") ? atoi(getenv("TNET_GEMM_DIAG")) : 0;
+  int cfg = forced_cfg();
   GemmP p = p_in;
-  p.diag_noload = noload;
+  p.group = g_group > 0 ? g_group : 8;
+  if (cfg != CFG_m64x128k64s2 && cfg != CFG_m64x64k32s4 && cfg != CFG_m64x64k64s2)
+    cfg = (long)cdiv(p.M, 64) * cdiv(p.N, 128) >= 200 ? CFG_m64x128k64s2 : CFG_m64x64k32s4;
+  bool ok = false;
+  if (cfg == CFG_m64x128k64s2) ok = launch_cfg<1, 64, 128, 64, 2, 2, 2, 0, true, true, EPI_DSIG_CS>(p, st);
+  else if (cfg == CFG_m64x64k64s2) ok = launch_cfg<1, 64, 64, 64, 2, 2, 2, 0, true, true, EPI_DSIG_CS>(p, st);
+  else ok = launch_cfg<1, 64, 64, 32, 2, 2, 4, 0, true, true, EPI_DSIG_CS>(p, st);
+  if (!ok) return TNET_ERR_UNSUPPORTED;
+  TNET_LAUNCH_CHECK();
+  return TNET_OK;
+}
+
+// the configuration and split-K count of a GEMM: the forced ones (TNET_GEMM_CFG / _SPLITK,
+// tnet_gemm_config) or the measured per-shape choice
+struct GemmPlan {
+  int cfg, ks;
+};
+template <bool A_KC>
+static GemmPlan plan_gemm(const GemmP& p, bool splittable) {
   int cfg = forced_cfg();
   if (cfg < 0) {
     // measured per-shape choice (tools/gemm_sweep.py on MI355X, round 1): the largest tile that
@@ -1503,17 +1675,18 @@ static int launch_gemm(const GemmP& p_in, hipStream_t st) {
     else if (t128 >= 240) cfg = CFG_m128x128k64s2;
     else if (A_KC && t64x128 >= 200) cfg = CFG_m64x128k64s2;  // incl. the K = 440 first layer (one round)
     else if (t64 >= 200) cfg = CFG_m64x64k32s4w41;
-    else if (t32x64 >= 128) cfg = CFG_m32x64k64s2;
+    // 32x64 tiles only in the K-contiguous A layout: over the update's [K][M] A they ran 35.5 us where
+    // 64x64 ran 22.4 (MLP3's 598 x 1024 update over K = 1024, round 2)
+    else if (A_KC && t32x64 >= 128) cfg = CFG_m32x64k64s2;
     else cfg = CFG_m64x64k32s4w41;
   }
-  p.group = g_group > 0 ? g_group : 8;
-  if constexpr (epi_splittable(EPI)) {
+  int ks = 1;
+  if (splittable) {
     // split-K where few output tiles meet a long K (the RBM reconstruction 256 x 440 over K = 2048:
     // 28 tiles of 64x64 for 256 CUs)
     int tbm, tbn, kind;
     cfg_shape(cfg, &tbm, &tbn, &kind);
     const long tiles = (long)cdiv(p.M, tbm) * cdiv(p.N, tbn);
-    int ks = 1;
     if (g_split > 0) {
       ks = g_split < kMaxSplit ? g_split : kMaxSplit;
     } else if (tiles < 100 && p.K >= 1024) {
@@ -1527,8 +1700,24 @@ static int launch_gemm(const GemmP& p_in, hipStream_t st) {
       }
     }
     while (ks > 1 && (p.K % (4 * ks) != 0 || p.K / ks < 64)) ks /= 2;
-    if (ks > 1) return launch_splitk<A_KC, B_KC, EPI>(p, kind == 1 ? cfg : CFG_m64x64k32s4w41, ks, st);
+    if (ks > 1 && kind != 1) cfg = CFG_m64x64k32s4w41;  // slices: 16x16 kernel only
   }
+  return GemmPlan{cfg, ks};
+}
+
+template <bool A_KC, bool B_KC, int EPI>
+static int launch_gemm(const GemmP& p_in, hipStream_t st) {
+  if constexpr (EPI == EPI_DSIG_CS) {
+    return launch_colsum_bwd(p_in, st);
+  } else {
+  if (p_in.M <= 0 || p_in.N <= 0) return TNET_OK;
+  static const int noload = getenv("TNET_GEMM_DIAG") ? atoi(getenv("TNET_GEMM_DIAG")) : 0;
+  GemmP p = p_in;
+  p.diag_noload = noload;
+  const GemmPlan pl = plan_gemm<A_KC>(p, epi_splittable(EPI));
+  const int cfg = pl.cfg;
+  p.group = g_group > 0 ? g_group : 8;
+  if (pl.ks > 1) return launch_splitk<A_KC, B_KC, EPI>(p, cfg, pl.ks, st);
   bool ok = false;
   switch (cfg) {
 #define X(name, KIND, BM, BN, BK, WM, WN, S, IL) \
@@ -1606,6 +1795,42 @@ extern "C" int tnet_affine_fwd_t(const float* X, TnetMatrixDim dX, const float* 
   if (st) return st;
   if (act == 1) return launch_gemm<true, true, EPI_BIAS_SIG>(p, (hipStream_t)stream);
   return launch_gemm<true, true, EPI_BIAS>(p, (hipStream_t)stream);
+}
+
+extern "C" int tnet_affine_softmax_xent(const float* X, TnetMatrixDim dX, const float* W, TnetMatrixDim dW,
+                                        const float* b, const int* labels, float* Z, int strideZ, float* Y,
+                                        int strideY, float* E, int strideE, double* stats, float* colpart,
+                                        int ldcolpart, void* stream) {
+  // the top <biasedlinearity> + <softmax> + cross-entropy for n_out <= 256: Z = X W + b (nullable),
+  // Y = softmax(Z) (nullable), E = Y - onehot(labels), stats, and (colpart non-null) E's 32-row slab
+  // column sums -- tnet_affine_fwd(act 0) + tnet_softmax_xent + tnet_colsum_slab_sums in two launches
+  if (dX.cols != dW.rows || !b || !labels || !E || dX.rows < 0 || strideE < dW.cols || (Z && strideZ < dW.cols) ||
+      (Y && strideY < dW.cols) || (colpart && ldcolpart < dW.cols))
+    return TNET_ERR_ARG;
+  if (dW.cols > kSxMaxN) return TNET_ERR_UNSUPPORTED;
+  if (dX.rows == 0 || dW.cols == 0) return TNET_OK;
+  GemmP p{};
+  p.M = dX.rows; p.N = dW.cols; p.K = dX.cols;
+  p.A = X; p.lda = dX.stride; p.B = W; p.ldb = dW.stride;  // C: the slices' workspace
+  p.bias = b;
+  int st = check_common(p);
+  if (st) return st;
+  hipStream_t s = (hipStream_t)stream;
+  const GemmPlan pl = plan_gemm<true>(p, true);
+  int cfg = pl.cfg, bm, bn, kind;
+  cfg_shape(cfg, &bm, &bn, &kind);
+  if (kind != 1) cfg = CFG_m64x64k32s4w41;  // slices: 16x16 kernel only
+  p.group = g_group > 0 ? g_group : 8;
+  Partials pt;
+  st = launch_partials<true, false>(p, cfg, pl.ks, s, &pt);
+  if (st) return st;
+  // softmax_xent_kernel's lane-to-column map: the 16-byte one where its launch would use it
+  const int v4 = (p.N & 3) == 0 && (!Z || (aligned16(Z) && (strideZ & 3) == 0)) &&
+                 (!Y || (aligned16(Y) && (strideY & 3) == 0)) && aligned16(E) && (strideE & 3) == 0;
+  affine_softmax_xent_kernel<<<(unsigned)cdiv(p.M, kColsumSlabRows), kSxThreads, 0, s>>>(
+      p, pt.ws, pt.slab, pl.ks, pt.ldp, labels, Z, strideZ, Y, strideY, E, strideE, stats, colpart, ldcolpart, v4);
+  TNET_LAUNCH_CHECK();
+  return TNET_OK;
 }
 
 extern "C" int tnet_rbm_update(const float* V, TnetMatrixDim dV, const float* H, TnetMatrixDim dH, float* W,

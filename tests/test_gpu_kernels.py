@@ -139,10 +139,19 @@ def slab_sums(M, slab=32):
     return np.stack([M[s * slab:(s + 1) * slab].astype(np.float64).sum(0) for s in range(n)])
 
 
+@pytest.fixture(params=["auto", "m64x128k64s2", "m64x64k32s4", "m64x64k64s2"])
+def colsum_cfg(request):
+    """the configurations the column-sum bwd accepts (32-row wave tiles)"""
+    check(lib().tnet_gemm_config(request.param.encode()))
+    yield request.param
+    check(lib().tnet_gemm_config(b"auto"))
+
+
 @pytest.mark.parametrize("rows,n_in,n_out", [(16, 32, 10), (33, 64, 40), (45, 37, 50), (1024, 2048, 2048),
-                                             (1000, 440, 2048), (1024, 2048, 4000)])
-def test_affine_bwd_colsum(rows, n_in, n_out):
-    """bwd + diff-sigmoid with the bias gradient of the layer below as 32-row slab column sums"""
+                                             (1000, 440, 2048), (1024, 2048, 4000), (1024, 1024, 135)])
+def test_affine_bwd_colsum(rows, n_in, n_out, colsum_cfg):
+    """bwd + diff-sigmoid with the bias gradient of the layer below as 32-row slab column sums (every
+    configuration with 32-row wave tiles)"""
     E, W = rnd((rows, n_out), 9), rnd((n_in, n_out), 10, 0.1)
     Yb = 1 / (1 + np.exp(-rnd((rows, n_in), 11)))
     dE, dW, dY, dO = (DeviceArray.from_numpy(E), DeviceArray.from_numpy(W), DeviceArray.from_numpy(Yb),
@@ -166,7 +175,7 @@ def test_affine_bwd_colsum(rows, n_in, n_out):
 
 @pytest.mark.parametrize("mmt", [0.0, 0.5])
 @pytest.mark.parametrize("rows,n_in,n_out", [(16, 24, 32), (1024, 2048, 2048), (1024, 440, 2048), (960, 1024, 135),
-                                             (1024, 2048, 4000)])
+                                             (1024, 1024, 135), (1024, 598, 1024), (1024, 2048, 4000)])
 def test_affine_update_bias(mmt, rows, n_in, n_out, gemm_cfg):
     """weight SGD + bias SGD (bias gradient from slab sums) in one launch"""
     X, E = rnd((rows, n_in), 12), rnd((rows, n_out), 13, 0.01)
@@ -196,7 +205,8 @@ def test_affine_update_bias(mmt, rows, n_in, n_out, gemm_cfg):
         np.testing.assert_allclose(dCb.numpy().ravel(), cb, rtol=1e-6, atol=1e-9)
 
 
-@pytest.mark.parametrize("rows,n_in,n_out", [(16, 24, 32), (1024, 2048, 2048), (1024, 440, 2048), (1000, 2048, 4000)])
+@pytest.mark.parametrize("rows,n_in,n_out", [(16, 24, 32), (1024, 2048, 2048), (1024, 440, 2048), (1000, 2048, 4000),
+                                             (1024, 1024, 135)])
 def test_affine_grad_bias(rows, n_in, n_out, gemm_cfg):
     """data-parallel gradient: G = X^T E and gradB = colsum(E) from slab sums, one launch"""
     X, E = rnd((rows, n_in), 12), rnd((rows, n_out), 13, 0.01)
@@ -207,6 +217,75 @@ def test_affine_grad_bias(rows, n_in, n_out, gemm_cfg):
     g, mag = gemm_ref("T", "N", X, E)
     assert np.all(np.abs(dG.numpy() - g) <= 2e-5 * mag + 1e-7)
     np.testing.assert_array_equal(dgb.numpy().ravel(), P.astype(np.float64).sum(0).astype(np.float32))
+
+
+@pytest.fixture(params=["auto", "auto+sk4", "m64x128k64s2", "m32x64k64s2+sk2", "g64x64k32s4w4"])
+def top_cfg(request):
+    check(lib().tnet_gemm_config(request.param.encode()))
+    yield request.param
+    check(lib().tnet_gemm_config(b"auto"))
+
+
+@pytest.mark.parametrize("keep_y", [False, True])
+@pytest.mark.parametrize("rows,n_in,n_out", [(1024, 1024, 135), (37, 20, 7), (1000, 598, 256), (64, 1024, 128),
+                                             (300, 2048, 200), (1, 5, 1)])
+def test_affine_softmax_xent(rows, n_in, n_out, keep_y, top_cfg):
+    """the fused top layer (slices + bias + softmax + xent + error + slab sums) gives the logits, the
+    softmax output and the error of tnet_affine_fwd + tnet_softmax_xent bit for bit, their statistics,
+    and slab sums of its own error"""
+    X, W, b = rnd((rows, n_in), 60), rnd((n_in, n_out), 61, 0.1), rnd(n_out, 62)
+    lab = np.random.default_rng(63).integers(0, n_out, size=rows).astype(np.int32)
+    lab[::7] = -1
+    lab[3::11] = n_out - 1
+    dX, dW, db, dL = (DeviceArray.from_numpy(X), DeviceArray.from_numpy(W), DeviceArray.vector(b),
+                      DeviceArray.vector(lab))
+    slabs = lib().tnet_colsum_slabs(rows)
+    res = []
+    for fused in (True, False):
+        dZ, dE = DeviceArray(rows, n_out), DeviceArray(rows, n_out)
+        dY = DeviceArray(rows, n_out) if keep_y else None
+        stats = DeviceArray(1, 1024, np.float64, stride=1024)
+        dP = DeviceArray.from_numpy(np.full((slabs, n_out), np.nan, np.float32))
+        yp, ys = (dY.ptr, dY.stride) if keep_y else (None, 0)
+        if fused:
+            check(lib().tnet_affine_softmax_xent(dX.ptr, dX.dim, dW.ptr, dW.dim, db.ptr, dL.ptr, dZ.ptr, dZ.stride,
+                                                 yp, ys, dE.ptr, dE.stride, stats.ptr, dP.ptr, dP.stride, S()))
+        else:
+            check(lib().tnet_affine_fwd(dX.ptr, dX.dim, dW.ptr, dW.dim, db.ptr, dZ.ptr, dZ.dim, 0, S()))
+            check(lib().tnet_softmax_xent(dZ.ptr, dZ.dim, dL.ptr, yp, ys, dE.ptr, dE.stride, stats.ptr, S()))
+        s = stats.numpy()[0]
+        res.append((dZ.numpy(), dY.numpy() if keep_y else None, dE.numpy(), s[0::2].sum(), s[1::2].sum(),
+                    dP.numpy()))
+    (Z, Y, E, xe, cor, P), (Z0, Y0, E0, xe0, cor0, _) = res
+    if top_cfg != "g64x64k32s4w4":  # that 32x32x2 kernel has no slice form: the fused path takes 16x16x4 tiles
+        np.testing.assert_array_equal(Z, Z0)
+        np.testing.assert_array_equal(E, E0)
+        if keep_y:
+            np.testing.assert_array_equal(Y, Y0)
+        np.testing.assert_allclose(xe, xe0, rtol=1e-12, atol=1e-12)
+        assert cor == cor0
+    # and the objective itself against the oracle
+    z, mag = gemm_ref("N", "N", X, W)
+    assert np.all(np.abs(Z - (z + b)) <= 2e-5 * mag + 1e-6)
+    Yref = orc.softmax(Z)
+    Eref, xent, correct = orc.xent_eval(Yref, lab)
+    np.testing.assert_allclose(E, Eref, rtol=2e-5, atol=1e-7)
+    np.testing.assert_allclose(xe, xent, rtol=1e-5, atol=1e-5)
+    assert int(round(cor)) == correct
+    # slab sums: fp32 in row order over the slab's rows of E
+    ref = slab_sums(E)
+    assert np.all(np.abs(P - ref) <= 32 * 1.2e-7 * slab_sums(np.abs(E)) + 1e-7)
+
+
+def test_affine_softmax_xent_limits():
+    """more than TNET_AFFINE_SOFTMAX_MAX_N classes: unsupported (the caller takes the three calls)"""
+    X, W, b = rnd((8, 4), 64), rnd((4, 257), 65), rnd(257, 66)
+    dX, dW, db = DeviceArray.from_numpy(X), DeviceArray.from_numpy(W), DeviceArray.vector(b)
+    dL, dE = DeviceArray.vector(np.zeros(8, np.int32)), DeviceArray(8, 257)
+    assert lib().tnet_affine_softmax_xent(dX.ptr, dX.dim, dW.ptr, dW.dim, db.ptr, dL.ptr, None, 0, None, 0, dE.ptr,
+                                          dE.stride, None, None, 0, S()) == -4
+    assert lib().tnet_affine_softmax_xent(dX.ptr, dX.dim, dW.ptr, dW.dim, None, dL.ptr, None, 0, None, 0, dE.ptr,
+                                          dE.stride, None, None, 0, S()) == -1
 
 
 @pytest.mark.parametrize("mmt", [0.0, 0.9])

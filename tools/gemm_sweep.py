@@ -4,7 +4,8 @@ suffix forces a split-K count, TNET_GEMM_SPLITK) over the SGD-step shapes on the
 
 Each configuration runs in its own process (the config is read once per process); every shape is
 timed with hipEvents on the library stream over `iters` back-to-back launches of the FUSED kernels
-the training step uses (affine fwd + sigmoid, affine bwd + diff-sigmoid, affine update + SGD)."""
+the training step uses (affine fwd + sigmoid, affine bwd + diff-sigmoid, affine update + SGD; kinds
+"bwdcs" / "updb" add the bias-gradient slab sums / the bias SGD, as CuNetwork's step calls them)."""
 import json
 import os
 import subprocess
@@ -35,11 +36,21 @@ for kind, rows, ni, no in shapes:
     b = DeviceArray.vector(np.zeros(no, np.float32))
     Y = DeviceArray(rows, no)
     Eo = DeviceArray(rows, ni)
+    slabs = lib().tnet_colsum_slabs(rows)
+    Po = DeviceArray(slabs, ni)
+    Pi = DeviceArray.from_numpy(np.zeros((slabs, no), np.float32))
+    bb = DeviceArray.vector(np.zeros(no, np.float32))
     def run():
         if kind == "fwd":
             check(lib().tnet_affine_fwd(X.ptr, X.dim, W.ptr, W.dim, b.ptr, Y.ptr, Y.dim, 1, S))
         elif kind == "bwd":
             check(lib().tnet_affine_bwd(E.ptr, E.dim, W.ptr, W.dim, X.ptr, X.stride, Eo.ptr, Eo.dim, 1, S))
+        elif kind == "bwdcs":  # the training step's bwd: + diff-sigmoid + slab column sums
+            check(lib().tnet_affine_bwd_colsum(E.ptr, E.dim, W.ptr, W.dim, X.ptr, X.stride, Eo.ptr, Eo.dim, Po.ptr,
+                                               Po.stride, S))
+        elif kind == "updb":  # the training step's update: + the bias SGD from slab sums
+            check(lib().tnet_affine_update_bias(X.ptr, X.dim, E.ptr, E.dim, W.ptr, W.dim, None, 0, -1e-6, 0.0, 0.0,
+                                                Pi.ptr, Pi.stride, bb.ptr, None, S))
         else:
             check(lib().tnet_affine_update(X.ptr, X.dim, E.ptr, E.dim, W.ptr, W.dim, None, 0, -1e-6, 0.0, 0.0, S))
     for _ in range(3): run()
