@@ -131,14 +131,18 @@ int tnet_gather_bunch(float* y, const float* x, int* labels_out, const int* labe
  *   C[m x n] = alpha * op(A) * op(B) + beta * C,  op(X) = X or X^T ('N' / 'T')
  * fp32 in / fp32 accumulate on the f32 MFMA (v_mfma_f32_16x16x4_f32; exact f32 FMA chain per k).
  * Shapes with few output tiles and a long K (fewer than ~100 tiles, K >= 1024) are split over K:
- * the slices' partial products are added in slice order (deterministic) before the epilogue.
+ * the slices' partial products are added in slice order (deterministic) before the epilogue, by a
+ * second launch (or, opt-in "+il1"/"+il2" below, by each tile's last-finishing slice inside the
+ * launch: agent-scope release/acquire + a tile counter; measured slower on MI355X).
  * Requirements: lda/ldb/ldc multiples of 4 elements, pointers 16-byte aligned.
  * ---------------------------------------------------------------------------------- */
 int tnet_sgemm(char transa, char transb, int m, int n, int k, float alpha, const float* A, int lda,
                const float* B, int ldb, float beta, float* C, int ldc, void* stream);
 /* Tuning knob: force one GEMM tile configuration for every later launch in this process
  * ("auto" = per-shape heuristic; names as in gemm_f32.hip, e.g. "m64x128k64s2"), optionally with a
- * forced split-K count ("m64x64k32s4w41+sk8").  Not thread-safe. */
+ * forced split-K count ("m64x64k32s4w41+sk8") and the combine mode ("+il0" second launch (default),
+ * "+il1" in-launch up to 64 KB a tile, "+il2" in-launch for every 64x64 / 32x64 tile; sticky).
+ * Not thread-safe. */
 int tnet_gemm_config(const char* name);
 
 /* ------------------------------------------------------------------------------------

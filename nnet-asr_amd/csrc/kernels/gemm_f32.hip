@@ -46,6 +46,7 @@ enum { EPI_STORE = 0, EPI_BIAS = 1, EPI_BIAS_SIG = 2, EPI_DSIG = 3, EPI_SGD = 4,
        // data-parallel gradient: EPI_STORE of X^T E plus the raw bias gradient from the slab sums
        EPI_STORE_BG = 10 };
 constexpr int kColsumSlabRows = 32;
+constexpr int kMaxSplit = 8;  // split-K slices at most
 // base epilogue of a fused one
 constexpr int epi_base(int e) {
   return e == EPI_DSIG_CS ? EPI_DSIG : e == EPI_SGD_B ? EPI_SGD : e == EPI_STORE_BG ? EPI_STORE : e;
@@ -74,6 +75,12 @@ struct GemmP {
   int ksplit;
   long kstepA, kstepB, slabC;
   int early_issue;  // gemm16_kernel prologue: issue all S ring slots before the first wait (TNET_GEMM_EARLY)
+  // in-launch split-K combine (gemm16_kernel EPI_T >= kEpiInLaunch): the last slice of a tile to
+  // finish sums the tile's slices (C is the slice workspace, rows of ldc) and applies the epilogue
+  // into C2 / ldc2 with alpha2 / beta2; the other epilogue operands are the fields above
+  unsigned* tile_cnt;
+  float* C2; long ldc2;
+  float alpha2, beta2;
 };
 
 
@@ -174,6 +181,100 @@ __device__ __forceinline__ void bias_pre_finish(const GemmP& p, int bn, const Bi
   p.bvec[col] = bp.b + p.bscale * g;
 }
 
+// ---- split-K combine of 4 columns of one row: C = epilogue(P[0] + ... + P[splits-1]) summed in
+// slice order (fixed: deterministic), with gemm16_kernel's epilogue arithmetic (EPI = a base epilogue)
+template <int EPI>
+__device__ __forceinline__ void combine4(const GemmP& p, const float* __restrict__ P, long slab, int splits, int ldp,
+                                         int row, int col) {
+  const float* q = P + (long)row * ldp + col;
+  float* cp = p.C + (long)row * p.ldc + col;
+  const int nv = min(4, p.N - col);
+  const bool full = nv == 4;
+  // the epilogue's operands first (W / corr, Y below, C, bias): independent of the slices, so every
+  // load of the thread is in flight before the first add -- 16-byte where the 4 columns are live
+  constexpr bool BIAS = EPI == EPI_BIAS || EPI == EPI_BIAS_SIG || EPI == EPI_BIAS_NSIG || EPI == EPI_BIAS_NEG;
+  const float* asrc = nullptr;
+  if constexpr (EPI == EPI_DSIG) asrc = p.aux + (long)row * p.ldaux + col;
+  else if constexpr (EPI == EPI_STORE) asrc = p.beta != 0.f ? cp : nullptr;
+  else if constexpr (EPI == EPI_SGD || EPI == EPI_RBM) asrc = cp;
+  float* qsrc = (EPI == EPI_SGD || EPI == EPI_RBM) && p.corr ? p.corr + (long)row * p.ldcorr + col : nullptr;
+  f32x4 a = {0.f, 0.f, 0.f, 0.f}, qv = {0.f, 0.f, 0.f, 0.f}, bb = {0.f, 0.f, 0.f, 0.f};
+  auto ld4 = [&](const float* src, f32x4& d) {
+    if (full) {
+      d = *reinterpret_cast<const f32x4*>(src);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (e < nv) d[e] = src[e];
+    }
+  };
+  if (asrc) ld4(asrc, a);
+  if (qsrc) ld4(qsrc, qv);
+  if constexpr (BIAS)
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      if (e < nv) bb[e] = p.bias[col + e];
+  // every slice's load in flight before the first add (splits <= kMaxSplit)
+  f32x4 t[kMaxSplit];
+#pragma unroll
+  for (int z = 0; z < kMaxSplit; ++z)
+    if (z < splits) t[z] = *reinterpret_cast<const f32x4*>(q + z * slab);
+  f32x4 v = t[0];
+#pragma unroll
+  for (int z = 1; z < kMaxSplit; ++z)
+    if (z < splits)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = v[e] + t[z][e];
+  f32x4 o = {0.f, 0.f, 0.f, 0.f}, qn = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const float x = v[e];
+    if constexpr (EPI == EPI_STORE) {
+      o[e] = (p.beta == 0.f) ? p.alpha * x : p.alpha * x + p.beta * a[e];
+    } else if constexpr (BIAS) {
+      const float y = x + bb[e];
+      o[e] = EPI == EPI_BIAS ? y : EPI == EPI_BIAS_SIG ? sigmoidf_ref(y) : EPI == EPI_BIAS_NSIG ? -sigmoidf_ref(y) : -y;
+    } else if constexpr (EPI == EPI_DSIG) {
+      const float y = a[e];
+      o[e] = y * (1.f - y) * x;
+    } else if constexpr (EPI == EPI_RBM) {
+      const float w = a[e];
+      const float c = p.mmt * qv[e] + p.scale * x + p.l2 * w;
+      qn[e] = c;
+      o[e] = w + c;
+    } else if constexpr (EPI == EPI_SGD) {
+      float c = x;
+      if (qsrc) c = x + p.mmt * qv[e];
+      qn[e] = c;
+      float w = a[e];
+      w = w + p.scale * c;
+      w = w + p.l2 * w;
+      o[e] = w;
+    }
+  }
+  if (full) {
+    *reinterpret_cast<f32x4*>(cp) = o;
+    if (qsrc) *reinterpret_cast<f32x4*>(qsrc) = qn;
+  } else {
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      if (e < nv) {
+        cp[e] = o[e];
+        if (qsrc) qsrc[e] = qn[e];
+      }
+  }
+}
+
+// every 4-column group of the BMxBN tile at (bm, bn), NT threads (the in-launch split-K combine)
+template <int EPI>
+__device__ void combine_tile_t(const GemmP& r, const float* P, long slab, int splits, int ldp, int bm, int bn,
+                               int BM, int BN, int NT) {
+  const int q = BN / 4;
+  for (int u = threadIdx.x; u < BM * q; u += NT) {
+    const int row = bm + u / q, col = bn + 4 * (u % q);
+    if (row < r.M && col < r.N) combine4<EPI>(r, P, slab, splits, ldp, row, col);
+  }
+}
 // =============================================================================================
 // LDS-DMA pipelined GEMM.  BMxBN workgroup tile, BK k-depth per ring slot, WMxWN waves each
 // owning (BM/WM)x(BN/WN) = TMxTN blocks of 32x32 MFMA accumulators.
@@ -517,10 +618,15 @@ __device__ __forceinline__ void lds_vec(const float* p, float (&x)[4]) {
 //     slot of tile t.  MEASURED SLOWER (2048^2 main loop 185k vs 149k cycles): the issue cost is paid
 //     by the loader's SIMD, whose compute wave then trails the other three at every seam barrier --
 //     kept as one config (m64x128k64s2L) for the record, not chosen by the heuristic.
-template <int BM, int BN, int BK, int WM, int WN, int S, int SP, bool A_KC, bool B_KC, int EPI>
+// EPI_T >= kEpiInLaunch: a split-K slice kernel (EPI_STORE into the workspace) whose tiles' last
+// slices combine the slices with epilogue EPI_T - kEpiInLaunch inside the launch
+constexpr int kEpiInLaunch = 32;
+template <int BM, int BN, int BK, int WM, int WN, int S, int SP, bool A_KC, bool B_KC, int EPI_T>
 __global__ __launch_bounds__((WM * WN + (SP == 2)) * 64)
 __attribute__((amdgpu_waves_per_eu((WM * WN + (SP == 2) + 3) / 4, (WM * WN + (SP == 2) + 3) / 4)))
 void gemm16_kernel(const GemmP p_in) {
+  constexpr bool INL = EPI_T >= kEpiInLaunch;
+  constexpr int EPI = INL ? EPI_STORE : EPI_T;  // the tile epilogue
   GemmP p = p_in;
   if (p.ksplit > 1) {
     const long z = blockIdx.y;
@@ -1268,6 +1374,46 @@ void gemm16_kernel(const GemmP p_in) {
     }
   }
   }
+  if constexpr (INL) {
+    // ---- in-launch split-K combine (cdna_hip_programming.md section 5, 'In-launch split-K
+    // reduction', the Guideline 16 counter form): every wave drains its slice stores, one lane
+    // releases at agent scope and draws a ticket; the tile's last slice acquires and combines all
+    // slices in slice order (the combine kernel's arithmetic), whatever XCDs the slices ran on
+    constexpr int EPI_C = EPI_T - kEpiInLaunch;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __attribute__((address_space(1))) unsigned* cnt =
+          (__attribute__((address_space(1))) unsigned*)(p.tile_cnt + blockIdx.x);
+      const unsigned ticket = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const bool last = ticket == (unsigned)(p.ksplit - 1);
+      if (last) {
+        __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // ready for the next launch
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      smem[0] = last ? 1.f : 0.f;  // broadcast through the ring array (no second __shared__ object)
+    }
+    __syncthreads();
+    if (smem[0] != 0.f) {
+      GemmP r = p_in;
+      r.C = p_in.C2;
+      r.ldc = p_in.ldc2;
+      r.alpha = p_in.alpha2;
+      r.beta = p_in.beta2;
+      combine_tile_t<epi_base(EPI_C)>(r, p_in.C, p_in.slabC, p_in.ksplit, (int)p_in.ldc, bm, bn, BM, BN, NT);
+      // EPI_SGD_B / EPI_STORE_BG: the first tile-row's combiners also do the bias of their columns
+      if constexpr (epi_bias_slabs(EPI_C)) {
+        if (bm == 0) {
+          BiasPre bpc;
+          bias_pre_load<BN, EPI_C == EPI_STORE_BG>(r, bn, bpc);
+          bias_pre_finish<BN, EPI_C == EPI_STORE_BG>(r, bn, bpc);
+        }
+      }
+    }
+  }
   TNET_STAMP(3);
   TNET_STAMP_RT(5);
 }
@@ -1277,7 +1423,6 @@ void gemm16_kernel(const GemmP p_in) {
 // result is deterministic), then the same epilogue arithmetic as gemm16_kernel; 4 columns / thread
 // ---------------------------------------------------------------------------------------------
 constexpr bool epi_splittable(int e) { return e != EPI_DSIG_CS; }
-constexpr int kMaxSplit = 8;
 
 template <int EPI_FULL>
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(const GemmP p, const float* __restrict__ P, long slab,
@@ -1299,50 +1444,7 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const GemmP p, const
   const long i = (long)blockIdx.x * 256 + threadIdx.x;
   if (i >= (long)p.M * N4) return;
   const int row = (int)(i / N4), col = (int)(i % N4) * 4;
-  const float* q = P + (long)row * ldp + col;
-  // every slice's load in flight before the first add (splits <= kMaxSplit)
-  f32x4 t[kMaxSplit];
-#pragma unroll
-  for (int z = 0; z < kMaxSplit; ++z)
-    if (z < splits) t[z] = *reinterpret_cast<const f32x4*>(q + z * slab);
-  f32x4 v = t[0];
-#pragma unroll
-  for (int z = 1; z < kMaxSplit; ++z)
-    if (z < splits)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] = v[e] + t[z][e];
-  float* cp = p.C + (long)row * p.ldc + col;
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    if (col + e >= p.N) break;
-    const float x = v[e];
-    if constexpr (EPI == EPI_STORE) {
-      cp[e] = (p.beta == 0.f) ? p.alpha * x : p.alpha * x + p.beta * cp[e];
-    } else if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_SIG || EPI == EPI_BIAS_NSIG || EPI == EPI_BIAS_NEG) {
-      const float y = x + p.bias[col + e];
-      cp[e] = EPI == EPI_BIAS ? y : EPI == EPI_BIAS_SIG ? sigmoidf_ref(y) : EPI == EPI_BIAS_NSIG ? -sigmoidf_ref(y) : -y;
-    } else if constexpr (EPI == EPI_DSIG) {
-      const float y = p.aux[(long)row * p.ldaux + col + e];
-      cp[e] = y * (1.f - y) * x;
-    } else if constexpr (EPI == EPI_RBM) {
-      float* qp = p.corr + (long)row * p.ldcorr + col + e;
-      const float w = cp[e];
-      const float c = p.mmt * *qp + p.scale * x + p.l2 * w;
-      *qp = c;
-      cp[e] = w + c;
-    } else if constexpr (EPI == EPI_SGD) {
-      float c = x;
-      if (p.corr) {
-        float* qp = p.corr + (long)row * p.ldcorr + col + e;
-        c = x + p.mmt * *qp;
-        *qp = c;
-      }
-      float w = cp[e];
-      w = w + p.scale * c;
-      w = w + p.l2 * w;
-      cp[e] = w;
-    }
-  }
+  combine4<EPI>(p, P, slab, splits, ldp, row, col);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1496,6 +1598,27 @@ static float* splitk_workspace(size_t bytes, hipStream_t st) {
   return (float*)w.first;
 }
 
+// per-stream tile counters of the in-launch combine: zeroed at allocation, and every tile's last
+// slice puts its counter back to 0, so a stream's next launch finds them zero
+static std::map<hipStream_t, std::pair<unsigned*, size_t>> g_skcnt;
+static unsigned* splitk_counters(size_t n, hipStream_t st) {
+  std::lock_guard<std::mutex> lk(g_skws_mu);
+  auto& w = g_skcnt[st];
+  if (n > w.second) {
+    if (w.first) {
+      if (hipStreamSynchronize(st) != hipSuccess) return nullptr;
+      (void)hipFree(w.first);
+      w = {nullptr, 0};
+    }
+    const size_t cap = (n + 1023) & ~(size_t)1023;
+    void* q = nullptr;
+    if (hipMalloc(&q, cap * sizeof(unsigned)) != hipSuccess) return nullptr;
+    if (hipMemsetAsync(q, 0, cap * sizeof(unsigned), st) != hipSuccess) return nullptr;
+    w = {(unsigned*)q, cap};
+  }
+  return w.first;
+}
+
 // ---------------------------------------------------------------------------------------------
 // host-side dispatch
 // ---------------------------------------------------------------------------------------------
@@ -1534,6 +1657,11 @@ static int g_cfg = -2;  // -2: not initialised, -1: automatic
 static int g_group = -1;
 static int g_split = -1;  // TNET_GEMM_SPLITK: forced split-K count (diagnostics / sweeps), -1 automatic
 static int g_early = 1;   // TNET_GEMM_EARLY=0: prologue issues S-1 slots before the first wait (round-1 form)
+// TNET_SPLITK_INLAUNCH: split-K combine 0 second launch (default) | 1 in-launch <= 64 KB | 2 in-launch.
+// Measured (round 2, MLP3 shapes): the in-launch combine is SLOWER -- the 1024 x 135 update 19.0 vs
+// 14.6 us, the RBM reconstruction 256 x 440 over K = 2048 20.7 vs 14.4 us, MLP3 10.45M vs 10.96M
+// frames/s: the agent-scope release (L2 write-back) + acquire cost more than the launch boundary
+static int g_inlaunch = 0;
 static int forced_cfg() {
   if (g_cfg == -2) {
     g_cfg = -1;
@@ -1547,6 +1675,8 @@ static int forced_cfg() {
     if (sk) g_split = atoi(sk);
     const char* ea = getenv("TNET_GEMM_EARLY");
     if (ea) g_early = atoi(ea);
+    const char* il = getenv("TNET_SPLITK_INLAUNCH");
+    if (il) g_inlaunch = atoi(il);
   }
   return g_cfg;
 }
@@ -1581,22 +1711,32 @@ static void cfg_shape(int cfg, int* bm, int* bn, int* kind) {
   }
 }
 
-// split-K: the K range is cut into ks slices (blockIdx.y) whose partial products go to the stream's
-// workspace; splitk_reduce_kernel adds them in slice order and applies the epilogue
-// the ks slices' raw products A B (no epilogue) into the stream's workspace: slice z at ws + z * slab,
-// rows of ldp = N rounded up to 4 floats
+// split-K: the K range is cut into ks slices (blockIdx.y) whose raw products A B go to the stream's
+// workspace (slice z at ws + z * slab, rows of ldp = N rounded up to 4 floats); then either the
+// tile's last slice combines them inside the launch (tile counters; 64x64 and 32x64 tiles) or
+// splitk_reduce_kernel does, in slice order, with the epilogue
 struct Partials {
   float* ws;
   long slab;
   int ldp;
 };
-template <bool A_KC, bool B_KC>
-static int launch_partials(const GemmP& p, int cfg, int ks, hipStream_t st, Partials* out) {
+template <bool A_KC, bool B_KC, int EPI2 = EPI_STORE>
+static int launch_partials(const GemmP& p, int cfg, int ks, hipStream_t st, Partials* out, bool inl = false) {
   const int ldp = (p.N + 3) & ~3;
   const long slab = (long)p.M * ldp;
   float* ws = splitk_workspace(sizeof(float) * (size_t)slab * ks, st);
   if (!ws) return TNET_ERR_RUNTIME;
   GemmP q = p;
+  if (inl) {
+    int bm, bn, kind;
+    cfg_shape(cfg, &bm, &bn, &kind);
+    q.tile_cnt = splitk_counters((size_t)cdiv(p.M, bm) * cdiv(p.N, bn), st);
+    if (!q.tile_cnt) return TNET_ERR_RUNTIME;
+    q.C2 = p.C;
+    q.ldc2 = p.ldc;
+    q.alpha2 = p.alpha;
+    q.beta2 = p.beta;
+  }
   q.K = p.K / ks;
   q.ksplit = ks;
   q.kstepA = A_KC ? (long)q.K : (long)q.K * p.lda;
@@ -1607,12 +1747,20 @@ static int launch_partials(const GemmP& p, int cfg, int ks, hipStream_t st, Part
   q.alpha = 1.f;
   q.beta = 0.f;
   bool ok = false;
-  switch (cfg) {
+  if (inl) {
+    // in-launch combine: the split-K planner's two tile shapes only
+    if (cfg == CFG_m64x64k32s4w41)
+      ok = launch_cfg<1, 64, 64, 32, 4, 1, 4, 0, A_KC, B_KC, kEpiInLaunch + EPI2>(q, st);
+    else if (cfg == CFG_m32x64k64s2)
+      ok = launch_cfg<1, 32, 64, 64, 2, 2, 2, 0, A_KC, B_KC, kEpiInLaunch + EPI2>(q, st);
+  } else {
+    switch (cfg) {
 #define X(name, KIND, BM, BN, BK, WM, WN, S, IL) \
   case CFG_##name: if (KIND == 1) ok = launch_cfg<KIND, BM, BN, BK, WM, WN, S, IL, A_KC, B_KC, EPI_STORE>(q, st); break;
-    TNET_GEMM_CFGS(X)
+      TNET_GEMM_CFGS(X)
 #undef X
-    default: break;
+      default: break;
+    }
   }
   if (!ok) return TNET_ERR_UNSUPPORTED;
   TNET_LAUNCH_CHECK();
@@ -1623,6 +1771,13 @@ static int launch_partials(const GemmP& p, int cfg, int ks, hipStream_t st, Part
 template <bool A_KC, bool B_KC, int EPI>
 static int launch_splitk(const GemmP& p, int cfg, int ks, hipStream_t st) {
   Partials pt;
+  // in-launch combine where a tile's slices are a few tens of KB (cdna_hip_programming.md section 5)
+  int bm, bn, kind;
+  cfg_shape(cfg, &bm, &bn, &kind);
+  if (g_inlaunch == 2 || (g_inlaunch == 1 && (long)ks * bm * bn * 4 <= 64 * 1024)) {
+    const int rc = launch_partials<A_KC, B_KC, EPI>(p, cfg, ks, st, &pt, true);
+    if (rc != TNET_ERR_UNSUPPORTED) return rc;  // configs without an in-launch form: second launch
+  }
   const int rc = launch_partials<A_KC, B_KC>(p, cfg, ks, st, &pt);
   if (rc) return rc;
   float* ws = pt.ws;
@@ -1961,18 +2116,23 @@ extern "C" int tnet_affine_grad(const float* X, TnetMatrixDim dX, const float* E
 
 extern "C" int tnet_gemm_config(const char* name) {
   forced_cfg();  // read the environment once, before it could override this call
-  // "<cfg>[+sk<n>]": a tile configuration (or "auto") and optionally a forced split-K count
+  // "<cfg>[+sk<n>][+il<m>]": a tile configuration (or "auto"), optionally a forced split-K count and
+  // the split-K combine (il0: a second launch (default), il1: in-launch where a tile's slices are <= 64 KB,
+  // il2: in-launch whatever their size; in-launch only for 64x64 / 32x64 tiles, other tiles always
+  // combine in a second launch); the combine mode stays as set until the next il suffix
   char base[64] = "auto";
-  int split = -1;
+  int split = -1, inl = -1;
   if (name) {
     const char* plus = strchr(name, '+');
     const size_t n = plus ? (size_t)(plus - name) : strlen(name);
     if (n >= sizeof(base)) return TNET_ERR_ARG;
     memcpy(base, name, n);
     base[n] = 0;
-    if (plus) {
-      if (strncmp(plus, "+sk", 3) != 0 || atoi(plus + 3) < 1) return TNET_ERR_ARG;
-      split = atoi(plus + 3);
+    while (plus) {
+      if (!strncmp(plus, "+sk", 3) && atoi(plus + 3) >= 1) split = atoi(plus + 3);
+      else if (!strncmp(plus, "+il", 3) && plus[3] >= '0' && plus[3] <= '2') inl = plus[3] - '0';
+      else return TNET_ERR_ARG;
+      plus = strchr(plus + 1, '+');
     }
   }
   int cfg = -2;
@@ -1982,6 +2142,7 @@ extern "C" int tnet_gemm_config(const char* name) {
   if (cfg == -2) return TNET_ERR_ARG;
   g_cfg = cfg;
   g_split = split;
+  if (inl >= 0) g_inlaunch = inl;
   return TNET_OK;
 }
 

@@ -37,14 +37,19 @@ GEMM_CFGS = ["auto", "g64x64k32s4w4", "m64x128k32s4", "m64x128k64s3", "m64x64k32
              "m64x64k64s2", "m64x64k32s4", "m32x64k64s2",
              # split-K (K cut into slices + an in-order combine with the epilogue); counts that do not
              # divide K fall back to fewer slices
-             "auto+sk4", "m64x64k32s4w41+sk8", "m32x64k64s2+sk2", "m64x128k64s2+sk3"]
+             "auto+sk4", "m64x64k32s4w41+sk8", "m32x64k64s2+sk2", "m64x128k64s2+sk3",
+             # the combine inside the GEMM launch by each tile's last slice (opt-in: il1 up to 64 KB a
+             # tile, il2 whatever the slices' size; tiles other than 64x64 / 32x64 always combine in a
+             # second launch, the default il0)
+             "m64x64k32s4w41+sk2+il1", "m64x64k32s4w41+sk4+il2", "m32x64k64s2+sk8+il2", "m64x128k64s2+sk3+il2",
+             "m128x128k64s2+sk2+il2"]
 
 
 @pytest.fixture(params=GEMM_CFGS)
 def gemm_cfg(request):
     check(lib().tnet_gemm_config(request.param.encode()))
     yield request.param
-    check(lib().tnet_gemm_config(b"auto"))
+    check(lib().tnet_gemm_config(b"auto+il0"))
 
 
 GEMM_SHAPES = [(1, 1, 1), (7, 5, 3), (33, 65, 31), (64, 64, 32), (130, 70, 598), (200, 135, 1024),
@@ -144,7 +149,7 @@ def colsum_cfg(request):
     """the configurations the column-sum bwd accepts (32-row wave tiles)"""
     check(lib().tnet_gemm_config(request.param.encode()))
     yield request.param
-    check(lib().tnet_gemm_config(b"auto"))
+    check(lib().tnet_gemm_config(b"auto+il0"))
 
 
 @pytest.mark.parametrize("rows,n_in,n_out", [(16, 32, 10), (33, 64, 40), (45, 37, 50), (1024, 2048, 2048),
@@ -223,7 +228,7 @@ def test_affine_grad_bias(rows, n_in, n_out, gemm_cfg):
 def top_cfg(request):
     check(lib().tnet_gemm_config(request.param.encode()))
     yield request.param
-    check(lib().tnet_gemm_config(b"auto"))
+    check(lib().tnet_gemm_config(b"auto+il0"))
 
 
 @pytest.mark.parametrize("keep_y", [False, True])

@@ -81,6 +81,8 @@ def main():
                 env["TNET_GEMM_GROUP"] = extra[1:]
             elif extra.startswith("sk") and extra[2:].isdigit():
                 env["TNET_GEMM_SPLITK"] = extra[2:]
+            elif extra.startswith("il") and extra[2:].isdigit():
+                env["TNET_SPLITK_INLAUNCH"] = extra[2:]
         p = subprocess.run([sys.executable, "-c", CHILD, REPO, json.dumps(shapes), str(iters)], env=env,
                            capture_output=True, text=True, timeout=300)
         line = [l for l in p.stdout.splitlines() if l.startswith("RESULT ")]
