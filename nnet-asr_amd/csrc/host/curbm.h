@@ -86,6 +86,10 @@ class CuRandState {
   void Rand(CuMatrix<BaseFloat>& tgt);
   void GaussRand(CuMatrix<BaseFloat>& tgt);
   void BinarizeProbs(const CuMatrix<BaseFloat>& probs, CuMatrix<BaseFloat>& states);
+  /// probs = sigmoid(X W + b) and BinarizeProbs(probs, states) in one launch (tnet_affine_fwd_sample);
+  /// probs already sized like the generator
+  void AffineSigmoidSample(const CuMatrix<BaseFloat>& X, const CuMatrix<BaseFloat>& W, const CuVector<BaseFloat>& b,
+                           CuMatrix<BaseFloat>& probs, CuMatrix<BaseFloat>& states);
   void AddGaussNoise(CuMatrix<BaseFloat>& tgt, BaseFloat gscale = 1.0f);
   size_t Rows() const { return z[0].Rows(); }
   size_t Cols() const { return z[0].Cols(); }

@@ -44,12 +44,16 @@ enum { EPI_STORE = 0, EPI_BIAS = 1, EPI_BIAS_SIG = 2, EPI_DSIG = 3, EPI_SGD = 4,
        // the slab sums, done by the first tile-row's workgroups in the prologue
        EPI_DSIG_CS = 8, EPI_SGD_B = 9,
        // data-parallel gradient: EPI_STORE of X^T E plus the raw bias gradient from the slab sums
-       EPI_STORE_BG = 10 };
+       EPI_STORE_BG = 10,
+       // RBM positive phase: EPI_BIAS_SIG, then the workgroup samples its tile (states = y > U, U the
+       // elements' HybridTaus draws) -- CuRand::BinarizeProbs fused into the launch
+       EPI_BIAS_SIG_BIN = 11 };
 constexpr int kColsumSlabRows = 32;
 constexpr int kMaxSplit = 8;  // split-K slices at most
 // base epilogue of a fused one
 constexpr int epi_base(int e) {
-  return e == EPI_DSIG_CS ? EPI_DSIG : e == EPI_SGD_B ? EPI_SGD : e == EPI_STORE_BG ? EPI_STORE : e;
+  return e == EPI_DSIG_CS ? EPI_DSIG : e == EPI_SGD_B ? EPI_SGD : e == EPI_STORE_BG ? EPI_STORE
+       : e == EPI_BIAS_SIG_BIN ? EPI_BIAS_SIG : e;
 }
 // epilogues that also produce the bias (SGD update or raw gradient) from slab sums
 constexpr bool epi_bias_slabs(int e) { return e == EPI_SGD_B || e == EPI_STORE_BG; }
@@ -81,6 +85,10 @@ struct GemmP {
   unsigned* tile_cnt;
   float* C2; long ldc2;
   float alpha2, beta2;
+  // EPI_BIAS_SIG_BIN: sampled states [M x N] (row stride ldbin) and the four HybridTaus state arrays,
+  // indexed row * ldc + col like the probabilities C (the reference indexes them with C's MatrixDim)
+  float* bin; long ldbin;
+  unsigned* rz[4];
 };
 
 
@@ -275,6 +283,45 @@ __device__ void combine_tile_t(const GemmP& r, const float* P, long slab, int sp
     if (row < r.M && col < r.N) combine4<EPI>(r, P, slab, splits, ldp, row, col);
   }
 }
+// EPI_BIAS_SIG_BIN: after the tile's probabilities are stored, the workgroup reads them back (its own
+// stores: drained + barrier) with every element's four generator states, draws U and writes the
+// sampled state and the advanced generator states (rand.hip rand_kernel<2>'s arithmetic per element)
+template <int BM, int BN, int NT>
+__device__ __forceinline__ void binarize_tile(const GemmP& p, int bm, int bn) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  // elements per thread per batch (5 loads each in flight): the whole tile in one batch up to 64x128
+  constexpr int PER = (BM * BN / NT) < 32 ? (BM * BN / NT > 0 ? BM * BN / NT : 1) : 32;
+  for (int u0 = 0; u0 < BM * BN; u0 += NT * PER) {
+    float pr[PER];
+    unsigned z[4][PER];
+    long si[PER];
+    bool ok[PER];
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const int u = u0 + (int)threadIdx.x + NT * k, row = bm + u / BN, col = bn + u % BN;
+      ok[k] = u < BM * BN && row < p.M && col < p.N;
+      const int rr = ok[k] ? row : 0, cc = ok[k] ? col : 0;
+      si[k] = (long)rr * p.ldc + cc;
+      pr[k] = p.C[si[k]];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) z[q][k] = p.rz[q][si[k]];
+    }
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      if (!ok[k]) continue;
+      const int u = u0 + (int)threadIdx.x + NT * k, row = bm + u / BN, col = bn + u % BN;
+      unsigned a = z[0][k], b = z[1][k], c = z[2][k], e = z[3][k];
+      const float x = hybrid_taus(a, b, c, e);
+      p.bin[(long)row * p.ldbin + col] = pr[k] > x ? 1.0f : 0.0f;
+      p.rz[0][si[k]] = a;
+      p.rz[1][si[k]] = b;
+      p.rz[2][si[k]] = c;
+      p.rz[3][si[k]] = e;
+    }
+  }
+}
+
 // =============================================================================================
 // LDS-DMA pipelined GEMM.  BMxBN workgroup tile, BK k-depth per ring slot, WMxWN waves each
 // owning (BM/WM)x(BN/WN) = TMxTN blocks of 32x32 MFMA accumulators.
@@ -555,6 +602,7 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_f32_glds_kernel(const GemmP
   if constexpr (epi_bias_slabs(EPI))
     if (bm == 0) bias_pre_finish<BN, EPI == EPI_STORE_BG>(p, bn, bpre);
   epilogue<TM, TN, epi_base(EPI)>(p, acc, bm, bn, wm0, wn0, li, lh);
+  if constexpr (EPI == EPI_BIAS_SIG_BIN) binarize_tile<BM, BN, WM * WN * 64>(p, bm, bn);
 }
 
 
@@ -1374,6 +1422,7 @@ void gemm16_kernel(const GemmP p_in) {
     }
   }
   }
+  if constexpr (EPI == EPI_BIAS_SIG_BIN) binarize_tile<BM, BN, NT>(p, bm, bn);
   if constexpr (INL) {
     // ---- in-launch split-K combine (cdna_hip_programming.md section 5, 'In-launch split-K
     // reduction', the Guideline 16 counter form): every wave drains its slice stores, one lane
@@ -1422,7 +1471,7 @@ void gemm16_kernel(const GemmP p_in) {
 // split-K combine: C = epilogue(P[0] + P[1] + ... + P[splits-1]) summed in split order (fixed, so the
 // result is deterministic), then the same epilogue arithmetic as gemm16_kernel; 4 columns / thread
 // ---------------------------------------------------------------------------------------------
-constexpr bool epi_splittable(int e) { return e != EPI_DSIG_CS; }
+constexpr bool epi_splittable(int e) { return e != EPI_DSIG_CS && e != EPI_BIAS_SIG_BIN; }
 
 template <int EPI_FULL>
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(const GemmP p, const float* __restrict__ P, long slab,
@@ -1936,6 +1985,25 @@ extern "C" int tnet_affine_fwd(const float* X, TnetMatrixDim dX, const float* W,
     case 3: return launch_gemm<true, false, EPI_BIAS_NSIG>(p, (hipStream_t)stream);
     default: return launch_gemm<true, false, EPI_BIAS>(p, (hipStream_t)stream);
   }
+}
+
+extern "C" int tnet_affine_fwd_sample(const float* X, TnetMatrixDim dX, const float* W, TnetMatrixDim dW,
+                                      const float* b, float* Y, TnetMatrixDim dY, float* states, int ld_states,
+                                      unsigned* z1, unsigned* z2, unsigned* z3, unsigned* z4, void* stream) {
+  // Y = sigmoid(X W + b), states = (Y > U) with U the HybridTaus draws of states z1..z4 (indexed with Y's
+  // stride) -- tnet_affine_fwd(act 1) + tnet_rand_binarize in one launch
+  if (dX.cols != dW.rows || dY.rows != dX.rows || dY.cols != dW.cols || !b || !states || ld_states < dY.cols ||
+      !z1 || !z2 || !z3 || !z4)
+    return TNET_ERR_ARG;
+  GemmP p{};
+  p.M = dX.rows; p.N = dW.cols; p.K = dX.cols;
+  p.A = X; p.lda = dX.stride; p.B = W; p.ldb = dW.stride; p.C = Y; p.ldc = dY.stride;
+  p.bias = b;
+  p.bin = states; p.ldbin = ld_states;
+  p.rz[0] = z1; p.rz[1] = z2; p.rz[2] = z3; p.rz[3] = z4;
+  int st = check_common(p);
+  if (st) return st;
+  return launch_gemm<true, false, EPI_BIAS_SIG_BIN>(p, (hipStream_t)stream);
 }
 
 extern "C" int tnet_affine_fwd_t(const float* X, TnetMatrixDim dX, const float* W, TnetMatrixDim dW, const float* b,

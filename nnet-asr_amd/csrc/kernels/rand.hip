@@ -17,22 +17,6 @@
 
 namespace tnetk {
 
-__device__ __forceinline__ unsigned taus_step(unsigned& z, int s1, int s2, int s3, unsigned m) {
-  const unsigned b = ((z << s1) ^ z) >> s2;
-  return z = ((z & m) << s3) ^ b;
-}
-__device__ __forceinline__ unsigned lcg_step(unsigned& z) { return z = 1664525u * z + 1013904223u; }
-
-__device__ __forceinline__ float hybrid_taus(unsigned& z1, unsigned& z2, unsigned& z3, unsigned& z4) {
-  float r;
-  do {
-    const unsigned x = taus_step(z1, 13, 19, 12, 4294967294u) ^ taus_step(z2, 2, 25, 4, 4294967288u) ^
-                       taus_step(z3, 3, 11, 17, 4294967280u) ^ lcg_step(z4);
-    r = (float)(2.3283064365387e-10 * (double)x);
-  } while (!(r > 0.0f && r < 1.0f));
-  return r;
-}
-
 __device__ __forceinline__ float box_muller(unsigned& z1, unsigned& z2, unsigned& z3, unsigned& z4) {
   const float two_pi = 6.283185307179586476925286766558f;
   const float u0 = hybrid_taus(z1, z2, z3, z4), u1 = hybrid_taus(z1, z2, z3, z4);

@@ -358,18 +358,47 @@ extern "C" int tnet_rbm_bias_update(const float* M, TnetMatrixDim d, int neg_fro
 // the sum runs exactly as colsum_partial + colsum_final do it: fp32 over the cs_slabs(rows) slabs (row
 // sub-group g takes rows r0+g, r0+g+4, ...; the four sub-group sums added in order g = 0..3), slabs
 // combined in fp64 in slab order -- bit-identical bias updates.  Lane 16g + j of a wave holds
-// sub-group g of column j; the 4 waves take slabs round-robin; the slab sums meet in LDS.  The visible
-// blocks then add sum_r (neg_vis - pos_vis)^2 of their columns to the MSE statistics.
+// sub-group g of column j; the 4 waves take slabs round-robin; the slab sums meet in LDS.  The last
+// blocks (from nvb + nhb on) add sum (neg_vis - pos_vis)^2 over RS_MROWS rows each to the MSE
+// statistics (a row range per block: every load of a block in flight at once).
 constexpr int RS_COLS = 16;
 constexpr int RS_MAX_SLABS = 256;  // cs_slabs() cap
+constexpr int RS_MROWS = 8;        // MSE rows per block
 __global__ __launch_bounds__(256) void rbm_stats_kernel(const float* __restrict__ Vs, TnetMatrixDim dV,
                                                         const float* __restrict__ Hs, TnetMatrixDim dH, int B,
                                                         int nvb, float* __restrict__ vb, float* __restrict__ cvb,
                                                         float* __restrict__ hb, float* __restrict__ chb, float scale,
-                                                        float mmt, double* __restrict__ stats) {
+                                                        float mmt, double* __restrict__ stats, int nhb) {
   __shared__ float ts[RS_MAX_SLABS][RS_COLS];
   __shared__ double dred[4];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, j = lane & 15;
+  if ((int)blockIdx.x >= nvb + nhb) {
+    // ---- reconstruction MSE over rows [r0, r0 + RS_MROWS) of the visible statistics
+    const int r0 = ((int)blockIdx.x - nvb - nhb) * RS_MROWS, nr = min(RS_MROWS, B - r0), C = dV.cols;
+    constexpr int PER = 16;  // elements per thread per batch
+    double e2 = 0.0;
+    for (int i0 = 0; i0 < nr * C; i0 += 256 * PER) {
+      float a[PER], b[PER];
+#pragma unroll
+      for (int k = 0; k < PER; ++k) {
+        const int i = min(i0 + (int)threadIdx.x + 256 * k, nr * C - 1), r = r0 + i / C, c = i % C;
+        a[k] = Vs[(long)(B + r) * dV.stride + c];
+        b[k] = Vs[(long)r * dV.stride + c];
+      }
+#pragma unroll
+      for (int k = 0; k < PER; ++k)
+        if (i0 + (int)threadIdx.x + 256 * k < nr * C) {
+          const float e = a[k] - b[k];
+          e2 += (double)(e * e);
+        }
+    }
+    e2 = wave_sum_d(e2);
+    if (lane == 0) dred[w] = e2;
+    __syncthreads();
+    if (threadIdx.x == 0)
+      atomicAdd(stats + 2 * (blockIdx.x % TNET_STATS_SLOTS), dred[0] + dred[1] + dred[2] + dred[3]);
+    return;
+  }
   const bool vis = (int)blockIdx.x < nvb;
   const float* M = vis ? Vs : Hs;
   const TnetMatrixDim d = vis ? dV : dH;
@@ -377,9 +406,9 @@ __global__ __launch_bounds__(256) void rbm_stats_kernel(const float* __restrict_
   const int c = (vis ? (int)blockIdx.x : (int)blockIdx.x - nvb) * RS_COLS + j;
   const bool cok = c < d.cols;
   const int slabs = cs_slabs(d.rows), rows_per = (d.rows + slabs - 1) / slabs;
-  // a wave takes slabs w, w+4, w+8, w+12 together (32 loads per lane in flight at 32-row slabs), then
-  // the next four; each slab's rows are still added in row order
-  constexpr int SG = 4, RMAX = CS_ROWS / CS_WAVES;  // slabs per group, rows per sub-group at full slabs
+  // a wave takes slabs w, w+4, ..., w+28 together (64 loads per lane in flight at 32-row slabs), then
+  // the next eight; each slab's rows are still added in row order
+  constexpr int SG = 8, RMAX = CS_ROWS / CS_WAVES;  // slabs per group, rows per sub-group at full slabs
   for (int s0 = w; s0 < slabs; s0 += 4 * SG) {
     float x[SG][RMAX];
 #pragma unroll
@@ -416,18 +445,6 @@ __global__ __launch_bounds__(256) void rbm_stats_kernel(const float* __restrict_
     cv[c] = gr;
     bv[c] = bv[c] + gr;
   }
-  if (!vis || !stats) return;
-  double e2 = 0.0;
-  if (cok)
-#pragma unroll 8
-    for (int r = 4 * w + g; r < B; r += 16) {
-      const float e = M[(long)(B + r) * d.stride + c] - M[(long)r * d.stride + c];
-      e2 += (double)(e * e);
-    }
-  e2 = wave_sum_d(e2);
-  if (lane == 0) dred[w] = e2;
-  __syncthreads();
-  if (threadIdx.x == 0) atomicAdd(stats + 2 * (blockIdx.x % TNET_STATS_SLOTS), dred[0] + dred[1] + dred[2] + dred[3]);
 }
 
 // Wide rows (1025..4096 columns, 16-B aligned), class-id targets, logits in Z: one 256-thread block
@@ -574,9 +591,9 @@ extern "C" int tnet_rbm_stats_update(const float* Vs, TnetMatrixDim dV, const fl
     return TNET_ERR_ARG;
   if (!B) return TNET_OK;
   if (2 * B > CS_ROWS * RS_MAX_SLABS) return TNET_ERR_UNSUPPORTED;  // slabs of more than 32 rows
-  const int nvb = cdiv(dV.cols, RS_COLS), nhb = cdiv(dH.cols, RS_COLS);
-  rbm_stats_kernel<<<nvb + nhb, 256, 0, (hipStream_t)stream>>>(Vs, dV, Hs, dH, B, nvb, vb, cvb, hb, chb, scale, mmt,
-                                                               mse_stats);
+  const int nvb = cdiv(dV.cols, RS_COLS), nhb = cdiv(dH.cols, RS_COLS), nmb = mse_stats ? cdiv(B, RS_MROWS) : 0;
+  rbm_stats_kernel<<<nvb + nhb + nmb, 256, 0, (hipStream_t)stream>>>(Vs, dV, Hs, dH, B, nvb, vb, cvb, hb, chb, scale,
+                                                                     mmt, mse_stats, nhb);
   TNET_LAUNCH_CHECK();
   return TNET_OK;
 }

@@ -73,6 +73,44 @@ def test_rand_binarize_bitexact():
     np.testing.assert_array_equal(st2.numpy(), (P > rs.uniform()).astype(np.float32))
 
 
+@pytest.mark.parametrize("cfg", ["auto", "g64x64k32s4w4", "m64x128k64s2"])
+@pytest.mark.parametrize("rows,V,H", [(256, 440, 2048), (1024, 440, 2048), (33, 37, 70), (1, 5, 3)])
+def test_affine_fwd_sample_matches_two_launches(rows, V, H, cfg):
+    """positive phase + HybridTaus binarisation in one launch: probabilities, sampled states and the
+    advanced generator states bit-identical to tnet_affine_fwd(act 1) + tnet_rand_binarize, and the
+    states equal to the oracle's draws"""
+    rng = np.random.default_rng(rows + V)
+    X = rng.standard_normal((rows, V)).astype(np.float32)
+    W = (0.05 * rng.standard_normal((V, H))).astype(np.float32)
+    b = rng.standard_normal(H).astype(np.float32)
+    dX, dW, db = DeviceArray.from_numpy(X), DeviceArray.from_numpy(W), DeviceArray.vector(b)
+    check(lib().tnet_gemm_config(cfg.encode()))
+    try:
+        out = []
+        for fused in (True, False):
+            rs = orc.RandState(31, rows, H)
+            z = _state_dev(rs, rows, H)
+            Y, st = DeviceArray(rows, H), DeviceArray(rows, H)
+            if fused:
+                check(lib().tnet_affine_fwd_sample(dX.ptr, dX.dim, dW.ptr, dW.dim, db.ptr, Y.ptr, Y.dim, st.ptr,
+                                                   st.stride, *[a.ptr for a in z], S()))
+            else:
+                check(lib().tnet_affine_fwd(dX.ptr, dX.dim, dW.ptr, dW.dim, db.ptr, Y.ptr, Y.dim, 1, S()))
+                check(lib().tnet_rand_binarize(st.ptr, st.stride, Y.ptr, Y.dim, *[a.ptr for a in z], S()))
+            out.append((Y.numpy(), st.numpy(), [a.numpy() for a in z]))
+            if fused:
+                np.testing.assert_array_equal(st.numpy(), (Y.numpy() > rs.uniform()).astype(np.float32))
+                for a, zb in zip(z, rs.z):
+                    np.testing.assert_array_equal(a.numpy().reshape(-1), zb)
+    finally:
+        check(lib().tnet_gemm_config(b"auto"))
+    (Y1, s1, z1), (Y2, s2, z2) = out
+    np.testing.assert_array_equal(Y1, Y2)
+    np.testing.assert_array_equal(s1, s2)
+    for a, b2 in zip(z1, z2):
+        np.testing.assert_array_equal(a, b2)
+
+
 @pytest.mark.parametrize("act", [0, 1, 2, 3])
 def test_affine_fwd_negated_and_transposed(act):
     rng = np.random.default_rng(act)
