@@ -253,7 +253,10 @@ def main():
 
     if rank == 0:
         line = {
-            "metric": "training frames/sec (whole node), 440->2048x4->senone MLP",
+            # BASELINE.json's metric for its config (dnn4); the other configs name their own network
+            "metric": ("training frames/sec (whole node), 440\u21922048\u00d74\u2192senone MLP, 1/2/4/8 MI355X"
+                       if args.config == "dnn4" else
+                       f"training frames/sec (whole node), {'x'.join(map(str, dims))} MLP"),
             "value": round(value, 1), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
