@@ -1,0 +1,70 @@
+"""bench.py keeps the driver's contract: one JSON line from rank 0 with BASELINE.json's metric, the
+required fields, the roofline object, and (N > 1) the whole-job value of every rank's frames over the
+slowest rank's time.  Small windows and caches: this checks the contract and the multi-process launch,
+not the number (the number is bench.py's own run, profiles/)."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REQUIRED = {"metric": str, "value": float, "unit": str, "n_gpus": int, "steps": int, "warmup": int,
+            "ms_per_step": float, "higher_is_better": bool, "scaling": str, "dtype": str, "data": str,
+            "config": dict}
+
+
+def _line(out):
+    lines = [l for l in out.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out[-2000:]
+    return json.loads(lines[0])
+
+
+def _check_contract(d, n, steps, warmup):
+    for k, t in REQUIRED.items():
+        assert isinstance(d[k], t), (k, d[k])
+    assert "vs_baseline" in d and d["vs_baseline"] is None  # BASELINE.md publishes no frames/s figure
+    base = json.load(open(os.path.join(REPO, "BASELINE.json")))
+    assert d["metric"] == base["metric"]
+    assert d["unit"] == "frames/s" and d["higher_is_better"] and d["scaling"] == "weak"
+    assert d["n_gpus"] == n and d["steps"] == steps and d["warmup"] == warmup
+    assert d["value"] > 0 and d["ms_per_step"] > 0
+    # value = every rank's frames over the slowest rank's time
+    bunch = d["config"]["bunch_per_gpu"]
+    assert abs(d["value"] - n * bunch * 1000.0 / d["ms_per_step"]) <= 0.01 * d["value"]
+    assert d["config"]["global_bunch"] == n * bunch
+
+
+def test_bench_contract_one_gpu():
+    cmd = [sys.executable, "bench.py", "--steps", "3", "--warmup", "1", "--no-cpu-baseline", "--cache", "4096",
+           "--breakdown-steps", "1"]
+    p = subprocess.run(cmd, cwd=REPO, capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-3000:]
+    d = _line(p.stdout)
+    _check_contract(d, 1, 3, 1)
+    r = d["roofline"]
+    assert r["bound"] == "mfma" and r["unit"] == "TFLOP/s" and r["peak"] == 157.3
+    assert 0 < r["frac"] <= 1 and abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-3
+    assert "traffic" in r and d["kernels"]
+
+
+def test_bench_two_ranks_rehearsal():
+    """the torch.distributed.run launch the driver uses at N > 1, rehearsed on one GPU (both ranks on
+    device 0, gradients summed through host memory): rendezvous, barriers, max-over-ranks timing, teardown"""
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "2", "--steps", "2", "--warmup", "1",
+           "--no-cpu-baseline", "--cache", "4096", "--comm", "host", "--same-device", "--kernel-timing", "0",
+           "--breakdown-steps", "0"]
+    env = dict(os.environ, OMP_NUM_THREADS="2")
+    p = subprocess.run(cmd, cwd=REPO, capture_output=True, text=True, timeout=300, env=env)
+    assert p.returncode == 0, p.stderr[-3000:]
+    d = _line(p.stdout)
+    _check_contract(d, 2, 2, 1)
+    assert d["roofline"] is None  # kernel timing off
