@@ -46,6 +46,13 @@ class CuCache {
   void Randomize();
   void GetBunch(CuMatrix<BaseFloat>& rFeatures, CuMatrix<BaseFloat>& rDesired);
   void GetBunchLabels(CuMatrix<BaseFloat>& rFeatures, CuVector<int>& rLabels);
+  /// Another bunch of the shuffled class-id fill being exhausted follows the one just taken (it can be
+  /// gathered ahead: GatherAheadLabels)
+  bool HasBunchAhead() const { return mMode == LABELS && mRandomized && mState == EXHAUST; }
+  /// GetBunchLabels of that next bunch on `stream` (the caller orders the stream after the compute
+  /// stream's use of the destination buffers; the permutation and the fill are already waited for
+  /// there, EnterExhaust / Randomize being compute-stream ordered)
+  void GatherAheadLabels(CuMatrix<BaseFloat>& rFeatures, CuVector<int>& rLabels, hipStream_t stream);
 
   bool Full() { return mState == FULL; }
   bool Empty() { return mState == EMPTY || mIntakePos < mBunchsize; }

@@ -30,11 +30,46 @@ CuTrainer::CuTrainer(CuNetwork* net, CuObjectiveFunction* obj, const TrainerOpti
   mCache.Trace(mOpt.trace);
 }
 
-CuTrainer::~CuTrainer() {}
+CuTrainer::~CuTrainer() {
+  if (mAheadStream) (void)hipStreamSynchronize(mAheadStream);
+  for (hipEvent_t e : {mMark, mGathered})
+    if (e) (void)hipEventDestroy(e);
+  if (mAheadStream) (void)hipStreamDestroy(mAheadStream);
+}
 
 void CuTrainer::Step() {
-  mCache.GetBunchLabels(mFeats, mLabels);
-  mNet->TrainBunch(mFeats, mLabels, *mObj, !mOpt.crossval, mOpt.crossval ? nullptr : mExchange);
+  hipStream_t cs = CuDevice::Instantiate().Stream();
+  if (mAhead) {  // gathered during the previous step
+    mCur ^= 1;
+    TNET_HIP_CALL(hipStreamWaitEvent(cs, mGathered, 0));
+    mAhead = false;
+  } else {
+    mCache.GetBunchLabels(mFeatsB[mCur], mLabelsB[mCur]);
+  }
+  // the next bunch of the fill into the other buffer, beside this step's kernels: the gather stream
+  // first waits for everything queued on the compute stream so far (the previous step, which read
+  // that buffer; the buffer allocations; the permutation upload and the fill wait)
+  // Opt-in (TNET_GATHER_AHEAD=1): measured SLOWER on MI355X -- MLP3 9.7 M vs 11.0 M frames/s, dnn4
+  // 939 k vs 952 k: the cross-stream wait per step and the gather's workgroups beside the step's
+  // GEMMs cost more than the 6 us gather they take off the chain
+  static const bool ahead = getenv("TNET_GATHER_AHEAD") && getenv("TNET_GATHER_AHEAD")[0] == '1';
+  if (ahead && mCache.HasBunchAhead()) {
+    if (!mAheadStream) {
+      TNET_HIP_CALL(hipStreamCreateWithFlags(&mAheadStream, hipStreamNonBlocking));
+      TNET_HIP_CALL(hipEventCreateWithFlags(&mMark, hipEventDisableTiming));
+      TNET_HIP_CALL(hipEventCreateWithFlags(&mGathered, hipEventDisableTiming));
+    }
+    CuMatrix<BaseFloat>& nf = mFeatsB[mCur ^ 1];
+    CuVector<int>& nl = mLabelsB[mCur ^ 1];
+    nf.Init(mCache.Bunchsize(), mFeatsB[mCur].Cols());
+    nl.Init(mCache.Bunchsize());
+    TNET_HIP_CALL(hipEventRecord(mMark, cs));
+    TNET_HIP_CALL(hipStreamWaitEvent(mAheadStream, mMark, 0));
+    mCache.GatherAheadLabels(nf, nl, mAheadStream);
+    TNET_HIP_CALL(hipEventRecord(mGathered, mAheadStream));
+    mAhead = true;
+  }
+  mNet->TrainBunch(mFeatsB[mCur], mLabelsB[mCur], *mObj, !mOpt.crossval, mOpt.crossval ? nullptr : mExchange);
   if (mOpt.trace & 2) std::cout << "." << std::flush;
   mSteps++;
 }
@@ -43,7 +78,7 @@ bool CuTrainer::DrainCache(bool final) {
   if (mOpt.randomize) mCache.Randomize();
   mTrainedSinceFill = true;
   if (DataParallel()) return DpRound((long)(mCache.IntakePos() / mCache.Bunchsize()), final);
-  while (!mCache.Empty()) Step();
+  while (mAhead || !mCache.Empty()) Step();
   return true;
 }
 
@@ -129,7 +164,7 @@ size_t CuTrainer::Prefill(const float* feats, size_t rows, size_t cols, size_t l
 
 void CuTrainer::Replay(long n) {
   for (long i = 0; i < n; i++) {
-    if (mCache.Empty()) {
+    if (!mAhead && mCache.Empty()) {
       mCache.Rewind();
       if (mOpt.randomize) mCache.Randomize();
     }

@@ -72,8 +72,14 @@ class CuTrainer {
   GradExchange* mExchange = nullptr;
   CuCache mCache;
   Rng48 mRng;
-  CuMatrix<BaseFloat> mFeats;
-  CuVector<int> mLabels;
+  // bunch buffers: with TNET_GATHER_AHEAD=1 the step trains buffer mCur while the next shuffled bunch
+  // of the fill is gathered into the other one on mAheadStream (measured slower: off by default)
+  CuMatrix<BaseFloat> mFeatsB[2];
+  CuVector<int> mLabelsB[2];
+  int mCur = 0;
+  bool mAhead = false;        // buffer mCur ^ 1 holds the next bunch (gathered ahead)
+  hipStream_t mAheadStream = nullptr;
+  hipEvent_t mMark = nullptr, mGathered = nullptr;
   CuNetwork* mTransform = nullptr;
   size_t mStartExt = 0, mEndExt = 0;
   std::vector<float> mExtHost;
