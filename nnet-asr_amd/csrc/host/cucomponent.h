@@ -116,7 +116,10 @@ class CuComponent {
 struct CuParamBlock {
   float* grad;   // gradient buffer (device), n elements
   long n;
+  float* param;  // the parameters it updates, same n-element layout (sharded apply: all-gathered)
 };
+
+class GradExchange;
 
 class CuUpdatableComponent : public CuComponent {
  public:
@@ -132,11 +135,13 @@ class CuUpdatableComponent : public CuComponent {
   // ---- data-parallel split of Update() (MI355X addition)
   /// Compute the local gradient into the component's gradient buffers (no parameter change).
   virtual void ComputeGradient() { Error(std::string(GetName()) + ": ComputeGradient not supported"); }
-  /// Apply the (already all-reduced) gradient; `frames` = global rows contributing.
-  /// stream: where to enqueue the update (nullptr: the library stream)
-  virtual void ApplyGradient(size_t frames, void* stream = nullptr) {
+  /// Apply the (already reduced) gradient; `frames` = global rows contributing.
+  /// stream: where to enqueue the update (nullptr: the library stream); ex: the exchange whose
+  /// ApplyRanges pick the elements this rank updates (nullptr: all of them)
+  virtual void ApplyGradient(size_t frames, void* stream = nullptr, const GradExchange* ex = nullptr) {
     (void)frames;
     (void)stream;
+    (void)ex;
     Error(std::string(GetName()) + ": ApplyGradient not supported");
   }
   /// Gradient buffers of this component (valid after ComputeGradient()).

@@ -1,6 +1,8 @@
 // culayers.cpp -- <biasedlinearity>, <sigmoid>, <softmax> on the fused gfx950 kernels.
 #include "culayers.h"
 
+#include "gradexchange.h"
+
 #include <cctype>
 #include <cstdlib>
 
@@ -190,28 +192,35 @@ void CuBiasedLinearity::ComputeGradientColsum(const CuMatrix<BaseFloat>& colpart
 std::vector<CuParamBlock> CuBiasedLinearity::GradientBlocks() {
   mGradW.Init(mLinearity.Rows(), mLinearity.Cols());
   mGradB.Init(mBias.Dim());
-  return {CuParamBlock{mGradW.pCUData(), (long)(mGradW.Rows() * mGradW.Stride())},
-          CuParamBlock{mGradB.pCUData(), (long)mGradB.Dim()}};
+  return {CuParamBlock{mGradW.pCUData(), (long)(mGradW.Rows() * mGradW.Stride()), mLinearity.pCUData()},
+          CuParamBlock{mGradB.pCUData(), (long)mGradB.Dim(), mBias.pCUData()}};
 }
 
-void CuBiasedLinearity::ApplyGradient(size_t frames, void* stream) {
+void CuBiasedLinearity::ApplyGradient(size_t frames, void* stream, const GradExchange* ex) {
   CuProfileScope p("CuBiasedLinearity::ApplyGradient");
   float scale, l2;
   UpdateConstants(frames, &scale, &l2);
   const bool mmt = mMomentum != 0.0f;
   // padding columns of W and of the gradient are zero, so the flat update keeps them zero; W and b
-  // in one launch
-  TnetSgdSeg seg[2] = {
-      {mLinearity.pCUData(), mGradW.pCUData(), mmt ? mLinearityCorrection.pCUData() : nullptr,
-       (long)(mLinearity.Rows() * mLinearity.Stride()), l2},
-      {mBias.pCUData(), mGradB.pCUData(), mmt ? mBiasCorrection.pCUData() : nullptr, (long)mBias.Dim(), 0.f}};
+  // in one launch, each as the element ranges this rank applies (sharded apply: its shard + the tail)
+  TnetSgdSeg seg[4];
+  int nseg = 0;
+  auto add = [&](float* prm, float* grd, float* corr, long n, float wl2) {
+    long lo[2], hi[2];
+    const int nr = ex ? ex->ApplyRanges(n, lo, hi) : GradExchange::FullRange(n, lo, hi);
+    for (int k = 0; k < nr; ++k)
+      if (hi[k] > lo[k]) seg[nseg++] = {prm + lo[k], grd + lo[k], corr ? corr + lo[k] : nullptr, hi[k] - lo[k], wl2};
+  };
+  add(mLinearity.pCUData(), mGradW.pCUData(), mmt ? mLinearityCorrection.pCUData() : nullptr,
+      (long)(mLinearity.Rows() * mLinearity.Stride()), l2);
+  add(mBias.pCUData(), mGradB.pCUData(), mmt ? mBiasCorrection.pCUData() : nullptr, (long)mBias.Dim(), 0.f);
   if (stream) {  // beside the compute stream (GradExchange::ApplyStream): no library-stream timing
-    TNET_SAFE_CALL(tnet_sgd_update_multi(seg, 2, scale, mMomentum, stream));
+    TNET_SAFE_CALL(tnet_sgd_update_multi(seg, nseg, scale, mMomentum, stream));
     return;
   }
   KTScope kt("sgd_apply:" + std::to_string(GetNInputs()) + "x" + std::to_string(GetNOutputs()),
              12.0 * (double)(mLinearity.Rows() * mLinearity.Stride() + mBias.Dim()));
-  TNET_SAFE_CALL(tnet_sgd_update_multi(seg, 2, scale, mMomentum, S));
+  TNET_SAFE_CALL(tnet_sgd_update_multi(seg, nseg, scale, mMomentum, S));
 }
 
 void CuBiasedLinearity::ReadFromStream(std::istream& rIn) {

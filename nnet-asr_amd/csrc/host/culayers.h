@@ -25,7 +25,7 @@ class CuBiasedLinearity : public CuUpdatableComponent {
   void ComputeGradient() override;
   // ComputeGradient with the bias gradient from the slab column sums of E (tnet_affine_grad_bias)
   void ComputeGradientColsum(const CuMatrix<BaseFloat>& colpart);
-  void ApplyGradient(size_t frames, void* stream = nullptr) override;
+  void ApplyGradient(size_t frames, void* stream = nullptr, const GradExchange* ex = nullptr) override;
   std::vector<CuParamBlock> GradientBlocks() override;
 
   void ReadFromStream(std::istream& rIn) override;

@@ -218,20 +218,26 @@ void CuNetwork::TrainEmpty(GradExchange& exchange) {
   for (int l = nl - 1; l >= 0; l--) {  // applies beside the reductions where the transport allows
     auto* lin = static_cast<CuBiasedLinearity*>(mNetComponents[2 * l]);
     if (lin->LearnRate() > 0.0f) {
-      void* as = exchange.ApplyStream(i++);
+      void* as = exchange.ApplyStream(i);
       if (!as) {
         inline_apply = false;
         break;
       }
-      lin->ApplyGradient(grows, as);
+      lin->ApplyGradient(grows, as, &exchange);
+      exchange.GatherParams(*lin, i, as);
+      i++;
     }
     if (lin == mpPropagErrorStopper) break;
   }
   exchange.WaitAll();
   if (inline_apply) return;
+  int j = 0;
   for (int l = nl - 1; l >= 0; l--) {
     auto* lin = static_cast<CuBiasedLinearity*>(mNetComponents[2 * l]);
-    if (lin->LearnRate() > 0.0f) lin->ApplyGradient(grows);
+    if (lin->LearnRate() > 0.0f) {
+      lin->ApplyGradient(grows, nullptr, &exchange);
+      exchange.GatherParams(*lin, j++, nullptr);
+    }
     if (lin == mpPropagErrorStopper) break;
   }
 }
@@ -386,8 +392,12 @@ void CuNetwork::TrainBunch(const CuMatrix<BaseFloat>& X, const CuVector<int>& la
         // the layer's SGD update right behind its reduction, beside the backward GEMMs below (W_l is
         // read for the last time by this layer's backward GEMM, already enqueued)
         void* as = submitted.empty() ? exchange->ApplyStream(n_submitted) : nullptr;
-        if (as) lin->ApplyGradient(grows, as);
-        else submitted.push_back(lin);
+        if (as) {
+          lin->ApplyGradient(grows, as, exchange);
+          exchange->GatherParams(*lin, n_submitted, as);  // sharded apply: the other ranks' shards
+        } else {
+          submitted.push_back(lin);
+        }
         n_submitted++;
       } else if (err_colsum) {
         lin->UpdateFromColsum(*acts[l], *err, *mColPart[l]);
@@ -405,7 +415,8 @@ void CuNetwork::TrainBunch(const CuMatrix<BaseFloat>& X, const CuVector<int>& la
     const int first = n_submitted - (int)submitted.size();
     for (size_t i = 0; i < submitted.size(); i++) {
       exchange->WaitFor(first + (int)i);
-      submitted[i]->ApplyGradient(grows);
+      submitted[i]->ApplyGradient(grows, nullptr, exchange);
+      exchange->GatherParams(*submitted[i], first + (int)i, nullptr);
     }
     exchange->WaitAll();
   }

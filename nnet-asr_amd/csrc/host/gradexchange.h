@@ -43,6 +43,40 @@ class GradExchange {
   /// Sum small host statistics over ranks (epoch-end MergeStats, step planning); blocking.
   virtual void AllReduceHost(double* v, int n) = 0;
 
+  // ---- sharded apply (ZeRO-1 style: reduce-scatter, each rank updates its shard, all-gather)
+  /// The element ranges [lo[k], hi[k]) of an n-element block this rank applies after the block's
+  /// reduction; returns the range count (<= 2).  Default: the whole block.
+  virtual int ApplyRanges(long n, long* lo, long* hi) const { return FullRange(n, lo, hi); }
+  /// After submission i's applies were enqueued (on `stream`; nullptr = the compute stream): bring
+  /// every rank's updated elements of comp's parameter blocks.  No-op without sharding.
+  virtual void GatherParams(CuUpdatableComponent& comp, int i, void* stream) {
+    (void)comp;
+    (void)i;
+    (void)stream;
+  }
+  static int FullRange(long n, long* lo, long* hi) {
+    lo[0] = 0;
+    hi[0] = n;
+    return 1;
+  }
+  /// The shard split of an n-element block over `world` ranks: rank r owns [r c, (r + 1) c) with c
+  /// a multiple of 4 elements (16-byte aligned shards), every rank also applies the tail [world c, n)
+  /// (fewer than 4 world elements, all-reduced whole).  Returns c.
+  static long ShardChunk(long n, int world) { return (n / (4L * world)) * 4L; }
+  static int ShardRanges(long n, int rank, int world, long* lo, long* hi) {
+    const long c = ShardChunk(n, world), main = c * world;
+    int k = 0;
+    if (c > 0) {
+      lo[k] = rank * c;
+      hi[k++] = rank * c + c;
+    }
+    if (main < n) {
+      lo[k] = main;
+      hi[k++] = n;
+    }
+    return k;
+  }
+
   /// Frames of the global bunch (sum over ranks) for the GRADDIVFRM normalisation: the row
   /// count planned for this step (SetStepRows), else every rank is assumed to hold local_rows.
   size_t GlobalRows(size_t local_rows) const {

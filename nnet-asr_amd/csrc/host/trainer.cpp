@@ -196,6 +196,36 @@ DpRoundPlan DpPlanRound(GradExchange& ex, long n, bool final) {
 // ======================================================================================
 // host-transport exchange
 // ======================================================================================
+static bool shard_env(bool dflt) {
+  const char* e = getenv("TNET_DP_SHARD");
+  return e ? e[0] == '1' : dflt;
+}
+
+HostExchange::HostExchange(int rank, int world, HostAllReduceFn fn, void* user)
+    : mRank(rank), mWorld(world), mShard(shard_env(false)), mFn(fn), mUser(user) {}
+
+int HostExchange::ApplyRanges(long n, long* lo, long* hi) const {
+  return mShard ? ShardRanges(n, mRank, mWorld, lo, hi) : FullRange(n, lo, hi);
+}
+
+void HostExchange::GatherParams(CuUpdatableComponent& comp, int i, void* stream) {
+  (void)i;
+  if (!mShard) return;
+  CuDevice& dev = CuDevice::Instantiate();
+  TNET_HIP_CALL(hipStreamSynchronize(stream ? (hipStream_t)stream : dev.Stream()));
+  for (auto& b : comp.GradientBlocks()) {
+    mStage.resize((size_t)b.n);
+    TNET_HIP_CALL(hipMemcpy(mStage.data(), b.param, (size_t)b.n * sizeof(float), hipMemcpyDeviceToHost));
+    const long c = ShardChunk(b.n, mWorld), main = c * mWorld;
+    for (long k = 0; k < b.n; ++k) {
+      const bool mine = k < main ? (k / c) == mRank : mRank == 0;
+      if (!mine) mStage[(size_t)k] = 0.f;
+    }
+    if (mFn(mUser, mStage.data(), b.n, 0) != 0) Error("HostExchange: all-reduce callback failed");
+    TNET_HIP_CALL(hipMemcpy(b.param, mStage.data(), (size_t)b.n * sizeof(float), hipMemcpyHostToDevice));
+  }
+}
+
 void HostExchange::Submit(CuUpdatableComponent& comp) {
   CuDevice& dev = CuDevice::Instantiate();
   TNET_HIP_CALL(hipStreamSynchronize(dev.Stream()));
@@ -241,6 +271,7 @@ struct RcclExchange::Impl {
   hipStream_t apply_stream = nullptr;
   hipEvent_t apply_done = nullptr;
   bool applied = false;
+  std::vector<hipEvent_t> gather_ev;  // apply stream -> comm stream (a layer's shard applied), per submit
   double* dscratch = nullptr;
 };
 
@@ -251,7 +282,8 @@ void RcclExchange::UniqueId(char out[128]) {
   std::memcpy(out, &id, 128);
 }
 
-RcclExchange::RcclExchange(int rank, int world, const char id[128]) : mImpl(new Impl), mRank(rank), mWorld(world) {
+RcclExchange::RcclExchange(int rank, int world, const char id[128])
+    : mImpl(new Impl), mRank(rank), mWorld(world), mShard(shard_env(world > 1)) {
   CuDevice& dev = CuDevice::Instantiate();
   ncclUniqueId uid;
   std::memcpy(&uid, id, 128);
@@ -270,6 +302,7 @@ RcclExchange::~RcclExchange() {
   if (mImpl->apply_stream) (void)hipStreamSynchronize(mImpl->apply_stream);
   for (auto e : mImpl->events) (void)hipEventDestroy(e);
   for (auto e : mImpl->ar_done) (void)hipEventDestroy(e);
+  for (auto e : mImpl->gather_ev) (void)hipEventDestroy(e);
   if (mImpl->done) (void)hipEventDestroy(mImpl->done);
   if (mImpl->apply_done) (void)hipEventDestroy(mImpl->apply_done);
   if (mImpl->apply_stream) (void)hipStreamDestroy(mImpl->apply_stream);
@@ -294,10 +327,49 @@ void RcclExchange::Submit(CuUpdatableComponent& comp) {
   TNET_HIP_CALL(hipStreamWaitEvent(mImpl->comm_stream, ev, 0));
   std::vector<CuParamBlock> blocks = comp.GradientBlocks();
   NCCL_CALL(ncclGroupStart());
-  for (auto& b : blocks)
-    NCCL_CALL(ncclAllReduce(b.grad, b.grad, (size_t)b.n, ncclFloat, ncclSum, mImpl->comm, mImpl->comm_stream));
+  for (auto& b : blocks) {
+    if (!mShard) {
+      NCCL_CALL(ncclAllReduce(b.grad, b.grad, (size_t)b.n, ncclFloat, ncclSum, mImpl->comm, mImpl->comm_stream));
+      continue;
+    }
+    // in place: this rank's reduced shard lands at grad + rank * c; the tail is reduced whole
+    const long c = ShardChunk(b.n, mWorld), main = c * mWorld;
+    if (c > 0)
+      NCCL_CALL(ncclReduceScatter(b.grad, b.grad + (long)mRank * c, (size_t)c, ncclFloat, ncclSum, mImpl->comm,
+                                  mImpl->comm_stream));
+    if (main < b.n)
+      NCCL_CALL(ncclAllReduce(b.grad + main, b.grad + main, (size_t)(b.n - main), ncclFloat, ncclSum, mImpl->comm,
+                              mImpl->comm_stream));
+  }
   NCCL_CALL(ncclGroupEnd());
   TNET_HIP_CALL(hipEventRecord(mImpl->ar_done[idx], mImpl->comm_stream));
+}
+
+int RcclExchange::ApplyRanges(long n, long* lo, long* hi) const {
+  return mShard ? ShardRanges(n, mRank, mWorld, lo, hi) : FullRange(n, lo, hi);
+}
+
+void RcclExchange::GatherParams(CuUpdatableComponent& comp, int i, void* stream) {
+  if (!mShard) return;
+  if (i < 0 || (size_t)i >= mImpl->next_event) Error("RcclExchange::GatherParams: no such reduction");
+  // the comm stream waits for this layer's applies (their stream), then all-gathers the shards in
+  // place: the next collectives queue behind it, the compute stream joins at WaitAll
+  if (mImpl->gather_ev.size() <= (size_t)i) {
+    hipEvent_t e;
+    TNET_HIP_CALL(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    mImpl->gather_ev.push_back(e);
+  }
+  hipEvent_t ev = mImpl->gather_ev[(size_t)i];
+  TNET_HIP_CALL(hipEventRecord(ev, stream ? (hipStream_t)stream : CuDevice::Instantiate().Stream()));
+  TNET_HIP_CALL(hipStreamWaitEvent(mImpl->comm_stream, ev, 0));
+  NCCL_CALL(ncclGroupStart());
+  for (auto& b : comp.GradientBlocks()) {
+    const long c = ShardChunk(b.n, mWorld);
+    if (c > 0)
+      NCCL_CALL(ncclAllGather(b.param + (long)mRank * c, b.param, (size_t)c, ncclFloat, mImpl->comm,
+                              mImpl->comm_stream));
+  }
+  NCCL_CALL(ncclGroupEnd());
 }
 
 void RcclExchange::WaitFor(int i) {

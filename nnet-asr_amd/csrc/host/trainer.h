@@ -97,17 +97,23 @@ class CuTrainer {
 typedef int (*HostAllReduceFn)(void* user, void* buf, long n, int is_double);
 class HostExchange : public GradExchange {
  public:
-  HostExchange(int rank, int world, HostAllReduceFn fn, void* user)
-      : mRank(rank), mWorld(world), mFn(fn), mUser(user) {}
+  HostExchange(int rank, int world, HostAllReduceFn fn, void* user);
   int Rank() const override { return mRank; }
   int WorldSize() const override { return mWorld; }
   void Submit(CuUpdatableComponent& comp) override;
   void WaitAll() override {}
   void AllReduceHost(double* v, int n) override;
   void AllReduceDevice(float* buf, size_t n);
+  /// TNET_DP_SHARD=1: the sharded-apply protocol of RcclExchange emulated through the host
+  /// all-reduce (full reduction; each rank applies its ranges; the parameter blocks are then summed
+  /// with every element outside the rank's shard zeroed, rank 0 contributing the tails) -- a test
+  /// of the shard split on one device, not a fast path
+  int ApplyRanges(long n, long* lo, long* hi) const override;
+  void GatherParams(CuUpdatableComponent& comp, int i, void* stream) override;
 
  private:
   int mRank, mWorld;
+  bool mShard = false;
   HostAllReduceFn mFn;
   void* mUser;
   std::vector<float> mStage;
@@ -128,11 +134,18 @@ class RcclExchange : public GradExchange {
   void AllReduceHost(double* v, int n) override;
   /// all-reduce (sum) of a device float buffer on the communication stream, synchronous
   void AllReduceDevice(float* buf, size_t n);
+  /// Sharded apply (world > 1 unless TNET_DP_SHARD=0; TNET_DP_SHARD=1 also at world 1): Submit
+  /// reduce-scatters each gradient block (ShardRanges; the tail all-reduced), the rank applies its
+  /// shard, GatherParams all-gathers the updated parameters in place on the communication stream --
+  /// the apply's HBM traffic divided by the world size, the same bytes over xGMI as an all-reduce
+  int ApplyRanges(long n, long* lo, long* hi) const override;
+  void GatherParams(CuUpdatableComponent& comp, int i, void* stream) override;
 
  private:
   struct Impl;
   std::unique_ptr<Impl> mImpl;
   int mRank, mWorld;
+  bool mShard = false;
 };
 
 }  // namespace TNet

@@ -28,9 +28,9 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _run_ranks(mode, tmp_path, world=2):
+def _run_ranks(mode, tmp_path, world=2, shard="0"):
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), WORLD_SIZE=str(world),
-               OMP_NUM_THREADS="1")
+               OMP_NUM_THREADS="1", TNET_DP_SHARD=shard)
     outs = [str(tmp_path / f"{mode}_r{r}.npz") for r in range(world)]
     procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "dp_worker.py"), mode, outs[r]],
                               env=dict(env, RANK=str(r)), stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
@@ -56,23 +56,30 @@ def _assert_params(got, net, rtol=2e-4, atol=1e-6):
         np.testing.assert_allclose(got[f"b{k}"], net.b[k], rtol=rtol, atol=atol)
 
 
-def test_dp_network_two_ranks_matches_global_bunch(tmp_path):
+@pytest.mark.parametrize("world,shard", [(2, "0"), (2, "1"), (3, "1")])
+def test_dp_network_ranks_match_global_bunch(tmp_path, world, shard):
+    """shard "1": the sharded apply (reduce, each rank updates its shard + the tails, the parameter
+    blocks gathered back) -- RcclExchange's protocol, emulated over the host transport; world 3
+    leaves tails (blocks whose size is not a multiple of 4 x 3 elements)"""
     c = dp_cases.NET
-    ranks = _run_ranks("net", tmp_path)
+    ranks = _run_ranks("net", tmp_path, world, shard)
     # every rank holds identical parameters
-    for k in ranks[0][1]:
-        np.testing.assert_array_equal(ranks[0][1][k], ranks[1][1][k])
+    for r in range(1, world):
+        for k in ranks[0][1]:
+            np.testing.assert_array_equal(ranks[0][1][k], ranks[r][1][k])
     net = orc.MLP.from_layers(formats.gen_mlp_init(c["dims"], seed=c["init_seed"]))
-    for X, L, _ in dp_cases.net_bunches(2):
+    for X, L, _ in dp_cases.net_bunches(world):
         net.step(X, L, c["lr"], graddivfrm=True)
     _assert_params(ranks[0][1], net)
     assert ranks[0][0]["frames"] == c["bunch"] * c["steps"]
-    assert ranks[1][0]["frames"] == c["bunch"] * (c["steps"] - 1)
+    for r in range(1, world):
+        assert ranks[r][0]["frames"] == c["bunch"] * (c["steps"] - 1)
 
 
-def test_dp_trainer_uneven_shards(tmp_path):
+@pytest.mark.parametrize("shard", ["0", "1"])
+def test_dp_trainer_uneven_shards(tmp_path, shard):
     c = dp_cases.TRAINER
-    ranks = _run_ranks("trainer", tmp_path)
+    ranks = _run_ranks("trainer", tmp_path, 2, shard)
     for k in ranks[0][1]:
         np.testing.assert_array_equal(ranks[0][1][k], ranks[1][1][k])
     corpus = dp_cases.trainer_corpus()
@@ -89,10 +96,13 @@ def test_dp_trainer_uneven_shards(tmp_path):
     assert ranks[0][0]["frames"] + ranks[1][0]["frames"] == net.frames
 
 
-def test_dp_rccl_world1_equals_local_update():
+@pytest.mark.parametrize("shard", ["0", "1"])
+def test_dp_rccl_world1_equals_local_update(monkeypatch, shard):
     """RCCL communicator at world 1: the split ComputeGradient -> all-reduce -> ApplyGradient path
-    gives the fused local update's result."""
+    gives the fused local update's result (shard "1": the reduce-scatter -> shard apply -> in-place
+    all-gather form, one rank)."""
     c = dp_cases.NET
+    monkeypatch.setenv("TNET_DP_SHARD", shard)
     comm = Comm(0, 1, Comm.unique_id())
     nets = []
     for use_comm in (False, True):
