@@ -203,43 +203,35 @@ void CuNetwork::TrainBunchGeneric(const CuMatrix<BaseFloat>& X, const CuVector<i
 void CuNetwork::TrainEmpty(GradExchange& exchange) {
   if (!IsFusableMLP()) Error("CuNetwork::TrainEmpty: data-parallel training needs the sigmoid-MLP topology");
   const int nl = (int)mNetComponents.size() / 2;
-  // same layer order (top down to the stopper) as TrainBunch, so the collectives pair up
+  const size_t grows = exchange.GlobalRows(0);
+  // the collectives in TrainBunch's order (top down to the stopper; a layer's reduction, then -- with
+  // an apply stream -- its apply and parameter gather before the next layer's reduction), so every
+  // rank issues the same sequence whether it trained a bunch or not
+  std::vector<CuBiasedLinearity*> submitted;
+  int n_submitted = 0;
   for (int l = nl - 1; l >= 0; l--) {
     auto* lin = static_cast<CuBiasedLinearity*>(mNetComponents[2 * l]);
     if (lin->LearnRate() > 0.0f) {
       lin->ZeroGradient();
       exchange.Submit(*lin);
+      void* as = submitted.empty() ? exchange.ApplyStream(n_submitted) : nullptr;
+      if (as) {
+        lin->ApplyGradient(grows, as, &exchange);
+        exchange.GatherParams(*lin, n_submitted, as);
+      } else {
+        submitted.push_back(lin);
+      }
+      n_submitted++;
     }
     if (lin == mpPropagErrorStopper) break;
   }
-  const size_t grows = exchange.GlobalRows(0);
-  int i = 0;
-  bool inline_apply = true;
-  for (int l = nl - 1; l >= 0; l--) {  // applies beside the reductions where the transport allows
-    auto* lin = static_cast<CuBiasedLinearity*>(mNetComponents[2 * l]);
-    if (lin->LearnRate() > 0.0f) {
-      void* as = exchange.ApplyStream(i);
-      if (!as) {
-        inline_apply = false;
-        break;
-      }
-      lin->ApplyGradient(grows, as, &exchange);
-      exchange.GatherParams(*lin, i, as);
-      i++;
-    }
-    if (lin == mpPropagErrorStopper) break;
+  const int first = n_submitted - (int)submitted.size();
+  for (size_t i = 0; i < submitted.size(); i++) {
+    exchange.WaitFor(first + (int)i);
+    submitted[i]->ApplyGradient(grows, nullptr, &exchange);
+    exchange.GatherParams(*submitted[i], first + (int)i, nullptr);
   }
   exchange.WaitAll();
-  if (inline_apply) return;
-  int j = 0;
-  for (int l = nl - 1; l >= 0; l--) {
-    auto* lin = static_cast<CuBiasedLinearity*>(mNetComponents[2 * l]);
-    if (lin->LearnRate() > 0.0f) {
-      lin->ApplyGradient(grows, nullptr, &exchange);
-      exchange.GatherParams(*lin, j++, nullptr);
-    }
-    if (lin == mpPropagErrorStopper) break;
-  }
 }
 
 void CuUpdatableComponent::ZeroGradient() {
