@@ -202,7 +202,13 @@ static bool shard_env(bool dflt) {
 }
 
 HostExchange::HostExchange(int rank, int world, HostAllReduceFn fn, void* user)
-    : mRank(rank), mWorld(world), mShard(shard_env(false)), mFn(fn), mUser(user) {}
+    : mRank(rank), mWorld(world), mShard(shard_env(false)),
+      mInline(getenv("TNET_DP_HOST_INLINE") && getenv("TNET_DP_HOST_INLINE")[0] == '1'), mFn(fn), mUser(user) {}
+
+void* HostExchange::ApplyStream(int i) {
+  (void)i;
+  return mInline ? (void*)CuDevice::Instantiate().Stream() : nullptr;
+}
 
 int HostExchange::ApplyRanges(long n, long* lo, long* hi) const {
   return mShard ? ShardRanges(n, mRank, mWorld, lo, hi) : FullRange(n, lo, hi);

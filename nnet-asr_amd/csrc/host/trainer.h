@@ -110,10 +110,15 @@ class HostExchange : public GradExchange {
   /// of the shard split on one device, not a fast path
   int ApplyRanges(long n, long* lo, long* hi) const override;
   void GatherParams(CuUpdatableComponent& comp, int i, void* stream) override;
+  /// TNET_DP_HOST_INLINE=1: hand out the compute stream as the apply stream (Submit is synchronous,
+  /// so the layer's reduction is done), which puts CuNetwork on the per-layer reduce -> apply ->
+  /// gather order RcclExchange takes -- tests of that collective order with several ranks
+  void* ApplyStream(int i) override;
 
  private:
   int mRank, mWorld;
   bool mShard = false;
+  bool mInline = false;
   HostAllReduceFn mFn;
   void* mUser;
   std::vector<float> mStage;

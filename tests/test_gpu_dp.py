@@ -28,9 +28,9 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _run_ranks(mode, tmp_path, world=2, shard="0"):
+def _run_ranks(mode, tmp_path, world=2, shard="0", inline="0"):
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), WORLD_SIZE=str(world),
-               OMP_NUM_THREADS="1", TNET_DP_SHARD=shard)
+               OMP_NUM_THREADS="1", TNET_DP_SHARD=shard, TNET_DP_HOST_INLINE=inline)
     outs = [str(tmp_path / f"{mode}_r{r}.npz") for r in range(world)]
     procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "dp_worker.py"), mode, outs[r]],
                               env=dict(env, RANK=str(r)), stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
@@ -56,13 +56,13 @@ def _assert_params(got, net, rtol=2e-4, atol=1e-6):
         np.testing.assert_allclose(got[f"b{k}"], net.b[k], rtol=rtol, atol=atol)
 
 
-@pytest.mark.parametrize("world,shard", [(2, "0"), (2, "1"), (3, "1")])
-def test_dp_network_ranks_match_global_bunch(tmp_path, world, shard):
+@pytest.mark.parametrize("world,shard,inline", [(2, "0", "0"), (2, "1", "0"), (3, "1", "0"), (3, "1", "1")])
+def test_dp_network_ranks_match_global_bunch(tmp_path, world, shard, inline):
     """shard "1": the sharded apply (reduce, each rank updates its shard + the tails, the parameter
     blocks gathered back) -- RcclExchange's protocol, emulated over the host transport; world 3
     leaves tails (blocks whose size is not a multiple of 4 x 3 elements)"""
     c = dp_cases.NET
-    ranks = _run_ranks("net", tmp_path, world, shard)
+    ranks = _run_ranks("net", tmp_path, world, shard, inline)
     # every rank holds identical parameters
     for r in range(1, world):
         for k in ranks[0][1]:
@@ -76,10 +76,13 @@ def test_dp_network_ranks_match_global_bunch(tmp_path, world, shard):
         assert ranks[r][0]["frames"] == c["bunch"] * (c["steps"] - 1)
 
 
-@pytest.mark.parametrize("shard", ["0", "1"])
-def test_dp_trainer_uneven_shards(tmp_path, shard):
+@pytest.mark.parametrize("shard,inline", [("0", "0"), ("1", "0"), ("1", "1")])
+def test_dp_trainer_uneven_shards(tmp_path, shard, inline):
+    """inline "1": every layer's reduction, apply and parameter gather in turn (RcclExchange's order),
+    with one rank training bunches while the other joins with zero gradients (TrainEmpty): the two
+    must issue the same collective sequence or the host all-reduces pair up wrongly"""
     c = dp_cases.TRAINER
-    ranks = _run_ranks("trainer", tmp_path, 2, shard)
+    ranks = _run_ranks("trainer", tmp_path, 2, shard, inline)
     for k in ranks[0][1]:
         np.testing.assert_array_equal(ranks[0][1][k], ranks[1][1][k])
     corpus = dp_cases.trainer_corpus()
