@@ -100,6 +100,12 @@ def parse_kernel_report(text):
     return out
 
 
+def dp_mode(world):
+    """the RCCL exchange's form (RcclExchange: sharded apply at N > 1 unless TNET_DP_SHARD=0)"""
+    shard = os.environ.get("TNET_DP_SHARD", "1" if world > 1 else "0") == "1"
+    return (" (RCCL reduce-scatter, sharded SGD apply, all-gather)" if shard else " (RCCL all-reduce)")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -262,7 +268,7 @@ def main():
             "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
             "config": {"workload": f"TNet SGD step, {'x'.join(map(str, dims))} sigmoid MLP + softmax xent",
                        "bunch_per_gpu": B, "global_bunch": B * world, "frames_resident_per_gpu": args.cache,
-                       "parallelism": f"dp{world}" + ((" (RCCL all-reduce)" if args.comm == "rccl" else
+                       "parallelism": f"dp{world}" + ((dp_mode(world) if args.comm == "rccl" else
                                                        " (host all-reduce rehearsal)")
                                                       if world > 1 or args.force_dp else ""),
                        "flops_per_frame": flops_per_frame(dims),
