@@ -77,11 +77,9 @@ def _run_platform(files, init, bunch, cache, threads, seed=123, lr=1e-4):
     cmd = [REF_HARNESS, "train", init, files["scp"], files["mlf"], files["states"], "*/", str(threads), str(bunch),
            str(cache), repr(lr), str(seed)]
     p = subprocess.run(cmd, capture_output=True, text=True, env=env)
-    if p.returncode != 0:
-        raise RuntimeError(f"reference Platform training failed: {p.stderr[-2000:]}")
     m = re.search(r"HARNESS_RESULT frames (\d+) seconds ([0-9.e+-]+)", p.stderr)
-    if not m:
-        raise RuntimeError(f"reference Platform training printed no result: {p.stderr[-1000:]}")
+    if not m:  # (a result line is complete: the timed loop had finished when it was printed)
+        raise RuntimeError(f"reference Platform training failed (rc {p.returncode}): {p.stderr[-2000:]}")
     return int(m.group(1)), float(m.group(2))
 
 
