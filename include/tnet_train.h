@@ -171,6 +171,11 @@ TnetComm* tnet_comm_create_host(int rank, int world, tnet_host_allreduce_fn fn, 
  * ranks are final.  Pure host logic. */
 int tnet_dp_plan_round(TnetComm* comm, long n, int final, long* steps, int* ranks_at_step, long cap,
                        int* all_final);
+/* The sharded apply's split of an n-element parameter block over `world` ranks (what the RCCL
+ * communicator reduce-scatters / all-gathers; a maintainer's own transport needs the same split):
+ * rank r updates [lo[k], hi[k]) for k < *count (<= 2): its shard [r c, (r + 1) c), c a multiple of
+ * 4 elements, and the tail [world c, n) that every rank updates.  Pure host logic. */
+int tnet_dp_shard_ranges(long n, int rank, int world, long* lo, long* hi, int* count);
 /* Network-level data parallelism: tnet_net_train_bunch all-reduces the weight gradients over
  * comm (NULL = local update); a rank without a bunch calls tnet_net_train_empty with the global
  * row count of the step. */

@@ -573,6 +573,12 @@ int tnet_dp_plan_round(TnetComm* c, long n, int final, long* steps, int* ranks_a
   for (long j = 0; j < plan.steps; j++) ranks_at_step[j] = plan.ranks_at_step[(size_t)j];
   TRY_END
 }
+int tnet_dp_shard_ranges(long n, int rank, int world, long* lo, long* hi, int* count) {
+  TRY_BEGIN if (n < 0 || world < 1 || rank < 0 || rank >= world || !lo || !hi || !count)
+      Error("tnet_dp_shard_ranges: bad arguments");
+  *count = GradExchange::ShardRanges(n, rank, world, lo, hi);
+  TRY_END
+}
 int tnet_comm_free(TnetComm* c) {
   TRY_BEGIN delete c;
   TRY_END

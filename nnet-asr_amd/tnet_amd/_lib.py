@@ -188,6 +188,7 @@ _SIGS = {
     "tnet_rand_binarize": (i32, [vp, i32, vp, MatrixDim, vp, vp, vp, vp, vp]),
     "tnet_add_gauss_noise": (i32, [vp, MatrixDim, f32, vp, vp, vp, vp, vp]),
     "tnet_dp_plan_round": (i32, [vp, i64, i32, C.POINTER(i64), C.POINTER(i32), i64, C.POINTER(i32)]),
+    "tnet_dp_shard_ranges": (i32, [i64, i32, i32, C.POINTER(i64), C.POINTER(i64), C.POINTER(i32)]),
     "tnet_net_set_comm": (i32, [vp, vp]),
     "tnet_comm_set_step_rows": (i32, [vp, i64]),
     "tnet_net_train_empty": (i32, [vp, vp, i64]),

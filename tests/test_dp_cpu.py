@@ -89,3 +89,33 @@ def test_dp_plan_gloo_world2():
         assert got == [[len(s) for s in rnd] for rnd in expected]
         assert [f for _, f in o["rounds"]] == [False] * (len(expected) - 1) + [True]
         assert o["sum"] == [3.0, 4.0]
+
+
+@pytest.mark.parametrize("n", [0, 1, 3, 4, 7, 12, 23, 96, 135, 440 * 2048, 2048 * 4000 + 5])
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+def test_shard_ranges_cover_every_element_once(n, world):
+    """the sharded apply's split (trainer/gradexchange ShardRanges through tnet_dp_shard_ranges):
+    the ranks' shards are disjoint, 16-byte aligned and equal; the tail (applied by every rank) and
+    the shards together cover [0, n) exactly once per element"""
+    import ctypes as C
+    sys.path.insert(0, os.path.join(os.path.dirname(HERE), "nnet-asr_amd"))
+    from tnet_amd._lib import check, lib
+    owner = np.zeros(n, np.int32)
+    tails = []
+    for r in range(world):
+        lo, hi, cnt = (C.c_long * 2)(), (C.c_long * 2)(), C.c_int()
+        check(lib().tnet_dp_shard_ranges(n, r, world, lo, hi, C.byref(cnt)))
+        rng = [(lo[k], hi[k]) for k in range(cnt.value)]
+        for a, b in rng:
+            assert 0 <= a <= b <= n
+        c = (n // (4 * world)) * 4
+        if c > 0:
+            assert rng[0] == (r * c, r * c + c) and (r * c) % 4 == 0
+            owner[r * c:r * c + c] += 1
+        tail = [t for t in rng if t[0] >= c * world]
+        tails.append(tail)
+    main = (n // (4 * world)) * 4 * world
+    assert all(t == tails[0] for t in tails)
+    assert tails[0] == ([(main, n)] if main < n else [])
+    owner[main:] += 1
+    assert np.all(owner == 1)
