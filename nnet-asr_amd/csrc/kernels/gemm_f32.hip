@@ -79,6 +79,7 @@ struct GemmP {
   int ksplit;
   long kstepA, kstepB, slabC;
   int early_issue;  // gemm16_kernel prologue: issue all S ring slots before the first wait (TNET_GEMM_EARLY)
+  int wt;           // gemm16_kernel epilogue: 16-B output stores write-through (sc1) (TNET_GEMM_WT)
   // in-launch split-K combine (gemm16_kernel EPI_T >= kEpiInLaunch): the last slice of a tile to
   // finish sums the tile's slices (C is the slice workspace, rows of ldc) and applies the epilogue
   // into C2 / ldc2 with alpha2 / beta2; the other epilogue operands are the fields above
@@ -343,6 +344,18 @@ __device__ __forceinline__ void wait_vmcnt_le(int n) {
   } else {
     if (n >= N) wait_vmcnt<N>();
     else wait_vmcnt_le<N - 1>(n);
+  }
+}
+
+// s_waitcnt vmcnt(n) for a wave-uniform runtime n in [LO, HI] (binary search over the immediates)
+template <int LO, int HI>
+__device__ __forceinline__ void wait_vmcnt_bin(int n) {
+  if constexpr (LO >= HI) {
+    wait_vmcnt<LO>();
+  } else {
+    constexpr int MID = (LO + HI) / 2;
+    if (n <= MID) wait_vmcnt_bin<LO, MID>(n);
+    else wait_vmcnt_bin<MID + 1, HI>(n);
   }
 }
 
@@ -669,7 +682,10 @@ __device__ __forceinline__ void lds_vec(const float* p, float (&x)[4]) {
 // EPI_T >= kEpiInLaunch: a split-K slice kernel (EPI_STORE into the workspace) whose tiles' last
 // slices combine the slices with epilogue EPI_T - kEpiInLaunch inside the launch
 constexpr int kEpiInLaunch = 32;
-template <int BM, int BN, int BK, int WM, int WN, int S, int SP, bool A_KC, bool B_KC, int EPI_T>
+// PX (exact prefetch): the tile grid covers M x N exactly and the epilogue operands are 16-B aligned
+// (launch_cfg checks), so the epilogue-operand prefetch is a known number of unconditional loads per
+// wave and the first seam waits for the ring only, not for them (TNET_GEMM_PRE0=0: off)
+template <int BM, int BN, int BK, int WM, int WN, int S, int SP, bool A_KC, bool B_KC, int EPI_T, bool PX = false>
 __global__ __launch_bounds__((WM * WN + (SP == 2)) * 64)
 __attribute__((amdgpu_waves_per_eu((WM * WN + (SP == 2) + 3) / 4, (WM * WN + (SP == 2) + 3) / 4)))
 void gemm16_kernel(const GemmP p_in) {
@@ -699,7 +715,9 @@ void gemm16_kernel(const GemmP p_in) {
   constexpr int GA = A_SZ / 4 / NT, GB = B_SZ / 4 / NT, G = GA + GB;
   static_assert(A_SZ % (4 * NT) == 0 && B_SZ % (4 * NT) == 0, "tile splits into 1-KiB wave pieces");
   static_assert(3 * G < 64, "vmcnt range");
-  __shared__ __attribute__((aligned(16))) float smem[S * ST_SZ];
+  // PX + bias epilogue: 32 slabs x 8 columns of bias-gradient slab sums after the ring (see PXB below)
+  constexpr bool PXB0 = PX && epi_bias_slabs(EPI_T);
+  __shared__ __attribute__((aligned(16))) float smem[S * ST_SZ + (PXB0 ? kBiasPreSlabs * 8 : 0)];
   TNET_STAMP_RT(4);
   TNET_STAMP(0);
 
@@ -939,6 +957,7 @@ void gemm16_kernel(const GemmP p_in) {
     if (!SP && !early) issue(min(S - 1, tlast), S - 1);
     read_frags(smem, 0, 0);
   }
+  asm volatile("" ::: "memory");  // the prefetch loads below stay younger than every prologue DMA piece
   // Epilogue operands (bias / y of the layer below / W and the momentum buffer) are loaded into
   // registers HERE, right after the prologue (issued inside the main loop at tile 1 instead, they
   // shortened the prologue by 3-4k cycles but stretched the main loop by 4-7k): the main loop hides their latency (a seam's counted
@@ -999,52 +1018,121 @@ void gemm16_kernel(const GemmP p_in) {
     return v;
   };
   const bool has_q = PRE_Q && p.corr != nullptr;
+  // exact prefetch (PX): every epilogue-operand load below is one unconditional
+  // 16-B load (or one 4-B slab-sum load), npre counts this wave's, and the first seam lets them stay
+  // in flight (vmcnt is in order: the npre youngest operations are exactly these loads)
+  constexpr bool PEX = !SP && !LDR && (!PRE_BIAS || NE == 4) && (TRE || !(PRE_C || PRE_AUX || PRE_Q) || NE == 4);
+  constexpr bool pex = PEX && PX;
+  int npre = 0;
   if constexpr (PRE_BIAS) {
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
       const int col = ecol(j);
       f32x4 v = {0.f, 0.f, 0.f, 0.f};
+      if (pex) {
+        v = *reinterpret_cast<const f32x4*>(p.bias + col);
+      } else {
 #pragma unroll
-      for (int e = 0; e < NE; ++e) v[e] = col + e < N ? p.bias[col + e] : 0.f;
+        for (int e = 0; e < NE; ++e) v[e] = col + e < N ? p.bias[col + e] : 0.f;
+      }
       pre_bias[j] = v;
     }
+    npre += NJ;
   }
   // tiles of more than 128 prefetched floats per lane (128x256 tiles) are loaded at the epilogue
   // instead, all at once (one round trip): held across the main loop they would spill
   constexpr int PRE_TILE = TM * 4 * NJ * NE;
   constexpr bool EARLY = ((PRE_C || PRE_AUX) ? PRE_TILE : 0) + (PRE_Q ? PRE_TILE : 0) <= 128;
   auto prefetch_tiles = [&]() {
+    auto ld16 = [&](const float* base, long ld, int row, int col) {
+      return *reinterpret_cast<const f32x4*>(base + (long)row * ld + col);
+    };
+    // one branch on pex around each operand's whole tile (not one per load)
     if constexpr (TRE) {
-      if constexpr (PRE_AUX)
+      if constexpr (PRE_AUX) {
+        if (pex) {
 #pragma unroll
-        for (int q = 0; q < TP; ++q) pre_t[q] = ld_row4(p.aux, p.ldaux, bm + wm0 + tr0 + RPP * q, bn + wn0 + 4 * tcq);
+          for (int q = 0; q < TP; ++q) pre_t[q] = ld16(p.aux, p.ldaux, bm + wm0 + tr0 + RPP * q, bn + wn0 + 4 * tcq);
+        } else {
+#pragma unroll
+          for (int q = 0; q < TP; ++q)
+            pre_t[q] = ld_row4(p.aux, p.ldaux, bm + wm0 + tr0 + RPP * q, bn + wn0 + 4 * tcq);
+        }
+        npre += TP;
+      }
     } else if constexpr (PRE_C || PRE_AUX) {
       const float* base = PRE_AUX ? p.aux : p.C;
       const long ld = PRE_AUX ? p.ldaux : p.ldc;
-#pragma unroll
-      for (int a = 0; a < TM; ++a)
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-#pragma unroll
-          for (int j = 0; j < NJ; ++j) pre_a[a][r][j] = ld_tile(base, ld, erow(a, r), ecol(j));
-    }
-    if constexpr (PRE_Q) {
-      if (has_q) {
+      if (pex) {
 #pragma unroll
         for (int a = 0; a < TM; ++a)
 #pragma unroll
           for (int r = 0; r < 4; ++r)
 #pragma unroll
-            for (int j = 0; j < NJ; ++j) pre_q[a][r][j] = ld_tile(p.corr, p.ldcorr, erow(a, r), ecol(j));
+            for (int j = 0; j < NJ; ++j) pre_a[a][r][j] = ld16(base, ld, erow(a, r), ecol(j));
+      } else {
+#pragma unroll
+        for (int a = 0; a < TM; ++a)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) pre_a[a][r][j] = ld_tile(base, ld, erow(a, r), ecol(j));
+      }
+      npre += TM * 4 * NJ;
+    }
+    if constexpr (PRE_Q) {
+      if (has_q) {
+        if (pex) {
+#pragma unroll
+          for (int a = 0; a < TM; ++a)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+#pragma unroll
+              for (int j = 0; j < NJ; ++j) pre_q[a][r][j] = ld16(p.corr, p.ldcorr, erow(a, r), ecol(j));
+        } else {
+#pragma unroll
+          for (int a = 0; a < TM; ++a)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+#pragma unroll
+              for (int j = 0; j < NJ; ++j) pre_q[a][r][j] = ld_tile(p.corr, p.ldcorr, erow(a, r), ecol(j));
+        }
+        npre += TM * 4 * NJ;
       }
     }
   };
   if constexpr (EARLY) prefetch_tiles();
 
   static_assert(!epi_bias_slabs(EPI) || BN <= NT, "one thread per bias column");
+  // The bias of the tile's BN columns (EPI_SGD_B / EPI_STORE_BG).  Without PX the first tile-row's
+  // workgroups do it all (bias_pre_load / _finish).  With PX (PXB) it is spread over the tile-rows:
+  // tile-row i owns columns [i*cpw, (i+1)*cpw) of the tile (cpw <= 8, launch_cfg checks), thread u loads
+  // slab u/8 of column u%8 -- ONE straight-line load per lane (+ b, + corr) issued with the prefetch
+  // above, so every workgroup carries the same small share and no seam waits for it; the slab sums
+  // meet in LDS after the main loop and thread u < cpw adds its column's 32 slab sums in fp64 in slab
+  // order (bias_pre_finish's arithmetic)
+  constexpr bool PXB = pex && epi_bias_slabs(EPI);
   BiasPre bpre;
-  if constexpr (epi_bias_slabs(EPI))
+  if constexpr (epi_bias_slabs(EPI) && !pex)
     if (bm == 0) bias_pre_load<BN, EPI == EPI_STORE_BG>(p, bn, bpre);
+  float pxb_v = 0.f, pxb_b = 0.f, pxb_q = 0.f;
+  int pxb_col = 0, pxb_cpw = 0;
+  if constexpr (PXB) {
+    const int nbm_ = M / BM, tr = bm / BM;
+    pxb_cpw = (BN + nbm_ - 1) / nbm_;
+    const int u = threadIdx.x, slab = u >> 3, cl = u & 7;
+    pxb_col = bn + min(tr * pxb_cpw + min(cl, pxb_cpw - 1), BN - 1);
+    pxb_v = p.bpart[(long)min(slab, p.bslabs - 1) * p.ldbpart + pxb_col];
+    npre += 1;
+    if constexpr (EPI != EPI_STORE_BG) {
+      pxb_b = p.bvec[pxb_col];
+      npre += 1;
+      if (p.bcorr) {
+        pxb_q = p.bcorr[pxb_col];
+        npre += 1;
+      }
+    }
+  }
 
   TNET_STAMP(1);
   // one fragment read (r < TM: operand A, else B) of chunk c of the slot at st into buffer buf
@@ -1120,7 +1208,12 @@ void gemm16_kernel(const GemmP p_in) {
         // hand over to tile t+1: own reads of tile t retired, tile t+1 landed, everyone past
         __builtin_amdgcn_sched_barrier(0);
         __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
-        if constexpr (!LDR) wait_vmcnt<SEAM_VM>();
+        if constexpr (!LDR) {
+          // seam 0 under PX: tile 1 only, the prefetch loads behind it may still be in flight
+          // (more than 63 - SEAM_VM of them: vmcnt saturates, the wait for 63 is still exact)
+          if (pex && t == 0) wait_vmcnt_bin<SEAM_VM, 63>(min(SEAM_VM + npre, 63));
+          else wait_vmcnt<SEAM_VM>();
+        }
 #ifdef TNET_GEMM_DIAG_NOBAR
         if constexpr (LDR) barrier();  // the loader wave meets the compute waves at every seam barrier
 #else
@@ -1263,10 +1356,33 @@ void gemm16_kernel(const GemmP p_in) {
     }
   }
 
-  if constexpr (epi_bias_slabs(EPI))
+  if constexpr (epi_bias_slabs(EPI) && !PXB)
     if (bm == 0) bias_pre_finish<BN, EPI == EPI_STORE_BG>(p, bn, bpre);
+  if constexpr (PXB) {
+    float* bsm = smem + S * ST_SZ;
+    const int u = threadIdx.x;
+    bsm[u] = (u >> 3) < p.bslabs ? pxb_v : 0.f;
+    __syncthreads();
+    if (u < pxb_cpw && (bm / BM) * pxb_cpw + u < BN) {
+      double sum = 0.0;
+#pragma unroll
+      for (int k = 0; k < kBiasPreSlabs; ++k) sum += (double)bsm[k * 8 + u];
+      float g = (float)sum;
+      if constexpr (EPI == EPI_STORE_BG) {
+        p.bvec[pxb_col] = g;
+      } else {
+        if (p.bcorr) {
+          g = g + p.bmmt * pxb_q;
+          p.bcorr[pxb_col] = g;
+        }
+        p.bvec[pxb_col] = pxb_b + p.bscale * g;
+      }
+    }
+  }
 
   if constexpr (!EARLY) prefetch_tiles();
+  const __amdgpu_buffer_rsrc_t rs_c = tile_rsrc(p.C + (long)bm * p.ldc + bn);
+  const __amdgpu_buffer_rsrc_t rs_q = tile_rsrc(p.corr ? p.corr + (long)bm * p.ldcorr + bn : p.C);
   constexpr bool CS = EPI == EPI_DSIG_CS;
   static_assert(!CS || (A_KC && B_KC && WTM == kColsumSlabRows), "column sums: bwd layout, 32-row wave tiles");
   if constexpr (TRE) {
@@ -1302,7 +1418,8 @@ void gemm16_kernel(const GemmP p_in) {
       }
       float* cp = p.C + (long)row * p.ldc + col;
       if (col + 3 < N) {
-        *reinterpret_cast<f32x4*>(cp) = o;
+        if (p.wt) st_wt(rs_c, (long)(row - bm) * p.ldc + (col - bn), o);
+        else *reinterpret_cast<f32x4*>(cp) = o;
       } else {
 #pragma unroll
         for (int e = 0; e < 4; ++e)
@@ -1391,8 +1508,14 @@ void gemm16_kernel(const GemmP p_in) {
         float* cp = p.C + (long)row * p.ldc + col;
         float* qp = has_q ? p.corr + (long)row * p.ldcorr + col : nullptr;
         if (NE == 4 && col + 3 < N) {
-          *reinterpret_cast<f32x4*>(cp) = o;
-          if (has_q) *reinterpret_cast<f32x4*>(qp) = qn;
+          if (p.wt) {
+            const long eo = (long)(row - bm) * p.ldc + (col - bn);
+            st_wt(rs_c, eo, o);
+            if (has_q) st_wt(rs_q, (long)(row - bm) * p.ldcorr + (col - bn), qn);
+          } else {
+            *reinterpret_cast<f32x4*>(cp) = o;
+            if (has_q) *reinterpret_cast<f32x4*>(qp) = qn;
+          }
         } else if (NE == 2 && col + 1 < N) {
           *reinterpret_cast<float2*>(cp) = float2{o[0], o[1]};
           if (has_q) *reinterpret_cast<float2*>(qp) = float2{qn[0], qn[1]};
@@ -1711,6 +1834,8 @@ static int g_early = 1;   // TNET_GEMM_EARLY=0: prologue issues S-1 slots before
 // 14.6 us, the RBM reconstruction 256 x 440 over K = 2048 20.7 vs 14.4 us, MLP3 10.45M vs 10.96M
 // frames/s: the agent-scope release (L2 write-back) + acquire cost more than the launch boundary
 static int g_inlaunch = 0;
+static int g_pre0 = 1;  // TNET_GEMM_PRE0=0: the first seam also waits for the epilogue-operand prefetch
+static int g_wt = 1;  // TNET_GEMM_WT=0: plain 16-B epilogue stores instead of write-through (sc1; measured +1.4 % frames/s)
 static int forced_cfg() {
   if (g_cfg == -2) {
     g_cfg = -1;
@@ -1724,6 +1849,10 @@ static int forced_cfg() {
     if (sk) g_split = atoi(sk);
     const char* ea = getenv("TNET_GEMM_EARLY");
     if (ea) g_early = atoi(ea);
+    const char* p0 = getenv("TNET_GEMM_PRE0");
+    if (p0) g_pre0 = atoi(p0);
+    const char* wt = getenv("TNET_GEMM_WT");
+    if (wt) g_wt = atoi(wt);
     const char* il = getenv("TNET_SPLITK_INLAUNCH");
     if (il) g_inlaunch = atoi(il);
   }
@@ -1745,6 +1874,29 @@ static bool launch_cfg(const GemmP& p, hipStream_t st) {
     const dim3 grid(tiles, p.ksplit > 1 ? p.ksplit : 1);
     GemmP q = p;
     q.early_issue = g_early;
+    // write-through epilogue stores: not where the workgroup reads its own stores back (RBM sampling)
+    q.wt = EPI == EPI_BIAS_SIG_BIN ? 0 : g_wt;
+    // the exact-prefetch instantiation (PX) only for the training step's large-layer kernels: the
+    // hidden forward (64x128 NN + bias + sigmoid), backward (64x128 NT + diff-sigmoid + slab sums)
+    // and update (128x128 TN + SGD / the data-parallel gradient)
+    constexpr bool PXK = IL == 0 && BK == 64 && S == 2 &&
+                         ((BM == 64 && BN == 128 && A_KC && !B_KC && EPI == EPI_BIAS_SIG) ||
+                          (BM == 64 && BN == 128 && A_KC && B_KC && EPI == EPI_DSIG_CS) ||
+                          (BM == 128 && BN == 128 && !A_KC && !B_KC &&
+                           (EPI == EPI_SGD_B || EPI == EPI_SGD || EPI == EPI_STORE_BG)));
+    auto a16 = [](const void* v) { return ((uintptr_t)v & 15) == 0; };
+    const bool exact = g_pre0 && p.ksplit <= 1 && p.M % BM == 0 && p.N % BN == 0 && (p.ldc & 3) == 0 && a16(p.C) &&
+                       (!p.bias || a16(p.bias)) && (!p.aux || (a16(p.aux) && (p.ldaux & 3) == 0)) &&
+                       (!p.corr || (a16(p.corr) && (p.ldcorr & 3) == 0)) &&
+                       // PX bias: every column's slab sums in one workgroup's 256 lanes (32 slabs x 8 columns)
+                       (!epi_bias_slabs(EPI) ||
+                        (p.bslabs >= 1 && p.bslabs <= kBiasPreSlabs && (BN + p.M / BM - 1) / (p.M / BM) <= 8));
+    if constexpr (PXK) {
+      if (exact) {
+        gemm16_kernel<BM, BN, BK, WM, WN, S, IL, A_KC, B_KC, EPI, true><<<grid, WM * WN * 64, 0, st>>>(q);
+        return true;
+      }
+    }
     gemm16_kernel<BM, BN, BK, WM, WN, S, IL, A_KC, B_KC, EPI><<<grid, (WM * WN + (IL == 2)) * 64, 0, st>>>(q);
     return true;
   }

@@ -37,6 +37,20 @@ __device__ __forceinline__ float sigmoidf_ref(float x) {
   return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-1.44269504088896341f * x));
 }
 
+// Write-through (sc1) 16-B output stores through a buffer descriptor of the workgroup's output tile (or row).  A
+// plain store leaves its line dirty in the XCD's L2 and the kernel-end release writes every dirty line
+// back AFTER the last workgroup has finished (MI355X_MICROARCH.md price list, 'boundary': + B / 6 TB/s
+// for B dirty bytes); an sc1 store sends the line out as it is written, overlapped with the other
+// workgroups' main loops.  Nothing is lost by dropping the line: the next kernel reads the output on
+// other XCDs (L2s are not coherent across XCDs; a kernel boundary invalidates them).
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t tile_rsrc(const float* base) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, 0x7FFFFFF0, 0x00020000);
+}
+__device__ __forceinline__ void st_wt(__amdgpu_buffer_rsrc_t r, long elem_off, f32x4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, (int)(elem_off * 4), 0, 16);
+}
+
 struct ArgMax {
   float v;
   int i;

@@ -499,6 +499,8 @@ __global__ __launch_bounds__(256) void softmax_xent_row4_kernel(const float* __r
   if (t >= N) t = -1;  // out of range: an unlabeled row (the host intake rejects one, CheckLabels)
   float* yrow = Y ? Y + (long)row * strideY : nullptr;
   float* erow = E ? E + (long)row * strideE : nullptr;
+  // write-through row stores (kcommon.h st_wt): E is 16 MB at 4000 senones, read next on other XCDs
+  const __amdgpu_buffer_rsrc_t ry = tile_rsrc(yrow ? yrow : Z), re = tile_rsrc(erow ? erow : Z);
   ArgMax ay{-1e20f, 0x7fffffff};
 #pragma unroll
   for (int q = 0; q < CPW; ++q) {
@@ -511,8 +513,8 @@ __global__ __launch_bounds__(256) void softmax_xent_row4_kernel(const float* __r
         if (y[k] > ay.v) { ay.v = y[k]; ay.i = c + k; }
         e[k] = y[k] - ((c + k == t) ? 1.f : 0.f);
       }
-      if (yrow) *reinterpret_cast<f32x4*>(yrow + c) = y;
-      if (erow) *reinterpret_cast<f32x4*>(erow + c) = e;
+      if (yrow) st_wt(ry, c, y);
+      if (erow) st_wt(re, c, e);
     }
   }
   ay = wave_argmax(ay);
