@@ -107,6 +107,11 @@ def dp_mode(world):
 
 
 def main():
+    # stdout carries exactly the one JSON result line: the native libraries' own prints (RCCL's version
+    # banner at communicator creation, on every rank) go to stderr with everything else
+    result_fd = os.dup(1)
+    sys.stdout.flush()
+    os.dup2(2, 1)
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     # default window: 100 timed steps (~110 ms); a 20-step window (~22 ms) reads 1-2 % lower on the
@@ -228,7 +233,7 @@ def main():
         launches, ms, flops = tot["launches"], tot["ms"], tot["work"]
         achieved = flops / (ms * 1e-3) / 1e12
         traffic, traffic_src = pmc_traffic()
-        roof = {"bound": "mfma", "kernel": "gemm_f32 2048x2048 (fwd/bwd/update)", "achieved": round(achieved, 2),
+        roof = {"bound": "mfma", "kernel": "gemm_f32 2048x2048 (fwd/bwd/update; a paired update + backward launch counts as its two GEMMs)", "achieved": round(achieved, 2),
                 "peak": PEAK_FP32_MFMA, "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_MFMA, 4),
                 "traffic": traffic, "traffic_unit": "bytes/launch", "traffic_source": traffic_src,
                 "algorithmic_bytes_per_launch": 4.0 * ((2 * B * 2048 + 2048 ** 2) + (3 * B * 2048 + 2048 ** 2) +
@@ -281,7 +286,7 @@ def main():
                             "(event pairs add stream time: the value region has none, the roofline region times "
                             "only the roofline kernels)",
         }
-        print(json.dumps(line), flush=True)
+        os.write(result_fd, (json.dumps(line) + "\n").encode())
     # release the library objects in dependency order (trainer -> objective / network -> communicator)
     # while the HIP runtime and the process group are still up
     tnet_amd.synchronize()

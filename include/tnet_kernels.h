@@ -214,6 +214,17 @@ int tnet_affine_softmax_xent(const float* X, TnetMatrixDim dX, const float* W, T
 int tnet_affine_update_bias(const float* X, TnetMatrixDim dX, const float* E, TnetMatrixDim dE, float* W,
                             TnetMatrixDim dW, float* corrW, int strideCorr, float scale, float mmt, float l2,
                             const float* colpart, int ldcolpart, float* b, float* corr_b, void* stream);
+/* tnet_affine_update_bias(X, E, W, ...) of layer l and tnet_affine_bwd_colsum(E2, W2, Ybelow, Eo,
+ * colpart2) of layer l-1 in ONE launch (the two GEMMs are independent: CuNetwork::Backpropagate,
+ * cuNetwork.h:170-194, runs layer l's Update after its backprop, and layer l-1's backprop reads only
+ * W_{l-1}); same results as the two calls.  TNET_ERR_UNSUPPORTED when either GEMM would run another
+ * tile configuration than the pair kernel's (the caller then makes the two calls). */
+int tnet_affine_update_bwd_pair(const float* X, TnetMatrixDim dX, const float* E, TnetMatrixDim dE, float* W,
+                                TnetMatrixDim dW, float* corrW, int strideCorr, float scale, float mmt, float l2,
+                                const float* colpart, int ldcolpart, float* b, float* corr_b, const float* E2,
+                                TnetMatrixDim dE2, const float* W2, TnetMatrixDim dW2, const float* Ybelow,
+                                int strideYbelow, float* Eo, TnetMatrixDim dEo, float* colpart2, int ldcolpart2,
+                                void* stream);
 /* G = X^T E into a gradient buffer (data-parallel path: all-reduced before tnet_sgd_update). */
 int tnet_affine_grad(const float* X, TnetMatrixDim dX, const float* E, TnetMatrixDim dE, float* G,
                      TnetMatrixDim dG, void* stream);

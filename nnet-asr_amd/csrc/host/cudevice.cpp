@@ -114,8 +114,8 @@ hipEvent_t CuDevice::KTEvent() {
   return mKTPool[mKTNext++];
 }
 
-void CuDevice::KTRecord(const std::string& tag, double work, hipEvent_t a, hipEvent_t b) {
-  mKT.push_back(KTRec{tag, work, a, b});
+void CuDevice::KTRecord(const std::string& tag, double work, hipEvent_t a, hipEvent_t b, int count) {
+  mKT.push_back(KTRec{tag, work, a, b, count});
 }
 
 void CuDevice::KTRunBegin() {
@@ -127,10 +127,10 @@ void CuDevice::KTRunBegin() {
   mKTRunOpen = true;
 }
 
-void CuDevice::KTRunAdd(const std::string& tag, double work) {
+void CuDevice::KTRunAdd(const std::string& tag, double work, int count) {
   if (!mKTRunOpen) return;
   auto& t = mKTRunList.back().tags[tag];
-  t.first++;
+  t.first += count;
   t.second += work;
 }
 
@@ -153,7 +153,7 @@ std::string CuDevice::KTCollect() {
     float ms = 0.f;
     TNET_HIP_CALL(hipEventElapsedTime(&ms, r.a, r.b));
     Agg& g = agg[r.tag];
-    g.n++;
+    g.n += r.count;
     g.ms += ms;
     g.work += r.work;
   }
@@ -185,7 +185,7 @@ std::string CuDevice::KTCollect() {
   return os.str();
 }
 
-KTScope::KTScope(const std::string& tag, double work) : mTag(tag), mWork(work) {
+KTScope::KTScope(const std::string& tag, double work, int count) : mTag(tag), mWork(work), mCount(count) {
   CuDevice& d = CuDevice::Instantiate();
   if (!d.KernelTiming()) return;
   if (d.KernelTimingRuns()) {
@@ -205,13 +205,13 @@ KTScope::KTScope(const std::string& tag, double work) : mTag(tag), mWork(work) {
 KTScope::~KTScope() {
   CuDevice& d = CuDevice::Instantiate();
   if (mRun) {
-    d.KTRunAdd(mTag, mWork);
+    d.KTRunAdd(mTag, mWork, mCount);
     return;
   }
   if (!mA) return;
   hipEvent_t b = d.KTEvent();
   (void)hipEventRecord(b, d.Stream());
-  d.KTRecord(mTag, mWork, mA, b);
+  d.KTRecord(mTag, mWork, mA, b, mCount);
 }
 
 CuProfileScope::CuProfileScope(const char* key) : mKey(key) {

@@ -54,7 +54,7 @@ class CuDevice {
   /// run mode: a timed launch begins (opens a run unless one is open)
   void KTRunBegin();
   /// run mode: a timed launch ended (its work joins the open run)
-  void KTRunAdd(const std::string& tag, double work);
+  void KTRunAdd(const std::string& tag, double work, int count = 1);
   /// run mode: an untimed launch begins / the report is taken: close the open run
   void KTCloseRun();
   /// time only the launches whose tag contains `filter` (empty = all): each event pair costs
@@ -63,7 +63,7 @@ class CuDevice {
   bool KernelTimed(const std::string& tag) const {
     return mKTOn && (mKTFilter.empty() || tag.find(mKTFilter) != std::string::npos);
   }
-  void KTRecord(const std::string& tag, double work, hipEvent_t a, hipEvent_t b);
+  void KTRecord(const std::string& tag, double work, hipEvent_t a, hipEvent_t b, int count = 1);
   hipEvent_t KTEvent();
   /// sync, aggregate "tag count total_ms total_work" lines, reset
   std::string KTCollect();
@@ -105,6 +105,7 @@ class CuDevice {
     std::string tag;
     double work;
     hipEvent_t a, b;
+    int count;
   };
   std::vector<KTRec> mKT;
   std::vector<hipEvent_t> mKTPool;
@@ -114,12 +115,19 @@ class CuDevice {
 /// RAII device timing of the launches enqueued in its scope (when KernelTiming is on).
 class KTScope {
  public:
-  KTScope(const std::string& tag, double work);
+  /// count: the GEMMs the scope's launch carries (a paired launch counts as its two)
+  KTScope(const std::string& tag, double work, int count = 1);
   ~KTScope();
+  /// nothing was launched in the scope after all: record nothing
+  void Cancel() {
+    mRun = false;
+    mA = nullptr;
+  }
 
  private:
   std::string mTag;
   double mWork;
+  int mCount;
   hipEvent_t mA = nullptr;
   bool mRun = false;
 };

@@ -161,6 +161,33 @@ void CuBiasedLinearity::UpdateFromColsum(const CuMatrix<BaseFloat>& X, const CuM
                                          mmt ? mBiasCorrection.pCUData() : nullptr, S));
 }
 
+bool CuBiasedLinearity::UpdateFromColsumWithBwd(const CuMatrix<BaseFloat>& X, const CuMatrix<BaseFloat>& E,
+                                                const CuMatrix<BaseFloat>& colpart, const CuBiasedLinearity& below,
+                                                const CuMatrix<BaseFloat>& E2, const CuMatrix<BaseFloat>& Ybelow,
+                                                CuMatrix<BaseFloat>& Eo, CuMatrix<BaseFloat>& colpart2) {
+  CuProfileScope p("CuBiasedLinearity::Update+Backpropagate");
+  float scale, l2;
+  UpdateConstants(X.Rows(), &scale, &l2);
+  const bool mmt = mMomentum != 0.0f;
+  const std::string su = std::to_string(GetNInputs()) + "x" + std::to_string(GetNOutputs());
+  const std::string sb = std::to_string(below.GetNInputs()) + "x" + std::to_string(below.GetNOutputs());
+  KTScope kt("gemm_upd+bwd:" + (su == sb ? su : su + "+" + sb),
+             2.0 * X.Rows() * GetNInputs() * GetNOutputs() + 2.0 * E2.Rows() * below.GetNInputs() * below.GetNOutputs(),
+             2);
+  const int st = tnet_affine_update_bwd_pair(
+      X.pCUData(), X.Dim(), E.pCUData(), E.Dim(), mLinearity.pCUData(), mLinearity.Dim(),
+      mmt ? mLinearityCorrection.pCUData() : nullptr, (int)mLinearityCorrection.Stride(), scale, mMomentum, l2,
+      colpart.pCUData(), (int)colpart.Stride(), mBias.pCUData(), mmt ? mBiasCorrection.pCUData() : nullptr,
+      E2.pCUData(), E2.Dim(), below.Linearity().pCUData(), below.Linearity().Dim(), Ybelow.pCUData(),
+      (int)Ybelow.Stride(), Eo.pCUData(), Eo.Dim(), colpart2.pCUData(), (int)colpart2.Stride(), S);
+  if (st == TNET_ERR_UNSUPPORTED) {
+    kt.Cancel();
+    return false;
+  }
+  TNET_SAFE_CALL(st);
+  return true;
+}
+
 void CuBiasedLinearity::Update() { UpdateFrom(GetInput(), GetErrorInput()); }
 
 void CuBiasedLinearity::ComputeGradient() {

@@ -33,6 +33,7 @@ class CuBiasedLinearity : public CuUpdatableComponent {
 
   // ---- access for the fused network-level kernels and the C ABI
   CuMatrix<BaseFloat>& Linearity() { return mLinearity; }
+  const CuMatrix<BaseFloat>& Linearity() const { return mLinearity; }
   CuVector<BaseFloat>& Bias() { return mBias; }
   CuMatrix<BaseFloat>& LinearityCorrection() { return mLinearityCorrection; }
   CuVector<BaseFloat>& BiasCorrection() { return mBiasCorrection; }
@@ -47,6 +48,13 @@ class CuBiasedLinearity : public CuUpdatableComponent {
   // same update with the bias gradient taken from the 32-row slab column sums of E that the backward
   // GEMM of the layer above wrote (tnet_affine_bwd_colsum): one launch instead of three
   void UpdateFromColsum(const CuMatrix<BaseFloat>& X, const CuMatrix<BaseFloat>& E, const CuMatrix<BaseFloat>& colpart);
+  /// UpdateFromColsum and, in the same launch, the backward GEMM of the layer below
+  /// (tnet_affine_update_bwd_pair): Eo = (E2 below.W^T) .* Ybelow (1 - Ybelow) + Eo's slab sums into
+  /// colpart2.  False (nothing enqueued) when the pair kernel does not take these shapes.
+  bool UpdateFromColsumWithBwd(const CuMatrix<BaseFloat>& X, const CuMatrix<BaseFloat>& E,
+                               const CuMatrix<BaseFloat>& colpart, const CuBiasedLinearity& below,
+                               const CuMatrix<BaseFloat>& E2, const CuMatrix<BaseFloat>& Ybelow,
+                               CuMatrix<BaseFloat>& Eo, CuMatrix<BaseFloat>& colpart2);
 
  protected:
   CuMatrix<BaseFloat> mLinearity;            ///< [nIn x nOut] (file stores the transpose)

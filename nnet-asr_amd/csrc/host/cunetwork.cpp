@@ -343,6 +343,21 @@ void CuNetwork::TrainBunch(const CuMatrix<BaseFloat>& X, const CuVector<int>& la
       err_colsum = true;
     }
   }  // slab column sums of *err are in mColPart[l] (bias gradient fused, no exchange)
+  // Without data parallelism the fused update of layer l is held back one layer and enqueued with the
+  // backward GEMM of layer l-1 as ONE launch where the pair kernel takes both shapes
+  // (tnet_affine_update_bwd_pair: the two are independent -- layer l-1's backward reads W_{l-1} only);
+  // otherwise (or TNET_GEMM_PAIR=0 in the library) the update runs right before that backward GEMM.
+  struct Pending {
+    CuBiasedLinearity* lin = nullptr;
+    const CuMatrix<BaseFloat>* X = nullptr;
+    const CuMatrix<BaseFloat>* E = nullptr;
+    int l = -1;
+  } pend;
+  auto flush = [&]() {
+    if (!pend.lin) return;
+    pend.lin->UpdateFromColsum(*pend.X, *pend.E, *mColPart[pend.l]);
+    pend.lin = nullptr;
+  };
   for (int l = nl - 1; l >= 0; l--) {
     auto* lin = static_cast<CuBiasedLinearity*>(mNetComponents[2 * l]);
     const bool stopper = (lin == mpPropagErrorStopper);
@@ -351,27 +366,38 @@ void CuNetwork::TrainBunch(const CuMatrix<BaseFloat>& X, const CuVector<int>& la
     if (!stopper && l > 0) {
       eo = mErr[l].get();
       eo->Init(rows, lin->GetNInputs());
-      KTScope kt("gemm_bwd:" + std::to_string(lin->GetNInputs()) + "x" + std::to_string(lin->GetNOutputs()),
-                 2.0 * rows * lin->GetNInputs() * lin->GetNOutputs());
+      const std::string shape = std::to_string(lin->GetNInputs()) + "x" + std::to_string(lin->GetNOutputs());
       // E_l = (E_{l+1} W_l^T) .* y_l (1 - y_l)   (backprop through <biasedlinearity> and the <sigmoid> below);
       // when the layer below is trained here, the same launch writes the bias gradient of E_l as slab sums
       auto* below = static_cast<CuBiasedLinearity*>(mNetComponents[2 * (l - 1)]);
       if (below->LearnRate() > 0.0f) {
         CuMatrix<BaseFloat>& cp = *mColPart[l - 1];
         cp.Init(tnet_colsum_slabs((int)rows), lin->GetNInputs());
-        const int st = tnet_affine_bwd_colsum(err->pCUData(), err->Dim(), lin->Linearity().pCUData(),
-                                              lin->Linearity().Dim(), acts[l]->pCUData(), (int)acts[l]->Stride(),
-                                              eo->pCUData(), eo->Dim(), cp.pCUData(), (int)cp.Stride(), S);
-        if (st != TNET_ERR_UNSUPPORTED) {
-          TNET_SAFE_CALL(st);
+        if (pend.lin && pend.lin->UpdateFromColsumWithBwd(*pend.X, *pend.E, *mColPart[pend.l], *lin, *err, *acts[l],
+                                                         *eo, cp)) {
+          pend.lin = nullptr;
           eo_colsum = true;
+        } else {
+          flush();
+          KTScope kt("gemm_bwd:" + shape, 2.0 * rows * lin->GetNInputs() * lin->GetNOutputs());
+          const int st = tnet_affine_bwd_colsum(err->pCUData(), err->Dim(), lin->Linearity().pCUData(),
+                                                lin->Linearity().Dim(), acts[l]->pCUData(), (int)acts[l]->Stride(),
+                                                eo->pCUData(), eo->Dim(), cp.pCUData(), (int)cp.Stride(), S);
+          if (st != TNET_ERR_UNSUPPORTED) {
+            TNET_SAFE_CALL(st);
+            eo_colsum = true;
+          }
         }
       }
-      if (!eo_colsum)
+      if (!eo_colsum) {
+        flush();
+        KTScope kt("gemm_bwd:" + shape, 2.0 * rows * lin->GetNInputs() * lin->GetNOutputs());
         TNET_SAFE_CALL(tnet_affine_bwd(err->pCUData(), err->Dim(), lin->Linearity().pCUData(),
                                        lin->Linearity().Dim(), acts[l]->pCUData(), (int)acts[l]->Stride(),
                                        eo->pCUData(), eo->Dim(), 1, S));
+      }
     }
+    flush();  // a held-back update no backward GEMM took
     if (lin->LearnRate() > 0.0f) {
       if (exchange) {
         lin->SetInput(*acts[l]);
@@ -392,7 +418,10 @@ void CuNetwork::TrainBunch(const CuMatrix<BaseFloat>& X, const CuVector<int>& la
         }
         n_submitted++;
       } else if (err_colsum) {
-        lin->UpdateFromColsum(*acts[l], *err, *mColPart[l]);
+        pend.lin = lin;  // held back for the next layer's backward GEMM (flushed there or below)
+        pend.X = acts[l];
+        pend.E = err;
+        pend.l = l;
       } else {
         lin->UpdateFrom(*acts[l], *err);
       }
@@ -401,6 +430,7 @@ void CuNetwork::TrainBunch(const CuMatrix<BaseFloat>& X, const CuVector<int>& la
     err = eo;
     err_colsum = eo_colsum;
   }
+  flush();
   if (exchange) {
     // transports without an apply stream: apply each layer on the compute stream as soon as its own
     // reduction is done (top layer first), overlapping the reductions of the layers below

@@ -151,11 +151,16 @@ __global__ __launch_bounds__(EW_THREADS) void sgd_multi_kernel(const SgdSegs seg
     f32x4* p = reinterpret_cast<f32x4*>(sg.p);
     const f32x4* g = reinterpret_cast<const f32x4*>(sg.g);
     f32x4* q = reinterpret_cast<f32x4*>(sg.corr);
+    // parameters and momentum written through (kcommon.h st_wt): read next by the all-gather / the
+    // next step's forward, from any XCD -- nothing is gained by leaving them dirty in this XCD's L2
+    const bool wt = sg.n < (1L << 29);  // byte offsets of the descriptor stay below 2^31
+    const __amdgpu_buffer_rsrc_t rp = tile_rsrc(sg.p), rq = tile_rsrc(q ? sg.corr : sg.p);
     for (long i = t0; i < sg.n / 4; i += step) {
       f32x4 c = g[i];
       if (q) {
         c = c + mmt * q[i];
-        q[i] = c;
+        if (wt) st_wt(rq, 4 * i, c);
+        else q[i] = c;
       }
       f32x4 w = p[i];
 #pragma unroll
@@ -163,7 +168,8 @@ __global__ __launch_bounds__(EW_THREADS) void sgd_multi_kernel(const SgdSegs seg
         w[e] = w[e] + scale * c[e];
         w[e] = w[e] + sg.l2 * w[e];
       }
-      p[i] = w;
+      if (wt) st_wt(rp, 4 * i, w);
+      else p[i] = w;
     }
   } else {
     for (long i = t0; i < sg.n; i += step) {

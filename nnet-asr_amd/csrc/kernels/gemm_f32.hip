@@ -685,10 +685,14 @@ constexpr int kEpiInLaunch = 32;
 // PX (exact prefetch): the tile grid covers M x N exactly and the epilogue operands are 16-B aligned
 // (launch_cfg checks), so the epilogue-operand prefetch is a known number of unconditional loads per
 // wave and the first seam waits for the ring only, not for them (TNET_GEMM_PRE0=0: off)
-template <int BM, int BN, int BK, int WM, int WN, int S, int SP, bool A_KC, bool B_KC, int EPI_T, bool PX = false>
-__global__ __launch_bounds__((WM * WN + (SP == 2)) * 64)
-__attribute__((amdgpu_waves_per_eu((WM * WN + (SP == 2) + 3) / 4, (WM * WN + (SP == 2) + 3) / 4)))
-void gemm16_kernel(const GemmP p_in) {
+// The body of one workgroup (tile bid_x of the grid) over the caller's LDS array (gemm16_smem_floats
+// floats): gemm16_kernel runs one GEMM, gemm16_pair_kernel two independent ones in one launch.
+template <int BM, int BN, int BK, int S, int EPI_T, bool PX>
+constexpr int gemm16_smem_floats() {
+  return S * (BM + BN) * BK + ((PX && epi_bias_slabs(EPI_T)) ? kBiasPreSlabs * 8 : 0);
+}
+template <int BM, int BN, int BK, int WM, int WN, int S, int SP, bool A_KC, bool B_KC, int EPI_T, bool PX>
+__device__ __forceinline__ void gemm16_body(const GemmP& p_in, float* __restrict__ smem, const int bid_x) {
   constexpr bool INL = EPI_T >= kEpiInLaunch;
   constexpr int EPI = INL ? EPI_STORE : EPI_T;  // the tile epilogue
   GemmP p = p_in;
@@ -715,16 +719,15 @@ void gemm16_kernel(const GemmP p_in) {
   constexpr int GA = A_SZ / 4 / NT, GB = B_SZ / 4 / NT, G = GA + GB;
   static_assert(A_SZ % (4 * NT) == 0 && B_SZ % (4 * NT) == 0, "tile splits into 1-KiB wave pieces");
   static_assert(3 * G < 64, "vmcnt range");
-  // PX + bias epilogue: 32 slabs x 8 columns of bias-gradient slab sums after the ring (see PXB below)
-  constexpr bool PXB0 = PX && epi_bias_slabs(EPI_T);
-  __shared__ __attribute__((aligned(16))) float smem[S * ST_SZ + (PXB0 ? kBiasPreSlabs * 8 : 0)];
+  // smem: the ring (S slots of ST_SZ floats) and, with PX + a bias epilogue, 32 slabs x 8 columns of
+  // bias-gradient slab sums after it (see PXB below)
   TNET_STAMP_RT(4);
   TNET_STAMP(0);
 
   const int M = p.M, N = p.N, K = p.K;
   const int nbn = (N + BN - 1) / BN, nbm = (M + BM - 1) / BM;
   const int nwg = nbm * nbn;
-  const int bid = blockIdx.x, xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int bid = bid_x, xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
   const int L = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
   const int grp = p.group, per_group = grp * nbn;
   const int first_m = (L / per_group) * grp;
@@ -1558,7 +1561,7 @@ void gemm16_kernel(const GemmP p_in) {
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __attribute__((address_space(1))) unsigned* cnt =
-          (__attribute__((address_space(1))) unsigned*)(p.tile_cnt + blockIdx.x);
+          (__attribute__((address_space(1))) unsigned*)(p.tile_cnt + bid_x);
       const unsigned ticket = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       const bool last = ticket == (unsigned)(p.ksplit - 1);
       if (last) {
@@ -1588,6 +1591,30 @@ void gemm16_kernel(const GemmP p_in) {
   }
   TNET_STAMP(3);
   TNET_STAMP_RT(5);
+}
+
+template <int BM, int BN, int BK, int WM, int WN, int S, int SP, bool A_KC, bool B_KC, int EPI_T, bool PX = false>
+__global__ __launch_bounds__((WM * WN + (SP == 2)) * 64)
+__attribute__((amdgpu_waves_per_eu((WM * WN + (SP == 2) + 3) / 4, (WM * WN + (SP == 2) + 3) / 4)))
+void gemm16_kernel(const GemmP p_in) {
+  __shared__ __attribute__((aligned(16))) float smem[gemm16_smem_floats<BM, BN, BK, S, EPI_T, PX>()];
+  gemm16_body<BM, BN, BK, WM, WN, S, SP, A_KC, B_KC, EPI_T, PX>(p_in, smem, blockIdx.x);
+}
+
+// Two independent GEMMs in ONE launch: blocks [0, na) are GEMM A's tiles, the rest GEMM B's (2x2-wave
+// BK-64 two-slot configurations; one LDS array of the larger size, one workgroup per CU).  The training
+// step pairs the weight update of layer l with the backward GEMM of layer l-1 (disjoint operands: the
+// update writes W_l, the backward reads W_{l-1}): the blocks are dispatched in index order, so B's
+// workgroups start on the CUs A's finish on -- B's operand fill overlaps A's epilogue stores and tail
+// instead of waiting for a kernel boundary, A's end-of-kernel drain and B's start-up spread.
+template <int BMA, int BNA, bool AKA, bool BKA, int EPIA, bool PXA, int BMB, int BNB, bool AKB, bool BKB, int EPIB,
+          bool PXB>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
+void gemm16_pair_kernel(const GemmP pa, const GemmP pb, const int na) {
+  constexpr int SA = gemm16_smem_floats<BMA, BNA, 64, 2, EPIA, PXA>(), SB = gemm16_smem_floats<BMB, BNB, 64, 2, EPIB, PXB>();
+  __shared__ __attribute__((aligned(16))) float smem[SA > SB ? SA : SB];
+  if ((int)blockIdx.x < na) gemm16_body<BMA, BNA, 64, 2, 2, 2, 0, AKA, BKA, EPIA, PXA>(pa, smem, blockIdx.x);
+  else gemm16_body<BMB, BNB, 64, 2, 2, 2, 0, AKB, BKB, EPIB, PXB>(pb, smem, (int)blockIdx.x - na);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1834,6 +1861,7 @@ static int g_early = 1;   // TNET_GEMM_EARLY=0: prologue issues S-1 slots before
 // 14.6 us, the RBM reconstruction 256 x 440 over K = 2048 20.7 vs 14.4 us, MLP3 10.45M vs 10.96M
 // frames/s: the agent-scope release (L2 write-back) + acquire cost more than the launch boundary
 static int g_inlaunch = 0;
+static int g_pair = 1;  // TNET_GEMM_PAIR=0: tnet_affine_update_bwd_pair never pairs (A/B measurements)
 static int g_pre0 = 1;  // TNET_GEMM_PRE0=0: the first seam also waits for the epilogue-operand prefetch
 static int g_wt = 1;  // TNET_GEMM_WT=0: plain 16-B epilogue stores instead of write-through (sc1; measured +1.4 % frames/s)
 static int forced_cfg() {
@@ -1849,6 +1877,8 @@ static int forced_cfg() {
     if (sk) g_split = atoi(sk);
     const char* ea = getenv("TNET_GEMM_EARLY");
     if (ea) g_early = atoi(ea);
+    const char* pr = getenv("TNET_GEMM_PAIR");
+    if (pr) g_pair = atoi(pr);
     const char* p0 = getenv("TNET_GEMM_PRE0");
     if (p0) g_pre0 = atoi(p0);
     const char* wt = getenv("TNET_GEMM_WT");
@@ -1857,6 +1887,19 @@ static int forced_cfg() {
     if (il) g_inlaunch = atoi(il);
   }
   return g_cfg;
+}
+
+// the exact-prefetch instantiation (PX) may run this launch: the grid covers M x N exactly, the epilogue
+// operands are 16-B aligned, and (bias epilogues) every column's slab sums fit one workgroup's 256 lanes
+// (32 slabs x 8 columns of the tile per tile-row)
+template <int BM, int BN, int EPI>
+static bool px_exact(const GemmP& p) {
+  auto a16 = [](const void* v) { return ((uintptr_t)v & 15) == 0; };
+  return g_pre0 && p.ksplit <= 1 && p.M % BM == 0 && p.N % BN == 0 && (p.ldc & 3) == 0 && a16(p.C) &&
+         (!p.bias || a16(p.bias)) && (!p.aux || (a16(p.aux) && (p.ldaux & 3) == 0)) &&
+         (!p.corr || (a16(p.corr) && (p.ldcorr & 3) == 0)) &&
+         (!epi_bias_slabs(EPI) ||
+          (p.bslabs >= 1 && p.bslabs <= kBiasPreSlabs && (BN + p.M / BM - 1) / (p.M / BM) <= 8));
 }
 
 template <int KIND, int BM, int BN, int BK, int WM, int WN, int S, int IL, bool A_KC, bool B_KC, int EPI>
@@ -1884,13 +1927,7 @@ static bool launch_cfg(const GemmP& p, hipStream_t st) {
                           (BM == 64 && BN == 128 && A_KC && B_KC && EPI == EPI_DSIG_CS) ||
                           (BM == 128 && BN == 128 && !A_KC && !B_KC &&
                            (EPI == EPI_SGD_B || EPI == EPI_SGD || EPI == EPI_STORE_BG)));
-    auto a16 = [](const void* v) { return ((uintptr_t)v & 15) == 0; };
-    const bool exact = g_pre0 && p.ksplit <= 1 && p.M % BM == 0 && p.N % BN == 0 && (p.ldc & 3) == 0 && a16(p.C) &&
-                       (!p.bias || a16(p.bias)) && (!p.aux || (a16(p.aux) && (p.ldaux & 3) == 0)) &&
-                       (!p.corr || (a16(p.corr) && (p.ldcorr & 3) == 0)) &&
-                       // PX bias: every column's slab sums in one workgroup's 256 lanes (32 slabs x 8 columns)
-                       (!epi_bias_slabs(EPI) ||
-                        (p.bslabs >= 1 && p.bslabs <= kBiasPreSlabs && (BN + p.M / BM - 1) / (p.M / BM) <= 8));
+    const bool exact = px_exact<BM, BN, EPI>(p);
     if constexpr (PXK) {
       if (exact) {
         gemm16_kernel<BM, BN, BK, WM, WN, S, IL, A_KC, B_KC, EPI, true><<<grid, WM * WN * 64, 0, st>>>(q);
@@ -2086,6 +2123,36 @@ static int launch_gemm(const GemmP& p_in, hipStream_t st) {
   TNET_LAUNCH_CHECK();
   return TNET_OK;
   }
+}
+
+// tnet_affine_update_bwd_pair: the update GEMM (A: fused SGD + bias SGD, the 128x128 configuration the
+// planner gives it) and an independent backward GEMM (B: diff-sigmoid + slab sums, 64x128) as one
+// gemm16_pair_kernel launch; TNET_ERR_UNSUPPORTED where either would run another configuration (the
+// caller then makes the two calls)
+static int launch_pair_upd_bwd(GemmP pu, GemmP pb, hipStream_t st) {
+  if (forced_cfg() >= 0 || !g_pair) return TNET_ERR_UNSUPPORTED;
+  if (pu.M <= 0 || pu.N <= 0 || pb.M <= 0 || pb.N <= 0) return TNET_ERR_UNSUPPORTED;
+  const GemmPlan pl = plan_gemm<false>(pu, true);
+  if (pl.cfg != CFG_m128x128k64s2 || pl.ks != 1) return TNET_ERR_UNSUPPORTED;
+  if ((long)cdiv(pb.M, 64) * cdiv(pb.N, 128) < 200) return TNET_ERR_UNSUPPORTED;  // launch_colsum_bwd's 64x128 rule
+  pu.group = pb.group = g_group > 0 ? g_group : 8;
+  pu.early_issue = pb.early_issue = g_early;
+  pu.wt = pb.wt = g_wt;
+  // the 16x16 kernel's 32-bit tile offsets (launch_cfg's check)
+  const long extA_u = 64L * pu.lda + pu.M, extB_u = 64L * pu.ldb + pu.N;
+  const long extA_b = (long)pb.M * pb.lda, extB_b = (long)pb.N * pb.ldb;
+  if (4 * extA_u >= (1L << 32) || 4 * extB_u >= (1L << 32) || 4 * extA_b >= (1L << 32) || 4 * extB_b >= (1L << 32))
+    return TNET_ERR_UNSUPPORTED;
+  if (!px_exact<64, 128, EPI_DSIG_CS>(pb)) return TNET_ERR_UNSUPPORTED;
+  const int na = cdiv(pu.M, 128) * cdiv(pu.N, 128), nb = cdiv(pb.M, 64) * cdiv(pb.N, 128);
+  if (px_exact<128, 128, EPI_SGD_B>(pu))
+    gemm16_pair_kernel<128, 128, false, false, EPI_SGD_B, true, 64, 128, true, true, EPI_DSIG_CS, true>
+        <<<na + nb, 256, 0, st>>>(pu, pb, na);
+  else
+    gemm16_pair_kernel<128, 128, false, false, EPI_SGD_B, false, 64, 128, true, true, EPI_DSIG_CS, true>
+        <<<na + nb, 256, 0, st>>>(pu, pb, na);
+  TNET_LAUNCH_CHECK();
+  return TNET_OK;
 }
 
 static bool aligned16(const void* q) { return ((uintptr_t)q & 15) == 0; }
@@ -2302,6 +2369,42 @@ extern "C" int tnet_affine_update_bias(const float* X, TnetMatrixDim dX, const f
   if (st) return st;
   if (p.M <= 0 || p.N <= 0) return TNET_OK;
   return launch_gemm<false, false, EPI_SGD_B>(p, (hipStream_t)stream);
+}
+
+extern "C" int tnet_affine_update_bwd_pair(const float* X, TnetMatrixDim dX, const float* E, TnetMatrixDim dE,
+                                          float* W, TnetMatrixDim dW, float* corrW, int strideCorr, float scale,
+                                          float mmt, float l2, const float* colpart, int ldcolpart, float* b,
+                                          float* corr_b, const float* E2, TnetMatrixDim dE2, const float* W2,
+                                          TnetMatrixDim dW2, const float* Ybelow, int strideYbelow, float* Eo,
+                                          TnetMatrixDim dEo, float* colpart2, int ldcolpart2, void* stream) {
+  // tnet_affine_update_bias(X, E, W, ...) and tnet_affine_bwd_colsum(E2, W2, Ybelow, Eo, colpart2) in one
+  // launch; the two must be independent (W is not W2, Eo / colpart2 overlap none of the update's operands)
+  if (dX.rows != dE.rows || dW.rows != dX.cols || dW.cols != dE.cols || !colpart || !b || ldcolpart < dE.cols)
+    return TNET_ERR_ARG;
+  if (mmt != 0.f && (!corrW || !corr_b)) return TNET_ERR_ARG;
+  if (dE2.cols != dW2.cols || dEo.rows != dE2.rows || dEo.cols != dW2.rows || !Ybelow || !colpart2 ||
+      ldcolpart2 < dEo.cols || !aligned16(Ybelow) || (strideYbelow & 3))
+    return TNET_ERR_ARG;
+  if (W == W2) return TNET_ERR_ARG;
+  GemmP pu{};
+  pu.M = dX.cols; pu.N = dE.cols; pu.K = dX.rows;
+  pu.A = X; pu.lda = dX.stride; pu.B = E; pu.ldb = dE.stride; pu.C = W; pu.ldc = dW.stride;
+  pu.corr = (mmt != 0.f || corrW) ? corrW : nullptr; pu.ldcorr = strideCorr;
+  if (pu.corr && (pu.ldcorr & 3)) return TNET_ERR_ARG;
+  pu.scale = scale; pu.mmt = mmt; pu.l2 = l2;
+  pu.bpart = colpart; pu.ldbpart = ldcolpart; pu.bslabs = tnet_colsum_slabs(dE.rows);
+  pu.bvec = b; pu.bcorr = mmt != 0.f ? corr_b : nullptr; pu.bscale = scale; pu.bmmt = mmt;
+  int st = check_common(pu);
+  if (st) return st;
+  GemmP pb{};
+  pb.M = dE2.rows; pb.N = dW2.rows; pb.K = dE2.cols;
+  pb.A = E2; pb.lda = dE2.stride; pb.B = W2; pb.ldb = dW2.stride; pb.C = Eo; pb.ldc = dEo.stride;
+  pb.alpha = 1.f; pb.beta = 0.f;
+  pb.aux = Ybelow; pb.ldaux = strideYbelow;
+  pb.cpart = colpart2; pb.ldcpart = ldcolpart2;
+  st = check_common(pb);
+  if (st) return st;
+  return launch_pair_upd_bwd(pu, pb, (hipStream_t)stream);
 }
 
 extern "C" int tnet_affine_grad_bias(const float* X, TnetMatrixDim dX, const float* E, TnetMatrixDim dE, float* G,

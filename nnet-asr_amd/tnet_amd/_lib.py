@@ -80,6 +80,8 @@ _SIGS = {
     "tnet_affine_bwd_colsum": (i32, [vp, MatrixDim, vp, MatrixDim, vp, i32, vp, MatrixDim, vp, i32, vp]),
     "tnet_affine_update_bias": (i32, [vp, MatrixDim, vp, MatrixDim, vp, MatrixDim, vp, i32, f32, f32, f32, vp, i32,
                                       vp, vp, vp]),
+    "tnet_affine_update_bwd_pair": (i32, [vp, MatrixDim, vp, MatrixDim, vp, MatrixDim, vp, i32, f32, f32, f32, vp, i32,
+                                          vp, vp, vp, MatrixDim, vp, MatrixDim, vp, i32, vp, MatrixDim, vp, i32, vp]),
     "tnet_affine_grad": (i32, [vp, MatrixDim, vp, MatrixDim, vp, MatrixDim, vp]),
     "tnet_sgd_update": (i32, [vp, vp, vp, i64, f32, f32, f32, vp]),
     "tnet_bias_update": (i32, [vp, MatrixDim, vp, vp, vp, f32, f32, vp, vp]),

@@ -17,6 +17,9 @@ from tnet_amd import DeviceArray, _lib, synchronize  # noqa: E402
 from tnet_amd._lib import MatrixDim, check, lib  # noqa: E402
 
 
+TNET_ERR_ARG, TNET_ERR_UNSUPPORTED = -1, -4  # include/tnet_kernels.h
+
+
 def S():
     """the library stream: kernels and the DeviceArray copies must be stream-ordered"""
     return lib().tnet_stream()
@@ -208,6 +211,67 @@ def test_affine_update_bias(mmt, rows, n_in, n_out, gemm_cfg):
     np.testing.assert_allclose(db.numpy().ravel(), b + scale * cb, rtol=1e-6, atol=1e-7)
     if mmt:
         np.testing.assert_allclose(dCb.numpy().ravel(), cb, rtol=1e-6, atol=1e-9)
+
+
+@pytest.mark.parametrize("mmt", [0.0, 0.5])
+@pytest.mark.parametrize("rows,n_in,n_out,n_below", [(1024, 2048, 2048, 2048), (1024, 2048, 4000, 2048),
+                                                     (2048, 2048, 2048, 2048), (1024, 1024, 2048, 1024)])
+def test_affine_update_bwd_pair(mmt, rows, n_in, n_out, n_below):
+    """tnet_affine_update_bwd_pair (layer l's fused update + layer l-1's backward GEMM in one launch)
+    gives exactly what the two calls give (same tile bodies: bit-identical), or declines with
+    TNET_ERR_UNSUPPORTED where the pair kernel does not take the shapes"""
+    X, E = rnd((rows, n_in), 21), rnd((rows, n_out), 22, 0.01)
+    W, corr = rnd((n_in, n_out), 23, 0.1), rnd((n_in, n_out), 24, 0.01)
+    b, corr_b = rnd(n_out, 25), rnd(n_out, 26, 0.01)
+    P = slab_sums(E).astype(np.float32)
+    # layer below: W2 [n_below x n_in], E2 = the error at its output [rows x n_in], Yb its input's y
+    W2, E2 = rnd((n_below, n_in), 27, 0.1), rnd((rows, n_in), 28)
+    Yb = (1 / (1 + np.exp(-rnd((rows, n_below), 29)))).astype(np.float32)
+    scale, l2 = -0.3 / rows, -1e-4
+    slabs = lib().tnet_colsum_slabs(rows)
+
+    def run(pair):
+        d = dict(X=DeviceArray.from_numpy(X), E=DeviceArray.from_numpy(E), W=DeviceArray.from_numpy(W),
+                 P=DeviceArray.from_numpy(P), b=DeviceArray.vector(b),
+                 C=DeviceArray.from_numpy(corr) if mmt else None, Cb=DeviceArray.vector(corr_b) if mmt else None,
+                 W2=DeviceArray.from_numpy(W2), E2=DeviceArray.from_numpy(E2), Y=DeviceArray.from_numpy(Yb),
+                 O=DeviceArray(rows, n_below), P2=DeviceArray.from_numpy(np.full((slabs, n_below), np.nan, np.float32)))
+        C, Cb = d["C"], d["Cb"]
+        upd = (d["X"].ptr, d["X"].dim, d["E"].ptr, d["E"].dim, d["W"].ptr, d["W"].dim, C.ptr if C else None,
+               C.stride if C else 0, scale, mmt, l2, d["P"].ptr, d["P"].stride, d["b"].ptr, Cb.ptr if Cb else None)
+        bwd = (d["E2"].ptr, d["E2"].dim, d["W2"].ptr, d["W2"].dim, d["Y"].ptr, d["Y"].stride, d["O"].ptr, d["O"].dim,
+               d["P2"].ptr, d["P2"].stride)
+        if pair:
+            st = lib().tnet_affine_update_bwd_pair(*upd, *bwd, S())
+            if st == TNET_ERR_UNSUPPORTED:
+                return None
+            check(st)
+        else:
+            check(lib().tnet_affine_update_bias(*upd, S()))
+            check(lib().tnet_affine_bwd_colsum(*bwd, S()))
+        synchronize()
+        return {k: v.numpy() for k, v in d.items() if v is not None and k in ("W", "b", "C", "Cb", "O", "P2")}
+
+    got, ref = run(True), run(False)
+    if (n_in, n_out, n_below) == (2048, 2048, 2048):
+        assert got is not None, "the step's 2048-wide layers must run as one launch"
+    if n_out == 4000:  # the planner gives that update 128x256 tiles: not the pair kernel's
+        assert got is None
+    if got is None:
+        return
+    for k in ref:
+        np.testing.assert_array_equal(got[k], ref[k], err_msg=k)
+
+
+def test_affine_update_bwd_pair_rejects_shared_weights():
+    X, E = rnd((64, 128), 1), rnd((64, 128), 2)
+    dX, dE, dW, dP, db = (DeviceArray.from_numpy(X), DeviceArray.from_numpy(E), DeviceArray(128, 128),
+                          DeviceArray(2, 128), DeviceArray.vector(np.zeros(128, np.float32)))
+    dY, dO, dP2 = DeviceArray(64, 128), DeviceArray(64, 128), DeviceArray(2, 128)
+    st = lib().tnet_affine_update_bwd_pair(dX.ptr, dX.dim, dE.ptr, dE.dim, dW.ptr, dW.dim, None, 0, -0.1, 0.0, 0.0,
+                                           dP.ptr, dP.stride, db.ptr, None, dE.ptr, dE.dim, dW.ptr, dW.dim, dY.ptr,
+                                           dY.stride, dO.ptr, dO.dim, dP2.ptr, dP2.stride, S())
+    assert st == TNET_ERR_ARG
 
 
 @pytest.mark.parametrize("rows,n_in,n_out", [(16, 24, 32), (1024, 2048, 2048), (1024, 440, 2048), (1000, 2048, 4000),

@@ -20,6 +20,7 @@ diff-sigmoid launches except the first after softmax_xent (that one has K=4000);
 import csv
 import json
 import os
+import re
 import shutil
 import sys
 
@@ -29,14 +30,16 @@ import pmc_summary  # noqa: E402
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-FWD = "gemm16_kernel<64, 128, 64, 2, 2, 2, 0, true, false, 2>"    # bias + sigmoid
-BWD = "gemm16_kernel<64, 128, 64, 2, 2, 2, 0, true, true, 8>"     # diff-sigmoid + slab column sums
-UPD = "gemm16_kernel<128, 128, 64, 2, 2, 2, 0, false, false, 9>"  # SGD + bias SGD
+# (round 3: a trailing ", true" = the exact-prefetch instantiation, PX)
+FWD = re.compile(r"gemm16_kernel<64, 128, 64, 2, 2, 2, 0, true, false, 2(, (true|false))?>")    # bias + sigmoid
+BWD = re.compile(r"gemm16_kernel<64, 128, 64, 2, 2, 2, 0, true, true, 8(, (true|false))?>")     # diff-sigmoid + sums
+PAIR = re.compile(r"gemm16_pair_kernel<128, 128, false, false, 9, (true|false), 64, 128, true, true, 8, true>")
+UPD = re.compile(r"gemm16_kernel<128, 128, 64, 2, 2, 2, 0, false, false, 9(, (true|false))?>")  # SGD + bias SGD
 
 
 def classify_trace(path):
     rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
-    cls = {"fwd": [], "bwd": [], "upd": []}
+    cls = {"fwd": [], "bwd": [], "upd": [], "pair": []}
     after_softmax = False
     after_gather = False
     for r in rows:
@@ -49,18 +52,22 @@ def classify_trace(path):
         if "gather_rows" in name:
             after_gather = True
             continue
-        if FWD in name:
+        if FWD.search(name):
             if after_gather:           # K = 440 (the first layer, same tile config)
                 after_gather = False
             else:
                 cls["fwd"].append(dur)
-        elif BWD in name:
+        elif BWD.search(name):
             if after_softmax:          # K = 4000 (error into the last hidden layer)
                 after_softmax = False
             else:
                 cls["bwd"].append(dur)
-        elif UPD in name and grid == 65536:
+        elif UPD.search(name) and grid == 65536:
             cls["upd"].append(dur)
+        elif PAIR.search(name) and grid == 2 * 65536:
+            # round 3: a 2048x2048 update + the 2048x2048 backward of the layer below in one launch
+            # (tnet_affine_update_bwd_pair): two GEMMs, each counted at half the launch
+            cls["pair"] += [dur / 2, dur / 2]
     return cls
 
 
@@ -74,7 +81,7 @@ def main():
     shutil.copyfile(os.path.join(src, "prof_stats", "bench_kernel_stats.csv"),
                     os.path.join(prof, f"{tag}_bench_dnn4_kernel_stats.csv"))
     cls = classify_trace(os.path.join(src, "prof_stats", "bench_kernel_trace.csv"))
-    allv = cls["fwd"] + cls["bwd"] + cls["upd"]
+    allv = cls["fwd"] + cls["bwd"] + cls["upd"] + cls["pair"]
     prof_bench = json.loads(open(os.path.join(src, "bench_prof.json")).read().strip().splitlines()[-1])
     tr = {"source": "rocprofv3 --kernel-trace --stats -- python3 bench.py --no-cpu-baseline",
           "per_class_avg_us": {k: round(sum(v) / len(v), 2) for k, v in cls.items() if v},
