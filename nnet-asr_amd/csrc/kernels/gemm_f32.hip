@@ -687,9 +687,11 @@ constexpr int kEpiInLaunch = 32;
 // wave and the first seam waits for the ring only, not for them (TNET_GEMM_PRE0=0: off)
 // The body of one workgroup (tile bid_x of the grid) over the caller's LDS array (gemm16_smem_floats
 // floats): gemm16_kernel runs one GEMM, gemm16_pair_kernel two independent ones in one launch.
+// (exactly the ring: 128 KB for 128x128 tiles -- one float more and the grid's start-up spread grew from
+// ~1.1 to 2.9-3.9 us, in-kernel stamps; the PX bias slab sums reuse the ring after the main loop)
 template <int BM, int BN, int BK, int S, int EPI_T, bool PX>
 constexpr int gemm16_smem_floats() {
-  return S * (BM + BN) * BK + ((PX && epi_bias_slabs(EPI_T)) ? kBiasPreSlabs * 8 : 0);
+  return S * (BM + BN) * BK;
 }
 template <int BM, int BN, int BK, int WM, int WN, int S, int SP, bool A_KC, bool B_KC, int EPI_T, bool PX>
 __device__ __forceinline__ void gemm16_body(const GemmP& p_in, float* __restrict__ smem, const int bid_x) {
@@ -719,8 +721,7 @@ __device__ __forceinline__ void gemm16_body(const GemmP& p_in, float* __restrict
   constexpr int GA = A_SZ / 4 / NT, GB = B_SZ / 4 / NT, G = GA + GB;
   static_assert(A_SZ % (4 * NT) == 0 && B_SZ % (4 * NT) == 0, "tile splits into 1-KiB wave pieces");
   static_assert(3 * G < 64, "vmcnt range");
-  // smem: the ring (S slots of ST_SZ floats) and, with PX + a bias epilogue, 32 slabs x 8 columns of
-  // bias-gradient slab sums after it (see PXB below)
+  // smem: the ring (S slots of ST_SZ floats; after the main loop the PX bias slab sums, see PXB below)
   TNET_STAMP_RT(4);
   TNET_STAMP(0);
 
@@ -1362,8 +1363,11 @@ __device__ __forceinline__ void gemm16_body(const GemmP& p_in, float* __restrict
   if constexpr (epi_bias_slabs(EPI) && !PXB)
     if (bm == 0) bias_pre_finish<BN, EPI == EPI_STORE_BG>(p, bn, bpre);
   if constexpr (PXB) {
-    float* bsm = smem + S * ST_SZ;
+    static_assert(S * ST_SZ >= kBiasPreSlabs * 8 && WM * WN * 64 == kBiasPreSlabs * 8, "PX bias layout");
+    float* bsm = smem;  // the ring's first 1 KB, once every wave's last fragment reads have retired
     const int u = threadIdx.x;
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+    __syncthreads();
     bsm[u] = (u >> 3) < p.bslabs ? pxb_v : 0.f;
     __syncthreads();
     if (u < pxb_cpw && (bm / BM) * pxb_cpw + u < BN) {
