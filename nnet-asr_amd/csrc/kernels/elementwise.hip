@@ -102,8 +102,9 @@ __global__ __launch_bounds__(EW_THREADS) void gather_rows_kernel(float* __restri
     const long src = (long)ir * din.stride;
     const long dst = (long)r * dout.stride;
     if (vec4) {
-      for (int c = lane * 4; c < dout.cols; c += 256)
-        *reinterpret_cast<f32x4*>(y + dst + c) = *reinterpret_cast<const f32x4*>(x + src + c);
+      // the bunch row written through (kcommon.h st_wt): the step's first GEMM reads it on every XCD
+      const __amdgpu_buffer_rsrc_t ry = tile_rsrc(y + dst);
+      for (int c = lane * 4; c < dout.cols; c += 256) st_wt(ry, c, *reinterpret_cast<const f32x4*>(x + src + c));
     } else {
       for (int c = lane; c < dout.cols; c += 64) y[dst + c] = x[src + c];
     }

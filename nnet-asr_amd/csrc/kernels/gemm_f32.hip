@@ -261,7 +261,10 @@ __device__ __forceinline__ void combine4(const GemmP& p, const float* __restrict
       o[e] = w;
     }
   }
-  if (full) {
+  if (full && p.wt) {  // write-through (kcommon.h st_wt); launch_splitk checks the 2^31-byte offsets
+    st_wt(tile_rsrc(p.C), (long)row * p.ldc + col, o);
+    if (qsrc) st_wt(tile_rsrc(p.corr), (long)row * p.ldcorr + col, qn);
+  } else if (full) {
     *reinterpret_cast<f32x4*>(cp) = o;
     if (qsrc) *reinterpret_cast<f32x4*>(qsrc) = qn;
   } else {
@@ -1582,6 +1585,7 @@ __device__ __forceinline__ void gemm16_body(const GemmP& p_in, float* __restrict
       r.ldc = p_in.ldc2;
       r.alpha = p_in.alpha2;
       r.beta = p_in.beta2;
+      r.wt = 0;  // plain stores (the descriptor offsets are not checked for this path)
       combine_tile_t<epi_base(EPI_C)>(r, p_in.C, p_in.slabC, p_in.ksplit, (int)p_in.ldc, bm, bn, BM, BN, NT);
       // EPI_SGD_B / EPI_STORE_BG: the first tile-row's combiners also do the bias of their columns
       if constexpr (epi_bias_slabs(EPI_C)) {
@@ -2027,8 +2031,10 @@ static int launch_splitk(const GemmP& p, int cfg, int ks, hipStream_t st) {
   const int ldp = pt.ldp;
   const long n = (long)p.M * ((p.N + 3) >> 2);
   const unsigned main_blocks = (unsigned)cdiv(n, 256);
+  GemmP pc = p;  // the combine's output stores write-through where the byte offsets fit the descriptor
+  pc.wt = g_wt && (long)p.M * p.ldc < (1L << 29) && (!p.corr || (long)p.M * p.ldcorr < (1L << 29));
   const unsigned bias_blocks = epi_bias_slabs(EPI) ? (unsigned)cdiv(p.N, 256) : 0u;
-  splitk_reduce_kernel<EPI><<<main_blocks + bias_blocks, 256, 0, st>>>(p, ws, slab, ks, ldp, main_blocks);
+  splitk_reduce_kernel<EPI><<<main_blocks + bias_blocks, 256, 0, st>>>(pc, ws, slab, ks, ldp, main_blocks);
   TNET_LAUNCH_CHECK();
   return TNET_OK;
 }
