@@ -2,6 +2,7 @@
 #include "curecurrent.h"
 
 #include <cstdlib>
+#include <cstring>
 
 #include "cunetwork.h"
 
@@ -87,6 +88,22 @@ void CuRecurrent::UpdateFromDiff0() {
                                  mLearningRate, mMomentum, mWeightcost, S));
 }
 
+static uint64_t fbits(float v) {
+  uint32_t u;
+  std::memcpy(&u, &v, 4);
+  return u;
+}
+
+void CuRecurrent::ChainKey(std::vector<uint64_t>& k) const {
+  for (const void* p : {(const void*)mLinearity.pCUData(), (const void*)mBias.pCUData(),
+                        (const void*)mBiasCorrection.pCUData(), (const void*)mOutput.pCUData(),
+                        (const void*)mInputHistory.pCUData(), (const void*)mDiff.pCUData()})
+    k.push_back((uint64_t)(uintptr_t)p);
+  k.insert(k.end(), {(uint64_t)mLinearity.Stride(), (uint64_t)mInputHistory.Rows(), (uint64_t)mInputHistory.Stride(),
+                     (uint64_t)mDiff.Stride(), (uint64_t)mBpttOrder, (uint64_t)mHead, fbits(mLearningRate),
+                     fbits(mMomentum), fbits(mWeightcost)});
+}
+
 void CuRecurrent::ReadFromStream(std::istream& rIn) {
   // W^T [nOut x (nIn + nOut)] then the bias (cuRecurrent.cc:158-168)
   BfMatrix transpose;
@@ -123,6 +140,8 @@ CuRecurrentTrainer::~CuRecurrentTrainer() {
   if (mArgKey) (void)hipFree(mArgKey);
   if (mXbuf) (void)hipFree(mXbuf);
   if (mErrFlag) (void)hipFree(mErrFlag);
+  for (auto& kv : mGraphs)
+    if (kv.second.exec) (void)hipGraphExecDestroy(kv.second.exec);
 }
 
 void* CuRecurrentTrainer::Scratch(void*& p, size_t& have, size_t bytes) {
@@ -156,25 +175,114 @@ void CuRecurrentTrainer::TrainUtterance(const float* feats, size_t rows, size_t 
     mFrames += (long)rows;
     return;
   }
-  if (fused) {  // per-frame argmax keys of this utterance, read by tnet_argmax_correct at its end
+  if (fused) {
+    // per-frame argmax keys of this utterance, read by tnet_argmax_correct at its end
     Scratch(mArgKey, mArgKeyBytes, rows * sizeof(unsigned long long));
     TNET_HIP_CALL(hipMemsetAsync(mArgKey, 0, rows * sizeof(unsigned long long), CuDevice::Instantiate().Stream()));
+    RunFrames(rows);
+    TNET_SAFE_CALL(tnet_argmax_correct((const unsigned long long*)mArgKey, mLabels.pCUData(), (int)rows,
+                                       (int)mNet->GetNOutputs(), mObj->DeviceStats(), S));
+    mFrames += (long)rows;
+    return;
   }
   for (size_t f = 0; f < rows; f++) {
     CuMatrix<BaseFloat>::MakeView(mRow, mFeats.pCURowData(f), 1, cols, mFeats.Stride());
-    if (fused) {
-      TrainFrameFused(f);
-      continue;
-    }
     CuVector<int>::MakeView(mLabelRow, mLabels.pCUData() + f, 1);
     mNet->Propagate(mRow, mOut);
     mObj->EvaluateLabels(mOut, mLabelRow, mErr);
     if (!mCrossval) mNet->Backpropagate(mErr);
   }
-  if (fused)
-    TNET_SAFE_CALL(tnet_argmax_correct((const unsigned long long*)mArgKey, mLabels.pCUData(), (int)rows,
-                                       (int)mNet->GetNOutputs(), mObj->DeviceStats(), S));
   mFrames += (long)rows;
+}
+
+bool CuRecurrentTrainer::GraphsEnabled() const {
+  const char* e = getenv("TNET_RNN_GRAPH");
+  if (e && e[0] == '0') return false;
+  const CuDevice& dev = CuDevice::Instantiate();
+  return !dev.KernelTiming() && !dev.Profile();  // event records do not belong in a recorded chain
+}
+
+// Every value the fused chain's launches take for an utterance of `rows` frames: the buffers (the
+// features, labels, argmax keys, scratch, both layers' parameters, outputs and history), their
+// strides, the ring head at the start and the hyper-parameters.  Equal keys => identical launches.
+std::vector<uint64_t> CuRecurrentTrainer::ChainKey(size_t rows) {
+  auto& rec = dynamic_cast<CuRecurrent&>(mNet->Layer(0));
+  auto& lin = dynamic_cast<CuBiasedLinearity&>(mNet->Layer(1));
+  std::vector<uint64_t> k = {(uint64_t)rows, (uint64_t)mCrossval};
+  for (const void* p : {(const void*)mFeats.pCUData(), (const void*)mLabels.pCUData(), (const void*)mArgKey,
+                        (const void*)mSmx, (const void*)mRecPart.pCUData(), (const void*)mOutPart.pCUData(),
+                        (const void*)lin.Linearity().pCUData(), (const void*)lin.Bias().pCUData(),
+                        (const void*)lin.LinearityCorrection().pCUData(), (const void*)lin.BiasCorrection().pCUData(),
+                        (const void*)lin.Output().pCUData(), (const void*)lin.ErrorOutput().pCUData(),
+                        (const void*)mObj->DeviceStats()})
+    k.push_back((uint64_t)(uintptr_t)p);
+  float scale, l2;
+  lin.UpdateConstants(1, &scale, &l2);
+  k.insert(k.end(), {(uint64_t)mFeats.Stride(), (uint64_t)lin.Linearity().Stride(),
+                     (uint64_t)lin.LinearityCorrection().Stride(), fbits(scale), fbits(l2), fbits(lin.Momentum())});
+  rec.ChainKey(k);
+  return k;
+}
+
+// The utterance's frames on the fused chain.  Per-frame launches are short (4-9 us), so the chain is
+// recorded once per utterance length (stream capture of exactly the eager launches) and replayed as
+// one hipGraph: the host submits one graph instead of ~9 launches a frame.  The host state the frames
+// advance (ring head, frame count) is set as the recorded run left it.
+void CuRecurrentTrainer::RunFrames(size_t rows) {
+  const size_t cols = mFeats.Cols();
+  auto eager = [&]() {
+    for (size_t f = 0; f < rows; f++) {
+      CuMatrix<BaseFloat>::MakeView(mRow, mFeats.pCURowData(f), 1, cols, mFeats.Stride());
+      TrainFrameFused(f);
+    }
+  };
+  if (!GraphsEnabled()) {
+    eager();
+    return;
+  }
+  auto& rec = dynamic_cast<CuRecurrent&>(mNet->Layer(0));
+  hipStream_t st = CuDevice::Instantiate().Stream();
+  const std::vector<uint64_t> key = ChainKey(rows);
+  auto it = mGraphs.find(rows);
+  if (it == mGraphs.end()) {
+    if (mGraphs.size() >= 64) {  // bounded: lengths beyond the first 64 distinct ones run eagerly
+      eager();
+      return;
+    }
+    it = mGraphs.emplace(rows, ChainGraph()).first;
+  }
+  ChainGraph& g = it->second;
+  if (g.exec && g.key == key) {
+    TNET_HIP_CALL(hipGraphLaunch(g.exec, st));
+    rec.SetHead(g.head_after);
+    mObj->AddFrames(rows);
+    return;
+  }
+  if (g.key != key) {
+    if (g.exec) TNET_HIP_CALL(hipGraphExecDestroy(g.exec));
+    g.exec = nullptr;
+    g.key = key;
+    g.seen = 0;
+  }
+  if (++g.seen < 2) {  // first sighting: every buffer the chain touches gets allocated eagerly
+    eager();
+    return;
+  }
+  hipGraph_t graph = nullptr;
+  TNET_HIP_CALL(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
+  try {
+    eager();  // recorded, not run; the host state (head, frames) advances as in an eager run
+  } catch (...) {
+    (void)hipStreamEndCapture(st, &graph);
+    if (graph) (void)hipGraphDestroy(graph);
+    throw;
+  }
+  TNET_HIP_CALL(hipStreamEndCapture(st, &graph));
+  const hipError_t e = hipGraphInstantiate(&g.exec, graph, nullptr, nullptr, 0);
+  (void)hipGraphDestroy(graph);
+  TNET_HIP_CALL(e);
+  g.head_after = rec.Head();
+  TNET_HIP_CALL(hipGraphLaunch(g.exec, st));
 }
 
 // TRecurrentCu.cc:346-371 for one utterance in one launch: the frames' forward, cross-entropy,

@@ -13,6 +13,10 @@
 // is one pass over W.
 #pragma once
 
+#include <cstdint>
+#include <map>
+#include <vector>
+
 #include "cuobjective.h"
 #include "culayers.h"
 
@@ -52,6 +56,13 @@ class CuRecurrent : public CuUpdatableComponent {
   CuMatrix<BaseFloat>& Linearity() { return mLinearity; }  ///< [(nIn + nOut) x nOut]
   CuVector<BaseFloat>& Bias() { return mBias; }
   CuVector<BaseFloat>& BiasCorrection() { return mBiasCorrection; }
+
+  /// ring head (host state the per-frame chain advances; a graph replay sets it as the capture left it)
+  int Head() const { return mHead; }
+  void SetHead(int h) { mHead = h; }
+  /// everything the fused frame chain's launches take from this layer (device pointers, ring shape,
+  /// hyper-parameters): a recorded chain replays only while all of it is unchanged
+  void ChainKey(std::vector<uint64_t>& k) const;
 
  private:
   const float* HistRow(int i) const {  // logical history row i (0 = present)
@@ -98,6 +109,19 @@ class CuRecurrentTrainer {
   size_t mXbufBytes = 0;
   int* mErrFlag = nullptr;
   unsigned mEpoch = 0;
+  // the utterance's fused frame chain recorded as a hipGraph and replayed (TNET_RNN_GRAPH=0: off):
+  // one entry per utterance length; a key is recorded the second time it is seen (a length seen once
+  // runs eagerly) and replayed from the third on
+  struct ChainGraph {
+    std::vector<uint64_t> key;
+    int seen = 0;
+    hipGraphExec_t exec = nullptr;
+    int head_after = 0;
+  };
+  std::map<size_t, ChainGraph> mGraphs;
+  std::vector<uint64_t> ChainKey(size_t rows);
+  bool GraphsEnabled() const;
+  void RunFrames(size_t rows);
 
  public:
   ~CuRecurrentTrainer();

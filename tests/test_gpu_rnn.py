@@ -139,6 +139,39 @@ def test_rnn_fused_frame_matches_component_chain(S, bptt, mmt, wc, persistent):
         np.testing.assert_allclose(x, y, rtol=1e-4, atol=1e-6)
 
 
+@pytest.mark.parametrize("S,bptt,mmt", [(135, 4, 0.0), (4000, 2, 0.5)])
+def test_rnn_graph_replay_matches_eager(S, bptt, mmt):
+    """the per-frame chain recorded once per utterance length and replayed as a hipGraph (default)
+    vs the same chain launched eagerly (TNET_RNN_GRAPH=0): bit-identical statistics and weights.
+    Lengths repeat (recorded on the second sighting, replayed from the third), interleave, and the
+    learning rate changes between passes (a new key: recorded again)."""
+    nIn, H = 40, 64
+    rng = np.random.default_rng(S + bptt)
+    layers = formats.gen_recurrent_init(nIn, H, S, seed=13)
+    lens = [30, 30, 30, 21, 30, 21, 21, 30]
+    feats = [rng.standard_normal((T, nIn)).astype(np.float32) for T in lens]
+    labels = [rng.integers(0, S, T).astype(np.int32) for T in lens]
+
+    def run(graph):
+        os.environ["TNET_RNN_GRAPH"] = graph
+        try:
+            net = Network.from_layers(layers)
+            net.set_momentum(mmt)
+            obj = Objective()
+            tr = RnnTrainer(net, obj, bptt=bptt)
+            for lr in (0.02, 0.01):
+                net.set_learn_rate(lr)
+                tr.train_corpus(feats, labels)
+            return obj.stats(), net.recurrent_params(0) + net.linear_params()[0]
+        finally:
+            os.environ.pop("TNET_RNN_GRAPH", None)
+
+    (sa, pa), (sb, pb) = run("1"), run("0")
+    assert sa == sb and sa[1] == 2 * sum(lens)
+    for x, y in zip(pa, pb):
+        np.testing.assert_array_equal(x, y)
+
+
 @pytest.mark.parametrize("persistent", [False, True])
 def test_rnn_fused_crossval_leaves_weights(persistent):
     nIn, H, S = 24, 32, 10
