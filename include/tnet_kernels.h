@@ -394,6 +394,14 @@ int tnet_add_gauss_noise(float* mat, TnetMatrixDim d, float scale, unsigned* z1,
  * Z == NULL: Y already holds the network output (softmax not recomputed). */
 int tnet_softmax_xent(const float* Z, TnetMatrixDim dZ, const int* labels, float* Y, int strideY, float* E,
                       int strideE, double* stats, void* stream);
+/* tnet_softmax_xent + tnet_colsum_slab_sums(E) in ONE pass (one workgroup per 32-row slab; Z, Y, E,
+ * the statistics and the slab sums bit-identical to the two calls): the top layer's objective and
+ * bias-gradient slab sums for tnet_affine_update_bias (CuSoftmax::PropagateFnc +
+ * CuCrossEntropy::Evaluate, cuActivation.cc:28-31, cuObjectiveFunction.cc:50-83, and the bias gradient of
+ * CuBiasedLinearity::Update, cuBiasedLinearity.cc:36-41).  Z required; TNET_ERR_UNSUPPORTED outside
+ * 1025..4096 columns (16-B aligned rows) or when rows is not a multiple of 32 (make the two calls). */
+int tnet_softmax_xent_slabs(const float* Z, TnetMatrixDim dZ, const int* labels, float* Y, int strideY, float* E,
+                            int strideE, double* stats, float* colpart, int ldcolpart, void* stream);
 /* Same objective for dense desired matrices D (any soft targets; cuObjectiveFunction.cc:50-83):
  * Y = softmax(Z) (if Z != NULL, else Y already holds the network output), E = Y - D, stats as above
  * with xent = -sum D log(max(Y, FLT_MIN)). */

@@ -317,13 +317,31 @@ void CuNetwork::TrainBunch(const CuMatrix<BaseFloat>& X, const CuVector<int>& la
     act = &dst;
     acts[l + 1] = &dst;
   }
-  // ---- objective: softmax + xent + error (+ optional softmax output)
+  // ---- objective: softmax + xent + error (+ optional softmax output); for wide outputs with the top
+  // layer trained, the error's slab sums (its bias gradient) in the same pass (TNET_SOFTMAX_SLABS=0: two
+  // launches, A/B measurements)
   if (!fused_top) {
     CuMatrix<BaseFloat>& logits = mNetComponents[2 * (nl - 1)]->Output();
-    KTScope kts("softmax_xent:" + std::to_string(GetNOutputs()),
-                (double)rows * GetNOutputs() * 4.0 * (mKeepOutput ? 3 : 2) + rows * 4.0);
-    TNET_SAFE_CALL(tnet_softmax_xent(logits.pCUData(), logits.Dim(), labels.pCUData(), yout, ystride,
-                                     mGlobErr.pCUData(), (int)mGlobErr.Stride(), obj.DeviceStats(), S));
+    static const bool slab_pass = !(getenv("TNET_SOFTMAX_SLABS") && getenv("TNET_SOFTMAX_SLABS")[0] == '0');
+    int st = TNET_ERR_UNSUPPORTED;
+    if (top_colsum && slab_pass) {
+      CuMatrix<BaseFloat>& cp = *mColPart[nl - 1];
+      cp.Init(tnet_colsum_slabs((int)rows), GetNOutputs());
+      KTScope kts("softmax_xent+colsum:" + std::to_string(GetNOutputs()),
+                  (double)rows * GetNOutputs() * 4.0 * (mKeepOutput ? 3 : 2) + rows * 4.0);
+      st = tnet_softmax_xent_slabs(logits.pCUData(), logits.Dim(), labels.pCUData(), yout, ystride,
+                                   mGlobErr.pCUData(), (int)mGlobErr.Stride(), obj.DeviceStats(), cp.pCUData(),
+                                   (int)cp.Stride(), S);
+      if (st == TNET_ERR_UNSUPPORTED) kts.Cancel();
+      else err_colsum = true;
+    }
+    if (st == TNET_ERR_UNSUPPORTED) {
+      KTScope kts("softmax_xent:" + std::to_string(GetNOutputs()),
+                  (double)rows * GetNOutputs() * 4.0 * (mKeepOutput ? 3 : 2) + rows * 4.0);
+      st = tnet_softmax_xent(logits.pCUData(), logits.Dim(), labels.pCUData(), yout, ystride, mGlobErr.pCUData(),
+                             (int)mGlobErr.Stride(), obj.DeviceStats(), S);
+    }
+    TNET_SAFE_CALL(st);
   }
   obj.AddFrames(rows);
   if (!train) return;
@@ -333,7 +351,7 @@ void CuNetwork::TrainBunch(const CuMatrix<BaseFloat>& X, const CuVector<int>& la
   std::vector<CuBiasedLinearity*> submitted;  // data-parallel: layers in reduction order, not yet applied
   const size_t grows = exchange ? exchange->GlobalRows(rows) : rows;
   int n_submitted = 0;
-  if (top_colsum && !fused_top) {
+  if (top_colsum && !fused_top && !err_colsum) {
     CuMatrix<BaseFloat>& cp = *mColPart[nl - 1];
     cp.Init(tnet_colsum_slabs((int)rows), GetNOutputs());
     KTScope kt("colsum:" + std::to_string(GetNOutputs()), 4.0 * rows * GetNOutputs());

@@ -538,7 +538,147 @@ __global__ __launch_bounds__(256) void softmax_xent_row4_kernel(const float* __r
   }
 }
 
+// The wide-row softmax (softmax_xent_row4_kernel) and the error's 32-row slab column sums
+// (tnet_colsum_slab_sums / colsum_partial_kernel) in ONE pass: a 1024-thread workgroup per slab, whose
+// row-group g (waves 4g..4g+3) takes the slab's rows r0+g, r0+g+4, ..., r0+g+28 -- colsum_partial's row
+// sub-group g -- one at a time with row4's arithmetic and lane-to-column map (Y, E, the statistics
+// bit-identical), adding each error row into registers in that row order; the four row-groups' sums
+// meet in LDS and are added in group order (colsum_partial's order: the slab sums bit-identical too).
+// The error is formed once and never read back (the separate column-sum launch re-read 16 MB at 4000
+// senones).
+__global__ __launch_bounds__(1024) void softmax_xent_slab_kernel(const float* __restrict__ Z, TnetMatrixDim d,
+                                                                 const int* __restrict__ labels,
+                                                                 float* __restrict__ Y, int strideY,
+                                                                 float* __restrict__ E, int strideE,
+                                                                 double* __restrict__ stats,
+                                                                 float* __restrict__ colpart, long ldp) {
+  constexpr int CPW = SX_MAXV4 / 4;  // chunks per wave
+  __shared__ float smax[16];
+  __shared__ double ssum[16];
+  __shared__ ArgMax sarg[16];
+  __shared__ float red[3][SX_MAXV4 * 256];  // row-groups 1..3's column sums
+  const int lane = threadIdx.x & 63, w16 = threadIdx.x >> 6, g = w16 >> 2, wv = w16 & 3;
+  const int N = d.cols, r0 = blockIdx.x * CS_ROWS;
+  float acc[CPW][4];
+#pragma unroll
+  for (int q = 0; q < CPW; ++q)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) acc[q][k] = 0.f;
+  for (int it = 0; it < CS_ROWS / 4; ++it) {
+    const int row = r0 + g + 4 * it;
+    const float* src = Z + (long)row * d.stride;
+    f32x4 rv[CPW];
+    float m = -1e20f;
+#pragma unroll
+    for (int q = 0; q < CPW; ++q) {
+      const int c = (wv + 4 * q) * 256 + lane * 4;
+      f32x4 x = {-1e30f, -1e30f, -1e30f, -1e30f};
+      if (c < N) x = *reinterpret_cast<const f32x4*>(src + c);
+      rv[q] = x;
+      m = fmaxf(m, fmaxf(fmaxf(x[0], x[1]), fmaxf(x[2], x[3])));
+    }
+    m = wave_max(m);
+    if (lane == 0) smax[w16] = m;
+    __syncthreads();
+    m = fmaxf(fmaxf(smax[4 * g], smax[4 * g + 1]), fmaxf(smax[4 * g + 2], smax[4 * g + 3]));
+    float s = 0.f;
+#pragma unroll
+    for (int q = 0; q < CPW; ++q) {
+      const int c = (wv + 4 * q) * 256 + lane * 4;
+      if (c < N) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const float e = fast_exp(rv[q][k] - m);
+          rv[q][k] = e;
+          s += e;
+        }
+      }
+    }
+    const double ws = wave_sum_d((double)s);
+    if (lane == 0) ssum[w16] = ws;
+    __syncthreads();
+    const float sum = (float)(ssum[4 * g] + ssum[4 * g + 1] + ssum[4 * g + 2] + ssum[4 * g + 3]);
+    const float rsum = 1.f / sum;
+    int t = labels[row];
+    if (t >= N) t = -1;  // out of range: an unlabeled row (the host intake rejects one, CheckLabels)
+    float* yrow = Y ? Y + (long)row * strideY : nullptr;
+    float* erow = E + (long)row * strideE;
+    const __amdgpu_buffer_rsrc_t ry = tile_rsrc(yrow ? yrow : erow), re = tile_rsrc(erow);
+    ArgMax ay{-1e20f, 0x7fffffff};
+#pragma unroll
+    for (int q = 0; q < CPW; ++q) {
+      const int c = (wv + 4 * q) * 256 + lane * 4;
+      if (c < N) {
+        f32x4 y, e;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          y[k] = rv[q][k] * rsum;
+          if (y[k] > ay.v) { ay.v = y[k]; ay.i = c + k; }
+          e[k] = y[k] - ((c + k == t) ? 1.f : 0.f);
+          acc[q][k] += e[k];
+        }
+        if (yrow) st_wt(ry, c, y);
+        st_wt(re, c, e);
+      }
+    }
+    ay = wave_argmax(ay);
+    if (lane == 0) sarg[w16] = ay;
+    __syncthreads();
+    if (wv == 0 && lane == 0) {
+      ArgMax a = sarg[4 * g];
+#pragma unroll
+      for (int w = 1; w < 4; ++w) a = argmax_merge(a, sarg[4 * g + w]);
+      const int des = t >= 0 ? t : 0;  // all-zero target row: first max of zeros is column 0
+      double xent = 0.0;
+      if (t >= 0) {
+        const float yt = fast_exp(src[t] - m) * rsum;  // the y written for column t
+        xent = -(double)logf(fmaxf(yt, FLT_MIN));
+      }
+      if (stats) {
+        const int slot = row % TNET_STATS_SLOTS;  // row4's slot (its block index is the row)
+        atomicAdd(stats + 2 * slot, xent);
+        atomicAdd(stats + 2 * slot + 1, (a.i == des) ? 1.0 : 0.0);
+      }
+    }
+  }
+  if (g > 0) {
+#pragma unroll
+    for (int q = 0; q < CPW; ++q) {
+      const int c = (wv + 4 * q) * 256 + lane * 4;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) red[g - 1][c + k] = acc[q][k];
+    }
+  }
+  __syncthreads();
+  if (g == 0) {
+    float* dst = colpart + (long)blockIdx.x * ldp;
+#pragma unroll
+    for (int q = 0; q < CPW; ++q) {
+      const int c = (wv + 4 * q) * 256 + lane * 4;
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (c + k < N) dst[c + k] = ((acc[q][k] + red[0][c + k]) + red[1][c + k]) + red[2][c + k];
+    }
+  }
+}
+
 static bool v4ok(const void* p, int stride) { return ((uintptr_t)p & 15) == 0 && (stride & 3) == 0; }
+
+extern "C" int tnet_softmax_xent_slabs(const float* Z, TnetMatrixDim dZ, const int* labels, float* Y, int strideY,
+                                       float* E, int strideE, double* stats, float* colpart, int ldcolpart,
+                                       void* stream) {
+  if (dZ.rows < 0 || dZ.cols <= 0 || !labels || !Z || !E || !colpart || ldcolpart < dZ.cols) return TNET_ERR_ARG;
+  if (!dZ.rows) return TNET_OK;
+  // row4's domain (16-B aligned rows of 1025..4096 columns) and whole 32-row slabs of the uncapped count
+  const bool v4 = (dZ.cols & 3) == 0 && v4ok(Z, dZ.stride) && (!Y || v4ok(Y, strideY)) && v4ok(E, strideE);
+  if (!v4 || dZ.cols <= 1024 || dZ.cols > SX_MAXV4 * 256 || dZ.rows % CS_ROWS != 0 ||
+      cs_slabs(dZ.rows) != dZ.rows / CS_ROWS)
+    return TNET_ERR_UNSUPPORTED;
+  softmax_xent_slab_kernel<<<dZ.rows / CS_ROWS, 1024, 0, (hipStream_t)stream>>>(Z, dZ, labels, Y, strideY, E, strideE,
+                                                                                stats, colpart, ldcolpart);
+  TNET_LAUNCH_CHECK();
+  return TNET_OK;
+}
 
 extern "C" int tnet_softmax_xent(const float* Z, TnetMatrixDim dZ, const int* labels, float* Y, int strideY, float* E,
                                  int strideE, double* stats, void* stream) {

@@ -86,6 +86,7 @@ _SIGS = {
     "tnet_sgd_update": (i32, [vp, vp, vp, i64, f32, f32, f32, vp]),
     "tnet_bias_update": (i32, [vp, MatrixDim, vp, vp, vp, f32, f32, vp, vp]),
     "tnet_softmax_xent": (i32, [vp, MatrixDim, vp, vp, i32, vp, i32, vp, vp]),
+    "tnet_softmax_xent_slabs": (i32, [vp, MatrixDim, vp, vp, i32, vp, i32, vp, vp, i32, vp]),
     "tnet_softmax_xent_dense": (i32, [vp, MatrixDim, vp, i32, vp, i32, vp, i32, vp, vp]),
     "tnet_mse": (i32, [vp, MatrixDim, vp, i32, vp, i32, vp, vp]),
     "tnet_stats_fetch": (i32, [vp, dp, dp, vp]),

@@ -560,6 +560,59 @@ def test_colsum_slab_sums(rows, cols):
         assert np.all(np.abs(P - slab_sums(E)) <= 32 * 1.2e-7 * slab_sums(np.abs(E)) + 1e-7)
 
 
+@pytest.mark.parametrize("rows,cols,keep_y", [(1024, 4000, False), (1024, 4000, True), (64, 1028, True),
+                                               (96, 4096, False), (32, 2048, False)])
+def test_softmax_xent_slabs_matches_two_calls(rows, cols, keep_y):
+    """tnet_softmax_xent_slabs (one workgroup per 32-row slab) vs tnet_softmax_xent +
+    tnet_colsum_slab_sums: Y, E, the statistics slots and the slab sums bit-identical; unlabeled and
+    out-of-range class ids included"""
+    Z = rnd((rows, cols), 41, 3.0)
+    lab = np.random.default_rng(42).integers(0, cols, size=rows).astype(np.int32)
+    lab[::7] = -1
+    lab[3::11] = cols + 5
+    slabs = lib().tnet_colsum_slabs(rows)
+    out = []
+    for fused in (True, False):
+        dZ, dL = DeviceArray.from_numpy(Z), DeviceArray.vector(lab)
+        dY = DeviceArray(rows, cols) if keep_y else None
+        dE = DeviceArray(rows, cols)
+        dP = DeviceArray.from_numpy(np.full((slabs, cols), np.nan, np.float32))
+        stats = DeviceArray(1, 1024, np.float64, stride=1024)
+        yp, ys = (dY.ptr, dY.stride) if keep_y else (None, 0)
+        if fused:
+            check(lib().tnet_softmax_xent_slabs(dZ.ptr, dZ.dim, dL.ptr, yp, ys, dE.ptr, dE.stride, stats.ptr, dP.ptr,
+                                                dP.stride, S()))
+        else:
+            check(lib().tnet_softmax_xent(dZ.ptr, dZ.dim, dL.ptr, yp, ys, dE.ptr, dE.stride, stats.ptr, S()))
+            check(lib().tnet_colsum_slab_sums(dE.ptr, dE.dim, dP.ptr, dP.stride, S()))
+        out.append((dY.numpy() if keep_y else None, dE.numpy(), dP.numpy(), stats.numpy()[0]))
+    (ya, ea, pa, sa), (yb, eb, pb, sb) = out
+    if keep_y:
+        np.testing.assert_array_equal(ya, yb)
+    np.testing.assert_array_equal(ea, eb)
+    np.testing.assert_array_equal(pa, pb)
+    # per-slot sums of fp64 atomics: the same addends, order free -- equal to rounding
+    np.testing.assert_allclose(sa, sb, rtol=1e-12, atol=1e-12)
+    ref = lab.copy()
+    ref[ref >= cols] = -1
+    Eref, xent, correct = orc.xent_eval(orc.softmax(Z), ref)
+    np.testing.assert_allclose(ea, Eref, rtol=2e-5, atol=1e-8)
+    assert int(round(sa[1::2].sum())) == correct
+
+
+@pytest.mark.parametrize("rows,cols", [(100, 4000), (64, 1024), (64, 4100), (64, 135)])
+def test_softmax_xent_slabs_unsupported_shapes(rows, cols):
+    """outside whole 32-row slabs of 1025..4096 columns the fused pass declines (the caller makes the
+    two calls)"""
+    dZ, dL = DeviceArray.from_numpy(rnd((rows, cols), 43)), DeviceArray.vector(np.zeros(rows, np.int32))
+    dE = DeviceArray(rows, cols)
+    dP = DeviceArray(max(1, lib().tnet_colsum_slabs(rows)), cols)
+    stats = DeviceArray(1, 1024, np.float64, stride=1024)
+    st = lib().tnet_softmax_xent_slabs(dZ.ptr, dZ.dim, dL.ptr, None, 0, dE.ptr, dE.stride, stats.ptr, dP.ptr,
+                                       dP.stride, S())
+    assert st == TNET_ERR_UNSUPPORTED
+
+
 def test_check_class_first_max_wins():
     out = np.array([[0.1, 0.5, 0.5, 0.2], [0.3, 0.3, 0.3, 0.3], [0, 0, 0, 1]], np.float32)
     des = np.array([[0, 1, 0, 0], [1, 0, 0, 0], [0, 0, 1, 0]], np.float32)
