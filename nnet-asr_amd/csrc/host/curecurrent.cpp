@@ -198,8 +198,9 @@ void CuRecurrentTrainer::TrainUtterance(const float* feats, size_t rows, size_t 
 bool CuRecurrentTrainer::GraphsEnabled() const {
   const char* e = getenv("TNET_RNN_GRAPH");
   if (e && e[0] == '0') return false;
-  const CuDevice& dev = CuDevice::Instantiate();
-  return !dev.KernelTiming() && !dev.Profile();  // event records do not belong in a recorded chain
+  CuDevice& dev = CuDevice::Instantiate();
+  // event records do not belong in a recorded chain; the legacy null stream cannot be captured
+  return !dev.KernelTiming() && !dev.Profile() && dev.Stream() != nullptr;
 }
 
 // Every value the fused chain's launches take for an utterance of `rows` frames: the buffers (the
