@@ -139,8 +139,9 @@ def test_rnn_fused_frame_matches_component_chain(S, bptt, mmt, wc, persistent):
         np.testing.assert_allclose(x, y, rtol=1e-4, atol=1e-6)
 
 
+@pytest.mark.parametrize("crossval", [False, True])
 @pytest.mark.parametrize("S,bptt,mmt", [(135, 4, 0.0), (4000, 2, 0.5)])
-def test_rnn_graph_replay_matches_eager(S, bptt, mmt):
+def test_rnn_graph_replay_matches_eager(S, bptt, mmt, crossval):
     """the per-frame chain recorded once per utterance length and replayed as a hipGraph (default)
     vs the same chain launched eagerly (TNET_RNN_GRAPH=0): bit-identical statistics and weights.
     Lengths repeat (recorded on the second sighting, replayed from the third), interleave, and the
@@ -158,7 +159,7 @@ def test_rnn_graph_replay_matches_eager(S, bptt, mmt):
             net = Network.from_layers(layers)
             net.set_momentum(mmt)
             obj = Objective()
-            tr = RnnTrainer(net, obj, bptt=bptt)
+            tr = RnnTrainer(net, obj, bptt=bptt, crossval=crossval)
             for lr in (0.02, 0.01):
                 net.set_learn_rate(lr)
                 tr.train_corpus(feats, labels)
@@ -170,6 +171,9 @@ def test_rnn_graph_replay_matches_eager(S, bptt, mmt):
     assert sa == sb and sa[1] == 2 * sum(lens)
     for x, y in zip(pa, pb):
         np.testing.assert_array_equal(x, y)
+    if crossval:  # cross-validation replays leave the weights as read
+        np.testing.assert_array_equal(pa[0], layers[0].W)
+        np.testing.assert_array_equal(pa[2], layers[1].W)
 
 
 @pytest.mark.parametrize("persistent", [False, True])
