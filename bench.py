@@ -20,6 +20,7 @@ kernels (per-kernel breakdown from extra all-events steps after the timed region
 reference CPU TNet on this host, rank 0 at N=1).
 """
 import argparse
+import ctypes
 import json
 import os
 import sys
@@ -146,7 +147,11 @@ def main():
     dims = CONFIGS[args.config]
     B = args.bunch
 
-    check(lib().tnet_select_gpu(0 if args.same_device else local_rank), "select_gpu")
+    # one GPU per rank; a launcher that leaves each rank only its own device visible gets device 0
+    ndev = ctypes.c_int(0)
+    check(lib().tnet_device_count(ctypes.byref(ndev)), "device_count")
+    check(lib().tnet_select_gpu(0 if args.same_device or ndev.value <= 0 else local_rank % ndev.value),
+          "select_gpu")
     dist = None
     comm = None
     if world > 1:
@@ -194,7 +199,6 @@ def main():
     dt = time.perf_counter() - t0
     # roofline region: the next K steps of the same workload with one hipEvent pair around each run of
     # back-to-back roofline kernels (each pair adds ~3 us of stream time, so not inside the value region)
-    import ctypes
     buf = ctypes.create_string_buffer(1 << 16)
     kern = {}
     if args.kernel_timing:
