@@ -10,7 +10,10 @@ TNetCu per-bunch loop (src/TNetCu.cc:427-441).
 Multi-GPU (launched by torch.distributed.run): one process per GPU, utterance-sharded caches
 (weak scaling: 1024 frames per GPU per step), per-layer RCCL all-reduce of the gradients over
 xGMI, global-bunch GRADDIVFRM normalisation.  torch is used only for the gloo rendezvous /
-barrier / max-reduce of the timings; at N>1 it is imported before the HIP library (one ROCm runtime, clean exit).
+barrier / max-reduce of the timings (tnet_amd maps torch's ROCm runtime before the library whenever
+torch is installed: one HIP runtime and one RCCL per process, whatever the import order).  After the
+timed region every rank checksums its parameters and the ranks compare them: replicas that differ
+(a broken exchange) end the run with a non-zero exit instead of a number.
 
 Extra JSON fields: roofline (dominant kernel = the 2048x2048 affine-layer GEMMs, timed with hipEvents
 on the library stream over K further steps of the same workload right after the timed region: one
@@ -32,11 +35,6 @@ sys.path.insert(0, os.path.join(REPO, "oracle"))
 
 import numpy as np  # noqa: E402
 
-if int(os.environ.get("WORLD_SIZE", "1")) > 1 or os.environ.get("TNET_BENCH_TORCH_FIRST"):
-    # multi-rank: torch (rendezvous / barrier / max over ranks) is loaded BEFORE the HIP library, so its
-    # bundled ROCm runtime serves both -- the order of tests/dp_worker.py.  Loaded after, the process
-    # aborted in runtime teardown at exit ("double free or corruption") once the JSON line was out.
-    import torch  # noqa: E402,F401
 import tnet_amd  # noqa: E402
 from tnet_amd import Comm, Network, Objective, Trainer, formats  # noqa: E402
 from tnet_amd._lib import check, lib  # noqa: E402
@@ -90,6 +88,20 @@ def pmc_traffic():
     return d["traffic_MB_per_launch"] * 1e6, os.path.relpath(files[-1], REPO)
 
 
+def param_checksum(net):
+    """(sha256 of every parameter's bytes, float64 sum): replicas of a data-parallel run must be
+    bit-identical (every rank applies the same reduced gradient / gathers the same shards)."""
+    import hashlib
+    h = hashlib.sha256()
+    tot = 0.0
+    for W, b in net.linear_params():
+        for a in (W, b):
+            a = np.ascontiguousarray(a, np.float32)
+            h.update(a.tobytes())
+            tot += float(a.sum(dtype=np.float64))
+    return h.hexdigest()[:16], repr(tot)
+
+
 def parse_kernel_report(text):
     out = {}
     for line in text.strip().splitlines():
@@ -102,8 +114,8 @@ def parse_kernel_report(text):
 
 
 def dp_mode(world):
-    """the RCCL exchange's form (RcclExchange: sharded apply at N > 1 unless TNET_DP_SHARD=0)"""
-    shard = os.environ.get("TNET_DP_SHARD", "1" if world > 1 else "0") == "1"
+    """the RCCL exchange's form (RcclExchange: all-reduce unless TNET_DP_SHARD=1)"""
+    shard = os.environ.get("TNET_DP_SHARD", "0") == "1"
     return (" (RCCL reduce-scatter, sharded SGD apply, all-gather)" if shard else " (RCCL all-reduce)")
 
 
@@ -147,11 +159,20 @@ def main():
     dims = CONFIGS[args.config]
     B = args.bunch
 
-    # one GPU per rank; a launcher that leaves each rank only its own device visible gets device 0
+    # one GPU per rank: device local_rank; a launcher that leaves each rank only its own device visible
+    # gives device 0.  Anything in between would put two ranks on one GPU and report an oversubscribed
+    # whole-node number, so it is an error (--same-device is the explicit rehearsal form).
     ndev = ctypes.c_int(0)
     check(lib().tnet_device_count(ctypes.byref(ndev)), "device_count")
-    check(lib().tnet_select_gpu(0 if args.same_device or ndev.value <= 0 else local_rank % ndev.value),
-          "select_gpu")
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+    if args.same_device or ndev.value == 1:
+        dev = 0
+    elif ndev.value >= local_world:
+        dev = local_rank
+    else:
+        raise SystemExit(f"{ndev.value} GPUs visible to rank {rank} for {local_world} local ranks: "
+                         "one GPU per rank needed (or --same-device for a host-transport rehearsal)")
+    check(lib().tnet_select_gpu(dev), "select_gpu")
     dist = None
     comm = None
     if world > 1:
@@ -223,6 +244,14 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
 
+    replicas = param_checksum(net)
+    if dist is not None:
+        got = [None] * world
+        dist.all_gather_object(got, replicas)
+        if any(g != got[0] for g in got):
+            print("bench: parameter replicas differ across ranks after the run: " + json.dumps(got), file=sys.stderr)
+            raise SystemExit(3)
+
     frames = world * args.steps * B
     value = frames / dt
     ms_per_step = 1000.0 * dt / args.steps
@@ -285,6 +314,8 @@ def main():
                        "gemm_share_of_kernel_time": round(all_gemm_ms / all_ms, 4) if all_ms else None},
             "roofline": roof,
             "cpu_baseline": cpu,
+            "replica_check": {"ranks": world, "identical": True, "param_sha256_16": replicas[0],
+                              "param_sum": replicas[1]},
             "kernels": kernels,
             "kernels_note": f"every launch event-timed, {args.breakdown_steps} extra steps after the timed region "
                             "(event pairs add stream time: the value region has none, the roofline region times "

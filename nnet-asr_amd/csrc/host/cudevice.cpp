@@ -1,11 +1,40 @@
 // cudevice.cpp -- see cudevice.h.
 #include "cudevice.h"
 
+#include <execinfo.h>
+#include <signal.h>
+#include <unistd.h>
+
+#include <cstdlib>
 #include <iomanip>
 #include <iostream>
 #include <sstream>
 
 namespace TNet {
+
+// TNET_SEGV_TRACE=1: a host SIGSEGV / SIGABRT prints the faulting thread's native backtrace to stderr
+// before the default action (diagnostics for crashes inside the runtime or a profiler tool, where no
+// debugger may attach; the frames are resolved offline with addr2line / llvm-symbolizer).
+static void segv_trace(int sig) {
+  void* frames[64];
+  const int n = backtrace(frames, 64);
+  const char msg[] = "\n*** tnet: fatal signal, native backtrace:\n";
+  (void)!write(2, msg, sizeof(msg) - 1);
+  backtrace_symbols_fd(frames, n, 2);
+  signal(sig, SIG_DFL);
+  raise(sig);
+}
+
+static void install_segv_trace() {
+  static bool done = false;
+  if (done) return;
+  done = true;
+  const char* e = getenv("TNET_SEGV_TRACE");
+  if (!e || e[0] != '1') return;
+  signal(SIGSEGV, segv_trace);
+  signal(SIGBUS, segv_trace);
+  signal(SIGABRT, segv_trace);
+}
 
 CuDevice& CuDevice::Instantiate() {
   static CuDevice dev;
@@ -17,6 +46,7 @@ CuDevice::CuDevice() {}
 
 void CuDevice::EnsureInit() {
   if (mInit) return;
+  install_segv_trace();
   int n = 0;
   TNET_HIP_CALL(hipGetDeviceCount(&n));
   if (n <= 0) Error("CuDevice: no HIP device visible");

@@ -199,8 +199,9 @@ bool CuRecurrentTrainer::GraphsEnabled() const {
   const char* e = getenv("TNET_RNN_GRAPH");
   if (e && e[0] == '0') return false;
   // under a rocprofiler-sdk tool (rocprofv3 sets ROCP_TOOL_LIBRARIES) the recorded chain crashed inside
-  // the runtime (rocprofv3 --kernel-trace, this image's ROCm 7.2): profile the eager chain instead
-  if (getenv("ROCP_TOOL_LIBRARIES")) return false;
+  // the runtime (rocprofv3 --kernel-trace, this image's ROCm 7.2): profile the eager chain instead,
+  // unless TNET_RNN_GRAPH=1 asks for the graphs explicitly (the diagnosis runs)
+  if (getenv("ROCP_TOOL_LIBRARIES") && !(e && e[0] == '1')) return false;
   CuDevice& dev = CuDevice::Instantiate();
   // event records do not belong in a recorded chain; the legacy null stream cannot be captured
   return !dev.KernelTiming() && !dev.Profile() && dev.Stream() != nullptr;

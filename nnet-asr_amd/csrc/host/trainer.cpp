@@ -196,14 +196,31 @@ DpRoundPlan DpPlanRound(GradExchange& ex, long n, bool final) {
 // ======================================================================================
 // host-transport exchange
 // ======================================================================================
-static bool shard_env(bool dflt) {
+// TNET_DP_SHARD=1: reduce-scatter + sharded apply + all-gather instead of the all-reduce.  Off by
+// default on every transport until a multi-rank RCCL run has shown the sharded parameters equal the
+// all-reduce path's (the protocol is tested over the host transport only).  Under sharding a rank's
+// momentum buffers are valid only on its own shard (+ the tail): a later purely local update (no
+// communicator) would let the replicas drift apart.
+static bool shard_env() {
   const char* e = getenv("TNET_DP_SHARD");
-  return e ? e[0] == '1' : dflt;
+  return e && e[0] == '1';
+}
+
+// every rank must run the same exchange form: one rank issuing reduce-scatter / all-gather while
+// another issues all-reduce hangs or corrupts the collectives
+static void check_same_shard_mode(GradExchange& ex, bool shard, int world) {
+  double v[2] = {shard ? 1.0 : 0.0, 1.0};
+  ex.AllReduceHost(v, 2);
+  if (v[1] != (double)world) Error("GradExchange: rank count mismatch at communicator creation");
+  if (v[0] != 0.0 && v[0] != (double)world)
+    Error("GradExchange: ranks disagree on TNET_DP_SHARD (sharded apply on some ranks only)");
 }
 
 HostExchange::HostExchange(int rank, int world, HostAllReduceFn fn, void* user)
-    : mRank(rank), mWorld(world), mShard(shard_env(false)),
-      mInline(getenv("TNET_DP_HOST_INLINE") && getenv("TNET_DP_HOST_INLINE")[0] == '1'), mFn(fn), mUser(user) {}
+    : mRank(rank), mWorld(world), mShard(shard_env()),
+      mInline(getenv("TNET_DP_HOST_INLINE") && getenv("TNET_DP_HOST_INLINE")[0] == '1'), mFn(fn), mUser(user) {
+  check_same_shard_mode(*this, mShard, mWorld);
+}
 
 void* HostExchange::ApplyStream(int i) {
   (void)i;
@@ -289,7 +306,7 @@ void RcclExchange::UniqueId(char out[128]) {
 }
 
 RcclExchange::RcclExchange(int rank, int world, const char id[128])
-    : mImpl(new Impl), mRank(rank), mWorld(world), mShard(shard_env(world > 1)) {
+    : mImpl(new Impl), mRank(rank), mWorld(world), mShard(shard_env()) {
   CuDevice& dev = CuDevice::Instantiate();
   ncclUniqueId uid;
   std::memcpy(&uid, id, 128);
@@ -300,6 +317,7 @@ RcclExchange::RcclExchange(int rank, int world, const char id[128])
   TNET_HIP_CALL(hipEventCreateWithFlags(&mImpl->apply_done, hipEventDisableTiming));
   TNET_HIP_CALL(hipMalloc(&mImpl->dscratch, 4096));
   (void)dev;
+  check_same_shard_mode(*this, mShard, mWorld);
 }
 
 RcclExchange::~RcclExchange() {
@@ -360,7 +378,7 @@ void RcclExchange::GatherParams(CuUpdatableComponent& comp, int i, void* stream)
   if (i < 0 || (size_t)i >= mImpl->next_event) Error("RcclExchange::GatherParams: no such reduction");
   // the comm stream waits for this layer's applies (their stream), then all-gathers the shards in
   // place: the next collectives queue behind it, the compute stream joins at WaitAll
-  if (mImpl->gather_ev.size() <= (size_t)i) {
+  while (mImpl->gather_ev.size() <= (size_t)i) {
     hipEvent_t e;
     TNET_HIP_CALL(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     mImpl->gather_ev.push_back(e);

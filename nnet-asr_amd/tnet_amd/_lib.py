@@ -212,12 +212,62 @@ def header_symbols():
     return sorted(set(names))
 
 
+def _torch_rocm_dir():
+    """torch's bundled ROCm runtime directory, found WITHOUT importing torch (None if absent)."""
+    import importlib.util
+    try:
+        spec = importlib.util.find_spec("torch")
+    except (ImportError, ValueError):
+        return None
+    if spec is None or not spec.origin:
+        return None
+    d = os.path.join(os.path.dirname(spec.origin), "lib")
+    return d if os.path.exists(os.path.join(d, "libamdhip64.so")) else None
+
+
+def hip_runtimes_mapped():
+    """Distinct libamdhip64 files mapped into this process (/proc/self/maps)."""
+    seen = set()
+    try:
+        with open("/proc/self/maps") as f:
+            for line in f:
+                p = line.split()[-1] if line.strip() else ""
+                if "libamdhip64.so" in os.path.basename(p):
+                    seen.add(os.path.realpath(p))
+    except OSError:
+        pass
+    return sorted(seen)
+
+
+def _one_hip_runtime():
+    """Exactly one HIP runtime and one RCCL per process, whatever the import order.
+
+    PyTorch-ROCm ships its own libamdhip64 / libhsa-runtime64 / librccl (torch/lib, RPATH $ORIGIN,
+    NEEDED by file name "libamdhip64.so", "librccl.so"); this library links /opt/rocm's by soname
+    (libamdhip64.so.7, librccl.so.1).  Loaded before torch, ours makes torch map a second HIP runtime
+    and a second RCCL beside it, and any librccl mapped before libtorch_hip -- torch's own copy
+    included -- ends the process in "double free or corruption" at exit (reproduced here without a
+    GPU).  Loaded after torch, our sonames resolve to torch's already-mapped files: one runtime, one
+    RCCL, clean exit.  So when torch is installed it is imported first (bench.py and the DP tests use
+    torch.distributed for rendezvous anyway).  TNET_HIP_RUNTIME=system skips this (then the process
+    must not import torch later); processes without torch -- the drop-in drivers, C callers -- use
+    /opt/rocm's runtime."""
+    if os.environ.get("TNET_HIP_RUNTIME", "") == "system" or _torch_rocm_dir() is None:
+        return
+    import torch  # noqa: F401
+
+
 def lib():
     global _lib
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             raise TnetError(f"{LIB_PATH} not built: run `make -C nnet-asr_amd` (or __graft_entry__.build())")
+        _one_hip_runtime()
         L = C.CDLL(LIB_PATH, mode=C.RTLD_GLOBAL)
+        rt = hip_runtimes_mapped()
+        if len(rt) > 1:
+            raise TnetError("two HIP runtimes mapped into one process: " + ", ".join(rt) +
+                            " (load libtnet_amd through tnet_amd, or set TNET_HIP_RUNTIME consistently)")
         for name, (res, args) in _SIGS.items():
             fn = getattr(L, name)
             fn.restype = res

@@ -287,6 +287,82 @@ def read_htk(path: str) -> np.ndarray:
     return data.reshape(n, size // 4)
 
 
+def read_htk_header(path: str):
+    """(frames, sample period [100 ns], bytes per frame, parameter kind)."""
+    with open(path, "rb") as f:
+        return struct.unpack(">iihh", f.read(12))
+
+
+def read_state_map(path: str) -> dict:
+    """LabelRepository::ReadOutputLabelMap (src/KaldiLib/Labels.cc:192-212): whitespace-separated
+    state tags, id = position."""
+    tags = open(path).read().split()
+    if len(set(tags)) != len(tags):
+        raise ValueError(f"{path}: duplicate state tag")
+    return {t: i for i, t in enumerate(tags)}
+
+
+def read_mlf(path: str) -> dict:
+    """An HTK master label file -> {pattern: [(beg, end, tag), ...]} (times in 100 ns units)."""
+    out, cur = {}, None
+    with open(path) as f:
+        for line in f:
+            s = line.strip()
+            if not s or s.startswith("#"):
+                continue
+            if s.startswith('"'):
+                cur = out.setdefault(s.strip('"'), [])
+            elif s == ".":
+                cur = None
+            elif cur is not None:
+                beg, end, tag = s.split()[:3]
+                cur.append((int(beg), int(end), tag))
+    return out
+
+
+def mlf_class_ids(segments, n_frames: int, samp_period: int, state_map: dict) -> np.ndarray:
+    """LabelRepository::GenDesiredMatrix (src/KaldiLib/Labels.cc:42-186) as class ids: frame
+    interval [(beg + P/2) / P, (end + P/2) / P), frames past the feature end dropped, a frame
+    labelled twice or never is an error (the reference's row-sum check)."""
+    lab = np.full(n_frames, -1, np.int32)
+    half = samp_period // 2
+    for beg, end, tag in segments:
+        if tag not in state_map:
+            raise ValueError(f"Unknown state tag: '{tag}'")
+        b, e = (beg + half) // samp_period, (end + half) // samp_period
+        for t in range(b, min(e, n_frames)):
+            if lab[t] != -1:
+                raise ValueError(f"Frame already assigned to other state, frame: {t}")
+            lab[t] = state_map[tag]
+    if (lab < 0).any():
+        raise ValueError(f"Desired vector sum isn't 1.0, row: {int(np.argmax(lab < 0))}")
+    return lab
+
+
+def read_corpus(scp: str, mlf: str, states: str, label_dir: str = "*/", label_ext: str = "lab",
+                base: Optional[str] = None) -> "Corpus":
+    """The FeatureRepository + LabelRepository intake of TNet / TNetCu (-S scp -I mlf -L dir -X ext
+    -m states): HTK features in scp order, per-frame class ids from the MLF.  Relative scp paths are
+    taken from ``base`` (default: the scp's directory)."""
+    base = base or os.path.dirname(os.path.abspath(scp))
+    smap = read_state_map(states)
+    mlfd = read_mlf(mlf)
+    feats, labels = [], []
+    for l in open(scp):
+        p = l.strip()
+        if not p:
+            continue
+        path = p if os.path.isabs(p) else os.path.join(base, p)
+        n, period, _, _ = read_htk_header(path)
+        x = read_htk(path)
+        key = label_dir.rstrip("/") + "/" + os.path.splitext(os.path.basename(p))[0] + "." + label_ext
+        if key not in mlfd:
+            raise ValueError(f"Cannot open label MLF record: {key}")
+        feats.append(x)
+        labels.append(mlf_class_ids(mlfd[key], n, period, smap))
+    return Corpus(feats, labels)
+
+
 def write_mlf(path: str, utts: Sequence[str], labels: Sequence[np.ndarray], state_names: Sequence[str],
               samp_period: int = 100000) -> None:
     """One label segment per run of equal class ids; '*/<utt>.lab' patterns like examples/01."""

@@ -14,7 +14,7 @@ def test_library_built():
 
 
 def test_exports_every_header_symbol():
-    L = ctypes.CDLL(_lib.LIB_PATH)
+    L = _lib.lib()
     missing = [n for n in _lib.header_symbols() if not hasattr(L, n)]
     assert not missing, f"declared in include/*.h but not exported: {missing}"
 
@@ -30,6 +30,24 @@ def test_no_torch_or_oracle_dependency():
     out = subprocess.run(["ldd", _lib.LIB_PATH], capture_output=True, text=True).stdout
     assert "libtorch" not in out and "oracle" not in out
     assert "libamdhip64" in out and "librccl" in out
+
+
+@pytest.mark.parametrize("order", ["lib_then_torch", "torch_then_lib"])
+def test_one_hip_runtime_and_clean_exit(order):
+    """One HIP runtime and one RCCL per process whatever the import order (tnet_amd maps torch's
+    before the library), and the process exits cleanly (a second RCCL mapped before libtorch_hip
+    ended in 'double free or corruption' at exit)."""
+    import sys
+    steps = ["import tnet_amd; tnet_amd._lib.lib()", "import torch, torch.distributed"]
+    if order == "torch_then_lib":
+        steps.reverse()
+    code = ("import sys; sys.path.insert(0, %r); " % os.path.dirname(os.path.dirname(_lib.__file__)) +
+            "; ".join(steps) + "; from tnet_amd import _lib; rt = _lib.hip_runtimes_mapped(); "
+            "rc = sorted({l.split()[-1] for l in open('/proc/self/maps') if 'librccl' in l}); "
+            "print(len(rt), len(rc))")
+    p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-2000:]
+    assert p.stdout.split() == ["1", "1"], p.stdout
 
 
 def test_gfx950_code_object():

@@ -1,0 +1,320 @@
+"""The reference's own integration test, examples/01test_MLP3_compare_multithread_cuda_decode_phn,
+on its own data (tests/golden/ex01/: the 100 HTK FBANK utterances, test_3s.mlf, the 135-state map
+and the real lib/Hamm_dct_norm transform, copied as data).  Reference outputs come from the
+reference CPU TNet / TFeaCat / training_scheduler_xent.sh run in the build container
+(tests/golden/make_ex01.py -> ex01_epoch.json, ex01_feacat.npz, ex01_newbob.json).
+
+The reference's claim (README:1-5): CPU TNet 23.40 % vs CUDA TNetCu 23.41 % frame accuracy after one
+epoch of run_test.{CPU,GPU}.sh -- the same recipe on both, --GRAD-DIV-FRM=F on the GPU.  Here the
+init is seeded (formats.gen_mlp_init, the reference's generator is unseeded Python 2), so the
+absolute numbers differ from the README's; the equivalence is what is tested.
+
+Measured here (make_ex01.py "band"): on these files the recipe is chaotic at fp32 rounding level.
+The reference CPU TNet itself, rerun under 8 BLAS summation orders (MKL_CBWR x MKL_NUM_THREADS),
+reports Xent 186,957 .. 188,072 and accuracy 23.06 .. 23.52 % (bunch 960), and 189,808 .. 191,419 /
+23.01 .. 23.54 % (bunch 1024): an ulp of difference in the first bunch grows to ~0.5 % by the end of
+the epoch.  (SURVEY.md's 1e-5 MKL-threading band was measured on a different init; the README's
+23.40 / 23.41 % is one draw.)  So:
+
+Tolerances (written per test): the first 3 SGD steps on the real frames (before the divergence has
+grown) against the reference step by step -- outputs rtol 2e-4 / atol 2e-6, weight row sums and
+biases rtol 2e-5; one epoch: Xent and accuracy inside the reference's own band widened by half its
+width on each side;
+front-end outputs: checksums relative 1e-6 (fp32 DCT vs the reference's float sgemm), full
+utterances 2e-5 absolute; posteriors (--GMMBYPASS log-posteriors) 1e-4; the scheduler: the identical
+sequence of learning rates, accept / reject decisions and weight files, every iteration's err/frm
+inside the reference's own spread (widened by half its width, at least 1 % of its mean).
+"""
+import json
+import os
+import re
+import subprocess
+import tempfile
+
+import numpy as np
+import pytest
+
+import oracle as orc
+from tnet_amd import formats, newbob
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLD = os.path.join(REPO, "tests", "golden")
+EX = os.path.join(GOLD, "ex01")
+REPORT = re.compile(r"TR Xent:(\S+) frames:(\d+) err/frm:(\S+) correct\[(\S+)%\]")
+
+
+def _files():
+    return dict(scp=os.path.join(EX, "test.scp"), mlf=os.path.join(EX, "test_3s.mlf"),
+                states=os.path.join(EX, "mono_state_phn_set_135_phn"), transform=os.path.join(EX, "Hamm_dct_norm"))
+
+
+def _corpus():
+    f = _files()
+    return formats.read_corpus(f["scp"], f["mlf"], f["states"])
+
+
+def _epoch_cfg(name):
+    g = json.load(open(os.path.join(GOLD, "ex01_epoch.json")))
+    return g["init"], next(e for e in g["epochs"] if e["name"] == name)
+
+
+def _driver(name):
+    return os.path.join(REPO, "oracle", "_ref", f"{name}_amd")
+
+
+def _assert_in_band(cfg, xent, correct_pct):
+    """inside the reference's own summation-order band, widened by half its width on each side"""
+    xs = [b["xent"] for b in cfg["band"]]
+    cs = [b["correct_pct"] for b in cfg["band"]]
+    xr, cr = max(xs) - min(xs), max(cs) - min(cs)
+    print(f"{cfg['name']}: Xent {xent} (reference band {min(xs)} .. {max(xs)}), accuracy {correct_pct:.4f} % "
+          f"(band {min(cs)} .. {max(cs)})")
+    assert min(xs) - 0.5 * xr <= xent <= max(xs) + 0.5 * xr, (xent, min(xs), max(xs))
+    assert min(cs) - 0.5 * cr <= correct_pct <= max(cs) + 0.5 * cr, (correct_pct, min(cs), max(cs))
+
+
+# ------------------------------------------------------------------------- CPU: data + oracle
+
+def test_ex01_data_intake():
+    """FeatureRepository / LabelRepository semantics on the real files: 100 utterances, 55,457
+    frames, every frame labelled, 23-dim FBANK at 10 ms."""
+    c = _corpus()
+    assert len(c.feats) == 100 and c.frames == 55457
+    assert all(x.shape[1] == 23 for x in c.feats)
+    assert all(l.min() >= 0 and l.max() < 135 for l in c.labels)
+    n, period, size, kind = formats.read_htk_header(os.path.join(EX, "features", "001.fea"))
+    assert (period, size) == (100000, 92)
+
+
+def test_oracle_frontend_vs_reference_tfeacat():
+    """oracle.frontend_forward (our restatement of cuCRBEDctFeat.h) on the real Hamm_dct_norm vs the
+    reference CPU TFeaCat output on every utterance: pins the restatement on real data."""
+    c = _corpus()
+    L = formats.read_nnet(_files()["transform"])
+    g = np.load(os.path.join(GOLD, "ex01_feacat.npz"))
+    for k, x in enumerate(c.feats):
+        y = orc.frontend_forward(L, x, 25, 25).astype(np.float64)
+        assert y.shape[0] == int(g["transform_rows"][k])
+        if f"transform_Y_{k}" in g:
+            np.testing.assert_allclose(y, g[f"transform_Y_{k}"], rtol=0, atol=2e-5)
+        assert abs(y.sum() - g["transform_sum"][k]) <= 1e-6 * np.abs(y).sum()
+        assert abs((y ** 2).sum() - g["transform_sumsq"][k]) <= 1e-6 * g["transform_sumsq"][k]
+
+
+def test_newbob_decisions_replay_reference_log():
+    """tnet_amd.newbob.Newbob fed the reference scheduler's own TR / CV err/frm values takes the
+    script's decisions: the same learning-rate text each iteration, accept / reject, stop."""
+    g = json.load(open(os.path.join(GOLD, "ex01_newbob.json")))
+    assert g["restatement_matches_script"]
+    nb = newbob.Newbob(g["learnrate"], g["bunch"], threads=g["threads"], max_iter=g["max_iter"],
+                       end_halving_inc=g["end_halving_inc"])
+    nb.initial(g["initial_cv"])
+    for it in g["iterations"]:
+        assert nb.lrate == it["lrate"], it
+        acc = nb.decide(it["iter"], it["xent_train"], it["xent_cv"], "w")
+        assert acc == it["accepted"], it
+        if nb.done:
+            break
+    assert len(nb.history) == len(g["iterations"])
+    assert nb.done == (len(g["iterations"]) < g["max_iter"])
+
+
+def test_g5_is_bash_printf():
+    """file names use bash's printf %.5g (long double): 3.47165 -> 3.4717 (double would give 3.4716)"""
+    assert newbob._g5("3.47165") == "3.4717"
+    assert newbob._g5("2.01998") == "2.02"
+    assert newbob._g5("0.0005") == "0.0005"
+    assert newbob._g5("123456789") == "1.2346e+08"
+    assert newbob._g5("0.000012345") == "1.2345e-05"
+
+
+def test_parse_xent_is_the_scheduler_regex():
+    out = "junk\n-- TR Xent:188072 frames:54720 err/frm:3.43699 correct[23.2474%]\n" \
+          "-- CV Xent:1 frames:2 err/frm:0.5 correct[1%]\n"
+    assert newbob.parse_xent(out) == "0.5"
+    assert newbob.parse_xent("nothing") is None
+    assert newbob._awk_num(0.008 * 0.5) == "0.004" and newbob._awk_num(7.68 / 960) == "0.008"
+    assert newbob._awk_num(3.0) == "3"
+
+
+# ----------------------------------------------------------------------------- GPU parity
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not os.path.exists(_driver("TNetCu")), reason="oracle/_ref/TNetCu_amd not built")
+@pytest.mark.parametrize("name", ["run_test_cpu_b960", "config2_b1024"])
+def test_reference_tnetcu_run_test_gpu_recipe(name):
+    """run_test.GPU.sh:44-58 verbatim (reference TNetCu on this library, --GRAD-DIV-FRM=F) vs
+    run_test.CPU.sh:54-68 (reference CPU TNet, THREADS=1) on examples/01's own files."""
+    init_cfg, cfg = _epoch_cfg(name)
+    f = _files()
+    with tempfile.TemporaryDirectory() as td:
+        init = os.path.join(td, "test_mlp.init_weights")
+        formats.write_nnet(formats.gen_mlp_init(init_cfg["dims"], seed=init_cfg["seed"]), init, precision=6)
+        out = os.path.join(td, "test_mlp.epoch1-CUDA")
+        p = subprocess.run([_driver("TNetCu"), "-A", "-D", "-V", "-T", "021", "-H", init, "-I", f["mlf"], "-L", "*/",
+                            "-X", "lab", "-S", f["scp"], "-m", f["states"], "-n", repr(cfg["lr"]), "--GRAD-DIV-FRM=F",
+                            f"--TARGETMMF={out}", f"--BUNCHSIZE={cfg['bunch']}", f"--CACHESIZE={cfg['cache']}",
+                            "--RANDOMIZE=TRUE", f"--SEED={cfg['seed']}", f"--FEATURETRANSFORM={f['transform']}",
+                            f"--STARTFRMEXT={cfg['frm_ext']}", f"--ENDFRMEXT={cfg['frm_ext']}"],
+                           capture_output=True, text=True, cwd=EX, timeout=600)
+        assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-2000:]
+        m = REPORT.search(p.stdout)
+        assert m, p.stdout[-2000:]
+        assert int(m.group(2)) == cfg["frames"]
+        _assert_in_band(cfg, float(m.group(1)), float(m.group(4)))
+        assert [L.tag for L in formats.read_nnet(out)] == ["<biasedlinearity>", "<sigmoid>", "<biasedlinearity>",
+                                                          "<softmax>"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["run_test_cpu_b960", "config2_b1024"])
+def test_native_trainer_on_ex01(name):
+    """The library's own TNetCu loop (tnet_trainer_*, transform on the GPU via
+    tnet_trainer_set_transform) fed by formats.read_corpus: the same Report as the reference CPU
+    TNet on examples/01."""
+    import tnet_amd
+    init_cfg, cfg = _epoch_cfg(name)
+    c = _corpus()
+    transform = tnet_amd.Network(path=_files()["transform"])
+    net = tnet_amd.Network.from_layers(formats.round_trip_text(
+        formats.gen_mlp_init(init_cfg["dims"], seed=init_cfg["seed"]), 6))
+    net.set_learn_rate(cfg["lr"])
+    net.set_grad_div_frm(False)
+    obj = tnet_amd.Objective()
+    tr = tnet_amd.Trainer(net, obj, bunchsize=cfg["bunch"], cachesize=cfg["cache"], seed=cfg["seed"])
+    tr.set_transform(transform, cfg["frm_ext"], cfg["frm_ext"])
+    tr.train_corpus(c.feats, c.labels)
+    err, frames, correct = obj.stats()
+    assert frames == cfg["frames"]
+    _assert_in_band(cfg, err, 100.0 * correct / frames)
+
+
+@pytest.mark.gpu
+def test_first_steps_on_real_frames_match_reference():
+    """run_test.CPU.sh's first 3 bunches (examples/01 frames through Hamm_dct_norm, the reference's
+    cache order) through the fused TrainBunch with GRADDIVFRM=F vs oracle/_ref/ref_harness (the
+    reference TNetLib step, THREADS=1): outputs per step, then the weights (row sums / squares) and
+    biases.  Exact parity on real data before the epoch's chaos grows."""
+    import importlib.util
+    import tnet_amd
+    spec = importlib.util.spec_from_file_location("make_ex01", os.path.join(GOLD, "make_ex01.py"))
+    mk = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mk)
+    init_cfg, cfg = _epoch_cfg(mk.STEPS["epoch"])
+    n = mk.STEPS["nsteps"]
+    X, lab = mk.step_inputs(cfg, n)
+    g = np.load(os.path.join(GOLD, "ex01_steps.npz"))
+    net = tnet_amd.Network.from_layers(formats.round_trip_text(
+        formats.gen_mlp_init(init_cfg["dims"], seed=init_cfg["seed"]), 6))
+    net.set_learn_rate(cfg["lr"])
+    net.set_grad_div_frm(False)
+    net.keep_output(True)
+    obj = tnet_amd.Objective()
+    B = cfg["bunch"]
+    for s_ in range(n):
+        net.train_bunch(obj, tnet_amd.DeviceArray.from_numpy(X[s_ * B:(s_ + 1) * B]),
+                        tnet_amd.DeviceArray.vector(lab[s_ * B:(s_ + 1) * B].astype(np.int32)))
+        np.testing.assert_allclose(net.output(3, B), g[f"Y_{s_}"], rtol=2e-4, atol=2e-6, err_msg=f"step {s_}")
+    for k, (W, b) in enumerate(net.linear_params()):
+        W = W.astype(np.float64)
+        np.testing.assert_allclose(W.sum(1), g[f"W{k}_rowsum"], rtol=2e-5, atol=2e-5)
+        np.testing.assert_allclose((W ** 2).sum(1), g[f"W{k}_rowsq"], rtol=2e-5)
+        np.testing.assert_allclose(b, g[f"b{k}"], rtol=2e-5, atol=2e-6)
+    err, frames, _ = obj.stats()
+    assert frames == int(g["frames"])
+    np.testing.assert_allclose(err, float(g["xent_sum"]), rtol=1e-5)
+
+
+@pytest.mark.gpu
+def test_gpu_transform_vs_reference_tfeacat():
+    """The Hamm_dct_norm network on the GPU (CuExpand .. CuWindow) vs the reference TFeaCat output."""
+    import tnet_amd
+    c = _corpus()
+    net = tnet_amd.Network(path=_files()["transform"])
+    g = np.load(os.path.join(GOLD, "ex01_feacat.npz"))
+    for k, x in enumerate(c.feats):
+        xe = formats.extend_frames(x, 25, 25)
+        y = net.propagate(tnet_amd.DeviceArray.from_numpy(xe)).numpy()[25:-25].astype(np.float64)
+        assert y.shape[0] == int(g["transform_rows"][k])
+        if f"transform_Y_{k}" in g:
+            np.testing.assert_allclose(y, g[f"transform_Y_{k}"], rtol=0, atol=2e-5)
+        assert abs(y.sum() - g["transform_sum"][k]) <= 1e-6 * np.abs(y).sum()
+        assert abs((y ** 2).sum() - g["transform_sumsq"][k]) <= 1e-6 * g["transform_sumsq"][k]
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not os.path.exists(_driver("TFeaCatCu")), reason="oracle/_ref/TFeaCatCu_amd not built")
+def test_reference_tfeacatcu_decode_recipe():
+    """decode.sh:41-49 (TFeaCatCu --FEATURETRANSFORM --GMMBYPASS=true, ext 25) on this library vs
+    the reference CPU TFeaCat, every utterance of examples/01."""
+    init_cfg, _ = _epoch_cfg("run_test_cpu_b960")
+    f = _files()
+    g = np.load(os.path.join(GOLD, "ex01_feacat.npz"))
+    with tempfile.TemporaryDirectory() as td:
+        init = os.path.join(td, "mlp.nnet")
+        formats.write_nnet(formats.gen_mlp_init(init_cfg["dims"], seed=init_cfg["seed"]), init, precision=6)
+        outdir = os.path.join(td, "posteriors")
+        os.makedirs(outdir)
+        p = subprocess.run([_driver("TFeaCatCu"), "-D", "-A", "-T", "1", "-S", f["scp"], "-H", init, "-l", outdir,
+                            "-y", "fea", f"--FEATURETRANSFORM={f['transform']}", "--GMMBYPASS=true",
+                            "--START-FRM-EXT=25", "--END-FRM-EXT=25"], capture_output=True, text=True, cwd=EX,
+                           timeout=600)
+        assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-2000:]
+        names = [os.path.splitext(os.path.basename(l.strip()))[0] for l in open(f["scp"]) if l.strip()]
+        for k, n in enumerate(names):
+            y = formats.read_htk(os.path.join(outdir, n + ".fea")).astype(np.float64)
+            assert y.shape[0] == int(g["gmmbypass_rows"][k])
+            if f"gmmbypass_Y_{k}" in g:
+                np.testing.assert_allclose(y, g[f"gmmbypass_Y_{k}"], rtol=1e-4, atol=1e-4)
+            assert abs(y.sum() - g["gmmbypass_sum"][k]) <= 1e-4 * np.abs(y).sum()
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not os.path.exists(_driver("TNetCu")), reason="oracle/_ref/TNetCu_amd not built")
+def test_newbob_scheduler_over_tnetcu_matches_reference():
+    """training_scheduler_xent.sh's protocol (tnet_amd.newbob) over the reference TNetCu driver on
+    this library (CUDA mode: no THREADS, GRADDIVFRM=T, LEARNRATE per bunch) vs the reference script
+    over the CPU TNet (THREADS=1: rate / BUNCHSIZE, gradient sums): the learning-rate sequence,
+    accept / reject, the stopping iteration and the weight files exactly; initial CV and per-iteration
+    TR / CV err/frm (the 6-digit model text round trip between epochs included) inside the
+    reference's own spread over BLAS summation orders."""
+    g = json.load(open(os.path.join(GOLD, "ex01_newbob.json")))
+    f = _files()
+    lines = [l for l in open(f["scp"]) if l.strip()]
+    with tempfile.TemporaryDirectory() as td:
+        tr, cv = os.path.join(td, "train.scp"), os.path.join(td, "cv.scp")
+        open(tr, "w").writelines(os.path.join(EX, l.strip()) + "\n" for l in lines[:g["n_train"]])
+        open(cv, "w").writelines(os.path.join(EX, l.strip()) + "\n" for l in lines[g["n_train"]:])
+        init = os.path.join(td, "mlp.init")
+        formats.write_nnet(formats.gen_mlp_init(g["init"]["dims"], seed=g["init"]["seed"]), init, precision=6)
+        conf = os.path.join(td, "tnet.conf")          # the data order: SEED through an STK config (-C)
+        open(conf, "w").write(f"SEED = {g['seed']}\n")
+        nb = newbob.run([_driver("TNetCu")], init, f["mlf"], f["mlf"], tr, cv, f["states"], g["learnrate"], td,
+                        bunchsize=g["bunch"], cachesize=g["cache"], frm_ext=g["frm_ext"],
+                        feature_transform=f["transform"], max_iter=g["max_iter"],
+                        end_halving_inc=g["end_halving_inc"], config=conf)
+        final = sorted(os.listdir(os.path.join(td, "weights")))
+    # the reference's own per-iteration spread: the script's run + the same schedule under 3 other
+    # BLAS summation orders (make_ex01.py); a value passes inside that spread widened by half its
+    # width or by 1 % of its mean, whichever is larger (iteration 1's CV spreads 3.30 .. 3.62 there)
+    runs = [dict(initial_cv=g["initial_cv"], iterations=g["iterations"])] + g["band"]
+
+    def inside(v, vals, what):
+        vals = [float(x) for x in vals]
+        lo, hi = min(vals), max(vals)
+        m = max(0.5 * (hi - lo), 0.01 * sum(vals) / len(vals))
+        print(f"{what}: {v} (reference {lo} .. {hi})")
+        assert lo - m <= float(v) <= hi + m, (what, v, lo, hi)
+
+    inside(nb.initial_cv, [r["initial_cv"] for r in runs], "initial CV")
+    assert len(nb.history) == len(g["iterations"])
+    for k, (h, r) in enumerate(zip(nb.history, g["iterations"])):
+        # CUDA mode passes the per-bunch rate; the CPU script passes rate / BUNCHSIZE
+        assert abs(float(h.lrate) / g["bunch"] - float(r["lrate"])) <= 1e-6 * float(r["lrate"]), (h, r)
+        assert h.accepted == r["accepted"] and all(b["iterations"][k]["accepted"] == r["accepted"] for b in g["band"])
+        inside(h.xent_train, [x["iterations"][k]["xent_train"] for x in runs], f"iter {h.iter} TR")
+        inside(h.xent_cv, [x["iterations"][k]["xent_cv"] for x in runs], f"iter {h.iter} CV")
+    # the scheduler's file protocol: same iteration files (names carry lr / tr / cv at 5 digits: the
+    # last digit may differ within the tolerance above) and the final copy
+    assert len(final) == len(g["weights"])
+    assert [w.split("_lr")[0] for w in final] == [w.split("_lr")[0] for w in g["weights"]]

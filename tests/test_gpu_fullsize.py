@@ -1,0 +1,147 @@
+"""Every BASELINE.json config at its FULL size on the GPU against the oracle (oracle/tnet_oracle.c,
+fp64-accumulated restatement of the reference arithmetic; its MLP step is pinned by the reference CPU
+TNet fixtures, tests/test_oracle_golden.py):
+
+  config 2/3/metric  440->2048x4->4000 and 440->2048x5->4000 sigmoid MLP, bunch 1024, GRADDIVFRM=T,
+                     two SGD steps of the fused TrainBunch path (the bench's step) -- TNetCu.cc:427-441
+  config 4           Gauss-Bernoulli RBM 440->2048, bunch 256, CD-1 with momentum + weight cost, a few
+                     TRbmCu steps (TRbmCu.cc:326-354) -- parity restated (CUDA-only reference)
+  config 5           Elman RNN 440->512 (BPTT 4)->135 and ->4000 over 1000-frame utterances, per-frame
+                     SGD (TRecurrentCu.cc:319-375), with the hipGraph replay of the frame chain engaged
+                     -- parity restated
+
+Tolerances (and why):
+  MLP outputs per step: rtol 2e-4, atol 2e-6 (fp32 MFMA accumulation over K = 2048 / 4000 vs fp64).
+  MLP parameters: |W_gpu - W_ref| <= 2 ulp(W) + 1e-4 max|W_ref - W_init| per layer (and the same for
+  the biases).  The update, not W, is the quantity under test (comparing W alone would hide an update
+  error behind the 0.1-scale weights); both sides store W in fp32, so two ulps of W are the floor
+  under which the two roundings of the same update cannot agree -- for the first layer, whose update
+  is ~1e-5 of W (saturated sigmoids, 1/1024 frame division), that floor is most of the update.
+  RBM: hidden states are Bernoulli samples (p > u): a p within an ulp of its uniform can flip between
+  fp32 orders of summation, and a flipped unit moves one row of the statistics by lr/B * v.  So: at
+  most 1e-4 of the weights outside rtol 2e-4 / atol 2e-6, every weight within that flip bound, MSE
+  rtol 1e-3.
+  RNN (1000 frames of per-frame SGD, weights updated every frame, fp32 GEMV order vs fp64): Xent rtol
+  1e-4, correct frames within 0.1 %, parameters' change from init in relative Frobenius norm <= 1e-4
+  (measured on MI355X over 3000 frames: 0.6-2.3e-6 -- no drift builds up; round 2's rtol 2e-3 was set
+  on 60-frame toys).
+"""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+import oracle as orc  # noqa: E402
+from tnet_amd import DeviceArray, Network, Objective, RbmTrainer, RnnTrainer, formats  # noqa: E402
+
+
+def _assert_update_close(after_gpu, after_ref, before, rtol, what):
+    ref = np.asarray(after_ref, np.float32)
+    upd = np.abs(ref.astype(np.float64) - before)
+    tol = 2.0 * np.spacing(np.abs(ref)).astype(np.float64) + rtol * upd.max()
+    err = np.abs(np.asarray(after_gpu, np.float64) - ref)
+    worst = float((err / tol).max())
+    print(f"{what}: max|update| {upd.max():.3e}, max err {err.max():.3e}, worst err/tol {worst:.3f}")
+    assert worst <= 1.0, (what, worst)
+
+
+def _rel_update_err(after_gpu, after_ref, before):
+    d_ref = after_ref.astype(np.float64) - before
+    d_gpu = after_gpu.astype(np.float64) - before
+    return np.linalg.norm(d_gpu - d_ref) / max(np.linalg.norm(d_ref), 1e-30)
+
+
+@pytest.mark.parametrize("name,dims", [("metric_dnn4", [440, 2048, 2048, 2048, 2048, 4000]),
+                                       ("config3_dnn5", [440, 2048, 2048, 2048, 2048, 2048, 4000])])
+def test_dnn_two_steps_full_size(name, dims):
+    B, lr = 1024, 1.0
+    layers = formats.gen_mlp_init(dims, seed=2)
+    net = Network.from_layers(layers)
+    net.set_learn_rate(lr)
+    net.set_grad_div_frm(True)
+    net.keep_output(True)
+    obj = Objective()
+    ref = orc.MLP.from_layers(layers)
+    W0 = [w.astype(np.float64) for w in ref.W]
+    b0 = [b.astype(np.float64) for b in ref.b]
+    rng = np.random.default_rng(7)
+    for s in range(2):
+        X = rng.standard_normal((B, dims[0])).astype(np.float32)
+        L = rng.integers(0, dims[-1], B).astype(np.int32)
+        net.train_bunch(obj, DeviceArray.from_numpy(X), DeviceArray.vector(L))
+        Y = net.output(2 * (len(dims) - 1) - 1, B)
+        Yr, _ = ref.step(X, L, lr)
+        np.testing.assert_allclose(Y, Yr, rtol=2e-4, atol=2e-6, err_msg=f"step {s} output")
+    for k, (W, b) in enumerate(net.linear_params()):
+        _assert_update_close(W, ref.W[k], W0[k], 1e-4, f"{name} layer {k} W")
+        _assert_update_close(b, ref.b[k], b0[k], 1e-4, f"{name} layer {k} b")
+    err, frames, correct = obj.stats()
+    assert frames == 2 * B
+    np.testing.assert_allclose(err, ref.xent, rtol=1e-5)
+    assert abs(correct - ref.correct) <= 1
+
+
+def test_rbm_cd1_full_size():
+    """TRbmCu defaults (lr 0.1, momentum 0.5, weight cost 2e-4, TRbmCu.cc:169-171) at 440->2048,
+    bunch 256: 4 CD-1 steps of the native RbmTrainer (cache fill, lrand48 shuffle after the CuRand
+    seeds, fused sampling GEMM, stacked update) vs orc_rbm_step on the same schedule."""
+    V, H, B, cache, seed = 440, 2048, 256, 1024, 17
+    lr, mmt, wc = 0.1, 0.5, 0.0002
+    rng = np.random.default_rng(3)
+    feats = [rng.standard_normal((n, V)).astype(np.float32) for n in (300, 500, 224)]   # 1024 frames
+    layer = formats.round_trip_text(formats.gen_rbm_init(V, H, seed=4), 9)[0]
+    net = Network.from_layers([layer])
+    tr = RbmTrainer(net, bunchsize=B, cachesize=cache, seed=seed, learn_rate=lr, momentum=mmt, weightcost=wc)
+    tr.train_corpus(feats)
+    rs = orc.RandState(seed, B, H)
+    X = np.concatenate(feats)
+    sched = orc.epoch_schedule_x([len(f) for f in feats], cache, B, rs.x_after)
+    m = orc.RBM.from_layer(layer)
+    for b in sched:
+        m.step(X[b], rs, lr, mmt, wc)
+    assert tr.steps == len(sched) == 4
+    mse, frames = tr.stats()
+    assert frames == m.frames == 1024
+    np.testing.assert_allclose(mse, m.mse, rtol=1e-3)
+    W, vb, hb, _ = net.rbm_params(0)
+    bad = ~np.isclose(W, m.W, rtol=2e-4, atol=2e-6)
+    assert bad.mean() <= 1e-4, f"{bad.sum()} weights off"
+    flip = 4 * lr / B * float(np.abs(X).max()) * 2.0
+    assert np.abs(W - m.W).max() <= flip
+    np.testing.assert_allclose(vb, m.vb, rtol=2e-4, atol=flip)
+    np.testing.assert_allclose(hb, m.hb, rtol=2e-4, atol=flip)
+
+
+@pytest.mark.parametrize("S", [135, 4000])
+def test_rnn_1000_frame_utterances_full_size(S, monkeypatch):
+    """TRecurrentCu's 440->512 Elman RNN (BPTT 4) over three 1000-frame utterances: the first runs
+    the frame chain eagerly, the second records it as a hipGraph and runs it, the third replays the
+    recorded graph (curecurrent.cpp RunFrames) -- all against orc_rnn_utterance."""
+    monkeypatch.delenv("TNET_RNN_GRAPH", raising=False)
+    monkeypatch.delenv("TNET_RNN_PERSIST", raising=False)
+    nIn, H, bptt, lr, T = 440, 512, 4, 0.02, 1000
+    rng = np.random.default_rng(S)
+    layers = formats.round_trip_text(formats.gen_recurrent_init(nIn, H, S, seed=11), 9)
+    feats = [rng.standard_normal((T, nIn)).astype(np.float32) for _ in range(3)]
+    labels = [rng.integers(0, S, T).astype(np.int32) for _ in range(3)]
+    net = Network.from_layers(layers)
+    net.set_learn_rate(lr)
+    obj = Objective()
+    tr = RnnTrainer(net, obj, bptt=bptt)
+    tr.train_corpus(feats, labels)
+    m = orc.RNN(layers[0].W, layers[0].b, layers[1].W, layers[1].b)
+    for f, l in zip(feats, labels):
+        m.utterance(f, l, bptt, lr)
+    err, frames, correct = obj.stats()
+    assert frames == m.frames == 3 * T
+    np.testing.assert_allclose(err, m.xent, rtol=1e-4)
+    assert abs(correct - m.correct) <= 0.001 * frames
+    Wr, br = net.recurrent_params(0)
+    W2, b2 = net.linear_params()[0]
+    for got, want, init, what in ((Wr, m.Wr, layers[0].W, "Wr"), (br, m.br, layers[0].b, "br"),
+                                  (W2, m.W2, layers[1].W, "W2"), (b2, m.b2, layers[1].b, "b2")):
+        e = _rel_update_err(got, want, init.astype(np.float64))
+        print(f"S={S} {what}: relative update error {e:.3e}")
+        assert e <= 1e-4, (what, e)
