@@ -102,6 +102,16 @@ def param_checksum(net):
     return h.hexdigest()[:16], repr(tot)
 
 
+def roofline_shape(dims):
+    """the dominant kernel's layer shape: the 2048x2048 hidden layers of the metric / dnn5 networks, else
+    the layer with the most weights (MLP3: the 598x1024 input layer)"""
+    shapes = [(dims[i], dims[i + 1]) for i in range(len(dims) - 1)]
+    if (2048, 2048) in shapes:
+        return ":2048x2048"
+    ni, no = max(shapes, key=lambda s: s[0] * s[1])
+    return f":{ni}x{no}"
+
+
 def parse_kernel_report(text):
     out = {}
     for line in text.strip().splitlines():
@@ -222,8 +232,9 @@ def main():
     # back-to-back roofline kernels (each pair adds ~3 us of stream time, so not inside the value region)
     buf = ctypes.create_string_buffer(1 << 16)
     kern = {}
+    roof_shape = roofline_shape(dims)
     if args.kernel_timing:
-        check(lib().tnet_kernel_timing_filter(b":2048x2048"), "timing_filter")
+        check(lib().tnet_kernel_timing_filter(roof_shape.encode()), "timing_filter")
         check(lib().tnet_kernel_timing(2 if args.kernel_timing == 1 else 1), "kernel_timing")
         trainer.replay(args.steps)
         check(lib().tnet_kernel_timing(0), "kernel_timing")
@@ -257,7 +268,7 @@ def main():
     ms_per_step = 1000.0 * dt / args.steps
 
     # ---- roofline of the dominant kernel: the 2048x2048 affine-layer GEMMs (fwd + bwd + fused update)
-    hid = [v for k, v in kern.items() if k.startswith("gemm_") and k.endswith(":2048x2048")]
+    hid = [v for k, v in kern.items() if k.startswith("gemm_") and k.endswith(roof_shape)]
     roof = None
     if hid:
         # run mode: exact totals of the event-bracketed runs (every launch in a run is a roofline GEMM)
@@ -265,12 +276,15 @@ def main():
                                     "work": sum(v["work"] for v in hid)}
         launches, ms, flops = tot["launches"], tot["ms"], tot["work"]
         achieved = flops / (ms * 1e-3) / 1e12
-        traffic, traffic_src = pmc_traffic()
-        roof = {"bound": "mfma", "kernel": "gemm_f32 2048x2048 (fwd/bwd/update; a paired update + backward launch counts as its two GEMMs)", "achieved": round(achieved, 2),
+        traffic, traffic_src = pmc_traffic() if roof_shape == ":2048x2048" else (None, None)
+        ni, no = (int(v) for v in roof_shape[1:].split("x"))
+        roof = {"bound": "mfma", "kernel": f"gemm_f32 {roof_shape[1:]} (fwd/bwd/update; a paired update + backward "
+                                           "launch counts as its two GEMMs)", "achieved": round(achieved, 2),
                 "peak": PEAK_FP32_MFMA, "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_MFMA, 4),
                 "traffic": traffic, "traffic_unit": "bytes/launch", "traffic_source": traffic_src,
-                "algorithmic_bytes_per_launch": 4.0 * ((2 * B * 2048 + 2048 ** 2) + (3 * B * 2048 + 2048 ** 2) +
-                                                       (2 * B * 2048 + 2 * 2048 ** 2)) / 3,  # fwd, bwd, upd
+                # fwd: X, Y, W; bwd: E, W, y below, E below; upd: X, E, W read + write
+                "algorithmic_bytes_per_launch": 4.0 * ((B * ni + B * no + ni * no) + (B * no + 2 * B * ni + ni * no) +
+                                                       (B * ni + B * no + 2 * ni * no)) / 3,
                 "launches": launches, "avg_launch_us": round(1000.0 * ms / launches, 2),
                 "timing": (f"hipEvent pairs on the library stream around each run of back-to-back roofline launches "
                            f"({kern['@runs']['runs']} runs), {args.steps} steps right after the value region"
@@ -311,6 +325,8 @@ def main():
                                                       if world > 1 or args.force_dp else ""),
                        "flops_per_frame": flops_per_frame(dims),
                        "achieved_tflops_whole_step": round(value * flops_per_frame(dims) / 1e12 / world, 2),
+                       "whole_step_frac_of_fp32_peak": round(value * flops_per_frame(dims) / 1e12 / world /
+                                                             PEAK_FP32_MFMA, 4),
                        "gemm_share_of_kernel_time": round(all_gemm_ms / all_ms, 4) if all_ms else None},
             "roofline": roof,
             "cpu_baseline": cpu,

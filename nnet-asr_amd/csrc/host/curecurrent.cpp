@@ -1,6 +1,7 @@
 // curecurrent.cpp -- see curecurrent.h.
 #include "curecurrent.h"
 
+#include <algorithm>
 #include <cstdlib>
 #include <cstring>
 
@@ -140,8 +141,12 @@ CuRecurrentTrainer::~CuRecurrentTrainer() {
   if (mArgKey) (void)hipFree(mArgKey);
   if (mXbuf) (void)hipFree(mXbuf);
   if (mErrFlag) (void)hipFree(mErrFlag);
-  for (auto& kv : mGraphs)
-    if (kv.second.exec) (void)hipGraphExecDestroy(kv.second.exec);
+  for (auto& kv : mGraphs) DestroyExecs(kv.second);
+}
+
+void CuRecurrentTrainer::DestroyExecs(ChainGraph& g) {
+  for (auto e : g.execs) (void)hipGraphExecDestroy(e);
+  g.execs.clear();
 }
 
 void* CuRecurrentTrainer::Scratch(void*& p, size_t& have, size_t bytes) {
@@ -198,10 +203,6 @@ void CuRecurrentTrainer::TrainUtterance(const float* feats, size_t rows, size_t 
 bool CuRecurrentTrainer::GraphsEnabled() const {
   const char* e = getenv("TNET_RNN_GRAPH");
   if (e && e[0] == '0') return false;
-  // under a rocprofiler-sdk tool (rocprofv3 sets ROCP_TOOL_LIBRARIES) the recorded chain crashed inside
-  // the runtime (rocprofv3 --kernel-trace, this image's ROCm 7.2): profile the eager chain instead,
-  // unless TNET_RNN_GRAPH=1 asks for the graphs explicitly (the diagnosis runs)
-  if (getenv("ROCP_TOOL_LIBRARIES") && !(e && e[0] == '1')) return false;
   CuDevice& dev = CuDevice::Instantiate();
   // event records do not belong in a recorded chain; the legacy null stream cannot be captured
   return !dev.KernelTiming() && !dev.Profile() && dev.Stream() != nullptr;
@@ -235,14 +236,14 @@ std::vector<uint64_t> CuRecurrentTrainer::ChainKey(size_t rows) {
 // advance (ring head, frame count) is set as the recorded run left it.
 void CuRecurrentTrainer::RunFrames(size_t rows) {
   const size_t cols = mFeats.Cols();
-  auto eager = [&]() {
-    for (size_t f = 0; f < rows; f++) {
+  auto eager = [&](size_t f0, size_t f1) {
+    for (size_t f = f0; f < f1; f++) {
       CuMatrix<BaseFloat>::MakeView(mRow, mFeats.pCURowData(f), 1, cols, mFeats.Stride());
       TrainFrameFused(f);
     }
   };
   if (!GraphsEnabled()) {
-    eager();
+    eager(0, rows);
     return;
   }
   auto& rec = dynamic_cast<CuRecurrent&>(mNet->Layer(0));
@@ -251,43 +252,57 @@ void CuRecurrentTrainer::RunFrames(size_t rows) {
   auto it = mGraphs.find(rows);
   if (it == mGraphs.end()) {
     if (mGraphs.size() >= 64) {  // bounded: lengths beyond the first 64 distinct ones run eagerly
-      eager();
+      eager(0, rows);
       return;
     }
     it = mGraphs.emplace(rows, ChainGraph()).first;
   }
   ChainGraph& g = it->second;
-  if (g.exec && g.key == key) {
-    TNET_HIP_CALL(hipGraphLaunch(g.exec, st));
+  if (!g.execs.empty() && g.key == key) {
+    for (auto e : g.execs) TNET_HIP_CALL(hipGraphLaunch(e, st));
     rec.SetHead(g.head_after);
     mObj->AddFrames(rows);
     return;
   }
   if (g.key != key) {
-    if (g.exec) TNET_HIP_CALL(hipGraphExecDestroy(g.exec));
-    g.exec = nullptr;
+    DestroyExecs(g);
     g.key = key;
     g.seen = 0;
   }
   if (++g.seen < 2) {  // first sighting: every buffer the chain touches gets allocated eagerly
-    eager();
+    eager(0, rows);
     return;
   }
-  hipGraph_t graph = nullptr;
-  TNET_HIP_CALL(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
-  try {
-    eager();  // recorded, not run; the host state (head, frames) advances as in an eager run
-  } catch (...) {
-    (void)hipStreamEndCapture(st, &graph);
-    if (graph) (void)hipGraphDestroy(graph);
-    throw;
+  static const size_t seg = [] {
+    const char* e = getenv("TNET_RNN_GRAPH_FRAMES");
+    const long v = e ? atol(e) : 96;
+    return (size_t)(v > 0 ? v : 96);
+  }();
+  // record segment by segment, each launched right after its recording: the host state the frames
+  // advance (ring head, frame count) moves exactly as in an eager run
+  for (size_t f0 = 0; f0 < rows; f0 += seg) {
+    const size_t f1 = std::min(rows, f0 + seg);
+    hipGraph_t graph = nullptr;
+    TNET_HIP_CALL(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
+    try {
+      eager(f0, f1);  // recorded, not run
+    } catch (...) {
+      (void)hipStreamEndCapture(st, &graph);
+      if (graph) (void)hipGraphDestroy(graph);
+      DestroyExecs(g);
+      g.seen = 0;
+      throw;
+    }
+    TNET_HIP_CALL(hipStreamEndCapture(st, &graph));
+    hipGraphExec_t exec = nullptr;
+    const hipError_t e = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(graph);
+    if (e != hipSuccess) DestroyExecs(g);
+    TNET_HIP_CALL(e);
+    g.execs.push_back(exec);
+    TNET_HIP_CALL(hipGraphLaunch(exec, st));
   }
-  TNET_HIP_CALL(hipStreamEndCapture(st, &graph));
-  const hipError_t e = hipGraphInstantiate(&g.exec, graph, nullptr, nullptr, 0);
-  (void)hipGraphDestroy(graph);
-  TNET_HIP_CALL(e);
   g.head_after = rec.Head();
-  TNET_HIP_CALL(hipGraphLaunch(g.exec, st));
 }
 
 // TRecurrentCu.cc:346-371 for one utterance in one launch: the frames' forward, cross-entropy,

@@ -109,15 +109,19 @@ class CuRecurrentTrainer {
   size_t mXbufBytes = 0;
   int* mErrFlag = nullptr;
   unsigned mEpoch = 0;
-  // the utterance's fused frame chain recorded as a hipGraph and replayed (TNET_RNN_GRAPH=0: off):
+  // the utterance's fused frame chain recorded as hipGraphs and replayed (TNET_RNN_GRAPH=0: off):
   // one entry per utterance length; a key is recorded the second time it is seen (a length seen once
-  // runs eagerly) and replayed from the third on
+  // runs eagerly) and replayed from the third on.  The chain is cut into segments of at most
+  // TNET_RNN_GRAPH_FRAMES frames (default 96, ~870 kernel nodes): rocprofiler-sdk (ROCm 7.2) faults
+  // inside hipGraphLaunch on graphs of a few thousand kernel nodes (tools/graph_probe.hip: 1000 nodes
+  // fine, 3000 SIGSEGV, profiles/r03_graph_probe_rocprof.txt), and a segment launch costs ~2 us
   struct ChainGraph {
     std::vector<uint64_t> key;
     int seen = 0;
-    hipGraphExec_t exec = nullptr;
+    std::vector<hipGraphExec_t> execs;
     int head_after = 0;
   };
+  void DestroyExecs(ChainGraph& g);
   std::map<size_t, ChainGraph> mGraphs;
   std::vector<uint64_t> ChainKey(size_t rows);
   bool GraphsEnabled() const;

@@ -33,9 +33,14 @@ __device__ __forceinline__ float wave_max(float v) {
 // sigmoid the largest part of the fused forward GEMM's epilogue.  Error <= ~3e-7 absolute for
 // |x| <= 16 (the scaled exponent's rounding, damped by sigma(1-sigma) <= 1/4), well inside the
 // kernel tests' 2e-6; exp overflow / underflow give exactly 0 / 1.
+#ifdef TNET_PRECISE_TRANSCENDENTALS
+// diagnostics build (make precise): the reference's double-precision formula, and libm-accurate exp
+__device__ __forceinline__ float sigmoidf_ref(float x) { return (float)(1.0 / (1.0 + exp(-(double)x))); }
+#else
 __device__ __forceinline__ float sigmoidf_ref(float x) {
   return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-1.44269504088896341f * x));
 }
+#endif
 
 // Write-through (sc1) 16-B output stores through a buffer descriptor of the workgroup's output tile (or row).  A
 // plain store leaves its line dirty in the XCD's L2 and the kernel-end release writes every dirty line
@@ -71,7 +76,11 @@ __device__ __forceinline__ ArgMax wave_argmax(ArgMax a) {
 
 // exp(x) for x <= 0 on v_exp_f32: exp2(x*log2 e); relative error ~|x|*6e-8 (the rounding of the
 // scaled argument), i.e. <= 1e-6 over the 16 nats that carry any probability mass
+#ifdef TNET_PRECISE_TRANSCENDENTALS
+__device__ __forceinline__ float fast_exp(float x) { return (float)exp((double)x); }
+#else
 __device__ __forceinline__ float fast_exp(float x) { return __builtin_amdgcn_exp2f(1.44269504088896341f * x); }
+#endif
 
 inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }
 

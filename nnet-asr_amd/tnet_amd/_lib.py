@@ -15,6 +15,8 @@ LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "libtnet_amd.so")
 if os.environ.get("TNET_DIAG_STAMP_LIB"):  # diagnostics only (tools/gemm_clock.py): clock-stamped GEMM build
     _v = os.environ["TNET_DIAG_STAMP_LIB"]
     LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "libtnet_amd_stamp" + ("" if _v == "1" else "_" + _v) + ".so")
+if os.environ.get("TNET_LIB_VARIANT"):  # diagnostics only: e.g. "precise" (make -C nnet-asr_amd precise)
+    LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "libtnet_amd_" + os.environ["TNET_LIB_VARIANT"] + ".so")
 INCLUDE_DIR = os.path.join(os.path.dirname(os.path.dirname(_HERE)), "include")
 
 _lib = None

@@ -23,7 +23,8 @@ width on each side;
 front-end outputs: checksums relative 1e-6 (fp32 DCT vs the reference's float sgemm), full
 utterances 2e-5 absolute; posteriors (--GMMBYPASS log-posteriors) 1e-4; the scheduler: the identical
 sequence of learning rates, accept / reject decisions and weight files, every iteration's err/frm
-inside the reference's own spread (widened by half its width, at least 1 % of its mean).
+inside the reference's own spread (widened by half its width, at least 1.5 % of its mean: the
+recipe's measured rounding chaos, profiles/r03_ex01_chaos.txt).
 """
 import json
 import os
@@ -296,13 +297,18 @@ def test_newbob_scheduler_over_tnetcu_matches_reference():
         final = sorted(os.listdir(os.path.join(td, "weights")))
     # the reference's own per-iteration spread: the script's run + the same schedule under 3 other
     # BLAS summation orders (make_ex01.py); a value passes inside that spread widened by half its
-    # width or by 1 % of its mean, whichever is larger (iteration 1's CV spreads 3.30 .. 3.62 there)
+    # width or by 1.5 % of its mean, whichever is larger.  Why 1.5 %: the recipe is chaotic at the
+    # rounding level (profiles/r03_ex01_chaos.txt: two oracle runs differing only in the rounding of
+    # the update, and the GPU against the oracle, separate from ~1e-6 at step 0 at the same
+    # exponential rate to ~10-20 % of the weight change after one epoch), and one epoch of the same
+    # data on the GPU lands at err/frm 3.4535 (GRADDIVFRM=F) / 3.4924 (=T): 1.1 % apart by rounding
+    # alone; iteration 1's CV spreads 3.30 .. 3.62 across the reference's own runs
     runs = [dict(initial_cv=g["initial_cv"], iterations=g["iterations"])] + g["band"]
 
     def inside(v, vals, what):
         vals = [float(x) for x in vals]
         lo, hi = min(vals), max(vals)
-        m = max(0.5 * (hi - lo), 0.01 * sum(vals) / len(vals))
+        m = max(0.5 * (hi - lo), 0.015 * sum(vals) / len(vals))
         print(f"{what}: {v} (reference {lo} .. {hi})")
         assert lo - m <= float(v) <= hi + m, (what, v, lo, hi)
 
@@ -317,4 +323,5 @@ def test_newbob_scheduler_over_tnetcu_matches_reference():
     # the scheduler's file protocol: same iteration files (names carry lr / tr / cv at 5 digits: the
     # last digit may differ within the tolerance above) and the final copy
     assert len(final) == len(g["weights"])
-    assert [w.split("_lr")[0] for w in final] == [w.split("_lr")[0] for w in g["weights"]]
+    stem = re.compile(r"^(.*?_(?:iter\d+|final_iters\d+))(_lr|_tr)")
+    assert [stem.match(w).group(1) for w in final] == [stem.match(w).group(1) for w in g["weights"]]

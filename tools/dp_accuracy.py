@@ -13,8 +13,17 @@ linearly with N (lr_N = N lr_1: the same step per epoch of frames; --scale sqrt:
 TNetCu-style pass, fresh cache / shuffle seed per epoch, TNetCu.cc:330-441) rank 0 evaluates a
 held-out set in cross-validation mode (TNetCu -c).
 
+--newbob: the epochs are driven by the reference's newbob schedule (tools/train/
+training_scheduler_xent.sh:56-214, restated in tnet_amd.newbob): after every epoch the held-out
+cross-entropy decides accept (keep the weights) or reject (restore the previous best), halving starts
+once an epoch improves the CV cross-entropy by less than START_HALVING_INC and training stops once a
+halving epoch improves it by less than END_HALVING_INC (--end-halving-inc, the script's 0.1 by
+default); --epochs is then MAX_ITER.  --warmup F: in the first epoch the learning rate ramps linearly
+from lr_1 to lr_N over the first fraction F of the rank's utterances (the large-global-bunch runs
+otherwise take their first steps at N times the single-GPU rate from random weights).
+
 usage: python tools/dp_accuracy.py [--worlds 1,2,4,8] [--epochs 4] [--utts 800] [--lr 1.0]
-       (worker mode is internal)"""
+       [--newbob] [--warmup 0.5] (worker mode is internal)"""
 import argparse
 import json
 import os
@@ -67,34 +76,80 @@ def worker(a):
     mine = tnet_amd.shard_utterances(list(range(a.utts)), rank, world)
     train = [utterance(i, T, 0) for i in mine]
     held = [utterance(i, T, 1) for i in range(a.cv_utts)] if rank == 0 else []
+    from tnet_amd import newbob
     net = Network.from_layers(formats.gen_mlp_init(DIMS, seed=SEED))
     lr = a.lr * (world if a.scale == "linear" else world ** 0.5)
     net.set_learn_rate(lr)
     net.set_grad_div_frm(True)
+    nb = newbob.Newbob(repr(lr), a.bunch, max_iter=a.epochs, end_halving_inc=a.end_halving_inc) if a.newbob else None
+    best = None
     log = []
     t0 = time.time()
+
+    def cv_eval():
+        cobj = Objective()
+        cv = Trainer(net, cobj, bunchsize=a.bunch, cachesize=a.cache, seed=0, randomize=False, crossval=True)
+        cv.train_corpus([x for x, _ in held], [y for _, y in held])
+        return cobj.stats()
+
+    def bcast_cv():
+        """rank 0's held-out statistics, to every rank (the schedule's decisions must agree)"""
+        v = np.zeros(3, np.float64)
+        if rank == 0:
+            v[:] = cv_eval()
+        return comm.allreduce_host(v) if comm is not None else v
+
+    if nb is not None:
+        ce, cf, _ = bcast_cv()
+        nb.initial("%.6g" % (ce / cf))
+        best = [(W.copy(), b.copy()) for W, b in net.linear_params()]
     for ep in range(a.epochs):
         obj = Objective()
         tr = Trainer(net, obj, bunchsize=a.bunch, cachesize=a.cache, seed=1 + 1000 * ep + rank)
         if comm is not None:
             tr.set_comm(comm)
-        tr.train_corpus([x for x, _ in train], [y for _, y in train])
+        ep_lr = float(nb.lrate) if nb is not None else lr
+        if ep == 0 and a.warmup > 0 and world > 1:
+            nw = max(1, int(a.warmup * len(train)))
+            for k, (x, y) in enumerate(train):
+                net.set_learn_rate(a.lr + (ep_lr - a.lr) * min(1.0, k / nw))
+                tr.add_utterance(x, y)
+            tr.finish()
+        else:
+            net.set_learn_rate(ep_lr)
+            tr.train_corpus([x for x, _ in train], [y for _, y in train])
         err, frames, correct = obj.stats()
         st = np.array([err, frames, correct], np.float64)
         if comm is not None:
             st = comm.allreduce_host(st)
-        rec = {"epoch": ep + 1, "train_xent_per_frame": st[0] / st[1], "train_acc": 100.0 * st[2] / st[1],
-               "train_frames": int(st[1]), "steps_rank0": tr.steps}
-        if rank == 0:
-            cobj = Objective()
-            cv = Trainer(net, cobj, bunchsize=a.bunch, cachesize=a.cache, seed=0, randomize=False, crossval=True)
-            cv.train_corpus([x for x, _ in held], [y for _, y in held])
-            ce, cf, cc = cobj.stats()
-            rec.update(cv_xent_per_frame=ce / cf, cv_acc=100.0 * cc / cf, cv_frames=int(cf))
-        log.append(rec)
+        rec = {"epoch": ep + 1, "lr": ep_lr, "train_xent_per_frame": st[0] / st[1],
+               "train_acc": 100.0 * st[2] / st[1], "train_frames": int(st[1]), "steps_rank0": tr.steps}
         del tr
+        ce, cf, cc = bcast_cv()
+        rec.update(cv_xent_per_frame=ce / cf, cv_acc=100.0 * cc / cf, cv_frames=int(cf))
+        if nb is not None:
+            acc = nb.decide(ep + 1, "%.6g" % rec["train_xent_per_frame"], "%.6g" % (ce / cf), f"epoch{ep + 1}")
+            rec["accepted"] = acc
+            if acc:
+                best = [(W.copy(), b.copy()) for W, b in net.linear_params()]
+            else:                                   # the script reverts to the best network
+                for k, (W, b) in enumerate(best):
+                    net.set_params(2 * k, W, b)
+        log.append(rec)
+        if rank == 0 and a.progress:
+            with open(a.progress, "a") as fh:
+                fh.write(json.dumps(dict(rec, world=world, t=round(time.time() - t0, 1))) + "\n")
+        if nb is not None and nb.done:
+            break
+    if nb is not None:
+        for k, (W, b) in enumerate(best):
+            net.set_params(2 * k, W, b)
+        ce, cf, cc = bcast_cv()
+        log.append({"final_best": True, "cv_xent_per_frame": ce / cf, "cv_acc": 100.0 * cc / cf})
     if rank == 0:
-        print("RESULT " + json.dumps({"world": world, "lr": lr, "lr_scaling": a.scale, "bunch_per_rank": a.bunch,
+        print("RESULT " + json.dumps({"world": world, "lr": lr, "lr_scaling": a.scale, "newbob": a.newbob,
+                                      "warmup": a.warmup, "end_halving_inc": a.end_halving_inc,
+                                      "bunch_per_rank": a.bunch,
                                       "global_bunch": a.bunch * world, "epochs": log,
                                       "wall_s": round(time.time() - t0, 1)}), flush=True)
     if comm is not None:
@@ -119,6 +174,10 @@ def main():
     ap.add_argument("--cache", type=int, default=16384)
     ap.add_argument("--lr", type=float, default=1.0)
     ap.add_argument("--scale", default="linear", choices=["linear", "sqrt"], help="lr_N = lr_1 N or lr_1 sqrt(N)")
+    ap.add_argument("--newbob", action="store_true")
+    ap.add_argument("--end-halving-inc", type=float, default=0.1)
+    ap.add_argument("--warmup", type=float, default=0.0)
+    ap.add_argument("--progress", default="", help="rank 0 appends one JSON line per epoch to this file")
     a = ap.parse_args()
     if a.mode == "worker":
         worker(a)
@@ -129,7 +188,10 @@ def main():
                    OMP_NUM_THREADS="2")
         args = [sys.executable, os.path.abspath(__file__), "worker", "--epochs", str(a.epochs), "--utts",
                 str(a.utts), "--cv-utts", str(a.cv_utts), "--bunch", str(a.bunch), "--cache", str(a.cache), "--lr",
-                str(a.lr), "--scale", a.scale]
+                str(a.lr), "--scale", a.scale, "--end-halving-inc", str(a.end_halving_inc), "--warmup", str(a.warmup),
+                "--progress", a.progress]
+        if a.newbob:
+            args.append("--newbob")
         procs = [subprocess.Popen(args, env=dict(env, RANK=str(r)), stdout=subprocess.PIPE, stderr=subprocess.PIPE,
                                   text=True) for r in range(world)]
         res = None
@@ -143,8 +205,8 @@ def main():
         print(json.dumps(res), flush=True)
         out.append(res)
     print("SUMMARY " + json.dumps([{"world": r["world"], "lr": r["lr"], "cv_acc": [round(e["cv_acc"], 2) for e in r["epochs"]],
-                                     "train_acc": [round(e["train_acc"], 2) for e in r["epochs"]]} for r in out]),
-          flush=True)
+                                     "train_acc": [round(e["train_acc"], 2) for e in r["epochs"] if "train_acc" in e]}
+                                    for r in out]), flush=True)
 
 
 if __name__ == "__main__":

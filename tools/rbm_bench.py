@@ -59,5 +59,9 @@ cpu = cpu_steps * B / (time.perf_counter() - t0)
 print(json.dumps({"config": f"TRbmCu Gauss-Bernoulli RBM {V}->{H}, CD-1, bunch {B}", "steps": steps,
                   "gpu_frames_per_s": round(gpu, 1), "ms_per_step": round(1e3 * dt / steps, 4),
                   "gpu_tflops": round(gpu * flop_per_frame / 1e12, 2),
+                  "roofline": {"bound": "mfma", "achieved": round(gpu * flop_per_frame / 1e12, 2), "peak": 157.3,
+                               "unit": "TFLOP/s", "frac": round(gpu * flop_per_frame / 1e12 / 157.3, 4),
+                               "basis": "whole CD-1 step: 10 * 440 * 2048 flop/frame (pos, recon, neg, stacked "
+                                        "statistics) / step time, dense fp32 MFMA peak"},
                   "cpu_frames_per_s": round(cpu, 1),
                   "cpu": f"oracle C restatement orc_rbm_step, 1 core, {cpu_steps} steps"}), flush=True)

@@ -5,6 +5,7 @@ one host core (oracle/tnet_oracle.c orc_rnn_utterance: the reference's CuRecurre
 plain C -- a CPU stand-in, not the reference binary, which is CUDA-only).
 
 usage: python tools/rnn_bench.py [utterances] [senones]"""
+import json
 import os
 import sys
 import time
@@ -44,5 +45,21 @@ m = orc.RNN(layers[0].W, layers[0].b, layers[1].W, layers[1].b)
 t0 = time.perf_counter()
 m.utterance(feats[0], labels[0], bptt, lr, 0.0, 0.0)
 cpu = T / (time.perf_counter() - t0)
+# per-frame HBM bound (the weights are updated every frame, so every frame streams them): recurrent
+# forward reads Wr [(nIn+H) x H]; the output layer reads W2 [H x S] once for z and once more + writes it
+# for the fused backprop/update; the BPTT GEMVs read the recurrent block [H x H] bptt times; the
+# recurrent update reads and writes Wr
+wr, w2, hh = 4.0 * (nIn + H) * H, 4.0 * H * S, 4.0 * H * H
+bytes_frame = wr + w2 + 2 * w2 + bptt * hh + 2 * wr
+bound = 8000e9 / bytes_frame
+print(json.dumps({"config": f"TRecurrentCu RNN {nIn}->{H} (BPTT {bptt})->{S}, {T}-frame utterances",
+                  "gpu_frames_per_s": round(gpu, 1),
+                  "roofline": {"bound": "hbm", "achieved": round(gpu * bytes_frame / 1e9, 1), "peak": 8000.0,
+                               "unit": "GB/s", "frac": round(gpu / bound, 4),
+                               "algorithmic_bytes_per_frame": bytes_frame,
+                               "basis": "per-frame weight streaming (Wr fwd + W2 fwd + W2 read/write in the fused "
+                                        "backprop/update + bptt x recurrent block + Wr read/write)"},
+                  "cpu_frames_per_s": round(cpu, 1), "cpu": "oracle C restatement orc_rnn_utterance, 1 core"}),
+      flush=True)
 print(f"RNN {nIn}->{H}(recurrent, bptt {bptt})->{S}, {T}-frame utterances: GPU {gpu:.0f} frames/s (median of "
       f"{', '.join(f'{r:.0f}' for r in rates)}), oracle C restatement (1 core) {cpu:.0f} frames/s", flush=True)
