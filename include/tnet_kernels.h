@@ -141,9 +141,15 @@ int tnet_sgemm(char transa, char transb, int m, int n, int k, float alpha, const
 /* Tuning knob: force one GEMM tile configuration for every later launch in this process
  * ("auto" = per-shape heuristic; names as in gemm_f32.hip, e.g. "m64x128k64s2"), optionally with a
  * forced split-K count ("m64x64k32s4w41+sk8") and the combine mode ("+il0" second launch (default),
- * "+il1" in-launch up to 64 KB a tile, "+il2" in-launch for every 64x64 / 32x64 tile; sticky).
- * Not thread-safe. */
+ * "+il1" in-launch up to 64 KB a tile, "+il2" in-launch for every 64x64 / 32x64 tile; sticky) and a CU
+ * reservation ("+rsv<R>", as tnet_gemm_reserve; sticky).  Not thread-safe. */
 int tnet_gemm_config(const char* name);
+/* R CUs held by another kernel while the caller's next GEMMs run (the data-parallel exchange sets it
+ * while RCCL's collectives are in flight, 0 when they are done): the step's 64x128 backward / forward
+ * and 128x128 gradient shapes then run as stream-K over CUs - R workgroups (gemm16_sk_kernel) instead of
+ * a one-tile-per-CU grid whose last tiles would wait for a second round.  No reference counterpart
+ * (the reference has no multi-GPU path).  Not thread-safe. */
+int tnet_gemm_reserve(int cus);
 
 /* ------------------------------------------------------------------------------------
  * Fused kernels of the MI355X SGD path (no reference counterpart: each replaces a chain of

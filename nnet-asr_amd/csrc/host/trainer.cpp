@@ -298,15 +298,39 @@ struct RcclExchange::Impl {
   double* dscratch = nullptr;
 };
 
+// RCCL channels and the CUs reserved for them.  RCCL runs one workgroup per channel (512 threads,
+// 37.6 KB LDS, 248-256 VGPRs, resident for the whole collective: tools/cohab_probe.hip), and a GEMM
+// grid of exactly one tile round per CU loses a whole second round beside them (1.8x,
+// profiles/r02_rccl_cohab_probe.txt).  So the channel count is capped (NCCL_MAX_NCHANNELS, when the
+// user has not set it: TNET_DP_RCCL_CHANNELS, default 16) and while this rank's reductions are in
+// flight the GEMMs run stream-K over CUs - R workgroups, R = the cap (TNET_DP_RESERVE_CUS overrides;
+// 0: off).  Single-rank communicators launch no channel kernels: no reservation unless asked for.
+// the cap, set before RCCL reads its environment (UniqueId on rank 0, the communicator on every rank)
+static int rccl_channels() {
+  const char* mx = getenv("NCCL_MAX_NCHANNELS");
+  if (mx) return atoi(mx);
+  const char* ch = getenv("TNET_DP_RCCL_CHANNELS");
+  const int channels = ch ? atoi(ch) : 16;
+  if (channels > 0) setenv("NCCL_MAX_NCHANNELS", std::to_string(channels).c_str(), 0);
+  return channels;
+}
+static int rccl_reserve(int world) {
+  const int channels = rccl_channels();
+  const char* rv = getenv("TNET_DP_RESERVE_CUS");  // explicit: also at world 1 (tests)
+  if (rv) return atoi(rv) > 0 ? atoi(rv) : 0;
+  return world > 1 && channels > 0 ? channels : 0;
+}
+
 void RcclExchange::UniqueId(char out[128]) {
   static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId size");
   ncclUniqueId id;
+  (void)rccl_channels();
   NCCL_CALL(ncclGetUniqueId(&id));
   std::memcpy(out, &id, 128);
 }
 
 RcclExchange::RcclExchange(int rank, int world, const char id[128])
-    : mImpl(new Impl), mRank(rank), mWorld(world), mShard(shard_env()) {
+    : mImpl(new Impl), mRank(rank), mWorld(world), mShard(shard_env()), mReserve(rccl_reserve(world)) {
   CuDevice& dev = CuDevice::Instantiate();
   ncclUniqueId uid;
   std::memcpy(&uid, id, 128);
@@ -345,6 +369,7 @@ void RcclExchange::Submit(CuUpdatableComponent& comp) {
     mImpl->ar_done.push_back(d);
   }
   const size_t idx = mImpl->next_event++;
+  if (idx == 0 && mReserve > 0) TNET_SAFE_CALL(tnet_gemm_reserve(mReserve));
   hipEvent_t ev = mImpl->events[idx];
   // the gradient kernels were enqueued on the compute stream: order the reduction after them
   TNET_HIP_CALL(hipEventRecord(ev, dev.Stream()));
@@ -420,6 +445,7 @@ void RcclExchange::WaitAll() {
     mImpl->applied = false;
   }
   mImpl->next_event = 0;
+  if (mReserve > 0) TNET_SAFE_CALL(tnet_gemm_reserve(0));
 }
 
 void RcclExchange::AllReduceHost(double* v, int n) {

@@ -139,7 +139,7 @@ class RcclExchange : public GradExchange {
   void AllReduceHost(double* v, int n) override;
   /// all-reduce (sum) of a device float buffer on the communication stream, synchronous
   void AllReduceDevice(float* buf, size_t n);
-  /// Sharded apply (world > 1 unless TNET_DP_SHARD=0; TNET_DP_SHARD=1 also at world 1): Submit
+  /// Sharded apply (TNET_DP_SHARD=1 on every rank; off by default): Submit
   /// reduce-scatters each gradient block (ShardRanges; the tail all-reduced), the rank applies its
   /// shard, GatherParams all-gathers the updated parameters in place on the communication stream --
   /// the apply's HBM traffic divided by the world size, the same bytes over xGMI as an all-reduce
@@ -151,6 +151,9 @@ class RcclExchange : public GradExchange {
   std::unique_ptr<Impl> mImpl;
   int mRank, mWorld;
   bool mShard = false;
+  // CUs the 2048^2-class GEMMs leave to RCCL's channel workgroups while collectives are in flight
+  // (tnet_gemm_reserve: stream-K over CUs - R workgroups from the first Submit of a step to WaitAll)
+  int mReserve = 0;
 };
 
 }  // namespace TNet

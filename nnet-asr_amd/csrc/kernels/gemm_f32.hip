@@ -90,6 +90,10 @@ struct GemmP {
   // indexed row * ldc + col like the probabilities C (the reference indexes them with C's MatrixDim)
   float* bin; long ldbin;
   unsigned* rz[4];
+  // stream-K piece (gemm16_body EPI_T >= kEpiStreamK, gemm16_sk_kernel): ksplit = the tile's piece count
+  // (1 or 2); the first of a split tile's pieces to finish stores its accumulators to skws + tile * BM * BN
+  // (fragment order), the second adds them to its own and runs the tile's epilogue (tile_cnt[tile])
+  float* skws;
 };
 
 
@@ -685,6 +689,8 @@ __device__ __forceinline__ void lds_vec(const float* p, float (&x)[4]) {
 // EPI_T >= kEpiInLaunch: a split-K slice kernel (EPI_STORE into the workspace) whose tiles' last
 // slices combine the slices with epilogue EPI_T - kEpiInLaunch inside the launch
 constexpr int kEpiInLaunch = 32;
+// EPI_T >= kEpiStreamK: a stream-K piece (gemm16_sk_kernel) whose tile epilogue is EPI_T - kEpiStreamK
+constexpr int kEpiStreamK = 64;
 // PX (exact prefetch): the tile grid covers M x N exactly and the epilogue operands are 16-B aligned
 // (launch_cfg checks), so the epilogue-operand prefetch is a known number of unconditional loads per
 // wave and the first seam waits for the ring only, not for them (TNET_GEMM_PRE0=0: off)
@@ -696,12 +702,15 @@ template <int BM, int BN, int BK, int S, int EPI_T, bool PX>
 constexpr int gemm16_smem_floats() {
   return S * (BM + BN) * BK;
 }
+// SKM (EPI_T >= kEpiStreamK): a stream-K piece; bid_x is the tile's index in the grouped order itself
+// (gemm16_sk_kernel gives each XCD a contiguous range of it)
 template <int BM, int BN, int BK, int WM, int WN, int S, int SP, bool A_KC, bool B_KC, int EPI_T, bool PX>
 __device__ __forceinline__ void gemm16_body(const GemmP& p_in, float* __restrict__ smem, const int bid_x) {
-  constexpr bool INL = EPI_T >= kEpiInLaunch;
-  constexpr int EPI = INL ? EPI_STORE : EPI_T;  // the tile epilogue
+  constexpr bool SKM = EPI_T >= kEpiStreamK;
+  constexpr bool INL = !SKM && EPI_T >= kEpiInLaunch;
+  constexpr int EPI = SKM ? EPI_T - kEpiStreamK : INL ? EPI_STORE : EPI_T;  // the tile epilogue
   GemmP p = p_in;
-  if (p.ksplit > 1) {
+  if (!SKM && p.ksplit > 1) {
     const long z = blockIdx.y;
     p.A += z * p.kstepA;
     p.B += z * p.kstepB;
@@ -732,7 +741,7 @@ __device__ __forceinline__ void gemm16_body(const GemmP& p_in, float* __restrict
   const int nbn = (N + BN - 1) / BN, nbm = (M + BM - 1) / BM;
   const int nwg = nbm * nbn;
   const int bid = bid_x, xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
-  const int L = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int L = SKM ? bid : (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
   const int grp = p.group, per_group = grp * nbn;
   const int first_m = (L / per_group) * grp;
   const int gsz = min(nbm - first_m, grp);
@@ -1271,6 +1280,7 @@ __device__ __forceinline__ void gemm16_body(const GemmP& p_in, float* __restrict
   }
   wait_vmcnt<0>();  // repeat loads of the last tile still land in LDS
   TNET_STAMP(2);
+
   if (!LDR && K % BK && K % 4 == 0) {
     // partial last k-tile (Kt = K % BK deep) through the same LDS-DMA images, in slot nfull % S (the
     // final seam read it: every wave's reads retire before the barrier).  Sources past K are clamped
@@ -1363,6 +1373,56 @@ __device__ __forceinline__ void gemm16_body(const GemmP& p_in, float* __restrict
     }
   }
 
+  if constexpr (SKM) {
+    // ---- stream-K fixup: a split tile has exactly two pieces (gemm16_sk_kernel's ranges are at least
+    // a tile long).  Each draws a ticket as it finishes its k-range; the first stores its accumulators
+    // and flags them stored, the second waits for that flag -- the first piece is running by then (it
+    // drew its ticket), so the wait is bounded by one tile store whatever else holds the CUs -- and adds
+    // the stored partial to its own accumulators, then runs the tile's epilogue.  Two-term fp32 sums
+    // commute exactly: the result is the same whichever piece finishes last.  The hand-off is the sc1
+    // form of cdna_hip_programming.md's in-launch reduction (placement-independent, no L2 writeback or
+    // invalidate): sc1 (write-through) stores in fragment order (lane-contiguous 16 B), drained before
+    // the relaxed agent-scope flag; sc1 loads of every stored word.  tile_cnt[tile]: tickets in the low
+    // half, the stored flag in the high half; the second piece resets it for the next launch.
+    if (p.ksplit > 1) {
+      constexpr int SLICE = BM * BN;
+      const __amdgpu_buffer_rsrc_t rw = tile_rsrc(p.skws + (long)bid_x * SLICE);
+      __attribute__((address_space(1))) unsigned* cnt =
+          (__attribute__((address_space(1))) unsigned*)(p.tile_cnt + bid_x);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();  // every wave's ring reads retired (smem[0] below is in slot 0)
+      if (threadIdx.x == 0) {
+        const unsigned ticket = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        smem[0] = (ticket & 0xFFFFu) == 0 ? 0.f : 1.f;
+      }
+      __syncthreads();
+      if (smem[0] == 0.f) {
+#pragma unroll
+        for (int a = 0; a < TM; ++a)
+#pragma unroll
+          for (int b = 0; b < TN; ++b) st_wt(rw, ((long)(a * TN + b) * NT + threadIdx.x) * 4, acc[a][b]);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0) __hip_atomic_fetch_add(cnt, 0x10000u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return;  // uniform: the workgroup's next piece (after the caller's barrier)
+      }
+      if (threadIdx.x == 0) {
+        while ((__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> 16) == 0u)
+          __builtin_amdgcn_s_sleep(2);
+        __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // ready for the next launch
+      }
+      __syncthreads();
+      f32x4 t[TM][TN];
+#pragma unroll
+      for (int a = 0; a < TM; ++a)
+#pragma unroll
+        for (int b = 0; b < TN; ++b) t[a][b] = ld_sc1(rw, ((long)(a * TN + b) * NT + threadIdx.x) * 4);
+#pragma unroll
+      for (int a = 0; a < TM; ++a)
+#pragma unroll
+        for (int b = 0; b < TN; ++b) acc[a][b] = acc[a][b] + t[a][b];
+    }
+  }
   if constexpr (epi_bias_slabs(EPI) && !PXB)
     if (bm == 0) bias_pre_finish<BN, EPI == EPI_STORE_BG>(p, bn, bpre);
   if constexpr (PXB) {
@@ -1587,8 +1647,8 @@ __device__ __forceinline__ void gemm16_body(const GemmP& p_in, float* __restrict
       r.beta = p_in.beta2;
       r.wt = 0;  // plain stores (the descriptor offsets are not checked for this path)
       combine_tile_t<epi_base(EPI_C)>(r, p_in.C, p_in.slabC, p_in.ksplit, (int)p_in.ldc, bm, bn, BM, BN, NT);
-      // EPI_SGD_B / EPI_STORE_BG: the first tile-row's combiners also do the bias of their columns
       if constexpr (epi_bias_slabs(EPI_C)) {
+        // EPI_SGD_B / EPI_STORE_BG: the first tile-row's combiners also do the bias of their columns
         if (bm == 0) {
           BiasPre bpc;
           bias_pre_load<BN, EPI_C == EPI_STORE_BG>(r, bn, bpc);
@@ -1599,6 +1659,44 @@ __device__ __forceinline__ void gemm16_body(const GemmP& p_in, float* __restrict
   }
   TNET_STAMP(3);
   TNET_STAMP_RT(5);
+}
+
+// Stream-K over G workgroups (the GEMMs beside RCCL).  A tile grid of one
+// workgroup per CU loses a whole second round when R CUs are held by another kernel (RCCL's channel
+// workgroups keep 37.6 KB LDS and 248-256 VGPRs per lane for the whole collective:
+// tools/cohab_probe.hip), so while collectives are in flight the data-parallel step's GEMMs run on
+// G = CUs - R workgroups: the T tiles' T * KT k-tiles (tiles in the grouped order) are cut into G equal
+// contiguous ranges, and the ranges go to the workgroups XCD by XCD (workgroup b runs on XCD b % 8: each
+// XCD gets a contiguous run of ranges, so a tile's pieces meet in one L2 and its neighbours share
+// operands there, as in the plain grid).  T >= G: a range is at least a tile long, so it covers whole
+// tiles and at most a piece at either end, and a split tile has exactly two pieces; they combine through
+// gemm16_body's stream-K fixup and the second to finish runs the tile's own epilogue.  Static and
+// deterministic: no claims, no queues.
+template <int BM, int BN, int BK, int WM, int WN, int S, bool A_KC, bool B_KC, int EPI>
+__global__ __launch_bounds__(WM * WN * 64)
+__attribute__((amdgpu_waves_per_eu((WM * WN + 3) / 4, (WM * WN + 3) / 4)))
+void gemm16_sk_kernel(const GemmP p, const int G) {
+  __shared__ __attribute__((aligned(16))) float smem[gemm16_smem_floats<BM, BN, BK, S, EPI, true>()];
+  const int T = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN), KT = p.K / BK;
+  const long I = (long)T * KT;
+  const int b = blockIdx.x, xcd = b & 7, q8 = G >> 3, r8 = G & 7;
+  const int v = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (b >> 3);
+  const long s = (long)v * I / G, e = (long)(v + 1) * I / G;
+  for (long k0 = s; k0 < e;) {
+    const int t = (int)(k0 / KT);
+    const long tb = (long)t * KT, te = tb + KT, k1 = e < te ? e : te;
+    if (k0 != s) __syncthreads();  // the previous piece is done with the ring
+    // the ranges holding the tile's first and last k-tile: w(k) = ((k + 1) G - 1) / I
+    const int w0 = (int)(((tb + 1) * G - 1) / I), w1 = (int)((te * G - 1) / I);
+    GemmP q = p;
+    q.ksplit = w1 - w0 + 1;
+    const long kk = (k0 - tb) * BK;
+    q.A = p.A + (A_KC ? kk : kk * p.lda);
+    q.B = p.B + (B_KC ? kk : kk * p.ldb);
+    q.K = (int)((k1 - k0) * BK);
+    gemm16_body<BM, BN, BK, WM, WN, S, 0, A_KC, B_KC, kEpiStreamK + EPI, true>(q, smem, t);
+    k0 = k1;
+  }
 }
 
 template <int BM, int BN, int BK, int WM, int WN, int S, int SP, bool A_KC, bool B_KC, int EPI_T, bool PX = false>
@@ -1871,6 +1969,11 @@ static int g_early = 1;   // TNET_GEMM_EARLY=0: prologue issues S-1 slots before
 static int g_inlaunch = 0;
 static int g_pair = 1;  // TNET_GEMM_PAIR=0: tnet_affine_update_bwd_pair never pairs (A/B measurements)
 static int g_pre0 = 1;  // TNET_GEMM_PRE0=0: the first seam also waits for the epilogue-operand prefetch
+// CUs reserved for another kernel (RCCL's channel workgroups) while the data-parallel step's collectives
+// are in flight (tnet_gemm_reserve, set by the gradient exchange; tnet_gemm_config "+rsv<R>" for tests):
+// the 64x128 backward / forward and the 128x128 gradient then run as stream-K over CUs - R workgroups
+// (gemm16_sk_kernel).  0: the plain tile grid.
+static int g_reserve = 0, g_cus = 0;
 static int g_wt = 1;  // TNET_GEMM_WT=0: plain 16-B epilogue stores instead of write-through (sc1; measured +1.4 % frames/s)
 static int forced_cfg() {
   if (g_cfg == -2) {
@@ -1893,6 +1996,7 @@ static int forced_cfg() {
     if (wt) g_wt = atoi(wt);
     const char* il = getenv("TNET_SPLITK_INLAUNCH");
     if (il) g_inlaunch = atoi(il);
+
   }
   return g_cfg;
 }
@@ -1954,6 +2058,45 @@ static void cfg_shape(int cfg, int* bm, int* bn, int* kind) {
     TNET_GEMM_CFGS(X)
 #undef X
     default: *bm = 64; *bn = 64; *kind = 0;
+  }
+}
+
+// gemm16_sk_kernel launch of a PX-exact 64x128 / 128x128 BK-64 two-slot shape over CUs - g_reserve
+// workgroups; false: not applicable (no reservation, other shapes)
+template <int BM, int BN, bool A_KC, bool B_KC, int EPI>
+static bool launch_sk(const GemmP& p, hipStream_t st) {
+  forced_cfg();
+  if (g_reserve <= 0) return false;
+  constexpr bool OK = (BM == 64 && BN == 128 && A_KC && B_KC && EPI == EPI_DSIG_CS) ||
+                      (BM == 64 && BN == 128 && A_KC && !B_KC && EPI == EPI_BIAS_SIG) ||
+                      (BM == 128 && BN == 128 && !A_KC && !B_KC && (EPI == EPI_STORE_BG || EPI == EPI_STORE));
+  if constexpr (!OK) {
+    return false;
+  } else {
+    if (!g_cus) {
+      int dev = 0;
+      hipDeviceProp_t prop;
+      if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess) return false;
+      g_cus = prop.multiProcessorCount;
+    }
+    const long T = (long)cdiv(p.M, BM) * cdiv(p.N, BN);
+    const int G = g_cus - g_reserve;
+    if (G < 1 || T < G || T > 8L * G || p.K % 64 || p.K < 128 || !px_exact<BM, BN, EPI>(p)) return false;
+    const long extA = A_KC ? (long)p.M * p.lda : 64L * p.lda + p.M;
+    const long extB = B_KC ? (long)p.N * p.ldb : 64L * p.ldb + p.N;
+    if (4 * extA >= (1L << 32) || 4 * extB >= (1L << 32)) return false;
+    // T >= G: every range is at least KT k-tiles long, so a tile is cut into at most two pieces
+    float* ws = splitk_workspace(sizeof(float) * (size_t)T * BM * BN, st);
+    unsigned* cnt = ws ? splitk_counters((size_t)T, st) : nullptr;
+    if (!cnt) return false;
+    GemmP q = p;
+    q.group = g_group > 0 ? g_group : 8;
+    q.early_issue = g_early;
+    q.wt = g_wt;
+    q.skws = ws;
+    q.tile_cnt = cnt;
+    gemm16_sk_kernel<BM, BN, 64, 2, 2, 2, A_KC, B_KC, EPI><<<(unsigned)G, 256, 0, st>>>(q, G);
+    return true;
   }
 }
 
@@ -2048,6 +2191,10 @@ static int launch_colsum_bwd(const GemmP& p_in, hipStream_t st) {
   p.group = g_group > 0 ? g_group : 8;
   if (cfg != CFG_m64x128k64s2 && cfg != CFG_m64x64k32s4 && cfg != CFG_m64x64k64s2)
     cfg = (long)cdiv(p.M, 64) * cdiv(p.N, 128) >= 200 ? CFG_m64x128k64s2 : CFG_m64x64k32s4;
+  if (cfg == CFG_m64x128k64s2 && launch_sk<64, 128, true, true, EPI_DSIG_CS>(p, st)) {
+    TNET_LAUNCH_CHECK();
+    return TNET_OK;
+  }
   bool ok = false;
   if (cfg == CFG_m64x128k64s2) ok = launch_cfg<1, 64, 128, 64, 2, 2, 2, 0, true, true, EPI_DSIG_CS>(p, st);
   else if (cfg == CFG_m64x64k64s2) ok = launch_cfg<1, 64, 64, 64, 2, 2, 2, 0, true, true, EPI_DSIG_CS>(p, st);
@@ -2121,6 +2268,13 @@ static int launch_gemm(const GemmP& p_in, hipStream_t st) {
   const int cfg = pl.cfg;
   p.group = g_group > 0 ? g_group : 8;
   if (pl.ks > 1) return launch_splitk<A_KC, B_KC, EPI>(p, cfg, pl.ks, st);
+  bool sk_done = false;
+  if (cfg == CFG_m64x128k64s2) sk_done = launch_sk<64, 128, A_KC, B_KC, EPI>(p, st);
+  else if (cfg == CFG_m128x128k64s2) sk_done = launch_sk<128, 128, A_KC, B_KC, EPI>(p, st);
+  if (sk_done) {
+    TNET_LAUNCH_CHECK();
+    return TNET_OK;
+  }
   bool ok = false;
   switch (cfg) {
 #define X(name, KIND, BM, BN, BK, WM, WN, S, IL) \
@@ -2452,9 +2606,11 @@ extern "C" int tnet_gemm_config(const char* name) {
   // "<cfg>[+sk<n>][+il<m>]": a tile configuration (or "auto"), optionally a forced split-K count and
   // the split-K combine (il0: a second launch (default), il1: in-launch where a tile's slices are <= 64 KB,
   // il2: in-launch whatever their size; in-launch only for 64x64 / 32x64 tiles, other tiles always
-  // combine in a second launch); the combine mode stays as set until the next il suffix
+  // combine in a second launch); the combine mode stays as set until the next il suffix.
+  // "+rsv<R>": R CUs reserved (gemm16_sk_kernel over CUs - R workgroups for the data-parallel shapes),
+  // 0 none -- as tnet_gemm_reserve, stays as set until changed
   char base[64] = "auto";
-  int split = -1, inl = -1;
+  int split = -1, inl = -1, rsv = -1;
   if (name) {
     const char* plus = strchr(name, '+');
     const size_t n = plus ? (size_t)(plus - name) : strlen(name);
@@ -2464,6 +2620,7 @@ extern "C" int tnet_gemm_config(const char* name) {
     while (plus) {
       if (!strncmp(plus, "+sk", 3) && atoi(plus + 3) >= 1) split = atoi(plus + 3);
       else if (!strncmp(plus, "+il", 3) && plus[3] >= '0' && plus[3] <= '2') inl = plus[3] - '0';
+      else if (!strncmp(plus, "+rsv", 4) && plus[4] >= '0' && plus[4] <= '9') rsv = atoi(plus + 4);
       else return TNET_ERR_ARG;
       plus = strchr(plus + 1, '+');
     }
@@ -2476,6 +2633,14 @@ extern "C" int tnet_gemm_config(const char* name) {
   g_cfg = cfg;
   g_split = split;
   if (inl >= 0) g_inlaunch = inl;
+  if (rsv >= 0) g_reserve = rsv;
+  return TNET_OK;
+}
+
+extern "C" int tnet_gemm_reserve(int cus) {
+  if (cus < 0) return TNET_ERR_ARG;
+  forced_cfg();
+  g_reserve = cus;
   return TNET_OK;
 }
 

@@ -55,6 +55,11 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t tile_rsrc(const float* base) {
 __device__ __forceinline__ void st_wt(__amdgpu_buffer_rsrc_t r, long elem_off, f32x4 v) {
   __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, (int)(elem_off * 4), 0, 16);
 }
+// the matching sc1 load: reads what another workgroup stored with st_wt without an acquire fence
+// (cdna_hip_programming.md, in-launch split-K reduction, sc1 form)
+__device__ __forceinline__ f32x4 ld_sc1(__amdgpu_buffer_rsrc_t r, long elem_off) {
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)(elem_off * 4), 0, 16));
+}
 
 struct ArgMax {
   float v;

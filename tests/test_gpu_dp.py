@@ -123,3 +123,48 @@ def test_dp_rccl_world1_equals_local_update(monkeypatch, shard):
         np.testing.assert_allclose(b1, b0, rtol=1e-5, atol=1e-7)
     v = comm.allreduce_host(np.array([1.5, -2.0]))
     assert v.tolist() == [1.5, -2.0]
+
+
+def _assert_update_close(after_gpu, after_ref, before, rtol, what):
+    ref = np.asarray(after_ref, np.float32)
+    upd = np.abs(ref.astype(np.float64) - before)
+    tol = 2.0 * np.spacing(np.abs(ref)).astype(np.float64) + rtol * upd.max()
+    worst = float((np.abs(np.asarray(after_gpu, np.float64) - ref) / tol).max())
+    assert worst <= 1.0, (what, worst)
+
+
+def test_dp_rccl_reserved_cus_full_size(monkeypatch):
+    """The RCCL exchange's CU reservation (TNET_DP_RESERVE_CUS, explicit at world 1): from the first
+    reduction of a step to WaitAll the 2048^2 GEMMs run stream-K over CUs - 8 workgroups (split tiles
+    combined in-launch).  Two full-size steps through the communicator match the oracle's steps with the
+    tolerance of tests/test_gpu_fullsize.py (2 ulp + 1e-4 of the largest update), and differ from the
+    unreserved local run in summation order only (evidence the stream-K path ran)."""
+    dims, B, lr = [440, 2048, 2048, 2048, 135], 1024, 1.0
+    layers = formats.gen_mlp_init(dims, seed=3)
+    monkeypatch.setenv("TNET_DP_RESERVE_CUS", "8")
+    comm = Comm(0, 1, Comm.unique_id())
+    rng = np.random.default_rng(11)
+    bunches = [(rng.standard_normal((B, dims[0])).astype(np.float32), rng.integers(0, dims[-1], B).astype(np.int32))
+               for _ in range(2)]
+    runs = []
+    for use_comm in (False, True):
+        net = Network.from_layers(layers)
+        net.set_learn_rate(lr)
+        net.set_grad_div_frm(True)
+        if use_comm:
+            net.set_comm(comm)
+        obj = Objective()
+        for X, L in bunches:
+            net.train_bunch(obj, DeviceArray.from_numpy(X), DeviceArray.vector(L))
+        runs.append((net.linear_params(), obj.stats()))
+    ref = orc.MLP.from_layers(layers)
+    W0 = [w.astype(np.float64) for w in ref.W]
+    b0 = [b.astype(np.float64) for b in ref.b]
+    for X, L in bunches:
+        ref.step(X, L, lr)
+    for params, stats in runs:
+        for k, (W, b) in enumerate(params):
+            _assert_update_close(W, ref.W[k], W0[k], 1e-4, f"layer {k} W")
+            _assert_update_close(b, ref.b[k], b0[k], 1e-4, f"layer {k} b")
+        np.testing.assert_allclose(stats[0], ref.xent, rtol=1e-5)
+    assert any(not np.array_equal(runs[0][0][k][0], runs[1][0][k][0]) for k in (1, 2))

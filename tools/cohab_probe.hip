@@ -16,6 +16,7 @@
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <thread>
 #include <vector>
 
@@ -60,7 +61,78 @@ __global__ __launch_bounds__(NT) void occupier(float* out, long ticks) {
   if (acc == -1.f) out[threadIdx.x] = acc;
 }
 
+// ./tools/cohab_probe steal [nocc]: the step's backward-pass GEMM shapes (gradient 128x128, backward
+// 64x128 + diff-sigmoid + slab sums, forward 64x128 + bias + sigmoid) alone and beside nocc RCCL-footprint
+// occupiers (512 threads, 37.6 KB LDS, 256 VGPRs), on the plain tile grid and as stream-K over CUs - R
+// workgroups (tnet_gemm_config "+rsv<R>", gemm16_sk_kernel)
+static int steal_probe(int nocc) {
+  const int M = 1024, K = 2048, N = 2048, reps = 20;
+  CT(tnet_select_gpu(0));
+  std::vector<float> h((size_t)K * N);
+  for (size_t i = 0; i < h.size(); ++i) h[i] = (float)((i * 2654435761u) % 1000) * 1e-3f - 0.5f;
+  float *X, *E, *G, *W, *Y, *bias, *P, *gb, *junk;
+  CK(hipMalloc(&X, (size_t)M * K * 4));
+  CK(hipMalloc(&E, (size_t)M * N * 4));
+  CK(hipMalloc(&G, (size_t)K * N * 4));
+  CK(hipMalloc(&W, (size_t)K * N * 4));
+  CK(hipMalloc(&Y, (size_t)M * K * 4));
+  CK(hipMalloc(&bias, N * 4));
+  CK(hipMalloc(&P, 64 * N * 4));
+  CK(hipMalloc(&gb, N * 4));
+  CK(hipMalloc(&junk, 4096));
+  CK(hipMemcpy(X, h.data(), (size_t)M * K * 4, hipMemcpyHostToDevice));
+  CK(hipMemcpy(E, h.data(), (size_t)M * N * 4, hipMemcpyHostToDevice));
+  CK(hipMemcpy(W, h.data(), (size_t)K * N * 4, hipMemcpyHostToDevice));
+  CK(hipMemcpy(Y, h.data(), (size_t)M * K * 4, hipMemcpyHostToDevice));
+  CK(hipMemset(bias, 0, N * 4));
+  CK(hipMemset(P, 0, 64 * N * 4));
+  const TnetMatrixDim dX = {M, K, K}, dE = {M, N, N}, dG = {K, N, N}, dW = {K, N, N}, dY = {M, K, K};
+  hipStream_t s1 = (hipStream_t)tnet_stream(), s2;
+  CK(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
+  hipEvent_t a, b;
+  CK(hipEventCreate(&a));
+  CK(hipEventCreate(&b));
+  const char* names[] = {"grad+bias 1024x2048 -> 2048x2048 (128x128)", "bwd+dsig+slabs 1024x2048 x 2048x2048^T (64x128)",
+                         "fwd+bias+sigmoid 1024x2048 x 2048x2048 (64x128)"};
+  auto run = [&](int which) {
+    for (int i = 0; i < reps; ++i) {
+      if (which == 0) CT(tnet_affine_grad_bias(X, dX, E, dE, G, dG, P, N, gb, s1));
+      else if (which == 1) CT(tnet_affine_bwd_colsum(E, dE, W, dW, Y, K, X, dX, P, K, s1));
+      else CT(tnet_affine_fwd(X, dX, W, dW, bias, Y, dY, 1, s1));
+    }
+  };
+  auto timed = [&](int which) {
+    float ms = 0.f;
+    CK(hipEventRecord(a, s1));
+    run(which);
+    CK(hipEventRecord(b, s1));
+    CK(hipEventSynchronize(b));
+    CK(hipEventElapsedTime(&ms, a, b));
+    return ms;
+  };
+  const char* modes[] = {"auto+rsv0", "auto+rsv8", "auto+rsv16"};
+  for (int which = 0; which < 3; ++which)
+    for (const char* mode : modes) {
+      CT(tnet_gemm_config(mode));
+      run(which);
+      CK(hipStreamSynchronize(s1));
+      const float alone = timed(which);
+      const long ticks = (long)(alone * 4.0f * 1e5f) + 20000;
+      occupier<512><<<nocc, 512, 0, s2>>>(junk, ticks);
+      CK(hipGetLastError());
+      std::this_thread::sleep_for(std::chrono::microseconds(200));
+      const float occ = timed(which);
+      CK(hipStreamSynchronize(s2));
+      printf("%-50s %-9s: alone %.1f us; beside %d RCCL-footprint occupiers (512 thr, 37.6 KB, 256 VGPR): %.1f us "
+             "(x%.2f)\n", names[which], mode, 1e3f * alone / reps, nocc, 1e3f * occ / reps, occ / alone);
+      fflush(stdout);
+    }
+  CT(tnet_gemm_config("auto+rsv0"));
+  return 0;
+}
+
 int main(int argc, char** argv) {
+  if (argc > 1 && !strcmp(argv[1], "steal")) return steal_probe(argc > 2 ? atoi(argv[2]) : 8);
   const int nocc = argc > 1 ? atoi(argv[1]) : 32;
   const int M = 1024, K = 2048, N = 2048, reps = 20;
   CT(tnet_select_gpu(0));
