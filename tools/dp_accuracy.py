@@ -81,7 +81,8 @@ def worker(a):
     lr = a.lr * (world if a.scale == "linear" else world ** 0.5)
     net.set_learn_rate(lr)
     net.set_grad_div_frm(True)
-    nb = newbob.Newbob(repr(lr), a.bunch, max_iter=a.epochs, end_halving_inc=a.end_halving_inc) if a.newbob else None
+    nb = newbob.Newbob(repr(lr), a.bunch, max_iter=a.epochs, end_halving_inc=a.end_halving_inc,
+                       start_halving_inc=a.start_halving_inc) if a.newbob else None
     best = None
     log = []
     t0 = time.time()
@@ -149,6 +150,7 @@ def worker(a):
     if rank == 0:
         print("RESULT " + json.dumps({"world": world, "lr": lr, "lr_scaling": a.scale, "newbob": a.newbob,
                                       "warmup": a.warmup, "end_halving_inc": a.end_halving_inc,
+                                      "start_halving_inc": a.start_halving_inc,
                                       "bunch_per_rank": a.bunch,
                                       "global_bunch": a.bunch * world, "epochs": log,
                                       "wall_s": round(time.time() - t0, 1)}), flush=True)
@@ -176,6 +178,7 @@ def main():
     ap.add_argument("--scale", default="linear", choices=["linear", "sqrt"], help="lr_N = lr_1 N or lr_1 sqrt(N)")
     ap.add_argument("--newbob", action="store_true")
     ap.add_argument("--end-halving-inc", type=float, default=0.1)
+    ap.add_argument("--start-halving-inc", type=float, default=0.5)
     ap.add_argument("--warmup", type=float, default=0.0)
     ap.add_argument("--progress", default="", help="rank 0 appends one JSON line per epoch to this file")
     a = ap.parse_args()
@@ -188,7 +191,8 @@ def main():
                    OMP_NUM_THREADS="2")
         args = [sys.executable, os.path.abspath(__file__), "worker", "--epochs", str(a.epochs), "--utts",
                 str(a.utts), "--cv-utts", str(a.cv_utts), "--bunch", str(a.bunch), "--cache", str(a.cache), "--lr",
-                str(a.lr), "--scale", a.scale, "--end-halving-inc", str(a.end_halving_inc), "--warmup", str(a.warmup),
+                str(a.lr), "--scale", a.scale, "--end-halving-inc", str(a.end_halving_inc),
+                "--start-halving-inc", str(a.start_halving_inc), "--warmup", str(a.warmup),
                 "--progress", a.progress]
         if a.newbob:
             args.append("--newbob")
