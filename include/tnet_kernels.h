@@ -291,7 +291,7 @@ int tnet_gemv_rowvec_cat(const float* v0, int K0, const float* v1, int K1, float
  * N <= 4096 (else TNET_ERR_UNSUPPORTED); workspace: tnet_gemv_workspace(K, N) bytes. */
 int tnet_gemv_rowvec_softmax_xent(const float* v, int K, const float* W, int ldw, const float* b, float* z, float* y,
                                   float* e, int N, const int* label, double* stats, void* workspace, void* stream);
-/* ---- the TRecurrentCu frame chain in five launches + the BPTT (CuRecurrentTrainer's fused path) ----
+/* ---- the TRecurrentCu frame chain (CuRecurrentTrainer's fused path) ----
  * [<recurrent> nIn->H, <biasedlinearity> H->N, <softmax>] + cross-entropy, one frame
  * (TRecurrentCu.cc:360-368 over cuRecurrent.cc:16-53 and cuBiasedLinearity.cc:11-64):
  *   tnet_gemv_rowvec_partial : split-K partials of [v0, v1] W (ceil(K/64) x N floats; vout: the
@@ -301,7 +301,18 @@ int tnet_gemv_rowvec_softmax_xent(const float* v, int K, const float* W, int ldw
  *                              and the split-K partials of h Wo (ceil(H/64) x N floats)
  *   tnet_rnn_out_stats       : z = bo + sum of those partials (z may be NULL: not stored) and per 256
  *                              columns the pair {max z, sum exp(z - max)} into smx (2*ceil(N/256) doubles)
- *   tnet_rnn_out_bwd_update  : e = softmax(z) - onehot(*label) formed in place from z and smx; with
+ *   tnet_rnn_out_full        : tnet_rnn_out_partial + tnet_rnn_out_stats in one launch without output
+ *                              partials: every workgroup finishes all of h, then the complete z of 64
+ *                              columns and their pair (2*ceil(N/64) doubles; H <= 2048, N <= 4096, else
+ *                              TNET_ERR_UNSUPPORTED) -- the trainer's path
+ *   tnet_gemv_rowvec_partial_update : tnet_gemv_rowvec_partial with the previous frame's recurrent
+ *                              update (tnet_rnn_update's arguments and arithmetic per element) applied
+ *                              to W as it is read -- the update's own launch folded into the next
+ *                              frame's forward; needs steps < R (the history push must not overwrite a
+ *                              row the update reads) and steps <= 9 (else TNET_ERR_UNSUPPORTED)
+ *   tnet_rnn_out_bwd_update  : e = softmax(z) - onehot(*label) formed in place from z and the `pairs`
+ *                              softmax pairs in smx (<= 64: ceil(N/256) from tnet_rnn_out_stats,
+ *                              ceil(N/64) from tnet_rnn_out_full); with
  *                              train: the output layer's backprop + SGD of tnet_affine_bwd_update_row
  *                              (e_out = Wo e, d = e_out .* h (1 - h)); cross-entropy into stats slot 0;
  *                              the frame's argmax folded into *argkey (zero it first) by atomicMax of
@@ -312,8 +323,14 @@ int tnet_gemv_rowvec_partial(const float* v0, int K0, const float* v1, int K1, f
 int tnet_rnn_out_partial(const float* hpart, int hslices, const float* hb, float* h, int H, const float* Wo, int ldwo,
                          int N, float* opart, void* stream);
 int tnet_rnn_out_stats(const float* opart, int H, int N, const float* bo, float* z, double* smx, void* stream);
-int tnet_rnn_out_bwd_update(const float* z, const double* smx, int N, const int* label, const float* h, int H,
-                            float* Wo, int ldwo, float* corrWo, int ldc, float* bo, float* corr_bo, float scale,
+int tnet_rnn_out_full(const float* hpart, int hslices, const float* hb, float* h, int H, const float* Wo, int ldwo,
+                      int N, const float* bo, float* z, double* smx, void* stream);
+int tnet_gemv_rowvec_partial_update(const float* v0, int K0, const float* v1, int K1, float* vout, float* W, int ldw,
+                                    int N, float* partial, const float* hist, int ldh, int head, int R, const float* D,
+                                    int ldd, int steps, float* b, float* corr_b, float lr, float mmt, float wc,
+                                    void* stream);
+int tnet_rnn_out_bwd_update(const float* z, const double* smx, int pairs, int N, const int* label, const float* h,
+                            int H, float* Wo, int ldwo, float* corrWo, int ldc, float* bo, float* corr_bo, float scale,
                             float mmt, float l2, float* y, float* e, float* e_out, float* d, double* stats,
                             unsigned long long* argkey, int train, void* stream);
 int tnet_argmax_correct(const unsigned long long* keys, const int* labels, int T, int N, double* stats,

@@ -13,14 +13,16 @@ namespace TNet {
 
 void CuRecurrent::BpttOrder(int ord) {
   if (ord < 0) Error("CuRecurrent::BpttOrder: negative order");
+  FlushPendingUpdate();
   mBpttOrder = ord;
-  mInputHistory.Init((size_t)ord + 1, GetNInputs() + GetNOutputs());
+  mInputHistory.Init((size_t)ord + 2, GetNInputs() + GetNOutputs());
   mDiff.Init((size_t)ord + 1, GetNOutputs());
   mDiffTmp.Init(1, GetNOutputs());
   mHead = 0;
 }
 
 void CuRecurrent::ClearHistory() {
+  FlushPendingUpdate();
   mInputHistory.SetZero();
   if (mOutput.MSize() > 0) mOutput.SetZero();
   mHead = 0;
@@ -30,6 +32,7 @@ void CuRecurrent::PropagateFnc(const CuMatrix<BaseFloat>& X, CuMatrix<BaseFloat>
   CuProfileScope p("CuRecurrent::Propagate");
   if (X.Rows() != 1 || Y.Rows() != 1) Error("CuRecurrent: frame-by-frame (one row) propagation only");
   if (mInputHistory.Rows() == 0) Error("Bptt order was not set");
+  FlushPendingUpdate();
   // push back the history: the ring head moves to the row of the oldest entry (cuRecurrent.cc:26-29)
   const int R = (int)mInputHistory.Rows();
   mHead = (mHead + R - 1) % R;
@@ -50,6 +53,19 @@ void CuRecurrent::PropagatePartial(const CuMatrix<BaseFloat>& X, float* part) {
   mOutput.Init(1, GetNOutputs());  // y_{t-1}: kept across frames (no-op when allocated, cumatrix.tcc:20-23)
   const int R = (int)mInputHistory.Rows();
   mHead = (mHead + R - 1) % R;
+  if (mPending) {
+    mPending = false;
+    const int st = tnet_gemv_rowvec_partial_update(
+        X.pCUData(), (int)X.Cols(), mOutput.pCUData(), (int)mOutput.Cols(), mInputHistory.pCURowData((size_t)mHead),
+        mLinearity.pCUData(), (int)mLinearity.Stride(), (int)GetNOutputs(), part, mInputHistory.pCUData(),
+        (int)mInputHistory.Stride(), mPendHead, R, mDiff.pCUData(), (int)mDiff.Stride(), mBpttOrder + 1,
+        mBias.pCUData(), mBiasCorrection.pCUData(), mLearningRate, mMomentum, mWeightcost, S);
+    if (st != TNET_ERR_UNSUPPORTED) {
+      TNET_SAFE_CALL(st);
+      return;
+    }
+    RunUpdate(mPendHead);  // (bptt > 8) on its own, before the forward reads W
+  }
   TNET_SAFE_CALL(tnet_gemv_rowvec_partial(X.pCUData(), (int)X.Cols(), mOutput.pCUData(), (int)mOutput.Cols(),
                                           mInputHistory.pCURowData((size_t)mHead), mLinearity.pCUData(),
                                           (int)mLinearity.Stride(), (int)GetNOutputs(), part, S));
@@ -57,6 +73,7 @@ void CuRecurrent::PropagatePartial(const CuMatrix<BaseFloat>& X, float* part) {
 
 void CuRecurrent::BackpropagateFnc(const CuMatrix<BaseFloat>& X, CuMatrix<BaseFloat>& Y) {
   CuProfileScope p("CuRecurrent::Backpropagate");
+  FlushPendingUpdate();
   // diff = e .* y(1-y) ; Y += W[0:nIn] diff  (OffsetGemv('N', beta = 1.0), cuRecurrent.cc:58-83:
   // the reference accumulates into the persistent error buffer; kept as is)
   mDiffTmp.Init(1, GetNOutputs());
@@ -67,6 +84,7 @@ void CuRecurrent::BackpropagateFnc(const CuMatrix<BaseFloat>& X, CuMatrix<BaseFl
 
 void CuRecurrent::Update() {
   CuProfileScope p("CuRecurrent::Update");
+  FlushPendingUpdate();
   const int nIn = (int)GetNInputs(), nOut = (int)GetNOutputs(), R = (int)mInputHistory.Rows();
   // d_0 = e .* y(1-y) (present frame)
   CuMatrix<BaseFloat> d0;
@@ -75,18 +93,35 @@ void CuRecurrent::Update() {
   UpdateFromDiff0();
 }
 
-void CuRecurrent::UpdateFromDiff0() {
-  const int nIn = (int)GetNInputs(), nOut = (int)GetNOutputs(), R = (int)mInputHistory.Rows();
+void CuRecurrent::UpdateFromDiff0(bool defer) {
+  FlushPendingUpdate();
+  const int nIn = (int)GetNInputs(), nOut = (int)GetNOutputs();
   // BPTT: d_i = (W[nIn:nIn+nOut] d_{i-1}) .* y_{t-i}(1 - y_{t-i}), y_{t-i} = y part of history row i-1
   for (int i = 1; i <= mBpttOrder; i++)
     TNET_SAFE_CALL(tnet_gemv_rows(mLinearity.pCUData(), (int)mLinearity.Stride(), nIn, nOut, nOut,
                                   mDiff.pCURowData((size_t)i - 1), mDiff.pCURowData((size_t)i), 0.0f,
                                   HistRow(i - 1) + nIn, S));
-  // corr = sum_i -lr h_i (x) d_i ; corr += -lr wc W ; W += corr ; bias with momentum (cuRecurrent.cc:88-153)
+  if (defer) {
+    mPending = true;
+    mPendHead = mHead;
+    return;
+  }
+  RunUpdate(mHead);
+}
+
+// corr = sum_i -lr h_i (x) d_i ; corr += -lr wc W ; W += corr ; bias with momentum (cuRecurrent.cc:88-153)
+void CuRecurrent::RunUpdate(int head) {
+  const int nIn = (int)GetNInputs(), nOut = (int)GetNOutputs(), R = (int)mInputHistory.Rows();
   TNET_SAFE_CALL(tnet_rnn_update(mLinearity.pCUData(), (int)mLinearity.Stride(), nIn + nOut, nOut,
-                                 mInputHistory.pCUData(), (int)mInputHistory.Stride(), mHead, R, mDiff.pCUData(),
+                                 mInputHistory.pCUData(), (int)mInputHistory.Stride(), head, R, mDiff.pCUData(),
                                  (int)mDiff.Stride(), mBpttOrder + 1, mBias.pCUData(), mBiasCorrection.pCUData(),
                                  mLearningRate, mMomentum, mWeightcost, S));
+}
+
+void CuRecurrent::FlushPendingUpdate() {
+  if (!mPending) return;
+  mPending = false;
+  RunUpdate(mPendHead);
 }
 
 static uint64_t fbits(float v) {
@@ -119,6 +154,7 @@ void CuRecurrent::ReadFromStream(std::istream& rIn) {
 }
 
 void CuRecurrent::WriteToStream(std::ostream& rOut) {
+  FlushPendingUpdate();
   BfMatrix tmp;
   mLinearity.CopyTo(tmp);
   rOut << BfMatrix(tmp, TRANS);
@@ -236,6 +272,7 @@ std::vector<uint64_t> CuRecurrentTrainer::ChainKey(size_t rows) {
 // advance (ring head, frame count) is set as the recorded run left it.
 void CuRecurrentTrainer::RunFrames(size_t rows) {
   const size_t cols = mFeats.Cols();
+  mUttRows = rows;
   auto eager = [&](size_t f0, size_t f1) {
     for (size_t f = f0; f < f1; f++) {
       CuMatrix<BaseFloat>::MakeView(mRow, mFeats.pCURowData(f), 1, cols, mFeats.Stride());
@@ -359,7 +396,8 @@ bool CuRecurrentTrainer::FusedFrameOk() const {
   if (generic && generic[0] == '1') return false;
   if (mNet->Layers() != 3 || mNet->Layer(0).GetType() != CuComponent::RECURRENT ||
       mNet->Layer(1).GetType() != CuComponent::BIASED_LINEARITY || mNet->Layer(2).GetType() != CuComponent::SOFTMAX ||
-      !dynamic_cast<CuCrossEntropy*>(mObj) || mNet->Layer(2).GetNOutputs() > 4096)
+      !dynamic_cast<CuCrossEntropy*>(mObj) || mNet->Layer(2).GetNOutputs() > 4096 ||
+      mNet->Layer(1).GetNInputs() > 2048)  // tnet_rnn_out_full's limits
     return false;
   if (mCrossval) return true;
   // both layers trained: the stopper is the recurrent layer (its error output is never formed)
@@ -378,30 +416,28 @@ void CuRecurrentTrainer::TrainFrameFused(size_t f) {
   auto& rec = dynamic_cast<CuRecurrent&>(mNet->Layer(0));
   auto& lin = dynamic_cast<CuBiasedLinearity&>(mNet->Layer(1));
   const int nIn = (int)rec.GetNInputs(), H = (int)lin.GetNInputs(), N = (int)lin.GetNOutputs();
-  const int hs = (nIn + H + 63) / 64, os = (H + 63) / 64, G = (N + 255) / 256;
+  const int hs = (nIn + H + 63) / 64, G = (N + 63) / 64;
   mRecPart.Init((size_t)hs, (size_t)H);
-  mOutPart.Init((size_t)os, (size_t)N);
   double* smx = (double*)Scratch(mSmx, mSmxBytes, sizeof(double) * 2 * (size_t)G);
   rec.PropagatePartial(mRow, mRecPart.pCUData());
-  // (the partial kernels address [slices x cols] densely inside these allocations)
+  // (the partial kernel addresses [slices x cols] densely inside this allocation)
   lin.Output().Init(1, (size_t)N);
-  TNET_SAFE_CALL(tnet_rnn_out_partial(mRecPart.pCUData(), hs, rec.Bias().pCUData(), rec.Output().pCUData(), H,
-                                      lin.Linearity().pCUData(), (int)lin.Linearity().Stride(), N,
-                                      mOutPart.pCUData(), S));
-  TNET_SAFE_CALL(tnet_rnn_out_stats(mOutPart.pCUData(), H, N, lin.Bias().pCUData(), lin.Output().pCUData(), smx, S));
+  TNET_SAFE_CALL(tnet_rnn_out_full(mRecPart.pCUData(), hs, rec.Bias().pCUData(), rec.Output().pCUData(), H,
+                                   lin.Linearity().pCUData(), (int)lin.Linearity().Stride(), N, lin.Bias().pCUData(),
+                                   lin.Output().pCUData(), smx, S));
   float scale, l2;
   lin.UpdateConstants(1, &scale, &l2);
   const bool mmt = lin.Momentum() != 0.0f;
   lin.ErrorOutput().Init(1, (size_t)H);
   TNET_SAFE_CALL(tnet_rnn_out_bwd_update(
-      lin.Output().pCUData(), smx, N, mLabels.pCUData() + f, rec.Output().pCUData(), H, lin.Linearity().pCUData(),
+      lin.Output().pCUData(), smx, G, N, mLabels.pCUData() + f, rec.Output().pCUData(), H, lin.Linearity().pCUData(),
       (int)lin.Linearity().Stride(), mmt ? lin.LinearityCorrection().pCUData() : nullptr,
       (int)lin.LinearityCorrection().Stride(), lin.Bias().pCUData(), mmt ? lin.BiasCorrection().pCUData() : nullptr,
       scale, lin.Momentum(), l2, nullptr, nullptr, lin.ErrorOutput().pCUData(), rec.DiffRow0(), mObj->DeviceStats(),
       (unsigned long long*)mArgKey + f, mCrossval ? 0 : 1, S));
   mObj->AddFrames(1);
   if (mCrossval) return;
-  rec.UpdateFromDiff0();
+  rec.UpdateFromDiff0(f + 1 < mUttRows);  // the last frame's update runs on its own: no state leaves the utterance
 }
 
 }  // namespace TNet

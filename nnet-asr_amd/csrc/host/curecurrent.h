@@ -36,15 +36,20 @@ class CuRecurrent : public CuUpdatableComponent {
   void PropagateFnc(const CuMatrix<BaseFloat>& X, CuMatrix<BaseFloat>& Y) override;
   void BackpropagateFnc(const CuMatrix<BaseFloat>& X, CuMatrix<BaseFloat>& Y) override;
   void Update() override;
-  /// Update with d_0 = e .* y(1-y) already in DiffRow0() (written by the fused output-layer kernel)
-  void UpdateFromDiff0();
+  /// Update with d_0 = e .* y(1-y) already in DiffRow0() (written by the fused output-layer kernel).
+  /// defer: the BPTT now, the weight update carried into the next PropagatePartial (its launch folded
+  /// into the next frame's forward, tnet_gemv_rowvec_partial_update); any other use of the layer
+  /// first runs it on its own (FlushPendingUpdate)
+  void UpdateFromDiff0(bool defer = false);
+  void FlushPendingUpdate();
   /// Fused-chain forward, first half: push the history row [x_t, y_{t-1}] and write the split-K
-  /// partials of row W to `part` (tnet_gemv_rowvec_partial); the bias + sigmoid finish is done by
-  /// the output layer's kernel, which stores y_t into GetOutput().
+  /// partials of row W to `part` (tnet_gemv_rowvec_partial, with a deferred update applied); the bias
+  /// + sigmoid finish is done by the output layer's kernel, which stores y_t into GetOutput().
   void PropagatePartial(const CuMatrix<BaseFloat>& X, float* part);
   float* DiffRow0() { return mDiff.pCURowData(0); }
 
-  /// BPTT order; allocates the (ord+1)-row input history (cuRecurrent.h:30-33)
+  /// BPTT order; allocates the input history (cuRecurrent.h:30-33: ord+1 rows; here a ring of ord+2,
+  /// so the next frame's push never lands on a row a deferred update still reads)
   void BpttOrder(int ord);
   int GetBpttOrder() const { return mBpttOrder; }
   /// zero the history and the previous output (cuRecurrent.h:34-39)
@@ -70,11 +75,14 @@ class CuRecurrent : public CuUpdatableComponent {
   }
   CuMatrix<BaseFloat> mLinearity;
   CuVector<BaseFloat> mBias, mBiasCorrection;
-  CuMatrix<BaseFloat> mInputHistory;  // ring of bptt+1 rows [x, y_prev]
+  CuMatrix<BaseFloat> mInputHistory;  // ring of bptt+2 rows [x, y_prev] (the update reads bptt+1)
   CuMatrix<BaseFloat> mDiff;          // [bptt+1 x nOut] back-propagated errors of the present update
   CuMatrix<BaseFloat> mDiffTmp;       // [1 x nOut]
   int mBpttOrder = -1;
   int mHead = 0;
+  bool mPending = false;  // UpdateFromDiff0(defer): the update of the ring at mPendHead not yet applied
+  int mPendHead = 0;
+  void RunUpdate(int head);
 };
 
 /// The TRecurrentCu loop over a network containing <recurrent> layers.
@@ -96,6 +104,7 @@ class CuRecurrentTrainer {
   CuMatrix<BaseFloat> mFeats, mOut, mErr, mRow;
   CuVector<int> mLabels, mLabelRow;
   long mFrames = 0;
+  size_t mUttRows = 0;  // frames of the utterance on the fused chain (the last one's update is not deferred)
   // fused-chain scratch: recurrent / output split-K partials, softmax pairs, per-frame argmax keys
   CuMatrix<BaseFloat> mRecPart, mOutPart;
   void* mSmx = nullptr;

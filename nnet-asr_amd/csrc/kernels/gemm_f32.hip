@@ -1699,6 +1699,26 @@ void gemm16_sk_kernel(const GemmP p, const int G) {
   }
 }
 
+// Split-K in two over 2T workgroups (tiles too few for the CUs, K long): the two k-halves of a tile are
+// two pieces of gemm16_body's stream-K fixup -- the first to finish stores its accumulators, the second
+// adds them and runs the tile's own fused epilogue (no second launch, no slice workspace pass over the
+// whole output).  Workgroups b are mapped XCD by XCD (the body's bijective remap over 2T), so a tile's
+// two pieces are neighbours on one XCD and start together.
+template <int BM, int BN, bool A_KC, bool B_KC, int EPI, bool PX>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
+void gemm16_split2_kernel(const GemmP p) {
+  __shared__ __attribute__((aligned(16))) float smem[gemm16_smem_floats<BM, BN, 64, 2, EPI, PX>()];
+  const int nwg = gridDim.x, b = blockIdx.x, xcd = b & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int v = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (b >> 3);
+  GemmP q = p;
+  const long kk = (long)(v & 1) * (p.K / 2);
+  q.A = p.A + (A_KC ? kk : kk * p.lda);
+  q.B = p.B + (B_KC ? kk : kk * p.ldb);
+  q.K = p.K / 2;
+  q.ksplit = 2;
+  gemm16_body<BM, BN, 64, 2, 2, 2, 0, A_KC, B_KC, kEpiStreamK + EPI, PX>(q, smem, v >> 1);
+}
+
 template <int BM, int BN, int BK, int WM, int WN, int S, int SP, bool A_KC, bool B_KC, int EPI_T, bool PX = false>
 __global__ __launch_bounds__((WM * WN + (SP == 2)) * 64)
 __attribute__((amdgpu_waves_per_eu((WM * WN + (SP == 2) + 3) / 4, (WM * WN + (SP == 2) + 3) / 4)))
@@ -2100,6 +2120,38 @@ static bool launch_sk(const GemmP& p, hipStream_t st) {
   }
 }
 
+// gemm16_split2_kernel for the update GEMMs whose 64x128 tiles are too few for the CUs (the first
+// layer's 440 x 2048 over K = 1024: 112 tiles -> 224 pieces of K = 512).  Opt-in (TNET_GEMM_SPLIT2=1):
+// MEASURED SLOWER on MI355X (tools/gemm_sweep.py, round 3): 28.3 vs 24.5 us with the bias SGD, 27.4 vs
+// 22.8 us without -- the update's m-contiguous A in 64-row tiles reads its fragments 8 B per lane, and
+// 8 k-tiles per piece leave the prologue / epilogue unamortised.  false: not applicable
+static int g_split2 = -1;
+template <bool A_KC, bool B_KC, int EPI>
+static bool launch_split2(const GemmP& p, hipStream_t st) {
+  if (g_split2 < 0) g_split2 = getenv("TNET_GEMM_SPLIT2") ? atoi(getenv("TNET_GEMM_SPLIT2")) : 0;
+  constexpr bool OK = !A_KC && !B_KC && (EPI == EPI_SGD_B || EPI == EPI_SGD || EPI == EPI_STORE_BG || EPI == EPI_STORE);
+  if constexpr (!OK) {
+    return false;
+  } else {
+    if (!g_split2 || forced_cfg() >= 0 || g_split > 0) return false;
+    const long T = (long)cdiv(p.M, 64) * cdiv(p.N, 128);
+    if (T < 90 || T > 160 || p.K % 128 || p.K < 512 || p.N % 128) return false;
+    const long extA = 64L * p.lda + p.M, extB = 64L * p.ldb + p.N;
+    if (4 * extA >= (1L << 32) || 4 * extB >= (1L << 32)) return false;
+    float* ws = splitk_workspace(sizeof(float) * (size_t)T * 64 * 128, st);
+    unsigned* cnt = ws ? splitk_counters((size_t)T, st) : nullptr;
+    if (!cnt) return false;
+    GemmP q = p;
+    q.group = g_group > 0 ? g_group : 8;
+    q.early_issue = g_early;
+    q.wt = g_wt;
+    q.skws = ws;
+    q.tile_cnt = cnt;
+    gemm16_split2_kernel<64, 128, A_KC, B_KC, EPI, false><<<(unsigned)(2 * T), 256, 0, st>>>(q);
+    return true;
+  }
+}
+
 // split-K: the K range is cut into ks slices (blockIdx.y) whose raw products A B go to the stream's
 // workspace (slice z at ws + z * slab, rows of ldp = N rounded up to 4 floats); then either the
 // tile's last slice combines them inside the launch (tile counters; 64x64 and 32x64 tiles) or
@@ -2264,9 +2316,13 @@ static int launch_gemm(const GemmP& p_in, hipStream_t st) {
   static const int noload = getenv("TNET_GEMM_DIAG") ? atoi(getenv("TNET_GEMM_DIAG")) : 0;
   GemmP p = p_in;
   p.diag_noload = noload;
+  p.group = g_group > 0 ? g_group : 8;
+  if (launch_split2<A_KC, B_KC, EPI>(p, st)) {
+    TNET_LAUNCH_CHECK();
+    return TNET_OK;
+  }
   const GemmPlan pl = plan_gemm<A_KC>(p, epi_splittable(EPI));
   const int cfg = pl.cfg;
-  p.group = g_group > 0 ? g_group : 8;
   if (pl.ks > 1) return launch_splitk<A_KC, B_KC, EPI>(p, cfg, pl.ks, st);
   bool sk_done = false;
   if (cfg == CFG_m64x128k64s2) sk_done = launch_sk<64, 128, A_KC, B_KC, EPI>(p, st);
@@ -2608,9 +2664,10 @@ extern "C" int tnet_gemm_config(const char* name) {
   // il2: in-launch whatever their size; in-launch only for 64x64 / 32x64 tiles, other tiles always
   // combine in a second launch); the combine mode stays as set until the next il suffix.
   // "+rsv<R>": R CUs reserved (gemm16_sk_kernel over CUs - R workgroups for the data-parallel shapes),
-  // 0 none -- as tnet_gemm_reserve, stays as set until changed
+  // 0 none -- as tnet_gemm_reserve, stays as set until changed; "+s2<0|1>": gemm16_split2_kernel for the
+  // few-tile updates off / on (TNET_GEMM_SPLIT2), stays as set
   char base[64] = "auto";
-  int split = -1, inl = -1, rsv = -1;
+  int split = -1, inl = -1, rsv = -1, s2 = -1;
   if (name) {
     const char* plus = strchr(name, '+');
     const size_t n = plus ? (size_t)(plus - name) : strlen(name);
@@ -2621,6 +2678,7 @@ extern "C" int tnet_gemm_config(const char* name) {
       if (!strncmp(plus, "+sk", 3) && atoi(plus + 3) >= 1) split = atoi(plus + 3);
       else if (!strncmp(plus, "+il", 3) && plus[3] >= '0' && plus[3] <= '2') inl = plus[3] - '0';
       else if (!strncmp(plus, "+rsv", 4) && plus[4] >= '0' && plus[4] <= '9') rsv = atoi(plus + 4);
+      else if (!strncmp(plus, "+s2", 3) && (plus[3] == '0' || plus[3] == '1')) s2 = plus[3] - '0';
       else return TNET_ERR_ARG;
       plus = strchr(plus + 1, '+');
     }
@@ -2634,6 +2692,7 @@ extern "C" int tnet_gemm_config(const char* name) {
   g_split = split;
   if (inl >= 0) g_inlaunch = inl;
   if (rsv >= 0) g_reserve = rsv;
+  if (s2 >= 0) g_split2 = s2;
   return TNET_OK;
 }
 

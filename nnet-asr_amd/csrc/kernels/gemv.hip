@@ -18,25 +18,109 @@ namespace tnetk {
 
 constexpr int GV_KSLICE = 64;  // k rows per split-K slice
 
+// The recurrent update of the previous frame (rnn_update_kernel's arithmetic) carried into the next
+// frame's forward: every W element is updated by the workgroup that reads it next (below)
+struct RnnPendingUpdate {
+  const float* hist;  // the history ring [R x ldh] at the update's head
+  long ldh;
+  int head, R;
+  const float* D;  // [steps x ldd] back-propagated errors d_0..d_{steps-1}
+  long ldd;
+  int steps;       // = the kernel's ST
+  float* b;
+  float* cb;
+  float lr, mmt, wc;
+};
+constexpr int GV_UPD_MAX = 9;  // steps = bptt + 1 of the folded form (deeper: the update's own launch)
+
 // partial[s][c] = sum_{k in slice s} v[k] * W[k][c], v = [v0[0:K0], v1[0:K-K0]] (the recurrent
 // layer's [x_t, y_{t-1}], read in place); the column-block-0 workgroups also store v to vout (the
-// history row, cuRecurrent.cc:31-35), so the two row copies need no launches of their own
-__global__ __launch_bounds__(256) void gemv_rowvec_partial(const float* __restrict__ v0, int K0,
-                                                           const float* __restrict__ v1, int K,
-                                                           const float* __restrict__ W, long ldw, int N,
-                                                           float* __restrict__ partial, float* __restrict__ vout) {
+// history row, cuRecurrent.cc:31-35), so the two row copies need no launches of their own.
+// UPD: the previous frame's recurrent update first (cuRecurrent.cc:88-153; per element exactly
+// rnn_update_kernel's sum in step order, corr = (-lr wc) w + acc, w = corr + w), written back and used
+// for this frame's product -- the update needs no launch of its own (every element of W is read by
+// exactly one workgroup here); the k-slice-0 workgroups update the bias.  The ring must not hand vout
+// a row the update reads (R >= steps + 1: CuRecurrent keeps bptt + 2 rows).
+template <bool UPD, int ST = 1>
+__global__ __launch_bounds__(256) void gemv_rowvec_partial_k(const float* __restrict__ v0, int K0,
+                                                             const float* __restrict__ v1, int K,
+                                                             float* __restrict__ W, long ldw, int N,
+                                                             float* __restrict__ partial, float* __restrict__ vout,
+                                                             RnnPendingUpdate u) {
   __shared__ float red[4][64];
+  __shared__ float hsl[UPD ? ST * GV_KSLICE : 1];  // the update's history values of this k-slice
+  constexpr int KPW = GV_KSLICE / 4;                       // k rows per wave
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + lane;
+  const int c = blockIdx.x * 64 + lane, cc = min(c, N - 1);
   const int k0 = blockIdx.y * GV_KSLICE, k1 = min(K, k0 + GV_KSLICE);
   auto vk = [&](int k) { return k < K0 ? v0[k] : v1[k - K0]; };
+  // every load of the workgroup in one round: the wave's KPW rows of W, the row vector, (UPD) the
+  // errors of column c and the slice's history rows
+  float wv[KPW], xv[KPW];
+#pragma unroll
+  for (int q = 0; q < KPW; ++q) {
+    const int k = min(k0 + w + 4 * q, K - 1);
+    wv[q] = W[(long)k * ldw + cc];
+    xv[q] = vk(k);
+  }
+  float acc = 0.f;
+  if constexpr (UPD) {
+    // (one round of loads: every value the update needs is requested before the first is used --
+    // the bias operands too, whose pointers the compiler cannot prove apart from W / cb)
+    // unconditional loads at clamped indices (a predicated load is a branch here, and the branches
+    // serialise the round); ST steps at compile time: straight-line code, the LDS reads batched
+    float dv[ST];
+#pragma unroll
+    for (int i = 0; i < ST; ++i) dv[i] = u.D[(long)i * u.ldd + cc];
+    constexpr int HPT = (ST * GV_KSLICE + 255) / 256;  // history values per thread
+    float hl[HPT];
+#pragma unroll
+    for (int q = 0; q < HPT; ++q) {
+      const int j = min((int)threadIdx.x + 256 * q, ST * GV_KSLICE - 1), i = j / GV_KSLICE;
+      const int k = min(k0 + j % GV_KSLICE, K - 1);
+      int r = u.head + i;
+      r = r >= u.R ? r - u.R : r;
+      hl[q] = u.hist[(long)r * u.ldh + k];
+    }
+    const bool bias = blockIdx.y == 0 && w == 0 && c < N;  // rnn_update_kernel's bias row
+    const float cbv = u.cb[cc], bv = u.b[cc];
+#pragma unroll
+    for (int q = 0; q < HPT; ++q)
+      if (threadIdx.x + 256 * q < ST * GV_KSLICE) hsl[threadIdx.x + 256 * q] = hl[q];
+    if (bias) {
+      float g = __fmaf_rn(-u.lr, dv[0], u.mmt * cbv);
+#pragma unroll
+      for (int i = 1; i < ST; ++i) g = __fmaf_rn(-u.lr, dv[i], g);
+      u.cb[c] = g;
+      u.b[c] = g + bv;
+    }
+    __syncthreads();
+    float hv[KPW][ST];
+#pragma unroll
+    for (int q = 0; q < KPW; ++q)
+#pragma unroll
+      for (int i = 0; i < ST; ++i) hv[q][i] = hsl[i * GV_KSLICE + w + 4 * q];
+#pragma unroll
+    for (int q = 0; q < KPW; ++q) {
+      const int k = k0 + w + 4 * q;
+      float a = 0.f;
+#pragma unroll
+      for (int i = 0; i < ST; ++i) a = __fmaf_rn(-u.lr * hv[q][i], dv[i], a);
+      const float corr = __fmaf_rn(-u.lr * u.wc, wv[q], a);
+      const float wn = corr + wv[q];
+      if (k < k1 && c < N) {
+        W[(long)k * ldw + c] = wn;
+        acc += xv[q] * wn;
+      }
+    }
+  } else {
+#pragma unroll
+    for (int q = 0; q < KPW; ++q)
+      if (k0 + w + 4 * q < k1) acc += xv[q] * wv[q];
+  }
+  // the history push after the update's reads of the ring (a different row: R >= steps + 1)
   if (vout && blockIdx.x == 0)
     for (int k = k0 + threadIdx.x; k < k1; k += blockDim.x) vout[k] = vk(k);
-  float acc = 0.f;
-  if (c < N) {
-#pragma unroll 4
-    for (int k = k0 + w; k < k1; k += 4) acc += vk(k) * W[(long)k * ldw + c];
-  }
   red[w][lane] = acc;
   __syncthreads();
   if (w == 0 && c < N) partial[(long)blockIdx.y * N + c] = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
@@ -141,7 +225,9 @@ __global__ __launch_bounds__(256) void gemv_softmax_xent_final(const float* __re
   }
 }
 
-// y[r] = beta*y[r] + dot(W[r0 + r, 0:n], x) ; then if s != NULL: y[r] *= s[r] (1 - s[r])
+// y[r] = beta*y[r] + dot(W[r0 + r, 0:n], x) ; then if s != NULL: y[r] *= s[r] (1 - s[r]).
+// Rows of <= 1024 aligned floats: every load of the wave (the row, x, s[r], y[r]) issued in one round
+// at clamped addresses, the products then added in the loop form's order (c = 4 lane + 256 q)
 __global__ __launch_bounds__(256) void gemv_rows_kernel(const float* __restrict__ W, long ldw, int r0, int nrows,
                                                         int n, const float* __restrict__ x, float* __restrict__ y,
                                                         float beta, const float* __restrict__ s) {
@@ -149,19 +235,34 @@ __global__ __launch_bounds__(256) void gemv_rows_kernel(const float* __restrict_
   const int r = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   if (r >= nrows) return;
   const float* row = W + (long)(r0 + r) * ldw;
+  const float sv = s ? s[r] : 0.f;
+  const float yv = beta != 0.f ? y[r] : 0.f;
   float acc = 0.f;
   if ((n & 3) == 0 && (ldw & 3) == 0 && (((uintptr_t)row | (uintptr_t)x) & 15) == 0) {
-    for (int c = lane * 4; c < n; c += 256) {
-      const f32x4 a = *reinterpret_cast<const f32x4*>(row + c), b = *reinterpret_cast<const f32x4*>(x + c);
-      acc += a[0] * b[0] + a[1] * b[1] + a[2] * b[2] + a[3] * b[3];
+    if (n <= 1024) {
+      f32x4 a[4], b[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int c = min(lane * 4 + 256 * q, n - 4);
+        a[q] = *reinterpret_cast<const f32x4*>(row + c);
+        b[q] = *reinterpret_cast<const f32x4*>(x + c);
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (lane * 4 + 256 * q < n) acc += a[q][0] * b[q][0] + a[q][1] * b[q][1] + a[q][2] * b[q][2] + a[q][3] * b[q][3];
+    } else {
+      for (int c = lane * 4; c < n; c += 256) {
+        const f32x4 a = *reinterpret_cast<const f32x4*>(row + c), b = *reinterpret_cast<const f32x4*>(x + c);
+        acc += a[0] * b[0] + a[1] * b[1] + a[2] * b[2] + a[3] * b[3];
+      }
     }
   } else {
     for (int c = lane; c < n; c += 64) acc += row[c] * x[c];
   }
   acc = wave_sum(acc);
   if (lane == 0) {
-    float o = beta == 0.f ? acc : beta * y[r] + acc;
-    if (s) o = o * (s[r] * (1.f - s[r]));
+    float o = beta == 0.f ? acc : beta * yv + acc;
+    if (s) o = o * (sv * (1.f - sv));
     y[r] = o;
   }
 }
@@ -179,9 +280,9 @@ __global__ __launch_bounds__(256) void rnn_update_kernel(float* __restrict__ W, 
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   const int k = blockIdx.y;
   if (c >= nout) return;
-  if (k == rows) {  // bias
-    float g = -lr * D[c] + mmt * cb[c];
-    for (int i = 1; i < steps; ++i) g = -lr * D[(long)i * ldd + c] + g;
+  if (k == rows) {  // bias (explicit fused multiply-adds: the same rounding in the folded form below)
+    float g = __fmaf_rn(-lr, D[c], mmt * cb[c]);
+    for (int i = 1; i < steps; ++i) g = __fmaf_rn(-lr, D[(long)i * ldd + c], g);
     cb[c] = g;
     b[c] = g + b[c];
     return;
@@ -199,9 +300,9 @@ __global__ __launch_bounds__(256) void rnn_update_kernel(float* __restrict__ W, 
     }
 #pragma unroll
     for (int q = 0; q < 8; ++q)
-      if (i0 + q < steps) acc += (-lr * hv[q]) * dv[q];
+      if (i0 + q < steps) acc = __fmaf_rn(-lr * hv[q], dv[q], acc);
   }
-  const float corr = (-lr * wc) * w + acc;
+  const float corr = __fmaf_rn(-lr * wc, w, acc);
   *wp = corr + w;
 }
 
@@ -386,20 +487,82 @@ __global__ __launch_bounds__(256) void rnn_out_stats_kernel(const float* __restr
   }
 }
 
-// the softmax normaliser from the stats workgroups' pairs: M = max m_g, S = sum s_g exp(m_g - M);
-// every wave loads the G <= 64 pairs in one pass (lane g) and reduces them itself
-__device__ __forceinline__ void rnn_softmax_norm(const double* __restrict__ smx, int G, float* M, float* rsum) {
-  const int lane = threadIdx.x & 63;
-  const float mg = lane < G ? (float)smx[2 * lane] : -1e30f;
-  const double sg = lane < G ? smx[2 * lane + 1] : 0.0;
-  const float m = wave_max(mg);
-  const double s = wave_sum_d(lane < G ? sg * (double)fast_exp(mg - m) : 0.0);
-  *M = m;
-  *rsum = 1.f / (float)s;
+// The output side's first two launches in one: every workgroup finishes ALL of h (the recurrent
+// sigmoid from the split-K partials, rnn_out_partial_kernel's order; workgroup 0 stores it), then the
+// complete z of its 64 columns -- 16 waves over interleaved k (wave w: k = w, w + 16, ...; 32 loads
+// of Wo in flight per lane at H = 512), wave sums added in wave order -- and the pair {max z, sum
+// exp(z - max)} of those columns (rnn_out_stats_kernel's arithmetic per 64 instead of 256 columns).
+// No output partials, no stats launch: ceil(N / 64) <= 64 pairs for rnn_out_bwd_kernel.
+constexpr int GV_FULL_MAXH = 2048;
+__global__ __launch_bounds__(1024) void rnn_out_full_kernel(const float* __restrict__ hpart, int hslices,
+                                                            const float* __restrict__ hb, float* __restrict__ h,
+                                                            int H, const float* __restrict__ Wo, long ldw, int N,
+                                                            const float* __restrict__ bo, float* __restrict__ z,
+                                                            double* __restrict__ smx) {
+  __shared__ float hs[GV_FULL_MAXH];
+  __shared__ float red[16][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane, cc = min(c, N - 1);
+  // the first 32 rows per lane of the column block's Wo issued before the h finish (their latency
+  // overlaps the partial-sum loads)
+  float wv[32];
+#pragma unroll
+  for (int q = 0; q < 32; ++q) {
+    const int k = w + 16 * q;
+    wv[q] = k < H ? Wo[(long)k * ldw + cc] : 0.f;
+  }
+  for (int k = threadIdx.x; k < H; k += 1024) {
+    float sacc = 0.f;
+    for (int q0 = 0; q0 < hslices; q0 += 16) {  // 16 slices' loads in flight, added in slice order
+      float p[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) p[q] = q0 + q < hslices ? hpart[(long)(q0 + q) * H + k] : 0.f;
+#pragma unroll
+      for (int q = 0; q < 16; ++q)
+        if (q0 + q < hslices) sacc += p[q];
+    }
+    const float hv = sigmoidf_ref((hb ? hb[k] : 0.f) + sacc);
+    hs[k] = hv;
+    if (blockIdx.x == 0) h[k] = hv;
+  }
+  __syncthreads();
+  float acc = 0.f;
+  for (int k0 = w; k0 < H; k0 += 16 * 32) {  // 32 rows of Wo per lane in flight
+    if (k0 != w) {
+#pragma unroll
+      for (int q = 0; q < 32; ++q) {
+        const int k = k0 + 16 * q;
+        wv[q] = k < H ? Wo[(long)k * ldw + cc] : 0.f;
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 32; ++q) {
+      const int k = k0 + 16 * q;
+      if (k < H) acc += hs[k] * wv[q];
+    }
+  }
+  red[w][lane] = acc;
+  __syncthreads();
+  if (w == 0) {
+    float t = red[0][lane];
+#pragma unroll
+    for (int q = 1; q < 16; ++q) t += red[q][lane];
+    const float a = c < N ? (bo ? bo[c] : 0.f) + t : -1e30f;
+    if (z && c < N) z[c] = a;
+    const float m = wave_max(a);
+    const double ws = wave_sum_d(c < N ? (double)fast_exp(a - m) : 0.0);
+    if (lane == 0) {
+      smx[2 * blockIdx.x] = (double)m;
+      smx[2 * blockIdx.x + 1] = ws;
+    }
+  }
 }
 
 // WPR waves per weight row (1: rows of <= 1024 columns, a wave each; 4: a workgroup per row, so a
-// 4000-column row has its 16 KB of W in flight at once and the row sums meet in LDS in wave order)
+// 4000-column row has its 16 KB of W in flight at once and the row sums meet in LDS in wave order).
+// Every load of a workgroup goes out in one round before the first is used -- the softmax pairs, the
+// label, h_i, and (rows of <= 4 passes) the whole row of W, z and the momentum row at clamped addresses
+// -- then the arithmetic in the per-pass order of the loop form.
 template <int WPR>
 __global__ __launch_bounds__(256) void rnn_out_bwd_kernel(
     const float* __restrict__ z, const double* __restrict__ smx, int G, const int* __restrict__ label,
@@ -409,16 +572,25 @@ __global__ __launch_bounds__(256) void rnn_out_bwd_kernel(
     double* __restrict__ stats, unsigned long long* __restrict__ argkey, int row_blocks, int train) {
   __shared__ ArgMax sarg[4];
   __shared__ float racc[4];
-  float M, rsum;
-  rnn_softmax_norm(smx, G, &M, &rsum);
-  const int t0 = label[0];
-  const int t = t0 < n_out ? t0 : -1;  // out of range: an unlabeled frame, as the batched kernels
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  // the softmax normaliser from the pairs {m_g, s_g}: M = max m_g, S = sum s_g exp(m_g - M), every wave
+  // reducing the G <= 64 pairs itself (lane g); their loads and the label's go out with the rest
+  const int gl = min(lane, G - 1);  // clamped, unconditional: no branch between the loads
+  const double mg_raw = smx[2 * gl], sg_raw = smx[2 * gl + 1];
+  const int t0 = label[0];
+  const float mg = lane < G ? (float)mg_raw : -1e30f;
+  const double sg = lane < G ? sg_raw : 0.0;
   if ((int)blockIdx.x >= row_blocks) {  // bias / statistics workgroups: 256 columns each
     const int j = (blockIdx.x - row_blocks) * blockDim.x + threadIdx.x;
+    const int jj = min(j, n_out - 1);
+    const float zj = z[jj];
+    const float cbj = (train && cb) ? cb[jj] : 0.f, bj = train ? b[jj] : 0.f;
+    const float M = wave_max(mg);
+    const float rsum = 1.f / (float)wave_sum_d(lane < G ? sg * (double)fast_exp(mg - M) : 0.0);
+    const int t = t0 < n_out ? t0 : -1;  // out of range: an unlabeled frame, as the batched kernels
     ArgMax ay{-1e20f, 0x7fffffff};
     if (j < n_out) {
-      const float yj = fast_exp(z[j] - M) * rsum;
+      const float yj = fast_exp(zj - M) * rsum;
       const float ej = yj - (j == t ? 1.f : 0.f);
       ay.v = yj;
       ay.i = j;
@@ -428,10 +600,10 @@ __global__ __launch_bounds__(256) void rnn_out_bwd_kernel(
       if (train) {
         float g = ej;
         if (cb) {
-          g = g + mmt * cb[j];
+          g = g + mmt * cbj;
           cb[j] = g;
         }
-        b[j] = b[j] + scale * g;
+        b[j] = bj + scale * g;
       }
     }
     ay = wave_argmax(ay);
@@ -465,27 +637,59 @@ __global__ __launch_bounds__(256) void rnn_out_bwd_kernel(
     w = w + scale * c;
     return w + l2 * w;
   };
-  auto err = [&](int c, float zc) { return fast_exp(zc - M) * rsum - (c == t ? 1.f : 0.f); };
+  constexpr int STEP = 256 * WPR;  // floats per pass of the row's waves
+  constexpr int NP = 4;            // passes held in registers (n_out <= 4 STEP)
+  const bool vec = (n_out & 3) == 0 && (ldw & 3) == 0 && (!qrow || (ldc & 3) == 0) &&
+                   (((uintptr_t)row | (uintptr_t)z | (uintptr_t)qrow) & 15) == 0;
   float acc = 0.f;
-  if (live) {
-    if ((n_out & 3) == 0 && (ldw & 3) == 0 && (!qrow || (ldc & 3) == 0) &&
-        (((uintptr_t)row | (uintptr_t)z | (uintptr_t)qrow) & 15) == 0) {
-      constexpr int STEP = 256 * WPR;  // floats per pass of the row's waves
+  if (vec && n_out <= NP * STEP) {
+    f32x4 a[NP], zv[NP], qv[NP];
+    const float* qsrc = qrow ? qrow : row;  // unconditional (no branch in the round); unused without momentum
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+      const int c = min((sub * 64 + lane) * 4 + p * STEP, n_out - 4);
+      a[p] = *reinterpret_cast<const f32x4*>(row + c);
+      zv[p] = *reinterpret_cast<const f32x4*>(z + c);
+      qv[p] = *reinterpret_cast<const f32x4*>(qsrc + c);
+    }
+    const float M = wave_max(mg);
+    const float rsum = 1.f / (float)wave_sum_d(lane < G ? sg * (double)fast_exp(mg - M) : 0.0);
+    const int t = t0 < n_out ? t0 : -1;
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+      const int c = (sub * 64 + lane) * 4 + p * STEP;
+      if (!live || c >= n_out) continue;
+      float ev[4], q[4] = {qv[p][0], qv[p][1], qv[p][2], qv[p][3]};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) ev[k] = fast_exp(zv[p][k] - M) * rsum - (c + k == t ? 1.f : 0.f);
+      f32x4 w4 = a[p];
+      acc += w4[0] * ev[0] + w4[1] * ev[1] + w4[2] * ev[2] + w4[3] * ev[3];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) w4[k] = upd(w4[k], ev[k], &q[k]);
+      *reinterpret_cast<f32x4*>(row + c) = w4;
+      if (qrow) *reinterpret_cast<f32x4*>(qrow + c) = f32x4{q[0], q[1], q[2], q[3]};
+    }
+  } else {
+    const float M = wave_max(mg);
+    const float rsum = 1.f / (float)wave_sum_d(lane < G ? sg * (double)fast_exp(mg - M) : 0.0);
+    const int t = t0 < n_out ? t0 : -1;
+    auto err = [&](int c, float zc) { return fast_exp(zc - M) * rsum - (c == t ? 1.f : 0.f); };
+    if (live && vec) {
 #pragma unroll 2
       for (int c = (sub * 64 + lane) * 4; c < n_out; c += STEP) {
         f32x4 a = *reinterpret_cast<const f32x4*>(row + c);
-        const f32x4 zv = *reinterpret_cast<const f32x4*>(z + c);
-        f32x4 qv = qrow ? *reinterpret_cast<const f32x4*>(qrow + c) : f32x4{0.f, 0.f, 0.f, 0.f};
-        float ev[4], q[4] = {qv[0], qv[1], qv[2], qv[3]};
+        const f32x4 z4 = *reinterpret_cast<const f32x4*>(z + c);
+        f32x4 q4 = qrow ? *reinterpret_cast<const f32x4*>(qrow + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+        float ev[4], q[4] = {q4[0], q4[1], q4[2], q4[3]};
 #pragma unroll
-        for (int k = 0; k < 4; ++k) ev[k] = err(c + k, zv[k]);
+        for (int k = 0; k < 4; ++k) ev[k] = err(c + k, z4[k]);
         acc += a[0] * ev[0] + a[1] * ev[1] + a[2] * ev[2] + a[3] * ev[3];
 #pragma unroll
         for (int k = 0; k < 4; ++k) a[k] = upd(a[k], ev[k], &q[k]);
         *reinterpret_cast<f32x4*>(row + c) = a;
         if (qrow) *reinterpret_cast<f32x4*>(qrow + c) = f32x4{q[0], q[1], q[2], q[3]};
       }
-    } else {
+    } else if (live) {
       for (int c = sub * 64 + lane; c < n_out; c += 64 * WPR) {
         const float w = row[c], ej = err(c, z[c]);
         acc += w * ej;
@@ -531,8 +735,8 @@ extern "C" int tnet_gemv_rowvec_partial(const float* v0, int K0, const float* v1
   const int K = K0 + K1;
   if (K0 < 0 || K1 < 0 || K <= 0 || N <= 0 || ldw < N || (K0 && !v0) || (K1 && !v1) || !W || !partial)
     return TNET_ERR_ARG;
-  gemv_rowvec_partial<<<dim3(cdiv(N, 64), cdiv(K, GV_KSLICE)), 256, 0, (hipStream_t)stream>>>(v0, K0, v1, K, W, ldw,
-                                                                                                N, partial, vout);
+  gemv_rowvec_partial_k<false><<<dim3(cdiv(N, 64), cdiv(K, GV_KSLICE)), 256, 0, (hipStream_t)stream>>>(
+      v0, K0, v1, K, const_cast<float*>(W), ldw, N, partial, vout, RnnPendingUpdate{});
   TNET_LAUNCH_CHECK();
   return TNET_OK;
 }
@@ -546,6 +750,39 @@ extern "C" int tnet_rnn_out_partial(const float* hpart, int hslices, const float
   return TNET_OK;
 }
 
+extern "C" int tnet_rnn_out_full(const float* hpart, int hslices, const float* hb, float* h, int H, const float* Wo,
+                                 int ldwo, int N, const float* bo, float* z, double* smx, void* stream) {
+  if (hslices <= 0 || H <= 0 || N <= 0 || ldwo < N || !hpart || !h || !Wo || !smx) return TNET_ERR_ARG;
+  if (H > GV_FULL_MAXH || cdiv(N, 64) > 64) return TNET_ERR_UNSUPPORTED;
+  rnn_out_full_kernel<<<cdiv(N, 64), 1024, 0, (hipStream_t)stream>>>(hpart, hslices, hb, h, H, Wo, ldwo, N, bo, z, smx);
+  TNET_LAUNCH_CHECK();
+  return TNET_OK;
+}
+
+extern "C" int tnet_gemv_rowvec_partial_update(const float* v0, int K0, const float* v1, int K1, float* vout,
+                                               float* W, int ldw, int N, float* partial, const float* hist, int ldh,
+                                               int head, int R, const float* D, int ldd, int steps, float* b,
+                                               float* corr_b, float lr, float mmt, float wc, void* stream) {
+  const int K = K0 + K1;
+  if (K0 < 0 || K1 < 0 || K <= 0 || N <= 0 || ldw < N || (K0 && !v0) || (K1 && !v1) || !W || !partial || !hist ||
+      !D || !b || !corr_b || steps <= 0 || head < 0 || head >= R || ldh < K || ldd < N)
+    return TNET_ERR_ARG;
+  if (steps > GV_UPD_MAX || steps >= R) return TNET_ERR_UNSUPPORTED;  // the push must not hit a row the update reads
+  const RnnPendingUpdate u{hist, ldh, head, R, D, ldd, steps, b, corr_b, lr, mmt, wc};
+  const dim3 grid(cdiv(N, 64), cdiv(K, GV_KSLICE));
+  hipStream_t st = (hipStream_t)stream;
+  switch (steps) {
+#define TNET_UPD_CASE(n) \
+  case n: gemv_rowvec_partial_k<true, n><<<grid, 256, 0, st>>>(v0, K0, v1, K, W, ldw, N, partial, vout, u); break;
+    TNET_UPD_CASE(1) TNET_UPD_CASE(2) TNET_UPD_CASE(3) TNET_UPD_CASE(4) TNET_UPD_CASE(5) TNET_UPD_CASE(6)
+    TNET_UPD_CASE(7) TNET_UPD_CASE(8) TNET_UPD_CASE(9)
+#undef TNET_UPD_CASE
+    default: return TNET_ERR_UNSUPPORTED;
+  }
+  TNET_LAUNCH_CHECK();
+  return TNET_OK;
+}
+
 extern "C" int tnet_rnn_out_stats(const float* opart, int H, int N, const float* bo, float* z, double* smx,
                                   void* stream) {
   if (H <= 0 || N <= 0 || !opart || !smx) return TNET_ERR_ARG;
@@ -554,24 +791,24 @@ extern "C" int tnet_rnn_out_stats(const float* opart, int H, int N, const float*
   return TNET_OK;
 }
 
-extern "C" int tnet_rnn_out_bwd_update(const float* z, const double* smx, int N, const int* label, const float* h,
-                                       int H, float* Wo, int ldwo, float* corrWo, int ldc, float* bo, float* corr_bo,
-                                       float scale, float mmt, float l2, float* y, float* e, float* eo, float* d,
-                                       double* stats, unsigned long long* argkey, int train, void* stream) {
+extern "C" int tnet_rnn_out_bwd_update(const float* z, const double* smx, int pairs, int N, const int* label,
+                                       const float* h, int H, float* Wo, int ldwo, float* corrWo, int ldc, float* bo,
+                                       float* corr_bo, float scale, float mmt, float l2, float* y, float* e, float* eo,
+                                       float* d, double* stats, unsigned long long* argkey, int train, void* stream) {
   if (N <= 0 || H <= 0 || !z || !smx || !label || !h || (train && (!Wo || !bo || ldwo < N)) ||
-      (train && mmt != 0.f && (!corrWo || !corr_bo || ldc < N)))
+      (train && mmt != 0.f && (!corrWo || !corr_bo || ldc < N)) || pairs < 1)
     return TNET_ERR_ARG;
-  if (cdiv(N, 256) > 64) return TNET_ERR_UNSUPPORTED;  // N <= 16384: one pair per lane in rnn_softmax_norm
+  if (pairs > 64) return TNET_ERR_UNSUPPORTED;  // one pair per lane in rnn_out_bwd_kernel's normaliser
   const bool wide = N > 1024;  // a workgroup per weight row
   const int row_blocks = train ? (wide ? H : cdiv(H, 4)) : 0;
   const dim3 grid(row_blocks + cdiv(N, 256));
   hipStream_t st = (hipStream_t)stream;
   if (wide)
-    rnn_out_bwd_kernel<4><<<grid, 256, 0, st>>>(z, smx, cdiv(N, 256), label, h, H, N, Wo, ldwo,
+    rnn_out_bwd_kernel<4><<<grid, 256, 0, st>>>(z, smx, pairs, label, h, H, N, Wo, ldwo,
                                                 mmt != 0.f ? corrWo : nullptr, ldc, bo, mmt != 0.f ? corr_bo : nullptr,
                                                 scale, mmt, l2, y, e, eo, d, stats, argkey, row_blocks, train);
   else
-    rnn_out_bwd_kernel<1><<<grid, 256, 0, st>>>(z, smx, cdiv(N, 256), label, h, H, N, Wo, ldwo,
+    rnn_out_bwd_kernel<1><<<grid, 256, 0, st>>>(z, smx, pairs, label, h, H, N, Wo, ldwo,
                                                 mmt != 0.f ? corrWo : nullptr, ldc, bo, mmt != 0.f ? corr_bo : nullptr,
                                                 scale, mmt, l2, y, e, eo, d, stats, argkey, row_blocks, train);
   TNET_LAUNCH_CHECK();
@@ -631,7 +868,8 @@ extern "C" int tnet_gemv_rowvec_cat(const float* v0, int K0, const float* v1, in
   const int slices = cdiv(K, GV_KSLICE);
   float* part = (float*)workspace;
   hipStream_t st = (hipStream_t)stream;
-  gemv_rowvec_partial<<<dim3(cdiv(N, 64), slices), 256, 0, st>>>(v0, K0, v1, K, W, ldw, N, part, vout);
+  gemv_rowvec_partial_k<false><<<dim3(cdiv(N, 64), slices), 256, 0, st>>>(v0, K0, v1, K, const_cast<float*>(W), ldw,
+                                                                          N, part, vout, RnnPendingUpdate{});
   TNET_LAUNCH_CHECK();
   gemv_rowvec_final<<<cdiv(N, 256), 256, 0, st>>>(part, slices, N, b, y, act);
   TNET_LAUNCH_CHECK();
@@ -646,7 +884,8 @@ extern "C" int tnet_gemv_rowvec_softmax_xent(const float* v, int K, const float*
   const int slices = cdiv(K, GV_KSLICE);
   float* part = (float*)workspace;
   hipStream_t st = (hipStream_t)stream;
-  gemv_rowvec_partial<<<dim3(cdiv(N, 64), slices), 256, 0, st>>>(v, K, nullptr, K, W, ldw, N, part, nullptr);
+  gemv_rowvec_partial_k<false><<<dim3(cdiv(N, 64), slices), 256, 0, st>>>(v, K, nullptr, K, const_cast<float*>(W), ldw,
+                                                                          N, part, nullptr, RnnPendingUpdate{});
   TNET_LAUNCH_CHECK();
   gemv_softmax_xent_final<<<1, 256, 0, st>>>(part, slices, N, b, z, y, e, label, stats);
   TNET_LAUNCH_CHECK();

@@ -181,8 +181,11 @@ _SIGS = {
     "tnet_gemv_rowvec_partial": (i32, [vp, i32, vp, i32, vp, vp, i32, i32, vp, vp]),
     "tnet_rnn_out_partial": (i32, [vp, i32, vp, vp, i32, vp, i32, i32, vp, vp]),
     "tnet_rnn_out_stats": (i32, [vp, i32, i32, vp, vp, vp, vp]),
-    "tnet_rnn_out_bwd_update": (i32, [vp, vp, i32, vp, vp, i32, vp, i32, vp, i32, vp, vp, f32, f32, f32, vp, vp, vp,
-                                      vp, vp, vp, i32, vp]),
+    "tnet_rnn_out_bwd_update": (i32, [vp, vp, i32, i32, vp, vp, i32, vp, i32, vp, i32, vp, vp, f32, f32, f32, vp, vp,
+                                      vp, vp, vp, vp, i32, vp]),
+    "tnet_rnn_out_full": (i32, [vp, i32, vp, vp, i32, vp, i32, i32, vp, vp, vp, vp]),
+    "tnet_gemv_rowvec_partial_update": (i32, [vp, i32, vp, i32, vp, vp, i32, i32, vp, vp, i32, i32, i32, vp, i32, i32,
+                                              vp, vp, f32, f32, f32, vp]),
     "tnet_argmax_correct": (i32, [vp, vp, i32, i32, vp, vp]),
     "tnet_rnn_utterance_workspace": (C.c_long, [i32, i32, i32]),
     "tnet_rnn_utterance_stamps": (i32, [vp]),

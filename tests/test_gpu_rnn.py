@@ -15,7 +15,7 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 import oracle as orc  # noqa: E402
-from tnet_amd import DeviceArray, Network, Objective, RnnTrainer, formats  # noqa: E402
+from tnet_amd import DeviceArray, Network, Objective, RnnTrainer, formats, synchronize  # noqa: E402
 from tnet_amd._lib import check, lib  # noqa: E402
 
 
@@ -297,7 +297,7 @@ def test_rnn_output_chain_kernels(nIn, H, N, t):
     check(lib().tnet_rnn_out_partial(hpart.ptr, hs, d["b"].ptr, h.ptr, H, d["Wo"].ptr, d["Wo"].stride, N, opart.ptr,
                                      S()))
     check(lib().tnet_rnn_out_stats(opart.ptr, H, N, d["bo"].ptr, z.ptr, smx.ptr, S()))
-    check(lib().tnet_rnn_out_bwd_update(z.ptr, smx.ptr, N, lab.ptr, h.ptr, H, d["Wo"].ptr, d["Wo"].stride, None, 0,
+    check(lib().tnet_rnn_out_bwd_update(z.ptr, smx.ptr, G, N, lab.ptr, h.ptr, H, d["Wo"].ptr, d["Wo"].stride, None, 0,
                                         d["bo"].ptr, None, scale, 0.0, l2, y.ptr, e.ptr, eo.ptr, dd.ptr, stats.ptr,
                                         key.ptr, 1, S()))
     v = np.concatenate([x, yp]).astype(np.float64)
@@ -326,3 +326,101 @@ def test_rnn_output_chain_kernels(nIn, H, N, t):
     st2 = DeviceArray(1, 1024, np.float64, stride=1024)
     check(lib().tnet_argmax_correct(key.ptr, lab.ptr, 1, N, st2.ptr, S()))
     assert st2.numpy()[0][1] == float(int(np.argmax(y.numpy().ravel())) == (tt if tt >= 0 else 0))
+
+
+@pytest.mark.parametrize("nIn,H,N,t", [(440, 512, 4000, 17), (440, 512, 135, 3), (30, 70, 300, -1), (8, 64, 5, 9)])
+def test_rnn_out_full(nIn, H, N, t):
+    """tnet_rnn_out_full (the trainer's output side: h finished by every workgroup, complete z per 64
+    columns, one softmax pair per 64 columns) -> tnet_rnn_out_bwd_update with ceil(N/64) pairs vs numpy
+    in fp64 (the tolerances of test_rnn_output_chain_kernels)"""
+    rng = np.random.default_rng(N + H + 1)
+    x = rng.standard_normal(nIn).astype(np.float32)
+    yp = rng.random(H).astype(np.float32)
+    W = (0.05 * rng.standard_normal((nIn + H, H))).astype(np.float32)
+    b = rng.standard_normal(H).astype(np.float32)
+    Wo = (0.05 * rng.standard_normal((H, N))).astype(np.float32)
+    bo = rng.standard_normal(N).astype(np.float32)
+    scale, l2 = -0.03, -1e-5
+    d = {k: DeviceArray.from_numpy(v.reshape(1, -1) if v.ndim == 1 else v) for k, v in
+         dict(x=x, yp=yp, W=W, b=b, Wo=Wo, bo=bo).items()}
+    hs, G = -(-(nIn + H) // 64), -(-N // 64)
+    hpart = DeviceArray(hs, H)
+    hist, h, z = DeviceArray(1, nIn + H), DeviceArray(1, H), DeviceArray(1, N)
+    smx = DeviceArray(1, 2 * G, np.float64, stride=2 * G)
+    lab = DeviceArray.vector(np.array([t], np.int32))
+    eo, dd, e, y = DeviceArray(1, H), DeviceArray(1, H), DeviceArray(1, N), DeviceArray(1, N)
+    stats = DeviceArray(1, 1024, np.float64, stride=1024)
+    key = DeviceArray.vector(np.zeros(2, np.int32))
+    check(lib().tnet_gemv_rowvec_partial(d["x"].ptr, nIn, d["yp"].ptr, H, hist.ptr, d["W"].ptr, d["W"].stride, H,
+                                         hpart.ptr, S()))
+    check(lib().tnet_rnn_out_full(hpart.ptr, hs, d["b"].ptr, h.ptr, H, d["Wo"].ptr, d["Wo"].stride, N, d["bo"].ptr,
+                                  z.ptr, smx.ptr, S()))
+    check(lib().tnet_rnn_out_bwd_update(z.ptr, smx.ptr, G, N, lab.ptr, h.ptr, H, d["Wo"].ptr, d["Wo"].stride, None, 0,
+                                        d["bo"].ptr, None, scale, 0.0, l2, y.ptr, e.ptr, eo.ptr, dd.ptr, stats.ptr,
+                                        key.ptr, 1, S()))
+    v = np.concatenate([x, yp]).astype(np.float64)
+    hr = 1 / (1 + np.exp(-(b + v @ W)))
+    np.testing.assert_allclose(h.numpy().ravel(), hr, rtol=1e-5, atol=1e-6)
+    zr = bo + hr @ Wo
+    np.testing.assert_allclose(z.numpy().ravel(), zr, rtol=1e-5, atol=1e-5)
+    yr = np.exp(zr - zr.max())
+    yr /= yr.sum()
+    tt = t if 0 <= t < N else -1
+    er = yr - (np.arange(N) == tt)
+    np.testing.assert_allclose(y.numpy().ravel(), yr, rtol=2e-5, atol=1e-9)
+    np.testing.assert_allclose(e.numpy().ravel(), er, rtol=2e-5, atol=1e-8)
+    eor = Wo.astype(np.float64) @ er
+    np.testing.assert_allclose(eo.numpy().ravel(), eor, rtol=1e-4, atol=1e-6)
+    np.testing.assert_allclose(dd.numpy().ravel(), eor * hr * (1 - hr), rtol=1e-4, atol=1e-6)
+    Wn = Wo + scale * np.outer(hr, er)
+    np.testing.assert_allclose(d["Wo"].numpy(), Wn + l2 * Wn, rtol=1e-5, atol=1e-7)
+    xent = -np.log(max(yr[tt], 1.1754944e-38)) if tt >= 0 else 0.0
+    np.testing.assert_allclose(stats.numpy()[0][0::2].sum(), xent, rtol=1e-5, atol=1e-6)
+    k = int(key.numpy().ravel().view(np.uint64)[0])
+    assert 0xFFFFFFFF - (k & 0xFFFFFFFF) == int(np.argmax(y.numpy().ravel()))
+
+
+@pytest.mark.parametrize("nIn,H,steps,R,head,mmt,wc", [(440, 512, 5, 6, 2, 0.0, 0.0), (440, 512, 5, 6, 5, 0.5, 1e-4),
+                                                      (30, 70, 3, 4, 0, 0.9, 1e-3), (8, 64, 1, 2, 1, 0.0, 0.0),
+                                                      (100, 200, 9, 10, 7, 0.5, 1e-4)])
+def test_gemv_rowvec_partial_update(nIn, H, steps, R, head, mmt, wc):
+    """tnet_gemv_rowvec_partial_update (the previous frame's recurrent update folded into the next
+    frame's forward) = tnet_rnn_update then tnet_gemv_rowvec_partial: W, b, corr_b, the partials and the
+    pushed history row bit-identical (same per-element arithmetic and order); the push lands on the ring
+    row the update does not read; steps > 9 or steps >= R are refused (TNET_ERR_UNSUPPORTED: the trainer
+    then runs the update on its own)"""
+    rng = np.random.default_rng(H + steps)
+    K = nIn + H
+    W = (0.05 * rng.standard_normal((K, H))).astype(np.float32)
+    b = rng.standard_normal(H).astype(np.float32)
+    cb = (0.01 * rng.standard_normal(H)).astype(np.float32)
+    hist = rng.standard_normal((R, K)).astype(np.float32)
+    D = (0.1 * rng.standard_normal((steps, H))).astype(np.float32)
+    x = rng.standard_normal(nIn).astype(np.float32)
+    yp = rng.random(H).astype(np.float32)
+    lr = 0.02
+    push = (head + R - 1) % R
+    outs = []
+    for fused in (False, True):
+        dW, db, dcb, dh, dD = (DeviceArray.from_numpy(W), DeviceArray.vector(b), DeviceArray.vector(cb),
+                               DeviceArray.from_numpy(hist), DeviceArray.from_numpy(D))
+        dx, dy = DeviceArray.vector(x), DeviceArray.vector(yp)
+        part = DeviceArray(-(-K // 64), H)
+        row = dh.ptr + push * dh.stride * 4
+        if fused:
+            check(lib().tnet_gemv_rowvec_partial_update(dx.ptr, nIn, dy.ptr, H, row, dW.ptr, dW.stride, H, part.ptr,
+                                                        dh.ptr, dh.stride, head, R, dD.ptr, dD.stride, steps, db.ptr,
+                                                        dcb.ptr, lr, mmt, wc, S()))
+        else:
+            check(lib().tnet_rnn_update(dW.ptr, dW.stride, K, H, dh.ptr, dh.stride, head, R, dD.ptr, dD.stride, steps,
+                                        db.ptr, dcb.ptr, lr, mmt, wc, S()))
+            check(lib().tnet_gemv_rowvec_partial(dx.ptr, nIn, dy.ptr, H, row, dW.ptr, dW.stride, H, part.ptr, S()))
+        synchronize()
+        outs.append([a.numpy() for a in (dW, db, dcb, part, dh)])
+    for a, c in zip(*outs):
+        np.testing.assert_array_equal(a, c)
+    np.testing.assert_array_equal(outs[1][4][push], np.concatenate([x, yp]))
+    dummy = DeviceArray(4, 64)
+    assert lib().tnet_gemv_rowvec_partial_update(dummy.ptr, 8, dummy.ptr, 8, None, dummy.ptr, 64, 8, dummy.ptr,
+                                                 dummy.ptr, 64, 0, 4, dummy.ptr, 64, 4, dummy.ptr, dummy.ptr, lr,
+                                                 mmt, wc, S()) != 0

@@ -8,6 +8,8 @@ Tolerances: the same kernel-level bounds as tests/test_gpu_kernels.py (|got - re
 body only by their summation order (checked against the fp64 reference, not bitwise); launches are
 deterministic (static plan, slices combined in order).
 """
+import ctypes
+
 import numpy as np
 import pytest
 
@@ -111,3 +113,56 @@ def test_reserve_api():
     check(lib().tnet_gemm_reserve(8))
     check(lib().tnet_gemm_reserve(0))
     assert lib().tnet_gemm_config(b"auto+rsvx") != 0
+
+
+@pytest.fixture
+def split2():
+    check(lib().tnet_gemm_config(b"auto+s21"))  # opt-in (measured slower than 64x64 tiles over the whole K)
+    yield
+    check(lib().tnet_gemm_config(b"auto+il0+s20"))
+
+
+@pytest.mark.parametrize("kind", ["updb", "upd", "gradb"])
+def test_update_split2_first_layer(split2, kind):
+    """gemm16_split2_kernel (the first layer's 440 x 2048 update over K = 1024: 112 tiles of 64x128, each
+    cut into two k-halves combined by the stream-K fixup before the fused SGD / bias epilogue; the last
+    tile-row is partial, rows 440..447 masked): against the fp64 update, bias from the slab sums,
+    deterministic launch to launch."""
+    rows, n_in, n_out, scale = 1024, 440, 2048, -0.5
+    X, E = rnd((rows, n_in), 21), rnd((rows, n_out), 22, 0.01)
+    W0 = rnd((n_in, n_out), 23, 0.05)
+    b0 = rnd(n_out, 24, 0.1)
+    P = slab_sums(E).astype(np.float32)
+    g, mag = gemm_ref("T", "N", X, E)
+    outs = []
+    for _ in range(2):
+        dX, dE, dP = DeviceArray.from_numpy(X), DeviceArray.from_numpy(E), DeviceArray.from_numpy(P)
+        dW, db = DeviceArray.from_numpy(W0), DeviceArray.vector(b0)
+        if kind == "updb":
+            check(lib().tnet_affine_update_bias(dX.ptr, dX.dim, dE.ptr, dE.dim, dW.ptr, dW.dim, None, 0,
+                                                ctypes.c_float(scale), ctypes.c_float(0.0), ctypes.c_float(0.0),
+                                                dP.ptr, dP.stride, db.ptr, None, S()))
+        elif kind == "upd":
+            check(lib().tnet_affine_update(dX.ptr, dX.dim, dE.ptr, dE.dim, dW.ptr, dW.dim, None, 0,
+                                           ctypes.c_float(scale), ctypes.c_float(0.0), ctypes.c_float(0.0), S()))
+        else:
+            dW = DeviceArray(n_in, n_out)
+            db = DeviceArray.vector(np.full(n_out, np.nan, np.float32))
+            check(lib().tnet_affine_grad_bias(dX.ptr, dX.dim, dE.ptr, dE.dim, dW.ptr, dW.dim, dP.ptr, dP.stride,
+                                              db.ptr, S()))
+        synchronize()
+        outs.append((dW.numpy(), db.numpy().ravel()))
+    Wg, bg = outs[0]
+    if kind == "gradb":
+        assert np.all(np.abs(Wg - g) <= 2e-5 * mag + 1e-7)
+        np.testing.assert_array_equal(bg, P.astype(np.float64).sum(0).astype(np.float32))
+    else:
+        want = W0.astype(np.float64) + scale * g
+        assert np.all(np.abs(Wg - want) <= abs(scale) * 2e-5 * mag + 2 * np.spacing(np.abs(want)) + 1e-7)
+        if kind == "updb":
+            bw = (b0 + np.float32(scale) * P.astype(np.float64).sum(0).astype(np.float32)).astype(np.float32)
+            np.testing.assert_allclose(bg, bw, rtol=0, atol=2 * np.spacing(np.abs(bw)).max())
+        else:
+            np.testing.assert_array_equal(bg, b0)
+    np.testing.assert_array_equal(outs[0][0], outs[1][0])
+    np.testing.assert_array_equal(outs[0][1], outs[1][1])

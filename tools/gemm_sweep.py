@@ -83,6 +83,8 @@ def main():
                 env["TNET_GEMM_SPLITK"] = extra[2:]
             elif extra.startswith("il") and extra[2:].isdigit():
                 env["TNET_SPLITK_INLAUNCH"] = extra[2:]
+            elif extra.startswith("split2_") and extra[7:].isdigit():
+                env["TNET_GEMM_SPLIT2"] = extra[7:]  # gemm16_split2_kernel for the few-tile updates
         p = subprocess.run([sys.executable, "-c", CHILD, REPO, json.dumps(shapes), str(iters)], env=env,
                            capture_output=True, text=True, timeout=300)
         line = [l for l in p.stdout.splitlines() if l.startswith("RESULT ")]
