@@ -120,6 +120,39 @@ int tnet_trainer_trace(TnetTrainer* t, int trace);
  * borrowed, may be NULL = off) and trimmed before the cache; labels stay one per input frame */
 int tnet_trainer_set_transform(TnetTrainer* t, TnetNetwork* transform, int start_ext, int end_ext);
 
+/* ---- host front end: HTK features + MLF targets, read ahead by a thread pool -----------------
+ * Replaces FeatureRepository (src/KaldiLib/Features.cc:349-477, 1009-1347: Init / AddFileList /
+ * ReadFullMatrix / MoveNext with STARTFRMEXT / ENDFRMEXT, TARGETKIND, NATURALREADORDER) and
+ * LabelRepository (src/KaldiLib/Labels.cc:11-186: Init / GenDesiredMatrix, as class ids), the
+ * intake TNetCu drives at TNetCu.cc:290-314, 376-419.  Pure host code (no device calls).
+ *   swap         : byte-swap the big-endian HTK data (!NATURALREADORDER on this host: 1)
+ *   target_kind  : HTK parameter kind, 12 = ANON (the first file's kind); deriv_order as DERIVWINDOWS
+ *                  (0 with ANON: derivatives in the file are dropped, as the reference; < 0: the
+ *                  first file's); deriv_win: NULL or deriv_order window lengths (default 2 each)
+ *   mlf == NULL  : features only (labels / n_labels come back NULL / 0)
+ *   label_dir / label_ext : SOURCETRANSCDIR / SOURCETRANSCEXT (NULL / "lab" in TNetCu)
+ *   threads, depth : reader threads and utterances read ahead of the consumer */
+typedef struct TnetFeatureReader TnetFeatureReader;
+TnetFeatureReader* tnet_reader_create(const char* scp, int swap, int start_ext, int end_ext, int target_kind,
+                                      int deriv_order, const int* deriv_win, const char* mlf, const char* label_map,
+                                      const char* label_dir, const char* label_ext, int threads, int depth);
+int tnet_reader_free(TnetFeatureReader* r);
+long tnet_reader_size(TnetFeatureReader* r);  /* records in the script */
+/* next utterance in script order: 1 = delivered, 0 = end of list, < 0 = this record's error (the
+ * reference's exception text in tnet_last_error).  feats [rows x cols] dense row-major incl. the
+ * context rows; labels [n_labels = rows - start_ext - end_ext]; pointers valid until the next call. */
+int tnet_reader_next(TnetFeatureReader* r, const float** feats, int* rows, int* cols, const int** labels,
+                     int* n_labels, int* samp_period, int* kind, char* logical, int logical_cap);
+int tnet_reader_rewind(TnetFeatureReader* r);  /* FeatureRepository::Rewind */
+/* one record ("logical=physical[s,e]" or a path) without a reader: out == NULL asks for the size only */
+int tnet_htk_read(const char* record, int swap, int start_ext, int end_ext, float* out, long cap, int* rows, int* cols,
+                  int* samp_period, int* kind);
+/* the cache fill of TNetCu.cc:376-419 from a reader: up to max_utts utterances (< 0: to the end of the
+ * list) into the trainer, each training the cache whenever it fills; returns the frames added (< 0 error).
+ * The reader's STARTFRMEXT / ENDFRMEXT must be the transform's (tnet_trainer_set_transform); without
+ * a transform the context rows are trimmed. */
+long tnet_trainer_add_reader(TnetTrainer* t, TnetFeatureReader* r, long max_utts);
+
 /* ---- RBM pre-training (CuRbm, cuRbm.cc; the TRbmCu loop, TRbmCu.cc:291-357) ----------------
  * <rbm> parameters: W [n_vis x n_hid] (host row-major), visible / hidden biases; types[0..1] =
  * visible / hidden unit type (0 Bernoulli, 1 Gaussian; -1 in set = keep). */

@@ -8,6 +8,7 @@
 #include "tnet_train.h"
 #include "curbm.h"
 #include "curecurrent.h"
+#include "htkio.h"
 #include "trainer.h"
 
 using namespace TNet;
@@ -47,6 +48,10 @@ struct TnetRbmTrainer {
 };
 struct TnetRnnTrainer {
   std::unique_ptr<CuRecurrentTrainer> t;
+};
+struct TnetFeatureReader {
+  std::unique_ptr<tnetio::FeatureReader> r;
+  int start_ext = 0, end_ext = 0;
 };
 struct TnetComm {
   std::unique_ptr<GradExchange> ex;
@@ -396,6 +401,104 @@ long tnet_trainer_empty_steps(TnetTrainer* t) { return t ? t->t->EmptySteps() : 
 int tnet_trainer_trace(TnetTrainer* t, int trace) {
   TRY_BEGIN t->t->Cache().Trace(trace);
   TRY_END
+}
+
+// ------------------------------------------------------------------------- host front end
+TnetFeatureReader* tnet_reader_create(const char* scp, int swap, int start_ext, int end_ext, int target_kind,
+                                      int deriv_order, const int* deriv_win, const char* mlf, const char* label_map,
+                                      const char* label_dir, const char* label_ext, int threads, int depth) {
+  try {
+    if (!scp) Error("tnet_reader_create: no script file");
+    if (start_ext < 0 || end_ext < 0) Error("tnet_reader_create: negative frame extension");
+    if (mlf && !label_map) Error("Output label map is missing [-m]");
+    tnetio::FeatureConfig cfg;
+    cfg.swap = swap != 0;
+    cfg.startExt = start_ext;
+    cfg.endExt = end_ext;
+    cfg.targetKind = target_kind;
+    cfg.derivOrder = deriv_order;
+    if (deriv_win)
+      for (int i = 0; i < deriv_order; i++) cfg.derivWin.push_back(deriv_win[i]);
+    std::shared_ptr<const tnetio::MlfLabels> labels;
+    if (mlf) labels = std::make_shared<tnetio::MlfLabels>(mlf, label_map, label_dir, label_ext);
+    std::unique_ptr<TnetFeatureReader> h(new TnetFeatureReader);
+    h->r.reset(new tnetio::FeatureReader(scp, cfg, labels, threads, depth));
+    h->start_ext = start_ext;
+    h->end_ext = end_ext;
+    return h.release();
+  }
+  TRY_END_PTR
+}
+int tnet_reader_free(TnetFeatureReader* r) {
+  delete r;
+  return TNET_OK;
+}
+long tnet_reader_size(TnetFeatureReader* r) { return r ? (long)r->r->Size() : -1; }
+int tnet_reader_next(TnetFeatureReader* r, const float** feats, int* rows, int* cols, const int** labels,
+                     int* n_labels, int* samp_period, int* kind, char* logical, int logical_cap) {
+  try {
+    if (!r) Error("tnet_reader_next: null reader");
+    const tnetio::Utterance* u = r->r->Next();
+    if (!u) return 0;
+    if (feats) *feats = u->feats.data();
+    if (rows) *rows = u->rows;
+    if (cols) *cols = u->cols;
+    if (labels) *labels = u->labels.empty() ? nullptr : u->labels.data();
+    if (n_labels) *n_labels = (int)u->labels.size();
+    if (samp_period) *samp_period = u->samplePeriod;
+    if (kind) *kind = u->kind;
+    if (logical && logical_cap > 0) {
+      std::strncpy(logical, u->logical.c_str(), (size_t)logical_cap - 1);
+      logical[logical_cap - 1] = '\0';
+    }
+    return 1;
+  } catch (std::exception& e) {
+    g_last_error = e.what();
+    return TNET_ERR_RUNTIME;
+  }
+}
+int tnet_reader_rewind(TnetFeatureReader* r) {
+  TRY_BEGIN if (!r) Error("tnet_reader_rewind: null reader");
+  r->r->Rewind();
+  TRY_END
+}
+int tnet_htk_read(const char* record, int swap, int start_ext, int end_ext, float* out, long cap, int* rows, int* cols,
+                  int* samp_period, int* kind) {
+  TRY_BEGIN if (!record) Error("tnet_htk_read: no record");
+  tnetio::FeatureConfig cfg;
+  cfg.swap = swap != 0;
+  cfg.startExt = start_ext;
+  cfg.endExt = end_ext;
+  int tk = cfg.targetKind, dord = cfg.derivOrder;
+  tnetio::Utterance u;
+  tnetio::ReadHtkFeatures(tnetio::ParseFileRecord(record), cfg, tk, dord, u);
+  if (rows) *rows = u.rows;
+  if (cols) *cols = u.cols;
+  if (samp_period) *samp_period = u.samplePeriod;
+  if (kind) *kind = u.kind;
+  if (out) {
+    if (cap < (long)u.feats.size()) Error("tnet_htk_read: output buffer too small");
+    std::memcpy(out, u.feats.data(), u.feats.size() * sizeof(float));
+  }
+  TRY_END
+}
+long tnet_trainer_add_reader(TnetTrainer* t, TnetFeatureReader* r, long max_utts) {
+  try {
+    if (!t || !r) Error("tnet_trainer_add_reader: null handle");
+    long frames = 0;
+    for (long n = 0; max_utts < 0 || n < max_utts; n++) {
+      const tnetio::Utterance* u = r->r->Next();
+      if (!u) break;
+      if (u->labels.empty()) Error("tnet_trainer_add_reader: the reader has no labels (no MLF)");
+      t->t->AddUtteranceExtended(u->feats.data(), (size_t)u->rows, (size_t)u->cols, (size_t)u->cols, u->labels.data(),
+                                 (size_t)r->start_ext, (size_t)r->end_ext);
+      frames += (long)u->labels.size();
+    }
+    return frames;
+  } catch (std::exception& e) {
+    g_last_error = e.what();
+    return TNET_ERR_RUNTIME;
+  }
 }
 
 // ------------------------------------------------------------------------------------ RBM

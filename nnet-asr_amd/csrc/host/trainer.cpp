@@ -115,20 +115,7 @@ void CuTrainer::AddUtterance(const float* feats, size_t rows, size_t cols, size_
       const size_t src = r < mStartExt ? 0 : (r - mStartExt >= rows ? rows - 1 : r - mStartExt);
       std::memcpy(&mExtHost[r * cols], feats + src * ld, cols * sizeof(float));
     }
-    mRaw.CopyFromHost(mExtHost.data(), R, cols, cols);
-    mTransform->Propagate(mRaw, mTransformed);
-    if (mTransformed.Cols() != mNet->GetNInputs()) {
-      std::ostringstream os;
-      os << "CuTrainer::AddUtterance: transformed feature dim " << mTransformed.Cols() << " != network input dim "
-         << mNet->GetNInputs();
-      Error(os.str());
-    }
-    mTrimmed.Init(rows, mTransformed.Cols());
-    mTrimmed.CopyRows(rows, mStartExt, mTransformed, 0);
-    mUttLabels.CopyFromHost(labels, rows);
-    mCache.AddDataLabels(mTrimmed, mUttLabels);
-    mTrainedSinceFill = false;
-    if (mCache.Full()) DrainCache(false);
+    TransformAndAdd(mExtHost.data(), R, cols, cols, labels, rows);
     return;
   }
   if (cols != mNet->GetNInputs()) {
@@ -140,6 +127,47 @@ void CuTrainer::AddUtterance(const float* feats, size_t rows, size_t cols, size_
   mCache.AddDataHost(feats, rows, cols, ld, labels);
   mTrainedSinceFill = false;
   if (mCache.Full()) DrainCache(false);
+}
+
+void CuTrainer::TransformAndAdd(const float* ext, size_t rows_ext, size_t cols, size_t ld, const int* labels,
+                                size_t rows) {
+  mRaw.CopyFromHost(ext, rows_ext, cols, ld);
+  mTransform->Propagate(mRaw, mTransformed);
+  if (mTransformed.Cols() != mNet->GetNInputs()) {
+    std::ostringstream os;
+    os << "CuTrainer::AddUtterance: transformed feature dim " << mTransformed.Cols() << " != network input dim "
+       << mNet->GetNInputs();
+    Error(os.str());
+  }
+  mTrimmed.Init(rows, mTransformed.Cols());
+  mTrimmed.CopyRows(rows, mStartExt, mTransformed, 0);
+  mUttLabels.CopyFromHost(labels, rows);
+  mCache.AddDataLabels(mTrimmed, mUttLabels);
+  mTrainedSinceFill = false;
+  if (mCache.Full()) DrainCache(false);
+}
+
+void CuTrainer::AddUtteranceExtended(const float* feats, size_t rows_ext, size_t cols, size_t ld, const int* labels,
+                                     size_t start_ext, size_t end_ext) {
+  if (rows_ext < start_ext + end_ext + 1) {
+    std::ostringstream os;
+    os << "CuTrainer::AddUtteranceExtended: " << rows_ext << " rows cannot carry " << start_ext << " + " << end_ext
+       << " context rows";
+    Error(os.str());
+  }
+  const size_t rows = rows_ext - start_ext - end_ext;
+  if (!mTransform) {  // TNetCu.cc:390-393 trims the context whatever the (empty) transform
+    AddUtterance(feats + start_ext * ld, rows, cols, ld, labels);
+    return;
+  }
+  if (start_ext != mStartExt || end_ext != mEndExt) {
+    std::ostringstream os;
+    os << "CuTrainer::AddUtteranceExtended: features carry " << start_ext << "/" << end_ext
+       << " context rows, the transform expects " << mStartExt << "/" << mEndExt;
+    Error(os.str());
+  }
+  CheckLabels(labels, rows, mNet->GetNOutputs(), "CuTrainer::AddUtteranceExtended");
+  TransformAndAdd(feats, rows_ext, cols, ld, labels, rows);
 }
 
 void CuTrainer::Finish() {

@@ -43,6 +43,13 @@ class CuTrainer {
 
   /// Append one utterance (host memory): features [rows x cols] with leading dim ld, class ids.
   void AddUtterance(const float* feats, size_t rows, size_t cols, size_t ld, const int* labels);
+  /// Append one utterance as the reference's FeatureRepository delivers it (TNetCu.cc:385-416):
+  /// `rows_ext` rows that already carry `start_ext` / `end_ext` context rows (edge replication, or
+  /// real neighbouring frames of a [s,e] range), labels for the rows_ext - start_ext - end_ext frames
+  /// between.  With a transform, the extension must be the transform's; without, the context rows
+  /// are trimmed.
+  void AddUtteranceExtended(const float* feats, size_t rows_ext, size_t cols, size_t ld, const int* labels,
+                            size_t start_ext, size_t end_ext);
   /// End of the utterance list.
   void Finish();
   /// Steps (bunches) trained so far.
@@ -63,6 +70,8 @@ class CuTrainer {
   /// (DpPlanRound).  Returns whether every rank has reached its final drain.
   bool DrainCache(bool final);
   bool DpRound(long n, bool final);
+  /// extended host rows -> transform on the device -> trim -> cache
+  void TransformAndAdd(const float* ext, size_t rows_ext, size_t cols, size_t ld, const int* labels, size_t rows);
   bool DataParallel() const { return mExchange && !mOpt.crossval && mExchange->WorldSize() > 1; }
   void Step();
 

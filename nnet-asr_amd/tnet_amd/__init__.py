@@ -16,6 +16,7 @@ from . import formats  # noqa: F401  (host formats; no device code)
 from ._lib import HOST_ALLREDUCE_FN, LIB_PATH, MatrixDim, TnetError, check, check_ptr, header_symbols, lib
 
 __all__ = ["DeviceArray", "Network", "Objective", "Trainer", "RbmTrainer", "RnnTrainer", "Comm", "TnetError", "synchronize",
+           "FeatureReader", "htk_read",
            "pad_stride",
            "device_count", "version", "LIB_PATH", "header_symbols", "formats"]
 
@@ -327,6 +328,13 @@ class Trainer:
         check(lib().tnet_trainer_set_transform(self.h, transform.h if transform else None, start_ext, end_ext),
               "set_transform")
 
+    def add_reader(self, reader: "FeatureReader", max_utts: int = -1) -> int:
+        """the TNetCu cache-fill loop (TNetCu.cc:376-419) over a native FeatureReader; returns frames added"""
+        n = lib().tnet_trainer_add_reader(self.h, reader.h, max_utts)
+        if n < 0:
+            check(int(n), "add_reader")
+        return int(n)
+
     def set_comm(self, comm: Optional["Comm"]) -> None:
         self._comm = comm
         check(lib().tnet_trainer_set_comm(self.h, comm.h if comm else None), "set_comm")
@@ -497,3 +505,73 @@ class Comm:
                 self.h = None
         except Exception:
             pass
+
+
+class FeatureReader:
+    """FeatureRepository + LabelRepository (src/KaldiLib/Features.cc, Labels.cc) in native code with a
+    read-ahead thread pool (csrc/host/htkio.cpp, include/tnet_train.h tnet_reader_*).  Iterating yields
+    (logical name, features [rows x cols] incl. the context rows, class ids [rows - start_ext - end_ext]
+    or None, sample period, parameter kind); the arrays are copies."""
+
+    def __init__(self, scp: str, mlf: Optional[str] = None, label_map: Optional[str] = None,
+                 label_dir: Optional[str] = None, label_ext: Optional[str] = "lab", start_ext: int = 0,
+                 end_ext: int = 0, swap: bool = True, target_kind: int = 12, deriv_order: int = 0,
+                 deriv_win: Optional[Sequence[int]] = None, threads: int = 4, depth: int = 16):
+        enc = lambda s: s.encode() if s is not None else None  # noqa: E731
+        self._win = (C.c_int * len(deriv_win))(*deriv_win) if deriv_win else None
+        self.start_ext, self.end_ext = start_ext, end_ext
+        self.h = check_ptr(lib().tnet_reader_create(enc(scp), int(swap), start_ext, end_ext, target_kind, deriv_order,
+                                                    C.cast(self._win, C.c_void_p) if self._win else None, enc(mlf),
+                                                    enc(label_map), enc(label_dir), enc(label_ext), threads, depth),
+                           "reader_create")
+
+    def __len__(self) -> int:
+        return int(lib().tnet_reader_size(self.h))
+
+    def next_raw(self):
+        """the next utterance as (name, feats, labels, period, kind) views into the reader's buffer
+        (valid until the next call), or None at the end of the list"""
+        fp, lp = C.c_void_p(), C.c_void_p()
+        rows, cols, nl, per, kind = C.c_int(), C.c_int(), C.c_int(), C.c_int(), C.c_int()
+        name = C.create_string_buffer(4096)
+        st = lib().tnet_reader_next(self.h, C.byref(fp), C.byref(rows), C.byref(cols), C.byref(lp), C.byref(nl),
+                                    C.byref(per), C.byref(kind), name, len(name))
+        if st == 0:
+            return None
+        check(st if st < 0 else 0, "reader_next")
+        n = rows.value * cols.value
+        x = np.ctypeslib.as_array(C.cast(fp, C.POINTER(C.c_float)), (n,)).reshape(rows.value, cols.value) if n else \
+            np.zeros((rows.value, cols.value), np.float32)
+        lab = np.ctypeslib.as_array(C.cast(lp, C.POINTER(C.c_int)), (nl.value,)) if lp.value else None
+        return name.value.decode(), x, lab, per.value, kind.value
+
+    def __iter__(self):
+        while True:
+            u = self.next_raw()
+            if u is None:
+                return
+            name, x, lab, per, kind = u
+            yield name, x.copy(), (lab.copy() if lab is not None else None), per, kind
+
+    def rewind(self) -> None:
+        check(lib().tnet_reader_rewind(self.h), "reader_rewind")
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            try:
+                lib().tnet_reader_free(self.h)
+            except Exception:
+                pass
+            self.h = None
+
+
+def htk_read(record: str, start_ext: int = 0, end_ext: int = 0, swap: bool = True):
+    """one HTK record ("logical=physical[s,e]" or a path) through the native reader:
+    (features [rows x cols], sample period, parameter kind)"""
+    rows, cols, per, kind = C.c_int(), C.c_int(), C.c_int(), C.c_int()
+    check(lib().tnet_htk_read(record.encode(), int(swap), start_ext, end_ext, None, 0, C.byref(rows), C.byref(cols),
+                              C.byref(per), C.byref(kind)), "htk_read")
+    out = np.empty((rows.value, cols.value), np.float32)
+    check(lib().tnet_htk_read(record.encode(), int(swap), start_ext, end_ext, out.ctypes.data, out.size, C.byref(rows),
+                              C.byref(cols), C.byref(per), C.byref(kind)), "htk_read")
+    return out, per.value, kind.value

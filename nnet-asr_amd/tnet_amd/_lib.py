@@ -146,6 +146,16 @@ _SIGS = {
     "tnet_trainer_set_comm": (i32, [vp, vp]),
     "tnet_trainer_trace": (i32, [vp, i32]),
     "tnet_trainer_set_transform": (i32, [vp, vp, i32, i32]),
+    "tnet_reader_create": (vp, [C.c_char_p, i32, i32, i32, i32, i32, vp, C.c_char_p, C.c_char_p, C.c_char_p,
+                                C.c_char_p, i32, i32]),
+    "tnet_reader_free": (i32, [vp]),
+    "tnet_reader_size": (i64, [vp]),
+    "tnet_reader_next": (i32, [vp, C.POINTER(vp), C.POINTER(i32), C.POINTER(i32), C.POINTER(vp), C.POINTER(i32),
+                              C.POINTER(i32), C.POINTER(i32), C.c_char_p, i32]),
+    "tnet_reader_rewind": (i32, [vp]),
+    "tnet_htk_read": (i32, [C.c_char_p, i32, i32, i32, vp, i64, C.POINTER(i32), C.POINTER(i32), C.POINTER(i32),
+                           C.POINTER(i32)]),
+    "tnet_trainer_add_reader": (i64, [vp, vp, i64]),
     "tnet_comm_unique_id": (i32, [C.c_char_p]),
     "tnet_comm_create": (vp, [i32, i32, C.c_char_p]),
     "tnet_comm_free": (i32, [vp]),

@@ -9,6 +9,9 @@
 //             CrossEntropy::Evaluate, clone->Backpropagate (Gradient()), master
 //             AccuGradient/AccuBunchsize/Update(0,1)/ResetBunchsize.
 //   train   : the multi-threaded Platform training loop timed around RunTrain (CPU baseline).
+//   features: FeatureRepository::ReadFullMatrix + LabelRepository::GenDesiredMatrix over a script,
+//             configured as TNetCu does (TNetCu.cc:192-196, 290-314; UserInterface.cc:352-460):
+//             every utterance's matrix and class ids, or the exception text of a failing record.
 //   shuffle : the cache permutation produced by Cache::Init(seed)+AddData+Randomize
 //             (src/TNetLib/Cache.cc:23-192) -- lrand48 + libstdc++ random_shuffle.
 //
@@ -28,6 +31,8 @@
 #include "Cache.h"
 #include "Matrix.h"
 #include "Platform.h"
+#include "Features.h"
+#include "Labels.h"
 #include "Timer.h"
 #include "UserInterface.h"
 
@@ -175,12 +180,74 @@ static int cmd_train(int argc, char** argv) {
   std::_Exit(0);
 }
 
+// features <scp> <swap> <start_ext> <end_ext> <TARGETKIND> <mlf|-> <map> <label_dir|-> <label_ext> <outdir>
+// outdir/index.txt: "k rows cols period kind n_labels logical" or "k ERROR <message>" per record;
+// outdir/f<k>.f32 (rows x cols), outdir/l<k>.i32 (argmax of each GenDesiredMatrix row)
+static int cmd_features(int argc, char** argv) {
+  if (argc < 12) { std::cerr << "usage: features scp swap sext eext TARGETKIND mlf map ldir lext outdir\n"; return 2; }
+  const bool swap = atoi(argv[3]) != 0;
+  const int sext = atoi(argv[4]), eext = atoi(argv[5]);
+  int target_kind = FeatureRepository::ReadParmKind(argv[6], false);
+  if (target_kind == -1) { std::cerr << "bad TARGETKIND\n"; return 2; }
+  // UserInterface::GetFeatureParams without DERIVWINDOWS (UserInterface.cc:444-459)
+  int deriv_order = target_kind & PARAMKIND_T ? 3 : target_kind & PARAMKIND_A ? 2 : target_kind & PARAMKIND_D ? 1 : 0;
+  int* win = NULL;
+  if (deriv_order || target_kind != PARAMKIND_ANON) {
+    win = (int*)malloc(3 * sizeof(int));
+    win[0] = win[1] = win[2] = 2;
+  }
+  const std::string mlf = argv[7], map = argv[8], ldir = argv[9], lext = argv[10], out = argv[11];
+  FeatureRepository repo;
+  repo.Init(swap, sext, eext, target_kind, deriv_order, win, NULL, NULL, NULL, NULL, NULL);
+  repo.AddFileList(argv[2]);
+  LabelRepository labels;
+  const bool use_mlf = mlf != "-";
+  if (use_mlf) labels.Init(mlf.c_str(), map.c_str(), ldir == "-" ? NULL : ldir.c_str(), lext.c_str());
+  std::ofstream idx((out + "/index.txt").c_str());
+  repo.Rewind();
+  for (int k = 0; !repo.EndOfList(); k++, repo.MoveNext()) {
+    try {
+      Matrix<BaseFloat> m;
+      repo.ReadFullMatrix(m);
+      std::ostringstream fn;
+      fn << out << "/f" << k << ".f32";
+      dump_matrix(fn.str(), m);
+      int nl = 0;
+      if (use_mlf) {
+        Matrix<BaseFloat> d;
+        labels.GenDesiredMatrix(d, m.Rows() - sext - eext, repo.CurrentHeader().mSamplePeriod,
+                                repo.Current().Logical().c_str());
+        std::ostringstream ln;
+        ln << out << "/l" << k << ".i32";
+        std::ofstream lf(ln.str().c_str(), std::ios::binary);
+        for (size_t r = 0; r < d.Rows(); r++) {
+          int best = -1;
+          for (size_t c = 0; c < d.Cols(); c++)
+            if (d(r, c) == 1.0f) best = (int)c;
+          lf.write((const char*)&best, 4);
+        }
+        nl = (int)d.Rows();
+      }
+      idx << k << " " << m.Rows() << " " << m.Cols() << " " << repo.CurrentHeader().mSamplePeriod << " "
+          << repo.CurrentHeader().mSampleKind << " " << nl << " " << repo.Current().Logical() << "\n";
+    } catch (std::exception& e) {
+      std::string msg = e.what();
+      for (size_t i = 0; i < msg.size(); i++)
+        if (msg[i] == '\n') msg[i] = ' ';
+      idx << k << " ERROR " << msg << "\n";
+    }
+  }
+  idx.flush();
+  std::_Exit(0);
+}
+
 int main(int argc, char** argv) try {
-  if (argc < 2) { std::cerr << "modes: step | shuffle | train\n"; return 2; }
+  if (argc < 2) { std::cerr << "modes: step | shuffle | train | features\n"; return 2; }
   std::string mode = argv[1];
   if (mode == "step") return cmd_step(argc, argv);
   if (mode == "shuffle") return cmd_shuffle(argc, argv);
   if (mode == "train") return cmd_train(argc, argv);
+  if (mode == "features") return cmd_features(argc, argv);
   std::cerr << "unknown mode\n";
   return 2;
 } catch (std::exception& e) {

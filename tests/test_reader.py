@@ -1,0 +1,175 @@
+"""Native host front end (csrc/host/htkio.cpp; include/tnet_train.h tnet_reader_*, tnet_htk_read) against
+the reference's own FeatureRepository / LabelRepository (src/KaldiLib/Features.cc:1009-1347,
+Labels.cc:42-186), run here through oracle/_ref/ref_harness `features` (tests/golden/make_reader.py ->
+tests/golden/reader.npz: the synthetic HTK inputs are stored in the fixture, examples/01's are
+tests/golden/ex01).
+
+Tolerance: none -- features, class ids, shapes, sample periods and parameter kinds are bit-exact (the
+reader only moves, byte-swaps and int16-decodes values; the _Z mean and the delta / acceleration
+columns use the reference's float operation order).  Error records: the native message equals the
+reference's exception text (KaldiLib's "(function:file:line)" prefix and stack trace removed); for the
+unlabelled-frame error the reference also prints the all-zero one-hot row, compared up to it.
+
+Pure host code: runs on CPU (no device calls)."""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+from tnet_amd import FeatureReader, TnetError, formats, htk_read
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLD = os.path.join(REPO, "tests", "golden")
+EX = os.path.join(GOLD, "ex01")
+
+_G = np.load(os.path.join(GOLD, "reader.npz"))
+META = json.loads(bytes(_G["meta"]).decode())
+
+
+@pytest.fixture(scope="module")
+def workdir(tmp_path_factory):
+    td = tmp_path_factory.mktemp("reader")
+    os.makedirs(td / "d")
+    for n in META["files"]:
+        (td / "d" / n).write_bytes(bytes(_G[f"file:{n}"]))
+    (td / "fb.fea").write_bytes(bytes(_G["file:fb.fea"]))
+    (td / "test.mlf").write_bytes(bytes(_G["mlf"]))
+    (td / "states.txt").write_bytes(bytes(_G["states"]))
+    return td
+
+
+def _kind(name):
+    """TARGETKIND text -> HTK kind code (FeatureRepository::ReadParmKind) and DERIVWINDOWS-less order"""
+    base = {"ANON": 12, "MFCC": 6, "FBANK": 7, "USER": 9}
+    parts = name.split("_")
+    k = base[parts[0]]
+    q = {"E": 0o100, "N": 0o200, "D": 0o400, "A": 0o1000, "Z": 0o4000, "0": 0o20000, "T": 0o100000}
+    for p in parts[1:]:
+        k |= q[p]
+    order = 3 if k & 0o100000 else 2 if k & 0o1000 else 1 if k & 0o400 else 0
+    return k, order
+
+
+def _reader(td, name, threads=3, depth=2):
+    c = META["configs"][name]
+    scp = td / f"{name}.scp"
+    scp.write_text("\n".join(c["scp"]) + "\n")
+    kind, order = _kind(c["target_kind"])
+    cwd = os.getcwd()
+    os.chdir(td)
+    try:
+        return FeatureReader(str(scp), mlf="test.mlf" if c["mlf"] else None, label_map="states.txt",
+                             label_dir=c["label_dir"], start_ext=c["start_ext"], end_ext=c["end_ext"],
+                             swap=bool(c["swap"]), target_kind=kind, deriv_order=order, threads=threads, depth=depth)
+    finally:
+        os.chdir(cwd)
+
+
+OK_CONFIGS = [n for n, c in META["configs"].items() if all("error" not in r for r in c["records"])]
+ERR_CONFIGS = [n for n, c in META["configs"].items() if any("error" in r for r in c["records"])]
+
+
+@pytest.mark.parametrize("name", OK_CONFIGS)
+def test_reader_matches_reference_feature_repository(workdir, name):
+    cwd = os.getcwd()
+    r = _reader(workdir, name)
+    os.chdir(workdir)
+    try:
+        got = list(r)
+    finally:
+        os.chdir(cwd)
+    recs = META["configs"][name]["records"]
+    assert len(got) == len(recs)
+    for k, (rec, (logical, x, lab, per, kind)) in enumerate(zip(recs, got)):
+        ref_x, ref_lab = _G[f"{name}:x{k}"], _G[f"{name}:lab{k}"]
+        assert (x.shape, per, kind, logical) == ((rec["rows"], rec["cols"]), rec["period"], rec["kind"], rec["logical"])
+        assert np.array_equal(x.view(np.uint32), ref_x.view(np.uint32)), f"{name} record {k}: features differ"
+        assert np.array_equal(lab, ref_lab), f"{name} record {k}: class ids differ"
+
+
+@pytest.mark.parametrize("name", ERR_CONFIGS)
+def test_reader_errors_match_reference(workdir, name):
+    ref = META["configs"][name]["records"][0]["error"]
+    cwd = os.getcwd()
+    r = _reader(workdir, name)
+    os.chdir(workdir)
+    try:
+        with pytest.raises(TnetError) as ei:
+            list(r)
+    finally:
+        os.chdir(cwd)
+    msg = str(ei.value).split(": status -")[0]
+    native = str(ei.value).split("reader_next: status ", 1)[1].split(": ", 1)[1].strip()
+    want = ref.split(" content:")[0].strip()
+    assert native.startswith(want), (native, want, msg)
+
+
+def test_reader_examples01_matches_reference():
+    """the first 20 examples/01 utterances with the run_test recipe's 25 / 25 frame extension and the MLF:
+    float bytes (sha256), shapes and class ids as the reference's FeatureRepository / LabelRepository"""
+    ex = META["ex01"]
+    cwd = os.getcwd()
+    os.chdir(EX)
+    try:
+        lines = [l.strip() for l in open("test.scp") if l.strip()][:20]
+        scp = os.path.join(os.path.dirname(EX), "..", "..", "tests", "golden", "ex01", "test.scp")  # noqa: F841
+        r = FeatureReader("test.scp", mlf="test_3s.mlf", label_map="mono_state_phn_set_135_phn", start_ext=25,
+                          end_ext=25, threads=4, depth=8)
+        for k, rec in enumerate(ex["records"]):
+            logical, x, lab, per, kind = r.next_raw()
+            assert logical == lines[k] == rec["utt"]
+            assert (x.shape, per, kind) == ((rec["rows"], rec["cols"]), rec["period"], rec["kind"])
+            assert hashlib.sha256(np.ascontiguousarray(x).tobytes()).hexdigest() == rec["sha256"]
+            assert np.array_equal(lab, _G[f"ex01:lab{k}"])
+    finally:
+        os.chdir(cwd)
+
+
+def test_reader_matches_python_reader_on_all_of_examples01():
+    """all 100 utterances, native vs tnet_amd.formats (itself pinned by the reference epoch fixtures)"""
+    c = formats.read_corpus(os.path.join(EX, "test.scp"), os.path.join(EX, "test_3s.mlf"),
+                            os.path.join(EX, "mono_state_phn_set_135_phn"))
+    cwd = os.getcwd()
+    os.chdir(EX)
+    try:
+        got = list(FeatureReader("test.scp", mlf="test_3s.mlf", label_map="mono_state_phn_set_135_phn", threads=8,
+                                 depth=4))
+    finally:
+        os.chdir(cwd)
+    assert len(got) == 100
+    for (_, x, lab, per, _), xr, lr in zip(got, c.feats, c.labels):
+        assert np.array_equal(x, xr) and np.array_equal(lab, lr) and per == 100000
+
+
+@pytest.mark.parametrize("threads,depth", [(1, 1), (2, 1), (8, 3), (16, 64)])
+def test_reader_order_and_rewind(threads, depth):
+    """script order whatever the pool size / read-ahead depth; rewind restarts the list"""
+    cwd = os.getcwd()
+    os.chdir(EX)
+    try:
+        r = FeatureReader("test.scp", mlf="test_3s.mlf", label_map="mono_state_phn_set_135_phn", threads=threads,
+                          depth=depth)
+        assert len(r) == 100
+        first = [(n, x.sum(dtype=np.float64)) for n, x, *_ in r]
+        assert [n for n, _ in first] == [l.strip() for l in open("test.scp") if l.strip()]
+        r.rewind()
+        again = [(n, x.sum(dtype=np.float64)) for n, x, *_ in r]
+        assert again == first
+    finally:
+        os.chdir(cwd)
+
+
+def test_htk_read_single_record(workdir):
+    """tnet_htk_read: one record without a reader, incl. a [s,e] range and edge extension"""
+    x, per, kind = htk_read(str(workdir / "d" / "long.fea") + "[5,20]", start_ext=3, end_ext=3)
+    assert np.array_equal(x, _G["ranges:x0"]) and per == 100000 and kind == 7
+    full = formats.read_htk(str(workdir / "d" / "long.fea"))
+    y, _, _ = htk_read(str(workdir / "d" / "long.fea"), start_ext=2, end_ext=4)
+    assert np.array_equal(y, formats.extend_frames(full, 2, 4))
+
+
+def test_reader_missing_script():
+    with pytest.raises(TnetError, match="Cannot not open list file"):
+        FeatureReader("/nonexistent/list.scp")
