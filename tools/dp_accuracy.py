@@ -72,10 +72,28 @@ def worker(a):
             dist.all_reduce(torch.from_numpy(v))
 
         comm = tnet_amd.Comm.host(rank, world, allreduce)
-    T = teacher(DIMS[0], DIMS[-1])
-    mine = tnet_amd.shard_utterances(list(range(a.utts)), rank, world)
-    train = [utterance(i, T, 0) for i in mine]
-    held = [utterance(i, T, 1) for i in range(a.cv_utts)] if rank == 0 else []
+    transform = None
+    if a.corpus == "ex01":
+        # examples/01's own files (tests/golden/ex01): raw 23-dim FBANK through the native reader, the real
+        # Hamm_dct_norm front end on the GPU (25/25 frame extension) -> 598 dims; the last 10 of the 100
+        # utterances held out
+        ex = os.path.join(REPO, "tests", "golden", "ex01")
+        cwd = os.getcwd()
+        os.chdir(ex)
+        try:
+            utts = [(x.copy(), lab.copy()) for _, x, lab, _, _ in
+                    tnet_amd.FeatureReader("test.scp", mlf="test_3s.mlf", label_map="mono_state_phn_set_135_phn")]
+        finally:
+            os.chdir(cwd)
+        transform = Network(path=os.path.join(ex, "Hamm_dct_norm"))
+        mine = tnet_amd.shard_utterances(list(range(90)), rank, world)
+        train = [utts[i] for i in mine]
+        held = utts[90:] if rank == 0 else []
+    else:
+        T = teacher(DIMS[0], DIMS[-1])
+        mine = tnet_amd.shard_utterances(list(range(a.utts)), rank, world)
+        train = [utterance(i, T, 0) for i in mine]
+        held = [utterance(i, T, 1) for i in range(a.cv_utts)] if rank == 0 else []
     from tnet_amd import newbob
     net = Network.from_layers(formats.gen_mlp_init(DIMS, seed=SEED))
     lr = a.lr * (world if a.scale == "linear" else world ** 0.5)
@@ -90,6 +108,8 @@ def worker(a):
     def cv_eval():
         cobj = Objective()
         cv = Trainer(net, cobj, bunchsize=a.bunch, cachesize=a.cache, seed=0, randomize=False, crossval=True)
+        if transform is not None:
+            cv.set_transform(transform, 25, 25)
         cv.train_corpus([x for x, _ in held], [y for _, y in held])
         return cobj.stats()
 
@@ -107,6 +127,8 @@ def worker(a):
     for ep in range(a.epochs):
         obj = Objective()
         tr = Trainer(net, obj, bunchsize=a.bunch, cachesize=a.cache, seed=1 + 1000 * ep + rank)
+        if transform is not None:
+            tr.set_transform(transform, 25, 25)
         if comm is not None:
             tr.set_comm(comm)
         ep_lr = float(nb.lrate) if nb is not None else lr
@@ -148,7 +170,8 @@ def worker(a):
         ce, cf, cc = bcast_cv()
         log.append({"final_best": True, "cv_xent_per_frame": ce / cf, "cv_acc": 100.0 * cc / cf})
     if rank == 0:
-        print("RESULT " + json.dumps({"world": world, "lr": lr, "lr_scaling": a.scale, "newbob": a.newbob,
+        print("RESULT " + json.dumps({"world": world, "corpus": a.corpus, "lr": lr, "lr_scaling": a.scale,
+                                      "newbob": a.newbob,
                                       "warmup": a.warmup, "end_halving_inc": a.end_halving_inc,
                                       "start_halving_inc": a.start_halving_inc,
                                       "bunch_per_rank": a.bunch,
@@ -181,6 +204,9 @@ def main():
     ap.add_argument("--start-halving-inc", type=float, default=0.5)
     ap.add_argument("--warmup", type=float, default=0.0)
     ap.add_argument("--progress", default="", help="rank 0 appends one JSON line per epoch to this file")
+    ap.add_argument("--corpus", default="teacher", choices=["teacher", "ex01"],
+                    help="teacher: the synthetic teacher-labelled corpus; ex01: examples/01's own files (90 train / "
+                         "10 held-out utterances) through the real Hamm_dct_norm front end")
     a = ap.parse_args()
     if a.mode == "worker":
         worker(a)
@@ -193,7 +219,7 @@ def main():
                 str(a.utts), "--cv-utts", str(a.cv_utts), "--bunch", str(a.bunch), "--cache", str(a.cache), "--lr",
                 str(a.lr), "--scale", a.scale, "--end-halving-inc", str(a.end_halving_inc),
                 "--start-halving-inc", str(a.start_halving_inc), "--warmup", str(a.warmup),
-                "--progress", a.progress]
+                "--progress", a.progress, "--corpus", a.corpus]
         if a.newbob:
             args.append("--newbob")
         procs = [subprocess.Popen(args, env=dict(env, RANK=str(r)), stdout=subprocess.PIPE, stderr=subprocess.PIPE,
