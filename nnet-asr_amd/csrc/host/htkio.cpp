@@ -96,11 +96,12 @@ FileRecord ParseFileRecord(const std::string& line) {
   return r;
 }
 
-HtkHeader ReadHtkHeader(const std::string& physical, bool swap) {
+HtkHeader ReadHtkHeader(const std::string& physical, bool swap, const std::string& base) {
   std::string name = physical;
   int a, b;
   SplitRange(name, a, b);
-  Fd f(open(name.c_str(), O_RDONLY));
+  const std::string where = (!base.empty() && !name.empty() && name[0] != '/') ? base + "/" + name : name;
+  Fd f(open(where.c_str(), O_RDONLY));
   if (f.fd < 0) Fail("Cannot open feature file: '" + name + "'");
   unsigned char hb[12];
   if (pread(f.fd, hb, 12, 0) != 12) Fail("Invalid HTK header in feature file: '" + name + "'");
@@ -112,8 +113,10 @@ void ReadHtkFeatures(const FileRecord& rec, const FeatureConfig& cfg, int& targe
   std::string name = rec.physical;
   int from_frame = 0, to_frame = 0;
   const bool ranged = SplitRange(name, from_frame, to_frame);
+  std::string where = name;  // the file opened: relative names against the directory of the record's creation
+  if (!rec.base.empty() && !name.empty() && name[0] != '/') where = rec.base + "/" + name;
 
-  Fd f(open(name.c_str(), O_RDONLY));
+  Fd f(open(where.c_str(), O_RDONLY));
   if (f.fd < 0) Fail("Cannot open feature file: '" + name + "'");
   unsigned char hb[12];
   if (pread(f.fd, hb, 12, 0) != 12) Fail("Invalid HTK header in feature file: '" + name + "'");
@@ -500,14 +503,21 @@ FeatureReader::FeatureReader(const std::string& scp, const FeatureConfig& cfg, s
     : mCfg(cfg), mLabels(std::move(labels)), mThreads(std::max(1, threads)), mDepth(std::max(1, depth)) {
   std::ifstream in(scp.c_str());
   if (!in.good()) Fail("Cannot not open list file " + scp);
+  // relative feature paths are taken from the working directory at creation (the reference's, which
+  // reads them later from the same directory): the pool reads ahead, so a later chdir must not move them
+  char cwd[4096];
+  const std::string base = getcwd(cwd, sizeof(cwd)) ? std::string(cwd) : std::string();
   std::string tok;
-  while (in >> tok) mRecords.push_back(ParseFileRecord(tok));
+  while (in >> tok) {
+    mRecords.push_back(ParseFileRecord(tok));
+    mRecords.back().base = base;
+  }
   mTargetKind = cfg.targetKind;
   mDerivOrder = cfg.derivOrder;
   if (!mRecords.empty()) {
     // the repository's latched target kind / derivative order come from the first file it reads
     try {
-      HtkHeader h = ReadHtkHeader(mRecords[0].physical, cfg.swap);
+      HtkHeader h = ReadHtkHeader(mRecords[0].physical, cfg.swap, mRecords[0].base);
       unsigned kind = h.sampleKind & ~kParmC;
       if (mTargetKind == kParmAnon) {
         mTargetKind = (int)kind;

@@ -55,6 +55,7 @@ struct HtkHeader {
 struct FileRecord {
   std::string logical, physical;
   float weight = 1.0f;
+  std::string base;  // directory relative physical names are opened from ("" = the current one)
 };
 FileRecord ParseFileRecord(const std::string& line);
 
@@ -82,7 +83,7 @@ void ReadHtkFeatures(const FileRecord& rec, const FeatureConfig& cfg, int& targe
                      Utterance& out);
 
 // Header of a record's physical file (frame-range suffix ignored), byte order as configured.
-HtkHeader ReadHtkHeader(const std::string& physical, bool swap);
+HtkHeader ReadHtkHeader(const std::string& physical, bool swap, const std::string& base = std::string());
 
 // MakeHtkFileName (Common.cc:118-172)
 std::string MakeHtkFileName(const std::string& in, const char* outDir, const char* outExt);

@@ -173,3 +173,20 @@ def test_htk_read_single_record(workdir):
 def test_reader_missing_script():
     with pytest.raises(TnetError, match="Cannot not open list file"):
         FeatureReader("/nonexistent/list.scp")
+
+
+def test_reader_paths_fixed_at_creation(tmp_path):
+    """relative script paths resolve against the working directory at creation: the pool reads ahead, so a
+    later chdir (the consumer's business) must not move them"""
+    cwd = os.getcwd()
+    os.chdir(EX)
+    try:
+        r = FeatureReader("test.scp", mlf="test_3s.mlf", label_map="mono_state_phn_set_135_phn", threads=2, depth=2)
+    finally:
+        os.chdir(cwd)
+    os.chdir(tmp_path)
+    try:
+        n = sum(1 for _ in r)
+    finally:
+        os.chdir(cwd)
+    assert n == 100
