@@ -188,3 +188,16 @@ def test_reader_paths_fixed_at_creation(tmp_path):
     finally:
         os.chdir(cwd)
     assert n == 100
+
+
+def test_reader_under_sanitizers():
+    """tools/htkio_sanitize.sh: the reader built with ThreadSanitizer (the read-ahead pool: several pool
+    shapes, rewind mid-list, a reader abandoned with workers still reading) and with AddressSanitizer +
+    UndefinedBehaviorSanitizer (the decoders) over examples/01, with and without frame extension"""
+    import shutil
+    import subprocess
+    if not shutil.which("g++"):
+        pytest.skip("no host compiler")
+    p = subprocess.run([os.path.join(REPO, "tools", "htkio_sanitize.sh")], capture_output=True, text=True, timeout=600)
+    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-4000:]
+    assert p.stdout.count("htkio_sanitize ok") == 4
