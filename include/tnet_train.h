@@ -150,7 +150,8 @@ int tnet_htk_read(const char* record, int swap, int start_ext, int end_ext, floa
 /* the cache fill of TNetCu.cc:376-419 from a reader: up to max_utts utterances (< 0: to the end of the
  * list) into the trainer, each training the cache whenever it fills; returns the frames added (< 0 error).
  * The reader's STARTFRMEXT / ENDFRMEXT must be the transform's (tnet_trainer_set_transform); without
- * a transform the context rows are trimmed. */
+ * a transform the context rows are trimmed.  An utterance holding a NaN / Inf is rejected with
+ * TNetCu's CheckData error (TNetCu.cc:386), as the reference driver does. */
 long tnet_trainer_add_reader(TnetTrainer* t, TnetFeatureReader* r, long max_utts);
 
 /* ---- RBM pre-training (CuRbm, cuRbm.cc; the TRbmCu loop, TRbmCu.cc:291-357) ----------------

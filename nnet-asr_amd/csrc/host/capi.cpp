@@ -490,6 +490,8 @@ long tnet_trainer_add_reader(TnetTrainer* t, TnetFeatureReader* r, long max_utts
       const tnetio::Utterance* u = r->r->Next();
       if (!u) break;
       if (u->labels.empty()) Error("tnet_trainer_add_reader: the reader has no labels (no MLF)");
+      const std::string bad = tnetio::CheckDataError(*u);  // feats_host.CheckData (TNetCu.cc:386)
+      if (!bad.empty()) Error(bad);
       t->t->AddUtteranceExtended(u->feats.data(), (size_t)u->rows, (size_t)u->cols, (size_t)u->cols, u->labels.data(),
                                  (size_t)r->start_ext, (size_t)r->end_ext);
       frames += (long)u->labels.size();

@@ -316,11 +316,35 @@ void ReadHtkFeatures(const FileRecord& rec, const FeatureConfig& cfg, int& targe
       }
   }
 
+  // CheckData's scan (the reference driver's, Matrix.h:238-252), done here on the reading thread
+  out.bad_row = out.bad_col = -1;
+  {
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(out.feats.data());
+    const size_t n = out.feats.size();
+    uint32_t any = 0;
+    for (size_t k = 0; k < n; k++) any |= (uint32_t)((w[k] & 0x7F800000u) == 0x7F800000u);
+    if (any)
+      for (size_t k = 0; k < n; k++)
+        if ((w[k] & 0x7F800000u) == 0x7F800000u) {
+          out.bad_row = (int)(k / (size_t)trg_vec);
+          out.bad_col = (int)(k % (size_t)trg_vec);
+          out.bad_value = out.feats[k];
+          break;
+        }
+  }
   out.logical = rec.logical;
   out.samplePeriod = h.samplePeriod;
   // Features.cc:1345-1347 then 1383-1385: the derivative flags of the delivered order
   out.kind = (targetKind & ~(kParmD | kParmA | kParmT)) |
              (derivOrder == 3 ? (kParmD | kParmA | kParmT) : derivOrder == 2 ? (kParmD | kParmA) : derivOrder == 1 ? kParmD : 0);
+}
+
+std::string CheckDataError(const Utterance& u) {
+  if (u.bad_row < 0) return std::string();
+  std::ostringstream os;
+  os << "Invalid value: " << u.bad_value << " in matrix row: " << u.bad_row << " col: " << u.bad_col
+     << " file: " << u.logical;
+  return os.str();
 }
 
 std::string MakeHtkFileName(const std::string& in, const char* outDir, const char* outExt) {

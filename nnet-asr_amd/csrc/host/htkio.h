@@ -74,7 +74,14 @@ struct Utterance {
   int samplePeriod = 0;      // of the file (GenDesiredMatrix's sourceRate)
   int kind = 0;              // the matrix's parameter kind (mHeader.mSampleKind after the read)
   std::vector<int> labels;   // class ids of rows - startExt - endExt frames (empty without labels)
+  // the first NaN / Inf of the matrix in row-major order (bad_row < 0: none) -- what TNetCu's
+  // feats_host.CheckData (TNetCu.cc:386, Matrix.h:238-252) rejects; found by the reading thread
+  int bad_row = -1, bad_col = -1;
+  float bad_value = 0.0f;
 };
+
+// TNetCu's CheckData message for u's first invalid value ("" if none)
+std::string CheckDataError(const Utterance& u);
 
 // Reads one record into `out` (feats, rows, cols, samplePeriod, kind).  `targetKind` / `derivOrder`
 // are the repository's latched state (ANON / < 0 resolve to this file's).  Throws std::runtime_error

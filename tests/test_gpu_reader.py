@@ -82,3 +82,26 @@ def test_reader_extension_must_match_the_transform():
             tr.add_reader(r, 1)
     finally:
         os.chdir(cwd)
+
+
+def test_add_reader_rejects_invalid_values(tmp_path):
+    """TNetCu checks every utterance for NaN / Inf before the transform (feats_host.CheckData,
+    TNetCu.cc:386, Matrix.h:238-252): the reader's intake rejects it with the same message"""
+    import tnet_amd
+    os.makedirs(tmp_path / "f")
+    x = np.zeros((20, 3), np.float32)
+    x[7, 2] = np.nan
+    formats.write_htk(str(tmp_path / "f" / "a.fea"), x)
+    (tmp_path / "list.scp").write_text("f/a.fea\n")
+    (tmp_path / "a.mlf").write_text('#!MLF!#\n"*/a.lab"\n0 2000000 s0\n.\n')
+    (tmp_path / "states").write_text("s0\ns1\n")
+    net = tnet_amd.Network.from_layers(formats.gen_mlp_init([3, 8, 2], seed=1))
+    tr = tnet_amd.Trainer(net, tnet_amd.Objective(), bunchsize=4, cachesize=16, seed=1)
+    cwd = os.getcwd()
+    os.chdir(tmp_path)
+    try:
+        r = tnet_amd.FeatureReader("list.scp", mlf="a.mlf", label_map="states")
+    finally:
+        os.chdir(cwd)
+    with pytest.raises(tnet_amd.TnetError, match=r"Invalid value: nan in matrix row: 7 col: 2 file: f/a.fea"):
+        tr.add_reader(r)
