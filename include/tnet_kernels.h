@@ -231,6 +231,17 @@ int tnet_affine_update_bwd_pair(const float* X, TnetMatrixDim dX, const float* E
                                 TnetMatrixDim dE2, const float* W2, TnetMatrixDim dW2, const float* Ybelow,
                                 int strideYbelow, float* Eo, TnetMatrixDim dEo, float* colpart2, int ldcolpart2,
                                 void* stream);
+/* Two tnet_affine_update_bias calls -- the updates of two layers (cuBiasedLinearity.cc:46-64) -- in ONE
+ * launch; the two must be independent (distinct W, b and momentum buffers).  For small layers whose
+ * tile grids together fit the CUs (CuNetwork runs the last two updates of a step this way, e.g. the
+ * MLP3's 1024x135 and 598x1024): results identical to the two calls made with the same tile
+ * configuration; TNET_ERR_UNSUPPORTED when the two grids do not fit one round (make the two calls). */
+int tnet_affine_update_bias_pair(const float* X, TnetMatrixDim dX, const float* E, TnetMatrixDim dE, float* W,
+                                 TnetMatrixDim dW, float* corrW, int strideCorr, float scale, float mmt, float l2,
+                                 const float* colpart, int ldcolpart, float* b, float* corr_b, const float* X2,
+                                 TnetMatrixDim dX2, const float* E2, TnetMatrixDim dE2, float* W2, TnetMatrixDim dW2,
+                                 float* corrW2, int strideCorr2, float scale2, float mmt2, float l22,
+                                 const float* colpart2, int ldcolpart2, float* b2, float* corr_b2, void* stream);
 /* G = X^T E into a gradient buffer (data-parallel path: all-reduced before tnet_sgd_update). */
 int tnet_affine_grad(const float* X, TnetMatrixDim dX, const float* E, TnetMatrixDim dE, float* G,
                      TnetMatrixDim dG, void* stream);

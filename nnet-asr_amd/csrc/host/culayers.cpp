@@ -188,6 +188,36 @@ bool CuBiasedLinearity::UpdateFromColsumWithBwd(const CuMatrix<BaseFloat>& X, co
   return true;
 }
 
+bool CuBiasedLinearity::UpdatePairFromColsum(const CuMatrix<BaseFloat>& X, const CuMatrix<BaseFloat>& E,
+                                             const CuMatrix<BaseFloat>& colpart, CuBiasedLinearity& other,
+                                             const CuMatrix<BaseFloat>& X2, const CuMatrix<BaseFloat>& E2,
+                                             const CuMatrix<BaseFloat>& colpart2) {
+  CuProfileScope p("CuBiasedLinearity::Update (pair)");
+  float scale, l2, scale2, l22;
+  UpdateConstants(X.Rows(), &scale, &l2);
+  other.UpdateConstants(X2.Rows(), &scale2, &l22);
+  const bool mmt = mMomentum != 0.0f, mmt2 = other.mMomentum != 0.0f;
+  const std::string sa = std::to_string(GetNInputs()) + "x" + std::to_string(GetNOutputs());
+  const std::string sb = std::to_string(other.GetNInputs()) + "x" + std::to_string(other.GetNOutputs());
+  KTScope kt("gemm_upd+upd:" + sa + "+" + sb,
+             2.0 * X.Rows() * GetNInputs() * GetNOutputs() + 2.0 * X2.Rows() * other.GetNInputs() * other.GetNOutputs(),
+             2);
+  const int st = tnet_affine_update_bias_pair(
+      X.pCUData(), X.Dim(), E.pCUData(), E.Dim(), mLinearity.pCUData(), mLinearity.Dim(),
+      mmt ? mLinearityCorrection.pCUData() : nullptr, (int)mLinearityCorrection.Stride(), scale, mMomentum, l2,
+      colpart.pCUData(), (int)colpart.Stride(), mBias.pCUData(), mmt ? mBiasCorrection.pCUData() : nullptr,
+      X2.pCUData(), X2.Dim(), E2.pCUData(), E2.Dim(), other.mLinearity.pCUData(), other.mLinearity.Dim(),
+      mmt2 ? other.mLinearityCorrection.pCUData() : nullptr, (int)other.mLinearityCorrection.Stride(), scale2,
+      other.mMomentum, l22, colpart2.pCUData(), (int)colpart2.Stride(), other.mBias.pCUData(),
+      mmt2 ? other.mBiasCorrection.pCUData() : nullptr, S);
+  if (st == TNET_ERR_UNSUPPORTED) {
+    kt.Cancel();
+    return false;
+  }
+  TNET_SAFE_CALL(st);
+  return true;
+}
+
 void CuBiasedLinearity::Update() { UpdateFrom(GetInput(), GetErrorInput()); }
 
 void CuBiasedLinearity::ComputeGradient() {

@@ -51,6 +51,12 @@ class CuBiasedLinearity : public CuUpdatableComponent {
   /// UpdateFromColsum and, in the same launch, the backward GEMM of the layer below
   /// (tnet_affine_update_bwd_pair): Eo = (E2 below.W^T) .* Ybelow (1 - Ybelow) + Eo's slab sums into
   /// colpart2.  False (nothing enqueued) when the pair kernel does not take these shapes.
+  /// This layer's UpdateFromColsum(X, E, colpart) and other's UpdateFromColsum(X2, E2, colpart2) in ONE
+  /// launch (tnet_affine_update_bias_pair) when the two small grids fit one round over the CUs; false:
+  /// nothing enqueued (make the two calls).
+  bool UpdatePairFromColsum(const CuMatrix<BaseFloat>& X, const CuMatrix<BaseFloat>& E,
+                            const CuMatrix<BaseFloat>& colpart, CuBiasedLinearity& other, const CuMatrix<BaseFloat>& X2,
+                            const CuMatrix<BaseFloat>& E2, const CuMatrix<BaseFloat>& colpart2);
   bool UpdateFromColsumWithBwd(const CuMatrix<BaseFloat>& X, const CuMatrix<BaseFloat>& E,
                                const CuMatrix<BaseFloat>& colpart, const CuBiasedLinearity& below,
                                const CuMatrix<BaseFloat>& E2, const CuMatrix<BaseFloat>& Ybelow,

@@ -416,6 +416,14 @@ void CuNetwork::TrainBunch(const CuMatrix<BaseFloat>& X, const CuVector<int>& la
                                        eo->pCUData(), eo->Dim(), 1, S));
       }
     }
+    // the last layer trained here: the held-back update of the layer above and this layer's own are
+    // independent (each reads its X, E and writes its own W, b) and no backward GEMM is left -- small ones
+    // (both grids in one round over the CUs) go out as ONE launch
+    if ((stopper || l == 0) && pend.lin && !exchange && err_colsum && lin->LearnRate() > 0.0f &&
+        pend.lin->UpdatePairFromColsum(*pend.X, *pend.E, *mColPart[pend.l], *lin, *acts[l], *err, *mColPart[l])) {
+      pend.lin = nullptr;
+      break;
+    }
     flush();  // a held-back update no backward GEMM took
     if (lin->LearnRate() > 0.0f) {
       if (exchange) {

@@ -1743,6 +1743,20 @@ void gemm16_pair_kernel(const GemmP pa, const GemmP pb, const int na) {
   else gemm16_body<BMB, BNB, 64, 2, 2, 2, 0, AKB, BKB, EPIB, PXB>(pb, smem, (int)blockIdx.x - na);
 }
 
+// Two independent SMALL weight updates (fused SGD + bias SGD, TN) in ONE launch, same tile
+// configuration for both (64x64, BK 32, four slots, 4x1 waves), blocks [0, na) update A, the rest B.
+// For the step's last two updates when neither fills the chip (the MLP3's 1024x135 and 598x1024: 48 +
+// 160 tiles): both grids run side by side in one round instead of back to back (and the 1024x135 one
+// without its split-K combine launch).  A second HIP stream for the same overlap was measured slower
+// (the cross-stream fork / join costs more than the overlap saves at this size).
+template <int BM, int BN, int BK, int WM, int WN, int S>
+__global__ __launch_bounds__(WM * WN * 64) __attribute__((amdgpu_waves_per_eu(1, 1)))
+void gemm16_upd_pair_kernel(const GemmP pa, const GemmP pb, const int na) {
+  __shared__ __attribute__((aligned(16))) float smem[gemm16_smem_floats<BM, BN, BK, S, EPI_SGD_B, false>()];
+  if ((int)blockIdx.x < na) gemm16_body<BM, BN, BK, WM, WN, S, 0, false, false, EPI_SGD_B, false>(pa, smem, blockIdx.x);
+  else gemm16_body<BM, BN, BK, WM, WN, S, 0, false, false, EPI_SGD_B, false>(pb, smem, (int)blockIdx.x - na);
+}
+
 // ---------------------------------------------------------------------------------------------
 // split-K combine: C = epilogue(P[0] + P[1] + ... + P[splits-1]) summed in split order (fixed, so the
 // result is deterministic), then the same epilogue arithmetic as gemm16_kernel; 4 columns / thread
@@ -2375,6 +2389,31 @@ static int launch_pair_upd_bwd(GemmP pu, GemmP pb, hipStream_t st) {
   return TNET_OK;
 }
 
+// tnet_affine_update_bias_pair: both updates in one gemm16_upd_pair_kernel launch when their 64x64 grids
+// together fit one round over the CUs; TNET_ERR_UNSUPPORTED otherwise (the caller makes the two calls)
+static int launch_upd_pair(GemmP pa, GemmP pb, hipStream_t st) {
+  if (forced_cfg() >= 0 || !g_pair) return TNET_ERR_UNSUPPORTED;
+  if (pa.M <= 0 || pa.N <= 0 || pb.M <= 0 || pb.N <= 0) return TNET_ERR_UNSUPPORTED;
+  if (!g_cus) {
+    int dev = 0;
+    hipDeviceProp_t prop;
+    if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess)
+      return TNET_ERR_UNSUPPORTED;
+    g_cus = prop.multiProcessorCount;
+  }
+  const int na = cdiv(pa.M, 64) * cdiv(pa.N, 64), nb = cdiv(pb.M, 64) * cdiv(pb.N, 64);
+  if (na + nb > g_cus - g_reserve) return TNET_ERR_UNSUPPORTED;
+  // the 16x16 kernel's 32-bit k-tile offsets (launch_cfg's check, BK 32, m- / n-contiguous operands)
+  for (const GemmP* q : {&pa, &pb})
+    if (4 * (32L * q->lda + q->M) >= (1L << 32) || 4 * (32L * q->ldb + q->N) >= (1L << 32)) return TNET_ERR_UNSUPPORTED;
+  pa.group = pb.group = g_group > 0 ? g_group : 8;
+  pa.early_issue = pb.early_issue = g_early;
+  pa.wt = pb.wt = g_wt;
+  gemm16_upd_pair_kernel<64, 64, 32, 4, 1, 4><<<na + nb, 256, 0, st>>>(pa, pb, na);
+  TNET_LAUNCH_CHECK();
+  return TNET_OK;
+}
+
 static bool aligned16(const void* q) { return ((uintptr_t)q & 15) == 0; }
 
 static int check_common(const GemmP& p) {
@@ -2589,6 +2628,45 @@ extern "C" int tnet_affine_update_bias(const float* X, TnetMatrixDim dX, const f
   if (st) return st;
   if (p.M <= 0 || p.N <= 0) return TNET_OK;
   return launch_gemm<false, false, EPI_SGD_B>(p, (hipStream_t)stream);
+}
+
+// the GemmP of tnet_affine_update_bias's launch (TNET_ERR_ARG on bad arguments)
+static int update_bias_params(GemmP& p, const float* X, TnetMatrixDim dX, const float* E, TnetMatrixDim dE, float* W,
+                              TnetMatrixDim dW, float* corrW, int strideCorr, float scale, float mmt, float l2,
+                              const float* colpart, int ldcolpart, float* b, float* corr_b) {
+  if (dX.rows != dE.rows || dW.rows != dX.cols || dW.cols != dE.cols || !colpart || !b || ldcolpart < dE.cols)
+    return TNET_ERR_ARG;
+  if (mmt != 0.f && (!corrW || !corr_b)) return TNET_ERR_ARG;
+  p = GemmP{};
+  p.M = dX.cols; p.N = dE.cols; p.K = dX.rows;
+  p.A = X; p.lda = dX.stride; p.B = E; p.ldb = dE.stride; p.C = W; p.ldc = dW.stride;
+  p.corr = (mmt != 0.f || corrW) ? corrW : nullptr; p.ldcorr = strideCorr;
+  if (p.corr && (p.ldcorr & 3)) return TNET_ERR_ARG;
+  p.scale = scale; p.mmt = mmt; p.l2 = l2;
+  p.bpart = colpart; p.ldbpart = ldcolpart; p.bslabs = tnet_colsum_slabs(dE.rows);
+  p.bvec = b; p.bcorr = mmt != 0.f ? corr_b : nullptr; p.bscale = scale; p.bmmt = mmt;
+  return check_common(p);
+}
+
+extern "C" int tnet_affine_update_bias_pair(const float* X, TnetMatrixDim dX, const float* E, TnetMatrixDim dE,
+                                           float* W, TnetMatrixDim dW, float* corrW, int strideCorr, float scale,
+                                           float mmt, float l2, const float* colpart, int ldcolpart, float* b,
+                                           float* corr_b, const float* X2, TnetMatrixDim dX2, const float* E2,
+                                           TnetMatrixDim dE2, float* W2, TnetMatrixDim dW2, float* corrW2,
+                                           int strideCorr2, float scale2, float mmt2, float l22,
+                                           const float* colpart2, int ldcolpart2, float* b2, float* corr_b2,
+                                           void* stream) {
+  // two tnet_affine_update_bias calls in one launch; they must be independent (distinct W, b, momentum
+  // buffers; neither reads what the other writes)
+  GemmP pa, pb;
+  int st = update_bias_params(pa, X, dX, E, dE, W, dW, corrW, strideCorr, scale, mmt, l2, colpart, ldcolpart, b,
+                              corr_b);
+  if (st) return st;
+  st = update_bias_params(pb, X2, dX2, E2, dE2, W2, dW2, corrW2, strideCorr2, scale2, mmt2, l22, colpart2, ldcolpart2,
+                          b2, corr_b2);
+  if (st) return st;
+  if (W == W2 || b == b2 || (corrW && corrW == corrW2)) return TNET_ERR_ARG;
+  return launch_upd_pair(pa, pb, (hipStream_t)stream);
 }
 
 extern "C" int tnet_affine_update_bwd_pair(const float* X, TnetMatrixDim dX, const float* E, TnetMatrixDim dE,

@@ -620,3 +620,49 @@ def test_check_class_first_max_wins():
     m = DeviceArray.vector(np.zeros(3, np.int32))
     check(lib().tnetF_check_class(dO.ptr, dD.ptr, m.ptr, dO.dim, S()))
     np.testing.assert_array_equal(m.numpy()[:, 0], [1, 1, 0])
+
+
+@pytest.mark.parametrize("mmt", [0.0, 0.5])
+@pytest.mark.parametrize("rows,a_in,a_out,b_in,b_out", [(1024, 1024, 135, 598, 1024), (1024, 256, 135, 440, 256),
+                                                        (512, 1024, 2048, 440, 2048)])
+def test_affine_update_bias_pair(mmt, rows, a_in, a_out, b_in, b_out):
+    """tnet_affine_update_bias_pair (two layers' fused weight + bias SGD in one launch, both on the 64x64
+    configuration): each layer's W, momentum, b against the fp64 formula with tnet_affine_update_bias's
+    tolerance; TNET_ERR_UNSUPPORTED when the two grids exceed one round over the CUs (the last case)"""
+    scale, l2 = -0.3 / rows, -1e-4
+    sides = []
+    for k, (n_in, n_out) in enumerate([(a_in, a_out), (b_in, b_out)]):
+        X, E = rnd((rows, n_in), 40 + k), rnd((rows, n_out), 50 + k, 0.01)
+        W, corr = rnd((n_in, n_out), 60 + k, 0.1), rnd((n_in, n_out), 70 + k, 0.01)
+        b, corr_b = rnd(n_out, 80 + k), rnd(n_out, 90 + k, 0.01)
+        P = slab_sums(E).astype(np.float32)
+        d = dict(X=X, E=E, W=W, corr=corr, b=b, corr_b=corr_b, P=P, dX=DeviceArray.from_numpy(X),
+                 dE=DeviceArray.from_numpy(E), dW=DeviceArray.from_numpy(W), dP=DeviceArray.from_numpy(P),
+                 db=DeviceArray.vector(b), dC=DeviceArray.from_numpy(corr) if mmt else None,
+                 dCb=DeviceArray.vector(corr_b) if mmt else None)
+        sides.append(d)
+    args = []
+    for d in sides:
+        args += [d["dX"].ptr, d["dX"].dim, d["dE"].ptr, d["dE"].dim, d["dW"].ptr, d["dW"].dim,
+                 d["dC"].ptr if d["dC"] else None, d["dC"].stride if d["dC"] else 0, scale, mmt, l2, d["dP"].ptr,
+                 d["dP"].stride, d["db"].ptr, d["dCb"].ptr if d["dCb"] else None]
+    st = lib().tnet_affine_update_bias_pair(*args, S())
+    n_tiles = sum(-(-n_in // 64) * -(-n_out // 64) for n_in, n_out in [(a_in, a_out), (b_in, b_out)])
+    if n_tiles > 256:
+        assert st == -4  # TNET_ERR_UNSUPPORTED
+        return
+    check(st)
+    for d in sides:
+        g, mag = gemm_ref("T", "N", d["X"], d["E"])
+        c = g + mmt * d["corr"]
+        w = d["W"] + scale * c
+        w = w + l2 * w
+        tol = 2e-5 * abs(scale) * mag + 2e-7 * np.abs(d["W"]) + 1e-7
+        assert np.all(np.abs(d["dW"].numpy() - w) <= tol)
+        if mmt:
+            assert np.all(np.abs(d["dC"].numpy() - c) <= 2e-5 * mag + 1e-6)
+        gb = d["P"].astype(np.float64).sum(0).astype(np.float32).astype(np.float64)
+        cb = gb + mmt * d["corr_b"]
+        np.testing.assert_allclose(d["db"].numpy().ravel(), d["b"] + scale * cb, rtol=1e-6, atol=1e-7)
+        if mmt:
+            np.testing.assert_allclose(d["dCb"].numpy().ravel(), cb, rtol=1e-6, atol=1e-9)

@@ -187,3 +187,34 @@ def test_out_of_range_label_rejected_at_intake():
     with pytest.raises(TnetError, match="outside"):
         rt.train_utterance(X, bad)
 
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mmt", [0.0, 0.5])
+def test_mlp3_step_with_update_pair_vs_oracle(mmt):
+    """BASELINE config 2 (598:1024:135, bunch 1024): the step's last two updates (1024x135 and 598x1024)
+    go out as ONE launch (tnet_affine_update_bias_pair); three steps against the oracle's fp64 step.
+    Tolerance as tests/test_gpu_fullsize.py: the update, not W, is under test -- |W_gpu - W_ref| <=
+    2 ulp(W) + 1e-4 max|W_ref - W_init| per layer, biases likewise; Xent rtol 1e-5."""
+    dims = [598, 1024, 135]
+    rng = np.random.default_rng(11)
+    layers = formats.gen_mlp_init(dims, seed=12)
+    net = Network.from_layers(layers)
+    net.set_learn_rate(0.5)
+    net.set_momentum(mmt)
+    net.set_grad_div_frm(True)
+    obj = Objective()
+    W0 = [L.W.copy() for L in layers if L.W is not None]
+    b0 = [L.b.copy() for L in layers if L.W is not None]
+    ref = orc.MLP([w.copy() for w in W0], [x.copy() for x in b0])
+    for _ in range(3):
+        X = rng.standard_normal((1024, dims[0])).astype(np.float32)
+        L = rng.integers(0, dims[-1], 1024).astype(np.int32)
+        net.train_bunch(obj, DeviceArray.from_numpy(X), DeviceArray.vector(L))
+        ref.step(X, L, 0.5, mmt=mmt, graddivfrm=True)
+    for k, (Wg, bg) in enumerate(net.linear_params()):
+        for got, want, init in ((Wg, ref.W[k], W0[k]), (bg, ref.b[k], b0[k])):
+            d = np.abs(np.asarray(want, np.float64) - init).max()
+            tol = 2 * np.spacing(np.abs(np.asarray(want, np.float32))) + 1e-4 * d
+            assert np.all(np.abs(got.astype(np.float64) - want) <= tol), (k, np.abs(got - want).max(), d)
+    np.testing.assert_allclose(obj.stats()[0], ref.xent, rtol=1e-5)
