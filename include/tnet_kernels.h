@@ -280,6 +280,14 @@ int tnet_rbm_update(const float* V, TnetMatrixDim dV, const float* H, TnetMatrix
  *   corr_b = mmt*corr_b + scale*(sum_{r<neg_from} M[r] - sum_{r>=neg_from} M[r]) ; b += corr_b. */
 int tnet_rbm_bias_update(const float* M, TnetMatrixDim d, int neg_from, float* b, float* corr_b, float scale,
                          float mmt, void* workspace, void* stream);
+/* tnet_rbm_update(V, H, W, corrW, scale, mmt, l2) and tnet_rbm_stats_update(V, H, B, vb, cvb, hb, chb, scale,
+ * mmt, mse_stats) -- one TRbmCu step's CD-1 weight update and its bias updates + reconstruction MSE
+ * (cuRbm.cc:133-174, TRbmCu.cc:350) -- in ONE launch (independent: both read the stacked statistics).
+ * Results identical to the two calls; TNET_ERR_UNSUPPORTED where the update would not run the 64x64
+ * configuration unsplit or the statistics kernel declines (make the two calls). */
+int tnet_rbm_update_stats(const float* V, TnetMatrixDim dV, const float* H, TnetMatrixDim dH, float* W,
+                          TnetMatrixDim dW, float* corrW, int strideCorr, float scale, float mmt, float l2, int B,
+                          float* vb, float* cvb, float* hb, float* chb, double* mse_stats, void* stream);
 /* The CD-1 bias updates and reconstruction error of one RBM step in one launch (replaces the
  * AddColSum / AddScaled pairs of cuRbm.cc:148-164 and CuMeanSquareError::Evaluate of TRbmCu.cc:350):
  * Vs = [pos_vis; neg_vis] (2B x V), Hs = [pos_hid; -neg_hid] (2B x H, negative phase stored negated);

@@ -239,18 +239,30 @@ void CuRbmTrainer::Step() {
                                    rbm.VisType() == CuRbm::BERNOULLI ? 1 : 0, S));
   TNET_SAFE_CALL(tnet_affine_fwd(mNegVis.pCUData(), mNegVis.Dim(), rbm.VisHid().pCUData(), rbm.VisHid().Dim(),
                                  rbm.HidBias().pCUData(), mNegHid.pCUData(), mNegHid.Dim(), hid_bern ? 3 : 2, S));
-  // CD-1 update (cuRbm.cc:133-174): one GEMM over the stacked statistics + two signed colsums
+  // CD-1 update (cuRbm.cc:133-174): one GEMM over the stacked statistics + two signed colsums; both
+  // bias updates and the reconstruction error (mse.Evaluate(neg_vis, pos_vis), TRbmCu.cc:350) in one
+  // launch over the stacked statistics -- and where the GEMM runs the 64x64 tiles unsplit (bunch 256),
+  // that launch and the GEMM's are one (tnet_rbm_update_stats: the statistics blocks beside the tiles)
   const float lr = rbm.LearnRate(), scale = lr / (float)B;
+  int st = tnet_rbm_update_stats(mV.pCUData(), mV.Dim(), mH.pCUData(), mH.Dim(), rbm.VisHid().pCUData(),
+                                 rbm.VisHid().Dim(), rbm.VisHidCorrection().pCUData(),
+                                 (int)rbm.VisHidCorrection().Stride(), scale, rbm.Momentum(), -lr * rbm.Weightcost(),
+                                 (int)B, rbm.VisBias().pCUData(), rbm.VisBiasCorrection().pCUData(),
+                                 rbm.HidBias().pCUData(), rbm.HidBiasCorrection().pCUData(), mMse.DeviceStats(), S);
+  if (st == TNET_OK) {
+    mMse.AddFrames(B);
+    if (mOpt.trace & 2) std::cout << "." << std::flush;
+    mSteps++;
+    return;
+  }
+  if (st != TNET_ERR_UNSUPPORTED) TNET_SAFE_CALL(st);
   TNET_SAFE_CALL(tnet_rbm_update(mV.pCUData(), mV.Dim(), mH.pCUData(), mH.Dim(), rbm.VisHid().pCUData(),
                                  rbm.VisHid().Dim(), rbm.VisHidCorrection().pCUData(),
                                  (int)rbm.VisHidCorrection().Stride(), scale, rbm.Momentum(), -lr * rbm.Weightcost(),
                                  S));
-  // both bias updates and the reconstruction error (mse.Evaluate(neg_vis, pos_vis), TRbmCu.cc:350) in
-  // one launch over the stacked statistics
-  const int st = tnet_rbm_stats_update(mV.pCUData(), mV.Dim(), mH.pCUData(), mH.Dim(), (int)B,
-                                       rbm.VisBias().pCUData(), rbm.VisBiasCorrection().pCUData(),
-                                       rbm.HidBias().pCUData(), rbm.HidBiasCorrection().pCUData(), scale,
-                                       rbm.Momentum(), mMse.DeviceStats(), S);
+  st = tnet_rbm_stats_update(mV.pCUData(), mV.Dim(), mH.pCUData(), mH.Dim(), (int)B, rbm.VisBias().pCUData(),
+                             rbm.VisBiasCorrection().pCUData(), rbm.HidBias().pCUData(),
+                             rbm.HidBiasCorrection().pCUData(), scale, rbm.Momentum(), mMse.DeviceStats(), S);
   if (st == TNET_ERR_UNSUPPORTED) {  // bunches above 4096 frames: the two column sums + the MSE kernel
     void* ws = CuDevice::Instantiate().Workspace(
         (size_t)std::max(tnet_col_sum_workspace(mV.Dim()), tnet_col_sum_workspace(mH.Dim())));

@@ -31,6 +31,7 @@
 #include <mutex>
 
 #include "kcommon.h"
+#include "rbm_stats.h"
 
 namespace tnetk {
 
@@ -1757,6 +1758,23 @@ void gemm16_upd_pair_kernel(const GemmP pa, const GemmP pb, const int na) {
   else gemm16_body<BM, BN, BK, WM, WN, S, 0, false, false, EPI_SGD_B, false>(pb, smem, (int)blockIdx.x - na);
 }
 
+// One RBM step's CD-1 weight update (tnet_rbm_update: 64x64 TN tiles + EPI_RBM) and its statistics
+// (tnet_rbm_stats_update: both bias updates + the reconstruction MSE, rbm_stats.h) in ONE launch: blocks
+// [0, na) the GEMM's tiles, the rest the statistics blocks.  Independent: both read the stacked V and H;
+// the GEMM writes W and its momentum, the statistics the biases, their momentum and the MSE slots.  The
+// statistics blocks run beside the GEMM's tiles instead of after them.
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
+void gemm16_rbm_update_stats_kernel(const GemmP p, const int na, const float* __restrict__ Vs, TnetMatrixDim dV,
+                                    const float* __restrict__ Hs, TnetMatrixDim dH, int B, int nvb,
+                                    float* __restrict__ vb, float* __restrict__ cvb, float* __restrict__ hb,
+                                    float* __restrict__ chb, float scale, float mmt, double* __restrict__ stats,
+                                    int nhb) {
+  constexpr int SG = gemm16_smem_floats<64, 64, 32, 4, EPI_RBM, false>();
+  __shared__ __attribute__((aligned(16))) float smem[SG > RS_SMEM_FLOATS ? SG : RS_SMEM_FLOATS];
+  if ((int)blockIdx.x < na) gemm16_body<64, 64, 32, 4, 1, 4, 0, false, false, EPI_RBM, false>(p, smem, blockIdx.x);
+  else rbm_stats_block((int)blockIdx.x - na, smem, Vs, dV, Hs, dH, B, nvb, vb, cvb, hb, chb, scale, mmt, stats, nhb);
+}
+
 // ---------------------------------------------------------------------------------------------
 // split-K combine: C = epilogue(P[0] + P[1] + ... + P[splits-1]) summed in split order (fixed, so the
 // result is deterministic), then the same epilogue arithmetic as gemm16_kernel; 4 columns / thread
@@ -2549,6 +2567,40 @@ extern "C" int tnet_rbm_update(const float* V, TnetMatrixDim dV, const float* H,
   int st = check_common(p);
   if (st) return st;
   return launch_gemm<false, false, EPI_RBM>(p, (hipStream_t)stream);
+}
+
+extern "C" int tnet_rbm_update_stats(const float* V, TnetMatrixDim dV, const float* H, TnetMatrixDim dH, float* W,
+                                     TnetMatrixDim dW, float* corrW, int strideCorr, float scale, float mmt, float l2,
+                                     int B, float* vb, float* cvb, float* hb, float* chb, double* mse_stats,
+                                     void* stream) {
+  // tnet_rbm_update(V, H, W, corrW, scale, mmt, l2) + tnet_rbm_stats_update(V, H, B, vb, cvb, hb, chb, scale, mmt,
+  // mse_stats) as one launch where the update runs the 64x64 configuration unsplit (what it runs alone,
+  // so the results are those of the two calls); TNET_ERR_UNSUPPORTED otherwise
+  if (dV.rows != dH.rows || dW.rows != dV.cols || dW.cols != dH.cols || !corrW || (strideCorr & 3))
+    return TNET_ERR_ARG;
+  if (B < 0 || dV.rows != 2 * B || dV.cols <= 0 || dH.cols <= 0 || dV.stride < dV.cols || dH.stride < dH.cols || !vb ||
+      !cvb || !hb || !chb)
+    return TNET_ERR_ARG;
+  if (!B || 2 * B > CS_ROWS * RS_MAX_SLABS || forced_cfg() >= 0 || !g_pair) return TNET_ERR_UNSUPPORTED;
+  GemmP p{};
+  p.M = dV.cols; p.N = dH.cols; p.K = dV.rows;
+  p.A = V; p.lda = dV.stride; p.B = H; p.ldb = dH.stride; p.C = W; p.ldc = dW.stride;
+  p.corr = corrW; p.ldcorr = strideCorr;
+  p.scale = scale; p.mmt = mmt; p.l2 = l2;
+  int st = check_common(p);
+  if (st) return st;
+  const GemmPlan pl = plan_gemm<false>(p, epi_splittable(EPI_RBM));
+  if (pl.cfg != CFG_m64x64k32s4w41 || pl.ks != 1) return TNET_ERR_UNSUPPORTED;
+  if (4 * (32L * p.lda + p.M) >= (1L << 32) || 4 * (32L * p.ldb + p.N) >= (1L << 32)) return TNET_ERR_UNSUPPORTED;
+  p.group = g_group > 0 ? g_group : 8;
+  p.early_issue = g_early;
+  p.wt = g_wt;
+  const int na = cdiv(p.M, 64) * cdiv(p.N, 64);
+  const int nvb = cdiv(dV.cols, RS_COLS), nhb = cdiv(dH.cols, RS_COLS), nmb = mse_stats ? cdiv(B, RS_MROWS) : 0;
+  gemm16_rbm_update_stats_kernel<<<na + nvb + nhb + nmb, 256, 0, (hipStream_t)stream>>>(
+      p, na, V, dV, H, dH, B, nvb, vb, cvb, hb, chb, scale, mmt, mse_stats, nhb);
+  TNET_LAUNCH_CHECK();
+  return TNET_OK;
 }
 
 extern "C" int tnet_affine_bwd(const float* E, TnetMatrixDim dE, const float* W, TnetMatrixDim dW,

@@ -265,3 +265,42 @@ def test_rbm_trainer_epoch_matches_oracle(vis, hid):
     np.testing.assert_allclose(hb, exp.hb, rtol=2e-4, atol=2e-6)
     rep = tr.report()
     assert rep.startswith("Mse:") and f"frames:{frames}" in rep
+
+
+@pytest.mark.parametrize("V,H,B", [(440, 2048, 256), (33, 70, 17), (440, 2048, 1024), (64, 130, 600)])
+def test_rbm_update_stats_one_launch_matches_two_calls(V, H, B):
+    """tnet_rbm_update_stats (the CD-1 weight update and the statistics blocks in ONE launch) gives exactly
+    what tnet_rbm_update + tnet_rbm_stats_update give (same tile bodies, same statistics blocks): W, its
+    momentum, both biases and their momenta bit for bit, the MSE statistics equal; or declines with
+    TNET_ERR_UNSUPPORTED where the update would run another configuration"""
+    rng = np.random.default_rng(V * 7 + B)
+    Vs = rng.standard_normal((2 * B, V)).astype(np.float32)
+    Vs[B:] *= -1
+    Hs = rng.random((2 * B, H)).astype(np.float32)
+    Hs[B:] *= -1
+    W0 = (0.05 * rng.standard_normal((V, H))).astype(np.float32)
+    cW0 = (0.01 * rng.standard_normal((V, H))).astype(np.float32)
+    vb, hb = (rng.standard_normal(n).astype(np.float32) for n in (V, H))
+    cvb, chb = (0.01 * rng.standard_normal(n).astype(np.float32) for n in (V, H))
+    lr, mmt, wc = 0.1, 0.5, 2e-4
+    dV, dH = DeviceArray.from_numpy(Vs), DeviceArray.from_numpy(Hs)
+    out = []
+    for one in (True, False):
+        dW, dc = DeviceArray.from_numpy(W0), DeviceArray.from_numpy(cW0)
+        d = [DeviceArray.vector(a) for a in (vb, cvb, hb, chb)]
+        st = DeviceArray(1, 1024, np.float64, stride=1024)
+        if one:
+            rc = lib().tnet_rbm_update_stats(dV.ptr, dV.dim, dH.ptr, dH.dim, dW.ptr, dW.dim, dc.ptr, dc.stride, lr / B,
+                                             mmt, -lr * wc, B, d[0].ptr, d[1].ptr, d[2].ptr, d[3].ptr, st.ptr, S())
+            if rc == -4:  # TNET_ERR_UNSUPPORTED: the trainer makes the two calls
+                return
+            check(rc)
+        else:
+            check(lib().tnet_rbm_update(dV.ptr, dV.dim, dH.ptr, dH.dim, dW.ptr, dW.dim, dc.ptr, dc.stride, lr / B, mmt,
+                                        -lr * wc, S()))
+            check(lib().tnet_rbm_stats_update(dV.ptr, dV.dim, dH.ptr, dH.dim, B, d[0].ptr, d[1].ptr, d[2].ptr,
+                                              d[3].ptr, lr / B, mmt, st.ptr, S()))
+        out.append(([dW.numpy(), dc.numpy()] + [a.numpy().reshape(-1) for a in d], st.numpy()[0][0::2]))
+    for a, b in zip(out[0][0], out[1][0]):
+        np.testing.assert_array_equal(a, b)
+    np.testing.assert_allclose(out[0][1].sum(), out[1][1].sum(), rtol=1e-12)
