@@ -242,6 +242,23 @@ int tnet_affine_update_bias_pair(const float* X, TnetMatrixDim dX, const float* 
                                  TnetMatrixDim dX2, const float* E2, TnetMatrixDim dE2, float* W2, TnetMatrixDim dW2,
                                  float* corrW2, int strideCorr2, float scale2, float mmt2, float l22,
                                  const float* colpart2, int ldcolpart2, float* b2, float* corr_b2, void* stream);
+/* The step's last weight update(s) and the NEXT bunch's gather in ONE launch: tnet_affine_update_bias(X, E,
+ * W, ...) -- and, when X2 is not NULL, tnet_affine_update_bias(X2, E2, W2, ...) as in
+ * tnet_affine_update_bias_pair -- plus tnet_gather_bunch(y, x, labels_out, labels_in, copy_from, dy, dx)
+ * (CuCache::GetBunch of the bunch after this one, cuCache.cc:155-200) as extra workgroups on the CUs the
+ * update's tiles leave free.  The gather must be independent of the updates (y / labels_out overlap none of
+ * their operands: the trainer gathers into the other half of a double-buffered bunch).  Results identical
+ * to the separate calls (the gather may also fill y's row padding up to the next multiple of 4 columns);
+ * TNET_ERR_UNSUPPORTED when the updates would run another tile configuration alone, fewer than 8 CUs are
+ * left for the gather, or the strides are not 16-B multiples (make the separate calls). */
+int tnet_affine_update_bias_gather(const float* X, TnetMatrixDim dX, const float* E, TnetMatrixDim dE, float* W,
+                                   TnetMatrixDim dW, float* corrW, int strideCorr, float scale, float mmt, float l2,
+                                   const float* colpart, int ldcolpart, float* b, float* corr_b, const float* X2,
+                                   TnetMatrixDim dX2, const float* E2, TnetMatrixDim dE2, float* W2,
+                                   TnetMatrixDim dW2, float* corrW2, int strideCorr2, float scale2, float mmt2,
+                                   float l22, const float* colpart2, int ldcolpart2, float* b2, float* corr_b2,
+                                   float* y, const float* x, int* labels_out, const int* labels_in,
+                                   const int* copy_from, TnetMatrixDim dy, TnetMatrixDim dx, void* stream);
 /* G = X^T E into a gradient buffer (data-parallel path: all-reduced before tnet_sgd_update). */
 int tnet_affine_grad(const float* X, TnetMatrixDim dX, const float* E, TnetMatrixDim dE, float* G,
                      TnetMatrixDim dG, void* stream);

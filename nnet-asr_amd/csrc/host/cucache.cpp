@@ -338,4 +338,20 @@ void CuCache::GatherAheadLabels(CuMatrix<BaseFloat>& rFeatures, CuVector<int>& r
   AdvanceAfterBunch();
 }
 
+BunchGather CuCache::AheadGather(CuMatrix<BaseFloat>& rFeatures, CuVector<int>& rLabels) {
+  if (!HasBunchAhead()) Error("CuCache::AheadGather: no shuffled bunch ahead");
+  if (rFeatures.Rows() != mBunchsize || rFeatures.Cols() != mFeatures.Cols() || rLabels.Dim() != mBunchsize)
+    Error("CuCache::AheadGather: destination not sized for a bunch");
+  BunchGather g;
+  g.y = rFeatures.pCUData();
+  g.x = mFeatures.pCUData();
+  g.labels_out = rLabels.pCUData();
+  g.labels_in = mLabels.pCUData();
+  g.copy_from = mPerm.pCUData() + mExhaustPos;
+  g.dy = rFeatures.Dim();
+  g.dx = mFeatures.Dim();
+  AdvanceAfterBunch();
+  return g;
+}
+
 }  // namespace TNet

@@ -53,6 +53,9 @@ class CuCache {
   /// stream's use of the destination buffers; the permutation and the fill are already waited for
   /// there, EnterExhaust / Randomize being compute-stream ordered)
   void GatherAheadLabels(CuMatrix<BaseFloat>& rFeatures, CuVector<int>& rLabels, hipStream_t stream);
+  /// the same gather's arguments, for a launch the caller enqueues on the COMPUTE stream before anything
+  /// else touches the cache (the step's last weight update carries it); advances past that bunch
+  BunchGather AheadGather(CuMatrix<BaseFloat>& rFeatures, CuVector<int>& rLabels);
 
   bool Full() { return mState == FULL; }
   bool Empty() { return mState == EMPTY || mIntakePos < mBunchsize; }

@@ -218,6 +218,43 @@ bool CuBiasedLinearity::UpdatePairFromColsum(const CuMatrix<BaseFloat>& X, const
   return true;
 }
 
+bool CuBiasedLinearity::UpdateFromColsumGather(const CuMatrix<BaseFloat>& X, const CuMatrix<BaseFloat>& E,
+                                               const CuMatrix<BaseFloat>& colpart, CuBiasedLinearity* other,
+                                               const CuMatrix<BaseFloat>* X2, const CuMatrix<BaseFloat>* E2,
+                                               const CuMatrix<BaseFloat>* colpart2, const BunchGather& g) {
+  CuProfileScope p(other ? "CuBiasedLinearity::Update (pair) + gather" : "CuBiasedLinearity::Update + gather");
+  float scale, l2, scale2 = 0.f, l22 = 0.f;
+  UpdateConstants(X.Rows(), &scale, &l2);
+  const bool mmt = mMomentum != 0.0f, mmt2 = other && other->mMomentum != 0.0f;
+  if (other) other->UpdateConstants(X2->Rows(), &scale2, &l22);
+  std::string name = "gemm_upd" + std::string(other ? "+upd" : "") + "+gather:" + std::to_string(GetNInputs()) + "x" +
+                     std::to_string(GetNOutputs());
+  double flops = 2.0 * X.Rows() * GetNInputs() * GetNOutputs();
+  if (other) {
+    name += "+" + std::to_string(other->GetNInputs()) + "x" + std::to_string(other->GetNOutputs());
+    flops += 2.0 * X2->Rows() * other->GetNInputs() * other->GetNOutputs();
+  }
+  KTScope kt(name, flops, other ? 2 : 1);
+  const TnetMatrixDim z{};
+  const int st = tnet_affine_update_bias_gather(
+      X.pCUData(), X.Dim(), E.pCUData(), E.Dim(), mLinearity.pCUData(), mLinearity.Dim(),
+      mmt ? mLinearityCorrection.pCUData() : nullptr, (int)mLinearityCorrection.Stride(), scale, mMomentum, l2,
+      colpart.pCUData(), (int)colpart.Stride(), mBias.pCUData(), mmt ? mBiasCorrection.pCUData() : nullptr,
+      other ? X2->pCUData() : nullptr, other ? X2->Dim() : z, other ? E2->pCUData() : nullptr, other ? E2->Dim() : z,
+      other ? other->mLinearity.pCUData() : nullptr, other ? other->mLinearity.Dim() : z,
+      mmt2 ? other->mLinearityCorrection.pCUData() : nullptr, other ? (int)other->mLinearityCorrection.Stride() : 0,
+      scale2, other ? other->mMomentum : 0.f, l22, other ? colpart2->pCUData() : nullptr,
+      other ? (int)colpart2->Stride() : 0, other ? other->mBias.pCUData() : nullptr,
+      mmt2 ? other->mBiasCorrection.pCUData() : nullptr, g.y, g.x, g.labels_out, g.labels_in, g.copy_from, g.dy, g.dx,
+      S);
+  if (st == TNET_ERR_UNSUPPORTED) {
+    kt.Cancel();
+    return false;
+  }
+  TNET_SAFE_CALL(st);
+  return true;
+}
+
 void CuBiasedLinearity::Update() { UpdateFrom(GetInput(), GetErrorInput()); }
 
 void CuBiasedLinearity::ComputeGradient() {

@@ -48,15 +48,22 @@ class CuBiasedLinearity : public CuUpdatableComponent {
   // same update with the bias gradient taken from the 32-row slab column sums of E that the backward
   // GEMM of the layer above wrote (tnet_affine_bwd_colsum): one launch instead of three
   void UpdateFromColsum(const CuMatrix<BaseFloat>& X, const CuMatrix<BaseFloat>& E, const CuMatrix<BaseFloat>& colpart);
-  /// UpdateFromColsum and, in the same launch, the backward GEMM of the layer below
-  /// (tnet_affine_update_bwd_pair): Eo = (E2 below.W^T) .* Ybelow (1 - Ybelow) + Eo's slab sums into
-  /// colpart2.  False (nothing enqueued) when the pair kernel does not take these shapes.
   /// This layer's UpdateFromColsum(X, E, colpart) and other's UpdateFromColsum(X2, E2, colpart2) in ONE
   /// launch (tnet_affine_update_bias_pair) when the two small grids fit one round over the CUs; false:
   /// nothing enqueued (make the two calls).
   bool UpdatePairFromColsum(const CuMatrix<BaseFloat>& X, const CuMatrix<BaseFloat>& E,
                             const CuMatrix<BaseFloat>& colpart, CuBiasedLinearity& other, const CuMatrix<BaseFloat>& X2,
                             const CuMatrix<BaseFloat>& E2, const CuMatrix<BaseFloat>& colpart2);
+  /// UpdateFromColsum (other == nullptr) or UpdatePairFromColsum, with the next bunch's gather `g` on the
+  /// CUs the update's tiles leave free, all in ONE launch (tnet_affine_update_bias_gather); false: nothing
+  /// enqueued (make the separate calls).
+  bool UpdateFromColsumGather(const CuMatrix<BaseFloat>& X, const CuMatrix<BaseFloat>& E,
+                              const CuMatrix<BaseFloat>& colpart, CuBiasedLinearity* other,
+                              const CuMatrix<BaseFloat>* X2, const CuMatrix<BaseFloat>* E2,
+                              const CuMatrix<BaseFloat>* colpart2, const BunchGather& g);
+  /// UpdateFromColsum and, in the same launch, the backward GEMM of the layer below
+  /// (tnet_affine_update_bwd_pair): Eo = (E2 below.W^T) .* Ybelow (1 - Ybelow) + Eo's slab sums into
+  /// colpart2.  False (nothing enqueued) when the pair kernel does not take these shapes.
   bool UpdateFromColsumWithBwd(const CuMatrix<BaseFloat>& X, const CuMatrix<BaseFloat>& E,
                                const CuMatrix<BaseFloat>& colpart, const CuBiasedLinearity& below,
                                const CuMatrix<BaseFloat>& E2, const CuMatrix<BaseFloat>& Ybelow,

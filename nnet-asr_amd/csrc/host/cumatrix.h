@@ -282,4 +282,16 @@ class CuVector {
   }
 };
 
+/// The arguments of one bunch gather (tnet_gather_bunch): bunch row r = cache row copy_from[r], its class
+/// id alongside.  CuCache hands them out for the NEXT bunch so the step's last weight-update launch can
+/// carry the gather (tnet_affine_update_bias_gather).
+struct BunchGather {
+  float* y = nullptr;
+  const float* x = nullptr;
+  int* labels_out = nullptr;
+  const int* labels_in = nullptr;
+  const int* copy_from = nullptr;
+  TnetMatrixDim dy{}, dx{};
+};
+
 }  // namespace TNet

@@ -419,10 +419,18 @@ void CuNetwork::TrainBunch(const CuMatrix<BaseFloat>& X, const CuVector<int>& la
     // the last layer trained here: the held-back update of the layer above and this layer's own are
     // independent (each reads its X, E and writes its own W, b) and no backward GEMM is left -- small ones
     // (both grids in one round over the CUs) go out as ONE launch
-    if ((stopper || l == 0) && pend.lin && !exchange && err_colsum && lin->LearnRate() > 0.0f &&
-        pend.lin->UpdatePairFromColsum(*pend.X, *pend.E, *mColPart[pend.l], *lin, *acts[l], *err, *mColPart[l])) {
-      pend.lin = nullptr;
-      break;
+    // (with the next bunch's gather on the CUs their tiles leave free, when the trainer handed one over)
+    if ((stopper || l == 0) && pend.lin && !exchange && err_colsum && lin->LearnRate() > 0.0f) {
+      if (mTailGather && pend.lin->UpdateFromColsumGather(*pend.X, *pend.E, *mColPart[pend.l], lin, acts[l], err,
+                                                          mColPart[l].get(), *mTailGather)) {
+        mTailDone = true;
+        pend.lin = nullptr;
+        break;
+      }
+      if (pend.lin->UpdatePairFromColsum(*pend.X, *pend.E, *mColPart[pend.l], *lin, *acts[l], *err, *mColPart[l])) {
+        pend.lin = nullptr;
+        break;
+      }
     }
     flush();  // a held-back update no backward GEMM took
     if (lin->LearnRate() > 0.0f) {
@@ -456,6 +464,13 @@ void CuNetwork::TrainBunch(const CuMatrix<BaseFloat>& X, const CuVector<int>& la
     if (stopper || l == 0) break;
     err = eo;
     err_colsum = eo_colsum;
+  }
+  // the step's last update (the stopper's): the next bunch's gather rides on its launch
+  if (pend.lin && mTailGather && !mTailDone &&
+      pend.lin->UpdateFromColsumGather(*pend.X, *pend.E, *mColPart[pend.l], nullptr, nullptr, nullptr, nullptr,
+                                       *mTailGather)) {
+    mTailDone = true;
+    pend.lin = nullptr;
   }
   flush();
   if (exchange) {

@@ -78,6 +78,14 @@ class CuNetwork {
   /// Keep the softmax output in the <softmax> component after TrainBunch (costs one extra
   /// [rows x classes] write per step; off by default).
   void KeepOutput(bool keep) { mKeepOutput = keep; }
+  /// The NEXT bunch's gather, carried by the last weight-update launch of the next TrainBunch where the
+  /// library takes it (tnet_affine_update_bias_gather: the update's tiles leave CUs free); TailGatherDone()
+  /// says whether it went out -- if not, the caller launches it.  `g` must outlive that TrainBunch.
+  void SetTailGather(const BunchGather* g) {
+    mTailGather = g;
+    mTailDone = false;
+  }
+  bool TailGatherDone() const { return mTailDone; }
 
  private:
   CuComponent* ComponentFactory(std::istream& In);
@@ -91,6 +99,8 @@ class CuNetwork {
   BaseFloat mGlobLearnRate = 0.0f;
   std::string mLearnRateFactors;
   bool mKeepOutput = false;
+  const BunchGather* mTailGather = nullptr;
+  bool mTailDone = false;
   // fused-path buffers: activations of sigmoid layers are the components' own outputs;
   // errors live here (one per affine layer input)
   std::vector<std::unique_ptr<CuMatrix<BaseFloat>>> mErr;

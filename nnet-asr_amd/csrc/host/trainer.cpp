@@ -41,7 +41,7 @@ void CuTrainer::Step() {
   hipStream_t cs = CuDevice::Instantiate().Stream();
   if (mAhead) {  // gathered during the previous step
     mCur ^= 1;
-    TNET_HIP_CALL(hipStreamWaitEvent(cs, mGathered, 0));
+    if (mAheadOnStream) TNET_HIP_CALL(hipStreamWaitEvent(cs, mGathered, 0));
     mAhead = false;
   } else {
     mCache.GetBunchLabels(mFeatsB[mCur], mLabelsB[mCur]);
@@ -68,8 +68,35 @@ void CuTrainer::Step() {
     mCache.GatherAheadLabels(nf, nl, mAheadStream);
     TNET_HIP_CALL(hipEventRecord(mGathered, mAheadStream));
     mAhead = true;
+    mAheadOnStream = true;
+  }
+  // Default (TNET_GATHER_TAIL=0: off): the next bunch of the fill is gathered into the other buffer by the
+  // step's LAST weight-update launch, on the CUs its tiles leave free (tnet_affine_update_bias_gather) --
+  // in stream order, so no cross-stream wait, and one launch less per step.  Where the library does not
+  // take it (shapes, data parallelism, cross-validation), the gather is launched right after the step.
+  static const bool tail = !(getenv("TNET_GATHER_TAIL") && getenv("TNET_GATHER_TAIL")[0] == '0');
+  BunchGather tg;
+  bool tail_now = false;
+  if (!mAhead && tail && mCache.HasBunchAhead()) {
+    CuMatrix<BaseFloat>& nf = mFeatsB[mCur ^ 1];
+    CuVector<int>& nl = mLabelsB[mCur ^ 1];
+    nf.Init(mCache.Bunchsize(), mFeatsB[mCur].Cols());
+    nl.Init(mCache.Bunchsize());
+    tg = mCache.AheadGather(nf, nl);
+    tail_now = true;
+    mAhead = true;
+    mAheadOnStream = false;
+    if (!mOpt.crossval && !mExchange) mNet->SetTailGather(&tg);
   }
   mNet->TrainBunch(mFeatsB[mCur], mLabelsB[mCur], *mObj, !mOpt.crossval, mOpt.crossval ? nullptr : mExchange);
+  if (tail_now) {
+    const bool done = mNet->TailGatherDone();
+    mNet->SetTailGather(nullptr);
+    if (!done) {
+      KTScope kt("gather", 2.0 * tg.dy.rows * tg.dy.cols * 4.0);
+      TNET_SAFE_CALL(tnet_gather_bunch(tg.y, tg.x, tg.labels_out, tg.labels_in, tg.copy_from, tg.dy, tg.dx, cs));
+    }
+  }
   if (mOpt.trace & 2) std::cout << "." << std::flush;
   mSteps++;
 }

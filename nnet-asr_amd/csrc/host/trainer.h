@@ -87,6 +87,7 @@ class CuTrainer {
   CuVector<int> mLabelsB[2];
   int mCur = 0;
   bool mAhead = false;        // buffer mCur ^ 1 holds the next bunch (gathered ahead)
+  bool mAheadOnStream = false;  // ... gathered on mAheadStream (else in compute-stream order: no wait)
   hipStream_t mAheadStream = nullptr;
   hipEvent_t mMark = nullptr, mGathered = nullptr;
   CuNetwork* mTransform = nullptr;

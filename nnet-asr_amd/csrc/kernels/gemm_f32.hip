@@ -1758,6 +1758,64 @@ void gemm16_upd_pair_kernel(const GemmP pa, const GemmP pb, const int na) {
   else gemm16_body<BM, BN, BK, WM, WN, S, 0, false, false, EPI_SGD_B, false>(pb, smem, (int)blockIdx.x - na);
 }
 
+// The next bunch's gather (tnet_gather_bunch: bunch row r = cache row idx[r], its class id alongside) as
+// workgroups of the step's last update launch.  Wave w of ngb*4 takes rows w, w + ngb*4, ...; R rows at a
+// time with every 16-B load of those rows issued before the first store (the rows' idx loads before
+// that), so a wave pays two memory round trips per R rows.  c4 = cols rounded up to 4 (16-B pieces; the
+// caller checked that both strides hold them).
+struct BunchGatherP {
+  float* y;
+  const float* x;
+  int* lab_out;
+  const int* lab_in;
+  const int* idx;
+  int rows, c4;
+  long ys, xs;
+};
+__device__ __forceinline__ void bunch_gather_block(const BunchGatherP& g, const int gb, const int ngb) {
+  constexpr int R = 4, CM = 2;  // rows and 256-column pieces per lane in flight
+  const int lane = threadIdx.x & 63, nw = blockDim.x >> 6;
+  const int w0 = gb * nw + (threadIdx.x >> 6), step = ngb * nw;
+  for (int r0 = w0; r0 < g.rows; r0 += R * step) {
+    int ir[R];
+#pragma unroll
+    for (int k = 0; k < R; ++k) ir[k] = r0 + k * step < g.rows ? g.idx[r0 + k * step] : -1;
+#pragma unroll
+    for (int k = 0; k < R; ++k)
+      if (ir[k] >= 0 && lane == 0) g.lab_out[r0 + k * step] = g.lab_in[ir[k]];
+    for (int cb = lane * 4; cb < g.c4; cb += 256 * CM) {
+      f32x4 v[R][CM];
+#pragma unroll
+      for (int k = 0; k < R; ++k)
+#pragma unroll
+        for (int j = 0; j < CM; ++j)
+          if (ir[k] >= 0 && cb + 256 * j < g.c4) v[k][j] = *reinterpret_cast<const f32x4*>(g.x + ir[k] * g.xs + cb + 256 * j);
+#pragma unroll
+      for (int k = 0; k < R; ++k) {
+        if (ir[k] < 0) continue;
+        // the bunch row written through (st_wt): the next step's first GEMM reads it on every XCD
+        const __amdgpu_buffer_rsrc_t ry = tile_rsrc(g.y + (long)(r0 + k * step) * g.ys);
+#pragma unroll
+        for (int j = 0; j < CM; ++j)
+          if (cb + 256 * j < g.c4) st_wt(ry, cb + 256 * j, v[k][j]);
+      }
+    }
+  }
+}
+
+// tnet_affine_update_bias_gather: the update pair kernel's tiles (nb = 0: one update) and ng gather blocks
+// after them.  Blocks are dispatched in index order, so the gather blocks take the CUs the update's tiles
+// leave free (one workgroup per CU: the ring's LDS and 1 wave per SIMD) and run beside the tiles.
+template <int BM, int BN, int BK, int WM, int WN, int S>
+__global__ __launch_bounds__(WM * WN * 64) __attribute__((amdgpu_waves_per_eu(1, 1)))
+void gemm16_upd_gather_kernel(const GemmP pa, const GemmP pb, const int na, const int nb, const BunchGatherP g) {
+  __shared__ __attribute__((aligned(16))) float smem[gemm16_smem_floats<BM, BN, BK, S, EPI_SGD_B, false>()];
+  const int b = blockIdx.x;
+  if (b < na) gemm16_body<BM, BN, BK, WM, WN, S, 0, false, false, EPI_SGD_B, false>(pa, smem, b);
+  else if (b < na + nb) gemm16_body<BM, BN, BK, WM, WN, S, 0, false, false, EPI_SGD_B, false>(pb, smem, b - na);
+  else bunch_gather_block(g, b - na - nb, (int)gridDim.x - na - nb);
+}
+
 // One RBM step's CD-1 weight update (tnet_rbm_update: 64x64 TN tiles + EPI_RBM) and its statistics
 // (tnet_rbm_stats_update: both bias updates + the reconstruction MSE, rbm_stats.h) in ONE launch: blocks
 // [0, na) the GEMM's tiles, the rest the statistics blocks.  Independent: both read the stacked V and H;
@@ -2407,6 +2465,20 @@ static int launch_pair_upd_bwd(GemmP pu, GemmP pb, hipStream_t st) {
   return TNET_OK;
 }
 
+static int cu_count() {
+  if (!g_cus) {
+    int dev = 0;
+    hipDeviceProp_t prop;
+    if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess) return 0;
+    g_cus = prop.multiProcessorCount;
+  }
+  return g_cus;
+}
+static bool split2_on() {
+  if (g_split2 < 0) g_split2 = getenv("TNET_GEMM_SPLIT2") ? atoi(getenv("TNET_GEMM_SPLIT2")) : 0;
+  return g_split2 != 0;
+}
+
 // tnet_affine_update_bias_pair: both updates in one gemm16_upd_pair_kernel launch when their 64x64 grids
 // together fit one round over the CUs; TNET_ERR_UNSUPPORTED otherwise (the caller makes the two calls)
 static int launch_upd_pair(GemmP pa, GemmP pb, hipStream_t st) {
@@ -2719,6 +2791,68 @@ extern "C" int tnet_affine_update_bias_pair(const float* X, TnetMatrixDim dX, co
   if (st) return st;
   if (W == W2 || b == b2 || (corrW && corrW == corrW2)) return TNET_ERR_ARG;
   return launch_upd_pair(pa, pb, (hipStream_t)stream);
+}
+
+extern "C" int tnet_affine_update_bias_gather(const float* X, TnetMatrixDim dX, const float* E, TnetMatrixDim dE,
+                                              float* W, TnetMatrixDim dW, float* corrW, int strideCorr, float scale,
+                                              float mmt, float l2, const float* colpart, int ldcolpart, float* b,
+                                              float* corr_b, const float* X2, TnetMatrixDim dX2, const float* E2,
+                                              TnetMatrixDim dE2, float* W2, TnetMatrixDim dW2, float* corrW2,
+                                              int strideCorr2, float scale2, float mmt2, float l22,
+                                              const float* colpart2, int ldcolpart2, float* b2, float* corr_b2,
+                                              float* y, const float* x, int* labels_out, const int* labels_in,
+                                              const int* copy_from, TnetMatrixDim dy, TnetMatrixDim dx,
+                                              void* stream) {
+  // tnet_affine_update_bias (X2 NULL) or tnet_affine_update_bias_pair, and tnet_gather_bunch, in one launch
+  GemmP pa, pb{};
+  int st = update_bias_params(pa, X, dX, E, dE, W, dW, corrW, strideCorr, scale, mmt, l2, colpart, ldcolpart, b,
+                              corr_b);
+  if (st) return st;
+  const bool two = X2 != nullptr;
+  if (two) {
+    st = update_bias_params(pb, X2, dX2, E2, dE2, W2, dW2, corrW2, strideCorr2, scale2, mmt2, l22, colpart2,
+                            ldcolpart2, b2, corr_b2);
+    if (st) return st;
+    if (W == W2 || b == b2 || (corrW && corrW == corrW2)) return TNET_ERR_ARG;
+  }
+  if (!y || !x || !labels_out || !labels_in || !copy_from || dy.cols != dx.cols || dy.rows < 0 || dy.stride < dy.cols ||
+      dx.stride < dx.cols)
+    return TNET_ERR_ARG;
+  const int c4 = (dy.cols + 3) & ~3;
+  if (((uintptr_t)y & 15) || ((uintptr_t)x & 15) || (dy.stride & 3) || (dx.stride & 3) || c4 > dy.stride ||
+      c4 > dx.stride)
+    return TNET_ERR_UNSUPPORTED;
+  if (forced_cfg() >= 0 || split2_on() || g_split > 0) return TNET_ERR_UNSUPPORTED;
+  if (pa.M <= 0 || pa.N <= 0 || (two && (pb.M <= 0 || pb.N <= 0))) return TNET_ERR_UNSUPPORTED;
+  int na, nb = 0;
+  if (two) {
+    // the pair kernel's conditions (launch_upd_pair): both 64x64 grids in one round over the CUs
+    if (!g_pair) return TNET_ERR_UNSUPPORTED;
+    na = cdiv(pa.M, 64) * cdiv(pa.N, 64);
+    nb = cdiv(pb.M, 64) * cdiv(pb.N, 64);
+  } else {
+    // what tnet_affine_update_bias runs alone: the 64x64 configuration, unsplit
+    const GemmPlan pl = plan_gemm<false>(pa, epi_splittable(EPI_SGD_B));
+    if (pl.cfg != CFG_m64x64k32s4w41 || pl.ks != 1) return TNET_ERR_UNSUPPORTED;
+    na = cdiv(pa.M, 64) * cdiv(pa.N, 64);
+  }
+  for (const GemmP* q : {&pa, &pb}) {
+    if (q == &pb && !two) break;
+    if (4 * (32L * q->lda + q->M) >= (1L << 32) || 4 * (32L * q->ldb + q->N) >= (1L << 32)) return TNET_ERR_UNSUPPORTED;
+  }
+  const int cus = cu_count();
+  if (cus <= 0) return TNET_ERR_UNSUPPORTED;
+  const int spare = cus - g_reserve - na - nb;
+  if (two && na + nb > cus - g_reserve) return TNET_ERR_UNSUPPORTED;
+  if (spare < 8) return TNET_ERR_UNSUPPORTED;
+  const int ng = spare < 64 ? spare : 64;
+  pa.group = pb.group = g_group > 0 ? g_group : 8;
+  pa.early_issue = pb.early_issue = g_early;
+  pa.wt = pb.wt = g_wt;
+  BunchGatherP g{y, x, labels_out, labels_in, copy_from, dy.rows, c4, dy.stride, dx.stride};
+  gemm16_upd_gather_kernel<64, 64, 32, 4, 1, 4><<<na + nb + ng, 256, 0, (hipStream_t)stream>>>(pa, pb, na, nb, g);
+  TNET_LAUNCH_CHECK();
+  return TNET_OK;
 }
 
 extern "C" int tnet_affine_update_bwd_pair(const float* X, TnetMatrixDim dX, const float* E, TnetMatrixDim dE,

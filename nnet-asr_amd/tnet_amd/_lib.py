@@ -86,6 +86,9 @@ _SIGS = {
     "tnet_affine_update_bias_pair": (i32, [vp, MatrixDim, vp, MatrixDim, vp, MatrixDim, vp, i32, f32, f32, f32, vp, i32,
                                            vp, vp, vp, MatrixDim, vp, MatrixDim, vp, MatrixDim, vp, i32, f32, f32,
                                            f32, vp, i32, vp, vp, vp]),
+    "tnet_affine_update_bias_gather": (i32, [vp, MatrixDim, vp, MatrixDim, vp, MatrixDim, vp, i32, f32, f32, f32, vp,
+                                             i32, vp, vp, vp, MatrixDim, vp, MatrixDim, vp, MatrixDim, vp, i32, f32,
+                                             f32, f32, vp, i32, vp, vp, vp, vp, vp, vp, vp, MatrixDim, MatrixDim, vp]),
     "tnet_affine_update_bwd_pair": (i32, [vp, MatrixDim, vp, MatrixDim, vp, MatrixDim, vp, i32, f32, f32, f32, vp, i32,
                                           vp, vp, vp, MatrixDim, vp, MatrixDim, vp, i32, vp, MatrixDim, vp, i32, vp]),
     "tnet_affine_grad": (i32, [vp, MatrixDim, vp, MatrixDim, vp, MatrixDim, vp]),

@@ -666,3 +666,71 @@ def test_affine_update_bias_pair(mmt, rows, a_in, a_out, b_in, b_out):
         np.testing.assert_allclose(d["db"].numpy().ravel(), d["b"] + scale * cb, rtol=1e-6, atol=1e-7)
         if mmt:
             np.testing.assert_allclose(d["dCb"].numpy().ravel(), cb, rtol=1e-6, atol=1e-9)
+
+
+@pytest.mark.parametrize("mmt", [0.0, 0.5])
+@pytest.mark.parametrize("rows,sides,gcols", [
+    (1024, [(440, 2048)], 440),                  # dnn4's first-layer update (the step's last launch)
+    (1024, [(598, 1024)], 598),                  # MLP3's first layer alone; 598 columns: 16-B pieces over 600
+    (1024, [(1024, 135), (598, 1024)], 598),     # MLP3's last two updates (the pair)
+    (256, [(440, 256)], 440),
+    (1024, [(2048, 2048)], 440),                 # 128x128 alone: declined
+])
+def test_affine_update_bias_gather_matches_separate_calls(mmt, rows, sides, gcols):
+    """tnet_affine_update_bias_gather (the step's last weight update(s) + the next bunch's gather in ONE launch)
+    against tnet_affine_update_bias / _pair followed by tnet_gather_bunch: W, momentum, b and its momentum
+    bit-identical, the gathered rows and class ids exact; TNET_ERR_UNSUPPORTED where the update alone would
+    run another tile configuration"""
+    scale, l2 = -0.3 / rows, -1e-4
+    cache_rows = 3000
+    Xc = rnd((cache_rows, gcols), 300)
+    labc = (np.arange(cache_rows, dtype=np.int32) * 7) % 4000
+    perm = np.random.default_rng(301).permutation(cache_rows).astype(np.int32)[:1024]
+    host = []
+    for k, (n_in, n_out) in enumerate(sides):
+        X, E = rnd((rows, n_in), 310 + k), rnd((rows, n_out), 320 + k, 0.01)
+        W, corr = rnd((n_in, n_out), 330 + k, 0.1), rnd((n_in, n_out), 340 + k, 0.01)
+        b, corr_b = rnd(n_out, 350 + k), rnd(n_out, 360 + k, 0.01)
+        host.append((X, E, W, corr, b, corr_b, slab_sums(E).astype(np.float32)))
+    results = []
+    for fused in (True, False):
+        dev, args = [], []
+        for X, E, W, corr, b, corr_b, P in host:
+            d = dict(dX=DeviceArray.from_numpy(X), dE=DeviceArray.from_numpy(E), dW=DeviceArray.from_numpy(W),
+                     dP=DeviceArray.from_numpy(P), db=DeviceArray.vector(b),
+                     dC=DeviceArray.from_numpy(corr) if mmt else None, dCb=DeviceArray.vector(corr_b) if mmt else None)
+            dev.append(d)
+            args.append([d["dX"].ptr, d["dX"].dim, d["dE"].ptr, d["dE"].dim, d["dW"].ptr, d["dW"].dim,
+                         d["dC"].ptr if d["dC"] else None, d["dC"].stride if d["dC"] else 0, scale, mmt, l2,
+                         d["dP"].ptr, d["dP"].stride, d["db"].ptr, d["dCb"].ptr if d["dCb"] else None])
+        dXc, dLc, dPerm = DeviceArray.from_numpy(Xc), DeviceArray.vector(labc), DeviceArray.vector(perm)
+        dY = DeviceArray.from_numpy(np.full((1024, gcols), np.nan, np.float32))
+        dLo = DeviceArray.vector(np.full(1024, -7, np.int32))
+        gargs = [dY.ptr, dXc.ptr, dLo.ptr, dLc.ptr, dPerm.ptr, dY.dim, dXc.dim]
+        if fused:
+            second = args[1] if len(args) > 1 else [None, MatrixDim(0, 0, 0), None, MatrixDim(0, 0, 0), None,
+                                                     MatrixDim(0, 0, 0), None, 0, 0.0, 0.0, 0.0, None, 0, None, None]
+            st = lib().tnet_affine_update_bias_gather(*args[0], *second, *gargs, S())
+            if sides == [(2048, 2048)]:
+                assert st == TNET_ERR_UNSUPPORTED
+                return
+            check(st)
+        else:
+            if len(args) > 1:
+                check(lib().tnet_affine_update_bias_pair(*args[0], *args[1], S()))
+            else:
+                check(lib().tnet_affine_update_bias(*args[0], S()))
+            check(lib().tnet_gather_bunch(*gargs, S()))
+        out = []
+        for d in dev:
+            out += [d["dW"].numpy(), d["db"].numpy()]
+            if mmt:
+                out += [d["dC"].numpy(), d["dCb"].numpy()]
+        results.append((out, dY.numpy(), dLo.numpy()[:, 0]))
+    (oa, ya, la), (ob, yb, lb) = results
+    for a, b_ in zip(oa, ob):
+        np.testing.assert_array_equal(a, b_)
+    np.testing.assert_array_equal(ya, Xc[perm])
+    np.testing.assert_array_equal(yb, Xc[perm])
+    np.testing.assert_array_equal(la, labc[perm])
+    np.testing.assert_array_equal(lb, labc[perm])
