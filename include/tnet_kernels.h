@@ -305,6 +305,17 @@ int tnet_rbm_bias_update(const float* M, TnetMatrixDim d, int neg_from, float* b
 int tnet_rbm_update_stats(const float* V, TnetMatrixDim dV, const float* H, TnetMatrixDim dH, float* W,
                           TnetMatrixDim dW, float* corrW, int strideCorr, float scale, float mmt, float l2, int B,
                           float* vb, float* cvb, float* hb, float* chb, double* mse_stats, void* stream);
+/* tnet_rbm_update_stats and tnet_gather_bunch(y, x, labels_out, labels_in, copy_from, dy, dx) -- the NEXT
+ * bunch's visible rows (CuCache::GetBunch, cuCache.cc:155-200) -- in ONE launch, the gather on CUs beside the
+ * update's tiles.  y must lie outside V (TNET_ERR_ARG; the trainer double-buffers the visible statistics).
+ * Results identical to the separate calls (y's row padding up to 4 columns may be written too);
+ * TNET_ERR_UNSUPPORTED where tnet_rbm_update_stats declines, fewer than 16 CUs are left beside the tiles,
+ * or the strides are not 16-B multiples (make the separate calls). */
+int tnet_rbm_update_stats_gather(const float* V, TnetMatrixDim dV, const float* H, TnetMatrixDim dH, float* W,
+                                 TnetMatrixDim dW, float* corrW, int strideCorr, float scale, float mmt, float l2,
+                                 int B, float* vb, float* cvb, float* hb, float* chb, double* mse_stats, float* y,
+                                 const float* x, int* labels_out, const int* labels_in, const int* copy_from,
+                                 TnetMatrixDim dy, TnetMatrixDim dx, void* stream);
 /* The CD-1 bias updates and reconstruction error of one RBM step in one launch (replaces the
  * AddColSum / AddScaled pairs of cuRbm.cc:148-164 and CuMeanSquareError::Evaluate of TRbmCu.cc:350):
  * Vs = [pos_vis; neg_vis] (2B x V), Hs = [pos_hid; -neg_hid] (2B x H, negative phase stored negated);

@@ -200,21 +200,38 @@ CuRbmTrainer::CuRbmTrainer(CuRbm* rbm, const RbmTrainerOptions& opt) : mRbm(rbm)
   mCache.Init(mOpt.cachesize, B);
   mCache.SetRng(&mRng);
   mCache.Trace(mOpt.trace);
-  mV.Init(2 * B, V);
+  mVB[0].Init(2 * B, V);
+  mVB[1].Init(2 * B, V);
   mH.Init(2 * B, H);
   mStates.Init(B, H);
-  CuMatrix<BaseFloat>::MakeView(mPosVis, mV.pCUData(), B, V, mV.Stride());
-  CuMatrix<BaseFloat>::MakeView(mNegVis, mV.pCURowData(B), B, V, mV.Stride());
+  ViewV();
   CuMatrix<BaseFloat>::MakeView(mPosHid, mH.pCUData(), B, H, mH.Stride());
   CuMatrix<BaseFloat>::MakeView(mNegHid, mH.pCURowData(B), B, H, mH.Stride());
+}
+
+void CuRbmTrainer::ViewV() {
+  const size_t B = mOpt.bunchsize, V = mRbm->GetNInputs();
+  CuMatrix<BaseFloat>& cur = mVB[mCurV];
+  CuMatrix<BaseFloat>& nxt = mVB[mCurV ^ 1];
+  CuMatrix<BaseFloat>::MakeView(mPosVis, cur.pCUData(), B, V, cur.Stride());
+  CuMatrix<BaseFloat>::MakeView(mNegVis, cur.pCURowData(B), B, V, cur.Stride());
+  CuMatrix<BaseFloat>::MakeView(mNextPosVis, nxt.pCUData(), B, V, nxt.Stride());
 }
 
 void CuRbmTrainer::Step() {
   const size_t B = mOpt.bunchsize;
   CuRbm& rbm = *mRbm;
   const bool hid_bern = rbm.HidType() == CuRbm::BERNOULLI;
-  // positive phase: pos_vis (gathered from the shuffled cache), pos_hid = p(h | v)
-  mCache.GetBunchLabels(mPosVis, mDummyLabels);
+  // positive phase: pos_vis (gathered from the shuffled cache -- by the previous step's last launch when
+  // that one carried it), pos_hid = p(h | v)
+  if (mAheadV) {
+    mCurV ^= 1;
+    mAheadV = false;
+    ViewV();
+  } else {
+    mCache.GetBunchLabels(mPosVis, mDummyLabels);
+  }
+  const CuMatrix<BaseFloat>& vs = mVB[mCurV];  // [pos_vis; neg_vis]
   // sample the hidden layer (TRbmCu.cc:336-341): Bernoulli units are sampled by the positive-phase
   // GEMM's own workgroups up to 2^20 units a bunch (bunch 256 x 2048: 62.1 -> 60.9 us a step); above,
   // the 32 B of generator state per unit make the sampling HBM-bound and the separate launch is as
@@ -243,30 +260,64 @@ void CuRbmTrainer::Step() {
   // bias updates and the reconstruction error (mse.Evaluate(neg_vis, pos_vis), TRbmCu.cc:350) in one
   // launch over the stacked statistics -- and where the GEMM runs the 64x64 tiles unsplit (bunch 256),
   // that launch and the GEMM's are one (tnet_rbm_update_stats: the statistics blocks beside the tiles)
+  // The next shuffled bunch of the fill is gathered into the other visible buffer by this last launch, on
+  // CUs beside the update's tiles (tnet_rbm_update_stats_gather; TNET_GATHER_TAIL=0: a gather launch at the
+  // start of the next step); where that launch is declined the gather follows the step.  Up to bunch 512:
+  // at bunch 256 4.19 M -> 4.25-4.44 M frames/s, at 1024 8.22 M -> 8.12 M (the 1024-row gather holds back the
+  // statistics blocks queued behind it; profiles/r03_gather_tail_ab.json), so larger bunches keep the
+  // separate gather launch.
   const float lr = rbm.LearnRate(), scale = lr / (float)B;
-  int st = tnet_rbm_update_stats(mV.pCUData(), mV.Dim(), mH.pCUData(), mH.Dim(), rbm.VisHid().pCUData(),
-                                 rbm.VisHid().Dim(), rbm.VisHidCorrection().pCUData(),
-                                 (int)rbm.VisHidCorrection().Stride(), scale, rbm.Momentum(), -lr * rbm.Weightcost(),
-                                 (int)B, rbm.VisBias().pCUData(), rbm.VisBiasCorrection().pCUData(),
-                                 rbm.HidBias().pCUData(), rbm.HidBiasCorrection().pCUData(), mMse.DeviceStats(), S);
+  static const bool tail = !(getenv("TNET_GATHER_TAIL") && getenv("TNET_GATHER_TAIL")[0] == '0');
+  BunchGather tg;
+  const bool tail_now = tail && B <= 512 && mCache.HasBunchAhead();
+  if (tail_now) tg = mCache.AheadGather(mNextPosVis, mDummyLabels);
+  auto finish_gather = [&](bool done) {
+    if (!tail_now) return;
+    mAheadV = true;
+    if (!done)
+      TNET_SAFE_CALL(tnet_gather_bunch(tg.y, tg.x, tg.labels_out, tg.labels_in, tg.copy_from, tg.dy, tg.dx, S));
+  };
+  int st = TNET_ERR_UNSUPPORTED;
+  if (tail_now) {
+    st = tnet_rbm_update_stats_gather(
+        vs.pCUData(), vs.Dim(), mH.pCUData(), mH.Dim(), rbm.VisHid().pCUData(), rbm.VisHid().Dim(),
+        rbm.VisHidCorrection().pCUData(), (int)rbm.VisHidCorrection().Stride(), scale, rbm.Momentum(),
+        -lr * rbm.Weightcost(), (int)B, rbm.VisBias().pCUData(), rbm.VisBiasCorrection().pCUData(),
+        rbm.HidBias().pCUData(), rbm.HidBiasCorrection().pCUData(), mMse.DeviceStats(), tg.y, tg.x, tg.labels_out,
+        tg.labels_in, tg.copy_from, tg.dy, tg.dx, S);
+    if (st == TNET_OK) {
+      finish_gather(true);
+      mMse.AddFrames(B);
+      if (mOpt.trace & 2) std::cout << "." << std::flush;
+      mSteps++;
+      return;
+    }
+  }
+  if (st == TNET_ERR_UNSUPPORTED)
+    st = tnet_rbm_update_stats(vs.pCUData(), vs.Dim(), mH.pCUData(), mH.Dim(), rbm.VisHid().pCUData(),
+                               rbm.VisHid().Dim(), rbm.VisHidCorrection().pCUData(),
+                               (int)rbm.VisHidCorrection().Stride(), scale, rbm.Momentum(), -lr * rbm.Weightcost(),
+                               (int)B, rbm.VisBias().pCUData(), rbm.VisBiasCorrection().pCUData(),
+                               rbm.HidBias().pCUData(), rbm.HidBiasCorrection().pCUData(), mMse.DeviceStats(), S);
   if (st == TNET_OK) {
+    finish_gather(false);
     mMse.AddFrames(B);
     if (mOpt.trace & 2) std::cout << "." << std::flush;
     mSteps++;
     return;
   }
   if (st != TNET_ERR_UNSUPPORTED) TNET_SAFE_CALL(st);
-  TNET_SAFE_CALL(tnet_rbm_update(mV.pCUData(), mV.Dim(), mH.pCUData(), mH.Dim(), rbm.VisHid().pCUData(),
+  TNET_SAFE_CALL(tnet_rbm_update(vs.pCUData(), vs.Dim(), mH.pCUData(), mH.Dim(), rbm.VisHid().pCUData(),
                                  rbm.VisHid().Dim(), rbm.VisHidCorrection().pCUData(),
                                  (int)rbm.VisHidCorrection().Stride(), scale, rbm.Momentum(), -lr * rbm.Weightcost(),
                                  S));
-  st = tnet_rbm_stats_update(mV.pCUData(), mV.Dim(), mH.pCUData(), mH.Dim(), (int)B, rbm.VisBias().pCUData(),
+  st = tnet_rbm_stats_update(vs.pCUData(), vs.Dim(), mH.pCUData(), mH.Dim(), (int)B, rbm.VisBias().pCUData(),
                              rbm.VisBiasCorrection().pCUData(), rbm.HidBias().pCUData(),
                              rbm.HidBiasCorrection().pCUData(), scale, rbm.Momentum(), mMse.DeviceStats(), S);
   if (st == TNET_ERR_UNSUPPORTED) {  // bunches above 4096 frames: the two column sums + the MSE kernel
     void* ws = CuDevice::Instantiate().Workspace(
-        (size_t)std::max(tnet_col_sum_workspace(mV.Dim()), tnet_col_sum_workspace(mH.Dim())));
-    TNET_SAFE_CALL(tnet_rbm_bias_update(mV.pCUData(), mV.Dim(), (int)B, rbm.VisBias().pCUData(),
+        (size_t)std::max(tnet_col_sum_workspace(vs.Dim()), tnet_col_sum_workspace(mH.Dim())));
+    TNET_SAFE_CALL(tnet_rbm_bias_update(vs.pCUData(), vs.Dim(), (int)B, rbm.VisBias().pCUData(),
                                         rbm.VisBiasCorrection().pCUData(), scale, rbm.Momentum(), ws, S));
     TNET_SAFE_CALL(tnet_rbm_bias_update(mH.pCUData(), mH.Dim(), (int)(2 * B), rbm.HidBias().pCUData(),
                                         rbm.HidBiasCorrection().pCUData(), scale, rbm.Momentum(), ws, S));
@@ -275,13 +326,14 @@ void CuRbmTrainer::Step() {
     TNET_SAFE_CALL(st);
     mMse.AddFrames(B);
   }
+  finish_gather(false);
   if (mOpt.trace & 2) std::cout << "." << std::flush;
   mSteps++;
 }
 
 void CuRbmTrainer::DrainCache() {
   if (mOpt.randomize) mCache.Randomize();
-  while (!mCache.Empty()) Step();
+  while (mAheadV || !mCache.Empty()) Step();
   mTrainedSinceFill = true;
 }
 
@@ -310,7 +362,7 @@ size_t CuRbmTrainer::Prefill(const float* feats, size_t rows, size_t cols, size_
 
 void CuRbmTrainer::Replay(long n) {
   for (long i = 0; i < n; i++) {
-    if (mCache.Empty()) {
+    if (!mAheadV && mCache.Empty()) {
       mCache.Rewind();
       if (mOpt.randomize) mCache.Randomize();
     }

@@ -139,8 +139,14 @@ class CuRbmTrainer {
   CuRandState mRand;
   CuCache mCache;
   CuMeanSquareError mMse;
-  CuMatrix<BaseFloat> mV, mH, mStates;               // [2B x vis], [2B x hid], [B x hid]
-  CuMatrix<BaseFloat> mPosVis, mNegVis, mPosHid, mNegHid;  // row views into mV / mH
+  // the stacked visible statistics twice: the step trains mVB[mCurV] while its last launch gathers the next
+  // bunch into the positive half of the other (tnet_rbm_update_stats_gather)
+  CuMatrix<BaseFloat> mVB[2], mH, mStates;           // [2B x vis] x 2, [2B x hid], [B x hid]
+  CuMatrix<BaseFloat> mPosVis, mNegVis, mPosHid, mNegHid;  // row views into mVB[mCurV] / mH
+  CuMatrix<BaseFloat> mNextPosVis;                   // the positive half of mVB[mCurV ^ 1]
+  int mCurV = 0;
+  bool mAheadV = false;  // mVB[mCurV ^ 1] holds the next bunch
+  void ViewV();
   CuVector<int> mDummyLabels;
   std::vector<int> mZeroLabels;
   long mSteps = 0;

@@ -1826,11 +1826,14 @@ void gemm16_rbm_update_stats_kernel(const GemmP p, const int na, const float* __
                                     const float* __restrict__ Hs, TnetMatrixDim dH, int B, int nvb,
                                     float* __restrict__ vb, float* __restrict__ cvb, float* __restrict__ hb,
                                     float* __restrict__ chb, float scale, float mmt, double* __restrict__ stats,
-                                    int nhb) {
+                                    int nhb, const BunchGatherP g, const int ng) {
+  // blocks [na, na + ng): the next bunch's gather (tnet_rbm_update_stats_gather; ng = 0 without one)
   constexpr int SG = gemm16_smem_floats<64, 64, 32, 4, EPI_RBM, false>();
   __shared__ __attribute__((aligned(16))) float smem[SG > RS_SMEM_FLOATS ? SG : RS_SMEM_FLOATS];
-  if ((int)blockIdx.x < na) gemm16_body<64, 64, 32, 4, 1, 4, 0, false, false, EPI_RBM, false>(p, smem, blockIdx.x);
-  else rbm_stats_block((int)blockIdx.x - na, smem, Vs, dV, Hs, dH, B, nvb, vb, cvb, hb, chb, scale, mmt, stats, nhb);
+  const int b = blockIdx.x;
+  if (b < na) gemm16_body<64, 64, 32, 4, 1, 4, 0, false, false, EPI_RBM, false>(p, smem, b);
+  else if (b < na + ng) bunch_gather_block(g, b - na, ng);
+  else rbm_stats_block(b - na - ng, smem, Vs, dV, Hs, dH, B, nvb, vb, cvb, hb, chb, scale, mmt, stats, nhb);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -2641,10 +2644,46 @@ extern "C" int tnet_rbm_update(const float* V, TnetMatrixDim dV, const float* H,
   return launch_gemm<false, false, EPI_RBM>(p, (hipStream_t)stream);
 }
 
+static int rbm_update_stats_run(const float* V, TnetMatrixDim dV, const float* H, TnetMatrixDim dH, float* W,
+                                TnetMatrixDim dW, float* corrW, int strideCorr, float scale, float mmt, float l2, int B,
+                                float* vb, float* cvb, float* hb, float* chb, double* mse_stats, const BunchGatherP& g,
+                                int ng, void* stream);
+
 extern "C" int tnet_rbm_update_stats(const float* V, TnetMatrixDim dV, const float* H, TnetMatrixDim dH, float* W,
                                      TnetMatrixDim dW, float* corrW, int strideCorr, float scale, float mmt, float l2,
                                      int B, float* vb, float* cvb, float* hb, float* chb, double* mse_stats,
                                      void* stream) {
+  return rbm_update_stats_run(V, dV, H, dH, W, dW, corrW, strideCorr, scale, mmt, l2, B, vb, cvb, hb, chb, mse_stats,
+                              BunchGatherP{}, 0, stream);
+}
+
+extern "C" int tnet_rbm_update_stats_gather(const float* V, TnetMatrixDim dV, const float* H, TnetMatrixDim dH,
+                                            float* W, TnetMatrixDim dW, float* corrW, int strideCorr, float scale,
+                                            float mmt, float l2, int B, float* vb, float* cvb, float* hb, float* chb,
+                                            double* mse_stats, float* y, const float* x, int* labels_out,
+                                            const int* labels_in, const int* copy_from, TnetMatrixDim dy,
+                                            TnetMatrixDim dx, void* stream) {
+  // tnet_rbm_update_stats + tnet_gather_bunch (the next bunch's visible rows) in one launch
+  if (!y || !x || !labels_out || !labels_in || !copy_from || dy.cols != dx.cols || dy.rows < 0 || dy.stride < dy.cols ||
+      dx.stride < dx.cols)
+    return TNET_ERR_ARG;
+  const int c4 = (dy.cols + 3) & ~3;
+  if (((uintptr_t)y & 15) || ((uintptr_t)x & 15) || (dy.stride & 3) || (dx.stride & 3) || c4 > dy.stride ||
+      c4 > dx.stride)
+    return TNET_ERR_UNSUPPORTED;
+  // the gather must not touch what the update reads: y outside V's rows
+  const float* v_end = V + (long)dV.rows * dV.stride;
+  const float* y_end = y + (long)dy.rows * dy.stride;
+  if (y < v_end && V < y_end) return TNET_ERR_ARG;
+  return rbm_update_stats_run(V, dV, H, dH, W, dW, corrW, strideCorr, scale, mmt, l2, B, vb, cvb, hb, chb, mse_stats,
+                              BunchGatherP{y, x, labels_out, labels_in, copy_from, dy.rows, c4, dy.stride, dx.stride},
+                              16, stream);
+}
+
+static int rbm_update_stats_run(const float* V, TnetMatrixDim dV, const float* H, TnetMatrixDim dH, float* W,
+                                TnetMatrixDim dW, float* corrW, int strideCorr, float scale, float mmt, float l2, int B,
+                                float* vb, float* cvb, float* hb, float* chb, double* mse_stats, const BunchGatherP& g,
+                                int ng, void* stream) {
   // tnet_rbm_update(V, H, W, corrW, scale, mmt, l2) + tnet_rbm_stats_update(V, H, B, vb, cvb, hb, chb, scale, mmt,
   // mse_stats) as one launch where the update runs the 64x64 configuration unsplit (what it runs alone,
   // so the results are those of the two calls); TNET_ERR_UNSUPPORTED otherwise
@@ -2669,8 +2708,9 @@ extern "C" int tnet_rbm_update_stats(const float* V, TnetMatrixDim dV, const flo
   p.wt = g_wt;
   const int na = cdiv(p.M, 64) * cdiv(p.N, 64);
   const int nvb = cdiv(dV.cols, RS_COLS), nhb = cdiv(dH.cols, RS_COLS), nmb = mse_stats ? cdiv(B, RS_MROWS) : 0;
-  gemm16_rbm_update_stats_kernel<<<na + nvb + nhb + nmb, 256, 0, (hipStream_t)stream>>>(
-      p, na, V, dV, H, dH, B, nvb, vb, cvb, hb, chb, scale, mmt, mse_stats, nhb);
+  if (ng && cu_count() - g_reserve - na < ng) return TNET_ERR_UNSUPPORTED;  // the gather's CUs beside the tiles
+  gemm16_rbm_update_stats_kernel<<<na + ng + nvb + nhb + nmb, 256, 0, (hipStream_t)stream>>>(
+      p, na, V, dV, H, dH, B, nvb, vb, cvb, hb, chb, scale, mmt, mse_stats, nhb, g, ng);
   TNET_LAUNCH_CHECK();
   return TNET_OK;
 }

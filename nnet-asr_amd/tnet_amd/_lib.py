@@ -194,6 +194,8 @@ _SIGS = {
     "tnet_rbm_update": (i32, [vp, MatrixDim, vp, MatrixDim, vp, MatrixDim, vp, i32, f32, f32, f32, vp]),
     "tnet_rbm_update_stats": (i32, [vp, MatrixDim, vp, MatrixDim, vp, MatrixDim, vp, i32, f32, f32, f32, i32, vp, vp,
                                     vp, vp, vp, vp]),
+    "tnet_rbm_update_stats_gather": (i32, [vp, MatrixDim, vp, MatrixDim, vp, MatrixDim, vp, i32, f32, f32, f32, i32, vp,
+                                           vp, vp, vp, vp, vp, vp, vp, vp, vp, MatrixDim, MatrixDim, vp]),
     "tnet_rbm_bias_update": (i32, [vp, MatrixDim, i32, vp, vp, f32, f32, vp, vp]),
     "tnet_rbm_stats_update": (i32, [vp, MatrixDim, vp, MatrixDim, i32, vp, vp, vp, vp, f32, f32, vp, vp]),
     "tnet_gemv_rowvec_partial": (i32, [vp, i32, vp, i32, vp, vp, i32, i32, vp, vp]),

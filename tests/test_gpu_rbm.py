@@ -18,7 +18,7 @@ pytestmark = pytest.mark.gpu
 
 import oracle as orc  # noqa: E402
 from tnet_amd import DeviceArray, Network, RbmTrainer, formats  # noqa: E402
-from tnet_amd._lib import check, lib  # noqa: E402
+from tnet_amd._lib import MatrixDim, check, lib  # noqa: E402
 
 
 def S():
@@ -304,3 +304,57 @@ def test_rbm_update_stats_one_launch_matches_two_calls(V, H, B):
     for a, b in zip(out[0][0], out[1][0]):
         np.testing.assert_array_equal(a, b)
     np.testing.assert_allclose(out[0][1].sum(), out[1][1].sum(), rtol=1e-12)
+
+
+@pytest.mark.parametrize("V,H,B", [(440, 2048, 256), (33, 70, 17), (440, 2048, 1024)])
+def test_rbm_update_stats_gather_matches_separate_calls(V, H, B):
+    """tnet_rbm_update_stats_gather (the CD-1 update, its statistics and the NEXT bunch's visible rows in ONE
+    launch) against tnet_rbm_update_stats + tnet_gather_bunch: W, momentum, biases, their momenta bit for bit,
+    the MSE statistics equal, the gathered rows and ids exact; TNET_ERR_UNSUPPORTED where the update would
+    run another configuration; TNET_ERR_ARG when the destination overlaps the statistics it reads"""
+    rng = np.random.default_rng(V * 11 + B)
+    Vs = rng.standard_normal((2 * B, V)).astype(np.float32)
+    Vs[B:] *= -1
+    Hs = rng.random((2 * B, H)).astype(np.float32)
+    Hs[B:] *= -1
+    W0 = (0.05 * rng.standard_normal((V, H))).astype(np.float32)
+    cW0 = (0.01 * rng.standard_normal((V, H))).astype(np.float32)
+    vb, hb = (rng.standard_normal(n).astype(np.float32) for n in (V, H))
+    cvb, chb = (0.01 * rng.standard_normal(n).astype(np.float32) for n in (V, H))
+    cache = rng.standard_normal((3 * B + 5, V)).astype(np.float32)
+    perm = rng.permutation(cache.shape[0]).astype(np.int32)[:B]
+    lab = np.zeros(cache.shape[0], np.int32)
+    lr, mmt, wc = 0.1, 0.5, 2e-4
+    dV, dH = DeviceArray.from_numpy(Vs), DeviceArray.from_numpy(Hs)
+    dC, dL, dP = DeviceArray.from_numpy(cache), DeviceArray.vector(lab), DeviceArray.vector(perm)
+    out = []
+    for one in (True, False):
+        dW, dc = DeviceArray.from_numpy(W0), DeviceArray.from_numpy(cW0)
+        d = [DeviceArray.vector(a) for a in (vb, cvb, hb, chb)]
+        st = DeviceArray(1, 1024, np.float64, stride=1024)
+        dY = DeviceArray.from_numpy(np.full((B, V), np.nan, np.float32))
+        dLo = DeviceArray.vector(np.full(B, 5, np.int32))
+        head = [dV.ptr, dV.dim, dH.ptr, dH.dim, dW.ptr, dW.dim, dc.ptr, dc.stride, lr / B, mmt, -lr * wc, B, d[0].ptr,
+                d[1].ptr, d[2].ptr, d[3].ptr, st.ptr]
+        gargs = [dY.ptr, dC.ptr, dLo.ptr, dL.ptr, dP.ptr, dY.dim, dC.dim]
+        if one:
+            # the destination inside V: refused
+            vview = MatrixDim(B, V, dV.stride)
+            assert lib().tnet_rbm_update_stats_gather(*head, dV.ptr, dC.ptr, dLo.ptr, dL.ptr, dP.ptr, vview, dC.dim,
+                                                      S()) == -1
+            rc = lib().tnet_rbm_update_stats_gather(*head, *gargs, S())
+            if rc == -4:
+                assert lib().tnet_rbm_update_stats(*head, S()) == -4
+                return
+            check(rc)
+        else:
+            check(lib().tnet_rbm_update_stats(*head, S()))
+            check(lib().tnet_gather_bunch(*gargs, S()))
+        out.append(([dW.numpy(), dc.numpy()] + [a.numpy().reshape(-1) for a in d], st.numpy()[0][0::2],
+                    dY.numpy(), dLo.numpy()[:, 0]))
+    for a, b in zip(out[0][0], out[1][0]):
+        np.testing.assert_array_equal(a, b)
+    np.testing.assert_allclose(out[0][1].sum(), out[1][1].sum(), rtol=1e-12)
+    for k in (0, 1):
+        np.testing.assert_array_equal(out[k][2], cache[perm])
+        np.testing.assert_array_equal(out[k][3], lab[perm])

@@ -13,7 +13,7 @@ usage: python tools/roofline_evidence.py gpurun_out rNN
 bench.py reads the newest profiles/r*_pmc_gemm2048.json for roofline.traffic.
 
 The 2048x2048 launches are found in the trace by dispatch order inside each step (split at the
-cache gather): forward = the three 64x128 BIAS_SIG launches after the K=440 layer; backward = the
+cache gather, or the update launch that carries it): forward = the three 64x128 BIAS_SIG launches after the K=440 layer; backward = the
 diff-sigmoid launches except the first after softmax_xent (that one has K=4000); update = the
 64-tile-row SGD launches with grid 65536 (the 4000-wide update has a larger grid).
 """
@@ -49,7 +49,9 @@ def classify_trace(path):
         if "softmax_xent" in name:
             after_softmax = True
             continue
-        if "gather_rows" in name:
+        # the bunch gather: its own launch, or (round 3, tnet_affine_update_bias_gather) riding on the
+        # previous step's last update launch (the 440x2048 update, not a roofline GEMM)
+        if "gather_rows" in name or "upd_gather" in name:
             after_gather = True
             continue
         if FWD.search(name):
