@@ -242,6 +242,14 @@ int tnet_affine_update_bias_pair(const float* X, TnetMatrixDim dX, const float* 
                                  TnetMatrixDim dX2, const float* E2, TnetMatrixDim dE2, float* W2, TnetMatrixDim dW2,
                                  float* corrW2, int strideCorr2, float scale2, float mmt2, float l22,
                                  const float* colpart2, int ldcolpart2, float* b2, float* corr_b2, void* stream);
+/* tnet_affine_bwd_colsum(E, W, Ybelow, Eo, colpart) and tnet_colsum_slab_sums(E, colpartE) -- the top layer's
+ * backward GEMM and the slab sums of its own input error (the softmax error: the top layer's bias gradient,
+ * cuBiasedLinearity.cc:46-64 AddColSum) -- in ONE launch, the slab-sum blocks on the CUs the GEMM tiles free.
+ * Results identical to the two calls; TNET_ERR_UNSUPPORTED where the backward would run another tile
+ * configuration or the slab sums another form (make the two calls). */
+int tnet_affine_bwd_colsum_slabs(const float* E, TnetMatrixDim dE, const float* W, TnetMatrixDim dW,
+                                 const float* Ybelow, int strideYbelow, float* Eo, TnetMatrixDim dEo, float* colpart,
+                                 int ldcolpart, float* colpartE, int ldcolpartE, void* stream);
 /* The step's last weight update(s) and the NEXT bunch's gather in ONE launch: tnet_affine_update_bias(X, E,
  * W, ...) -- and, when X2 is not NULL, tnet_affine_update_bias(X2, E2, W2, ...) as in
  * tnet_affine_update_bias_pair -- plus tnet_gather_bunch(y, x, labels_out, labels_in, copy_from, dy, dx)

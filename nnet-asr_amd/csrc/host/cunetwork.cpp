@@ -352,15 +352,25 @@ void CuNetwork::TrainBunch(const CuMatrix<BaseFloat>& X, const CuVector<int>& la
   std::vector<CuBiasedLinearity*> submitted;  // data-parallel: layers in reduction order, not yet applied
   const size_t grows = exchange ? exchange->GlobalRows(rows) : rows;
   int n_submitted = 0;
-  if (top_colsum && !fused_top && !err_colsum) {
+  // the top layer's bias gradient (the softmax error's slab sums): carried by the top layer's backward launch
+  // where that launch takes it (tnet_affine_bwd_colsum_slabs, its blocks on the CUs the GEMM tiles free;
+  // TNET_TOP_SLABS_RIDE=0: a launch of its own here)
+  static const bool slabs_ride = !(getenv("TNET_TOP_SLABS_RIDE") && getenv("TNET_TOP_SLABS_RIDE")[0] == '0');
+  bool top_slabs_ride = false;
+  auto top_slabs_launch = [&]() {
     CuMatrix<BaseFloat>& cp = *mColPart[nl - 1];
-    cp.Init(tnet_colsum_slabs((int)rows), GetNOutputs());
     KTScope kt("colsum:" + std::to_string(GetNOutputs()), 4.0 * rows * GetNOutputs());
     const int st = tnet_colsum_slab_sums(mGlobErr.pCUData(), mGlobErr.Dim(), cp.pCUData(), (int)cp.Stride(), S);
-    if (st != TNET_ERR_UNSUPPORTED) {
-      TNET_SAFE_CALL(st);
-      err_colsum = true;
-    }
+    if (st == TNET_ERR_UNSUPPORTED) return false;
+    TNET_SAFE_CALL(st);
+    return true;
+  };
+  if (top_colsum && !fused_top && !err_colsum) {
+    mColPart[nl - 1]->Init(tnet_colsum_slabs((int)rows), GetNOutputs());
+    const bool top_bwd = nl > 1 && mNetComponents[2 * (nl - 1)] != mpPropagErrorStopper &&
+                         static_cast<CuBiasedLinearity*>(mNetComponents[2 * (nl - 2)])->LearnRate() > 0.0f;
+    if (slabs_ride && top_bwd) top_slabs_ride = err_colsum = true;  // settled by the top layer's backward below
+    else err_colsum = top_slabs_launch();
   }  // slab column sums of *err are in mColPart[l] (bias gradient fused, no exchange)
   // Without data parallelism the fused update of layer l is held back one layer and enqueued with the
   // backward GEMM of layer l-1 as ONE launch where the pair kernel takes both shapes
@@ -399,9 +409,20 @@ void CuNetwork::TrainBunch(const CuMatrix<BaseFloat>& X, const CuVector<int>& la
         } else {
           flush();
           KTScope kt("gemm_bwd:" + shape, 2.0 * rows * lin->GetNInputs() * lin->GetNOutputs());
-          const int st = tnet_affine_bwd_colsum(err->pCUData(), err->Dim(), lin->Linearity().pCUData(),
-                                                lin->Linearity().Dim(), acts[l]->pCUData(), (int)acts[l]->Stride(),
-                                                eo->pCUData(), eo->Dim(), cp.pCUData(), (int)cp.Stride(), S);
+          int st = TNET_ERR_UNSUPPORTED;
+          if (top_slabs_ride) {  // l == nl - 1: err is the softmax error
+            top_slabs_ride = false;
+            CuMatrix<BaseFloat>& ct = *mColPart[nl - 1];
+            st = tnet_affine_bwd_colsum_slabs(err->pCUData(), err->Dim(), lin->Linearity().pCUData(),
+                                              lin->Linearity().Dim(), acts[l]->pCUData(), (int)acts[l]->Stride(),
+                                              eo->pCUData(), eo->Dim(), cp.pCUData(), (int)cp.Stride(),
+                                              ct.pCUData(), (int)ct.Stride(), S);
+            if (st == TNET_ERR_UNSUPPORTED) err_colsum = top_slabs_launch();
+          }
+          if (st == TNET_ERR_UNSUPPORTED)
+            st = tnet_affine_bwd_colsum(err->pCUData(), err->Dim(), lin->Linearity().pCUData(),
+                                        lin->Linearity().Dim(), acts[l]->pCUData(), (int)acts[l]->Stride(),
+                                        eo->pCUData(), eo->Dim(), cp.pCUData(), (int)cp.Stride(), S);
           if (st != TNET_ERR_UNSUPPORTED) {
             TNET_SAFE_CALL(st);
             eo_colsum = true;
@@ -415,6 +436,10 @@ void CuNetwork::TrainBunch(const CuMatrix<BaseFloat>& X, const CuVector<int>& la
                                        lin->Linearity().Dim(), acts[l]->pCUData(), (int)acts[l]->Stride(),
                                        eo->pCUData(), eo->Dim(), 1, S));
       }
+    }
+    if (top_slabs_ride) {  // no colsum backward launch took the top slab sums
+      top_slabs_ride = false;
+      err_colsum = top_slabs_launch();
     }
     // the last layer trained here: the held-back update of the layer above and this layer's own are
     // independent (each reads its X, E and writes its own W, b) and no backward GEMM is left -- small ones

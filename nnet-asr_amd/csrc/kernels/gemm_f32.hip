@@ -1816,6 +1816,24 @@ void gemm16_upd_gather_kernel(const GemmP pa, const GemmP pb, const int na, cons
   else bunch_gather_block(g, b - na - nb, (int)gridDim.x - na - nb);
 }
 
+// tnet_affine_bwd_colsum_slabs: the top layer's backward GEMM (64x128 NT + diff-sigmoid + Eo's slab sums,
+// na tiles) and the slab sums of its OWN input error E (the softmax error: the top layer's bias gradient,
+// colsum_partial blocks after the tiles).  Independent (the GEMM reads E, the blocks read E); the blocks
+// take the CUs as the tiles finish instead of a launch of their own before the GEMM.
+template <bool PX>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
+void gemm16_bwd_slabs_kernel(const GemmP p, const int na, const float* __restrict__ Et, const TnetMatrixDim dEt,
+                             float* __restrict__ cpt, const long ldcpt, const int slabs, const int ncb) {
+  __shared__ __attribute__((aligned(16))) float smem[gemm16_smem_floats<64, 128, 64, 2, EPI_DSIG_CS, PX>()];
+  const int b = blockIdx.x;
+  if (b < na) {
+    gemm16_body<64, 128, 64, 2, 2, 2, 0, true, true, EPI_DSIG_CS, PX>(p, smem, b);
+  } else {
+    const int c = b - na;
+    colsum_partial_block<true>(Et, dEt, cpt, slabs, 0x7fffffff, ldcpt, c % ncb, c / ncb, smem);
+  }
+}
+
 // One RBM step's CD-1 weight update (tnet_rbm_update: 64x64 TN tiles + EPI_RBM) and its statistics
 // (tnet_rbm_stats_update: both bias updates + the reconstruction MSE, rbm_stats.h) in ONE launch: blocks
 // [0, na) the GEMM's tiles, the rest the statistics blocks.  Independent: both read the stacked V and H;
@@ -2769,6 +2787,42 @@ extern "C" int tnet_affine_bwd_colsum(const float* E, TnetMatrixDim dE, const fl
   int st = check_common(p);
   if (st) return st;
   return launch_gemm<true, true, EPI_DSIG_CS>(p, (hipStream_t)stream);
+}
+
+extern "C" int tnet_affine_bwd_colsum_slabs(const float* E, TnetMatrixDim dE, const float* W, TnetMatrixDim dW,
+                                            const float* Ybelow, int strideYbelow, float* Eo, TnetMatrixDim dEo,
+                                            float* colpart, int ldcolpart, float* colpartE, int ldcolpartE,
+                                            void* stream) {
+  // tnet_affine_bwd_colsum(E, W, Ybelow, Eo, colpart) + tnet_colsum_slab_sums(E, colpartE) in one launch
+  if (dE.cols != dW.cols || dEo.rows != dE.rows || dEo.cols != dW.rows || !Ybelow || !colpart ||
+      ldcolpart < dEo.cols || !aligned16(Ybelow) || (strideYbelow & 3) || !colpartE || ldcolpartE < dE.cols)
+    return TNET_ERR_ARG;
+  GemmP p{};
+  p.M = dE.rows; p.N = dW.rows; p.K = dE.cols;
+  p.A = E; p.lda = dE.stride; p.B = W; p.ldb = dW.stride; p.C = Eo; p.ldc = dEo.stride;
+  p.alpha = 1.f; p.beta = 0.f;
+  p.aux = Ybelow; p.ldaux = strideYbelow;
+  p.cpart = colpart; p.ldcpart = ldcolpart;
+  int st = check_common(p);
+  if (st) return st;
+  // what launch_colsum_bwd runs alone: the plain 64x128 grid (no forced configuration, no stream-K)
+  if (p.M <= 0 || p.N <= 0 || forced_cfg() >= 0 || g_reserve > 0) return TNET_ERR_UNSUPPORTED;
+  if ((long)cdiv(p.M, 64) * cdiv(p.N, 128) < 200) return TNET_ERR_UNSUPPORTED;
+  if (4L * p.M * p.lda >= (1L << 32) || 4L * p.N * p.ldb >= (1L << 32)) return TNET_ERR_UNSUPPORTED;
+  // tnet_colsum_slab_sums's 16-B form
+  const int slabs = cs_slabs(dE.rows);
+  if (slabs != cdiv(dE.rows, CS_ROWS) || (dE.cols & 3) || (dE.stride & 3) || !aligned16(E)) return TNET_ERR_UNSUPPORTED;
+  p.group = g_group > 0 ? g_group : 8;
+  p.early_issue = g_early;
+  p.wt = g_wt;
+  const int na = cdiv(p.M, 64) * cdiv(p.N, 128), ncb = cdiv(dE.cols, CS_COLS * 4);
+  const unsigned grid = (unsigned)(na + ncb * slabs);
+  if (px_exact<64, 128, EPI_DSIG_CS>(p))
+    gemm16_bwd_slabs_kernel<true><<<grid, 256, 0, (hipStream_t)stream>>>(p, na, E, dE, colpartE, ldcolpartE, slabs, ncb);
+  else
+    gemm16_bwd_slabs_kernel<false><<<grid, 256, 0, (hipStream_t)stream>>>(p, na, E, dE, colpartE, ldcolpartE, slabs, ncb);
+  TNET_LAUNCH_CHECK();
+  return TNET_OK;
 }
 
 extern "C" int tnet_affine_update_bias(const float* X, TnetMatrixDim dX, const float* E, TnetMatrixDim dE, float* W,

@@ -16,6 +16,54 @@ __host__ __device__ static inline int cs_slabs(int rows) {
   return s;
 }
 
+// One block of the slab column sums (reduce.hip colsum_partial_kernel; gemm_f32.hip's backward GEMM +
+// slab-sum launch): partial[s][c] = sum of the rows of slab s in column c, row sub-group w (wave w) taking
+// rows r0+w, r0+w+4, ..., the CS_WAVES sub-group sums added in order.  Block (bx, s): CS_COLS * CW columns
+// from bx * CS_COLS * CW; `red`: CS_WAVES * CS_COLS * CW floats of the caller's LDS.
+template <bool V4>
+__device__ __forceinline__ void colsum_partial_block(const float* __restrict__ M, TnetMatrixDim d,
+                                                     float* __restrict__ partial, int slabs, int neg_from, long ldp,
+                                                     const int bx, const int s, float* __restrict__ red) {
+  constexpr int CW = V4 ? 4 : 1;  // columns per lane
+  constexpr int RW = CS_COLS * CW;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c0 = (bx * CS_COLS + lane) * CW;
+  const int rows_per = (d.rows + slabs - 1) / slabs;
+  const int r0 = s * rows_per, r1 = min(d.rows, r0 + rows_per);
+  float acc[CW];
+#pragma unroll
+  for (int k = 0; k < CW; ++k) acc[k] = 0.f;
+  if (c0 < d.cols) {
+#pragma unroll 8
+    for (int r = r0 + w; r < r1; r += CS_WAVES) {
+      // rows from neg_from on enter negated (RBM: positive minus negative phase statistics)
+      const float sg = r < neg_from ? 1.f : -1.f;
+      if (V4) {
+        const f32x4 v = *reinterpret_cast<const f32x4*>(M + (long)r * d.stride + c0);
+#pragma unroll
+        for (int k = 0; k < CW; ++k) acc[k] += sg * v[k];
+      } else {
+        acc[0] += sg * M[(long)r * d.stride + c0];
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < CW; ++k) red[w * RW + lane * CW + k] = acc[k];
+  __syncthreads();
+  if (w == 0) {
+#pragma unroll
+    for (int k = 0; k < CW; ++k) {
+      const int c = c0 + k;
+      if (c < d.cols) {
+        float t = red[lane * CW + k];
+#pragma unroll
+        for (int q = 1; q < CS_WAVES; ++q) t += red[q * RW + lane * CW + k];
+        partial[(long)s * ldp + c] = t;
+      }
+    }
+  }
+}
+
 // CD-1 statistics of one RBM step in ONE launch (cuRbm.cc:148-164 bias updates + the TRbmCu
 // reconstruction MSE, TRbmCu.cc:350), replacing two colsum_partial/colsum_final pairs and mse_kernel.
 // Blocks [0, nvb) take 16 visible columns of Vs = [pos_vis; neg_vis] (rows from B on enter negated),

@@ -19,45 +19,8 @@ template <bool V4>
 __global__ __launch_bounds__(256) void colsum_partial_kernel(const float* __restrict__ M, TnetMatrixDim d,
                                                              float* __restrict__ partial, int slabs, int neg_from,
                                                              long ldp) {
-  constexpr int CW = V4 ? 4 : 1;                 // columns per lane
-  __shared__ float red[CS_WAVES][CS_COLS * CW];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int c0 = (blockIdx.x * CS_COLS + lane) * CW;
-  const int s = blockIdx.y;
-  const int rows_per = (d.rows + slabs - 1) / slabs;
-  const int r0 = s * rows_per, r1 = min(d.rows, r0 + rows_per);
-  float acc[CW];
-#pragma unroll
-  for (int k = 0; k < CW; ++k) acc[k] = 0.f;
-  if (c0 < d.cols) {
-#pragma unroll 8
-    for (int r = r0 + w; r < r1; r += CS_WAVES) {
-      // rows from neg_from on enter negated (RBM: positive minus negative phase statistics)
-      const float sg = r < neg_from ? 1.f : -1.f;
-      if (V4) {
-        const f32x4 v = *reinterpret_cast<const f32x4*>(M + (long)r * d.stride + c0);
-#pragma unroll
-        for (int k = 0; k < CW; ++k) acc[k] += sg * v[k];
-      } else {
-        acc[0] += sg * M[(long)r * d.stride + c0];
-      }
-    }
-  }
-#pragma unroll
-  for (int k = 0; k < CW; ++k) red[w][lane * CW + k] = acc[k];
-  __syncthreads();
-  if (w == 0) {
-#pragma unroll
-    for (int k = 0; k < CW; ++k) {
-      const int c = c0 + k;
-      if (c < d.cols) {
-        float t = red[0][lane * CW + k];
-#pragma unroll
-        for (int q = 1; q < CS_WAVES; ++q) t += red[q][lane * CW + k];
-        partial[(long)s * ldp + c] = t;
-      }
-    }
-  }
+  __shared__ float red[CS_WAVES * CS_COLS * (V4 ? 4 : 1)];
+  colsum_partial_block<V4>(M, d, partial, slabs, neg_from, ldp, blockIdx.x, blockIdx.y, red);
 }
 
 // mode 0: v = alpha*sum + beta*v ; mode 1: bias update (c = sum + mmt*corr; b += scale*c; corr=c)

@@ -734,3 +734,36 @@ def test_affine_update_bias_gather_matches_separate_calls(mmt, rows, sides, gcol
     np.testing.assert_array_equal(yb, Xc[perm])
     np.testing.assert_array_equal(la, labc[perm])
     np.testing.assert_array_equal(lb, labc[perm])
+
+
+@pytest.mark.parametrize("rows,n_in,n_out", [(1024, 2048, 4000), (1024, 2048, 2048), (256, 512, 1000), (64, 128, 4000)])
+def test_affine_bwd_colsum_slabs_matches_two_calls(rows, n_in, n_out):
+    """tnet_affine_bwd_colsum_slabs (the top layer's backward GEMM + the slab sums of its input error in ONE
+    launch) against tnet_colsum_slab_sums + tnet_affine_bwd_colsum: Eo, Eo's slab sums and E's slab sums bit
+    for bit; TNET_ERR_UNSUPPORTED where the backward alone would run another tile configuration"""
+    E = rnd((rows, n_out), 400, 0.01)
+    W = rnd((n_in, n_out), 401, 0.05)
+    Yb = np.random.default_rng(402).random((rows, n_in)).astype(np.float32)
+    slabs = lib().tnet_colsum_slabs(rows)
+    dE, dW, dY = DeviceArray.from_numpy(E), DeviceArray.from_numpy(W), DeviceArray.from_numpy(Yb)
+    out = []
+    for one in (True, False):
+        dEo = DeviceArray.from_numpy(np.full((rows, n_in), np.nan, np.float32))
+        dP = DeviceArray.from_numpy(np.full((slabs, n_in), np.nan, np.float32))
+        dPt = DeviceArray.from_numpy(np.full((slabs, n_out), np.nan, np.float32))
+        if one:
+            st = lib().tnet_affine_bwd_colsum_slabs(dE.ptr, dE.dim, dW.ptr, dW.dim, dY.ptr, dY.stride, dEo.ptr, dEo.dim,
+                                                    dP.ptr, dP.stride, dPt.ptr, dPt.stride, S())
+            if -(-rows // 64) * -(-n_in // 128) < 200:
+                assert st == TNET_ERR_UNSUPPORTED
+                return
+            check(st)
+        else:
+            check(lib().tnet_colsum_slab_sums(dE.ptr, dE.dim, dPt.ptr, dPt.stride, S()))
+            check(lib().tnet_affine_bwd_colsum(dE.ptr, dE.dim, dW.ptr, dW.dim, dY.ptr, dY.stride, dEo.ptr, dEo.dim,
+                                               dP.ptr, dP.stride, S()))
+        out.append((dEo.numpy(), dP.numpy(), dPt.numpy()))
+    for a, b in zip(out[0], out[1]):
+        assert not np.isnan(a).any()
+        np.testing.assert_array_equal(a, b)
+    np.testing.assert_allclose(out[0][2], slab_sums(E), rtol=1e-5, atol=1e-6)
