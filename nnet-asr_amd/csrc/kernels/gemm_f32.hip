@@ -2912,6 +2912,10 @@ extern "C" int tnet_affine_update_bias_gather(const float* X, TnetMatrixDim dX, 
   if (!y || !x || !labels_out || !labels_in || !copy_from || dy.cols != dx.cols || dy.rows < 0 || dy.stride < dy.cols ||
       dx.stride < dx.cols)
     return TNET_ERR_ARG;
+  // the gather must not write what the updates read: y outside X and E (and X2, E2)
+  const float* y_end = y + (long)dy.rows * dy.stride;
+  auto overlaps = [&](const float* a, TnetMatrixDim d) { return a && y < a + (long)d.rows * d.stride && a < y_end; };
+  if (overlaps(X, dX) || overlaps(E, dE) || (two && (overlaps(X2, dX2) || overlaps(E2, dE2)))) return TNET_ERR_ARG;
   const int c4 = (dy.cols + 3) & ~3;
   if (((uintptr_t)y & 15) || ((uintptr_t)x & 15) || (dy.stride & 3) || (dx.stride & 3) || c4 > dy.stride ||
       c4 > dx.stride)

@@ -710,6 +710,11 @@ def test_affine_update_bias_gather_matches_separate_calls(mmt, rows, sides, gcol
         if fused:
             second = args[1] if len(args) > 1 else [None, MatrixDim(0, 0, 0), None, MatrixDim(0, 0, 0), None,
                                                      MatrixDim(0, 0, 0), None, 0, 0.0, 0.0, 0.0, None, 0, None, None]
+            # a destination inside the update's own X: refused before anything is launched
+            bad = [dev[0]["dX"].ptr, dXc.ptr, dLo.ptr, dLc.ptr, dPerm.ptr, MatrixDim(8, gcols, dev[0]["dX"].stride),
+                   dXc.dim]
+            if dev[0]["dX"].cols == gcols:
+                assert lib().tnet_affine_update_bias_gather(*args[0], *second, *bad, S()) == TNET_ERR_ARG
             st = lib().tnet_affine_update_bias_gather(*args[0], *second, *gargs, S())
             if sides == [(2048, 2048)]:
                 assert st == TNET_ERR_UNSUPPORTED
