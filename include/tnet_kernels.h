@@ -255,7 +255,8 @@ int tnet_affine_bwd_colsum_slabs(const float* E, TnetMatrixDim dE, const float* 
  * tnet_affine_update_bias_pair -- plus tnet_gather_bunch(y, x, labels_out, labels_in, copy_from, dy, dx)
  * (CuCache::GetBunch of the bunch after this one, cuCache.cc:155-200) as extra workgroups on the CUs the
  * update's tiles leave free.  The gather must be independent of the updates (y / labels_out overlap none of
- * their operands: the trainer gathers into the other half of a double-buffered bunch).  Results identical
+ * their operands -- TNET_ERR_ARG where y overlaps X, E, X2 or E2: the trainer gathers into the other half of a
+ * double-buffered bunch).  Results identical
  * to the separate calls (the gather may also fill y's row padding up to the next multiple of 4 columns);
  * TNET_ERR_UNSUPPORTED when the updates would run another tile configuration alone, fewer than 8 CUs are
  * left for the gather, or the strides are not 16-B multiples (make the separate calls). */
