@@ -1,7 +1,6 @@
 set -o pipefail
 mkdir -p gpurun_out
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-timeout -k 10 300 python3 -u -m pytest -x -q -rf --timeout 120 --timeout-method thread tests/test_gpu_kernels.py -k "gather" > gpurun_out/r3s3_gather_refuse.txt 2>&1 &&
-timeout -k 10 900 python3 -u -m pytest -q -rf --timeout 300 --timeout-method thread -m gpu tests > gpurun_out/r3s3_gpu_suite_last2.txt 2>&1 &&
-timeout -k 10 200 python3 -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r3s3_smoke_last2.log 2>&1
+timeout -k 10 300 python3 -u -m pytest -x -q -rf --timeout 120 --timeout-method thread tests/test_gpu_kernels.py tests/test_gpu_train.py > gpurun_out/r3s3_last_check.txt 2>&1 &&
+timeout -k 10 200 python3 -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r3s3_smoke_last3.log 2>&1
 echo "done $?"
