@@ -123,6 +123,22 @@ def parse_kernel_report(text):
     return out
 
 
+def mapped_runtime():
+    """the HIP runtime / RCCL this process actually mapped (with torch installed,
+    tnet_amd binds torch's bundled libamdhip64 / librccl, whose collective kernels' footprint is in
+    profiles/r04_rccl_footprint.json)"""
+    seen = {}
+    try:
+        for line in open("/proc/self/maps"):
+            p = line.split()[-1]
+            for key in ("librccl", "libamdhip64"):
+                if key in p:
+                    seen[key] = os.path.realpath(p)
+    except OSError:
+        pass
+    return seen
+
+
 def dp_mode(world):
     """the RCCL exchange's form (RcclExchange: all-reduce unless TNET_DP_SHARD=1)"""
     shard = os.environ.get("TNET_DP_SHARD", "0") == "1"
@@ -234,7 +250,9 @@ def main():
     kern = {}
     roof_shape = roofline_shape(dims)
     if args.kernel_timing:
-        check(lib().tnet_kernel_timing_filter(roof_shape.encode()), "timing_filter")
+        # "gemm_*<shape>": the GEMM launches of the roofline shape only (not the data-parallel SGD applies of
+        # that shape, which run on the apply stream); runs also close at every exchange step
+        check(lib().tnet_kernel_timing_filter(("gemm_*" + roof_shape).encode()), "timing_filter")
         check(lib().tnet_kernel_timing(2 if args.kernel_timing == 1 else 1), "kernel_timing")
         trainer.replay(args.steps)
         check(lib().tnet_kernel_timing(0), "kernel_timing")
@@ -332,6 +350,7 @@ def main():
             "cpu_baseline": cpu,
             "replica_check": {"ranks": world, "identical": True, "param_sha256_16": replicas[0],
                               "param_sum": replicas[1]},
+            "runtime": mapped_runtime(),
             "kernels": kernels,
             "kernels_note": f"every launch event-timed, {args.breakdown_steps} extra steps after the timed region "
                             "(event pairs add stream time: the value region has none, the roofline region times "

@@ -1,6 +1,9 @@
 set -o pipefail
 mkdir -p gpurun_out
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-timeout -k 10 300 python3 -u -m pytest -x -q -rf --timeout 120 --timeout-method thread tests/test_gpu_kernels.py tests/test_gpu_train.py > gpurun_out/r3s3_last_check.txt 2>&1 &&
-timeout -k 10 200 python3 -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r3s3_smoke_last3.log 2>&1
+timeout -k 10 300 python3 -u tools/diag_step_resync.py > gpurun_out/r4s1_resync.txt 2>&1
+timeout -k 10 900 python3 -u -m pytest -x -v -rf --timeout 400 --timeout-method thread -s \
+  "tests/test_ex01.py::test_every_step_of_the_epoch_matches_reference_step" tests/test_gpu_dp.py > gpurun_out/r4s1_new_b.txt 2>&1 &&
+timeout -k 10 300 python3 bench.py --steps 20 --warmup 5 > gpurun_out/r4s1_bench.json 2> gpurun_out/r4s1_bench.err &&
+timeout -k 10 300 python3 bench.py --steps 20 --warmup 5 --force-dp --no-cpu-baseline > gpurun_out/r4s1_bench_fdp.json 2> gpurun_out/r4s1_bench_fdp.err
 echo "done $?"

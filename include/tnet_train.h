@@ -111,6 +111,9 @@ long tnet_trainer_steps(TnetTrainer* t);
 int tnet_trainer_replay(TnetTrainer* t, long nsteps); /* benchmark: more steps over the resident cache */
 /* benchmark setup: load host frames into the cache without training; returns rows taken (<0 error) */
 long tnet_trainer_prefill(TnetTrainer* t, const float* feats, int rows, int cols, int ld, const int* labels);
+/* fault injection (tests): the n-th next network training step throws before it enqueues anything (the
+   call that ran it returns TNET_ERR_RUNTIME); 0 disarms.  No reference counterpart (test hook). */
+int tnet_debug_fail_train_bunch(long n);
 int tnet_trainer_set_comm(TnetTrainer* t, TnetComm* comm);
 /* data-parallel steps this rank joined without a bunch of its own (zero gradient) */
 long tnet_trainer_empty_steps(TnetTrainer* t);

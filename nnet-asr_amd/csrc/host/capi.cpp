@@ -376,6 +376,10 @@ int tnet_trainer_finish(TnetTrainer* t) {
   TRY_END
 }
 long tnet_trainer_steps(TnetTrainer* t) { return t ? t->t->Steps() : -1; }
+int tnet_debug_fail_train_bunch(long n) {
+  TRY_BEGIN CuNetwork::DebugFailTrainBunch(n < 0 ? 0 : n);
+  TRY_END
+}
 int tnet_trainer_replay(TnetTrainer* t, long n) {
   TRY_BEGIN t->t->Replay(n);
   TRY_END

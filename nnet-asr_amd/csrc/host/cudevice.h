@@ -60,8 +60,17 @@ class CuDevice {
   /// time only the launches whose tag contains `filter` (empty = all): each event pair costs
   /// a few microseconds of stream time, so a benchmark times only the kernel it reports
   void KernelTimingFilter(const std::string& filter) { mKTFilter = filter; }
+  /// the filter selects tags containing it, or -- "prefix*suffix" -- tags starting with prefix and ending
+  /// with suffix ("gemm_*:2048x2048": the 2048x2048 GEMM launches, not the data-parallel applies of that
+  /// shape, which run on another stream)
   bool KernelTimed(const std::string& tag) const {
-    return mKTOn && (mKTFilter.empty() || tag.find(mKTFilter) != std::string::npos);
+    if (!mKTOn) return false;
+    if (mKTFilter.empty()) return true;
+    const size_t star = mKTFilter.find('*');
+    if (star == std::string::npos) return tag.find(mKTFilter) != std::string::npos;
+    const size_t np = star, ns = mKTFilter.size() - star - 1;
+    return tag.size() >= np + ns && tag.compare(0, np, mKTFilter, 0, np) == 0 &&
+           tag.compare(tag.size() - ns, ns, mKTFilter, star + 1, ns) == 0;
   }
   void KTRecord(const std::string& tag, double work, hipEvent_t a, hipEvent_t b, int count = 1);
   hipEvent_t KTEvent();

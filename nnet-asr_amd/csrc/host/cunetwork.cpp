@@ -239,8 +239,13 @@ void CuUpdatableComponent::ZeroGradient() {
     TNET_HIP_CALL(hipMemsetAsync(b.grad, 0, (size_t)b.n * sizeof(float), CuDevice::Instantiate().Stream()));
 }
 
+// fault injection (tnet_debug_fail_train_bunch): the n-th next TrainBunch throws before it enqueues anything
+static long g_fail_train_bunch = 0;
+void CuNetwork::DebugFailTrainBunch(long n) { g_fail_train_bunch = n; }
+
 void CuNetwork::TrainBunch(const CuMatrix<BaseFloat>& X, const CuVector<int>& labels, CuObjectiveFunction& obj,
                            bool train, GradExchange* exchange) {
+  if (g_fail_train_bunch > 0 && --g_fail_train_bunch == 0) Error("CuNetwork::TrainBunch: injected fault");
   if (!IsFusableMLP() || obj.GetTypeId() != CuObjectiveFunction::CROSS_ENTROPY) {
     if (exchange) Error("CuNetwork::TrainBunch: data-parallel training needs the sigmoid-MLP topology");
     TrainBunchGeneric(X, labels, obj, train);
@@ -446,8 +451,8 @@ void CuNetwork::TrainBunch(const CuMatrix<BaseFloat>& X, const CuVector<int>& la
     // (both grids in one round over the CUs) go out as ONE launch
     // (with the next bunch's gather on the CUs their tiles leave free, when the trainer handed one over)
     if ((stopper || l == 0) && pend.lin && !exchange && err_colsum && lin->LearnRate() > 0.0f) {
-      if (mTailGather && pend.lin->UpdateFromColsumGather(*pend.X, *pend.E, *mColPart[pend.l], lin, acts[l], err,
-                                                          mColPart[l].get(), *mTailGather)) {
+      if (mHasTailGather && pend.lin->UpdateFromColsumGather(*pend.X, *pend.E, *mColPart[pend.l], lin, acts[l], err,
+                                                             mColPart[l].get(), mTailGather)) {
         mTailDone = true;
         pend.lin = nullptr;
         break;
@@ -491,9 +496,9 @@ void CuNetwork::TrainBunch(const CuMatrix<BaseFloat>& X, const CuVector<int>& la
     err_colsum = eo_colsum;
   }
   // the step's last update (the stopper's): the next bunch's gather rides on its launch
-  if (pend.lin && mTailGather && !mTailDone &&
+  if (pend.lin && mHasTailGather && !mTailDone &&
       pend.lin->UpdateFromColsumGather(*pend.X, *pend.E, *mColPart[pend.l], nullptr, nullptr, nullptr, nullptr,
-                                       *mTailGather)) {
+                                       mTailGather)) {
     mTailDone = true;
     pend.lin = nullptr;
   }

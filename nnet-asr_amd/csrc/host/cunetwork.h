@@ -80,12 +80,17 @@ class CuNetwork {
   void KeepOutput(bool keep) { mKeepOutput = keep; }
   /// The NEXT bunch's gather, carried by the last weight-update launch of the next TrainBunch where the
   /// library takes it (tnet_affine_update_bias_gather: the update's tiles leave CUs free); TailGatherDone()
-  /// says whether it went out -- if not, the caller launches it.  `g` must outlive that TrainBunch.
+  /// says whether it went out -- if not, the caller launches it.  The descriptor is copied (the network
+  /// never holds a pointer into the caller's frame); nullptr clears it.
   void SetTailGather(const BunchGather* g) {
-    mTailGather = g;
+    mHasTailGather = g != nullptr;
+    if (g) mTailGather = *g;
     mTailDone = false;
   }
   bool TailGatherDone() const { return mTailDone; }
+  /// Fault injection for the recovery tests: the n-th next TrainBunch (any network) throws before it
+  /// enqueues anything; 0 disarms.
+  static void DebugFailTrainBunch(long n);
 
  private:
   CuComponent* ComponentFactory(std::istream& In);
@@ -99,7 +104,8 @@ class CuNetwork {
   BaseFloat mGlobLearnRate = 0.0f;
   std::string mLearnRateFactors;
   bool mKeepOutput = false;
-  const BunchGather* mTailGather = nullptr;
+  BunchGather mTailGather;
+  bool mHasTailGather = false;
   bool mTailDone = false;
   // fused-path buffers: activations of sigmoid layers are the components' own outputs;
   // errors live here (one per affine layer input)

@@ -270,10 +270,25 @@ void CuRbmTrainer::Step() {
   static const bool tail = !(getenv("TNET_GATHER_TAIL") && getenv("TNET_GATHER_TAIL")[0] == '0');
   BunchGather tg;
   const bool tail_now = tail && B <= 512 && mCache.HasBunchAhead();
-  if (tail_now) tg = mCache.AheadGather(mNextPosVis, mDummyLabels);
+  // once the cache has moved past the next bunch it must land in the other buffer whatever happens below
+  // (ADVICE r3): mAheadV is set at once, and if the step throws before the gather went out, the guard
+  // launches it (unchecked) while unwinding
+  struct Pending {
+    const BunchGather* g = nullptr;
+    hipStream_t s = nullptr;
+    ~Pending() {
+      if (g) (void)tnet_gather_bunch(g->y, g->x, g->labels_out, g->labels_in, g->copy_from, g->dy, g->dx, s);
+    }
+  } pending;
+  if (tail_now) {
+    tg = mCache.AheadGather(mNextPosVis, mDummyLabels);
+    mAheadV = true;
+    pending.g = &tg;
+    pending.s = (hipStream_t)S;
+  }
   auto finish_gather = [&](bool done) {
     if (!tail_now) return;
-    mAheadV = true;
+    pending.g = nullptr;
     if (!done)
       TNET_SAFE_CALL(tnet_gather_bunch(tg.y, tg.x, tg.labels_out, tg.labels_in, tg.copy_from, tg.dy, tg.dx, S));
   };

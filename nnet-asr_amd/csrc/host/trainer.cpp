@@ -37,6 +37,38 @@ CuTrainer::~CuTrainer() {
   if (mAheadStream) (void)hipStreamDestroy(mAheadStream);
 }
 
+// The next bunch's gather handed to the network for the step's last launch (CuNetwork::SetTailGather).
+// Finish(): if no launch carried it, launch it now (checked).  If the step throws first, the destructor
+// clears the network's descriptor and launches the gather unchecked, so the bunch the cache already moved
+// past still lands in the other buffer and the next Step trains it.
+struct TailGatherGuard {
+  CuNetwork& net;
+  hipStream_t stream;
+  BunchGather g;
+  bool armed = false;
+  TailGatherGuard(CuNetwork& n, hipStream_t s) : net(n), stream(s) {}
+  void Arm(const BunchGather& gather, bool ride) {
+    g = gather;
+    armed = true;
+    if (ride) net.SetTailGather(&g);
+  }
+  bool Take() {
+    if (!armed) return false;
+    armed = false;
+    const bool done = net.TailGatherDone();
+    net.SetTailGather(nullptr);
+    return !done;
+  }
+  void Finish() {
+    if (!Take()) return;
+    KTScope kt("gather", 2.0 * g.dy.rows * g.dy.cols * 4.0);
+    TNET_SAFE_CALL(tnet_gather_bunch(g.y, g.x, g.labels_out, g.labels_in, g.copy_from, g.dy, g.dx, stream));
+  }
+  ~TailGatherGuard() {
+    if (Take()) (void)tnet_gather_bunch(g.y, g.x, g.labels_out, g.labels_in, g.copy_from, g.dy, g.dx, stream);
+  }
+};
+
 void CuTrainer::Step() {
   hipStream_t cs = CuDevice::Instantiate().Stream();
   if (mAhead) {  // gathered during the previous step
@@ -70,33 +102,26 @@ void CuTrainer::Step() {
     mAhead = true;
     mAheadOnStream = true;
   }
-  // Default (TNET_GATHER_TAIL=0: off): the next bunch of the fill is gathered into the other buffer by the
-  // step's LAST weight-update launch, on the CUs its tiles leave free (tnet_affine_update_bias_gather) --
-  // in stream order, so no cross-stream wait, and one launch less per step.  Where the library does not
-  // take it (shapes, data parallelism, cross-validation), the gather is launched right after the step.
+  // On by default (TNET_GATHER_TAIL=0 turns it off): the next bunch of the fill is gathered into the other
+  // buffer by the step's LAST weight-update launch, on the CUs its tiles leave free
+  // (tnet_affine_update_bias_gather) -- in stream order, so no cross-stream wait, and one launch less per
+  // step.  Where the library does not take it (shapes, data parallelism, cross-validation), the gather is
+  // launched right after the step.
   static const bool tail = !(getenv("TNET_GATHER_TAIL") && getenv("TNET_GATHER_TAIL")[0] == '0');
-  BunchGather tg;
-  bool tail_now = false;
+  TailGatherGuard guard(*mNet, cs);
   if (!mAhead && tail && mCache.HasBunchAhead()) {
     CuMatrix<BaseFloat>& nf = mFeatsB[mCur ^ 1];
     CuVector<int>& nl = mLabelsB[mCur ^ 1];
     nf.Init(mCache.Bunchsize(), mFeatsB[mCur].Cols());
     nl.Init(mCache.Bunchsize());
-    tg = mCache.AheadGather(nf, nl);
-    tail_now = true;
+    // from here the cache has moved past that bunch: mAhead stays true and the guard delivers the bunch into
+    // the other buffer whatever happens below (a throwing TrainBunch must not skip a bunch)
+    guard.Arm(mCache.AheadGather(nf, nl), !mOpt.crossval && !mExchange);
     mAhead = true;
     mAheadOnStream = false;
-    if (!mOpt.crossval && !mExchange) mNet->SetTailGather(&tg);
   }
   mNet->TrainBunch(mFeatsB[mCur], mLabelsB[mCur], *mObj, !mOpt.crossval, mOpt.crossval ? nullptr : mExchange);
-  if (tail_now) {
-    const bool done = mNet->TailGatherDone();
-    mNet->SetTailGather(nullptr);
-    if (!done) {
-      KTScope kt("gather", 2.0 * tg.dy.rows * tg.dy.cols * 4.0);
-      TNET_SAFE_CALL(tnet_gather_bunch(tg.y, tg.x, tg.labels_out, tg.labels_in, tg.copy_from, tg.dy, tg.dx, cs));
-    }
-  }
+  guard.Finish();
   if (mOpt.trace & 2) std::cout << "." << std::flush;
   mSteps++;
 }
@@ -287,6 +312,7 @@ int HostExchange::ApplyRanges(long n, long* lo, long* hi) const {
 }
 
 void HostExchange::GatherParams(CuUpdatableComponent& comp, int i, void* stream) {
+  CuDevice::Instantiate().KTCloseRun();  // no roofline timing run spans an exchange step
   (void)i;
   if (!mShard) return;
   CuDevice& dev = CuDevice::Instantiate();
@@ -305,12 +331,14 @@ void HostExchange::GatherParams(CuUpdatableComponent& comp, int i, void* stream)
 }
 
 void HostExchange::Submit(CuUpdatableComponent& comp) {
+  CuDevice::Instantiate().KTCloseRun();  // no roofline timing run spans an exchange step
   CuDevice& dev = CuDevice::Instantiate();
   TNET_HIP_CALL(hipStreamSynchronize(dev.Stream()));
   for (auto& b : comp.GradientBlocks()) AllReduceDevice(b.grad, (size_t)b.n);
 }
 
 void HostExchange::AllReduceDevice(float* buf, size_t n) {
+  CuDevice::Instantiate().KTCloseRun();  // no roofline timing run spans an exchange step
   CuDevice& dev = CuDevice::Instantiate();
   mStage.resize(n);
   TNET_HIP_CALL(hipMemcpyAsync(mStage.data(), buf, n * sizeof(float), hipMemcpyDeviceToHost, dev.Stream()));
@@ -477,6 +505,7 @@ void RcclExchange::GatherParams(CuUpdatableComponent& comp, int i, void* stream)
 }
 
 void RcclExchange::WaitFor(int i) {
+  CuDevice::Instantiate().KTCloseRun();  // no roofline timing run spans an exchange step
   if (i < 0 || (size_t)i >= mImpl->next_event) Error("RcclExchange::WaitFor: no such reduction");
   TNET_HIP_CALL(hipStreamWaitEvent(CuDevice::Instantiate().Stream(), mImpl->ar_done[(size_t)i], 0));
 }
@@ -491,6 +520,7 @@ void* RcclExchange::ApplyStream(int i) {
 }
 
 void RcclExchange::WaitAll() {
+  CuDevice::Instantiate().KTCloseRun();  // no roofline timing run spans an exchange step
   CuDevice& dev = CuDevice::Instantiate();
   TNET_HIP_CALL(hipEventRecord(mImpl->done, mImpl->comm_stream));
   TNET_HIP_CALL(hipStreamWaitEvent(dev.Stream(), mImpl->done, 0));
@@ -504,6 +534,7 @@ void RcclExchange::WaitAll() {
 }
 
 void RcclExchange::AllReduceHost(double* v, int n) {
+  CuDevice::Instantiate().KTCloseRun();  // no roofline timing run spans an exchange step
   if (n <= 0) return;
   if (n > 512) Error("RcclExchange::AllReduceHost: too many values");
   CuDevice& dev = CuDevice::Instantiate();
@@ -515,6 +546,7 @@ void RcclExchange::AllReduceHost(double* v, int n) {
 }
 
 void RcclExchange::AllReduceDevice(float* buf, size_t n) {
+  CuDevice::Instantiate().KTCloseRun();  // no roofline timing run spans an exchange step
   CuDevice& dev = CuDevice::Instantiate();
   TNET_HIP_CALL(hipStreamSynchronize(dev.Stream()));
   NCCL_CALL(ncclAllReduce(buf, buf, n, ncclFloat, ncclSum, mImpl->comm, mImpl->comm_stream));

@@ -26,7 +26,9 @@
 #include <float.h>
 
 #include <cstdlib>
+#include <array>
 #include <cstring>
+#include <initializer_list>
 #include <map>
 #include <mutex>
 
@@ -2667,6 +2669,45 @@ static int rbm_update_stats_run(const float* V, TnetMatrixDim dV, const float* H
                                 float* vb, float* cvb, float* hb, float* chb, double* mse_stats, const BunchGatherP& g,
                                 int ng, void* stream);
 
+// byte ranges one launch touches: a gather riding on an update launch must be independent of it -- nothing
+// the gather writes (y, labels_out) may be read or written by the update, nothing the update writes may be
+// read by the gather (x, labels_in, copy_from) -- or the combined launch is a race the separate calls are not
+struct ByteSpan {
+  const void* p;
+  size_t n;
+};
+static ByteSpan span_of(const void* p, long rows, long stride, size_t elem) {
+  return ByteSpan{p, p && rows > 0 && stride > 0 ? (size_t)rows * (size_t)stride * elem : 0};
+}
+static bool spans_overlap(ByteSpan a, ByteSpan b) {
+  if (!a.p || !b.p || !a.n || !b.n) return false;
+  const char *a0 = (const char*)a.p, *b0 = (const char*)b.p;
+  return a0 < b0 + b.n && b0 < a0 + a.n;
+}
+static bool any_overlap(std::initializer_list<ByteSpan> xs, std::initializer_list<ByteSpan> ys) {
+  for (const ByteSpan& x : xs)
+    for (const ByteSpan& y : ys)
+      if (spans_overlap(x, y)) return true;
+  return false;
+}
+// the gather's writes / reads (tnet_gather_bunch: y[dy.rows x dy.stride], labels_out[dy.rows] written;
+// x[dx.rows x dx.stride], labels_in[dx.rows], copy_from[dy.rows] read)
+static bool gather_independent(float* y, const float* x, int* labels_out, const int* labels_in, const int* copy_from,
+                               TnetMatrixDim dy, TnetMatrixDim dx, std::initializer_list<ByteSpan> upd_reads,
+                               std::initializer_list<ByteSpan> upd_writes) {
+  const ByteSpan gw[] = {span_of(y, dy.rows, dy.stride, 4), span_of(labels_out, dy.rows, 1, 4)};
+  const ByteSpan gr[] = {span_of(x, dx.rows, dx.stride, 4), span_of(labels_in, dx.rows, 1, 4),
+                         span_of(copy_from, dy.rows, 1, 4)};
+  for (const ByteSpan& w : gw) {
+    if (any_overlap({w}, upd_reads) || any_overlap({w}, upd_writes)) return false;
+    for (const ByteSpan& r : gr)
+      if (spans_overlap(w, r)) return false;
+  }
+  for (const ByteSpan& r : gr)
+    if (any_overlap({r}, upd_writes)) return false;
+  return true;
+}
+
 extern "C" int tnet_rbm_update_stats(const float* V, TnetMatrixDim dV, const float* H, TnetMatrixDim dH, float* W,
                                      TnetMatrixDim dW, float* corrW, int strideCorr, float scale, float mmt, float l2,
                                      int B, float* vb, float* cvb, float* hb, float* chb, double* mse_stats,
@@ -2689,10 +2730,14 @@ extern "C" int tnet_rbm_update_stats_gather(const float* V, TnetMatrixDim dV, co
   if (((uintptr_t)y & 15) || ((uintptr_t)x & 15) || (dy.stride & 3) || (dx.stride & 3) || c4 > dy.stride ||
       c4 > dx.stride)
     return TNET_ERR_UNSUPPORTED;
-  // the gather must not touch what the update reads: y outside V's rows
-  const float* v_end = V + (long)dV.rows * dV.stride;
-  const float* y_end = y + (long)dy.rows * dy.stride;
-  if (y < v_end && V < y_end) return TNET_ERR_ARG;
+  // the gather independent of the update + statistics (they read V, H; write W, its momentum, both biases and
+  // their momentum, the MSE slots)
+  if (!gather_independent(y, x, labels_out, labels_in, copy_from, dy, dx,
+                          {span_of(V, dV.rows, dV.stride, 4), span_of(H, dH.rows, dH.stride, 4)},
+                          {span_of(W, dW.rows, dW.stride, 4), span_of(corrW, dW.rows, strideCorr, 4),
+                           span_of(vb, dV.cols, 1, 4), span_of(cvb, dV.cols, 1, 4), span_of(hb, dH.cols, 1, 4),
+                           span_of(chb, dH.cols, 1, 4), span_of(mse_stats, TNET_STATS_WORDS, 1, 8)}))
+    return TNET_ERR_ARG;
   return rbm_update_stats_run(V, dV, H, dH, W, dW, corrW, strideCorr, scale, mmt, l2, B, vb, cvb, hb, chb, mse_stats,
                               BunchGatherP{y, x, labels_out, labels_in, copy_from, dy.rows, c4, dy.stride, dx.stride},
                               16, stream);
@@ -2912,10 +2957,21 @@ extern "C" int tnet_affine_update_bias_gather(const float* X, TnetMatrixDim dX, 
   if (!y || !x || !labels_out || !labels_in || !copy_from || dy.cols != dx.cols || dy.rows < 0 || dy.stride < dy.cols ||
       dx.stride < dx.cols)
     return TNET_ERR_ARG;
-  // the gather must not write what the updates read: y outside X and E (and X2, E2)
-  const float* y_end = y + (long)dy.rows * dy.stride;
-  auto overlaps = [&](const float* a, TnetMatrixDim d) { return a && y < a + (long)d.rows * d.stride && a < y_end; };
-  if (overlaps(X, dX) || overlaps(E, dE) || (two && (overlaps(X2, dX2) || overlaps(E2, dE2)))) return TNET_ERR_ARG;
+  // the gather independent of the update(s): they read X, E and the slab sums, read and write W, its momentum,
+  // b and its momentum
+  auto reads = [](const GemmP& q) {
+    return std::array<ByteSpan, 3>{span_of(q.A, q.K, q.lda, 4), span_of(q.B, q.K, q.ldb, 4),
+                                    span_of(q.bpart, q.bslabs, q.ldbpart, 4)};
+  };
+  auto writes = [](const GemmP& q) {
+    return std::array<ByteSpan, 4>{span_of(q.C, q.M, q.ldc, 4), span_of(q.corr, q.M, q.ldcorr, 4),
+                                   span_of(q.bvec, q.N, 1, 4), span_of(q.bcorr, q.N, 1, 4)};
+  };
+  const auto ra = reads(pa), rb = reads(pb);
+  const auto wa = writes(pa), wb = writes(pb);
+  if (!gather_independent(y, x, labels_out, labels_in, copy_from, dy, dx, {ra[0], ra[1], ra[2], rb[0], rb[1], rb[2]},
+                          {wa[0], wa[1], wa[2], wa[3], wb[0], wb[1], wb[2], wb[3]}))
+    return TNET_ERR_ARG;
   const int c4 = (dy.cols + 3) & ~3;
   if (((uintptr_t)y & 15) || ((uintptr_t)x & 15) || (dy.stride & 3) || (dx.stride & 3) || c4 > dy.stride ||
       c4 > dx.stride)

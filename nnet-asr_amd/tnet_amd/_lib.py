@@ -151,6 +151,7 @@ _SIGS = {
     "tnet_trainer_steps": (i64, [vp]),
     "tnet_trainer_replay": (i32, [vp, i64]),
     "tnet_trainer_prefill": (i64, [vp, vp, i32, i32, i32, vp]),
+    "tnet_debug_fail_train_bunch": (i32, [i64]),
     "tnet_trainer_set_comm": (i32, [vp, vp]),
     "tnet_trainer_trace": (i32, [vp, i32]),
     "tnet_trainer_set_transform": (i32, [vp, vp, i32, i32]),

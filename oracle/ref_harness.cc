@@ -4,6 +4,8 @@
 // read-only sources under /root/reference/src) and drives them exactly the way the
 // reference's single-thread training platform does, dumping full-precision results:
 //
+//   trajectory: the same step loop writing the parameters before / after every step in binary (the
+//             reference trajectory of the per-step resync test)
 //   step    : per-bunch SGD with TNet --THREADS=1 semantics, i.e. the Platform::Thread
 //             bunch loop (src/TNetLib/Platform.h:300-336): clone->Propagate,
 //             CrossEntropy::Evaluate, clone->Backpropagate (Gradient()), master
@@ -26,6 +28,7 @@
 #include <string>
 #include <vector>
 
+#include "BiasedLinearity.h"
 #include "Nnet.h"
 #include "ObjFun.h"
 #include "Cache.h"
@@ -103,6 +106,80 @@ static int cmd_step(int argc, char** argv) {
   std::ofstream rep((out + "/report.txt").c_str());
   rep.precision(17);
   rep << obj->GetError() << " " << obj->GetFrames() << "\n" << obj->Report();
+  delete obj;
+  delete clone;
+  return 0;
+}
+
+// the <biasedlinearity> parameters of a network as float32, in .nnet order per layer: W^T [out x in] row by row,
+// then b [out].  The weights are read through pointers to the protected members taken in a derived class
+// (well-defined access; nothing of TNetLib is modified)
+struct LinearityAccess : public BiasedLinearity {
+  static const Matrix<BaseFloat>& W(const BiasedLinearity& c) { return c.*(&LinearityAccess::mLinearity); }
+  static const Vector<BaseFloat>& b(const BiasedLinearity& c) { return c.*(&LinearityAccess::mBias); }
+};
+static void dump_params(std::ofstream& f, Network& nnet) {
+  for (int i = 0; i < nnet.Layers(); i++) {
+    Component& c = nnet.Layer(i);
+    if (c.GetType() != Component::BIASED_LINEARITY) continue;
+    const BiasedLinearity& bl = static_cast<const BiasedLinearity&>(c);
+    const Matrix<BaseFloat>& W = LinearityAccess::W(bl);  // [in x out]
+    const Vector<BaseFloat>& b = LinearityAccess::b(bl);
+    std::vector<float> buf(W.Rows() * W.Cols());
+    for (size_t o = 0; o < W.Cols(); o++)
+      for (size_t r = 0; r < W.Rows(); r++) buf[o * W.Rows() + r] = W(r, o);
+    f.write((const char*)&buf[0], buf.size() * 4);
+    for (size_t o = 0; o < b.Dim(); o++) {
+      float v = b[o];
+      f.write((const char*)&v, 4);
+    }
+  }
+}
+
+// trajectory <nnet> <X.f32> <lab.i32> <nIn> <nClasses> <bunch> <nsteps> <lr> <wc> <params.f32> <Y.f32>
+// The step loop of `step` (TNet --THREADS=1 semantics), writing the parameters BEFORE every step and after the
+// last (nsteps + 1 records of dump_params) and every step's network output: the reference trajectory the
+// per-step resync test restarts the GPU network from (tests/test_ex01.py)
+static int cmd_trajectory(int argc, char** argv) {
+  if (argc < 13) { std::cerr << "usage: trajectory nnet X lab nIn nCls bunch nsteps lr wc params Y\n"; return 2; }
+  int n_in = atoi(argv[5]), n_cls = atoi(argv[6]), bunch = atoi(argv[7]), nsteps = atoi(argv[8]);
+  float lr = (float)atof(argv[9]), wc = (float)atof(argv[10]);
+  std::vector<char> xb = slurp(argv[3]), lb = slurp(argv[4]);
+  const float* X = (const float*)&xb[0];
+  const int* L = (const int*)&lb[0];
+  if ((size_t)bunch * nsteps > xb.size() / 4 / n_in) { std::cerr << "not enough frames\n"; return 2; }
+  Network nnet;
+  nnet.ReadNetwork(argv[2]);
+  nnet.SetLearnRate(lr);
+  nnet.SetWeightcost(wc);
+  Network* clone = nnet.Clone();
+  ObjectiveFunction* obj = ObjectiveFunction::Factory(ObjectiveFunction::CROSS_ENTROPY);
+  std::ofstream pf(argv[11], std::ios::binary), yf(argv[12], std::ios::binary);
+  Matrix<BaseFloat> fea(bunch, n_in), lab(bunch, n_cls), outm, err;
+  dump_params(pf, nnet);
+  for (int s = 0; s < nsteps; s++) {
+    lab.Zero();
+    for (int r = 0; r < bunch; r++) {
+      size_t fr = (size_t)s * bunch + r;
+      for (int c = 0; c < n_in; c++) fea(r, c) = X[fr * n_in + c];
+      if (L[fr] >= 0) lab(r, L[fr]) = 1.0f;
+    }
+    clone->Propagate(fea, outm);
+    obj->Evaluate(outm, lab, &err);
+    clone->Backpropagate(err);
+    nnet.AccuGradient(*clone, 0, 1);
+    nnet.AccuBunchsize(*clone);
+    nnet.Update(0, 1);
+    nnet.ResetBunchsize();
+    for (size_t r = 0; r < outm.Rows(); r++)
+      for (size_t c = 0; c < outm.Cols(); c++) {
+        float v = outm(r, c);
+        yf.write((const char*)&v, 4);
+      }
+    dump_params(pf, nnet);
+  }
+  std::cout.precision(17);
+  std::cout << obj->GetError() << " " << obj->GetFrames() << "\n";
   delete obj;
   delete clone;
   return 0;
@@ -242,9 +319,10 @@ static int cmd_features(int argc, char** argv) {
 }
 
 int main(int argc, char** argv) try {
-  if (argc < 2) { std::cerr << "modes: step | shuffle | train | features\n"; return 2; }
+  if (argc < 2) { std::cerr << "modes: step | trajectory | shuffle | train | features\n"; return 2; }
   std::string mode = argv[1];
   if (mode == "step") return cmd_step(argc, argv);
+  if (mode == "trajectory") return cmd_trajectory(argc, argv);
   if (mode == "shuffle") return cmd_shuffle(argc, argv);
   if (mode == "train") return cmd_train(argc, argv);
   if (mode == "features") return cmd_features(argc, argv);

@@ -29,3 +29,17 @@ def trainer_corpus():
     c = TRAINER
     return formats.synth_corpus(c["n_utts"], c["dims"][0], c["dims"][-1], seed=c["corpus_seed"],
                                 min_len=c["min_len"], max_len=c["max_len"])
+
+
+# BASELINE config 3 at full network size through the data-parallel protocol: 440 -> 2048x5 -> 4000, the
+# global bunch of 1024 frames split over 8 ranks (128 each: the reference's Platform semantics,
+# Platform.h:159-160, bunch / N per worker), GRADDIVFRM=T over the global bunch, two steps
+FULL = dict(dims=[440, 2048, 2048, 2048, 2048, 2048, 4000], init_seed=3, lr=1.0, bunch=1024, steps=2, world=8)
+
+
+def full_bunches():
+    """[(X [1024 x 440], labels)] per step -- the global bunches"""
+    rng = np.random.default_rng(17)
+    B, d, n = FULL["bunch"], FULL["dims"][0], FULL["dims"][-1]
+    return [(rng.standard_normal((B, d)).astype(np.float32), rng.integers(0, n, B).astype(np.int32))
+            for _ in range(FULL["steps"])]

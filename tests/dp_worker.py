@@ -64,6 +64,19 @@ def main():
         tr.train_corpus([corpus.feats[i] for i in idx], [corpus.labels[i] for i in idx])
         err, frames, correct = obj.stats()
         res.update(steps=tr.steps, empty_steps=tr.empty_steps, xent=err, frames=frames, correct=correct)
+    elif mode == "full":
+        c = dp_cases.FULL
+        net = Network.from_layers(formats.gen_mlp_init(c["dims"], seed=c["init_seed"]))
+        net.set_learn_rate(c["lr"])
+        net.set_grad_div_frm(True)
+        net.set_comm(comm)
+        obj = Objective()
+        b = c["bunch"] // world
+        for X, L in dp_cases.full_bunches():
+            net.train_bunch(obj, DeviceArray.from_numpy(X[rank * b:(rank + 1) * b]),
+                            DeviceArray.vector(L[rank * b:(rank + 1) * b]))
+        err, frames, correct = obj.stats()
+        res.update(xent=err, frames=frames, correct=correct)
     else:
         raise SystemExit(f"unknown mode {mode}")
     arrs = {}

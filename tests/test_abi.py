@@ -78,3 +78,53 @@ def test_utterance_shape_checks_before_the_abi():
         _utterance(np.zeros((5, 3)), np.zeros((5, 1)))
     f, l = _utterance(np.zeros((2, 3)), None)
     assert l is None
+
+
+def _fake(base, k):
+    """a 16-B aligned device-address stand-in (never dereferenced: the refusals come before any launch)"""
+    return ctypes.c_void_p(base + k * (1 << 28))
+
+
+def test_gather_ride_refuses_dependent_operands():
+    """tnet_affine_update_bias_gather / tnet_rbm_update_stats_gather run a gather beside an update in ONE
+    launch; any operand the gather writes that the update reads or writes, or that the update writes and the
+    gather reads, is a race the separate calls do not have: TNET_ERR_ARG before anything is launched
+    (ADVICE r3).  CPU only: fake 16-B aligned addresses, refused before the first HIP call."""
+    from tnet_amd._lib import MatrixDim
+    L = _lib.lib()
+    base = 1 << 44
+    rows, n_in, n_out = 256, 64, 128
+    X, E, W, C, P, b, cb = (_fake(base, k) for k in range(7))
+    y, x, lo, li, cf = (_fake(base, k) for k in range(7, 12))
+    dX, dE, dW = MatrixDim(rows, n_in, n_in), MatrixDim(rows, n_out, n_out), MatrixDim(n_in, n_out, n_out)
+    dy, dx = MatrixDim(64, 40, 40), MatrixDim(1000, 40, 40)
+    nil = [None, MatrixDim(0, 0, 0), None, MatrixDim(0, 0, 0), None, MatrixDim(0, 0, 0), None, 0, 0.0, 0.0, 0.0,
+           None, 0, None, None]
+
+    def upd(y_, x_, lo_, li_, cf_):
+        return L.tnet_affine_update_bias_gather(X, dX, E, dE, W, dW, C, n_out, -0.1, 0.5, 0.0, P, n_out, b, cb, *nil,
+                                                y_, x_, lo_, li_, cf_, dy, dx, None)
+    assert upd(y, x, lo, li, cf) != -1  # independent: not refused for overlap
+    for bad in (X, E, W, C, P, b, cb):  # the gather's rows written into an update operand
+        assert upd(bad, x, lo, li, cf) == -1
+    for bad in (E, P, b, x, cf):        # the gather's class ids written into an update operand / its own source
+        assert upd(y, x, bad, li, cf) == -1
+    for bad in (W, C, b, cb):           # the gather reads what the update writes
+        assert upd(y, bad, lo, li, cf) == -1
+        assert upd(y, x, lo, bad, cf) == -1
+        assert upd(y, x, lo, li, bad) == -1
+
+    V, H, vb, cvb, hb, chb, ms = (_fake(base, k) for k in range(12, 19))
+    B, nv, nh = 64, 40, 256
+    dV, dH, dWr = MatrixDim(2 * B, nv, nv), MatrixDim(2 * B, nh, nh), MatrixDim(nv, nh, nh)
+
+    def rbm(y_, x_, lo_, li_, cf_):
+        return L.tnet_rbm_update_stats_gather(V, dV, H, dH, W, dWr, C, nh, 0.1, 0.5, 0.0, B, vb, cvb, hb, chb, ms,
+                                              y_, x_, lo_, li_, cf_, dy, dx, None)
+    assert rbm(y, x, lo, li, cf) != -1
+    for bad in (V, H, W, C, vb, cvb, hb, chb, ms):
+        assert rbm(bad, x, lo, li, cf) == -1
+        assert rbm(y, x, bad, li, cf) == -1
+    for bad in (W, C, vb, hb, ms):
+        assert rbm(y, bad, lo, li, cf) == -1
+        assert rbm(y, x, lo, li, bad) == -1

@@ -168,3 +168,31 @@ def test_dp_rccl_reserved_cus_full_size(monkeypatch):
             _assert_update_close(b, ref.b[k], b0[k], 1e-4, f"layer {k} b")
         np.testing.assert_allclose(stats[0], ref.xent, rtol=1e-5)
     assert any(not np.array_equal(runs[0][0][k][0], runs[1][0][k][0]) for k in (1, 2))
+
+
+@pytest.mark.parametrize("shard", ["0", "1"])
+def test_dp_config3_full_size_eight_ranks(tmp_path, shard):
+    """BASELINE config 3's network at FULL size through the data-parallel exchange: 440 -> 2048x5 -> 4000,
+    8 ranks (processes on one GPU, host transport over gloo -- RCCL needs a GPU per rank), 128 frames
+    each of a global bunch of 1024 (Platform.h:159-160: bunch / N per worker), GRADDIVFRM=T over the
+    global bunch, two steps; shard "1": reduce-scatter + sharded apply + all-gather (TNET_DP_SHARD=1).
+    Every rank must hold bit-identical parameters, equal to the oracle's two steps on the global bunches
+    within tests/test_gpu_fullsize.py's bound (2 ulp(W) + 1e-4 of the largest update per layer); the
+    ranks' summed cross-entropy within 1e-5 of the oracle's."""
+    c = dp_cases.FULL
+    world = c["world"]
+    ranks = _run_ranks("full", tmp_path, world, shard)
+    for r in range(1, world):
+        for k in ranks[0][1]:
+            np.testing.assert_array_equal(ranks[0][1][k], ranks[r][1][k], err_msg=f"rank {r} {k}")
+    layers = formats.gen_mlp_init(c["dims"], seed=c["init_seed"])
+    ref = orc.MLP.from_layers(layers)
+    W0 = [w.astype(np.float64) for w in ref.W]
+    b0 = [b.astype(np.float64) for b in ref.b]
+    for X, L in dp_cases.full_bunches():
+        ref.step(X, L, c["lr"], graddivfrm=True)
+    for k in range(len(ref.W)):
+        _assert_update_close(ranks[0][1][f"W{k}"], ref.W[k], W0[k], 1e-4, f"layer {k} W")
+        _assert_update_close(ranks[0][1][f"b{k}"], ref.b[k], b0[k], 1e-4, f"layer {k} b")
+    assert sum(r[0]["frames"] for r in ranks) == c["bunch"] * c["steps"]
+    np.testing.assert_allclose(sum(r[0]["xent"] for r in ranks), ref.xent, rtol=1e-5)

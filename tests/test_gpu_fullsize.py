@@ -145,3 +145,73 @@ def test_rnn_1000_frame_utterances_full_size(S, monkeypatch):
         e = _rel_update_err(got, want, init.astype(np.float64))
         print(f"S={S} {what}: relative update error {e:.3e}")
         assert e <= 1e-4, (what, e)
+
+
+def _first_layer_operands(rows=1024, n_in=440, n_out=2048, seed=71):
+    """the metric's first layer at bunch 1024: X = standardised 440-dim frames, E = the backpropagated error
+    of a sigmoid layer (y(1-y) e with y ~ saturated sigmoids: most entries ~1e-4, a few ~1e-2)"""
+    rng = np.random.default_rng(seed)
+    X = rng.standard_normal((rows, n_in)).astype(np.float32)
+    y = 1.0 / (1.0 + np.exp(-4.0 * rng.standard_normal((rows, n_out))))
+    E = (y * (1.0 - y) * 0.05 * rng.standard_normal((rows, n_out))).astype(np.float32)
+    return X, E
+
+
+def _check_against_fp64(got, X, E, scale, what):
+    ref = scale * (X.astype(np.float64).T @ E.astype(np.float64))
+    mag = abs(scale) * (np.abs(X.astype(np.float64)).T @ np.abs(E.astype(np.float64)))
+    err = np.abs(got.astype(np.float64) - ref)
+    rel = np.linalg.norm(got.astype(np.float64) - ref) / np.linalg.norm(ref)
+    print(f"{what}: norm-relative error {rel:.2e}, worst err/|X|^T|E| {float((err / (mag + 1e-30)).max()):.2e}")
+    assert rel <= 1e-6, (what, rel)
+    assert np.all(err <= 1e-5 * mag + 1e-12), what
+
+
+def test_first_layer_gradient_direct():
+    """the full-size first-layer update is checked directly, not through W (whose 2-ulp
+    floor is most of a ~1e-5-relative update).  The data-parallel gradient GEMM (tnet_affine_grad) of
+    440 x 2048 over 1024 rows against the fp64 X^T E: elementwise |err| <= 1e-5 (|X|^T |E|), norm-relative
+    <= 1e-6 (cuBiasedLinearity.cc:55)."""
+    from tnet_amd._lib import lib
+    X, E = _first_layer_operands()
+    dX, dE = DeviceArray.from_numpy(X), DeviceArray.from_numpy(E)
+    dG = DeviceArray.from_numpy(np.full((X.shape[1], E.shape[1]), np.nan, np.float32))
+    assert lib().tnet_affine_grad(dX.ptr, dX.dim, dE.ptr, dE.dim, dG.ptr, dG.dim, lib().tnet_stream()) == 0
+    _check_against_fp64(dG.numpy(), X, E, 1.0, "tnet_affine_grad 440x2048")
+
+
+@pytest.mark.parametrize("gather", [False, True])
+def test_first_layer_fused_update_direct(gather):
+    """The training step's own first-layer kernels -- the fused SGD update with the bias update
+    (tnet_affine_update_bias) and the form that also carries the next bunch's gather (the bench's last
+    launch, tnet_affine_update_bias_gather) -- from W = 0, b = 0, so W after the step IS scale * X^T E and
+    is compared with the fp64 product at the same bounds as the gradient GEMM (no ulp(W) floor)."""
+    from tnet_amd._lib import MatrixDim, lib
+    X, E = _first_layer_operands(seed=72)
+    rows, n_in, n_out = X.shape[0], X.shape[1], E.shape[1]
+    scale = -1.0 / rows
+    P = np.stack([E[s * 32:(s + 1) * 32].astype(np.float64).sum(0) for s in range(rows // 32)]).astype(np.float32)
+    dX, dE, dP = DeviceArray.from_numpy(X), DeviceArray.from_numpy(E), DeviceArray.from_numpy(P)
+    dW = DeviceArray.from_numpy(np.zeros((n_in, n_out), np.float32))
+    db = DeviceArray.vector(np.zeros(n_out, np.float32))
+    args = [dX.ptr, dX.dim, dE.ptr, dE.dim, dW.ptr, dW.dim, None, 0, scale, 0.0, 0.0, dP.ptr, dP.stride, db.ptr, None]
+    S = lib().tnet_stream()
+    if gather:
+        cache = np.random.default_rng(9).standard_normal((4096, n_in)).astype(np.float32)
+        lab = np.arange(4096, dtype=np.int32) % 4000
+        perm = np.random.default_rng(10).permutation(4096).astype(np.int32)[:rows]
+        dC, dL, dPm = DeviceArray.from_numpy(cache), DeviceArray.vector(lab), DeviceArray.vector(perm)
+        dY = DeviceArray.from_numpy(np.zeros((rows, n_in), np.float32))
+        dLo = DeviceArray.vector(np.zeros(rows, np.int32))
+        nil = [None, MatrixDim(0, 0, 0), None, MatrixDim(0, 0, 0), None, MatrixDim(0, 0, 0), None, 0, 0.0, 0.0,
+               0.0, None, 0, None, None]
+        st = lib().tnet_affine_update_bias_gather(*args, *nil, dY.ptr, dC.ptr, dLo.ptr, dL.ptr, dPm.ptr, dY.dim,
+                                                  dC.dim, S)
+        assert st == 0, st  # the metric's first layer takes the carried gather (bench: gemm_upd+gather:440x2048)
+        np.testing.assert_array_equal(dY.numpy(), cache[perm])
+        np.testing.assert_array_equal(dLo.numpy().ravel(), lab[perm])
+    else:
+        assert lib().tnet_affine_update_bias(*args, S) == 0
+    _check_against_fp64(dW.numpy(), X, E, scale, "fused first-layer update" + (" + gather" if gather else ""))
+    gb = scale * P.astype(np.float64).sum(0)
+    np.testing.assert_allclose(db.numpy().ravel(), gb, rtol=1e-6, atol=1e-12)
