@@ -370,20 +370,177 @@ std::string MakeHtkFileName(const std::string& in, const char* outDir, const cha
 // ------------------------------------------------------------------------------------------- MLF
 
 namespace {
-// HTK mask match ('*' any run, '?' one character; ProcessMask's '%' captures match as '?')
-bool GlobMatch(const char* s, const char* p) {
-  if (*p == '\0') return *s == '\0';
-  if (*p == '*') {
-    for (const char* t = s;; t++) {
-      if (GlobMatch(t, p + 1)) return true;
-      if (*t == '\0') return false;
+// The STK wildcard matcher the reference's MLF lookup uses (KaldiLib/StkMatch.cc matche /
+// matche_after_star): '?' and '%' one character, '*' any run, [..] / [!..] / [^..] sets with ranges and
+// backslash escapes inside a set, a text that ends early matches only a trailing '*'.  Restated step for
+// step (the return codes steer matche_after_star's search); parity: tests/test_reader.py MLF cases.
+enum { kMatchValid = 1, kMatchEnd, kMatchAbort, kMatchRange, kMatchLiteral, kMatchPattern };
+int StkMatchAfterStar(const char* p, const char* t);
+int StkMatche(const char* p, const char* t) {
+  for (; *p; p++, t++) {
+    if (!*t) return (*p == '*' && *++p == '\0') ? kMatchValid : kMatchAbort;
+    switch (*p) {
+      case '?':
+      case '%':
+        break;
+      case '*':
+        return StkMatchAfterStar(p, t);
+      case '[': {
+        p++;
+        bool invert = false;
+        if (*p == '!' || *p == '^') {
+          invert = true;
+          p++;
+        }
+        if (*p == ']') return kMatchPattern;
+        bool member = false, loop = true;
+        while (loop) {
+          if (*p == ']') {
+            loop = false;
+            continue;
+          }
+          char lo, hi;
+          if (*p == '\\') lo = hi = *++p;
+          else lo = hi = *p;
+          if (!*p) return kMatchPattern;
+          if (*++p == '-') {
+            hi = *++p;
+            if (hi == '\0' || hi == ']') return kMatchPattern;
+            if (hi == '\\') {
+              hi = *++p;
+              if (!hi) return kMatchPattern;
+            }
+            p++;
+          }
+          if (lo < hi) {
+            if (*t >= lo && *t <= hi) member = true, loop = false;
+          } else if (*t >= hi && *t <= lo) {
+            member = true, loop = false;
+          }
+        }
+        if ((invert && member) || !(invert || member)) return kMatchRange;
+        if (member) {
+          while (*p != ']') {
+            if (!*p) return kMatchPattern;
+            if (*p == '\\') {
+              p++;
+              if (!*p) return kMatchPattern;
+            }
+            p++;
+          }
+        }
+        break;
+      }
+      default:
+        if (*p != *t) return kMatchLiteral;
     }
   }
-  if (*s == '\0') return false;
-  if (*p == '?' || *p == '%' || *p == *s) return GlobMatch(s + 1, p + 1);
-  return false;
+  return *t ? kMatchEnd : kMatchValid;
+}
+int StkMatchAfterStar(const char* p, const char* t) {
+  int match = 0;
+  while (*p == '?' || *p == '%' || *p == '*') {
+    if ((*p == '?' || *p == '%') && !*t++) return kMatchAbort;
+    p++;
+  }
+  if (!*p) return kMatchValid;
+  const char nextp = *p;
+  do {
+    if (nextp == *t || nextp == '[') match = StkMatche(p, t);
+    if (!*t++) match = kMatchAbort;
+  } while (match != kMatchValid && match != kMatchAbort && match != kMatchPattern);
+  return match;
+}
+// ProcessMask (StkMatch.cc:453-490) as LabelContainer::FindInList calls it: "*/" prepended to a pattern that
+// does not start with '*', "/" to a label that does not start with '/'
+bool MaskMatches(const std::string& label, const std::string& pattern) {
+  const std::string w = (pattern.empty() || pattern[0] != '*') ? "*/" + pattern : pattern;
+  const std::string t = (label.empty() || label[0] != '/') ? "/" + label : label;
+  return StkMatche(w.c_str(), t.c_str()) == kMatchValid;
+}
+// PATH_MAX on Linux: MlfStream.h's MAX_LABEL_DEPTH, the depth of a name without a leading '*'
+constexpr size_t kMaxLabelDepth = 4096;
+size_t DirDepth(const std::string& path) {
+  return (size_t)std::count(path.begin(), path.end(), '/') + (size_t)std::count(path.begin(), path.end(), '\\');
 }
 }  // namespace
+
+// LabelContainer::FindInHash (MlfStream.cc:97-197), the reference's position arithmetic kept as it is
+// (including find_last_of from prev - 1 when prev is 0, which wraps to the whole label)
+bool MlfLabels::FindInHash(const std::string& label, size_t* rec, size_t* limit) const {
+  bool found = false;
+  std::string str;
+  size_t current_depth = kMaxLabelDepth, prev = label.size() + 1;
+  auto lookup = [&](const std::string& key) {
+    auto it = mHash.find(key);
+    if (it == mHash.end()) return false;
+    *rec = it->second.rec;
+    *limit = it->second.limit;
+    return true;
+  };
+  for (auto ri = mDepths.rbegin(); !found && ri != mDepths.rend(); ++ri) {
+    if (*ri == kMaxLabelDepth) {
+      found = lookup(label);
+    } else if (current_depth == kMaxLabelDepth) {
+      if (*ri > 0) {
+        for (size_t i = 1; i <= *ri && prev != std::string::npos; i++) prev = label.find_last_of("/\\", prev - 1);
+      } else {
+        prev = 0;
+      }
+      if (prev != std::string::npos) {
+        str.assign(label, prev, label.size());
+        str = '*' + str;
+        found = lookup(str);
+        current_depth = *ri;
+      } else {
+        prev = label.size() + 1;
+      }
+    } else {
+      while (current_depth > *ri) {
+        if ((prev = label.find_first_of("/\\", prev + 1)) != std::string::npos) current_depth--;
+        else return false;
+      }
+      str.assign(label, prev, label.size());
+      str = '*' + str;
+      found = lookup(str);
+    }
+  }
+  return found;
+}
+
+// LabelContainer::FindInList (MlfStream.cc:201-239): the first of the first `limit` patterns (0: all) that
+// ProcessMask matches
+bool MlfLabels::FindInList(const std::string& label, size_t limit, size_t* rec) const {
+  const size_t n = limit ? std::min(limit, mList.size()) : mList.size();
+  for (size_t k = 0; k < n; k++)
+    if (MaskMatches(label, mList[k].first)) {
+      *rec = mList[k].second;
+      return true;
+    }
+  return false;
+}
+
+// LabelContainer::Find (MlfStream.cc:243-262): a hash hit can be overridden by a list pattern defined before it
+const MlfLabels::Record* MlfLabels::Find(const std::string& label) const {
+  size_t rec = 0, limit = 0;
+  if (FindInHash(label, &rec, &limit)) {
+    (void)FindInList(label, limit, &rec);
+    return &mRecords[rec];
+  }
+  return FindInList(label, 0, &rec) ? &mRecords[rec] : nullptr;
+}
+
+// LabelContainer::Insert (MlfStream.cc:43-93): a pattern with no wildcard after its first character is
+// hashed -- unless an earlier definition (hashed or listed) already matches it -- else listed; every
+// '*'-led pattern records its directory depth for FindInHash's walk
+void MlfLabels::Insert(const std::string& pattern, size_t rec) {
+  mDepths.insert(!pattern.empty() && pattern[0] == '*' ? DirDepth(pattern) : kMaxLabelDepth);
+  if (pattern.find_first_of("*?%", 1) == std::string::npos) {
+    if (!Find(pattern)) mHash[pattern] = Hashed{rec, mList.size()};
+  } else {
+    mList.emplace_back(pattern, rec);
+  }
+}
 
 MlfLabels::MlfLabels(const std::string& mlf, const std::string& labelMap, const char* labelDir, const char* labelExt)
     : mMlf(mlf) {
@@ -416,18 +573,7 @@ MlfLabels::MlfLabels(const std::string& mlf, const std::string& labelMap, const 
         const size_t idx = mRecords.size();
         mRecords.emplace_back();
         cur = &mRecords.back();
-        // LabelContainer::Insert (MlfStream.cc:60-93): "*/a/b" patterns are hashed by depth, plain
-        // names exactly, anything else goes to the sequential list; the first definition wins
-        const bool star = pat.size() > 1 && pat[0] == '*' && (pat[1] == '/' || pat[1] == '\\');
-        const bool wild_rest = pat.find_first_of("*?%", star ? 1 : 0) != std::string::npos;
-        if (!wild_rest && star) {
-          int depth = (int)std::count(pat.begin(), pat.end(), '/') + (int)std::count(pat.begin(), pat.end(), '\\');
-          mByDepth[depth].emplace(pat, idx);
-        } else if (!wild_rest && pat.find('*') == std::string::npos) {
-          mExact.emplace(pat, idx);
-        } else {
-          mGlob.emplace_back(pat, idx);
-        }
+        Insert(pat, idx);
       }
       continue;
     }
@@ -456,28 +602,6 @@ MlfLabels::MlfLabels(const std::string& mlf, const std::string& labelMap, const 
     g.state = it == mStates.end() ? -1 : it->second;
     cur->segs.push_back(g);
   }
-}
-
-const MlfLabels::Record* MlfLabels::Find(const std::string& label) const {
-  auto e = mExact.find(label);
-  if (e != mExact.end()) return &mRecords[e->second];
-  for (auto& d : mByDepth) {  // deepest first (FindInHash walks the depths backwards)
-    size_t pos = label.size();
-    int k = 0;
-    while (k < d.first) {
-      if (pos == 0) break;
-      size_t p = label.find_last_of("/\\", pos - 1);
-      if (p == std::string::npos) break;
-      pos = p;
-      k++;
-    }
-    if (k < d.first) continue;
-    auto it = d.second.find("*" + label.substr(pos));
-    if (it != d.second.end()) return &mRecords[it->second];
-  }
-  for (auto& g : mGlob)
-    if (GlobMatch(label.c_str(), g.first.c_str())) return &mRecords[g.second];
-  return nullptr;
 }
 
 size_t MlfLabels::ClassIds(const std::string& featureLogical, size_t nFrames, size_t sourceRate, int* out) const {

@@ -22,6 +22,7 @@
 #include <condition_variable>
 #include <cstdint>
 #include <map>
+#include <set>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -116,7 +117,13 @@ class MlfLabels {
     std::vector<Segment> segs;
     std::string error;  // a line GenDesiredMatrix could not parse (reported when the record is used)
   };
+  // LabelContainer (MlfStream.cc:43-265): Find is FindInHash over the recorded depths (deepest first, the
+  // reference's position arithmetic included), then -- after a hash hit -- the list patterns defined before
+  // that record (all of them when the list was empty at its insertion), else the whole list in file order
   const Record* Find(const std::string& label) const;
+  bool FindInHash(const std::string& label, size_t* rec, size_t* limit) const;
+  bool FindInList(const std::string& label, size_t limit, size_t* rec) const;
+  void Insert(const std::string& pattern, size_t rec);
 
   std::string mMlf;
   const char* mDir;
@@ -124,9 +131,13 @@ class MlfLabels {
   std::string mDirS, mExtS;
   std::unordered_map<std::string, int> mStates;
   std::vector<std::string> mTags;
-  std::unordered_map<std::string, size_t> mExact;   // patterns without wildcards
-  std::map<int, std::unordered_map<std::string, size_t>, std::greater<int>> mByDepth;  // "*/a/b": depth 2
-  std::vector<std::pair<std::string, size_t>> mGlob;  // any other pattern, in file order
+  struct Hashed {
+    size_t rec;    // index into mRecords
+    size_t limit;  // list patterns defined before this record (0: the list was empty -- search it all)
+  };
+  std::unordered_map<std::string, Hashed> mHash;      // names and patterns without wildcards after position 0
+  std::set<size_t> mDepths;                           // DirDepth of every '*' pattern, kMaxLabelDepth for names
+  std::vector<std::pair<std::string, size_t>> mList;  // patterns with wildcards, in file order
   std::vector<Record> mRecords;
 };
 

@@ -12,17 +12,86 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 namespace tnetk {
 
+// Wave-wide butterfly reductions, partner lane i ^ o for o = 32, 16, 8, 4, 2, 1 (every lane ends with the
+// result).  The exchanges are VALU cross-lane moves instead of ds_bpermute (an LDS round trip and an lgkmcnt
+// wait per step): o = 32 / 16 by v_permlane32_swap / v_permlane16_swap (gfx950), o = 8 by the DPP row
+// rotation by 8 (= xor 8 inside a 16-lane row), o = 4 by the DPP row rotation by 4 -- lane j gets j + 4
+// mod 16, which is j ^ 4 or (j ^ 4) ^ 8, and after the o = 8 step lanes j and j ^ 8 hold the same value --
+// and o = 2 / 1 by DPP quad permutations.  Each step combines a lane with exactly the value the
+// __shfl_xor butterfly would give it, and fp addition is commutative, so the results are bit-identical to
+// the shfl form (tools/reduce_dpp_check.hip checks all four reductions bit for bit on MI355X).
+__device__ __forceinline__ unsigned xlane32(unsigned x) {  // lane i ^ 32's x
+  const auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+  return (__lane_id() & 32) ? r[0] : r[1];
+}
+__device__ __forceinline__ unsigned xlane16(unsigned x) {  // lane i ^ 16's x
+  const auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false);
+  return (__lane_id() & 16) ? r[0] : r[1];
+}
+template <int CTRL>
+__device__ __forceinline__ unsigned xdpp(unsigned x) {
+  return (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, 0xF, 0xF, false);
+}
+constexpr int kDppRor8 = 0x128, kDppRor4 = 0x124, kDppXor2 = 0x4E, kDppXor1 = 0xB1;
+// the partner's 32-bit word at butterfly step S (0: xor 32 .. 5: xor 1; step 3 relies on step 2's symmetry)
+template <int S>
+__device__ __forceinline__ unsigned xstep(unsigned x) {
+  if constexpr (S == 0) return xlane32(x);
+  else if constexpr (S == 1) return xlane16(x);
+  else if constexpr (S == 2) return xdpp<kDppRor8>(x);
+  else if constexpr (S == 3) return xdpp<kDppRor4>(x);
+  else if constexpr (S == 4) return xdpp<kDppXor2>(x);
+  else return xdpp<kDppXor1>(x);
+}
+template <int S>
+__device__ __forceinline__ float xstep_f(float v) {
+  return __uint_as_float(xstep<S>(__float_as_uint(v)));
+}
+template <int S>
+__device__ __forceinline__ double xstep_d(double v) {
+  const unsigned long long u = __double_as_longlong(v);
+  const unsigned lo = xstep<S>((unsigned)u), hi = xstep<S>((unsigned)(u >> 32));
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
 __device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  v += xstep_f<0>(v);
+  v += xstep_f<1>(v);
+  v += xstep_f<2>(v);
+  v += xstep_f<3>(v);
+  v += xstep_f<4>(v);
+  v += xstep_f<5>(v);
   return v;
 }
 __device__ __forceinline__ double wave_sum_d(double v) {
+  v += xstep_d<0>(v);
+  v += xstep_d<1>(v);
+  v += xstep_d<2>(v);
+  v += xstep_d<3>(v);
+  v += xstep_d<4>(v);
+  v += xstep_d<5>(v);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+  v = fmaxf(v, xstep_f<0>(v));
+  v = fmaxf(v, xstep_f<1>(v));
+  v = fmaxf(v, xstep_f<2>(v));
+  v = fmaxf(v, xstep_f<3>(v));
+  v = fmaxf(v, xstep_f<4>(v));
+  v = fmaxf(v, xstep_f<5>(v));
+  return v;
+}
+// the ds_bpermute butterflies these replace (tools/reduce_dpp_check.hip compares the two)
+__device__ __forceinline__ float wave_sum_shfl(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
 }
-__device__ __forceinline__ float wave_max(float v) {
+__device__ __forceinline__ double wave_sum_d_shfl(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max_shfl(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
   return v;
@@ -70,7 +139,21 @@ __device__ __forceinline__ ArgMax argmax_merge(ArgMax a, ArgMax b) {
   if (b.v > a.v || (b.v == a.v && b.i < a.i)) return b;
   return a;
 }
+template <int S>
+__device__ __forceinline__ ArgMax xstep_am(ArgMax a) {
+  return ArgMax{xstep_f<S>(a.v), (int)xstep<S>((unsigned)a.i)};
+}
+// argmax_merge is symmetric (the larger value, the smaller index on ties), so the butterfly steps above apply
 __device__ __forceinline__ ArgMax wave_argmax(ArgMax a) {
+  a = argmax_merge(a, xstep_am<0>(a));
+  a = argmax_merge(a, xstep_am<1>(a));
+  a = argmax_merge(a, xstep_am<2>(a));
+  a = argmax_merge(a, xstep_am<3>(a));
+  a = argmax_merge(a, xstep_am<4>(a));
+  a = argmax_merge(a, xstep_am<5>(a));
+  return a;
+}
+__device__ __forceinline__ ArgMax wave_argmax_shfl(ArgMax a) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
     ArgMax b{__shfl_xor(a.v, o, 64), __shfl_xor(a.i, o, 64)};

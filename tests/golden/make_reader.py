@@ -101,6 +101,38 @@ def synthetic(rng):
     return files, "\n".join(mlf) + "\n", states
 
 
+def lookup_mlf():
+    """LabelContainer's lookup order (MlfStream.cc:43-265): every record labels all 60 frames of
+    long.fea with its own state, so the class ids show which record a label resolved to.
+      a: a later exact pattern that an earlier list pattern already matches is never hashed (the list wins)
+      b: a hashed pattern resolves before a list pattern defined AFTER it
+      c: a hash hit is overridden by a list pattern defined BEFORE it that matches the label (not the pattern)
+      d: '*d1.lab' (no '/') is hashed at depth 0: it matches the label 'd1.lab' only (x/d1 has no record)
+      e: a plain name defined after a list pattern that matches it is never hashed
+      f: a label with a leading '/' and fewer '/' than a recorded depth: FindInHash's backward search wraps
+         (find_last_of from prev - 1 at prev 0) and lands on the depth-1 key before the depth-2 one
+      g/h: [..] and [!..] sets in list patterns"""
+    mlf = ["#!MLF!#"]
+
+    def rec(pattern, state):
+        mlf.extend([f'"{pattern}"', f"0 {60 * 100000} s{state}", "."])
+    rec("*/a?.lab", 1)
+    rec("*/a1.lab", 2)
+    rec("*/b1.lab", 3)
+    rec("*/b?.lab", 4)
+    rec("x/c?.lab", 5)
+    rec("*/c1.lab", 6)
+    rec("*d1.lab", 7)
+    rec("*/e?.lab", 8)
+    rec("x/e1.lab", 9)
+    rec("*/p/q/r.lab", 0)
+    rec("*/y/f1.lab", 2)
+    rec("*/f1.lab", 3)
+    rec("*/g[0-3]?.lab", 4)
+    rec("*/h[!0-3]?.lab", 5)
+    return "\n".join(mlf) + "\n"
+
+
 CONFIGS = {
     # name: (scp lines, swap, sext, eext, TARGETKIND, mlf?, label_dir)
     "plain": (["d/fb.fea", "d/fbc.fea", "d/long.fea"], 1, 3, 2, "ANON", True, None),
@@ -120,6 +152,11 @@ CONFIGS = {
     "err_gap": (["x/gap=d/long.fea"], 1, 0, 0, "ANON", True, None),
     "err_no_record": (["fb.fea"], 1, 0, 0, "ANON", True, None),
     "err_convert": (["d/fb.fea"], 1, 0, 0, "MFCC", True, None),
+    # LabelContainer lookup order (lookup_mlf)
+    "mlf_lookup": (["x/a1=d/long.fea", "x/b1=d/long.fea", "x/c1=d/long.fea", "d1=d/long.fea", "x/e1=d/long.fea",
+                    "/y/f1=d/long.fea", "x/g2z=d/long.fea", "x/h7z=d/long.fea"], 1, 0, 0, "ANON", "lookup.mlf", None),
+    "err_mlf_depth0": (["x/d1=d/long.fea"], 1, 0, 0, "ANON", "lookup.mlf", None),
+    "err_mlf_set": (["x/h2z=d/long.fea"], 1, 0, 0, "ANON", "lookup.mlf", None),
 }
 
 
@@ -158,18 +195,20 @@ def main():
         arrays[f"file:{n}"] = np.frombuffer(b, np.uint8)
     arrays["mlf"] = np.frombuffer(mlf.encode(), np.uint8)
     arrays["states"] = np.frombuffer(states.encode(), np.uint8)
+    arrays["mlf:lookup.mlf"] = np.frombuffer(lookup_mlf().encode(), np.uint8)
     with tempfile.TemporaryDirectory() as td:
         os.makedirs(os.path.join(td, "d"))
         for n, b in files.items():
             open(os.path.join(td, "d", n), "wb").write(b)
         open(os.path.join(td, "fb.fea"), "wb").write(files["fb.fea"])
         open(os.path.join(td, "test.mlf"), "w").write(mlf)
+        open(os.path.join(td, "lookup.mlf"), "w").write(lookup_mlf())
         open(os.path.join(td, "states.txt"), "w").write(states)
         for name, (lines, swap, sext, eext, tk, use_mlf, ldir) in CONFIGS.items():
             scp = os.path.join(td, f"{name}.scp")
             open(scp, "w").write("\n".join(lines) + "\n")
-            res = run_harness(td, scp, swap, sext, eext, tk, "test.mlf" if use_mlf else None, ldir,
-                              os.path.join(td, "out_" + name))
+            mlf_name = use_mlf if isinstance(use_mlf, str) else ("test.mlf" if use_mlf else None)
+            res = run_harness(td, scp, swap, sext, eext, tk, mlf_name, ldir, os.path.join(td, "out_" + name))
             cm = {"scp": lines, "swap": swap, "start_ext": sext, "end_ext": eext, "target_kind": tk,
                   "mlf": use_mlf, "label_dir": ldir, "records": []}
             for k, r in enumerate(res):

@@ -37,6 +37,9 @@ def workdir(tmp_path_factory):
     (td / "fb.fea").write_bytes(bytes(_G["file:fb.fea"]))
     (td / "test.mlf").write_bytes(bytes(_G["mlf"]))
     (td / "states.txt").write_bytes(bytes(_G["states"]))
+    for k in _G.files:  # per-config MLFs (make_reader.py lookup_mlf: LabelContainer's lookup order)
+        if k.startswith("mlf:"):
+            (td / k[4:]).write_bytes(bytes(_G[k]))
     return td
 
 
@@ -60,7 +63,8 @@ def _reader(td, name, threads=3, depth=2):
     cwd = os.getcwd()
     os.chdir(td)
     try:
-        return FeatureReader(str(scp), mlf="test.mlf" if c["mlf"] else None, label_map="states.txt",
+        mlf = c["mlf"] if isinstance(c["mlf"], str) else ("test.mlf" if c["mlf"] else None)
+        return FeatureReader(str(scp), mlf=mlf, label_map="states.txt",
                              label_dir=c["label_dir"], start_ext=c["start_ext"], end_ext=c["end_ext"],
                              swap=bool(c["swap"]), target_kind=kind, deriv_order=order, threads=threads, depth=depth)
     finally:

@@ -95,8 +95,8 @@ def worker(a):
         train = [utterance(i, T, 0) for i in mine]
         held = [utterance(i, T, 1) for i in range(a.cv_utts)] if rank == 0 else []
     from tnet_amd import newbob
-    net = Network.from_layers(formats.gen_mlp_init(DIMS, seed=SEED))
-    lr = a.lr * (world if a.scale == "linear" else world ** 0.5)
+    net = Network.from_layers(formats.gen_mlp_init(DIMS, seed=SEED + 101 * a.seed))
+    lr = a.lr * {"linear": world, "sqrt": world ** 0.5, "none": 1.0}[a.scale]
     net.set_learn_rate(lr)
     net.set_grad_div_frm(True)
     nb = newbob.Newbob(repr(lr), a.bunch, max_iter=a.epochs, end_halving_inc=a.end_halving_inc,
@@ -126,7 +126,7 @@ def worker(a):
         best = [(W.copy(), b.copy()) for W, b in net.linear_params()]
     for ep in range(a.epochs):
         obj = Objective()
-        tr = Trainer(net, obj, bunchsize=a.bunch, cachesize=a.cache, seed=1 + 1000 * ep + rank)
+        tr = Trainer(net, obj, bunchsize=a.bunch, cachesize=a.cache, seed=1 + 1000 * ep + rank + 7919 * a.seed)
         if transform is not None:
             tr.set_transform(transform, 25, 25)
         if comm is not None:
@@ -170,7 +170,7 @@ def worker(a):
         ce, cf, cc = bcast_cv()
         log.append({"final_best": True, "cv_xent_per_frame": ce / cf, "cv_acc": 100.0 * cc / cf})
     if rank == 0:
-        print("RESULT " + json.dumps({"world": world, "corpus": a.corpus, "lr": lr, "lr_scaling": a.scale,
+        print("RESULT " + json.dumps({"world": world, "corpus": a.corpus, "seed": a.seed, "lr": lr, "lr_scaling": a.scale,
                                       "newbob": a.newbob,
                                       "warmup": a.warmup, "end_halving_inc": a.end_halving_inc,
                                       "start_halving_inc": a.start_halving_inc,
@@ -198,7 +198,9 @@ def main():
     ap.add_argument("--bunch", type=int, default=1024)
     ap.add_argument("--cache", type=int, default=16384)
     ap.add_argument("--lr", type=float, default=1.0)
-    ap.add_argument("--scale", default="linear", choices=["linear", "sqrt"], help="lr_N = lr_1 N or lr_1 sqrt(N)")
+    ap.add_argument("--scale", default="linear", choices=["linear", "sqrt", "none"],
+                    help="lr_N = lr_1 N, lr_1 sqrt(N), or lr_1 (strong scaling: the global bunch stays the N=1 one)")
+    ap.add_argument("--seed", type=int, default=0, help="run seed: the initial network and every cache shuffle")
     ap.add_argument("--newbob", action="store_true")
     ap.add_argument("--end-halving-inc", type=float, default=0.1)
     ap.add_argument("--start-halving-inc", type=float, default=0.5)
@@ -219,7 +221,7 @@ def main():
                 str(a.utts), "--cv-utts", str(a.cv_utts), "--bunch", str(a.bunch), "--cache", str(a.cache), "--lr",
                 str(a.lr), "--scale", a.scale, "--end-halving-inc", str(a.end_halving_inc),
                 "--start-halving-inc", str(a.start_halving_inc), "--warmup", str(a.warmup),
-                "--progress", a.progress, "--corpus", a.corpus]
+                "--progress", a.progress, "--corpus", a.corpus, "--seed", str(a.seed)]
         if a.newbob:
             args.append("--newbob")
         procs = [subprocess.Popen(args, env=dict(env, RANK=str(r)), stdout=subprocess.PIPE, stderr=subprocess.PIPE,
