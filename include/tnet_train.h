@@ -139,6 +139,15 @@ typedef struct TnetFeatureReader TnetFeatureReader;
 TnetFeatureReader* tnet_reader_create(const char* scp, int swap, int start_ext, int end_ext, int target_kind,
                                       int deriv_order, const int* deriv_win, const char* mlf, const char* label_map,
                                       const char* label_dir, const char* label_ext, int threads, int depth);
+/* the same with cepstral mean / variance normalisation (Features.cc:1352-1410, the TNetCu keys CMEANDIR,
+ * CMEANMASK, VARSCALEDIR, VARSCALEMASK, VARSCALEFN; UserInterface.cc:385-410): a NULL mask (file) turns that
+ * step off; the mean / variance file of an utterance is <dir>/ + "/" + the characters the mask's '%'s
+ * capture from its logical name */
+TnetFeatureReader* tnet_reader_create_norm(const char* scp, int swap, int start_ext, int end_ext, int target_kind,
+                                           int deriv_order, const int* deriv_win, const char* mlf,
+                                           const char* label_map, const char* label_dir, const char* label_ext,
+                                           const char* cmn_dir, const char* cmn_mask, const char* cvn_dir,
+                                           const char* cvn_mask, const char* cvg_file, int threads, int depth);
 int tnet_reader_free(TnetFeatureReader* r);
 long tnet_reader_size(TnetFeatureReader* r);  /* records in the script */
 /* next utterance in script order: 1 = delivered, 0 = end of list, < 0 = this record's error (the

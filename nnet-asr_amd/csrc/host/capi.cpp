@@ -411,6 +411,14 @@ int tnet_trainer_trace(TnetTrainer* t, int trace) {
 TnetFeatureReader* tnet_reader_create(const char* scp, int swap, int start_ext, int end_ext, int target_kind,
                                       int deriv_order, const int* deriv_win, const char* mlf, const char* label_map,
                                       const char* label_dir, const char* label_ext, int threads, int depth) {
+  return tnet_reader_create_norm(scp, swap, start_ext, end_ext, target_kind, deriv_order, deriv_win, mlf, label_map,
+                                 label_dir, label_ext, nullptr, nullptr, nullptr, nullptr, nullptr, threads, depth);
+}
+TnetFeatureReader* tnet_reader_create_norm(const char* scp, int swap, int start_ext, int end_ext, int target_kind,
+                                           int deriv_order, const int* deriv_win, const char* mlf,
+                                           const char* label_map, const char* label_dir, const char* label_ext,
+                                           const char* cmn_dir, const char* cmn_mask, const char* cvn_dir,
+                                           const char* cvn_mask, const char* cvg_file, int threads, int depth) {
   try {
     if (!scp) Error("tnet_reader_create: no script file");
     if (start_ext < 0 || end_ext < 0) Error("tnet_reader_create: negative frame extension");
@@ -423,6 +431,14 @@ TnetFeatureReader* tnet_reader_create(const char* scp, int swap, int start_ext, 
     cfg.derivOrder = deriv_order;
     if (deriv_win)
       for (int i = 0; i < deriv_order; i++) cfg.derivWin.push_back(deriv_win[i]);
+    cfg.cmn = cmn_mask != nullptr;
+    cfg.cvn = cvn_mask != nullptr;
+    cfg.cvg = cvg_file != nullptr;
+    if (cmn_dir) cfg.cmnDir = cmn_dir;
+    if (cmn_mask) cfg.cmnMask = cmn_mask;
+    if (cvn_dir) cfg.cvnDir = cvn_dir;
+    if (cvn_mask) cfg.cvnMask = cvn_mask;
+    if (cvg_file) cfg.cvgFile = cvg_file;
     std::shared_ptr<const tnetio::MlfLabels> labels;
     if (mlf) labels = std::make_shared<tnetio::MlfLabels>(mlf, label_map, label_dir, label_ext);
     std::unique_ptr<TnetFeatureReader> h(new TnetFeatureReader);

@@ -5,6 +5,8 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <cctype>
+#include <cmath>
 #include <cstdio>
 #include <cstring>
 #include <fstream>
@@ -107,6 +109,10 @@ HtkHeader ReadHtkHeader(const std::string& physical, bool swap, const std::strin
   if (pread(f.fd, hb, 12, 0) != 12) Fail("Invalid HTK header in feature file: '" + name + "'");
   return DecodeHeader(hb, swap);
 }
+
+// CMEANDIR / VARSCALEDIR / VARSCALEFN normalisation of a read matrix (Features.cc:1352-1410; defined below)
+void ApplyCepsNorm(const FeatureConfig& cfg, const std::string& logical, int targetKind, int derivOrder, int coefs,
+                   int trg_N, int trg_vec, int tot, float* M);
 
 void ReadHtkFeatures(const FileRecord& rec, const FeatureConfig& cfg, int& targetKind, int& derivOrder,
                      Utterance& out) {
@@ -287,7 +293,7 @@ void ReadHtkFeatures(const FileRecord& rec, const FeatureConfig& cfg, int& targe
     memcpy(&out.feats[(size_t)i * trg_vec], &out.feats[(size_t)(tot - ext_right - 1) * trg_vec], ext_w * 4);
 
   float* M = out.feats.data();
-  if (!(kParmZ & h.sampleKind) && (kParmZ & targetKind)) {  // sentence mean (Features.cc:1279-1300)
+  if (!cfg.cmn && !(kParmZ & h.sampleKind) && (kParmZ & targetKind)) {  // sentence mean (Features.cc:1279-1300)
     if (trg_N) Fail("Cannot convert " + ParmKindStr(h.sampleKind) + " to " + ParmKindStr((unsigned)targetKind) +
                     ": sentence mean normalisation with suppressed energy is not supported");
     for (int j = 0; j < coefs; j++) {
@@ -315,6 +321,8 @@ void ReadHtkFeatures(const FileRecord& rec, const FeatureConfig& cfg, int& targe
         M[(size_t)i * trg_vec + (size_t)src_deriv * coefs + j + coefs] = d / norm;
       }
   }
+
+  if (cfg.cmn || cfg.cvn || cfg.cvg) ApplyCepsNorm(cfg, rec.logical, targetKind, derivOrder, coefs, trg_N, trg_vec, tot, M);
 
   // CheckData's scan (the reference driver's, Matrix.h:238-252), done here on the reading thread
   out.bad_row = out.bad_col = -1;
@@ -375,16 +383,19 @@ namespace {
 // backslash escapes inside a set, a text that ends early matches only a trailing '*'.  Restated step for
 // step (the return codes steer matche_after_star's search); parity: tests/test_reader.py MLF cases.
 enum { kMatchValid = 1, kMatchEnd, kMatchAbort, kMatchRange, kMatchLiteral, kMatchPattern };
-int StkMatchAfterStar(const char* p, const char* t);
-int StkMatche(const char* p, const char* t) {
+int StkMatchAfterStar(const char* p, const char* t, char* s);
+int StkMatche(const char* p, const char* t, char* s) {
   for (; *p; p++, t++) {
     if (!*t) return (*p == '*' && *++p == '\0') ? kMatchValid : kMatchAbort;
     switch (*p) {
       case '?':
-      case '%':
+        break;
+      case '%':  // one character, captured
+        *s++ = *t;
+        *s = '\0';
         break;
       case '*':
-        return StkMatchAfterStar(p, t);
+        return StkMatchAfterStar(p, t, s);
       case '[': {
         p++;
         bool invert = false;
@@ -437,27 +448,148 @@ int StkMatche(const char* p, const char* t) {
   }
   return *t ? kMatchEnd : kMatchValid;
 }
-int StkMatchAfterStar(const char* p, const char* t) {
+int StkMatchAfterStar(const char* p, const char* t, char* s) {
   int match = 0;
   while (*p == '?' || *p == '%' || *p == '*') {
-    if ((*p == '?' || *p == '%') && !*t++) return kMatchAbort;
+    if (*p == '?' && !*t++) return kMatchAbort;
+    if (*p == '%') {
+      *s++ = *t;
+      *s = '\0';
+      if (!*t++) return kMatchAbort;
+    }
     p++;
   }
   if (!*p) return kMatchValid;
   const char nextp = *p;
   do {
-    if (nextp == *t || nextp == '[') match = StkMatche(p, t);
+    if (nextp == *t || nextp == '[') match = StkMatche(p, t, s);
     if (!*t++) match = kMatchAbort;
   } while (match != kMatchValid && match != kMatchAbort && match != kMatchPattern);
   return match;
 }
 // ProcessMask (StkMatch.cc:453-490) as LabelContainer::FindInList calls it: "*/" prepended to a pattern that
 // does not start with '*', "/" to a label that does not start with '/'
-bool MaskMatches(const std::string& label, const std::string& pattern) {
+// (with the characters the '%'s capture: the CMN / CVN file names, Features.cc:1359-1392)
+bool ProcessMask(const std::string& label, const std::string& pattern, std::string* captured) {
+  std::vector<char> sub((size_t)std::count(pattern.begin(), pattern.end(), '%') + 2, '\0');
   const std::string w = (pattern.empty() || pattern[0] != '*') ? "*/" + pattern : pattern;
   const std::string t = (label.empty() || label[0] != '/') ? "/" + label : label;
-  return StkMatche(w.c_str(), t.c_str()) == kMatchValid;
+  const bool ok = StkMatche(w.c_str(), t.c_str(), sub.data()) == kMatchValid;
+  if (captured) *captured = ok ? std::string(sub.data()) : std::string();
+  return ok;
 }
+bool MaskMatches(const std::string& label, const std::string& pattern) { return ProcessMask(label, pattern, nullptr); }
+
+// FeatureRepository::ReadParmKind(str, false) (Features.cc:1438-1472), its prefix match of the base name included
+int ReadParmKindRef(const char* str) {
+  static const char* names[13] = {"WAVEFORM", "LPC", "LPREFC", "LPCEPSTRA", "LPDELCEP", "IREFC", "MFCC",
+                                  "FBANK", "MELSPEC", "USER", "DISCRETE", "PLP", "ANON"};
+  int kind = 0;
+  int slen = (int)strlen(str);
+  for (; slen >= 2 && str[slen - 2] == '_'; slen -= 2) {
+    const char q = str[slen - 1];
+    kind |= q == 'E' ? kParmE : q == 'N' ? kParmN : q == 'D' ? kParmD : q == 'A' ? kParmA : q == 'C' ? kParmC
+          : q == 'Z' ? kParmZ : q == 'K' ? 010000 : q == '0' ? kParm0 : q == 'V' ? 040000 : q == 'T' ? kParmT : -1;
+    if (kind == -1) return -1;
+  }
+  for (int i = 0; i < 13; i++)
+    if (!strncmp(str, names[i], (size_t)slen)) return kind | i;
+  return -1;
+}
+
+enum CepsNormType { kCnfMean, kCnfVariance, kCnfVarScale };
+
+// FeatureRepository::ReadCepsNormFile (Features.cc:96-178), the same stdio parse and error texts: a header
+// "<CEPSNORM> <kind>" (not for VARSCALE), "<MEAN|VARIANCE|VARSCALE> n" with n == coefs, n numbers, end of file;
+// VARIANCE values become 1 / sqrt(v), VARSCALE values sqrt(v)
+std::vector<float> ReadCepsNormFile(const std::string& name, int sampleKind, CepsNormType type, int coefs) {
+  const char* typeStr = type == kCnfMean ? "MEAN" : type == kCnfVariance ? "VARIANCE" : "VARSCALE";
+  const char* typeStr2 = type == kCnfMean ? "CMN" : type == kCnfVariance ? "CVN" : "VarScale";
+  FILE* fp = fopen(name.c_str(), "r");
+  if (!fp) Fail(std::string("Cannot open ") + typeStr2 + " pFileName: '" + name + "'");
+  struct Closer {
+    FILE* f;
+    ~Closer() { fclose(f); }
+  } closer{fp};
+  char s1[80] = {0}, s2[80] = {0};
+  int n = 0;
+  auto up = [](char* c) {
+    for (char* q = c; *q; q++) *q = (char)toupper((unsigned char)*q);
+    return c;
+  };
+  if ((type != kCnfVarScale && (fscanf(fp, " <%64[^>]> <%64[^>]>", s1, s2) != 2 || strcmp(up(s1), "CEPSNORM") ||
+                                ReadParmKindRef(s2) != sampleKind)) ||
+      fscanf(fp, " <%64[^>]> %d", s1, &n) != 2 || strcmp(up(s1), typeStr) || n != coefs) {
+    const std::string k = ParmKindStr((unsigned)sampleKind);
+    Fail(std::string("") + (type == kCnfVarScale ? "" : "<CEPSNORM> <") + (type == kCnfVarScale ? "" : k) +
+         (type == kCnfVarScale ? "" : ">") + " <" + typeStr + " ... expected in " + typeStr2 + " file " + name);
+  }
+  std::vector<float> v((size_t)coefs);
+  for (int i = 0; i < coefs; i++) {
+    if (fscanf(fp, " %g", &v[(size_t)i]) != 1) {
+      if (fscanf(fp, "%64s", s2) == 1)
+        Fail(std::string("Decimal number expected but '") + s2 + "' found in " + typeStr2 + " file " + name);
+      else if (feof(fp))
+        Fail(std::string("Unexpected end of ") + typeStr2 + " file " + name);
+      else
+        Fail(std::string("Cannot read ") + typeStr2 + " file " + name);
+    }
+    // double arithmetic: KaldiLib calls the C library's sqrt(double) (measured bit-exact against the reference)
+    if (type == kCnfVariance) v[(size_t)i] = (float)(1 / sqrt((double)v[(size_t)i]));
+    else if (type == kCnfVarScale) v[(size_t)i] = (float)sqrt((double)v[(size_t)i]);
+  }
+  if (fscanf(fp, "%64s", s2) == 1)
+    Fail(std::string("End of file expected but '") + s2 + "' found in " + typeStr2 + " file " + name);
+  return v;
+}
+}  // namespace
+
+void ApplyCepsNorm(const FeatureConfig& cfg, const std::string& logical, int targetKind, int derivOrder, int coefs,
+                   int trg_N, int trg_vec, int tot, float* M) {
+  // the parameter kind the files are checked against: mHeader.mSampleKind after the read (Features.cc:1349),
+  // without _Z for the mean file, with the delivered derivative flags for the variance file (:1383-1385)
+  int kind = targetKind & ~(kParmD | kParmA | kParmT);
+  // the last file of each kind is kept (the reference re-reads only when the name changes)
+  thread_local std::string last_cmn, last_cvn, last_cvg;
+  thread_local std::vector<float> cmn, cvn, cvg;
+  if (cfg.cmn) {
+    std::string name;
+    ProcessMask(logical, cfg.cmnMask, &name);
+    if (name.empty()) Fail("CMN Matching failed");
+    name = (cfg.cmnDir.empty() ? std::string() : cfg.cmnDir + "/") + "/" + name;
+    if (name != last_cmn) {
+      last_cmn.clear();
+      cmn = ReadCepsNormFile(name, kind & ~kParmZ, kCnfMean, coefs);
+      last_cmn = name;
+    }
+    for (int i = 0; i < tot; i++)
+      for (int j = trg_N; j < coefs; j++) M[(size_t)i * trg_vec + (j - trg_N)] -= cmn[(size_t)j];
+  }
+  kind |= derivOrder == 3 ? (kParmD | kParmA | kParmT) : derivOrder == 2 ? (kParmD | kParmA) : derivOrder == 1 ? kParmD : 0;
+  if (cfg.cvn) {
+    std::string name;
+    ProcessMask(logical, cfg.cvnMask, &name);
+    name = (cfg.cvnDir.empty() ? std::string() : cfg.cvnDir + "/") + "/" + name;
+    if (name != last_cvn) {
+      last_cvn.clear();
+      cvn = ReadCepsNormFile(name, kind, kCnfVariance, trg_vec);
+      last_cvn = name;
+    }
+    for (int i = 0; i < tot; i++)
+      for (int j = trg_N; j < trg_vec; j++) M[(size_t)i * trg_vec + (j - trg_N)] *= cvn[(size_t)j];
+  }
+  if (cfg.cvg) {
+    if (cfg.cvgFile != last_cvg) {
+      last_cvg.clear();
+      cvg = ReadCepsNormFile(cfg.cvgFile, -1, kCnfVarScale, trg_vec);
+      last_cvg = cfg.cvgFile;
+    }
+    for (int i = 0; i < tot; i++)
+      for (int j = trg_N; j < trg_vec; j++) M[(size_t)i * trg_vec + (j - trg_N)] *= cvg[(size_t)j];
+  }
+}
+
+namespace {
 // PATH_MAX on Linux: MlfStream.h's MAX_LABEL_DEPTH, the depth of a name without a leading '*'
 constexpr size_t kMaxLabelDepth = 4096;
 size_t DirDepth(const std::string& path) {

@@ -66,6 +66,12 @@ struct FeatureConfig {
   int targetKind = kParmAnon;  // TARGETKIND (UserInterface.cc:411-417); ANON latches the first file's kind
   int derivOrder = 0;        // 0 with TARGETKIND=ANON (UserInterface.cc:444-459); < 0: the first file's
   std::vector<int> derivWin; // DELTAWINDOW / ACCWINDOW / THIRDWINDOW (default 2 each)
+  // cepstral mean / variance normalisation files (UserInterface.cc:385-410, Features.cc:1352-1410): active when
+  // the mask is set; the file is <dir>/ + "/" + the characters the mask's '%'s capture from the logical name
+  bool cmn = false, cvn = false, cvg = false;
+  std::string cmnDir, cmnMask;  // CMEANDIR, CMEANMASK
+  std::string cvnDir, cvnMask;  // VARSCALEDIR, VARSCALEMASK
+  std::string cvgFile;          // VARSCALEFN
 };
 
 struct Utterance {

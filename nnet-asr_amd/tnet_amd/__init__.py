@@ -516,14 +516,18 @@ class FeatureReader:
     def __init__(self, scp: str, mlf: Optional[str] = None, label_map: Optional[str] = None,
                  label_dir: Optional[str] = None, label_ext: Optional[str] = "lab", start_ext: int = 0,
                  end_ext: int = 0, swap: bool = True, target_kind: int = 12, deriv_order: int = 0,
-                 deriv_win: Optional[Sequence[int]] = None, threads: int = 4, depth: int = 16):
+                 deriv_win: Optional[Sequence[int]] = None, threads: int = 4, depth: int = 16,
+                 cmn_dir: Optional[str] = None, cmn_mask: Optional[str] = None, cvn_dir: Optional[str] = None,
+                 cvn_mask: Optional[str] = None, cvg_file: Optional[str] = None):
+        """cmn_* / cvn_* / cvg_file: CMEANDIR / CMEANMASK, VARSCALEDIR / VARSCALEMASK, VARSCALEFN"""
         enc = lambda s: s.encode() if s is not None else None  # noqa: E731
         self._win = (C.c_int * len(deriv_win))(*deriv_win) if deriv_win else None
         self.start_ext, self.end_ext = start_ext, end_ext
-        self.h = check_ptr(lib().tnet_reader_create(enc(scp), int(swap), start_ext, end_ext, target_kind, deriv_order,
-                                                    C.cast(self._win, C.c_void_p) if self._win else None, enc(mlf),
-                                                    enc(label_map), enc(label_dir), enc(label_ext), threads, depth),
-                           "reader_create")
+        self.h = check_ptr(lib().tnet_reader_create_norm(
+            enc(scp), int(swap), start_ext, end_ext, target_kind, deriv_order,
+            C.cast(self._win, C.c_void_p) if self._win else None, enc(mlf), enc(label_map), enc(label_dir),
+            enc(label_ext), enc(cmn_dir), enc(cmn_mask), enc(cvn_dir), enc(cvn_mask), enc(cvg_file), threads, depth),
+            "reader_create")
 
     def __len__(self) -> int:
         return int(lib().tnet_reader_size(self.h))

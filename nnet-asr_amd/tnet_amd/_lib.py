@@ -157,6 +157,9 @@ _SIGS = {
     "tnet_trainer_set_transform": (i32, [vp, vp, i32, i32]),
     "tnet_reader_create": (vp, [C.c_char_p, i32, i32, i32, i32, i32, vp, C.c_char_p, C.c_char_p, C.c_char_p,
                                 C.c_char_p, i32, i32]),
+    "tnet_reader_create_norm": (vp, [C.c_char_p, i32, i32, i32, i32, i32, vp, C.c_char_p, C.c_char_p, C.c_char_p,
+                                     C.c_char_p, C.c_char_p, C.c_char_p, C.c_char_p, C.c_char_p, C.c_char_p, i32,
+                                     i32]),
     "tnet_reader_free": (i32, [vp]),
     "tnet_reader_size": (i64, [vp]),
     "tnet_reader_next": (i32, [vp, C.POINTER(vp), C.POINTER(i32), C.POINTER(i32), C.POINTER(vp), C.POINTER(i32),

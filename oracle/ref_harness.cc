@@ -258,6 +258,7 @@ static int cmd_train(int argc, char** argv) {
 }
 
 // features <scp> <swap> <start_ext> <end_ext> <TARGETKIND> <mlf|-> <map> <label_dir|-> <label_ext> <outdir>
+//          [<CMEANDIR|-> <CMEANMASK|-> <VARSCALEDIR|-> <VARSCALEMASK|-> <VARSCALEFN|->]
 // outdir/index.txt: "k rows cols period kind n_labels logical" or "k ERROR <message>" per record;
 // outdir/f<k>.f32 (rows x cols), outdir/l<k>.i32 (argmax of each GenDesiredMatrix row)
 static int cmd_features(int argc, char** argv) {
@@ -274,8 +275,24 @@ static int cmd_features(int argc, char** argv) {
     win[0] = win[1] = win[2] = 2;
   }
   const std::string mlf = argv[7], map = argv[8], ldir = argv[9], lext = argv[10], out = argv[11];
+  // optional: CMEANDIR CMEANMASK VARSCALEDIR VARSCALEMASK VARSCALEFN ("-" = unset), composed into the
+  // repository's paths as UserInterface::GetFeatureParams does (UserInterface.cc:385-410: dir + "/")
+  std::string cmn_path, cvn_path;
+  const char *cmn_mask = NULL, *cvn_mask = NULL, *cvg = NULL;
+  if (argc >= 17) {
+    if (strcmp(argv[13], "-")) {
+      cmn_mask = argv[13];
+      cmn_path = strcmp(argv[12], "-") ? std::string(argv[12]) + "/" : std::string();
+    }
+    if (strcmp(argv[15], "-")) {
+      cvn_mask = argv[15];
+      cvn_path = strcmp(argv[14], "-") ? std::string(argv[14]) + "/" : std::string();
+    }
+    if (strcmp(argv[16], "-")) cvg = argv[16];
+  }
   FeatureRepository repo;
-  repo.Init(swap, sext, eext, target_kind, deriv_order, win, NULL, NULL, NULL, NULL, NULL);
+  repo.Init(swap, sext, eext, target_kind, deriv_order, win, cmn_mask ? cmn_path.c_str() : NULL, cmn_mask,
+            cvn_mask ? cvn_path.c_str() : NULL, cvn_mask, cvg);
   repo.AddFileList(argv[2]);
   LabelRepository labels;
   const bool use_mlf = mlf != "-";

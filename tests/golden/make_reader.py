@@ -133,6 +133,30 @@ def lookup_mlf():
     return "\n".join(mlf) + "\n"
 
 
+def norm_files(rng):
+    """cepstral mean / variance files for the CMEANDIR / VARSCALEDIR / VARSCALEFN cases (Features.cc:96-178,
+    1352-1410): per-speaker files named by the first four characters of the logical name (mask %%%%*)"""
+    f = {}
+
+    def vec(n, lo=-1.0, hi=1.0):
+        return " ".join(f"{v:.7g}" for v in rng.uniform(lo, hi, n))
+    for spk in ("spkA", "spkB"):
+        f[f"norm/cmn/{spk}"] = f"<CEPSNORM> <FBANK>\n<MEAN> 12\n{vec(12)}\n"
+        f[f"norm/cvn/{spk}"] = f"<CEPSNORM> <FBANK>\n<VARIANCE> 12\n{vec(12, 0.2, 4.0)}\n"
+        f[f"norm/cmn_eda/{spk}"] = f"<cepsnorm> <MFCC_E>\n<mean> 13\n{vec(13)}\n"
+        f[f"norm/cvn_eda/{spk}"] = f"<CEPSNORM> <MFCC_E_D_A>\n<VARIANCE> 39\n{vec(39, 0.2, 4.0)}\n"
+        f[f"norm/cmn_z/{spk}"] = f"<CEPSNORM> <MFCC_0>\n<MEAN> 13\n{vec(13)}\n"
+    f["norm/varscale12"] = f"<VARSCALE> 12\n{vec(12, 0.5, 2.0)}\n"
+    f["norm/bad/kind/spkA"] = f"<CEPSNORM> <MFCC>\n<MEAN> 12\n{vec(12)}\n"
+    f["norm/bad/count/spkA"] = f"<CEPSNORM> <FBANK>\n<MEAN> 11\n{vec(11)}\n"
+    f["norm/bad/eof/spkA"] = f"<CEPSNORM> <FBANK>\n<MEAN> 12\n{vec(7)}\n"
+    f["norm/bad/junk/spkA"] = f"<CEPSNORM> <FBANK>\n<MEAN> 12\n{vec(12)} extra\n"
+    f["norm/bad/word/spkA"] = f"<CEPSNORM> <FBANK>\n<MEAN> 12\n{vec(5)} x7 {vec(6)}\n"
+    return f
+
+
+SPK = ["spkA_u1=d/fb.fea", "spkB_u2=d/fb.fea", "spkA_u3=d/fb.fea"]
+
 CONFIGS = {
     # name: (scp lines, swap, sext, eext, TARGETKIND, mlf?, label_dir)
     "plain": (["d/fb.fea", "d/fbc.fea", "d/long.fea"], 1, 3, 2, "ANON", True, None),
@@ -157,13 +181,28 @@ CONFIGS = {
                     "/y/f1=d/long.fea", "x/g2z=d/long.fea", "x/h7z=d/long.fea"], 1, 0, 0, "ANON", "lookup.mlf", None),
     "err_mlf_depth0": (["x/d1=d/long.fea"], 1, 0, 0, "ANON", "lookup.mlf", None),
     "err_mlf_set": (["x/h2z=d/long.fea"], 1, 0, 0, "ANON", "lookup.mlf", None),
+    # CMEANDIR / VARSCALEDIR / VARSCALEFN (8th field: cmn dir, cmn mask, cvn dir, cvn mask, VARSCALEFN)
+    "norm_cmn": (SPK, 1, 2, 1, "ANON", False, None, ("norm/cmn", "%%%%*", None, None, None)),
+    "norm_all": (SPK, 1, 2, 1, "ANON", False, None, ("norm/cmn", "%%%%*", "norm/cvn", "%%%%*", "norm/varscale12")),
+    "norm_eda": (["spkA_e=d/mfe.fea", "spkB_e=d/mfe.fea"], 1, 2, 2, "MFCC_E_D_A", False, None,
+                 ("norm/cmn_eda", "%%%%*", "norm/cvn_eda", "%%%%*", None)),
+    "norm_z": (["spkB_z=d/mf0.fea"], 1, 0, 0, "MFCC_0_Z", False, None, ("norm/cmn_z", "%%%%*", None, None, None)),
+    "err_norm_nomatch": (["u1=d/fb.fea"], 1, 0, 0, "ANON", False, None, ("norm/cmn", "%%%%?*", None, None, None)),
+    "err_norm_kind": (["spkA_u1=d/fb.fea"], 1, 0, 0, "ANON", False, None, ("norm/bad/kind", "%%%%*", None, None, None)),
+    "err_norm_count": (["spkA_u1=d/fb.fea"], 1, 0, 0, "ANON", False, None,
+                       ("norm/bad/count", "%%%%*", None, None, None)),
+    "err_norm_eof": (["spkA_u1=d/fb.fea"], 1, 0, 0, "ANON", False, None, ("norm/bad/eof", "%%%%*", None, None, None)),
+    "err_norm_junk": (["spkA_u1=d/fb.fea"], 1, 0, 0, "ANON", False, None, ("norm/bad/junk", "%%%%*", None, None, None)),
+    "err_norm_word": (["spkA_u1=d/fb.fea"], 1, 0, 0, "ANON", False, None, ("norm/bad/word", "%%%%*", None, None, None)),
+    "err_norm_cvn_missing": (["spkA_u1=d/fb.fea"], 1, 0, 0, "ANON", False, None,
+                             (None, None, "norm/nosuch", "%%%%*", None)),
 }
 
 
-def run_harness(td, scp, swap, sext, eext, tk, mlf, ldir, out):
+def run_harness(td, scp, swap, sext, eext, tk, mlf, ldir, out, norm=None):
     os.makedirs(out, exist_ok=True)
     cmd = [HARNESS, "features", scp, str(swap), str(sext), str(eext), tk, mlf or "-", "states.txt", ldir or "-", "lab",
-           out]
+           out] + ([v or "-" for v in norm] if norm else [])
     subprocess.run(cmd, cwd=td, check=True, capture_output=True)
     res = []
     for line in open(os.path.join(out, "index.txt")):
@@ -204,13 +243,20 @@ def main():
         open(os.path.join(td, "test.mlf"), "w").write(mlf)
         open(os.path.join(td, "lookup.mlf"), "w").write(lookup_mlf())
         open(os.path.join(td, "states.txt"), "w").write(states)
-        for name, (lines, swap, sext, eext, tk, use_mlf, ldir) in CONFIGS.items():
+        nf = norm_files(np.random.default_rng(11))
+        for rel, text in nf.items():
+            os.makedirs(os.path.join(td, os.path.dirname(rel)), exist_ok=True)
+            open(os.path.join(td, rel), "w").write(text)
+            arrays[f"norm:{rel}"] = np.frombuffer(text.encode(), np.uint8)
+        for name, cfg in CONFIGS.items():
+            lines, swap, sext, eext, tk, use_mlf, ldir = cfg[:7]
+            norm = cfg[7] if len(cfg) > 7 else None
             scp = os.path.join(td, f"{name}.scp")
             open(scp, "w").write("\n".join(lines) + "\n")
             mlf_name = use_mlf if isinstance(use_mlf, str) else ("test.mlf" if use_mlf else None)
-            res = run_harness(td, scp, swap, sext, eext, tk, mlf_name, ldir, os.path.join(td, "out_" + name))
+            res = run_harness(td, scp, swap, sext, eext, tk, mlf_name, ldir, os.path.join(td, "out_" + name), norm)
             cm = {"scp": lines, "swap": swap, "start_ext": sext, "end_ext": eext, "target_kind": tk,
-                  "mlf": use_mlf, "label_dir": ldir, "records": []}
+                  "mlf": use_mlf, "label_dir": ldir, "norm": list(norm) if norm else None, "records": []}
             for k, r in enumerate(res):
                 if "error" in r:
                     cm["records"].append({"error": r["error"]})

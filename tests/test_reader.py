@@ -40,6 +40,9 @@ def workdir(tmp_path_factory):
     for k in _G.files:  # per-config MLFs (make_reader.py lookup_mlf: LabelContainer's lookup order)
         if k.startswith("mlf:"):
             (td / k[4:]).write_bytes(bytes(_G[k]))
+        if k.startswith("norm:"):  # CMEANDIR / VARSCALEDIR / VARSCALEFN files (make_reader.py norm_files)
+            os.makedirs(td / os.path.dirname(k[5:]), exist_ok=True)
+            (td / k[5:]).write_bytes(bytes(_G[k]))
     return td
 
 
@@ -64,7 +67,9 @@ def _reader(td, name, threads=3, depth=2):
     os.chdir(td)
     try:
         mlf = c["mlf"] if isinstance(c["mlf"], str) else ("test.mlf" if c["mlf"] else None)
-        return FeatureReader(str(scp), mlf=mlf, label_map="states.txt",
+        norm = c.get("norm") or [None] * 5
+        return FeatureReader(str(scp), mlf=mlf, label_map="states.txt", cmn_dir=norm[0], cmn_mask=norm[1],
+                             cvn_dir=norm[2], cvn_mask=norm[3], cvg_file=norm[4],
                              label_dir=c["label_dir"], start_ext=c["start_ext"], end_ext=c["end_ext"],
                              swap=bool(c["swap"]), target_kind=kind, deriv_order=order, threads=threads, depth=depth)
     finally:
@@ -90,6 +95,7 @@ def test_reader_matches_reference_feature_repository(workdir, name):
         ref_x, ref_lab = _G[f"{name}:x{k}"], _G[f"{name}:lab{k}"]
         assert (x.shape, per, kind, logical) == ((rec["rows"], rec["cols"]), rec["period"], rec["kind"], rec["logical"])
         assert np.array_equal(x.view(np.uint32), ref_x.view(np.uint32)), f"{name} record {k}: features differ"
+        lab = np.zeros(0, np.int32) if lab is None else lab  # no MLF: the reference writes no class ids
         assert np.array_equal(lab, ref_lab), f"{name} record {k}: class ids differ"
 
 
