@@ -437,6 +437,17 @@ int tnet_gemv_rows(const float* W, int ldw, int r0, int nrows, int n, const floa
  *   corr = sum_{i<steps} (-lr h_i) (x) d_i ; corr += -lr*wc*W ; W += corr
  *   cb = -lr d_0 + mmt*cb ; cb = -lr d_i + cb (i >= 1) ; b += cb
  * h_i = row (head + i) % R of the history ring hist [R x rows], d_i = row i of D. */
+/* The `order` BPTT GEMVs of one frame (cuRecurrent.cc:106-145; tnet_gemv_rows with s = the history's y rows,
+   r0 = nIn, beta 0, x = row i-1 of D, y = row i of D, i = 1..order) in ONE launch on n / 64 co-resident
+   workgroups handing each step's vector on as write-through granules; bit-identical to the per-step launches.
+   workspace: tnet_rnn_bptt_chain_workspace(n, order) bytes, zeroed once before the first call and kept for the
+   layer's life (its epoch word orders the launches).  TNET_ERR_UNSUPPORTED outside n <= 1024 (n % 64 == 0 up
+   to 512, n % 32 == 0 above), 16-B aligned W / D, order < 16.  A hand-off that never arrives (a bug) sets an
+   error word instead of hanging: tnet_rnn_bptt_chain_error reads it (synchronous). */
+long tnet_rnn_bptt_chain_workspace(int n, int order);
+int tnet_rnn_bptt_chain(const float* W, int ldw, int r0, int n, float* D, int ldd, int order, const float* hist,
+                        int ldh, int head, int R, int hoff, void* workspace, void* stream);
+int tnet_rnn_bptt_chain_error(const void* workspace, int* err);
 int tnet_rnn_update(float* W, int ldw, int rows, int nout, const float* hist, int ldh, int head, int R,
                     const float* D, int ldd, int steps, float* b, float* corr_b, float lr, float mmt, float wc,
                     void* stream);

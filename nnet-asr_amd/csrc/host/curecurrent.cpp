@@ -19,6 +19,28 @@ void CuRecurrent::BpttOrder(int ord) {
   mDiff.Init((size_t)ord + 1, GetNOutputs());
   mDiffTmp.Init(1, GetNOutputs());
   mHead = 0;
+  // the one-launch BPTT chain's control words and granule slots (zeroed: epoch 0, no granule current)
+  const size_t cb = (size_t)tnet_rnn_bptt_chain_workspace((int)GetNOutputs(), ord);
+  if (cb > mChainBytes) {
+    if (mChainWs) TNET_HIP_CALL(hipFree(mChainWs));
+    mChainWs = nullptr;
+    mChainBytes = 0;
+    TNET_HIP_CALL(hipMalloc(&mChainWs, cb));
+    mChainBytes = cb;
+  }
+  TNET_HIP_CALL(hipMemset(mChainWs, 0, mChainBytes));
+}
+
+CuRecurrent::~CuRecurrent() {
+  if (mChainWs) (void)hipFree(mChainWs);
+}
+
+void CuRecurrent::CheckChain() const {
+  if (!mChainWs) return;
+  int err = 0;
+  TNET_SAFE_CALL(tnet_rnn_bptt_chain_error(mChainWs, &err));
+  if (err) Error("CuRecurrent: the one-launch BPTT chain timed out waiting for a hand-off (TNET_RNN_BPTT_CHAIN=0 "
+                 "runs the per-step launches)");
 }
 
 void CuRecurrent::ClearHistory() {
@@ -96,11 +118,23 @@ void CuRecurrent::Update() {
 void CuRecurrent::UpdateFromDiff0(bool defer) {
   FlushPendingUpdate();
   const int nIn = (int)GetNInputs(), nOut = (int)GetNOutputs();
-  // BPTT: d_i = (W[nIn:nIn+nOut] d_{i-1}) .* y_{t-i}(1 - y_{t-i}), y_{t-i} = y part of history row i-1
-  for (int i = 1; i <= mBpttOrder; i++)
-    TNET_SAFE_CALL(tnet_gemv_rows(mLinearity.pCUData(), (int)mLinearity.Stride(), nIn, nOut, nOut,
-                                  mDiff.pCURowData((size_t)i - 1), mDiff.pCURowData((size_t)i), 0.0f,
-                                  HistRow(i - 1) + nIn, S));
+  // BPTT: d_i = (W[nIn:nIn+nOut] d_{i-1}) .* y_{t-i}(1 - y_{t-i}), y_{t-i} = y part of history row i-1 --
+  // all `order` steps in one launch where the shape allows (tnet_rnn_bptt_chain, bit-identical to the
+  // per-step launches; TNET_RNN_BPTT_CHAIN=0: one tnet_gemv_rows launch per step)
+  static const bool chain = !(getenv("TNET_RNN_BPTT_CHAIN") && getenv("TNET_RNN_BPTT_CHAIN")[0] == '0');
+  int st = TNET_ERR_UNSUPPORTED;
+  if (chain && mChainWs && mBpttOrder > 0)
+    st = tnet_rnn_bptt_chain(mLinearity.pCUData(), (int)mLinearity.Stride(), nIn, nOut, mDiff.pCUData(),
+                             (int)mDiff.Stride(), mBpttOrder, mInputHistory.pCUData(), (int)mInputHistory.Stride(),
+                             mHead, (int)mInputHistory.Rows(), nIn, mChainWs, S);
+  if (st != TNET_ERR_UNSUPPORTED) {
+    TNET_SAFE_CALL(st);
+  } else {
+    for (int i = 1; i <= mBpttOrder; i++)
+      TNET_SAFE_CALL(tnet_gemv_rows(mLinearity.pCUData(), (int)mLinearity.Stride(), nIn, nOut, nOut,
+                                    mDiff.pCURowData((size_t)i - 1), mDiff.pCURowData((size_t)i), 0.0f,
+                                    HistRow(i - 1) + nIn, S));
+  }
   if (defer) {
     mPending = true;
     mPendHead = mHead;
@@ -223,6 +257,7 @@ void CuRecurrentTrainer::TrainUtterance(const float* feats, size_t rows, size_t 
     RunFrames(rows);
     TNET_SAFE_CALL(tnet_argmax_correct((const unsigned long long*)mArgKey, mLabels.pCUData(), (int)rows,
                                        (int)mNet->GetNOutputs(), mObj->DeviceStats(), S));
+    dynamic_cast<CuRecurrent&>(mNet->Layer(0)).CheckChain();  // one flag read per utterance
     mFrames += (long)rows;
     return;
   }

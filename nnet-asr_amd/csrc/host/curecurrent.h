@@ -30,8 +30,11 @@ class CuRecurrent : public CuUpdatableComponent {
       : CuUpdatableComponent(nInputs, nOutputs, pPred), mLinearity(nInputs + nOutputs, nOutputs), mBias(nOutputs),
         mBiasCorrection(nOutputs) {}
 
+  ~CuRecurrent() override;
   ComponentType GetType() const override { return RECURRENT; }
   const char* GetName() const override { return "<recurrent>"; }
+  /// Throws if the one-launch BPTT chain (tnet_rnn_bptt_chain) reported a timed-out hand-off (synchronises).
+  void CheckChain() const;
 
   void PropagateFnc(const CuMatrix<BaseFloat>& X, CuMatrix<BaseFloat>& Y) override;
   void BackpropagateFnc(const CuMatrix<BaseFloat>& X, CuMatrix<BaseFloat>& Y) override;
@@ -76,6 +79,8 @@ class CuRecurrent : public CuUpdatableComponent {
   CuMatrix<BaseFloat> mLinearity;
   CuVector<BaseFloat> mBias, mBiasCorrection;
   CuMatrix<BaseFloat> mInputHistory;  // ring of bptt+2 rows [x, y_prev] (the update reads bptt+1)
+  void* mChainWs = nullptr;            // tnet_rnn_bptt_chain's control words + granule slots
+  size_t mChainBytes = 0;
   CuMatrix<BaseFloat> mDiff;          // [bptt+1 x nOut] back-propagated errors of the present update
   CuMatrix<BaseFloat> mDiffTmp;       // [1 x nOut]
   int mBpttOrder = -1;

@@ -195,6 +195,9 @@ _SIGS = {
     "tnet_gemv_workspace": (i64, [i32, i32]),
     "tnet_gemv_rowvec": (i32, [vp, i32, vp, i32, vp, vp, i32, i32, vp, vp]),
     "tnet_gemv_rows": (i32, [vp, i32, i32, i32, i32, vp, vp, f32, vp, vp]),
+    "tnet_rnn_bptt_chain_workspace": (i64, [i32, i32]),
+    "tnet_rnn_bptt_chain": (i32, [vp, i32, i32, i32, vp, i32, i32, vp, i32, i32, i32, i32, vp, vp]),
+    "tnet_rnn_bptt_chain_error": (i32, [vp, vp]),
     "tnet_rnn_update": (i32, [vp, i32, i32, i32, vp, i32, i32, i32, vp, i32, i32, vp, vp, f32, f32, f32, vp]),
     "tnet_affine_fwd_t": (i32, [vp, MatrixDim, vp, MatrixDim, vp, vp, MatrixDim, i32, vp]),
     "tnet_rbm_update": (i32, [vp, MatrixDim, vp, MatrixDim, vp, MatrixDim, vp, i32, f32, f32, f32, vp]),

@@ -7,6 +7,7 @@ Tolerances: single-frame kernels rtol 1e-5; after whole utterances (hundreds of 
 per-frame SGD updates, each amplifying fp32 rounding differences) parameters rtol 2e-3 /
 atol 2e-5 and summed cross-entropy rtol 1e-4.
 """
+import ctypes
 import os
 
 import numpy as np
@@ -424,3 +425,41 @@ def test_gemv_rowvec_partial_update(nIn, H, steps, R, head, mmt, wc):
     assert lib().tnet_gemv_rowvec_partial_update(dummy.ptr, 8, dummy.ptr, 8, None, dummy.ptr, 64, 8, dummy.ptr,
                                                  dummy.ptr, 64, 0, 4, dummy.ptr, 64, 4, dummy.ptr, dummy.ptr, lr,
                                                  mmt, wc, S()) != 0
+
+
+@pytest.mark.parametrize("n_in,n,order", [(440, 512, 4), (440, 512, 1), (128, 256, 6), (64, 1024, 4), (40, 768, 3)])
+def test_bptt_chain_matches_per_step_launches(n_in, n, order):
+    """tnet_rnn_bptt_chain (the frame's `order` BPTT GEMVs in one launch, step vectors handed on as
+    write-through granules) against `order` tnet_gemv_rows launches: every row of D bit for bit, over
+    several consecutive launches with a moving ring head (each launch advances the granule epoch, so a
+    stale granule of the previous launch must never be taken as current)."""
+    from tnet_amd._lib import lib as L
+    rng = np.random.default_rng(n + order)
+    K, R = n_in + n, order + 2
+    W = (0.05 * rng.standard_normal((K, n))).astype(np.float32)
+    hist = rng.random((R, K)).astype(np.float32)
+    dW, dH = DeviceArray.from_numpy(W), DeviceArray.from_numpy(hist)
+    ws_bytes = L().tnet_rnn_bptt_chain_workspace(n, order)
+    ws = DeviceArray.from_numpy(np.zeros(-(-ws_bytes // 4), np.float32))
+    st = L().tnet_stream()
+    for launch in range(5):
+        head = launch % R
+        d0 = rng.standard_normal(n).astype(np.float32) * 0.1
+        outs = []
+        for chain in (True, False):
+            D = np.zeros((order + 1, n), np.float32)
+            D[0] = d0
+            dD = DeviceArray.from_numpy(D)
+            if chain:
+                rc = L().tnet_rnn_bptt_chain(dW.ptr, dW.stride, n_in, n, dD.ptr, dD.stride, order, dH.ptr, dH.stride,
+                                             head, R, n_in, ws.ptr, st)
+                assert rc == 0, rc
+            else:
+                for i in range(1, order + 1):
+                    srow = dH.ptr + 4 * (((head + i - 1) % R) * dH.stride + n_in)
+                    assert L().tnet_gemv_rows(dW.ptr, dW.stride, n_in, n, n, dD.ptr + 4 * (i - 1) * dD.stride,
+                                              dD.ptr + 4 * i * dD.stride, 0.0, srow, st) == 0
+            outs.append(dD.numpy())
+        np.testing.assert_array_equal(outs[0], outs[1], err_msg=f"launch {launch}")
+    err = ctypes.c_int(-1)
+    assert L().tnet_rnn_bptt_chain_error(ws.ptr, ctypes.byref(err)) == 0 and err.value == 0

@@ -53,6 +53,7 @@ __global__ __launch_bounds__(NT) void occupier(float* out, long ticks) {
     acc += lds[(threadIdx.x * 7 + (int)acc) & (LDSB / 4 - 1 < 1023 ? 255 : 1023)];
     __builtin_amdgcn_s_sleep(8);
   }
+  if constexpr (NV == 280) asm volatile("" ::: "v255", "a23");  // torch's librccl: 261-280 (VGPR + AGPR)
   if constexpr (NV == 256) asm volatile("" ::: "v255");
   if constexpr (NV == 192) asm volatile("" ::: "v191");
   if constexpr (NV == 128) asm volatile("" ::: "v127");
@@ -110,23 +111,31 @@ static int steal_probe(int nocc) {
     CK(hipEventElapsedTime(&ms, a, b));
     return ms;
   };
+  // the two RCCL builds this image carries (profiles/r04_rccl_footprint.json): /opt/rocm's
+  // ncclDevKernel_Generic (512 threads, 37,664 B LDS, 248-256 VGPRs) and torch's bundled rcclGenericKernel,
+  // the one a Python process maps (256 threads, 19,744 B LDS, 261-280 VGPRs)
   const char* modes[] = {"auto+rsv0", "auto+rsv8", "auto+rsv16"};
-  for (int which = 0; which < 3; ++which)
-    for (const char* mode : modes) {
-      CT(tnet_gemm_config(mode));
-      run(which);
-      CK(hipStreamSynchronize(s1));
-      const float alone = timed(which);
-      const long ticks = (long)(alone * 4.0f * 1e5f) + 20000;
-      occupier<512><<<nocc, 512, 0, s2>>>(junk, ticks);
-      CK(hipGetLastError());
-      std::this_thread::sleep_for(std::chrono::microseconds(200));
-      const float occ = timed(which);
-      CK(hipStreamSynchronize(s2));
-      printf("%-50s %-9s: alone %.1f us; beside %d RCCL-footprint occupiers (512 thr, 37.6 KB, 256 VGPR): %.1f us "
-             "(x%.2f)\n", names[which], mode, 1e3f * alone / reps, nocc, 1e3f * occ / reps, occ / alone);
-      fflush(stdout);
-    }
+  for (int fp = 0; fp < 2; ++fp)
+    for (int which = 0; which < 3; ++which)
+      for (const char* mode : modes) {
+        CT(tnet_gemm_config(mode));
+        run(which);
+        CK(hipStreamSynchronize(s1));
+        const float alone = timed(which);
+        const long ticks = (long)(alone * 4.0f * 1e5f) + 20000;
+        if (fp == 0) occupier<512><<<nocc, 512, 0, s2>>>(junk, ticks);
+        else occupier<256, 19744, 280><<<nocc, 256, 0, s2>>>(junk, ticks);
+        CK(hipGetLastError());
+        std::this_thread::sleep_for(std::chrono::microseconds(200));
+        const float occ = timed(which);
+        CK(hipStreamSynchronize(s2));
+        printf("%-50s %-9s: alone %.1f us; beside %d %s occupiers: %.1f us (x%.2f)\n", names[which], mode,
+               1e3f * alone / reps, nocc,
+               fp == 0 ? "/opt/rocm RCCL-footprint (512 thr, 37.6 KB, 256 VGPR)"
+                       : "torch RCCL-footprint (256 thr, 19.7 KB, 280 VGPR)",
+               1e3f * occ / reps, occ / alone);
+        fflush(stdout);
+      }
   CT(tnet_gemm_config("auto+rsv0"));
   return 0;
 }
