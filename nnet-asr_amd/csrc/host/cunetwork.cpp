@@ -504,6 +504,14 @@ void CuNetwork::TrainBunch(const CuMatrix<BaseFloat>& X, const CuVector<int>& la
   }
   flush();
   if (exchange) {
+    // the next bunch's gather right behind the last gradient GEMM on the compute stream, so it runs while the
+    // last reductions (and their applies) are still in flight instead of after WaitAll at the next step's start
+    if (mHasTailGather && !mTailDone) {
+      KTScope kt("gather", 2.0 * mTailGather.dy.rows * mTailGather.dy.cols * 4.0);
+      TNET_SAFE_CALL(tnet_gather_bunch(mTailGather.y, mTailGather.x, mTailGather.labels_out, mTailGather.labels_in,
+                                       mTailGather.copy_from, mTailGather.dy, mTailGather.dx, S));
+      mTailDone = true;
+    }
     // transports without an apply stream: apply each layer on the compute stream as soon as its own
     // reduction is done (top layer first), overlapping the reductions of the layers below
     const int first = n_submitted - (int)submitted.size();

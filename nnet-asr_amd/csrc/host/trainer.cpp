@@ -116,7 +116,8 @@ void CuTrainer::Step() {
     nl.Init(mCache.Bunchsize());
     // from here the cache has moved past that bunch: mAhead stays true and the guard delivers the bunch into
     // the other buffer whatever happens below (a throwing TrainBunch must not skip a bunch)
-    guard.Arm(mCache.AheadGather(nf, nl), !mOpt.crossval && !mExchange);
+    // (data parallel: the network launches it right behind its last gradient GEMM, beside the exchange)
+    guard.Arm(mCache.AheadGather(nf, nl), !mOpt.crossval);
     mAhead = true;
     mAheadOnStream = false;
   }

@@ -225,6 +225,14 @@ __global__ __launch_bounds__(256) void gemv_softmax_xent_final(const float* __re
   }
 }
 
+// a[0] b[0] + a[1] b[1] + a[2] b[2] + a[3] b[3] with every product rounded and the sums taken left to right
+// (no contraction): the vectoriser may turn the products into v_pk_mul_f32 in one kernel and leave them for
+// v_fmac in another, so gemv_rows_kernel and the BPTT chain pin the arithmetic here to stay bit-identical.
+__device__ __forceinline__ float dot4_rounded(const f32x4 a, const f32x4 b) {
+#pragma clang fp contract(off)
+  return a[0] * b[0] + a[1] * b[1] + a[2] * b[2] + a[3] * b[3];
+}
+
 // y[r] = beta*y[r] + dot(W[r0 + r, 0:n], x) ; then if s != NULL: y[r] *= s[r] (1 - s[r]).
 // Rows of <= 1024 aligned floats: every load of the wave (the row, x, s[r], y[r]) issued in one round
 // at clamped addresses, the products then added in the loop form's order (c = 4 lane + 256 q)
@@ -249,7 +257,7 @@ __global__ __launch_bounds__(256) void gemv_rows_kernel(const float* __restrict_
       }
 #pragma unroll
       for (int q = 0; q < 4; ++q)
-        if (lane * 4 + 256 * q < n) acc += a[q][0] * b[q][0] + a[q][1] * b[q][1] + a[q][2] * b[q][2] + a[q][3] * b[q][3];
+        if (lane * 4 + 256 * q < n) acc += dot4_rounded(a[q], b[q]);
     } else {
       for (int c = lane * 4; c < n; c += 256) {
         const f32x4 a = *reinterpret_cast<const f32x4*>(row + c), b = *reinterpret_cast<const f32x4*>(x + c);
@@ -311,7 +319,7 @@ __global__ __launch_bounds__(256) void rnn_bptt_chain_kernel(const float* __rest
       float t = 0.f;
 #pragma unroll
       for (int q = 0; q < QN; ++q)
-        if (lane * 4 + 256 * q < n) t += a[j][q][0] * b[q][0] + a[j][q][1] * b[q][1] + a[j][q][2] * b[q][2] + a[j][q][3] * b[q][3];
+        if (lane * 4 + 256 * q < n) t += dot4_rounded(a[j][q], b[q]);
       acc[j] = t;
     }
 #pragma unroll
