@@ -275,6 +275,14 @@ int tnet_affine_grad(const float* X, TnetMatrixDim dX, const float* E, TnetMatri
  * (data-parallel path: both gradients are all-reduced, then applied by tnet_sgd_update_multi). */
 int tnet_affine_grad_bias(const float* X, TnetMatrixDim dX, const float* E, TnetMatrixDim dE, float* G,
                           TnetMatrixDim dG, const float* colpart, int ldcolpart, float* gradB, void* stream);
+/* tnet_affine_grad_bias plus tnet_gather_bunch (the next bunch's CuCache::GetBunch, cuCache.cc:155-200) on the CUs
+ * the gradient GEMM's tiles leave free -- the data-parallel step's last gradient GEMM, tnet_affine_update_bias_gather's
+ * form and rules: the gather independent of the GEMM (TNET_ERR_ARG otherwise), results identical to the separate calls,
+ * TNET_ERR_UNSUPPORTED when the GEMM would run another tile configuration alone or fewer than 8 CUs are left. */
+int tnet_affine_grad_bias_gather(const float* X, TnetMatrixDim dX, const float* E, TnetMatrixDim dE, float* G,
+                                 TnetMatrixDim dG, const float* colpart, int ldcolpart, float* gradB, float* y,
+                                 const float* x, int* labels_out, const int* labels_in, const int* copy_from,
+                                 TnetMatrixDim dy, TnetMatrixDim dx, void* stream);
 /* Element-wise SGD of the same formula on flat arrays:  c = g + mmt*corr; p += scale*c; p += l2*p;
  * corr = c (corr may be NULL when mmt == 0). */
 int tnet_sgd_update(float* p, const float* g, float* corr, long n, float scale, float mmt, float l2,

@@ -283,6 +283,26 @@ void CuBiasedLinearity::ComputeGradientColsum(const CuMatrix<BaseFloat>& colpart
                                        colpart.pCUData(), (int)colpart.Stride(), mGradB.pCUData(), S));
 }
 
+bool CuBiasedLinearity::ComputeGradientColsumGather(const CuMatrix<BaseFloat>& colpart, const BunchGather& g) {
+  CuProfileScope p("CuBiasedLinearity::ComputeGradient");
+  const CuMatrix<BaseFloat>& X = GetInput();
+  const CuMatrix<BaseFloat>& E = GetErrorInput();
+  mGradW.Init(mLinearity.Rows(), mLinearity.Cols());
+  mGradB.Init(mBias.Dim());
+  KTScope kt("gemm_grad+gather:" + std::to_string(GetNInputs()) + "x" + std::to_string(GetNOutputs()),
+             2.0 * X.Rows() * GetNInputs() * GetNOutputs());
+  const int st = tnet_affine_grad_bias_gather(X.pCUData(), X.Dim(), E.pCUData(), E.Dim(), mGradW.pCUData(),
+                                              mGradW.Dim(), colpart.pCUData(), (int)colpart.Stride(),
+                                              mGradB.pCUData(), g.y, g.x, g.labels_out, g.labels_in, g.copy_from,
+                                              g.dy, g.dx, S);
+  if (st == TNET_ERR_UNSUPPORTED) {
+    kt.Cancel();
+    return false;
+  }
+  TNET_SAFE_CALL(st);
+  return true;
+}
+
 std::vector<CuParamBlock> CuBiasedLinearity::GradientBlocks() {
   mGradW.Init(mLinearity.Rows(), mLinearity.Cols());
   mGradB.Init(mBias.Dim());

@@ -25,6 +25,9 @@ class CuBiasedLinearity : public CuUpdatableComponent {
   void ComputeGradient() override;
   // ComputeGradient with the bias gradient from the slab column sums of E (tnet_affine_grad_bias)
   void ComputeGradientColsum(const CuMatrix<BaseFloat>& colpart);
+  // ComputeGradientColsum with the next bunch's gather `g` on the CUs the GEMM's tiles leave free, in ONE
+  // launch (tnet_affine_grad_bias_gather); false: nothing enqueued (make the separate calls)
+  bool ComputeGradientColsumGather(const CuMatrix<BaseFloat>& colpart, const BunchGather& g);
   void ApplyGradient(size_t frames, void* stream = nullptr, const GradExchange* ex = nullptr) override;
   std::vector<CuParamBlock> GradientBlocks() override;
 

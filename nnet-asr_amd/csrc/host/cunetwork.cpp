@@ -467,7 +467,11 @@ void CuNetwork::TrainBunch(const CuMatrix<BaseFloat>& X, const CuVector<int>& la
       if (exchange) {
         lin->SetInput(*acts[l]);
         lin->SetErrorInput(*err);
-        if (err_colsum)
+        // the step's last gradient GEMM carries the next bunch's gather (when the trainer handed one over)
+        if (err_colsum && (stopper || l == 0) && mHasTailGather && !mTailDone &&
+            lin->ComputeGradientColsumGather(*mColPart[l], mTailGather))
+          mTailDone = true;
+        else if (err_colsum)
           lin->ComputeGradientColsum(*mColPart[l]);
         else
           lin->ComputeGradient();

@@ -39,8 +39,8 @@ void CuRecurrent::CheckChain() const {
   if (!mChainWs) return;
   int err = 0;
   TNET_SAFE_CALL(tnet_rnn_bptt_chain_error(mChainWs, &err));
-  if (err) Error("CuRecurrent: the one-launch BPTT chain timed out waiting for a hand-off (TNET_RNN_BPTT_CHAIN=0 "
-                 "runs the per-step launches)");
+  if (err) Error("CuRecurrent: the one-launch BPTT chain timed out waiting for a hand-off (unset "
+                 "TNET_RNN_BPTT_CHAIN to run the per-step launches)");
 }
 
 void CuRecurrent::ClearHistory() {
@@ -119,9 +119,12 @@ void CuRecurrent::UpdateFromDiff0(bool defer) {
   FlushPendingUpdate();
   const int nIn = (int)GetNInputs(), nOut = (int)GetNOutputs();
   // BPTT: d_i = (W[nIn:nIn+nOut] d_{i-1}) .* y_{t-i}(1 - y_{t-i}), y_{t-i} = y part of history row i-1 --
-  // all `order` steps in one launch where the shape allows (tnet_rnn_bptt_chain, bit-identical to the
-  // per-step launches; TNET_RNN_BPTT_CHAIN=0: one tnet_gemv_rows launch per step)
-  static const bool chain = !(getenv("TNET_RNN_BPTT_CHAIN") && getenv("TNET_RNN_BPTT_CHAIN")[0] == '0');
+  // one tnet_gemv_rows launch per step.  TNET_RNN_BPTT_CHAIN=1 (opt-in): all `order` steps in one launch
+  // where the shape allows (tnet_rnn_bptt_chain, bit-identical) -- MEASURED SLOWER on MI355X: 35.7 k vs
+  // 45.4 k frames/s at 135 senones, 30.4 k vs 36.6 k at 4000 (profiles/r04_rnn_chain_ab.json): each step's
+  // all-to-all granule hand-off across the 8-16 workgroups costs more than the launch boundary it removes
+  // (MI355X_MICROARCH.md's allgather / boundary rows: 2.4-4 vs 1.45 us)
+  static const bool chain = getenv("TNET_RNN_BPTT_CHAIN") && getenv("TNET_RNN_BPTT_CHAIN")[0] == '1';
   int st = TNET_ERR_UNSUPPORTED;
   if (chain && mChainWs && mBpttOrder > 0)
     st = tnet_rnn_bptt_chain(mLinearity.pCUData(), (int)mLinearity.Stride(), nIn, nOut, mDiff.pCUData(),

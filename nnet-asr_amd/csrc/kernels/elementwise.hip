@@ -8,6 +8,7 @@
 #include <float.h>
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "kcommon.h"
 
@@ -149,28 +150,45 @@ __global__ __launch_bounds__(EW_THREADS) void sgd_multi_kernel(const SgdSegs seg
   const long t0 = (long)(blockIdx.x - segs.first[k]) * blockDim.x + threadIdx.x, step = nb * blockDim.x;
   const bool v4 = ((sg.n & 3) == 0) && (((uintptr_t)sg.p | (uintptr_t)sg.g | (uintptr_t)sg.corr) & 15) == 0;
   if (v4) {
-    f32x4* p = reinterpret_cast<f32x4*>(sg.p);
+    // U vectors per thread per pass, every load of the pass issued before the first store: the launch is
+    // a few hundred fat workgroups (not one 16-B vector per thread), so beside the GEMMs of the step it
+    // takes few wave launches and issue slots for its bytes
+    constexpr int U = 4;
     const f32x4* g = reinterpret_cast<const f32x4*>(sg.g);
-    f32x4* q = reinterpret_cast<f32x4*>(sg.corr);
+    const f32x4* p = reinterpret_cast<const f32x4*>(sg.p);
+    const f32x4* q = reinterpret_cast<const f32x4*>(sg.corr);
     // parameters and momentum written through (kcommon.h st_wt): read next by the all-gather / the
     // next step's forward, from any XCD -- nothing is gained by leaving them dirty in this XCD's L2
     const bool wt = sg.n < (1L << 29);  // byte offsets of the descriptor stay below 2^31
     const __amdgpu_buffer_rsrc_t rp = tile_rsrc(sg.p), rq = tile_rsrc(q ? sg.corr : sg.p);
-    for (long i = t0; i < sg.n / 4; i += step) {
-      f32x4 c = g[i];
-      if (q) {
-        c = c + mmt * q[i];
-        if (wt) st_wt(rq, 4 * i, c);
-        else q[i] = c;
-      }
-      f32x4 w = p[i];
+    const long n4 = sg.n / 4;
+    for (long i0 = t0; i0 < n4; i0 += U * step) {
+      f32x4 c[U], w[U];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        w[e] = w[e] + scale * c[e];
-        w[e] = w[e] + sg.l2 * w[e];
+      for (int u = 0; u < U; ++u) {
+        const long i = i0 + u * step;
+        if (i < n4) {
+          c[u] = g[i];
+          w[u] = p[i];
+          if (q) c[u] = c[u] + mmt * q[i];
+        }
       }
-      if (wt) st_wt(rp, 4 * i, w);
-      else p[i] = w;
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const long i = i0 + u * step;
+        if (i >= n4) break;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          w[u][e] = w[u][e] + scale * c[u][e];
+          w[u][e] = w[u][e] + sg.l2 * w[u][e];
+        }
+        if (q) {
+          if (wt) st_wt(rq, 4 * i, c[u]);
+          else reinterpret_cast<f32x4*>(sg.corr)[i] = c[u];
+        }
+        if (wt) st_wt(rp, 4 * i, w[u]);
+        else reinterpret_cast<f32x4*>(sg.p)[i] = w[u];
+      }
     }
   } else {
     for (long i = t0; i < sg.n; i += step) {
@@ -356,9 +374,12 @@ extern "C" int tnet_sgd_update_multi(const TnetSgdSeg* segs, int nseg, float sca
       a.s[a.nseg++] = sg;
     }
     if (!a.nseg) continue;
-    // blocks proportional to the segment sizes (at least one each): one 16-B vector per thread per
-    // pass, the whole launch capped at 8192 blocks (grid-stride beyond)
-    const long want = std::min(8192L, (total / 4 + EW_THREADS - 1) / EW_THREADS);
+    // blocks proportional to the segment sizes (at least one each), the whole launch capped at
+    // TNET_SGD_BLOCKS (default 1024: 4 per CU; grid-stride beyond, 4 vectors per thread per pass).  Beside
+    // the data-parallel step's backward GEMMs: 893 k frames/s at 1024 against 882 k at 512, 881 k at 256
+    // and 876 k at 8192 (one vector per thread, the round-3 form) -- profiles/r04_dp_apply_ab.json
+    static const long cap = getenv("TNET_SGD_BLOCKS") ? std::max(1L, atol(getenv("TNET_SGD_BLOCKS"))) : 1024L;
+    const long want = std::min(cap, (total / 4 + EW_THREADS - 1) / EW_THREADS);
     for (int k = 0; k < a.nseg; ++k) {
       a.first[k] = blocks;
       blocks += (int)std::max(1L, (long)((double)want * a.s[k].n / total + 0.5));

@@ -31,6 +31,7 @@
 #include <initializer_list>
 #include <map>
 #include <mutex>
+#include <type_traits>
 
 #include "kcommon.h"
 #include "rbm_stats.h"
@@ -721,6 +722,9 @@ __device__ __forceinline__ void gemm16_body(const GemmP& p_in, float* __restrict
   }
   constexpr int NT = WM * WN * 64, NW = WM * WN;
   constexpr bool LDR = SP == 2;
+  // SP >= 3: the direct form (no LDS ring; see the main loop), DD chunks of 16 k in flight per wave
+  constexpr bool DIR = SP >= 3;
+  constexpr int DD = (SP == 3 || SP == 5) ? 4 : 8;
   static_assert(SP != 1 || S >= 3, "spread DMA needs a 3-slot ring");
   constexpr int WTM = BM / WM, WTN = BN / WN;  // wave tile
   constexpr int TM = WTM / 16, TN = WTN / 16;
@@ -960,14 +964,14 @@ __device__ __forceinline__ void gemm16_body(const GemmP& p_in, float* __restrict
   // Prologue.  early: every slot's tile is issued before the first wait (tile S-1 lands while tile 0
   // computes) -- else tile S-1 goes out only after tile 0 has landed (SP spreads it over tile 0)
   const bool early = !SP && !LDR && p.early_issue;
-  if constexpr (!LDR) {
+  if constexpr (!LDR && !DIR) {
     if (nfull > 0) {
 #pragma unroll
       for (int t = 0; t < S - 1; ++t) issue(min(t, tlast), t);
       if (early) issue(min(S - 1, tlast), S - 1);
     }
   }
-  if (nfull > 0) {
+  if (!DIR && nfull > 0) {
     if constexpr (!LDR) {
       if (early) wait_vmcnt<(S - 1) * G>();
       else wait_vmcnt<(S - 2) * G>();
@@ -1040,7 +1044,7 @@ __device__ __forceinline__ void gemm16_body(const GemmP& p_in, float* __restrict
   // exact prefetch (PX): every epilogue-operand load below is one unconditional
   // 16-B load (or one 4-B slab-sum load), npre counts this wave's, and the first seam lets them stay
   // in flight (vmcnt is in order: the npre youngest operations are exactly these loads)
-  constexpr bool PEX = !SP && !LDR && (!PRE_BIAS || NE == 4) && (TRE || !(PRE_C || PRE_AUX || PRE_Q) || NE == 4);
+  constexpr bool PEX = (!SP || DIR) && !LDR && (!PRE_BIAS || NE == 4) && (TRE || !(PRE_C || PRE_AUX || PRE_Q) || NE == 4);
   constexpr bool pex = PEX && PX;
   int npre = 0;
   if constexpr (PRE_BIAS) {
@@ -1211,6 +1215,159 @@ __device__ __forceinline__ void gemm16_body(const GemmP& p_in, float* __restrict
   // then the chunk's DMA pieces (SP: PPC of tile t+S-1; seam without SP: all G of tile t+S).
   // Left to itself the scheduler sinks every read to just before its first use and waits
   // lgkmcnt(0) there, and bunches the DMA pieces behind the barrier with the MFMA pipe idle.
+  if constexpr (DIR) {
+    // ---- the direct form: every wave loads its own fragments from global memory straight into registers
+    // (16-B buffer loads in read_frags' lane map; the two waves that share an A row block or a B column
+    // block read the same lines, L1 / L2-served), DD chunks of 16 k in a register ring: chunk c's MFMAs
+    // run while chunks c+1..c+DD-2 are in flight and the loads of chunk c+DD-1 go out between them, into
+    // the slot chunk c-1 used.  No LDS, no LDS-DMA issue cost on the MFMA waves, no seam barrier.
+    constexpr int NR = NRA + NRB;
+    const __amdgpu_buffer_rsrc_t rA = tile_rsrc(p.A), rB = tile_rsrc(p.B);
+    unsigned oA[NRA], oB[NRB];
+#pragma unroll
+    for (int r = 0; r < NRA; ++r) {
+      // rows / columns past the matrix edge read the last valid ones (their outputs are never stored)
+      if (A_KC) {
+        oA[r] = 4u * (unsigned)(min(bm + wm0 + 16 * r + li, M - 1) * p.lda + 4 * lg);
+      } else {
+        const int s2 = r % 4, q = r / 4;
+        oA[r] = 4u * (unsigned)((4 * lg + s2) * p.lda + max(min(bm + wm0 + 16 * VM * q + VM * li, M - VM), 0));
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < NRB; ++r) {
+      if (B_KC) {
+        oB[r] = 4u * (unsigned)(min(bn + wn0 + 16 * r + li, N - 1) * p.ldb + 4 * lg);
+      } else {
+        const int s2 = r % 4, q = r / 4;
+        oB[r] = 4u * (unsigned)((4 * lg + s2) * p.ldb + max(min(bn + wn0 + 16 * VN * q + VN * li, N - VN), 0));
+      }
+    }
+    const int cA = A_KC ? 64 : 64 * p.lda, cB = B_KC ? 64 : 64 * p.ldb;  // bytes per chunk
+    const int nch = nfull * KCH;
+    // SP >= 5 (a<D> configurations): the ring's loads are inline-asm buffer loads the compiler does not
+    // track, waited for by one counted vmcnt per chunk that also ties the chunk's registers (the compiler's
+    // own waits drain the whole ring at every loop back edge); 16-B loads and 6 or 8 per chunk only
+    constexpr bool ASM = SP >= 5 && (A_KC || VM == 4) && (B_KC || VN == 4) && (NR == 6 || NR == 8);
+    if constexpr (ASM) {
+      const unsigned long long ba = (unsigned long long)(uintptr_t)p.A, bb = (unsigned long long)(uintptr_t)p.B;
+      const u32x4 dA = {(unsigned)ba, (unsigned)(ba >> 32), 0x7FFFFFF0u, 0x00020000u};
+      const u32x4 dB = {(unsigned)bb, (unsigned)(bb >> 32), 0x7FFFFFF0u, 0x00020000u};
+      f32x4 ring[DD][NR];
+      auto ld = [&](int c, int r) {
+        f32x4 v;
+        if (r < NRA)
+          asm volatile("buffer_load_dwordx4 %0, %1, %2, %3 offen" : "=v"(v) : "v"(oA[r]), "s"(dA), "s"(c * cA));
+        else
+          asm volatile("buffer_load_dwordx4 %0, %1, %2, %3 offen" : "=v"(v) : "v"(oB[r - NRA]), "s"(dB), "s"(c * cB));
+        return v;
+      };
+      constexpr int WV = (DD - 2) * NR;  // loads younger than a chunk's when it is consumed
+      auto wait_slot = [&](f32x4 (&q)[NR]) {
+        if constexpr (NR == 6)
+          asm volatile("s_waitcnt vmcnt(%6)" : "+v"(q[0]), "+v"(q[1]), "+v"(q[2]), "+v"(q[3]), "+v"(q[4]), "+v"(q[5])
+                       : "n"(WV));
+        else
+          asm volatile("s_waitcnt vmcnt(%8)"
+                       : "+v"(q[0]), "+v"(q[1]), "+v"(q[2]), "+v"(q[3]), "+v"(q[4]), "+v"(q[5]), "+v"(q[6]), "+v"(q[7])
+                       : "n"(WV));
+      };
+#pragma unroll
+      for (int j = 0; j < DD - 1; ++j)
+#pragma unroll
+        for (int r = 0; r < NR; ++r) ring[j][r] = ld(min(j, nch - 1), r);
+      for (int c0 = 0; c0 < nch; c0 += DD) {
+#pragma unroll
+        for (int j = 0; j < DD; ++j) {
+          const int cn = min(c0 + j + DD - 1, nch - 1);  // past the end: a repeat of the last chunk, never used
+          __builtin_amdgcn_sched_barrier(0);  // the wait stays after the previous chunk's MFMAs
+          wait_slot(ring[j]);
+          __builtin_amdgcn_sched_barrier(0);
+          int mi = 0;
+#pragma unroll
+          for (int s2 = 0; s2 < 4; ++s2)
+#pragma unroll
+            for (int a = 0; a < TM; ++a)
+#pragma unroll
+              for (int b = 0; b < TN; ++b) {
+                const float av_ = A_KC ? ring[j][a][s2] : ring[j][(a / 4) * 4 + s2][a % 4];
+                const float bv_ = B_KC ? ring[j][NRA + b][s2] : ring[j][NRA + (b / 4) * 4 + s2][b % 4];
+                acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(av_, bv_, acc[a][b], 0, 0, 0);
+                if (mi < NR) {
+                  __builtin_amdgcn_sched_barrier(0);
+                  ring[(j + DD - 1) % DD][mi] = ld(cn, mi);
+                  __builtin_amdgcn_sched_barrier(0);
+                }
+                ++mi;
+              }
+        }
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the repeat loads of the last chunk
+    } else {
+    float fa[DD][TM][4], fb[DD][TN][4];
+    auto gld = [&](__amdgpu_buffer_rsrc_t rs, unsigned off, int soff, float (&x)[4], auto vtag) {
+      constexpr int V = decltype(vtag)::value;
+      if constexpr (V == 4) {
+        const f32x4 v = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)off, soff, 0));
+        x[0] = v[0]; x[1] = v[1]; x[2] = v[2]; x[3] = v[3];
+      } else if constexpr (V == 2) {
+        const auto v = __builtin_amdgcn_raw_buffer_load_b64(rs, (int)off, soff, 0);
+        x[0] = __uint_as_float(v[0]); x[1] = __uint_as_float(v[1]);
+      } else {
+        x[0] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, (int)off, soff, 0));
+      }
+    };
+    auto load_one = [&](int c, float (&ra)[TM][4], float (&rb)[TN][4], int r) {
+      if (r < NRA) {
+        if (A_KC) {
+          gld(rA, oA[r], c * cA, ra[r], std::integral_constant<int, 4>{});
+        } else {
+          const int s2 = r % 4, q = r / 4;
+          float x[4];
+          gld(rA, oA[r], c * cA, x, std::integral_constant<int, VM>{});
+#pragma unroll
+          for (int e = 0; e < VM; ++e) ra[VM * q + e][s2] = x[e];
+        }
+      } else {
+        const int rb_ = r - NRA;
+        if (B_KC) {
+          gld(rB, oB[rb_], c * cB, rb[rb_], std::integral_constant<int, 4>{});
+        } else {
+          const int s2 = rb_ % 4, q = rb_ / 4;
+          float x[4];
+          gld(rB, oB[rb_], c * cB, x, std::integral_constant<int, VN>{});
+#pragma unroll
+          for (int e = 0; e < VN; ++e) rb[VN * q + e][s2] = x[e];
+        }
+      }
+    };
+#pragma unroll
+    for (int j = 0; j < DD - 1; ++j)
+#pragma unroll
+      for (int r = 0; r < NR; ++r) load_one(min(j, nch - 1), fa[j], fb[j], r);
+    for (int c0 = 0; c0 < nch; c0 += DD) {
+#pragma unroll
+      for (int j = 0; j < DD; ++j) {
+        const int cn = min(c0 + j + DD - 1, nch - 1);  // past the end: a repeat of the last chunk, never used
+        int mi = 0;
+#pragma unroll
+        for (int s2 = 0; s2 < 4; ++s2)
+#pragma unroll
+          for (int a = 0; a < TM; ++a)
+#pragma unroll
+            for (int b = 0; b < TN; ++b) {
+              acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[j][a][s2], fb[j][b][s2], acc[a][b], 0, 0, 0);
+              if (mi < NR) {
+                __builtin_amdgcn_sched_barrier(0);
+                load_one(cn, fa[(j + DD - 1) % DD], fb[(j + DD - 1) % DD], mi);
+                __builtin_amdgcn_sched_barrier(0);
+              }
+              ++mi;
+            }
+      }
+    }
+    }
+  } else {
   int sl = 0;  // slot of tile t
   for (int t = 0; t < nfull; ++t) {
     const float* st = smem + sl * ST_SZ;
@@ -1280,6 +1437,7 @@ __device__ __forceinline__ void gemm16_body(const GemmP& p_in, float* __restrict
       if (SP == 1) __builtin_amdgcn_s_setprio(0);
     }
     sl = sl1;
+  }
   }
   wait_vmcnt<0>();  // repeat loads of the last tile still land in LDS
   TNET_STAMP(2);
@@ -1736,13 +1894,14 @@ void gemm16_kernel(const GemmP p_in) {
 // update writes W_l, the backward reads W_{l-1}): the blocks are dispatched in index order, so B's
 // workgroups start on the CUs A's finish on -- B's operand fill overlaps A's epilogue stores and tail
 // instead of waiting for a kernel boundary, A's end-of-kernel drain and B's start-up spread.
+// SPA: GEMM A's form (0: the LDS ring, 5: the direct form -- TNET_GEMM_DIRECT)
 template <int BMA, int BNA, bool AKA, bool BKA, int EPIA, bool PXA, int BMB, int BNB, bool AKB, bool BKB, int EPIB,
-          bool PXB>
+          bool PXB, int SPA = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
 void gemm16_pair_kernel(const GemmP pa, const GemmP pb, const int na) {
   constexpr int SA = gemm16_smem_floats<BMA, BNA, 64, 2, EPIA, PXA>(), SB = gemm16_smem_floats<BMB, BNB, 64, 2, EPIB, PXB>();
   __shared__ __attribute__((aligned(16))) float smem[SA > SB ? SA : SB];
-  if ((int)blockIdx.x < na) gemm16_body<BMA, BNA, 64, 2, 2, 2, 0, AKA, BKA, EPIA, PXA>(pa, smem, blockIdx.x);
+  if ((int)blockIdx.x < na) gemm16_body<BMA, BNA, 64, 2, 2, 2, SPA, AKA, BKA, EPIA, PXA>(pa, smem, blockIdx.x);
   else gemm16_body<BMB, BNB, 64, 2, 2, 2, 0, AKB, BKB, EPIB, PXB>(pb, smem, (int)blockIdx.x - na);
 }
 
@@ -1808,13 +1967,14 @@ __device__ __forceinline__ void bunch_gather_block(const BunchGatherP& g, const 
 // tnet_affine_update_bias_gather: the update pair kernel's tiles (nb = 0: one update) and ng gather blocks
 // after them.  Blocks are dispatched in index order, so the gather blocks take the CUs the update's tiles
 // leave free (one workgroup per CU: the ring's LDS and 1 wave per SIMD) and run beside the tiles.
-template <int BM, int BN, int BK, int WM, int WN, int S>
+// EPI_STORE_BG: the data-parallel step's last gradient GEMM (tnet_affine_grad_bias_gather), nb = 0.
+template <int BM, int BN, int BK, int WM, int WN, int S, int EPI = EPI_SGD_B>
 __global__ __launch_bounds__(WM * WN * 64) __attribute__((amdgpu_waves_per_eu(1, 1)))
 void gemm16_upd_gather_kernel(const GemmP pa, const GemmP pb, const int na, const int nb, const BunchGatherP g) {
-  __shared__ __attribute__((aligned(16))) float smem[gemm16_smem_floats<BM, BN, BK, S, EPI_SGD_B, false>()];
+  __shared__ __attribute__((aligned(16))) float smem[gemm16_smem_floats<BM, BN, BK, S, EPI, false>()];
   const int b = blockIdx.x;
-  if (b < na) gemm16_body<BM, BN, BK, WM, WN, S, 0, false, false, EPI_SGD_B, false>(pa, smem, b);
-  else if (b < na + nb) gemm16_body<BM, BN, BK, WM, WN, S, 0, false, false, EPI_SGD_B, false>(pb, smem, b - na);
+  if (b < na) gemm16_body<BM, BN, BK, WM, WN, S, 0, false, false, EPI, false>(pa, smem, b);
+  else if (b < na + nb) gemm16_body<BM, BN, BK, WM, WN, S, 0, false, false, EPI, false>(pb, smem, b - na);
   else bunch_gather_block(g, b - na - nb, (int)gridDim.x - na - nb);
 }
 
@@ -2062,7 +2222,9 @@ static unsigned* splitk_counters(size_t n, hipStream_t st) {
 // ---------------------------------------------------------------------------------------------
 // name: g<BM>x<BN>k<BK>s<S>w<waves>[i]: 32x32x2 kernel (waves laid out WMxWN; i = DMA pieces
 //       interleaved); m<BM>x<BN>k<BK>s<S>[w<WM><WN>][p|L]: 16x16x4 kernel (default 2x2 waves; p = DMA
-//       pieces spread over the chunks + MFMA at setprio 1; L = one extra loader wave issues all DMA)
+//       pieces spread over the chunks + MFMA at setprio 1; L = one extra loader wave issues all DMA);
+//       m<BM>x<BN>d<D>: the 16x16x4 kernel's direct form (fragments loaded from global memory into a
+//       D-chunk register ring, no LDS ring)
 #define TNET_GEMM_CFGS(X)                         \
   X(g64x64k32s4w4, 0, 64, 64, 32, 2, 2, 4, 0)           \
   X(m64x128k32s4, 1, 64, 128, 32, 2, 2, 4, 0)           \
@@ -2074,6 +2236,12 @@ static unsigned* splitk_counters(size_t n, hipStream_t st) {
   X(m64x128k64s2w42, 1, 64, 128, 64, 4, 2, 2, 0)        \
   X(m64x128k64s3p, 1, 64, 128, 64, 2, 2, 3, 1)          \
   X(m64x128k64s2L, 1, 64, 128, 64, 2, 2, 2, 2)          \
+  X(m64x128d4, 1, 64, 128, 64, 2, 2, 2, 3)              \
+  X(m64x128d8, 1, 64, 128, 64, 2, 2, 2, 4)              \
+  X(m128x128d4, 1, 128, 128, 64, 2, 2, 2, 3)            \
+  X(m64x128a4, 1, 64, 128, 64, 2, 2, 2, 5)              \
+  X(m64x128a8, 1, 64, 128, 64, 2, 2, 2, 6)              \
+  X(m128x128a4, 1, 128, 128, 64, 2, 2, 2, 5)            \
   X(m128x256k32s3, 1, 128, 256, 32, 2, 2, 3, 0)         \
   X(m64x64k64s2, 1, 64, 64, 64, 2, 2, 2, 0)             \
   X(m64x64k32s4, 1, 64, 64, 32, 2, 2, 4, 0)             \
@@ -2107,6 +2275,10 @@ static int g_pre0 = 1;  // TNET_GEMM_PRE0=0: the first seam also waits for the e
 // the 64x128 backward / forward and the 128x128 gradient then run as stream-K over CUs - R workgroups
 // (gemm16_sk_kernel).  0: the plain tile grid.
 static int g_reserve = 0, g_cus = 0;
+// TNET_GEMM_DIRECT: the planner's m64x128k64s2 / m128x128k64s2 choices with an n-contiguous B (the forward
+// and update GEMMs; the backward's k-contiguous B reads 64-B row pieces, slower direct) run in the direct form
+// -- 1: m64x128a8 / m128x128a4 (also the update half of the update + backward pair kernel), 0: the LDS ring
+static int g_direct = -1;
 static int g_wt = 1;  // TNET_GEMM_WT=0: plain 16-B epilogue stores instead of write-through (sc1; measured +1.4 % frames/s)
 static int forced_cfg() {
   if (g_cfg == -2) {
@@ -2129,6 +2301,8 @@ static int forced_cfg() {
     if (wt) g_wt = atoi(wt);
     const char* il = getenv("TNET_SPLITK_INLAUNCH");
     if (il) g_inlaunch = atoi(il);
+    const char* dr = getenv("TNET_GEMM_DIRECT");
+    g_direct = dr ? atoi(dr) : 0;
 
   }
   return g_cfg;
@@ -2167,12 +2341,23 @@ static bool launch_cfg(const GemmP& p, hipStream_t st) {
     // the exact-prefetch instantiation (PX) only for the training step's large-layer kernels: the
     // hidden forward (64x128 NN + bias + sigmoid), backward (64x128 NT + diff-sigmoid + slab sums)
     // and update (128x128 TN + SGD / the data-parallel gradient)
-    constexpr bool PXK = IL == 0 && BK == 64 && S == 2 &&
+    constexpr bool PXK = (IL == 0 || IL >= 3) && BK == 64 && S == 2 &&
                          ((BM == 64 && BN == 128 && A_KC && !B_KC && EPI == EPI_BIAS_SIG) ||
                           (BM == 64 && BN == 128 && A_KC && B_KC && EPI == EPI_DSIG_CS) ||
                           (BM == 128 && BN == 128 && !A_KC && !B_KC &&
                            (EPI == EPI_SGD_B || EPI == EPI_SGD || EPI == EPI_STORE_BG)));
     const bool exact = px_exact<BM, BN, EPI>(p);
+    if constexpr (IL >= 3) {
+      // the direct form loads 16-B fragments (clamped at the M / N edges) over the full k-tiles: 16-B
+      // aligned operands, at least one full k-tile (DD = 8: an even count); otherwise the ring form
+      const int nfull = p.K / BK;
+      auto a16p = [](const void* v) { return ((uintptr_t)v & 15) == 0; };
+      // (an m / n-contiguous operand's 16-B vectors are either wholly inside or wholly past the edge:
+      // M / N a multiple of 4 there)
+      if (p.ksplit > 1 || nfull < 1 || (!A_KC && p.M % 4) || (!B_KC && p.N % 4) || ((IL == 4 || IL == 6) && nfull % 2) || (p.lda & 3) || (p.ldb & 3) || !a16p(p.A) ||
+          !a16p(p.B) || 4 * extA >= (1L << 31) || 4 * extB >= (1L << 31))
+        return launch_cfg<KIND, BM, BN, BK, WM, WN, S, 0, A_KC, B_KC, EPI>(p, st);
+    }
     if constexpr (PXK) {
       if (exact) {
         gemm16_kernel<BM, BN, BK, WM, WN, S, IL, A_KC, B_KC, EPI, true><<<grid, WM * WN * 64, 0, st>>>(q);
@@ -2444,8 +2629,13 @@ static int launch_gemm(const GemmP& p_in, hipStream_t st) {
     TNET_LAUNCH_CHECK();
     return TNET_OK;
   }
+  int rcfg = cfg;
+  if (g_direct > 0 && forced_cfg() < 0 && !B_KC) {
+    if (cfg == CFG_m64x128k64s2) rcfg = CFG_m64x128a8;
+    else if (cfg == CFG_m128x128k64s2) rcfg = CFG_m128x128a4;
+  }
   bool ok = false;
-  switch (cfg) {
+  switch (rcfg) {
 #define X(name, KIND, BM, BN, BK, WM, WN, S, IL) \
   case CFG_##name: ok = launch_cfg<KIND, BM, BN, BK, WM, WN, S, IL, A_KC, B_KC, EPI>(p, st); break;
     TNET_GEMM_CFGS(X)
@@ -2478,7 +2668,18 @@ static int launch_pair_upd_bwd(GemmP pu, GemmP pb, hipStream_t st) {
     return TNET_ERR_UNSUPPORTED;
   if (!px_exact<64, 128, EPI_DSIG_CS>(pb)) return TNET_ERR_UNSUPPORTED;
   const int na = cdiv(pu.M, 128) * cdiv(pu.N, 128), nb = cdiv(pb.M, 64) * cdiv(pb.N, 128);
-  if (px_exact<128, 128, EPI_SGD_B>(pu))
+  // the update half in the direct form (launch_cfg's direct-form conditions)
+  auto a16p = [](const void* v) { return ((uintptr_t)v & 15) == 0; };
+  const bool dir = g_direct > 0 && pu.K / 64 >= 1 && !(pu.lda & 3) && !(pu.ldb & 3) && a16p(pu.A) && a16p(pu.B) &&
+                   4 * ((long)pu.K * pu.lda) < (1L << 31) && 4 * ((long)pu.K * pu.ldb) < (1L << 31);
+  const bool px = px_exact<128, 128, EPI_SGD_B>(pu);
+  if (dir && px)
+    gemm16_pair_kernel<128, 128, false, false, EPI_SGD_B, true, 64, 128, true, true, EPI_DSIG_CS, true, 5>
+        <<<na + nb, 256, 0, st>>>(pu, pb, na);
+  else if (dir)
+    gemm16_pair_kernel<128, 128, false, false, EPI_SGD_B, false, 64, 128, true, true, EPI_DSIG_CS, true, 5>
+        <<<na + nb, 256, 0, st>>>(pu, pb, na);
+  else if (px)
     gemm16_pair_kernel<128, 128, false, false, EPI_SGD_B, true, 64, 128, true, true, EPI_DSIG_CS, true>
         <<<na + nb, 256, 0, st>>>(pu, pb, na);
   else
@@ -3061,6 +3262,57 @@ extern "C" int tnet_affine_grad_bias(const float* X, TnetMatrixDim dX, const flo
   if (st) return st;
   if (p.M <= 0 || p.N <= 0) return TNET_OK;
   return launch_gemm<false, false, EPI_STORE_BG>(p, (hipStream_t)stream);
+}
+
+extern "C" int tnet_affine_grad_bias_gather(const float* X, TnetMatrixDim dX, const float* E, TnetMatrixDim dE,
+                                            float* G, TnetMatrixDim dG, const float* colpart, int ldcolpart,
+                                            float* gradB, float* y, const float* x, int* labels_out,
+                                            const int* labels_in, const int* copy_from, TnetMatrixDim dy,
+                                            TnetMatrixDim dx, void* stream) {
+  // tnet_affine_grad_bias and tnet_gather_bunch in one launch (the data-parallel step's last gradient GEMM
+  // with the next bunch's gather on the CUs its tiles leave free: tnet_affine_update_bias_gather's form)
+  if (dX.rows != dE.rows || dG.rows != dX.cols || dG.cols != dE.cols || !colpart || !gradB || ldcolpart < dE.cols)
+    return TNET_ERR_ARG;
+  GemmP p{};
+  p.M = dX.cols; p.N = dE.cols; p.K = dX.rows;
+  p.A = X; p.lda = dX.stride; p.B = E; p.ldb = dE.stride; p.C = G; p.ldc = dG.stride;
+  p.alpha = 1.f; p.beta = 0.f;
+  p.bpart = colpart; p.ldbpart = ldcolpart; p.bslabs = tnet_colsum_slabs(dE.rows);
+  p.bvec = gradB;
+  int st = check_common(p);
+  if (st) return st;
+  if (!y || !x || !labels_out || !labels_in || !copy_from || dy.cols != dx.cols || dy.rows < 0 || dy.stride < dy.cols ||
+      dx.stride < dx.cols)
+    return TNET_ERR_ARG;
+  // the gather independent of the GEMM: it reads X, E and the slab sums, writes G and gradB
+  if (!gather_independent(y, x, labels_out, labels_in, copy_from, dy, dx,
+                          {span_of(p.A, p.K, p.lda, 4), span_of(p.B, p.K, p.ldb, 4), span_of(p.bpart, p.bslabs, p.ldbpart, 4)},
+                          {span_of(p.C, p.M, p.ldc, 4), span_of(p.bvec, p.N, 1, 4)}))
+    return TNET_ERR_ARG;
+  const int c4 = (dy.cols + 3) & ~3;
+  if (((uintptr_t)y & 15) || ((uintptr_t)x & 15) || (dy.stride & 3) || (dx.stride & 3) || c4 > dy.stride ||
+      c4 > dx.stride)
+    return TNET_ERR_UNSUPPORTED;
+  if (forced_cfg() >= 0 || split2_on() || g_split > 0) return TNET_ERR_UNSUPPORTED;
+  if (p.M <= 0 || p.N <= 0) return TNET_ERR_UNSUPPORTED;
+  // what tnet_affine_grad_bias runs alone: the 64x64 configuration, unsplit
+  const GemmPlan pl = plan_gemm<false>(p, epi_splittable(EPI_STORE_BG));
+  if (pl.cfg != CFG_m64x64k32s4w41 || pl.ks != 1) return TNET_ERR_UNSUPPORTED;
+  const int na = cdiv(p.M, 64) * cdiv(p.N, 64);
+  if (4 * (32L * p.lda + p.M) >= (1L << 32) || 4 * (32L * p.ldb + p.N) >= (1L << 32)) return TNET_ERR_UNSUPPORTED;
+  const int cus = cu_count();
+  if (cus <= 0) return TNET_ERR_UNSUPPORTED;
+  const int spare = cus - g_reserve - na;
+  if (spare < 8) return TNET_ERR_UNSUPPORTED;
+  const int ng = spare < 64 ? spare : 64;
+  p.group = g_group > 0 ? g_group : 8;
+  p.early_issue = g_early;
+  p.wt = g_wt;
+  BunchGatherP g{y, x, labels_out, labels_in, copy_from, dy.rows, c4, dy.stride, dx.stride};
+  GemmP pb{};
+  gemm16_upd_gather_kernel<64, 64, 32, 4, 1, 4, EPI_STORE_BG><<<na + ng, 256, 0, (hipStream_t)stream>>>(p, pb, na, 0, g);
+  TNET_LAUNCH_CHECK();
+  return TNET_OK;
 }
 
 extern "C" int tnet_affine_grad(const float* X, TnetMatrixDim dX, const float* E, TnetMatrixDim dE, float* G,

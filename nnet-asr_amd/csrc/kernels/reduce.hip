@@ -681,8 +681,11 @@ extern "C" int tnet_softmax_xent(const float* Z, TnetMatrixDim dZ, const int* la
   // when Z == NULL, Y already holds the softmax output (read through strideY)
   TnetMatrixDim dd = dZ;
   if (!Z) dd.stride = strideY;
-  // TNET_SOFTMAX_ROWS=1|2|4: rows per block of the wide-row kernel (1: softmax_xent_row4_kernel)
-  static const int rows_pb = getenv("TNET_SOFTMAX_ROWS") ? atoi(getenv("TNET_SOFTMAX_ROWS")) : 2;
+  // TNET_SOFTMAX_ROWS=1|2|4: rows per block of the wide-row kernel (1, the default: softmax_xent_row4_kernel;
+  // 2 / 4: softmax_xent_rows_kernel -- MEASURED SLOWER in the dnn4 step, 9.0-9.2 us for one row a block
+  // against 9.8-9.9 for two and 11.8 for four, profiles/r04_softmax_rows_ab.json: half / a quarter of the
+  // workgroups, each row's chain no shorter)
+  static const int rows_pb = getenv("TNET_SOFTMAX_ROWS") ? atoi(getenv("TNET_SOFTMAX_ROWS")) : 1;
   const bool wide = Z && v4 && dZ.cols > 1024 && dZ.cols <= SX_MAXV4 * 256;
   if (wide && E && (rows_pb == 2 || rows_pb == 4)) {
     auto launch = [&](auto kern, int R) {

@@ -114,6 +114,19 @@ def test_gather_ride_refuses_dependent_operands():
         assert upd(y, x, lo, bad, cf) == -1
         assert upd(y, x, lo, li, bad) == -1
 
+    G, gb = W, b  # the data-parallel form: the gradient and the bias gradient are what the GEMM writes
+
+    def grad(y_, x_, lo_, li_, cf_):
+        return L.tnet_affine_grad_bias_gather(X, dX, E, dE, G, dW, P, n_out, gb, y_, x_, lo_, li_, cf_, dy, dx, None)
+    assert grad(y, x, lo, li, cf) != -1
+    for bad in (X, E, G, P, gb):
+        assert grad(bad, x, lo, li, cf) == -1
+        assert grad(y, x, bad, li, cf) == -1
+    for bad in (G, gb):
+        assert grad(y, bad, lo, li, cf) == -1
+        assert grad(y, x, lo, bad, cf) == -1
+        assert grad(y, x, lo, li, bad) == -1
+
     V, H, vb, cvb, hb, chb, ms = (_fake(base, k) for k in range(12, 19))
     B, nv, nh = 64, 40, 256
     dV, dH, dWr = MatrixDim(2 * B, nv, nv), MatrixDim(2 * B, nh, nh), MatrixDim(nv, nh, nh)

@@ -38,6 +38,9 @@ def gemm_ref(ta, tb, A, B):
 GEMM_CFGS = ["auto", "g64x64k32s4w4", "m64x128k32s4", "m64x128k64s3", "m64x64k32s4w41", "m128x128k32s3",
              "m128x128k64s2", "m64x128k64s2", "m64x128k64s2w42", "m64x128k64s3p", "m64x128k64s2L", "m128x256k32s3",
              "m64x64k64s2", "m64x64k32s4", "m32x64k64s2",
+             # the direct form (fragments loaded into a register ring, no LDS ring; exact shapes only,
+             # the ring form otherwise)
+             "m64x128d4", "m64x128d8", "m128x128d4", "m64x128a4", "m64x128a8", "m128x128a4",
              # split-K (K cut into slices + an in-order combine with the epilogue); counts that do not
              # divide K fall back to fewer slices
              "auto+sk4", "m64x64k32s4w41+sk8", "m32x64k64s2+sk2", "m64x128k64s2+sk3",
@@ -139,6 +142,40 @@ def test_affine_update(mmt, rows, n_in, n_out, gemm_cfg):
     assert np.all(np.abs(dW.numpy() - w) <= tol)
     if mmt:
         assert np.all(np.abs(dC.numpy() - c) <= 2e-5 * mag + 1e-6)
+
+
+@pytest.mark.parametrize("direct,ring", [("m64x128d4", "m64x128k64s2"), ("m64x128a4", "m64x128k64s2"),
+                                         ("m64x128a8", "m64x128k64s2"), ("m128x128d4", "m128x128k64s2"),
+                                         ("m128x128a4", "m128x128k64s2")])
+@pytest.mark.parametrize("kind,rows,n_in,n_out", [("fwd", 1024, 2048, 2048), ("bwd", 1024, 2048, 2048),
+                                                  ("upd", 1024, 2048, 2048), ("upd", 1024, 2048, 4096)])
+def test_direct_form_bit_identical_to_ring(direct, ring, kind, rows, n_in, n_out):
+    """the GEMM's direct form (each wave loads its MFMA fragments from global memory into a register ring) runs
+    the ring form's MFMA sequence on the same operand values in the same order: the outputs bit for bit"""
+    X, E = rnd((rows, n_in), 60), rnd((rows, n_out), 61, 0.01)
+    W, b = rnd((n_in, n_out), 62, 0.1), rnd(n_out, 63)
+    Yb = 1 / (1 + np.exp(-rnd((rows, n_in), 64)))
+    out = []
+    for cfg in (direct, ring):
+        check(lib().tnet_gemm_config(cfg.encode()))
+        try:
+            dX, dE, dW, db, dY = (DeviceArray.from_numpy(X), DeviceArray.from_numpy(E), DeviceArray.from_numpy(W),
+                                  DeviceArray.vector(b), DeviceArray.from_numpy(Yb))
+            if kind == "fwd":
+                dO = DeviceArray(rows, n_out)
+                check(lib().tnet_affine_fwd(dX.ptr, dX.dim, dW.ptr, dW.dim, db.ptr, dO.ptr, dO.dim, 1, S()))
+                out.append(dO.numpy())
+            elif kind == "bwd":
+                dO = DeviceArray(rows, n_in)
+                check(lib().tnet_affine_bwd(dE.ptr, dE.dim, dW.ptr, dW.dim, dY.ptr, dY.stride, dO.ptr, dO.dim, 1, S()))
+                out.append(dO.numpy())
+            else:
+                check(lib().tnet_affine_update(dX.ptr, dX.dim, dE.ptr, dE.dim, dW.ptr, dW.dim, None, 0, -0.3 / rows, 0.0,
+                                               -1e-4, S()))
+                out.append(dW.numpy())
+        finally:
+            check(lib().tnet_gemm_config(b"auto+il0"))
+    np.testing.assert_array_equal(out[0], out[1])
 
 
 def slab_sums(M, slab=32):
@@ -739,6 +776,47 @@ def test_affine_update_bias_gather_matches_separate_calls(mmt, rows, sides, gcol
     np.testing.assert_array_equal(yb, Xc[perm])
     np.testing.assert_array_equal(la, labc[perm])
     np.testing.assert_array_equal(lb, labc[perm])
+
+
+@pytest.mark.parametrize("rows,n_in,n_out,gcols", [(1024, 440, 2048, 440), (1024, 598, 1024, 598), (256, 440, 256, 440),
+                                                  (1024, 2048, 2048, 440)])
+def test_affine_grad_bias_gather_matches_separate_calls(rows, n_in, n_out, gcols):
+    """tnet_affine_grad_bias_gather (the data-parallel step's last gradient GEMM + the next bunch's gather in ONE
+    launch) against tnet_affine_grad_bias followed by tnet_gather_bunch: G and the bias gradient bit-identical, the
+    gathered rows and class ids exact; TNET_ERR_UNSUPPORTED where the GEMM alone runs another tile configuration"""
+    cache_rows = 3000
+    Xc = rnd((cache_rows, gcols), 500)
+    labc = (np.arange(cache_rows, dtype=np.int32) * 7) % 4000
+    perm = np.random.default_rng(501).permutation(cache_rows).astype(np.int32)[:1024]
+    X, E = rnd((rows, n_in), 510), rnd((rows, n_out), 520, 0.01)
+    P = slab_sums(E).astype(np.float32)
+    dX, dE, dP = DeviceArray.from_numpy(X), DeviceArray.from_numpy(E), DeviceArray.from_numpy(P)
+    results = []
+    for fused in (True, False):
+        dG = DeviceArray.from_numpy(np.full((n_in, n_out), np.nan, np.float32))
+        dgb = DeviceArray.vector(np.full(n_out, np.nan, np.float32))
+        dXc, dLc, dPerm = DeviceArray.from_numpy(Xc), DeviceArray.vector(labc), DeviceArray.vector(perm)
+        dY = DeviceArray.from_numpy(np.full((1024, gcols), np.nan, np.float32))
+        dLo = DeviceArray.vector(np.full(1024, -7, np.int32))
+        gargs = [dY.ptr, dXc.ptr, dLo.ptr, dLc.ptr, dPerm.ptr, dY.dim, dXc.dim]
+        args = [dX.ptr, dX.dim, dE.ptr, dE.dim, dG.ptr, dG.dim, dP.ptr, dP.stride, dgb.ptr]
+        if fused:
+            st = lib().tnet_affine_grad_bias_gather(*args, *gargs, S())
+            if n_in == 2048:
+                assert st == TNET_ERR_UNSUPPORTED
+                return
+            check(st)
+        else:
+            check(lib().tnet_affine_grad_bias(*args, S()))
+            check(lib().tnet_gather_bunch(*gargs, S()))
+        results.append((dG.numpy(), dgb.numpy(), dY.numpy(), dLo.numpy()[:, 0]))
+    (ga, ba, ya, la), (gb_, bb, yb, lb) = results
+    np.testing.assert_array_equal(ga, gb_)
+    np.testing.assert_array_equal(ba, bb)
+    np.testing.assert_allclose(ga, X.astype(np.float64).T @ E.astype(np.float64), rtol=1e-4, atol=1e-5)
+    for y_, l_ in ((ya, la), (yb, lb)):
+        np.testing.assert_array_equal(y_, Xc[perm])
+        np.testing.assert_array_equal(l_, labc[perm])
 
 
 @pytest.mark.parametrize("rows,n_in,n_out", [(1024, 2048, 4000), (1024, 2048, 2048), (256, 512, 1000), (64, 128, 4000)])

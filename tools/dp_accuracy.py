@@ -107,7 +107,10 @@ def worker(a):
 
     def cv_eval():
         cobj = Objective()
-        cv = Trainer(net, cobj, bunchsize=a.bunch, cachesize=a.cache, seed=0, randomize=False, crossval=True)
+        # the held-out set in bunches of --cv-bunch (default: the training bunch): a fixed value keeps the
+        # evaluated frames the same for every world size (the cache drops the tail short of a bunch)
+        cv = Trainer(net, cobj, bunchsize=a.cv_bunch or a.bunch, cachesize=a.cache, seed=0, randomize=False,
+                     crossval=True)
         if transform is not None:
             cv.set_transform(transform, 25, 25)
         cv.train_corpus([x for x, _ in held], [y for _, y in held])
@@ -195,6 +198,7 @@ def main():
     ap.add_argument("--epochs", type=int, default=4)
     ap.add_argument("--utts", type=int, default=800)
     ap.add_argument("--cv-utts", type=int, default=40)
+    ap.add_argument("--cv-bunch", type=int, default=0, help="held-out bunch size (0: --bunch)")
     ap.add_argument("--bunch", type=int, default=1024)
     ap.add_argument("--cache", type=int, default=16384)
     ap.add_argument("--lr", type=float, default=1.0)
@@ -221,7 +225,8 @@ def main():
                 str(a.utts), "--cv-utts", str(a.cv_utts), "--bunch", str(a.bunch), "--cache", str(a.cache), "--lr",
                 str(a.lr), "--scale", a.scale, "--end-halving-inc", str(a.end_halving_inc),
                 "--start-halving-inc", str(a.start_halving_inc), "--warmup", str(a.warmup),
-                "--progress", a.progress, "--corpus", a.corpus, "--seed", str(a.seed)]
+                "--progress", a.progress, "--corpus", a.corpus, "--seed", str(a.seed),
+                "--cv-bunch", str(a.cv_bunch)]
         if a.newbob:
             args.append("--newbob")
         procs = [subprocess.Popen(args, env=dict(env, RANK=str(r)), stdout=subprocess.PIPE, stderr=subprocess.PIPE,
