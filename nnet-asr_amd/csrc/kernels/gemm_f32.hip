@@ -2276,8 +2276,11 @@ static int g_pre0 = 1;  // TNET_GEMM_PRE0=0: the first seam also waits for the e
 // (gemm16_sk_kernel).  0: the plain tile grid.
 static int g_reserve = 0, g_cus = 0;
 // TNET_GEMM_DIRECT: the planner's m64x128k64s2 / m128x128k64s2 choices with an n-contiguous B (the forward
-// and update GEMMs; the backward's k-contiguous B reads 64-B row pieces, slower direct) run in the direct form
-// -- 1: m64x128a8 / m128x128a4 (also the update half of the update + backward pair kernel), 0: the LDS ring
+// and update GEMMs; the backward's k-contiguous B reads 64-B row pieces, slower direct: 99 vs 78 us) run in
+// the direct form -- 1 (default): m64x128a8 / m128x128a4, also the update half of the update + backward pair
+// kernel (dnn4 969.9 k -> 1006.2 k frames/s, the 2048^2 set 69.1 -> 65.6 us a launch, roofline 0.790 ->
+// 0.832, profiles/r04_gemm_direct_ab.json); 2: m64x128d4 / m128x128d4 (compiler-tracked loads); 3:
+// m64x128a4 / m128x128a4; 0: the LDS ring everywhere
 static int g_direct = -1;
 static int g_wt = 1;  // TNET_GEMM_WT=0: plain 16-B epilogue stores instead of write-through (sc1; measured +1.4 % frames/s)
 static int forced_cfg() {
@@ -2302,7 +2305,7 @@ static int forced_cfg() {
     const char* il = getenv("TNET_SPLITK_INLAUNCH");
     if (il) g_inlaunch = atoi(il);
     const char* dr = getenv("TNET_GEMM_DIRECT");
-    g_direct = dr ? atoi(dr) : 0;
+    g_direct = dr ? atoi(dr) : 1;
 
   }
   return g_cfg;
@@ -2631,8 +2634,8 @@ static int launch_gemm(const GemmP& p_in, hipStream_t st) {
   }
   int rcfg = cfg;
   if (g_direct > 0 && forced_cfg() < 0 && !B_KC) {
-    if (cfg == CFG_m64x128k64s2) rcfg = CFG_m64x128a8;
-    else if (cfg == CFG_m128x128k64s2) rcfg = CFG_m128x128a4;
+    if (cfg == CFG_m64x128k64s2) rcfg = g_direct == 2 ? CFG_m64x128d4 : g_direct == 3 ? CFG_m64x128a4 : CFG_m64x128a8;
+    else if (cfg == CFG_m128x128k64s2) rcfg = g_direct == 2 ? CFG_m128x128d4 : CFG_m128x128a4;
   }
   bool ok = false;
   switch (rcfg) {
@@ -2673,7 +2676,10 @@ static int launch_pair_upd_bwd(GemmP pu, GemmP pb, hipStream_t st) {
   const bool dir = g_direct > 0 && pu.K / 64 >= 1 && !(pu.lda & 3) && !(pu.ldb & 3) && a16p(pu.A) && a16p(pu.B) &&
                    4 * ((long)pu.K * pu.lda) < (1L << 31) && 4 * ((long)pu.K * pu.ldb) < (1L << 31);
   const bool px = px_exact<128, 128, EPI_SGD_B>(pu);
-  if (dir && px)
+  if (dir && px && g_direct == 2)
+    gemm16_pair_kernel<128, 128, false, false, EPI_SGD_B, true, 64, 128, true, true, EPI_DSIG_CS, true, 3>
+        <<<na + nb, 256, 0, st>>>(pu, pb, na);
+  else if (dir && px)
     gemm16_pair_kernel<128, 128, false, false, EPI_SGD_B, true, 64, 128, true, true, EPI_DSIG_CS, true, 5>
         <<<na + nb, 256, 0, st>>>(pu, pb, na);
   else if (dir)
