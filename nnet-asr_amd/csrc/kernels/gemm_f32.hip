@@ -1833,7 +1833,8 @@ __device__ __forceinline__ void gemm16_body(const GemmP& p_in, float* __restrict
 // tiles and at most a piece at either end, and a split tile has exactly two pieces; they combine through
 // gemm16_body's stream-K fixup and the second to finish runs the tile's own epilogue.  Static and
 // deterministic: no claims, no queues.
-template <int BM, int BN, int BK, int WM, int WN, int S, bool A_KC, bool B_KC, int EPI>
+// SPK: the pieces' form (0: the LDS ring, 5: the direct form -- TNET_GEMM_DIRECT, n-contiguous B only)
+template <int BM, int BN, int BK, int WM, int WN, int S, bool A_KC, bool B_KC, int EPI, int SPK = 0>
 __global__ __launch_bounds__(WM * WN * 64)
 __attribute__((amdgpu_waves_per_eu((WM * WN + 3) / 4, (WM * WN + 3) / 4)))
 void gemm16_sk_kernel(const GemmP p, const int G) {
@@ -1855,7 +1856,7 @@ void gemm16_sk_kernel(const GemmP p, const int G) {
     q.A = p.A + (A_KC ? kk : kk * p.lda);
     q.B = p.B + (B_KC ? kk : kk * p.ldb);
     q.K = (int)((k1 - k0) * BK);
-    gemm16_body<BM, BN, BK, WM, WN, S, 0, A_KC, B_KC, kEpiStreamK + EPI, true>(q, smem, t);
+    gemm16_body<BM, BN, BK, WM, WN, S, SPK, A_KC, B_KC, kEpiStreamK + EPI, true>(q, smem, t);
     k0 = k1;
   }
 }
@@ -2357,8 +2358,10 @@ static bool launch_cfg(const GemmP& p, hipStream_t st) {
       auto a16p = [](const void* v) { return ((uintptr_t)v & 15) == 0; };
       // (an m / n-contiguous operand's 16-B vectors are either wholly inside or wholly past the edge:
       // M / N a multiple of 4 there)
-      if (p.ksplit > 1 || nfull < 1 || (!A_KC && p.M % 4) || (!B_KC && p.N % 4) || ((IL == 4 || IL == 6) && nfull % 2) || (p.lda & 3) || (p.ldb & 3) || !a16p(p.A) ||
-          !a16p(p.B) || 4 * extA >= (1L << 31) || 4 * extB >= (1L << 31))
+      if (p.ksplit > 1 || nfull < 1 || (!A_KC && p.M % 4) || (!B_KC && p.N % 4) || ((IL == 4 || IL == 6) && nfull % 2) ||
+          (p.lda & 3) || (p.ldb & 3) || !a16p(p.A) ||
+          !a16p(p.B) || 4 * (A_KC ? (long)p.M * p.lda : (long)p.K * p.lda) >= (1L << 31) ||
+          4 * (B_KC ? (long)p.N * p.ldb : (long)p.K * p.ldb) >= (1L << 31))
         return launch_cfg<KIND, BM, BN, BK, WM, WN, S, 0, A_KC, B_KC, EPI>(p, st);
     }
     if constexpr (PXK) {
@@ -2416,6 +2419,18 @@ static bool launch_sk(const GemmP& p, hipStream_t st) {
     q.wt = g_wt;
     q.skws = ws;
     q.tile_cnt = cnt;
+    // the pieces in the direct form where the plain grid would run it (n-contiguous B, aligned operands)
+    auto a16p = [](const void* v) { return ((uintptr_t)v & 15) == 0; };
+    const bool dir = g_direct > 0 && !B_KC && !(p.lda & 3) && !(p.ldb & 3) && a16p(p.A) && a16p(p.B) &&
+                     (A_KC || p.M % 4 == 0) && p.N % 4 == 0 &&
+                     4 * (A_KC ? (long)p.M * p.lda : (long)p.K * p.lda) < (1L << 31) &&
+                     4 * (B_KC ? (long)p.N * p.ldb : (long)p.K * p.ldb) < (1L << 31);
+    if constexpr (!B_KC) {
+      if (dir) {
+        gemm16_sk_kernel<BM, BN, 64, 2, 2, 2, A_KC, B_KC, EPI, 5><<<(unsigned)G, 256, 0, st>>>(q, G);
+        return true;
+      }
+    }
     gemm16_sk_kernel<BM, BN, 64, 2, 2, 2, A_KC, B_KC, EPI><<<(unsigned)G, 256, 0, st>>>(q, G);
     return true;
   }
@@ -2674,6 +2689,7 @@ static int launch_pair_upd_bwd(GemmP pu, GemmP pb, hipStream_t st) {
   // the update half in the direct form (launch_cfg's direct-form conditions)
   auto a16p = [](const void* v) { return ((uintptr_t)v & 15) == 0; };
   const bool dir = g_direct > 0 && pu.K / 64 >= 1 && !(pu.lda & 3) && !(pu.ldb & 3) && a16p(pu.A) && a16p(pu.B) &&
+                   pu.M % 4 == 0 && pu.N % 4 == 0 &&
                    4 * ((long)pu.K * pu.lda) < (1L << 31) && 4 * ((long)pu.K * pu.ldb) < (1L << 31);
   const bool px = px_exact<128, 128, EPI_SGD_B>(pu);
   if (dir && px && g_direct == 2)
