@@ -6,6 +6,9 @@ mkdir -p $O
 timeout -k 10 600 python3 -u -m pytest -x -q -rf --timeout 400 --timeout-method thread tests/test_gpu_steal.py tests/test_gpu_dp.py > $O/tests.txt 2>&1 &&
 timeout -k 10 120 ./tools/cohab_probe steal 16 > $O/cohab_steal16.txt 2>&1 &&
 bash tools/profile_round.sh > $O/profile_round.log 2>&1 &&
+timeout -k 10 300 python3 bench.py --steps 20 --warmup 5 --force-dp --no-cpu-baseline > $O/bench_fdp.json 2> $O/bench_fdp.err &&
+timeout -k 10 300 python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline > $O/bench_fused.json 2> $O/bench_fused.err &&
+timeout -k 10 300 python3 bench.py --steps 20 --warmup 5 --force-dp --no-cpu-baseline > $O/bench_fdp2.json 2> $O/bench_fdp2.err &&
 timeout -k 10 300 python3 bench.py --config mlp3 --force-dp --steps 200 --warmup 50 --no-cpu-baseline > $O/bench_mlp3_fdp.json 2> $O/bench_mlp3_fdp.err &&
 timeout -k 10 300 python3 bench.py --config mlp3 --steps 200 --warmup 50 --no-cpu-baseline > $O/bench_mlp3.json 2> $O/bench_mlp3.err &&
 timeout -k 10 300 python3 bench.py --config dnn5 --steps 20 --warmup 5 --no-cpu-baseline > $O/bench_dnn5.json 2> $O/bench_dnn5.err &&

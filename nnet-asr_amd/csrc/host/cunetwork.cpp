@@ -478,7 +478,9 @@ void CuNetwork::TrainBunch(const CuMatrix<BaseFloat>& X, const CuVector<int>& la
         exchange->Submit(*lin);
         // the layer's SGD update right behind its reduction, beside the backward GEMMs below (W_l is
         // read for the last time by this layer's backward GEMM, already enqueued)
-        void* as = submitted.empty() ? exchange->ApplyStream(n_submitted) : nullptr;
+        // (the step's last layer applies on the compute stream right behind its reduction: nothing is left
+        // to overlap it with, and the apply stream would add a hop in and a join out)
+        void* as = submitted.empty() && !(stopper || l == 0) ? exchange->ApplyStream(n_submitted) : nullptr;
         if (as) {
           lin->ApplyGradient(grows, as, exchange);
           exchange->GatherParams(*lin, n_submitted, as);  // sharded apply: the other ranks' shards
