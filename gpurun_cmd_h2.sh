@@ -4,6 +4,11 @@ cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 O=gpurun_out/r4h2
 mkdir -p $O
 timeout -k 10 600 python3 -u -m pytest -x -q -rf --timeout 400 --timeout-method thread tests/test_gpu_steal.py tests/test_gpu_dp.py > $O/tests.txt 2>&1 &&
+timeout -k 10 600 python3 -u -m pytest -x -q -rf --timeout 400 --timeout-method thread tests/test_gpu_kernels.py -k "m128x256a2 or direct_form" > $O/tests_a2.txt 2>&1 &&
+for v in 1 4 1 4; do
+  TNET_GEMM_DIRECT=$v timeout -k 10 300 python3 bench.py --steps 100 --warmup 20 --no-cpu-baseline > $O/bench_d$v.json 2>> $O/bench_dv.err || exit 1
+  cat $O/bench_d$v.json >> $O/bench_dv.jsonl
+done &&
 timeout -k 10 120 ./tools/cohab_probe steal 16 > $O/cohab_steal16.txt 2>&1 &&
 bash tools/profile_round.sh > $O/profile_round.log 2>&1 &&
 timeout -k 10 300 python3 bench.py --steps 20 --warmup 5 --force-dp --no-cpu-baseline > $O/bench_fdp.json 2> $O/bench_fdp.err &&

@@ -724,7 +724,7 @@ __device__ __forceinline__ void gemm16_body(const GemmP& p_in, float* __restrict
   constexpr bool LDR = SP == 2;
   // SP >= 3: the direct form (no LDS ring; see the main loop), DD chunks of 16 k in flight per wave
   constexpr bool DIR = SP >= 3;
-  constexpr int DD = (SP == 3 || SP == 5) ? 4 : 8;
+  constexpr int DD = (SP == 3 || SP == 5) ? 4 : SP == 7 ? 2 : 8;
   static_assert(SP != 1 || S >= 3, "spread DMA needs a 3-slot ring");
   constexpr int WTM = BM / WM, WTN = BN / WN;  // wave tile
   constexpr int TM = WTM / 16, TN = WTN / 16;
@@ -1248,7 +1248,7 @@ __device__ __forceinline__ void gemm16_body(const GemmP& p_in, float* __restrict
     // SP >= 5 (a<D> configurations): the ring's loads are inline-asm buffer loads the compiler does not
     // track, waited for by one counted vmcnt per chunk that also ties the chunk's registers (the compiler's
     // own waits drain the whole ring at every loop back edge); 16-B loads and 6 or 8 per chunk only
-    constexpr bool ASM = SP >= 5 && (A_KC || VM == 4) && (B_KC || VN == 4) && (NR == 6 || NR == 8);
+    constexpr bool ASM = SP >= 5 && (A_KC || VM == 4) && (B_KC || VN == 4) && (NR == 6 || NR == 8 || NR == 12);
     if constexpr (ASM) {
       const unsigned long long ba = (unsigned long long)(uintptr_t)p.A, bb = (unsigned long long)(uintptr_t)p.B;
       const u32x4 dA = {(unsigned)ba, (unsigned)(ba >> 32), 0x7FFFFFF0u, 0x00020000u};
@@ -1267,9 +1267,14 @@ __device__ __forceinline__ void gemm16_body(const GemmP& p_in, float* __restrict
         if constexpr (NR == 6)
           asm volatile("s_waitcnt vmcnt(%6)" : "+v"(q[0]), "+v"(q[1]), "+v"(q[2]), "+v"(q[3]), "+v"(q[4]), "+v"(q[5])
                        : "n"(WV));
-        else
+        else if constexpr (NR == 8)
           asm volatile("s_waitcnt vmcnt(%8)"
                        : "+v"(q[0]), "+v"(q[1]), "+v"(q[2]), "+v"(q[3]), "+v"(q[4]), "+v"(q[5]), "+v"(q[6]), "+v"(q[7])
+                       : "n"(WV));
+        else
+          asm volatile("s_waitcnt vmcnt(%12)"
+                       : "+v"(q[0]), "+v"(q[1]), "+v"(q[2]), "+v"(q[3]), "+v"(q[4]), "+v"(q[5]), "+v"(q[6]), "+v"(q[7]),
+                         "+v"(q[8]), "+v"(q[9]), "+v"(q[10]), "+v"(q[11])
                        : "n"(WV));
       };
 #pragma unroll
@@ -2243,6 +2248,7 @@ static unsigned* splitk_counters(size_t n, hipStream_t st) {
   X(m64x128a4, 1, 64, 128, 64, 2, 2, 2, 5)              \
   X(m64x128a8, 1, 64, 128, 64, 2, 2, 2, 6)              \
   X(m128x128a4, 1, 128, 128, 64, 2, 2, 2, 5)            \
+  X(m128x256a2, 1, 128, 256, 32, 2, 2, 3, 7)            \
   X(m128x256k32s3, 1, 128, 256, 32, 2, 2, 3, 0)         \
   X(m64x64k64s2, 1, 64, 64, 64, 2, 2, 2, 0)             \
   X(m64x64k32s4, 1, 64, 64, 32, 2, 2, 4, 0)             \
@@ -2281,7 +2287,8 @@ static int g_reserve = 0, g_cus = 0;
 // the direct form -- 1 (default): m64x128a8 / m128x128a4, also the update half of the update + backward pair
 // kernel (dnn4 969.9 k -> 1006.2 k frames/s, the 2048^2 set 69.1 -> 65.6 us a launch, roofline 0.790 ->
 // 0.832, profiles/r04_gemm_direct_ab.json); 2: m64x128d4 / m128x128d4 (compiler-tracked loads); 3:
-// m64x128a4 / m128x128a4; 0: the LDS ring everywhere
+// m64x128a4 / m128x128a4; 4: 1 + the 128x256 update (the top layer's) as m128x256a2; 0: the LDS ring
+// everywhere
 static int g_direct = -1;
 static int g_wt = 1;  // TNET_GEMM_WT=0: plain 16-B epilogue stores instead of write-through (sc1; measured +1.4 % frames/s)
 static int forced_cfg() {
@@ -2651,6 +2658,7 @@ static int launch_gemm(const GemmP& p_in, hipStream_t st) {
   if (g_direct > 0 && forced_cfg() < 0 && !B_KC) {
     if (cfg == CFG_m64x128k64s2) rcfg = g_direct == 2 ? CFG_m64x128d4 : g_direct == 3 ? CFG_m64x128a4 : CFG_m64x128a8;
     else if (cfg == CFG_m128x128k64s2) rcfg = g_direct == 2 ? CFG_m128x128d4 : CFG_m128x128a4;
+    else if (cfg == CFG_m128x256k32s3 && g_direct == 4) rcfg = CFG_m128x256a2;  // 4: 1 + the 128x256 update
   }
   bool ok = false;
   switch (rcfg) {

@@ -40,7 +40,7 @@ GEMM_CFGS = ["auto", "g64x64k32s4w4", "m64x128k32s4", "m64x128k64s3", "m64x64k32
              "m64x64k64s2", "m64x64k32s4", "m32x64k64s2",
              # the direct form (fragments loaded into a register ring, no LDS ring; exact shapes only,
              # the ring form otherwise)
-             "m64x128d4", "m64x128d8", "m128x128d4", "m64x128a4", "m64x128a8", "m128x128a4",
+             "m64x128d4", "m64x128d8", "m128x128d4", "m64x128a4", "m64x128a8", "m128x128a4", "m128x256a2",
              # split-K (K cut into slices + an in-order combine with the epilogue); counts that do not
              # divide K fall back to fewer slices
              "auto+sk4", "m64x64k32s4w41+sk8", "m32x64k64s2+sk2", "m64x128k64s2+sk3",
@@ -146,7 +146,7 @@ def test_affine_update(mmt, rows, n_in, n_out, gemm_cfg):
 
 @pytest.mark.parametrize("direct,ring", [("m64x128d4", "m64x128k64s2"), ("m64x128a4", "m64x128k64s2"),
                                          ("m64x128a8", "m64x128k64s2"), ("m128x128d4", "m128x128k64s2"),
-                                         ("m128x128a4", "m128x128k64s2")])
+                                         ("m128x128a4", "m128x128k64s2"), ("m128x256a2", "m128x256k32s3")])
 @pytest.mark.parametrize("kind,rows,n_in,n_out", [("fwd", 1024, 2048, 2048), ("bwd", 1024, 2048, 2048),
                                                   ("upd", 1024, 2048, 2048), ("upd", 1024, 2048, 4096)])
 def test_direct_form_bit_identical_to_ring(direct, ring, kind, rows, n_in, n_out):
