@@ -2284,11 +2284,11 @@ static int g_pre0 = 1;  // TNET_GEMM_PRE0=0: the first seam also waits for the e
 static int g_reserve = 0, g_cus = 0;
 // TNET_GEMM_DIRECT: the planner's m64x128k64s2 / m128x128k64s2 choices with an n-contiguous B (the forward
 // and update GEMMs; the backward's k-contiguous B reads 64-B row pieces, slower direct: 99 vs 78 us) run in
-// the direct form -- 1 (default): m64x128a8 / m128x128a4, also the update half of the update + backward pair
-// kernel (dnn4 969.9 k -> 1006.2 k frames/s, the 2048^2 set 69.1 -> 65.6 us a launch, roofline 0.790 ->
-// 0.832, profiles/r04_gemm_direct_ab.json); 2: m64x128d4 / m128x128d4 (compiler-tracked loads); 3:
-// m64x128a4 / m128x128a4; 4: 1 + the 128x256 update (the top layer's) as m128x256a2; 0: the LDS ring
-// everywhere
+// the direct form -- 1: m64x128a8 / m128x128a4, also the update half of the update + backward pair kernel
+// (dnn4 969.9 k -> 1006.2 k frames/s, the 2048^2 set 69.1 -> 65.6 us a launch, roofline 0.790 -> 0.832,
+// profiles/r04_gemm_direct_ab.json); 4 (default): 1 + the 128x256 update (the top layer's) as m128x256a2
+// (134.6 -> 126.3 us, dnn4 1005 k -> 1015 k, profiles/r04_gemm_direct_128x256_ab.jsonl); 2: m64x128d4 /
+// m128x128d4 (compiler-tracked loads); 3: m64x128a4 / m128x128a4; 0: the LDS ring everywhere
 static int g_direct = -1;
 static int g_wt = 1;  // TNET_GEMM_WT=0: plain 16-B epilogue stores instead of write-through (sc1; measured +1.4 % frames/s)
 static int forced_cfg() {
@@ -2313,7 +2313,7 @@ static int forced_cfg() {
     const char* il = getenv("TNET_SPLITK_INLAUNCH");
     if (il) g_inlaunch = atoi(il);
     const char* dr = getenv("TNET_GEMM_DIRECT");
-    g_direct = dr ? atoi(dr) : 1;
+    g_direct = dr ? atoi(dr) : 4;
 
   }
   return g_cfg;
