@@ -275,6 +275,17 @@ int tnet_affine_grad(const float* X, TnetMatrixDim dX, const float* E, TnetMatri
  * (data-parallel path: both gradients are all-reduced, then applied by tnet_sgd_update_multi). */
 int tnet_affine_grad_bias(const float* X, TnetMatrixDim dX, const float* E, TnetMatrixDim dE, float* G,
                           TnetMatrixDim dG, const float* colpart, int ldcolpart, float* gradB, void* stream);
+/* tnet_affine_grad_bias(X, E, G, colpart, gradB) and tnet_affine_bwd_colsum(E2, W2, Ybelow, Eo, colpart2) in ONE
+ * launch (the data-parallel step's gradient of layer l -- cuBiasedLinearity.cc:46-64's GEMM and AddColSum written
+ * to a buffer for the all-reduce -- and the backward GEMM of layer l-1, cuBiasedLinearity.cc:21-25, which reads
+ * W_{l-1} only), tnet_affine_update_bwd_pair's form; results identical to the two calls.  TNET_ERR_ARG when an
+ * output of one overlaps an operand of the other; TNET_ERR_UNSUPPORTED where either would run another
+ * configuration alone, or while CUs are reserved for RCCL (tnet_gemm_reserve: make the two calls). */
+int tnet_affine_grad_bwd_pair(const float* X, TnetMatrixDim dX, const float* E, TnetMatrixDim dE, float* G,
+                              TnetMatrixDim dG, const float* colpart, int ldcolpart, float* gradB, const float* E2,
+                              TnetMatrixDim dE2, const float* W2, TnetMatrixDim dW2, const float* Ybelow,
+                              int strideYbelow, float* Eo, TnetMatrixDim dEo, float* colpart2, int ldcolpart2,
+                              void* stream);
 /* tnet_affine_grad_bias plus tnet_gather_bunch (the next bunch's CuCache::GetBunch, cuCache.cc:155-200) on the CUs
  * the gradient GEMM's tiles leave free -- the data-parallel step's last gradient GEMM, tnet_affine_update_bias_gather's
  * form and rules: the gather independent of the GEMM (TNET_ERR_ARG otherwise), results identical to the separate calls,

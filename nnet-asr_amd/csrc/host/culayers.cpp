@@ -303,6 +303,32 @@ bool CuBiasedLinearity::ComputeGradientColsumGather(const CuMatrix<BaseFloat>& c
   return true;
 }
 
+bool CuBiasedLinearity::ComputeGradientColsumWithBwd(const CuMatrix<BaseFloat>& colpart, const CuBiasedLinearity& below,
+                                                     const CuMatrix<BaseFloat>& E2, const CuMatrix<BaseFloat>& Ybelow,
+                                                     CuMatrix<BaseFloat>& Eo, CuMatrix<BaseFloat>& colpart2) {
+  CuProfileScope p("CuBiasedLinearity::ComputeGradient+Backpropagate");
+  const CuMatrix<BaseFloat>& X = GetInput();
+  const CuMatrix<BaseFloat>& E = GetErrorInput();
+  mGradW.Init(mLinearity.Rows(), mLinearity.Cols());
+  mGradB.Init(mBias.Dim());
+  const std::string su = std::to_string(GetNInputs()) + "x" + std::to_string(GetNOutputs());
+  const std::string sb = std::to_string(below.GetNInputs()) + "x" + std::to_string(below.GetNOutputs());
+  KTScope kt("gemm_grad+bwd:" + (su == sb ? su : su + "+" + sb),
+             2.0 * X.Rows() * GetNInputs() * GetNOutputs() + 2.0 * E2.Rows() * below.GetNInputs() * below.GetNOutputs(),
+             2);
+  const int st = tnet_affine_grad_bwd_pair(
+      X.pCUData(), X.Dim(), E.pCUData(), E.Dim(), mGradW.pCUData(), mGradW.Dim(), colpart.pCUData(),
+      (int)colpart.Stride(), mGradB.pCUData(), E2.pCUData(), E2.Dim(), below.Linearity().pCUData(),
+      below.Linearity().Dim(), Ybelow.pCUData(), (int)Ybelow.Stride(), Eo.pCUData(), Eo.Dim(), colpart2.pCUData(),
+      (int)colpart2.Stride(), S);
+  if (st == TNET_ERR_UNSUPPORTED) {
+    kt.Cancel();
+    return false;
+  }
+  TNET_SAFE_CALL(st);
+  return true;
+}
+
 std::vector<CuParamBlock> CuBiasedLinearity::GradientBlocks() {
   mGradW.Init(mLinearity.Rows(), mLinearity.Cols());
   mGradB.Init(mBias.Dim());

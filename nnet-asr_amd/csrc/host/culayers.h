@@ -28,6 +28,12 @@ class CuBiasedLinearity : public CuUpdatableComponent {
   // ComputeGradientColsum with the next bunch's gather `g` on the CUs the GEMM's tiles leave free, in ONE
   // launch (tnet_affine_grad_bias_gather); false: nothing enqueued (make the separate calls)
   bool ComputeGradientColsumGather(const CuMatrix<BaseFloat>& colpart, const BunchGather& g);
+  // ComputeGradientColsum(colpart) of THIS layer (inputs as set by SetInput / SetErrorInput) and below's backward
+  // Eo = (E2 W_below^T) .* Ybelow (1 - Ybelow) + Eo's slab sums in ONE launch (tnet_affine_grad_bwd_pair); false:
+  // nothing enqueued (make the two calls)
+  bool ComputeGradientColsumWithBwd(const CuMatrix<BaseFloat>& colpart, const CuBiasedLinearity& below,
+                                    const CuMatrix<BaseFloat>& E2, const CuMatrix<BaseFloat>& Ybelow,
+                                    CuMatrix<BaseFloat>& Eo, CuMatrix<BaseFloat>& colpart2);
   void ApplyGradient(size_t frames, void* stream = nullptr, const GradExchange* ex = nullptr) override;
   std::vector<CuParamBlock> GradientBlocks() override;
 

@@ -243,6 +243,9 @@ void CuUpdatableComponent::ZeroGradient() {
 static long g_fail_train_bunch = 0;
 void CuNetwork::DebugFailTrainBunch(long n) { g_fail_train_bunch = n; }
 
+// TNET_DP_PAIR=0: the data-parallel step never pairs a gradient GEMM with the backward GEMM below (A/B)
+static const bool g_dp_pair = !(getenv("TNET_DP_PAIR") && getenv("TNET_DP_PAIR")[0] == '0');
+
 void CuNetwork::TrainBunch(const CuMatrix<BaseFloat>& X, const CuVector<int>& labels, CuObjectiveFunction& obj,
                            bool train, GradExchange* exchange) {
   if (g_fail_train_bunch > 0 && --g_fail_train_bunch == 0) Error("CuNetwork::TrainBunch: injected fault");
@@ -392,6 +395,33 @@ void CuNetwork::TrainBunch(const CuMatrix<BaseFloat>& X, const CuVector<int>& la
     pend.lin->UpdateFromColsum(*pend.X, *pend.E, *mColPart[pend.l]);
     pend.lin = nullptr;
   };
+  // Data parallel: a layer's reduction submitted, and its SGD apply right behind it (beside the backward GEMMs
+  // below: W_l is read for the last time by this layer's backward GEMM, already enqueued) -- the step's last layer
+  // on the compute stream (nothing is left to overlap it with, and the apply stream would add a hop in and a join
+  // out)
+  auto submit_layer = [&](CuBiasedLinearity* lin, bool last) {
+    exchange->Submit(*lin);
+    void* as = submitted.empty() && !last ? exchange->ApplyStream(n_submitted) : nullptr;
+    if (as) {
+      lin->ApplyGradient(grows, as, exchange);
+      exchange->GatherParams(*lin, n_submitted, as);  // sharded apply: the other ranks' shards
+    } else {
+      submitted.push_back(lin);
+    }
+    n_submitted++;
+  };
+  // ... and, while no CUs are reserved for RCCL (tnet_gemm_reserve: before the step's first submission, or a
+  // single-rank communicator), a layer's gradient GEMM is held back one layer and enqueued with the backward GEMM
+  // of the layer below as ONE launch (tnet_affine_grad_bwd_pair, the pair kernel of the fused step; independent:
+  // the gradient reads X_l, E_l, the backward E_l and W_{l-1})
+  CuBiasedLinearity* pgrad = nullptr;
+  int pgrad_l = -1;
+  auto flush_grad = [&]() {
+    if (!pgrad) return;
+    pgrad->ComputeGradientColsum(*mColPart[pgrad_l]);
+    submit_layer(pgrad, false);
+    pgrad = nullptr;
+  };
   for (int l = nl - 1; l >= 0; l--) {
     auto* lin = static_cast<CuBiasedLinearity*>(mNetComponents[2 * l]);
     const bool stopper = (lin == mpPropagErrorStopper);
@@ -407,11 +437,16 @@ void CuNetwork::TrainBunch(const CuMatrix<BaseFloat>& X, const CuVector<int>& la
       if (below->LearnRate() > 0.0f) {
         CuMatrix<BaseFloat>& cp = *mColPart[l - 1];
         cp.Init(tnet_colsum_slabs((int)rows), lin->GetNInputs());
-        if (pend.lin && pend.lin->UpdateFromColsumWithBwd(*pend.X, *pend.E, *mColPart[pend.l], *lin, *err, *acts[l],
-                                                         *eo, cp)) {
+        if (pgrad && pgrad->ComputeGradientColsumWithBwd(*mColPart[pgrad_l], *lin, *err, *acts[l], *eo, cp)) {
+          submit_layer(pgrad, false);
+          pgrad = nullptr;
+          eo_colsum = true;
+        } else if (pend.lin && pend.lin->UpdateFromColsumWithBwd(*pend.X, *pend.E, *mColPart[pend.l], *lin, *err,
+                                                                *acts[l], *eo, cp)) {
           pend.lin = nullptr;
           eo_colsum = true;
         } else {
+          flush_grad();
           flush();
           KTScope kt("gemm_bwd:" + shape, 2.0 * rows * lin->GetNInputs() * lin->GetNOutputs());
           int st = TNET_ERR_UNSUPPORTED;
@@ -435,6 +470,7 @@ void CuNetwork::TrainBunch(const CuMatrix<BaseFloat>& X, const CuVector<int>& la
         }
       }
       if (!eo_colsum) {
+        flush_grad();
         flush();
         KTScope kt("gemm_bwd:" + shape, 2.0 * rows * lin->GetNInputs() * lin->GetNOutputs());
         TNET_SAFE_CALL(tnet_affine_bwd(err->pCUData(), err->Dim(), lin->Linearity().pCUData(),
@@ -462,32 +498,27 @@ void CuNetwork::TrainBunch(const CuMatrix<BaseFloat>& X, const CuVector<int>& la
         break;
       }
     }
-    flush();  // a held-back update no backward GEMM took
+    flush();       // a held-back update no backward GEMM took
+    flush_grad();  // a held-back gradient no backward GEMM took
     if (lin->LearnRate() > 0.0f) {
       if (exchange) {
         lin->SetInput(*acts[l]);
         lin->SetErrorInput(*err);
-        // the step's last gradient GEMM carries the next bunch's gather (when the trainer handed one over)
-        if (err_colsum && (stopper || l == 0) && mHasTailGather && !mTailDone &&
-            lin->ComputeGradientColsumGather(*mColPart[l], mTailGather))
-          mTailDone = true;
-        else if (err_colsum)
-          lin->ComputeGradientColsum(*mColPart[l]);
-        else
-          lin->ComputeGradient();
-        exchange->Submit(*lin);
-        // the layer's SGD update right behind its reduction, beside the backward GEMMs below (W_l is
-        // read for the last time by this layer's backward GEMM, already enqueued)
-        // (the step's last layer applies on the compute stream right behind its reduction: nothing is left
-        // to overlap it with, and the apply stream would add a hop in and a join out)
-        void* as = submitted.empty() && !(stopper || l == 0) ? exchange->ApplyStream(n_submitted) : nullptr;
-        if (as) {
-          lin->ApplyGradient(grows, as, exchange);
-          exchange->GatherParams(*lin, n_submitted, as);  // sharded apply: the other ranks' shards
+        const bool last = stopper || l == 0;
+        if (err_colsum && !last && g_dp_pair) {
+          pgrad = lin;  // held back for the next layer's backward GEMM (flushed there or at the next layer)
+          pgrad_l = l;
         } else {
-          submitted.push_back(lin);
+          // the step's last gradient GEMM carries the next bunch's gather (when the trainer handed one over)
+          if (err_colsum && last && mHasTailGather && !mTailDone &&
+              lin->ComputeGradientColsumGather(*mColPart[l], mTailGather))
+            mTailDone = true;
+          else if (err_colsum)
+            lin->ComputeGradientColsum(*mColPart[l]);
+          else
+            lin->ComputeGradient();
+          submit_layer(lin, last);
         }
-        n_submitted++;
       } else if (err_colsum) {
         pend.lin = lin;  // held back for the next layer's backward GEMM (flushed there or below)
         pend.X = acts[l];
@@ -509,6 +540,7 @@ void CuNetwork::TrainBunch(const CuMatrix<BaseFloat>& X, const CuVector<int>& la
     pend.lin = nullptr;
   }
   flush();
+  flush_grad();
   if (exchange) {
     // the next bunch's gather right behind the last gradient GEMM on the compute stream, so it runs while the
     // last reductions (and their applies) are still in flight instead of after WaitAll at the next step's start

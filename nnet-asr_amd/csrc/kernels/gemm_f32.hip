@@ -2678,7 +2678,11 @@ static int launch_gemm(const GemmP& p_in, hipStream_t st) {
 // planner gives it) and an independent backward GEMM (B: diff-sigmoid + slab sums, 64x128) as one
 // gemm16_pair_kernel launch; TNET_ERR_UNSUPPORTED where either would run another configuration (the
 // caller then makes the two calls)
-static int launch_pair_upd_bwd(GemmP pu, GemmP pb, hipStream_t st) {
+template <int EPIA>
+static int launch_pair_a_bwd(GemmP pu, GemmP pb, hipStream_t st) {
+  // EPI_STORE_BG (the data-parallel gradient): not while CUs are reserved for RCCL (the exchange window runs the
+  // stream-K forms; a 512-workgroup pair would lose a second round on the held CUs)
+  if (EPIA == EPI_STORE_BG && g_reserve > 0) return TNET_ERR_UNSUPPORTED;
   if (forced_cfg() >= 0 || !g_pair) return TNET_ERR_UNSUPPORTED;
   if (pu.M <= 0 || pu.N <= 0 || pb.M <= 0 || pb.N <= 0) return TNET_ERR_UNSUPPORTED;
   const GemmPlan pl = plan_gemm<false>(pu, true);
@@ -2699,25 +2703,27 @@ static int launch_pair_upd_bwd(GemmP pu, GemmP pb, hipStream_t st) {
   const bool dir = g_direct > 0 && pu.K / 64 >= 1 && !(pu.lda & 3) && !(pu.ldb & 3) && a16p(pu.A) && a16p(pu.B) &&
                    pu.M % 4 == 0 && pu.N % 4 == 0 &&
                    4 * ((long)pu.K * pu.lda) < (1L << 31) && 4 * ((long)pu.K * pu.ldb) < (1L << 31);
-  const bool px = px_exact<128, 128, EPI_SGD_B>(pu);
+  const bool px = px_exact<128, 128, EPIA>(pu);
   if (dir && px && g_direct == 2)
-    gemm16_pair_kernel<128, 128, false, false, EPI_SGD_B, true, 64, 128, true, true, EPI_DSIG_CS, true, 3>
+    gemm16_pair_kernel<128, 128, false, false, EPIA, true, 64, 128, true, true, EPI_DSIG_CS, true, 3>
         <<<na + nb, 256, 0, st>>>(pu, pb, na);
   else if (dir && px)
-    gemm16_pair_kernel<128, 128, false, false, EPI_SGD_B, true, 64, 128, true, true, EPI_DSIG_CS, true, 5>
+    gemm16_pair_kernel<128, 128, false, false, EPIA, true, 64, 128, true, true, EPI_DSIG_CS, true, 5>
         <<<na + nb, 256, 0, st>>>(pu, pb, na);
   else if (dir)
-    gemm16_pair_kernel<128, 128, false, false, EPI_SGD_B, false, 64, 128, true, true, EPI_DSIG_CS, true, 5>
+    gemm16_pair_kernel<128, 128, false, false, EPIA, false, 64, 128, true, true, EPI_DSIG_CS, true, 5>
         <<<na + nb, 256, 0, st>>>(pu, pb, na);
   else if (px)
-    gemm16_pair_kernel<128, 128, false, false, EPI_SGD_B, true, 64, 128, true, true, EPI_DSIG_CS, true>
+    gemm16_pair_kernel<128, 128, false, false, EPIA, true, 64, 128, true, true, EPI_DSIG_CS, true>
         <<<na + nb, 256, 0, st>>>(pu, pb, na);
   else
-    gemm16_pair_kernel<128, 128, false, false, EPI_SGD_B, false, 64, 128, true, true, EPI_DSIG_CS, true>
+    gemm16_pair_kernel<128, 128, false, false, EPIA, false, 64, 128, true, true, EPI_DSIG_CS, true>
         <<<na + nb, 256, 0, st>>>(pu, pb, na);
   TNET_LAUNCH_CHECK();
   return TNET_OK;
 }
+
+static int launch_pair_upd_bwd(GemmP pu, GemmP pb, hipStream_t st) { return launch_pair_a_bwd<EPI_SGD_B>(pu, pb, st); }
 
 static int cu_count() {
   if (!g_cus) {
@@ -3274,6 +3280,46 @@ extern "C" int tnet_affine_update_bwd_pair(const float* X, TnetMatrixDim dX, con
   st = check_common(pb);
   if (st) return st;
   return launch_pair_upd_bwd(pu, pb, (hipStream_t)stream);
+}
+
+extern "C" int tnet_affine_grad_bwd_pair(const float* X, TnetMatrixDim dX, const float* E, TnetMatrixDim dE, float* G,
+                                        TnetMatrixDim dG, const float* colpart, int ldcolpart, float* gradB,
+                                        const float* E2, TnetMatrixDim dE2, const float* W2, TnetMatrixDim dW2,
+                                        const float* Ybelow, int strideYbelow, float* Eo, TnetMatrixDim dEo,
+                                        float* colpart2, int ldcolpart2, void* stream) {
+  // tnet_affine_grad_bias(X, E, G, colpart, gradB) and tnet_affine_bwd_colsum(E2, W2, Ybelow, Eo, colpart2) in one
+  // launch (the data-parallel step's gradient of layer l and the backward GEMM of layer l-1); independent: G / gradB
+  // / Eo / colpart2 overlap none of the other's operands
+  if (dX.rows != dE.rows || dG.rows != dX.cols || dG.cols != dE.cols || !colpart || !gradB || ldcolpart < dE.cols)
+    return TNET_ERR_ARG;
+  if (dE2.cols != dW2.cols || dEo.rows != dE2.rows || dEo.cols != dW2.rows || !Ybelow || !colpart2 ||
+      ldcolpart2 < dEo.cols || !aligned16(Ybelow) || (strideYbelow & 3))
+    return TNET_ERR_ARG;
+  GemmP pu{};
+  pu.M = dX.cols; pu.N = dE.cols; pu.K = dX.rows;
+  pu.A = X; pu.lda = dX.stride; pu.B = E; pu.ldb = dE.stride; pu.C = G; pu.ldc = dG.stride;
+  pu.alpha = 1.f; pu.beta = 0.f;
+  pu.bpart = colpart; pu.ldbpart = ldcolpart; pu.bslabs = tnet_colsum_slabs(dE.rows);
+  pu.bvec = gradB;
+  int st = check_common(pu);
+  if (st) return st;
+  GemmP pb{};
+  pb.M = dE2.rows; pb.N = dW2.rows; pb.K = dE2.cols;
+  pb.A = E2; pb.lda = dE2.stride; pb.B = W2; pb.ldb = dW2.stride; pb.C = Eo; pb.ldc = dEo.stride;
+  pb.alpha = 1.f; pb.beta = 0.f;
+  pb.aux = Ybelow; pb.ldaux = strideYbelow;
+  pb.cpart = colpart2; pb.ldcpart = ldcolpart2;
+  st = check_common(pb);
+  if (st) return st;
+  // the two launches' outputs must not feed the other launch
+  const std::array<ByteSpan, 2> wu{span_of(G, dG.rows, dG.stride, 4), span_of(gradB, dG.cols, 1, 4)};
+  const std::array<ByteSpan, 2> wb{span_of(Eo, dEo.rows, dEo.stride, 4), span_of(colpart2, tnet_colsum_slabs(dE2.rows), ldcolpart2, 4)};
+  if (any_overlap({wu[0], wu[1]}, {span_of(E2, dE2.rows, dE2.stride, 4), span_of(W2, dW2.rows, dW2.stride, 4),
+                                   span_of(Ybelow, dEo.rows, strideYbelow, 4), wb[0], wb[1]}) ||
+      any_overlap({wb[0], wb[1]}, {span_of(X, dX.rows, dX.stride, 4), span_of(E, dE.rows, dE.stride, 4),
+                                   span_of(colpart, tnet_colsum_slabs(dE.rows), ldcolpart, 4)}))
+    return TNET_ERR_ARG;
+  return launch_pair_a_bwd<EPI_STORE_BG>(pu, pb, (hipStream_t)stream);
 }
 
 extern "C" int tnet_affine_grad_bias(const float* X, TnetMatrixDim dX, const float* E, TnetMatrixDim dE, float* G,

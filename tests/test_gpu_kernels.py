@@ -300,6 +300,54 @@ def test_affine_update_bwd_pair(mmt, rows, n_in, n_out, n_below):
         np.testing.assert_array_equal(got[k], ref[k], err_msg=k)
 
 
+@pytest.mark.parametrize("rows,n_in,n_out,n_below", [(1024, 2048, 2048, 2048), (1024, 2048, 4000, 2048),
+                                                     (1024, 1024, 2048, 1024)])
+def test_affine_grad_bwd_pair(rows, n_in, n_out, n_below):
+    """tnet_affine_grad_bwd_pair (the data-parallel step's gradient of layer l + layer l-1's backward GEMM in one
+    launch) gives exactly what tnet_affine_grad_bias + tnet_affine_bwd_colsum give, or declines with
+    TNET_ERR_UNSUPPORTED where the pair kernel does not take the shapes, and while CUs are reserved for RCCL"""
+    X, E = rnd((rows, n_in), 31), rnd((rows, n_out), 32, 0.01)
+    P = slab_sums(E).astype(np.float32)
+    W2, E2 = rnd((n_below, n_in), 37, 0.1), rnd((rows, n_in), 38)
+    Yb = (1 / (1 + np.exp(-rnd((rows, n_below), 39)))).astype(np.float32)
+    slabs = lib().tnet_colsum_slabs(rows)
+
+    def run(pair, reserve=0):
+        d = dict(X=DeviceArray.from_numpy(X), E=DeviceArray.from_numpy(E), P=DeviceArray.from_numpy(P),
+                 G=DeviceArray.from_numpy(np.full((n_in, n_out), np.nan, np.float32)),
+                 gb=DeviceArray.vector(np.full(n_out, np.nan, np.float32)),
+                 W2=DeviceArray.from_numpy(W2), E2=DeviceArray.from_numpy(E2), Y=DeviceArray.from_numpy(Yb),
+                 O=DeviceArray(rows, n_below), P2=DeviceArray.from_numpy(np.full((slabs, n_below), np.nan, np.float32)))
+        grad = (d["X"].ptr, d["X"].dim, d["E"].ptr, d["E"].dim, d["G"].ptr, d["G"].dim, d["P"].ptr, d["P"].stride,
+                d["gb"].ptr)
+        bwd = (d["E2"].ptr, d["E2"].dim, d["W2"].ptr, d["W2"].dim, d["Y"].ptr, d["Y"].stride, d["O"].ptr, d["O"].dim,
+               d["P2"].ptr, d["P2"].stride)
+        if pair:
+            check(lib().tnet_gemm_reserve(reserve))
+            try:
+                st = lib().tnet_affine_grad_bwd_pair(*grad, *bwd, S())
+            finally:
+                check(lib().tnet_gemm_reserve(0))
+            if st == TNET_ERR_UNSUPPORTED:
+                return None
+            check(st)
+        else:
+            check(lib().tnet_affine_grad_bias(*grad, S()))
+            check(lib().tnet_affine_bwd_colsum(*bwd, S()))
+        synchronize()
+        return {k: v.numpy() for k, v in d.items() if k in ("G", "gb", "O", "P2")}
+
+    got, ref = run(True), run(False)
+    if (n_in, n_out, n_below) == (2048, 2048, 2048):
+        assert got is not None, "the step's 2048-wide layers must run as one launch"
+        assert run(True, reserve=16) is None, "no pair while CUs are reserved for RCCL"
+    if got is None:
+        return
+    for k in ref:
+        np.testing.assert_array_equal(got[k], ref[k], err_msg=k)
+    np.testing.assert_allclose(ref["G"], X.astype(np.float64).T @ E.astype(np.float64), rtol=1e-4, atol=1e-5)
+
+
 def test_affine_update_bwd_pair_rejects_shared_weights():
     X, E = rnd((64, 128), 1), rnd((64, 128), 2)
     dX, dE, dW, dP, db = (DeviceArray.from_numpy(X), DeviceArray.from_numpy(E), DeviceArray(128, 128),

@@ -31,10 +31,12 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 # (round 3: a trailing ", true" = the exact-prefetch instantiation, PX)
-FWD = re.compile(r"gemm16_kernel<64, 128, 64, 2, 2, 2, 0, true, false, 2(, (true|false))?>")    # bias + sigmoid
-BWD = re.compile(r"gemm16_kernel<64, 128, 64, 2, 2, 2, 0, true, true, 8(, (true|false))?>")     # diff-sigmoid + sums
-PAIR = re.compile(r"gemm16_pair_kernel<128, 128, false, false, 9, (true|false), 64, 128, true, true, 8, true>")
-UPD = re.compile(r"gemm16_kernel<128, 128, 64, 2, 2, 2, 0, false, false, 9(, (true|false))?>")  # SGD + bias SGD
+# (round 4: the form parameter SP -- 0 the LDS ring, 3..6 the direct forms -- and the pair kernel's form of its
+# update half)
+FWD = re.compile(r"gemm16_kernel<64, 128, 64, 2, 2, 2, \d+, true, false, 2(, (true|false))?>")    # bias + sigmoid
+BWD = re.compile(r"gemm16_kernel<64, 128, 64, 2, 2, 2, \d+, true, true, 8(, (true|false))?>")     # diff-sigmoid + sums
+PAIR = re.compile(r"gemm16_pair_kernel<128, 128, false, false, 9, (true|false), 64, 128, true, true, 8, true(, \d+)?>")
+UPD = re.compile(r"gemm16_kernel<128, 128, 64, 2, 2, 2, \d+, false, false, 9(, (true|false))?>")  # SGD + bias SGD
 
 
 def classify_trace(path):
@@ -113,13 +115,15 @@ def main():
            "algorithmic_MB_per_launch_avg": round(sum(algo.values()) / 3, 3)}
     # MFMA utilisation pass (GRBM_GUI_ACTIVE, SQ_VALU_MFMA_BUSY_CYCLES, SQ_INSTS_VALU_MFMA_MOPS_F32) and
     # the in-kernel clock stamps (tools/gemm_clock.py, separate stamped build)
-    mf = pmc_summary.summarise(os.path.join(src, "pmc_mfma"))
-    pmc["mfma_pass"] = {k: r for k, r in mf.items() if "gemm" in k}
-    pmc["mfma_pass_note"] = ("mfma_busy_frac = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE/8 * 1024 SIMDs); "
-                             "GRBM_GUI_ACTIVE/8/duration reads above the real clock on sub-0.3-ms dispatches "
-                             "(MI355X_MICROARCH.md 'DVFS give-back'), so the in-kernel stamps below are the "
-                             "clock and cycle reference")
-    clk = [l for l in open(os.path.join(src, "clock.log")) if l.startswith("CLOCK ")]
+    if os.path.isdir(os.path.join(src, "pmc_mfma")):  # optional passes (a round may skip them)
+        mf = pmc_summary.summarise(os.path.join(src, "pmc_mfma"))
+        pmc["mfma_pass"] = {k: r for k, r in mf.items() if "gemm" in k}
+        pmc["mfma_pass_note"] = ("mfma_busy_frac = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE/8 * 1024 SIMDs); "
+                                 "GRBM_GUI_ACTIVE/8/duration reads above the real clock on sub-0.3-ms dispatches "
+                                 "(MI355X_MICROARCH.md 'DVFS give-back'), so the in-kernel stamps below are the "
+                                 "clock and cycle reference")
+    clk = [l for l in open(os.path.join(src, "clock.log")) if l.startswith("CLOCK ")] \
+        if os.path.exists(os.path.join(src, "clock.log")) else []
     if clk:
         pmc["clock_stamps"] = json.loads(clk[-1][6:])
     with open(os.path.join(prof, f"{tag}_pmc_gemm2048.json"), "w") as f:
