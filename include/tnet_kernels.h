@@ -286,14 +286,18 @@ int tnet_affine_grad_bwd_pair(const float* X, TnetMatrixDim dX, const float* E, 
                               TnetMatrixDim dE2, const float* W2, TnetMatrixDim dW2, const float* Ybelow,
                               int strideYbelow, float* Eo, TnetMatrixDim dEo, float* colpart2, int ldcolpart2,
                               void* stream);
-/* tnet_affine_grad_bias plus tnet_gather_bunch (the next bunch's CuCache::GetBunch, cuCache.cc:155-200) on the CUs
- * the gradient GEMM's tiles leave free -- the data-parallel step's last gradient GEMM, tnet_affine_update_bias_gather's
- * form and rules: the gather independent of the GEMM (TNET_ERR_ARG otherwise), results identical to the separate calls,
- * TNET_ERR_UNSUPPORTED when the GEMM would run another tile configuration alone or fewer than 8 CUs are left. */
+/* tnet_affine_grad_bias (X2 NULL) or two of them (X2, E2, G2, colpart2, gradB2: the step's last two gradients when
+ * both 64x64 grids fit one round over the CUs) plus tnet_gather_bunch (the next bunch's CuCache::GetBunch,
+ * cuCache.cc:155-200) on the CUs the gradient GEMMs' tiles leave free -- the data-parallel step's last gradient
+ * launch, tnet_affine_update_bias_gather's form and rules: the gather independent of the GEMMs and the two GEMMs of
+ * each other (TNET_ERR_ARG otherwise), TNET_ERR_UNSUPPORTED when one GEMM would run another tile configuration
+ * alone, the pair does not fit one round, or fewer than 8 CUs are left. */
 int tnet_affine_grad_bias_gather(const float* X, TnetMatrixDim dX, const float* E, TnetMatrixDim dE, float* G,
-                                 TnetMatrixDim dG, const float* colpart, int ldcolpart, float* gradB, float* y,
-                                 const float* x, int* labels_out, const int* labels_in, const int* copy_from,
-                                 TnetMatrixDim dy, TnetMatrixDim dx, void* stream);
+                                 TnetMatrixDim dG, const float* colpart, int ldcolpart, float* gradB, const float* X2,
+                                 TnetMatrixDim dX2, const float* E2, TnetMatrixDim dE2, float* G2, TnetMatrixDim dG2,
+                                 const float* colpart2, int ldcolpart2, float* gradB2, float* y, const float* x,
+                                 int* labels_out, const int* labels_in, const int* copy_from, TnetMatrixDim dy,
+                                 TnetMatrixDim dx, void* stream);
 /* Element-wise SGD of the same formula on flat arrays:  c = g + mmt*corr; p += scale*c; p += l2*p;
  * corr = c (corr may be NULL when mmt == 0). */
 int tnet_sgd_update(float* p, const float* g, float* corr, long n, float scale, float mmt, float l2,

@@ -283,18 +283,37 @@ void CuBiasedLinearity::ComputeGradientColsum(const CuMatrix<BaseFloat>& colpart
                                        colpart.pCUData(), (int)colpart.Stride(), mGradB.pCUData(), S));
 }
 
-bool CuBiasedLinearity::ComputeGradientColsumGather(const CuMatrix<BaseFloat>& colpart, const BunchGather& g) {
-  CuProfileScope p("CuBiasedLinearity::ComputeGradient");
+bool CuBiasedLinearity::ComputeGradientColsumGather(const CuMatrix<BaseFloat>& colpart, const BunchGather& g,
+                                                    CuBiasedLinearity* other, const CuMatrix<BaseFloat>* colpart2) {
+  CuProfileScope p(other ? "CuBiasedLinearity::ComputeGradient (pair) + gather" : "CuBiasedLinearity::ComputeGradient + gather");
   const CuMatrix<BaseFloat>& X = GetInput();
   const CuMatrix<BaseFloat>& E = GetErrorInput();
   mGradW.Init(mLinearity.Rows(), mLinearity.Cols());
   mGradB.Init(mBias.Dim());
-  KTScope kt("gemm_grad+gather:" + std::to_string(GetNInputs()) + "x" + std::to_string(GetNOutputs()),
-             2.0 * X.Rows() * GetNInputs() * GetNOutputs());
-  const int st = tnet_affine_grad_bias_gather(X.pCUData(), X.Dim(), E.pCUData(), E.Dim(), mGradW.pCUData(),
-                                              mGradW.Dim(), colpart.pCUData(), (int)colpart.Stride(),
-                                              mGradB.pCUData(), g.y, g.x, g.labels_out, g.labels_in, g.copy_from,
-                                              g.dy, g.dx, S);
+  std::string name = "gemm_grad" + std::string(other ? "+grad" : "") + "+gather:" + std::to_string(GetNInputs()) + "x" +
+                     std::to_string(GetNOutputs());
+  double flops = 2.0 * X.Rows() * GetNInputs() * GetNOutputs();
+  const TnetMatrixDim z{};
+  const float* X2 = nullptr;
+  const float* E2 = nullptr;
+  TnetMatrixDim dX2 = z, dE2 = z, dG2 = z;
+  if (other) {
+    other->mGradW.Init(other->mLinearity.Rows(), other->mLinearity.Cols());
+    other->mGradB.Init(other->mBias.Dim());
+    X2 = other->GetInput().pCUData();
+    dX2 = other->GetInput().Dim();
+    E2 = other->GetErrorInput().pCUData();
+    dE2 = other->GetErrorInput().Dim();
+    dG2 = other->mGradW.Dim();
+    name += "+" + std::to_string(other->GetNInputs()) + "x" + std::to_string(other->GetNOutputs());
+    flops += 2.0 * other->GetInput().Rows() * other->GetNInputs() * other->GetNOutputs();
+  }
+  KTScope kt(name, flops, other ? 2 : 1);
+  const int st = tnet_affine_grad_bias_gather(
+      X.pCUData(), X.Dim(), E.pCUData(), E.Dim(), mGradW.pCUData(), mGradW.Dim(), colpart.pCUData(),
+      (int)colpart.Stride(), mGradB.pCUData(), X2, dX2, E2, dE2, other ? other->mGradW.pCUData() : nullptr, dG2,
+      other ? colpart2->pCUData() : nullptr, other ? (int)colpart2->Stride() : 0,
+      other ? other->mGradB.pCUData() : nullptr, g.y, g.x, g.labels_out, g.labels_in, g.copy_from, g.dy, g.dx, S);
   if (st == TNET_ERR_UNSUPPORTED) {
     kt.Cancel();
     return false;

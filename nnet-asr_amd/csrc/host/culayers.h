@@ -25,9 +25,11 @@ class CuBiasedLinearity : public CuUpdatableComponent {
   void ComputeGradient() override;
   // ComputeGradient with the bias gradient from the slab column sums of E (tnet_affine_grad_bias)
   void ComputeGradientColsum(const CuMatrix<BaseFloat>& colpart);
-  // ComputeGradientColsum with the next bunch's gather `g` on the CUs the GEMM's tiles leave free, in ONE
-  // launch (tnet_affine_grad_bias_gather); false: nothing enqueued (make the separate calls)
-  bool ComputeGradientColsumGather(const CuMatrix<BaseFloat>& colpart, const BunchGather& g);
+  // ComputeGradientColsum -- and with `other` (its inputs set by SetInput / SetErrorInput) also
+  // other->ComputeGradientColsum(*colpart2) -- with the next bunch's gather `g` on the CUs the GEMMs' tiles leave
+  // free, in ONE launch (tnet_affine_grad_bias_gather); false: nothing enqueued (make the separate calls)
+  bool ComputeGradientColsumGather(const CuMatrix<BaseFloat>& colpart, const BunchGather& g,
+                                   CuBiasedLinearity* other = nullptr, const CuMatrix<BaseFloat>* colpart2 = nullptr);
   // ComputeGradientColsum(colpart) of THIS layer (inputs as set by SetInput / SetErrorInput) and below's backward
   // Eo = (E2 W_below^T) .* Ybelow (1 - Ybelow) + Eo's slab sums in ONE launch (tnet_affine_grad_bwd_pair); false:
   // nothing enqueued (make the two calls)

@@ -498,25 +498,35 @@ void CuNetwork::TrainBunch(const CuMatrix<BaseFloat>& X, const CuVector<int>& la
         break;
       }
     }
-    flush();       // a held-back update no backward GEMM took
-    flush_grad();  // a held-back gradient no backward GEMM took
+    flush();  // a held-back update no backward GEMM took
+    const bool last = stopper || l == 0;
+    // a held-back gradient no backward GEMM took (the last layer may still take it, with the gather, below)
+    if (!(exchange && last && err_colsum && lin->LearnRate() > 0.0f && mHasTailGather && !mTailDone)) flush_grad();
     if (lin->LearnRate() > 0.0f) {
       if (exchange) {
         lin->SetInput(*acts[l]);
         lin->SetErrorInput(*err);
-        const bool last = stopper || l == 0;
         if (err_colsum && !last && g_dp_pair) {
           pgrad = lin;  // held back for the next layer's backward GEMM (flushed there or at the next layer)
           pgrad_l = l;
         } else {
-          // the step's last gradient GEMM carries the next bunch's gather (when the trainer handed one over)
-          if (err_colsum && last && mHasTailGather && !mTailDone &&
-              lin->ComputeGradientColsumGather(*mColPart[l], mTailGather))
+          // the step's last gradient GEMM carries the next bunch's gather (when the trainer handed one over) --
+          // with the held-back gradient of the layer above in the same launch where both grids fit one round
+          if (err_colsum && last && mHasTailGather && !mTailDone && pgrad &&
+              lin->ComputeGradientColsumGather(*mColPart[l], mTailGather, pgrad, mColPart[pgrad_l].get())) {
             mTailDone = true;
-          else if (err_colsum)
-            lin->ComputeGradientColsum(*mColPart[l]);
-          else
-            lin->ComputeGradient();
+            submit_layer(pgrad, false);
+            pgrad = nullptr;
+          } else {
+            flush_grad();
+            if (err_colsum && last && mHasTailGather && !mTailDone &&
+                lin->ComputeGradientColsumGather(*mColPart[l], mTailGather))
+              mTailDone = true;
+            else if (err_colsum)
+              lin->ComputeGradientColsum(*mColPart[l]);
+            else
+              lin->ComputeGradient();
+          }
           submit_layer(lin, last);
         }
       } else if (err_colsum) {

@@ -1973,7 +1973,7 @@ __device__ __forceinline__ void bunch_gather_block(const BunchGatherP& g, const 
 // tnet_affine_update_bias_gather: the update pair kernel's tiles (nb = 0: one update) and ng gather blocks
 // after them.  Blocks are dispatched in index order, so the gather blocks take the CUs the update's tiles
 // leave free (one workgroup per CU: the ring's LDS and 1 wave per SIMD) and run beside the tiles.
-// EPI_STORE_BG: the data-parallel step's last gradient GEMM (tnet_affine_grad_bias_gather), nb = 0.
+// EPI_STORE_BG: the data-parallel step's last gradient GEMM(s) (tnet_affine_grad_bias_gather).
 template <int BM, int BN, int BK, int WM, int WN, int S, int EPI = EPI_SGD_B>
 __global__ __launch_bounds__(WM * WN * 64) __attribute__((amdgpu_waves_per_eu(1, 1)))
 void gemm16_upd_gather_kernel(const GemmP pa, const GemmP pb, const int na, const int nb, const BunchGatherP g) {
@@ -3340,53 +3340,96 @@ extern "C" int tnet_affine_grad_bias(const float* X, TnetMatrixDim dX, const flo
   return launch_gemm<false, false, EPI_STORE_BG>(p, (hipStream_t)stream);
 }
 
-extern "C" int tnet_affine_grad_bias_gather(const float* X, TnetMatrixDim dX, const float* E, TnetMatrixDim dE,
-                                            float* G, TnetMatrixDim dG, const float* colpart, int ldcolpart,
-                                            float* gradB, float* y, const float* x, int* labels_out,
-                                            const int* labels_in, const int* copy_from, TnetMatrixDim dy,
-                                            TnetMatrixDim dx, void* stream) {
-  // tnet_affine_grad_bias and tnet_gather_bunch in one launch (the data-parallel step's last gradient GEMM
-  // with the next bunch's gather on the CUs its tiles leave free: tnet_affine_update_bias_gather's form)
+static int grad_bias_params(GemmP& p, const float* X, TnetMatrixDim dX, const float* E, TnetMatrixDim dE, float* G,
+                            TnetMatrixDim dG, const float* colpart, int ldcolpart, float* gradB) {
   if (dX.rows != dE.rows || dG.rows != dX.cols || dG.cols != dE.cols || !colpart || !gradB || ldcolpart < dE.cols)
     return TNET_ERR_ARG;
-  GemmP p{};
+  p = GemmP{};
   p.M = dX.cols; p.N = dE.cols; p.K = dX.rows;
   p.A = X; p.lda = dX.stride; p.B = E; p.ldb = dE.stride; p.C = G; p.ldc = dG.stride;
   p.alpha = 1.f; p.beta = 0.f;
   p.bpart = colpart; p.ldbpart = ldcolpart; p.bslabs = tnet_colsum_slabs(dE.rows);
   p.bvec = gradB;
-  int st = check_common(p);
+  return check_common(p);
+}
+
+extern "C" int tnet_affine_grad_bias_gather(const float* X, TnetMatrixDim dX, const float* E, TnetMatrixDim dE,
+                                            float* G, TnetMatrixDim dG, const float* colpart, int ldcolpart,
+                                            float* gradB, const float* X2, TnetMatrixDim dX2, const float* E2,
+                                            TnetMatrixDim dE2, float* G2, TnetMatrixDim dG2, const float* colpart2,
+                                            int ldcolpart2, float* gradB2, float* y, const float* x, int* labels_out,
+                                            const int* labels_in, const int* copy_from, TnetMatrixDim dy,
+                                            TnetMatrixDim dx, void* stream) {
+  // tnet_affine_grad_bias (X2 NULL) or two of them, and tnet_gather_bunch, in one launch (the data-parallel step's
+  // last gradient GEMM(s) with the next bunch's gather on the CUs their tiles leave free:
+  // tnet_affine_update_bias_gather's form)
+  GemmP pa, pb{};
+  int st = grad_bias_params(pa, X, dX, E, dE, G, dG, colpart, ldcolpart, gradB);
   if (st) return st;
+  const bool two = X2 != nullptr;
+  if (two) {
+    st = grad_bias_params(pb, X2, dX2, E2, dE2, G2, dG2, colpart2, ldcolpart2, gradB2);
+    if (st) return st;
+    // the two gradients must not feed each other
+    if (any_overlap({span_of(G, dG.rows, dG.stride, 4), span_of(gradB, dG.cols, 1, 4)},
+                    {span_of(X2, dX2.rows, dX2.stride, 4), span_of(E2, dE2.rows, dE2.stride, 4),
+                     span_of(colpart2, pb.bslabs, ldcolpart2, 4), span_of(G2, dG2.rows, dG2.stride, 4),
+                     span_of(gradB2, dG2.cols, 1, 4)}) ||
+        any_overlap({span_of(G2, dG2.rows, dG2.stride, 4), span_of(gradB2, dG2.cols, 1, 4)},
+                    {span_of(X, dX.rows, dX.stride, 4), span_of(E, dE.rows, dE.stride, 4),
+                     span_of(colpart, pa.bslabs, ldcolpart, 4)}))
+      return TNET_ERR_ARG;
+  }
   if (!y || !x || !labels_out || !labels_in || !copy_from || dy.cols != dx.cols || dy.rows < 0 || dy.stride < dy.cols ||
       dx.stride < dx.cols)
     return TNET_ERR_ARG;
-  // the gather independent of the GEMM: it reads X, E and the slab sums, writes G and gradB
-  if (!gather_independent(y, x, labels_out, labels_in, copy_from, dy, dx,
-                          {span_of(p.A, p.K, p.lda, 4), span_of(p.B, p.K, p.ldb, 4), span_of(p.bpart, p.bslabs, p.ldbpart, 4)},
-                          {span_of(p.C, p.M, p.ldc, 4), span_of(p.bvec, p.N, 1, 4)}))
+  // the gather independent of the GEMM(s): they read X, E and the slab sums, write G and gradB
+  auto reads = [](const GemmP& q) {
+    return std::array<ByteSpan, 3>{span_of(q.A, q.K, q.lda, 4), span_of(q.B, q.K, q.ldb, 4),
+                                    span_of(q.bpart, q.bslabs, q.ldbpart, 4)};
+  };
+  auto writes = [](const GemmP& q) {
+    return std::array<ByteSpan, 2>{span_of(q.C, q.M, q.ldc, 4), span_of(q.bvec, q.N, 1, 4)};
+  };
+  const auto ra = reads(pa), rb = reads(pb);
+  const auto wa = writes(pa), wb = writes(pb);
+  if (!gather_independent(y, x, labels_out, labels_in, copy_from, dy, dx, {ra[0], ra[1], ra[2], rb[0], rb[1], rb[2]},
+                          {wa[0], wa[1], wb[0], wb[1]}))
     return TNET_ERR_ARG;
   const int c4 = (dy.cols + 3) & ~3;
   if (((uintptr_t)y & 15) || ((uintptr_t)x & 15) || (dy.stride & 3) || (dx.stride & 3) || c4 > dy.stride ||
       c4 > dx.stride)
     return TNET_ERR_UNSUPPORTED;
   if (forced_cfg() >= 0 || split2_on() || g_split > 0) return TNET_ERR_UNSUPPORTED;
-  if (p.M <= 0 || p.N <= 0) return TNET_ERR_UNSUPPORTED;
-  // what tnet_affine_grad_bias runs alone: the 64x64 configuration, unsplit
-  const GemmPlan pl = plan_gemm<false>(p, epi_splittable(EPI_STORE_BG));
-  if (pl.cfg != CFG_m64x64k32s4w41 || pl.ks != 1) return TNET_ERR_UNSUPPORTED;
-  const int na = cdiv(p.M, 64) * cdiv(p.N, 64);
-  if (4 * (32L * p.lda + p.M) >= (1L << 32) || 4 * (32L * p.ldb + p.N) >= (1L << 32)) return TNET_ERR_UNSUPPORTED;
+  if (pa.M <= 0 || pa.N <= 0 || (two && (pb.M <= 0 || pb.N <= 0))) return TNET_ERR_UNSUPPORTED;
+  int na, nb = 0;
+  if (two) {
+    // both 64x64 grids in one round over the CUs (the update pair's rule)
+    if (!g_pair) return TNET_ERR_UNSUPPORTED;
+    na = cdiv(pa.M, 64) * cdiv(pa.N, 64);
+    nb = cdiv(pb.M, 64) * cdiv(pb.N, 64);
+  } else {
+    // what tnet_affine_grad_bias runs alone: the 64x64 configuration, unsplit
+    const GemmPlan pl = plan_gemm<false>(pa, epi_splittable(EPI_STORE_BG));
+    if (pl.cfg != CFG_m64x64k32s4w41 || pl.ks != 1) return TNET_ERR_UNSUPPORTED;
+    na = cdiv(pa.M, 64) * cdiv(pa.N, 64);
+  }
+  for (const GemmP* q : {&pa, &pb}) {
+    if (q == &pb && !two) break;
+    if (4 * (32L * q->lda + q->M) >= (1L << 32) || 4 * (32L * q->ldb + q->N) >= (1L << 32)) return TNET_ERR_UNSUPPORTED;
+  }
   const int cus = cu_count();
   if (cus <= 0) return TNET_ERR_UNSUPPORTED;
-  const int spare = cus - g_reserve - na;
+  if (two && na + nb > cus - g_reserve) return TNET_ERR_UNSUPPORTED;
+  const int spare = cus - g_reserve - na - nb;
   if (spare < 8) return TNET_ERR_UNSUPPORTED;
   const int ng = spare < 64 ? spare : 64;
-  p.group = g_group > 0 ? g_group : 8;
-  p.early_issue = g_early;
-  p.wt = g_wt;
+  pa.group = pb.group = g_group > 0 ? g_group : 8;
+  pa.early_issue = pb.early_issue = g_early;
+  pa.wt = pb.wt = g_wt;
   BunchGatherP g{y, x, labels_out, labels_in, copy_from, dy.rows, c4, dy.stride, dx.stride};
-  GemmP pb{};
-  gemm16_upd_gather_kernel<64, 64, 32, 4, 1, 4, EPI_STORE_BG><<<na + ng, 256, 0, (hipStream_t)stream>>>(p, pb, na, 0, g);
+  gemm16_upd_gather_kernel<64, 64, 32, 4, 1, 4, EPI_STORE_BG><<<na + nb + ng, 256, 0, (hipStream_t)stream>>>(
+      pa, pb, na, nb, g);
   TNET_LAUNCH_CHECK();
   return TNET_OK;
 }

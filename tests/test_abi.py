@@ -117,7 +117,9 @@ def test_gather_ride_refuses_dependent_operands():
     G, gb = W, b  # the data-parallel form: the gradient and the bias gradient are what the GEMM writes
 
     def grad(y_, x_, lo_, li_, cf_):
-        return L.tnet_affine_grad_bias_gather(X, dX, E, dE, G, dW, P, n_out, gb, y_, x_, lo_, li_, cf_, dy, dx, None)
+        return L.tnet_affine_grad_bias_gather(X, dX, E, dE, G, dW, P, n_out, gb, None, MatrixDim(0, 0, 0), None,
+                                              MatrixDim(0, 0, 0), None, MatrixDim(0, 0, 0), None, 0, None,
+                                              y_, x_, lo_, li_, cf_, dy, dx, None)
     assert grad(y, x, lo, li, cf) != -1
     for bad in (X, E, G, P, gb):
         assert grad(bad, x, lo, li, cf) == -1

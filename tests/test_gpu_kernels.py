@@ -144,6 +144,42 @@ def test_affine_update(mmt, rows, n_in, n_out, gemm_cfg):
         assert np.all(np.abs(dC.numpy() - c) <= 2e-5 * mag + 1e-6)
 
 
+@pytest.mark.parametrize("sides", [[(1024, 135), (598, 1024)], [(2048, 2048), (440, 2048)]])
+def test_affine_grad_pair_gather(sides):
+    """tnet_affine_grad_bias_gather with two gradients (MLP3's last two layers in a data-parallel step) and the next
+    bunch's gather in ONE launch: each G / bias gradient against the fp64 XᵀE and the slab sums (the pair runs the
+    64x64 tiles unsplit, so the standalone call -- split-K for 1024x135 -- is not bit-identical), the gathered rows
+    and class ids exact; TNET_ERR_UNSUPPORTED where the two grids do not fit one round (dnn4's 2048² + 440x2048)"""
+    rows, gcols = 1024, 598
+    Xc = rnd((3000, gcols), 600)
+    labc = (np.arange(3000, dtype=np.int32) * 7) % 4000
+    perm = np.random.default_rng(601).permutation(3000).astype(np.int32)[:1024]
+    host, dev, args = [], [], []
+    for k, (n_in, n_out) in enumerate(sides):
+        X, E = rnd((rows, n_in), 610 + k), rnd((rows, n_out), 620 + k, 0.01)
+        host.append((X, E))
+        d = dict(X=DeviceArray.from_numpy(X), E=DeviceArray.from_numpy(E), P=DeviceArray.from_numpy(slab_sums(E).astype(np.float32)),
+                 G=DeviceArray.from_numpy(np.full((n_in, n_out), np.nan, np.float32)),
+                 gb=DeviceArray.vector(np.full(n_out, np.nan, np.float32)))
+        dev.append(d)
+        args.append([d["X"].ptr, d["X"].dim, d["E"].ptr, d["E"].dim, d["G"].ptr, d["G"].dim, d["P"].ptr, d["P"].stride,
+                     d["gb"].ptr])
+    dXc, dLc, dPerm = DeviceArray.from_numpy(Xc), DeviceArray.vector(labc), DeviceArray.vector(perm)
+    dY = DeviceArray.from_numpy(np.full((1024, gcols), np.nan, np.float32))
+    dLo = DeviceArray.vector(np.full(1024, -7, np.int32))
+    st = lib().tnet_affine_grad_bias_gather(*args[0], *args[1], dY.ptr, dXc.ptr, dLo.ptr, dLc.ptr, dPerm.ptr, dY.dim,
+                                            dXc.dim, S())
+    if sides[0] == (2048, 2048):
+        assert st == TNET_ERR_UNSUPPORTED
+        return
+    check(st)
+    for (X, E), d in zip(host, dev):
+        np.testing.assert_allclose(d["G"].numpy(), X.astype(np.float64).T @ E.astype(np.float64), rtol=1e-4, atol=1e-5)
+        np.testing.assert_allclose(d["gb"].numpy().ravel(), E.astype(np.float64).sum(0), rtol=1e-4, atol=1e-5)
+    np.testing.assert_array_equal(dY.numpy(), Xc[perm])
+    np.testing.assert_array_equal(dLo.numpy()[:, 0], labc[perm])
+
+
 @pytest.mark.parametrize("direct,ring", [("m64x128d4", "m64x128k64s2"), ("m64x128a4", "m64x128k64s2"),
                                          ("m64x128a8", "m64x128k64s2"), ("m128x128d4", "m128x128k64s2"),
                                          ("m128x128a4", "m128x128k64s2"), ("m128x256a2", "m128x256k32s3")])
@@ -849,7 +885,8 @@ def test_affine_grad_bias_gather_matches_separate_calls(rows, n_in, n_out, gcols
         gargs = [dY.ptr, dXc.ptr, dLo.ptr, dLc.ptr, dPerm.ptr, dY.dim, dXc.dim]
         args = [dX.ptr, dX.dim, dE.ptr, dE.dim, dG.ptr, dG.dim, dP.ptr, dP.stride, dgb.ptr]
         if fused:
-            st = lib().tnet_affine_grad_bias_gather(*args, *gargs, S())
+            nil = [None, MatrixDim(0, 0, 0), None, MatrixDim(0, 0, 0), None, MatrixDim(0, 0, 0), None, 0, None]
+            st = lib().tnet_affine_grad_bias_gather(*args, *nil, *gargs, S())
             if n_in == 2048:
                 assert st == TNET_ERR_UNSUPPORTED
                 return
