@@ -724,7 +724,7 @@ __device__ __forceinline__ void gemm16_body(const GemmP& p_in, float* __restrict
   constexpr bool LDR = SP == 2;
   // SP >= 3: the direct form (no LDS ring; see the main loop), DD chunks of 16 k in flight per wave
   constexpr bool DIR = SP >= 3;
-  constexpr int DD = (SP == 3 || SP == 5) ? 4 : SP == 7 ? 2 : 8;
+  constexpr int DD = (SP == 3 || SP == 5 || SP == 9) ? 4 : SP == 7 ? 2 : 8;
   static_assert(SP != 1 || S >= 3, "spread DMA needs a 3-slot ring");
   constexpr int WTM = BM / WM, WTN = BN / WN;  // wave tile
   constexpr int TM = WTM / 16, TN = WTN / 16;
@@ -1222,13 +1222,26 @@ __device__ __forceinline__ void gemm16_body(const GemmP& p_in, float* __restrict
     // run while chunks c+1..c+DD-2 are in flight and the loads of chunk c+DD-1 go out between them, into
     // the slot chunk c-1 used.  No LDS, no LDS-DMA issue cost on the MFMA waves, no seam barrier.
     constexpr int NR = NRA + NRB;
+    // SP >= 5 (a<D> configurations): the ring's loads are inline-asm buffer loads the compiler does not
+    // track, waited for by one counted vmcnt per chunk that also ties the chunk's registers (the compiler's
+    // own waits drain the whole ring at every loop back edge); 16-B loads and 6, 8 or 12 per chunk only
+    constexpr bool ASM = SP >= 5 && (A_KC || VM == 4) && (B_KC || VN == 4) && (NR == 6 || NR == 8 || NR == 12);
+    // SP 8 / 9 (c<D> configurations) with a k-contiguous operand: in read_frags' lane map lane (li, lg) reads
+    // 16 B of row li, so the four lanes of a quad hit four rows and every lane is a request of its own (the
+    // backward's B: 101 vs 78 us direct vs ring).  Here the four lanes of a quad read one row's 64-B chunk
+    // piece (lane 4a + b: row a, k 4b..4b+3) and each lane then takes its fragment from the lane that loaded
+    // it (ds_bpermute, one per dword, issued a chunk ahead between the MFMAs): the same values in the same
+    // registers, so bit-identical to the ring and to the a<D> forms
+    constexpr bool CKC = ASM && SP >= 8 && (A_KC || B_KC);
+    constexpr int NKC = (A_KC ? NRA : 0) + (B_KC ? NRB : 0);  // k-contiguous fragment registers per chunk
+    const int rq = CKC ? lane >> 2 : li, kq = CKC ? lane & 3 : lg;  // the row and 16-B piece a lane loads
     const __amdgpu_buffer_rsrc_t rA = tile_rsrc(p.A), rB = tile_rsrc(p.B);
     unsigned oA[NRA], oB[NRB];
 #pragma unroll
     for (int r = 0; r < NRA; ++r) {
       // rows / columns past the matrix edge read the last valid ones (their outputs are never stored)
       if (A_KC) {
-        oA[r] = 4u * (unsigned)(min(bm + wm0 + 16 * r + li, M - 1) * p.lda + 4 * lg);
+        oA[r] = 4u * (unsigned)(min(bm + wm0 + 16 * r + rq, M - 1) * p.lda + 4 * kq);
       } else {
         const int s2 = r % 4, q = r / 4;
         oA[r] = 4u * (unsigned)((4 * lg + s2) * p.lda + max(min(bm + wm0 + 16 * VM * q + VM * li, M - VM), 0));
@@ -1237,7 +1250,7 @@ __device__ __forceinline__ void gemm16_body(const GemmP& p_in, float* __restrict
 #pragma unroll
     for (int r = 0; r < NRB; ++r) {
       if (B_KC) {
-        oB[r] = 4u * (unsigned)(min(bn + wn0 + 16 * r + li, N - 1) * p.ldb + 4 * lg);
+        oB[r] = 4u * (unsigned)(min(bn + wn0 + 16 * r + rq, N - 1) * p.ldb + 4 * kq);
       } else {
         const int s2 = r % 4, q = r / 4;
         oB[r] = 4u * (unsigned)((4 * lg + s2) * p.ldb + max(min(bn + wn0 + 16 * VN * q + VN * li, N - VN), 0));
@@ -1245,10 +1258,6 @@ __device__ __forceinline__ void gemm16_body(const GemmP& p_in, float* __restrict
     }
     const int cA = A_KC ? 64 : 64 * p.lda, cB = B_KC ? 64 : 64 * p.ldb;  // bytes per chunk
     const int nch = nfull * KCH;
-    // SP >= 5 (a<D> configurations): the ring's loads are inline-asm buffer loads the compiler does not
-    // track, waited for by one counted vmcnt per chunk that also ties the chunk's registers (the compiler's
-    // own waits drain the whole ring at every loop back edge); 16-B loads and 6 or 8 per chunk only
-    constexpr bool ASM = SP >= 5 && (A_KC || VM == 4) && (B_KC || VN == 4) && (NR == 6 || NR == 8 || NR == 12);
     if constexpr (ASM) {
       const unsigned long long ba = (unsigned long long)(uintptr_t)p.A, bb = (unsigned long long)(uintptr_t)p.B;
       const u32x4 dA = {(unsigned)ba, (unsigned)(ba >> 32), 0x7FFFFFF0u, 0x00020000u};
@@ -1277,17 +1286,35 @@ __device__ __forceinline__ void gemm16_body(const GemmP& p_in, float* __restrict
                          "+v"(q[8]), "+v"(q[9]), "+v"(q[10]), "+v"(q[11])
                        : "n"(WV));
       };
+      // CKC: lane (li, lg) takes its fragment from lane 4 li + lg; the t-th k-contiguous register of a slot
+      const int pperm = 4 * (4 * li + lg);
+      auto perm = [&](f32x4& v) {
+        f32x4 o;
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          o[e] = __int_as_float(__builtin_amdgcn_ds_bpermute(pperm, __float_as_int(v[e])));
+        v = o;
+      };
+      auto kc_reg = [](int t) { return A_KC ? t : NRA + t; };
+      static_assert(!CKC || 4 * TM * TN >= NR + NKC, "a chunk's MFMAs cover its loads and the next one's permutes");
 #pragma unroll
       for (int j = 0; j < DD - 1; ++j)
 #pragma unroll
         for (int r = 0; r < NR; ++r) ring[j][r] = ld(min(j, nch - 1), r);
+      if constexpr (CKC) {
+        wait_slot(ring[0]);
+#pragma unroll
+        for (int t = 0; t < NKC; ++t) perm(ring[0][kc_reg(t)]);
+      }
       for (int c0 = 0; c0 < nch; c0 += DD) {
 #pragma unroll
         for (int j = 0; j < DD; ++j) {
           const int cn = min(c0 + j + DD - 1, nch - 1);  // past the end: a repeat of the last chunk, never used
-          __builtin_amdgcn_sched_barrier(0);  // the wait stays after the previous chunk's MFMAs
-          wait_slot(ring[j]);
-          __builtin_amdgcn_sched_barrier(0);
+          if constexpr (!CKC) {
+            __builtin_amdgcn_sched_barrier(0);  // the wait stays after the previous chunk's MFMAs
+            wait_slot(ring[j]);
+            __builtin_amdgcn_sched_barrier(0);
+          }
           int mi = 0;
 #pragma unroll
           for (int s2 = 0; s2 < 4; ++s2)
@@ -1302,6 +1329,19 @@ __device__ __forceinline__ void gemm16_body(const GemmP& p_in, float* __restrict
                   __builtin_amdgcn_sched_barrier(0);
                   ring[(j + DD - 1) % DD][mi] = ld(cn, mi);
                   __builtin_amdgcn_sched_barrier(0);
+                }
+                if constexpr (CKC) {
+                  // the next chunk: its loads are DD - 2 chunks old once this chunk's are out (the same
+                  // count the a<D> forms wait for at the chunk's head); then its permutes between the MFMAs
+                  if (mi == NR - 1) {
+                    __builtin_amdgcn_sched_barrier(0);
+                    wait_slot(ring[(j + 1) % DD]);
+                    __builtin_amdgcn_sched_barrier(0);
+                  } else if (mi >= NR && mi < NR + NKC) {
+                    __builtin_amdgcn_sched_barrier(0);
+                    perm(ring[(j + 1) % DD][kc_reg(mi - NR)]);
+                    __builtin_amdgcn_sched_barrier(0);
+                  }
                 }
                 ++mi;
               }
@@ -1900,15 +1940,16 @@ void gemm16_kernel(const GemmP p_in) {
 // update writes W_l, the backward reads W_{l-1}): the blocks are dispatched in index order, so B's
 // workgroups start on the CUs A's finish on -- B's operand fill overlaps A's epilogue stores and tail
 // instead of waiting for a kernel boundary, A's end-of-kernel drain and B's start-up spread.
-// SPA: GEMM A's form (0: the LDS ring, 5: the direct form -- TNET_GEMM_DIRECT)
+// SPA: GEMM A's form (0: the LDS ring, 5: the direct form -- TNET_GEMM_DIRECT); SPB: GEMM B's (0, or 8: the
+// direct form with coalesced k-contiguous loads -- TNET_GEMM_KC)
 template <int BMA, int BNA, bool AKA, bool BKA, int EPIA, bool PXA, int BMB, int BNB, bool AKB, bool BKB, int EPIB,
-          bool PXB, int SPA = 0>
+          bool PXB, int SPA = 0, int SPB = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
 void gemm16_pair_kernel(const GemmP pa, const GemmP pb, const int na) {
   constexpr int SA = gemm16_smem_floats<BMA, BNA, 64, 2, EPIA, PXA>(), SB = gemm16_smem_floats<BMB, BNB, 64, 2, EPIB, PXB>();
   __shared__ __attribute__((aligned(16))) float smem[SA > SB ? SA : SB];
   if ((int)blockIdx.x < na) gemm16_body<BMA, BNA, 64, 2, 2, 2, SPA, AKA, BKA, EPIA, PXA>(pa, smem, blockIdx.x);
-  else gemm16_body<BMB, BNB, 64, 2, 2, 2, 0, AKB, BKB, EPIB, PXB>(pb, smem, (int)blockIdx.x - na);
+  else gemm16_body<BMB, BNB, 64, 2, 2, 2, SPB, AKB, BKB, EPIB, PXB>(pb, smem, (int)blockIdx.x - na);
 }
 
 // Two independent SMALL weight updates (fused SGD + bias SGD, TN) in ONE launch, same tile
@@ -1988,14 +2029,14 @@ void gemm16_upd_gather_kernel(const GemmP pa, const GemmP pb, const int na, cons
 // na tiles) and the slab sums of its OWN input error E (the softmax error: the top layer's bias gradient,
 // colsum_partial blocks after the tiles).  Independent (the GEMM reads E, the blocks read E); the blocks
 // take the CUs as the tiles finish instead of a launch of their own before the GEMM.
-template <bool PX>
+template <bool PX, int SP = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
 void gemm16_bwd_slabs_kernel(const GemmP p, const int na, const float* __restrict__ Et, const TnetMatrixDim dEt,
                              float* __restrict__ cpt, const long ldcpt, const int slabs, const int ncb) {
   __shared__ __attribute__((aligned(16))) float smem[gemm16_smem_floats<64, 128, 64, 2, EPI_DSIG_CS, PX>()];
   const int b = blockIdx.x;
   if (b < na) {
-    gemm16_body<64, 128, 64, 2, 2, 2, 0, true, true, EPI_DSIG_CS, PX>(p, smem, b);
+    gemm16_body<64, 128, 64, 2, 2, 2, SP, true, true, EPI_DSIG_CS, PX>(p, smem, b);
   } else {
     const int c = b - na;
     colsum_partial_block<true>(Et, dEt, cpt, slabs, 0x7fffffff, ldcpt, c % ncb, c / ncb, smem);
@@ -2249,6 +2290,8 @@ static unsigned* splitk_counters(size_t n, hipStream_t st) {
   X(m64x128a8, 1, 64, 128, 64, 2, 2, 2, 6)              \
   X(m128x128a4, 1, 128, 128, 64, 2, 2, 2, 5)            \
   X(m128x256a2, 1, 128, 256, 32, 2, 2, 3, 7)            \
+  X(m64x128c8, 1, 64, 128, 64, 2, 2, 2, 8)              \
+  X(m64x128c4, 1, 64, 128, 64, 2, 2, 2, 9)              \
   X(m128x256k32s3, 1, 128, 256, 32, 2, 2, 3, 0)         \
   X(m64x64k64s2, 1, 64, 64, 64, 2, 2, 2, 0)             \
   X(m64x64k32s4, 1, 64, 64, 32, 2, 2, 4, 0)             \
@@ -2290,6 +2333,12 @@ static int g_reserve = 0, g_cus = 0;
 // (134.6 -> 126.3 us, dnn4 1005 k -> 1015 k, profiles/r04_gemm_direct_128x256_ab.jsonl); 2: m64x128d4 /
 // m128x128d4 (compiler-tracked loads); 3: m64x128a4 / m128x128a4; 0: the LDS ring everywhere
 static int g_direct = -1;
+// TNET_GEMM_KC: the backward GEMMs (k-contiguous A and B, 64x128 tiles) in the direct form with coalesced loads,
+// m64x128c8, instead of the LDS ring -- 1 (default): the top layer's (1024 x 2048 over K = 4000, with its own
+// slab sums, tnet_affine_bwd_colsum_slabs): 135.1 -> 133.0 us in the SGD step; 2: also the 2048^2 backward
+// alone (71.3 -> 72.5 us, slower) and in the update + backward pair (67.2 -> 67.1 us); 0: the ring everywhere
+// (profiles/r04_gemm_kc_ab.json)
+static int g_kc = -1;
 static int g_wt = 1;  // TNET_GEMM_WT=0: plain 16-B epilogue stores instead of write-through (sc1; measured +1.4 % frames/s)
 static int forced_cfg() {
   if (g_cfg == -2) {
@@ -2314,6 +2363,8 @@ static int forced_cfg() {
     if (il) g_inlaunch = atoi(il);
     const char* dr = getenv("TNET_GEMM_DIRECT");
     g_direct = dr ? atoi(dr) : 4;
+    const char* kc = getenv("TNET_GEMM_KC");
+    g_kc = kc ? atoi(kc) : 1;
 
   }
   return g_cfg;
@@ -2365,7 +2416,7 @@ static bool launch_cfg(const GemmP& p, hipStream_t st) {
       auto a16p = [](const void* v) { return ((uintptr_t)v & 15) == 0; };
       // (an m / n-contiguous operand's 16-B vectors are either wholly inside or wholly past the edge:
       // M / N a multiple of 4 there)
-      if (p.ksplit > 1 || nfull < 1 || (!A_KC && p.M % 4) || (!B_KC && p.N % 4) || ((IL == 4 || IL == 6) && nfull % 2) ||
+      if (p.ksplit > 1 || nfull < 1 || (!A_KC && p.M % 4) || (!B_KC && p.N % 4) || ((IL == 4 || IL == 6 || IL == 8) && nfull % 2) ||
           (p.lda & 3) || (p.ldb & 3) || !a16p(p.A) ||
           !a16p(p.B) || 4 * (A_KC ? (long)p.M * p.lda : (long)p.K * p.lda) >= (1L << 31) ||
           4 * (B_KC ? (long)p.N * p.ldb : (long)p.K * p.ldb) >= (1L << 31))
@@ -2380,6 +2431,16 @@ static bool launch_cfg(const GemmP& p, hipStream_t st) {
     gemm16_kernel<BM, BN, BK, WM, WN, S, IL, A_KC, B_KC, EPI><<<grid, (WM * WN + (IL == 2)) * 64, 0, st>>>(q);
     return true;
   }
+}
+
+// a 64x128 backward grid (k-contiguous A and B) may run m64x128c8 (TNET_GEMM_KC; launch_cfg's direct-form
+// conditions: whole k-tiles in an even count, 16-B aligned operands, 31-bit offsets)
+static bool kc_direct(const GemmP& p) {
+  forced_cfg();
+  auto a16p = [](const void* v) { return ((uintptr_t)v & 15) == 0; };
+  const int nfull = p.K / 64;
+  return g_kc > 0 && p.ksplit <= 1 && nfull >= 1 && nfull % 2 == 0 && !(p.lda & 3) && !(p.ldb & 3) && a16p(p.A) &&
+         a16p(p.B) && 4L * p.M * p.lda < (1L << 31) && 4L * p.N * p.ldb < (1L << 31);
 }
 
 static void cfg_shape(int cfg, int* bm, int* bn, int* kind) {
@@ -2562,6 +2623,7 @@ static int launch_splitk(const GemmP& p, int cfg, int ks, hipStream_t st) {
 static int launch_colsum_bwd(const GemmP& p_in, hipStream_t st) {
   if (p_in.M <= 0 || p_in.N <= 0) return TNET_OK;
   int cfg = forced_cfg();
+  const bool autocfg = cfg < 0;
   GemmP p = p_in;
   p.group = g_group > 0 ? g_group : 8;
   if (cfg != CFG_m64x128k64s2 && cfg != CFG_m64x64k32s4 && cfg != CFG_m64x64k64s2)
@@ -2571,7 +2633,9 @@ static int launch_colsum_bwd(const GemmP& p_in, hipStream_t st) {
     return TNET_OK;
   }
   bool ok = false;
-  if (cfg == CFG_m64x128k64s2) ok = launch_cfg<1, 64, 128, 64, 2, 2, 2, 0, true, true, EPI_DSIG_CS>(p, st);
+  if (cfg == CFG_m64x128k64s2 && autocfg && g_kc >= 2)
+    ok = launch_cfg<1, 64, 128, 64, 2, 2, 2, 8, true, true, EPI_DSIG_CS>(p, st);  // (the ring where it must)
+  else if (cfg == CFG_m64x128k64s2) ok = launch_cfg<1, 64, 128, 64, 2, 2, 2, 0, true, true, EPI_DSIG_CS>(p, st);
   else if (cfg == CFG_m64x64k64s2) ok = launch_cfg<1, 64, 64, 64, 2, 2, 2, 0, true, true, EPI_DSIG_CS>(p, st);
   else ok = launch_cfg<1, 64, 64, 32, 2, 2, 4, 0, true, true, EPI_DSIG_CS>(p, st);
   if (!ok) return TNET_ERR_UNSUPPORTED;
@@ -2660,6 +2724,7 @@ static int launch_gemm(const GemmP& p_in, hipStream_t st) {
     else if (cfg == CFG_m128x128k64s2) rcfg = g_direct == 2 ? CFG_m128x128d4 : CFG_m128x128a4;
     else if (cfg == CFG_m128x256k32s3 && g_direct == 4) rcfg = CFG_m128x256a2;  // 4: 1 + the 128x256 update
   }
+  if (g_kc >= 2 && forced_cfg() < 0 && A_KC && B_KC && cfg == CFG_m64x128k64s2) rcfg = CFG_m64x128c8;
   bool ok = false;
   switch (rcfg) {
 #define X(name, KIND, BM, BN, BK, WM, WN, S, IL) \
@@ -2678,6 +2743,16 @@ static int launch_gemm(const GemmP& p_in, hipStream_t st) {
 // planner gives it) and an independent backward GEMM (B: diff-sigmoid + slab sums, 64x128) as one
 // gemm16_pair_kernel launch; TNET_ERR_UNSUPPORTED where either would run another configuration (the
 // caller then makes the two calls)
+template <int EPIA, bool PXA, int SPA>
+static void pair_go(const GemmP& pu, const GemmP& pb, int na, int nb, bool kc, hipStream_t st) {
+  if (kc)
+    gemm16_pair_kernel<128, 128, false, false, EPIA, PXA, 64, 128, true, true, EPI_DSIG_CS, true, SPA, 8>
+        <<<na + nb, 256, 0, st>>>(pu, pb, na);
+  else
+    gemm16_pair_kernel<128, 128, false, false, EPIA, PXA, 64, 128, true, true, EPI_DSIG_CS, true, SPA>
+        <<<na + nb, 256, 0, st>>>(pu, pb, na);
+}
+
 template <int EPIA>
 static int launch_pair_a_bwd(GemmP pu, GemmP pb, hipStream_t st) {
   // EPI_STORE_BG (the data-parallel gradient): not while CUs are reserved for RCCL (the exchange window runs the
@@ -2704,21 +2779,12 @@ static int launch_pair_a_bwd(GemmP pu, GemmP pb, hipStream_t st) {
                    pu.M % 4 == 0 && pu.N % 4 == 0 &&
                    4 * ((long)pu.K * pu.lda) < (1L << 31) && 4 * ((long)pu.K * pu.ldb) < (1L << 31);
   const bool px = px_exact<128, 128, EPIA>(pu);
-  if (dir && px && g_direct == 2)
-    gemm16_pair_kernel<128, 128, false, false, EPIA, true, 64, 128, true, true, EPI_DSIG_CS, true, 3>
-        <<<na + nb, 256, 0, st>>>(pu, pb, na);
-  else if (dir && px)
-    gemm16_pair_kernel<128, 128, false, false, EPIA, true, 64, 128, true, true, EPI_DSIG_CS, true, 5>
-        <<<na + nb, 256, 0, st>>>(pu, pb, na);
-  else if (dir)
-    gemm16_pair_kernel<128, 128, false, false, EPIA, false, 64, 128, true, true, EPI_DSIG_CS, true, 5>
-        <<<na + nb, 256, 0, st>>>(pu, pb, na);
-  else if (px)
-    gemm16_pair_kernel<128, 128, false, false, EPIA, true, 64, 128, true, true, EPI_DSIG_CS, true>
-        <<<na + nb, 256, 0, st>>>(pu, pb, na);
-  else
-    gemm16_pair_kernel<128, 128, false, false, EPIA, false, 64, 128, true, true, EPI_DSIG_CS, true>
-        <<<na + nb, 256, 0, st>>>(pu, pb, na);
+  const bool kc = g_kc >= 2 && kc_direct(pb);  // the backward half in the coalesced k-contiguous direct form
+  if (dir && px && g_direct == 2) pair_go<EPIA, true, 3>(pu, pb, na, nb, kc, st);
+  else if (dir && px) pair_go<EPIA, true, 5>(pu, pb, na, nb, kc, st);
+  else if (dir) pair_go<EPIA, false, 5>(pu, pb, na, nb, kc, st);
+  else if (px) pair_go<EPIA, true, 0>(pu, pb, na, nb, kc, st);
+  else pair_go<EPIA, false, 0>(pu, pb, na, nb, kc, st);
   TNET_LAUNCH_CHECK();
   return TNET_OK;
 }
@@ -3099,7 +3165,9 @@ extern "C" int tnet_affine_bwd_colsum_slabs(const float* E, TnetMatrixDim dE, co
   p.wt = g_wt;
   const int na = cdiv(p.M, 64) * cdiv(p.N, 128), ncb = cdiv(dE.cols, CS_COLS * 4);
   const unsigned grid = (unsigned)(na + ncb * slabs);
-  if (px_exact<64, 128, EPI_DSIG_CS>(p))
+  if (px_exact<64, 128, EPI_DSIG_CS>(p) && kc_direct(p))
+    gemm16_bwd_slabs_kernel<true, 8><<<grid, 256, 0, (hipStream_t)stream>>>(p, na, E, dE, colpartE, ldcolpartE, slabs, ncb);
+  else if (px_exact<64, 128, EPI_DSIG_CS>(p))
     gemm16_bwd_slabs_kernel<true><<<grid, 256, 0, (hipStream_t)stream>>>(p, na, E, dE, colpartE, ldcolpartE, slabs, ncb);
   else
     gemm16_bwd_slabs_kernel<false><<<grid, 256, 0, (hipStream_t)stream>>>(p, na, E, dE, colpartE, ldcolpartE, slabs, ncb);
