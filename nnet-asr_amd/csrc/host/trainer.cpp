@@ -398,6 +398,15 @@ static int rccl_channels() {
   if (channels > 0) setenv("NCCL_MAX_NCHANNELS", std::to_string(channels).c_str(), 0);
   return channels;
 }
+// The exchange's stream-ordering events (compute -> comm -> apply -> compute): every consumer is a stream of
+// this device (RCCL's kernels, the applies, the next GEMMs), and a kernel's completion already releases its
+// stores at device scope, so the events are recorded without HIP's default system-scope fence (L2 write-back
+// + invalidate at every record: the one-rank DP step showed 6-26 us compute-stream bubbles at each of the
+// step's exchange points, profiles/r04_dp_event_fence_ab.json).  TNET_DP_EVENT_FENCE=1: the default fence.
+static unsigned exchange_event_flags() {
+  static const bool fence = getenv("TNET_DP_EVENT_FENCE") && getenv("TNET_DP_EVENT_FENCE")[0] == '1';
+  return hipEventDisableTiming | (fence ? 0u : (unsigned)hipEventDisableSystemFence);
+}
 static int rccl_reserve(int world) {
   const int channels = rccl_channels();
   const char* rv = getenv("TNET_DP_RESERVE_CUS");  // explicit: also at world 1 (tests)
@@ -421,8 +430,8 @@ RcclExchange::RcclExchange(int rank, int world, const char id[128])
   NCCL_CALL(ncclCommInitRank(&mImpl->comm, world, uid, rank));
   TNET_HIP_CALL(hipStreamCreateWithFlags(&mImpl->comm_stream, hipStreamNonBlocking));
   TNET_HIP_CALL(hipStreamCreateWithFlags(&mImpl->apply_stream, hipStreamNonBlocking));
-  TNET_HIP_CALL(hipEventCreateWithFlags(&mImpl->done, hipEventDisableTiming));
-  TNET_HIP_CALL(hipEventCreateWithFlags(&mImpl->apply_done, hipEventDisableTiming));
+  TNET_HIP_CALL(hipEventCreateWithFlags(&mImpl->done, exchange_event_flags()));
+  TNET_HIP_CALL(hipEventCreateWithFlags(&mImpl->apply_done, exchange_event_flags()));
   TNET_HIP_CALL(hipMalloc(&mImpl->dscratch, 4096));
   (void)dev;
   check_same_shard_mode(*this, mShard, mWorld);
@@ -447,8 +456,8 @@ void RcclExchange::Submit(CuUpdatableComponent& comp) {
   CuDevice& dev = CuDevice::Instantiate();
   if (mImpl->next_event >= mImpl->events.size()) {
     hipEvent_t e, d;
-    TNET_HIP_CALL(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    TNET_HIP_CALL(hipEventCreateWithFlags(&d, hipEventDisableTiming));
+    TNET_HIP_CALL(hipEventCreateWithFlags(&e, exchange_event_flags()));
+    TNET_HIP_CALL(hipEventCreateWithFlags(&d, exchange_event_flags()));
     mImpl->events.push_back(e);
     mImpl->ar_done.push_back(d);
   }
@@ -489,7 +498,7 @@ void RcclExchange::GatherParams(CuUpdatableComponent& comp, int i, void* stream)
   // place: the next collectives queue behind it, the compute stream joins at WaitAll
   while (mImpl->gather_ev.size() <= (size_t)i) {
     hipEvent_t e;
-    TNET_HIP_CALL(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    TNET_HIP_CALL(hipEventCreateWithFlags(&e, exchange_event_flags()));
     mImpl->gather_ev.push_back(e);
   }
   hipEvent_t ev = mImpl->gather_ev[(size_t)i];
