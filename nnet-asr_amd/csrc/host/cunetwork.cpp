@@ -398,10 +398,11 @@ void CuNetwork::TrainBunch(const CuMatrix<BaseFloat>& X, const CuVector<int>& la
   // Data parallel: a layer's reduction submitted, and its SGD apply right behind it (beside the backward GEMMs
   // below: W_l is read for the last time by this layer's backward GEMM, already enqueued) -- the step's last layer
   // on the compute stream (nothing is left to overlap it with, and the apply stream would add a hop in and a join
-  // out)
+  // out; TNET_DP_LAST_APPLY_STREAM=1: on the apply stream too, A/B)
+  static const bool last_on_apply = getenv("TNET_DP_LAST_APPLY_STREAM") && getenv("TNET_DP_LAST_APPLY_STREAM")[0] == '1';
   auto submit_layer = [&](CuBiasedLinearity* lin, bool last) {
     exchange->Submit(*lin);
-    void* as = submitted.empty() && !last ? exchange->ApplyStream(n_submitted) : nullptr;
+    void* as = submitted.empty() && (!last || last_on_apply) ? exchange->ApplyStream(n_submitted) : nullptr;
     if (as) {
       lin->ApplyGradient(grows, as, exchange);
       exchange->GatherParams(*lin, n_submitted, as);  // sharded apply: the other ranks' shards

@@ -380,6 +380,12 @@ struct RcclExchange::Impl {
   bool applied = false;
   std::vector<hipEvent_t> gather_ev;  // apply stream -> comm stream (a layer's shard applied), per submit
   double* dscratch = nullptr;
+  // the comm stream's work in enqueue order (1, 2, ... per Submit / GatherParams), the position each
+  // submission's ar_done marks, and how far the compute / apply stream has already waited: WaitAll skips its
+  // own comm-stream wait when a stream it joins has covered everything (each wait is a barrier packet on the
+  // compute queue, ~5.5 us even when satisfied: profiles/r04_dp_event_fence_ab.json)
+  unsigned long comm_seq = 0, compute_covered = 0, apply_covered = 0;
+  std::vector<unsigned long> ar_seq;
 };
 
 // RCCL channels and the CUs reserved for them.  RCCL runs one workgroup per channel (512 threads,
@@ -460,6 +466,7 @@ void RcclExchange::Submit(CuUpdatableComponent& comp) {
     TNET_HIP_CALL(hipEventCreateWithFlags(&d, exchange_event_flags()));
     mImpl->events.push_back(e);
     mImpl->ar_done.push_back(d);
+    mImpl->ar_seq.push_back(0);
   }
   const size_t idx = mImpl->next_event++;
   if (idx == 0 && mReserve > 0) TNET_SAFE_CALL(tnet_gemm_reserve(mReserve));
@@ -485,6 +492,7 @@ void RcclExchange::Submit(CuUpdatableComponent& comp) {
   }
   NCCL_CALL(ncclGroupEnd());
   TNET_HIP_CALL(hipEventRecord(mImpl->ar_done[idx], mImpl->comm_stream));
+  mImpl->ar_seq[idx] = ++mImpl->comm_seq;
 }
 
 int RcclExchange::ApplyRanges(long n, long* lo, long* hi) const {
@@ -512,12 +520,14 @@ void RcclExchange::GatherParams(CuUpdatableComponent& comp, int i, void* stream)
                               mImpl->comm_stream));
   }
   NCCL_CALL(ncclGroupEnd());
+  ++mImpl->comm_seq;
 }
 
 void RcclExchange::WaitFor(int i) {
   CuDevice::Instantiate().KTCloseRun();  // no roofline timing run spans an exchange step
   if (i < 0 || (size_t)i >= mImpl->next_event) Error("RcclExchange::WaitFor: no such reduction");
   TNET_HIP_CALL(hipStreamWaitEvent(CuDevice::Instantiate().Stream(), mImpl->ar_done[(size_t)i], 0));
+  mImpl->compute_covered = std::max(mImpl->compute_covered, mImpl->ar_seq[(size_t)i]);
 }
 
 void* RcclExchange::ApplyStream(int i) {
@@ -525,6 +535,7 @@ void* RcclExchange::ApplyStream(int i) {
   if (off) return nullptr;  // A/B: the applies on the compute stream after WaitFor (round-1 form)
   if (i < 0 || (size_t)i >= mImpl->next_event) Error("RcclExchange::ApplyStream: no such reduction");
   TNET_HIP_CALL(hipStreamWaitEvent(mImpl->apply_stream, mImpl->ar_done[(size_t)i], 0));
+  mImpl->apply_covered = std::max(mImpl->apply_covered, mImpl->ar_seq[(size_t)i]);
   mImpl->applied = true;
   return (void*)mImpl->apply_stream;
 }
@@ -532,13 +543,21 @@ void* RcclExchange::ApplyStream(int i) {
 void RcclExchange::WaitAll() {
   CuDevice::Instantiate().KTCloseRun();  // no roofline timing run spans an exchange step
   CuDevice& dev = CuDevice::Instantiate();
-  TNET_HIP_CALL(hipEventRecord(mImpl->done, mImpl->comm_stream));
-  TNET_HIP_CALL(hipStreamWaitEvent(dev.Stream(), mImpl->done, 0));
+  // the comm stream's work is already behind the compute stream when it (or the apply stream it joins below)
+  // waited for the comm stream's last enqueued operation (TNET_DP_WAITALL_COMM=1: wait anyway, A/B)
+  static const bool always = getenv("TNET_DP_WAITALL_COMM") && getenv("TNET_DP_WAITALL_COMM")[0] == '1';
+  const bool covered = mImpl->compute_covered == mImpl->comm_seq ||
+                       (mImpl->applied && mImpl->apply_covered == mImpl->comm_seq);
+  if (always || !covered) {
+    TNET_HIP_CALL(hipEventRecord(mImpl->done, mImpl->comm_stream));
+    TNET_HIP_CALL(hipStreamWaitEvent(dev.Stream(), mImpl->done, 0));
+  }
   if (mImpl->applied) {
     TNET_HIP_CALL(hipEventRecord(mImpl->apply_done, mImpl->apply_stream));
     TNET_HIP_CALL(hipStreamWaitEvent(dev.Stream(), mImpl->apply_done, 0));
     mImpl->applied = false;
   }
+  mImpl->comm_seq = mImpl->compute_covered = mImpl->apply_covered = 0;
   mImpl->next_event = 0;
   if (mReserve > 0) TNET_SAFE_CALL(tnet_gemm_reserve(0));
 }
