@@ -138,7 +138,10 @@ CuDevice::~CuDevice() {
 hipEvent_t CuDevice::KTEvent() {
   if (mKTNext >= mKTPool.size()) {
     hipEvent_t e;
-    TNET_HIP_CALL(hipEventCreate(&e));
+    // timing only (no host inspection of the kernels' memory): without HIP's system-scope fence, whose L2
+    // write-back + invalidate at every record would slow the timed kernels (and start them cold) in a way the
+    // untimed step does not see
+    TNET_HIP_CALL(hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
     mKTPool.push_back(e);
   }
   return mKTPool[mKTNext++];

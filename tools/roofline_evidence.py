@@ -31,11 +31,11 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 # (round 3: a trailing ", true" = the exact-prefetch instantiation, PX)
-# (round 4: the form parameter SP -- 0 the LDS ring, 3..6 the direct forms -- and the pair kernel's form of its
-# update half)
+# (round 4: the form parameter SP -- 0 the LDS ring, 3..9 the direct forms -- and the pair kernel's forms of its
+# update half and its backward half)
 FWD = re.compile(r"gemm16_kernel<64, 128, 64, 2, 2, 2, \d+, true, false, 2(, (true|false))?>")    # bias + sigmoid
 BWD = re.compile(r"gemm16_kernel<64, 128, 64, 2, 2, 2, \d+, true, true, 8(, (true|false))?>")     # diff-sigmoid + sums
-PAIR = re.compile(r"gemm16_pair_kernel<128, 128, false, false, 9, (true|false), 64, 128, true, true, 8, true(, \d+)?>")
+PAIR = re.compile(r"gemm16_pair_kernel<128, 128, false, false, 9, (true|false), 64, 128, true, true, 8, true(, \d+)*>")
 UPD = re.compile(r"gemm16_kernel<128, 128, 64, 2, 2, 2, \d+, false, false, 9(, (true|false))?>")  # SGD + bias SGD
 
 
@@ -50,6 +50,11 @@ def classify_trace(path):
         grid = int(r["Grid_Size_X"])
         if "softmax_xent" in name:
             after_softmax = True
+            continue
+        # the top layer's backward (K = 4000) with its own slab sums, round 3+: gemm16_bwd_slabs_kernel -- then
+        # the next diff-sigmoid launch is the 2048^2 backward (the plain BWD below), not the K = 4000 one
+        if "gemm16_bwd_slabs_kernel" in name:
+            after_softmax = False
             continue
         # the bunch gather: its own launch, or (round 3, tnet_affine_update_bias_gather) riding on the
         # previous step's last update launch (the 440x2048 update, not a roofline GEMM)
