@@ -145,6 +145,25 @@ def dp_mode(world):
     return (" (RCCL reduce-scatter, sharded SGD apply, all-gather)" if shard else " (RCCL all-reduce)")
 
 
+def prewarm(ms):
+    """Scratch GEMMs of the step's own 2048^2 shape on the library stream for `ms` of wall time (synchronised
+    every 8 launches), on buffers of their own: the GPU leaves its idle clock state before the warm-up steps,
+    and nothing of the training state (weights, cache, generator) is touched.  Returns the time spent (ms)."""
+    if ms <= 0:
+        return 0.0
+    S = lib().tnet_stream()
+    A, Bm, C = (tnet_amd.DeviceArray(1024, 2048), tnet_amd.DeviceArray(2048, 2048), tnet_amd.DeviceArray(1024, 2048))
+    t0 = time.perf_counter()
+    while (time.perf_counter() - t0) * 1e3 < ms:
+        for _ in range(8):
+            check(lib().tnet_sgemm(b"N", b"N", 1024, 2048, 2048, 1.0, A.ptr, A.stride, Bm.ptr,
+                                   Bm.stride, 0.0, C.ptr, C.stride, S), "prewarm sgemm")
+        tnet_amd.synchronize()
+    spent = (time.perf_counter() - t0) * 1e3
+    del A, Bm, C
+    return spent
+
+
 def main():
     # stdout carries exactly the one JSON result line: the native libraries' own prints (RCCL's version
     # banner at communicator creation, on every rank) go to stderr with everything else
@@ -175,6 +194,12 @@ def main():
                     help="hipEvent timing in the roofline region (K steps after the timed region): 0 off, 1 the "
                          "roofline kernels (2048x2048 GEMMs), one event pair per RUN of back-to-back roofline "
                          "launches (each pair costs stream time), 2 a pair around every roofline launch")
+    ap.add_argument("--prewarm-ms", type=float, default=200.0,
+                    help="before the warm-up steps: this long of scratch 1024x2048x2048 GEMMs (no training state "
+                         "touched) to bring the GPU out of its idle clock state -- from idle the step takes 1.17 ms "
+                         "and settles at 1.01 ms only after ~20 ms of load (profiles/r04_warmup_trace.json), longer "
+                         "than a 5-step warm-up (20 / 5 window: 966-982 k without, 994-999 k at 40 ms, 1.007-1.009 M at 200 ms; 100 / 20:
+                         1.020 M -- profiles/r04_prewarm_ab.json); 0: off")
     ap.add_argument("--breakdown-steps", type=int, default=20,
                     help="extra steps after the timed region with every launch event-timed (kernels field)")
     args = ap.parse_args()
@@ -237,6 +262,7 @@ def main():
         if dist is not None:
             dist.barrier()
 
+    prewarm_ms = prewarm(args.prewarm_ms)
     trainer.replay(args.warmup)
     barrier()
     # timed region: K steps, no events on the stream (value, ms_per_step)
@@ -335,6 +361,9 @@ def main():
                        f"training frames/sec (whole node), {'x'.join(map(str, dims))} MLP"),
             "value": round(value, 1), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
+            "prewarm": {"ms": round(prewarm_ms, 1), "what": "scratch 1024x2048x2048 GEMMs before the warm-up steps "
+                        "(no training state touched): the GPU out of its idle clock state, whose ramp outlasts a "
+                        "5-step warm-up (profiles/r04_warmup_trace.json)"},
             "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
             "config": {"workload": f"TNet SGD step, {'x'.join(map(str, dims))} sigmoid MLP + softmax xent",
                        "bunch_per_gpu": B, "global_bunch": B * world, "frames_resident_per_gpu": args.cache,
