@@ -198,8 +198,8 @@ def main():
                     help="before the warm-up steps: this long of scratch 1024x2048x2048 GEMMs (no training state "
                          "touched) to bring the GPU out of its idle clock state -- from idle the step takes 1.17 ms "
                          "and settles at 1.01 ms only after ~20 ms of load (profiles/r04_warmup_trace.json), longer "
-                         "than a 5-step warm-up (20 / 5 window: 966-982 k without, 994-999 k at 40 ms, 1.007-1.009 M at 200 ms; 100 / 20:
-                         1.020 M -- profiles/r04_prewarm_ab.json); 0: off")
+                         "than a 5-step warm-up (20 / 5 window: 966-982 k without, 994-999 k at 40 ms, 1.007-1.009 M "
+                         "at 200 ms; 100 / 20: 1.020 M -- profiles/r04_prewarm_ab.json); 0: off")
     ap.add_argument("--breakdown-steps", type=int, default=20,
                     help="extra steps after the timed region with every launch event-timed (kernels field)")
     args = ap.parse_args()
