@@ -2025,6 +2025,23 @@ void gemm16_upd_gather_kernel(const GemmP pa, const GemmP pb, const int na, cons
   else bunch_gather_block(g, b - na - nb, (int)gridDim.x - na - nb);
 }
 
+// The fused step's last two weight updates when they take different tile configurations -- a 2048-wide layer's
+// (128x128 direct form, exact prefetch: what tnet_affine_update_bias runs for it) and the first layer's (64x64,
+// BK 32, four slots, 4x1 waves) -- and the next bunch's gather, in ONE launch: blocks [0, na) the big update's
+// tiles (one round over the CUs), then the small update's tiles and the gather blocks, which take the CUs as the
+// big grid's tail drains instead of after a kernel boundary.  Each half runs its separate launch's body: the
+// results are bit-identical to the two calls.
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
+void gemm16_upd_mixed_gather_kernel(const GemmP pa, const GemmP pb, const int na, const int nb, const BunchGatherP g) {
+  constexpr int SA = gemm16_smem_floats<128, 128, 64, 2, EPI_SGD_B, true>();
+  constexpr int SB = gemm16_smem_floats<64, 64, 32, 4, EPI_SGD_B, false>();
+  __shared__ __attribute__((aligned(16))) float smem[SA > SB ? SA : SB];
+  const int b = blockIdx.x;
+  if (b < na) gemm16_body<128, 128, 64, 2, 2, 2, 5, false, false, EPI_SGD_B, true>(pa, smem, b);
+  else if (b < na + nb) gemm16_body<64, 64, 32, 4, 1, 4, 0, false, false, EPI_SGD_B, false>(pb, smem, b - na);
+  else bunch_gather_block(g, b - na - nb, (int)gridDim.x - na - nb);
+}
+
 // tnet_affine_bwd_colsum_slabs: the top layer's backward GEMM (64x128 NT + diff-sigmoid + Eo's slab sums,
 // na tiles) and the slab sums of its OWN input error E (the softmax error: the top layer's bias gradient,
 // colsum_partial blocks after the tiles).  Independent (the GEMM reads E, the blocks read E); the blocks
@@ -3237,6 +3254,24 @@ extern "C" int tnet_affine_update_bias_pair(const float* X, TnetMatrixDim dX, co
   return launch_upd_pair(pa, pb, (hipStream_t)stream);
 }
 
+// gemm16_upd_mixed_gather_kernel's conditions (TNET_UPD_MIXED=0: never): A is what tnet_affine_update_bias runs as
+// m128x128a4 with the exact prefetch (the planner's m128x128k64s2, unsplit, the direct-form conditions, PX), B what
+// it runs as m64x64k32s4w41 unsplit; no CUs reserved
+static bool upd_mixed_ok(const GemmP& pa, const GemmP& pb) {
+  static const bool on = !(getenv("TNET_UPD_MIXED") && getenv("TNET_UPD_MIXED")[0] == '0');
+  if (!on || !g_pair || g_reserve > 0 || g_direct <= 0 || forced_cfg() >= 0) return false;
+  const GemmPlan la = plan_gemm<false>(pa, true), lb = plan_gemm<false>(pb, true);
+  if (la.cfg != CFG_m128x128k64s2 || la.ks != 1 || lb.cfg != CFG_m64x64k32s4w41 || lb.ks != 1) return false;
+  auto a16p = [](const void* v) { return ((uintptr_t)v & 15) == 0; };
+  const bool dir = pa.K / 64 >= 1 && !(pa.lda & 3) && !(pa.ldb & 3) && a16p(pa.A) && a16p(pa.B) && pa.M % 4 == 0 &&
+                   pa.N % 4 == 0 && 4 * ((long)pa.K * pa.lda) < (1L << 31) && 4 * ((long)pa.K * pa.ldb) < (1L << 31);
+  if (!dir || !px_exact<128, 128, EPI_SGD_B>(pa)) return false;
+  // the 16x16 kernel's 32-bit tile offsets (launch_cfg's checks)
+  if (4 * (64L * pa.lda + pa.M) >= (1L << 32) || 4 * (64L * pa.ldb + pa.N) >= (1L << 32)) return false;
+  if (4 * (32L * pb.lda + pb.M) >= (1L << 32) || 4 * (32L * pb.ldb + pb.N) >= (1L << 32)) return false;
+  return true;
+}
+
 extern "C" int tnet_affine_update_bias_gather(const float* X, TnetMatrixDim dX, const float* E, TnetMatrixDim dE,
                                               float* W, TnetMatrixDim dW, float* corrW, int strideCorr, float scale,
                                               float mmt, float l2, const float* colpart, int ldcolpart, float* b,
@@ -3284,6 +3319,22 @@ extern "C" int tnet_affine_update_bias_gather(const float* X, TnetMatrixDim dX, 
   if (forced_cfg() >= 0 || split2_on() || g_split > 0) return TNET_ERR_UNSUPPORTED;
   if (pa.M <= 0 || pa.N <= 0 || (two && (pb.M <= 0 || pb.N <= 0))) return TNET_ERR_UNSUPPORTED;
   int na, nb = 0;
+  if (two && upd_mixed_ok(pa, pb)) {
+    // a 2048-wide layer's update (128x128 direct) + the first layer's (64x64) + the gather
+    na = cdiv(pa.M, 128) * cdiv(pa.N, 128);
+    nb = cdiv(pb.M, 64) * cdiv(pb.N, 64);
+    const int cus = cu_count();
+    if (cus <= 0) return TNET_ERR_UNSUPPORTED;
+    const int spare = cus - nb;
+    const int ng = spare < 8 ? 8 : spare > 64 ? 64 : spare;
+    pa.group = pb.group = g_group > 0 ? g_group : 8;
+    pa.early_issue = pb.early_issue = g_early;
+    pa.wt = pb.wt = g_wt;
+    BunchGatherP g{y, x, labels_out, labels_in, copy_from, dy.rows, c4, dy.stride, dx.stride};
+    gemm16_upd_mixed_gather_kernel<<<na + nb + ng, 256, 0, (hipStream_t)stream>>>(pa, pb, na, nb, g);
+    TNET_LAUNCH_CHECK();
+    return TNET_OK;
+  }
   if (two) {
     // the pair kernel's conditions (launch_upd_pair): both 64x64 grids in one round over the CUs
     if (!g_pair) return TNET_ERR_UNSUPPORTED;
