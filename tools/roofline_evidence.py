@@ -58,7 +58,8 @@ def classify_trace(path):
             continue
         # the bunch gather: its own launch, or (round 3, tnet_affine_update_bias_gather) riding on the
         # previous step's last update launch (the 440x2048 update, not a roofline GEMM)
-        if "gather_rows" in name or "upd_gather" in name:
+        # (round 4: the last two updates + the gather, gemm16_upd_mixed_gather_kernel -- not a roofline launch)
+        if "gather_rows" in name or "upd_gather" in name or "upd_mixed_gather" in name:
             after_gather = True
             continue
         if FWD.search(name):
