@@ -290,8 +290,11 @@ int tnet_affine_grad_bwd_pair(const float* X, TnetMatrixDim dX, const float* E, 
  * both 64x64 grids fit one round over the CUs) plus tnet_gather_bunch (the next bunch's CuCache::GetBunch,
  * cuCache.cc:155-200) on the CUs the gradient GEMMs' tiles leave free -- the data-parallel step's last gradient
  * launch, tnet_affine_update_bias_gather's form and rules: the gather independent of the GEMMs and the two GEMMs of
- * each other (TNET_ERR_ARG otherwise), TNET_ERR_UNSUPPORTED when one GEMM would run another tile configuration
- * alone, the pair does not fit one round, or fewer than 8 CUs are left. */
+ * each other (TNET_ERR_ARG otherwise), TNET_ERR_UNSUPPORTED when the single GEMM would run another tile
+ * configuration alone, the pair does not fit one round, or fewer than 8 CUs are left.  The two-GEMM form runs both
+ * as unsplit 64x64 grids (sums in k order), also where the planner would split one of them over K alone: then
+ * that gradient differs from tnet_affine_grad_bias's in fp32 summation order only (the fused step's update pair,
+ * tnet_affine_update_bias_pair, has the same rule). */
 int tnet_affine_grad_bias_gather(const float* X, TnetMatrixDim dX, const float* E, TnetMatrixDim dE, float* G,
                                  TnetMatrixDim dG, const float* colpart, int ldcolpart, float* gradB, const float* X2,
                                  TnetMatrixDim dX2, const float* E2, TnetMatrixDim dE2, float* G2, TnetMatrixDim dG2,
@@ -466,11 +469,12 @@ int tnet_gemv_rows(const float* W, int ldw, int r0, int nrows, int n, const floa
    workspace: tnet_rnn_bptt_chain_workspace(n, order) bytes, zeroed once before the first call and kept for the
    layer's life (its epoch word orders the launches).  TNET_ERR_UNSUPPORTED outside n <= 1024 (n % 64 == 0 up
    to 512, n % 32 == 0 above), 16-B aligned W / D, order < 16.  A hand-off that never arrives (a bug) sets an
-   error word instead of hanging: tnet_rnn_bptt_chain_error reads it (synchronous). */
+   error word instead of hanging: tnet_rnn_bptt_chain_error reads it, ordered after the work already enqueued on
+   `stream` (the chain's stream; returns once that work has finished). */
 long tnet_rnn_bptt_chain_workspace(int n, int order);
 int tnet_rnn_bptt_chain(const float* W, int ldw, int r0, int n, float* D, int ldd, int order, const float* hist,
                         int ldh, int head, int R, int hoff, void* workspace, void* stream);
-int tnet_rnn_bptt_chain_error(const void* workspace, int* err);
+int tnet_rnn_bptt_chain_error(const void* workspace, int* err, void* stream);
 int tnet_rnn_update(float* W, int ldw, int rows, int nout, const float* hist, int ldh, int head, int R,
                     const float* D, int ldd, int steps, float* b, float* corr_b, float lr, float mmt, float wc,
                     void* stream);

@@ -159,6 +159,16 @@ int tnet_reader_rewind(TnetFeatureReader* r);  /* FeatureRepository::Rewind */
 /* one record ("logical=physical[s,e]" or a path) without a reader: out == NULL asks for the size only */
 int tnet_htk_read(const char* record, int swap, int start_ext, int end_ext, float* out, long cap, int* rows, int* cols,
                   int* samp_period, int* kind);
+/* label masks and the MLF record index on their own (csrc/host/labelindex.h):
+ *   tnet_mask_match: ProcessMask (src/KaldiLib/StkMatch.cc:453-490) -- 1 when `mask`, anchored at a path
+ *     component, matches `label`, with the characters its '%'s capture in captured[cap] (NUL-terminated,
+ *     truncated to cap); 0 when it does not; < 0 on an argument error
+ *   tnet_mlf_lookup: LabelContainer::Insert of patterns[k] as record k, k = 0..n_patterns-1, in order
+ *     (MlfStream.cc:43-93), then LabelContainer::Find of each label (MlfStream.cc:243-262): rec_out[i] = the
+ *     record label i resolves to, -1 for none */
+int tnet_mask_match(const char* mask, const char* label, char* captured, int cap);
+int tnet_mlf_lookup(const char* const* patterns, int n_patterns, const char* const* labels, int n_labels,
+                    int* rec_out);
 /* the cache fill of TNetCu.cc:376-419 from a reader: up to max_utts utterances (< 0: to the end of the
  * list) into the trainer, each training the cache whenever it fills; returns the frames added (< 0 error).
  * The reader's STARTFRMEXT / ENDFRMEXT must be the transform's (tnet_trainer_set_transform); without
@@ -206,6 +216,16 @@ TnetComm* tnet_comm_create(int rank, int world, const char id[128]);
 int tnet_comm_free(TnetComm* comm);
 int tnet_comm_allreduce_host(TnetComm* comm, double* v, int n);
 int tnet_comm_allreduce_device(TnetComm* comm, float* dbuf, long n);
+/* the reduction check (bench.py rccl_check; the reference's reduce is Platform.h:307-335): tnet_comm_capture(comm, 1)
+ * arms ONE step -- every gradient block the next step submits is copied to the host right before its reduction
+ * (this rank's local gradient) and right after it (the reduced values over the ranges this rank applies, NaN
+ * elsewhere); synchronous, for a check step outside the timed region.  The copies stay until the next arming:
+ * tnet_comm_captured = block count, tnet_comm_captured_block(i) fills local / reduced [n] (both NULL: n only).
+ * tnet_comm_transport_ranks: the rank count as the transport reports it (ncclCommCount for RCCL). */
+int tnet_comm_capture(TnetComm* comm, int on);
+long tnet_comm_captured(TnetComm* comm);
+int tnet_comm_captured_block(TnetComm* comm, long i, float* local, float* reduced, long cap, long* n);
+int tnet_comm_transport_ranks(TnetComm* comm, int* ranks);
 /* Host-transport communicator: gradients are staged through host memory and summed in place by
  * fn(user, buf, n, is_double) (float32 when is_double == 0); fn returns 0 on success.  For
  * transports without RCCL (gloo, MPI) and multi-process tests on one device; PCIe-bound. */

@@ -482,6 +482,32 @@ int tnet_reader_rewind(TnetFeatureReader* r) {
   r->r->Rewind();
   TRY_END
 }
+int tnet_mask_match(const char* mask, const char* label, char* captured, int cap) {
+  TRY_BEGIN if (!mask || !label || (cap > 0 && !captured)) Error("tnet_mask_match: null argument");
+  std::string sub;
+  const bool ok = tnetio::LabelMask::ForPath(mask).Matches(tnetio::LabelMask::AsPath(label), &sub);
+  if (cap > 0) {
+    const size_t n = std::min(sub.size(), (size_t)cap - 1);
+    std::memcpy(captured, sub.data(), n);
+    captured[n] = '\0';
+  }
+  return ok ? 1 : 0;
+  TRY_END
+}
+
+int tnet_mlf_lookup(const char* const* patterns, int n_patterns, const char* const* labels, int n_labels,
+                    int* rec_out) {
+  TRY_BEGIN if (n_patterns < 0 || n_labels < 0 || (n_patterns && !patterns) || (n_labels && (!labels || !rec_out)))
+      Error("tnet_mlf_lookup: bad arguments");
+  tnetio::LabelIndex index;
+  for (int k = 0; k < n_patterns; k++) index.Insert(patterns[k] ? patterns[k] : "", (size_t)k);
+  for (int i = 0; i < n_labels; i++) {
+    size_t rec = 0;
+    rec_out[i] = index.Find(labels[i] ? labels[i] : "", &rec) ? (int)rec : -1;
+  }
+  TRY_END
+}
+
 int tnet_htk_read(const char* record, int swap, int start_ext, int end_ext, float* out, long cap, int* rows, int* cols,
                   int* samp_period, int* kind) {
   TRY_BEGIN if (!record) Error("tnet_htk_read: no record");
@@ -710,6 +736,28 @@ int tnet_comm_free(TnetComm* c) {
 }
 int tnet_comm_allreduce_host(TnetComm* c, double* v, int n) {
   TRY_BEGIN c->ex->AllReduceHost(v, n);
+  TRY_END
+}
+int tnet_comm_capture(TnetComm* c, int on) {
+  TRY_BEGIN if (!c) Error("tnet_comm_capture: no communicator");
+  c->ex->ArmCapture(on != 0);
+  TRY_END
+}
+long tnet_comm_captured(TnetComm* c) { return c ? (long)c->ex->Captured().size() : -1; }
+int tnet_comm_captured_block(TnetComm* c, long i, float* local, float* reduced, long cap, long* n) {
+  TRY_BEGIN if (!c || !n || i < 0 || i >= (long)c->ex->Captured().size()) Error("tnet_comm_captured_block: bad arguments");
+  const GradExchange::CapturedBlock& b = c->ex->Captured()[(size_t)i];
+  *n = (long)b.local.size();
+  if (local || reduced) {
+    if (cap < *n || !local || !reduced) Error("tnet_comm_captured_block: buffers too small");
+    std::memcpy(local, b.local.data(), b.local.size() * sizeof(float));
+    std::memcpy(reduced, b.reduced.data(), b.reduced.size() * sizeof(float));
+  }
+  TRY_END
+}
+int tnet_comm_transport_ranks(TnetComm* c, int* ranks) {
+  TRY_BEGIN if (!c || !ranks) Error("tnet_comm_transport_ranks: bad arguments");
+  *ranks = c->ex->TransportRanks();
   TRY_END
 }
 int tnet_comm_allreduce_device(TnetComm* c, float* dbuf, long n) {

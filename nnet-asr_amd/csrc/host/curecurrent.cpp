@@ -19,16 +19,26 @@ void CuRecurrent::BpttOrder(int ord) {
   mDiff.Init((size_t)ord + 1, GetNOutputs());
   mDiffTmp.Init(1, GetNOutputs());
   mHead = 0;
-  // the one-launch BPTT chain's control words and granule slots (zeroed: epoch 0, no granule current)
+  if (!ChainEnabled()) return;
+  // the one-launch BPTT chain's control words and granule slots (zeroed: epoch 0, no granule current), on the
+  // compute stream so the zeroing is ordered with the chain launches
   const size_t cb = (size_t)tnet_rnn_bptt_chain_workspace((int)GetNOutputs(), ord);
   if (cb > mChainBytes) {
-    if (mChainWs) TNET_HIP_CALL(hipFree(mChainWs));
+    if (mChainWs) {
+      TNET_HIP_CALL(hipStreamSynchronize(CuDevice::Instantiate().Stream()));
+      TNET_HIP_CALL(hipFree(mChainWs));
+    }
     mChainWs = nullptr;
     mChainBytes = 0;
     TNET_HIP_CALL(hipMalloc(&mChainWs, cb));
     mChainBytes = cb;
   }
-  TNET_HIP_CALL(hipMemset(mChainWs, 0, mChainBytes));
+  TNET_HIP_CALL(hipMemsetAsync(mChainWs, 0, mChainBytes, CuDevice::Instantiate().Stream()));
+}
+
+bool CuRecurrent::ChainEnabled() {
+  static const bool on = getenv("TNET_RNN_BPTT_CHAIN") && getenv("TNET_RNN_BPTT_CHAIN")[0] == '1';
+  return on;
 }
 
 CuRecurrent::~CuRecurrent() {
@@ -38,7 +48,7 @@ CuRecurrent::~CuRecurrent() {
 void CuRecurrent::CheckChain() const {
   if (!mChainWs) return;
   int err = 0;
-  TNET_SAFE_CALL(tnet_rnn_bptt_chain_error(mChainWs, &err));
+  TNET_SAFE_CALL(tnet_rnn_bptt_chain_error(mChainWs, &err, S));
   if (err) Error("CuRecurrent: the one-launch BPTT chain timed out waiting for a hand-off (unset "
                  "TNET_RNN_BPTT_CHAIN to run the per-step launches)");
 }
@@ -124,7 +134,7 @@ void CuRecurrent::UpdateFromDiff0(bool defer) {
   // 45.4 k frames/s at 135 senones, 30.4 k vs 36.6 k at 4000 (profiles/r04_rnn_chain_ab.json): each step's
   // all-to-all granule hand-off across the 8-16 workgroups costs more than the launch boundary it removes
   // (MI355X_MICROARCH.md's allgather / boundary rows: 2.4-4 vs 1.45 us)
-  static const bool chain = getenv("TNET_RNN_BPTT_CHAIN") && getenv("TNET_RNN_BPTT_CHAIN")[0] == '1';
+  const bool chain = ChainEnabled();
   int st = TNET_ERR_UNSUPPORTED;
   if (chain && mChainWs && mBpttOrder > 0)
     st = tnet_rnn_bptt_chain(mLinearity.pCUData(), (int)mLinearity.Stride(), nIn, nOut, mDiff.pCUData(),
@@ -260,7 +270,9 @@ void CuRecurrentTrainer::TrainUtterance(const float* feats, size_t rows, size_t 
     RunFrames(rows);
     TNET_SAFE_CALL(tnet_argmax_correct((const unsigned long long*)mArgKey, mLabels.pCUData(), (int)rows,
                                        (int)mNet->GetNOutputs(), mObj->DeviceStats(), S));
-    dynamic_cast<CuRecurrent&>(mNet->Layer(0)).CheckChain();  // one flag read per utterance
+    if (CuRecurrent::ChainEnabled())  // one flag read per utterance and recurrent layer, opt-in chain only
+      for (int i = 0; i < mNet->Layers(); i++)
+        if (mNet->Layer(i).GetType() == CuComponent::RECURRENT) dynamic_cast<CuRecurrent&>(mNet->Layer(i)).CheckChain();
     mFrames += (long)rows;
     return;
   }

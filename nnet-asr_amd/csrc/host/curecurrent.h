@@ -35,6 +35,7 @@ class CuRecurrent : public CuUpdatableComponent {
   const char* GetName() const override { return "<recurrent>"; }
   /// Throws if the one-launch BPTT chain (tnet_rnn_bptt_chain) reported a timed-out hand-off (synchronises).
   void CheckChain() const;
+  static bool ChainEnabled();  // TNET_RNN_BPTT_CHAIN=1: the opt-in one-launch BPTT chain
 
   void PropagateFnc(const CuMatrix<BaseFloat>& X, CuMatrix<BaseFloat>& Y) override;
   void BackpropagateFnc(const CuMatrix<BaseFloat>& X, CuMatrix<BaseFloat>& Y) override;

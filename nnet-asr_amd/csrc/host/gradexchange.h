@@ -84,8 +84,33 @@ class GradExchange {
   }
   void SetStepRows(size_t rows) { mStepRows = rows; }
 
+  // ---- reduction check (bench.py rccl_check): armed for one step, every submitted gradient block is copied to
+  // the host right before its reduction (this rank's local gradient) and right after it (the reduced values over
+  // the ranges this rank applies, NaN elsewhere), so the caller can sum the local copies over another transport
+  // and compare.  Synchronous: for a check step outside any timed region.
+  struct CapturedBlock {
+    std::vector<float> local, reduced;
+  };
+  void ArmCapture(bool on) {
+    mCaptureArmed = on;
+    if (on) mCaptured.clear();
+  }
+  const std::vector<CapturedBlock>& Captured() const { return mCaptured; }
+  /// the communicator's rank count as the transport reports it (ncclCommCount for RCCL)
+  virtual int TransportRanks() const { return WorldSize(); }
+
+ protected:
+  /// Submit's halves of the capture (no-ops unless armed; `stream` orders the copies after the gradient kernels
+  /// and after the reduction respectively)
+  void CaptureLocal(CuUpdatableComponent& comp, void* stream);
+  void CaptureReduced(CuUpdatableComponent& comp, void* stream);
+  void DisarmCapture() { mCaptureArmed = false; }
+  bool mCaptureArmed = false;
+
  private:
   size_t mStepRows = 0;
+  size_t mCaptureFirst = 0;
+  std::vector<CapturedBlock> mCaptured;
 };
 
 /// One round of the data-parallel step plan (see DpPlanRound).

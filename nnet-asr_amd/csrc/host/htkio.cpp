@@ -75,6 +75,63 @@ bool SplitRange(std::string& name, int& from, int& to) {
   return true;
 }
 
+
+// One frame of a parameter kind: order + 1 blocks (statics, then deltas, accelerations, third
+// differences), each block `base` coefficients followed by C0 (_0) and the energy (_E) when the kind has
+// them; _N leaves the C0 / energy values out of the static block.
+struct FrameLayout {
+  bool c0 = false, energy = false;
+  int suppressed = 0;  // static values left out by _N
+  int order = 0;       // derivative blocks
+
+  static FrameLayout OfKind(int kind) {
+    FrameLayout l;
+    l.c0 = (kind & kParm0) != 0;
+    l.energy = (kind & kParmE) != 0;
+    l.suppressed = (kind & kParmN) ? l.Extras() : 0;
+    l.order = (kind & kParmT) ? 3 : (kind & kParmA) ? 2 : (kind & kParmD) ? 1 : 0;
+    return l;
+  }
+  int Extras() const { return (int)c0 + (int)energy; }
+  int Block(int base) const { return base + Extras(); }
+  int Width(int base) const { return Block(base) * (order + 1) - suppressed; }
+  int BaseFromWidth(int values) const { return (values + suppressed) / (order + 1) - Extras(); }
+  // the first `blocks` + 1 blocks of this layout and of t hold the same values in the same places
+  bool SameValues(const FrameLayout& t, int blocks) const {
+    return blocks == order && blocks == t.order && c0 == t.c0 && energy == t.energy && suppressed == t.suppressed;
+  }
+  // Column of the target row each value of a frame of this layout is written to, blocks 0..blocks.  A C0 /
+  // energy value the target does not keep is written where the next kept value goes (so it is replaced),
+  // or past the kept columns at the end of the row (the derivative columns computed afterwards replace it,
+  // a column past the row is dropped) -- the reference's decode into a row with a trailing cursor.
+  std::vector<int> PlacementIn(const FrameLayout& t, int base, int blocks) const {
+    std::vector<int> col;
+    int at = 0;
+    for (int b = 0; b <= blocks; b++) {
+      for (int k = 0; k < base; k++) col.push_back(at++);
+      const bool statics = b == 0;
+      const bool src_has[2] = {c0 && !(statics && suppressed), energy && !(statics && suppressed)};
+      const bool trg_has[2] = {t.c0 && !(statics && t.suppressed), t.energy && !(statics && t.suppressed)};
+      for (int x = 0; x < 2; x++) {
+        if (src_has[x]) col.push_back(at);
+        if (trg_has[x]) at++;
+      }
+    }
+    return col;
+  }
+};
+
+// Whether frames of layout s (base kind sb) convert to layout t (base kind tb): C0 and energy cannot be
+// made up, a value _N left out of the file cannot come back, _N needs a derivative block to keep the value
+// in, derivatives of a file with suppressed statics cannot be computed, and the base kinds must agree
+// unless the file's is ANON.
+bool Convertible(const FrameLayout& s, const FrameLayout& t, int sb, int tb) {
+  if ((t.energy && !s.energy) || (t.c0 && !s.c0)) return false;
+  if (s.suppressed && !t.suppressed) return false;
+  if (t.suppressed && t.order == 0) return false;
+  if (s.suppressed && s.order == 0 && t.order > 0) return false;
+  return sb == tb || sb == kParmAnon;
+}
 }  // namespace
 
 FileRecord ParseFileRecord(const std::string& line) {
@@ -150,179 +207,139 @@ void ReadHtkFeatures(const FileRecord& rec, const FeatureConfig& cfg, int& targe
     to_frame = h.nSamples - 1;
   }
 
-  int src_deriv = (h.sampleKind & kParmT) ? 3 : (h.sampleKind & kParmA) ? 2 : (h.sampleKind & kParmD) ? 1 : 0;
-  const int src_E = (h.sampleKind & kParmE) != 0;
-  const int src_0 = (h.sampleKind & kParm0) != 0;
-  const int src_N = ((h.sampleKind & kParmN) != 0) * (src_E + src_0);
   h.sampleKind &= ~kParmC;
-  if (targetKind == kParmAnon) {
-    targetKind = h.sampleKind;
-  } else if ((targetKind & 077) == kParmAnon) {
-    targetKind &= ~077;
-    targetKind |= h.sampleKind & 077;
-  }
-  const int trg_E = (targetKind & kParmE) != 0;
-  const int trg_0 = (targetKind & kParm0) != 0;
-  const int trg_N = ((targetKind & kParmN) != 0) * (trg_E + trg_0);
+  const FrameLayout src = FrameLayout::OfKind(h.sampleKind);
+  if (targetKind == kParmAnon) targetKind = h.sampleKind;  // ANON: the file's kind, qualifiers included
+  else if ((targetKind & 077) == kParmAnon) targetKind = (targetKind & ~077) | (h.sampleKind & 077);
+  FrameLayout trg = FrameLayout::OfKind(targetKind);
 
-  const int coef_size = comp ? 2 : 4;
-  int coefs = (h.sampleSize / coef_size + src_N) / (src_deriv + 1) - src_E - src_0;
-  const int src_vec = (coefs + src_E + src_0) * (src_deriv + 1) - src_N;
-  if (src_vec * coef_size != h.sampleSize)
+  const int value_bytes = comp ? 2 : 4;
+  const int coefs = src.BaseFromWidth(h.sampleSize / value_bytes);
+  const int src_vec = src.Width(coefs);
+  if (src_vec * value_bytes != h.sampleSize)
     Fail("Invalid HTK header in feature file: '" + name + "' mSampleSize do not match with parmKind");
-  if (derivOrder < 0) derivOrder = src_deriv;
-
-  if ((!src_E && trg_E) || (!src_0 && trg_0) || (src_N && !trg_N) || (trg_N && !trg_E && !trg_0) ||
-      (trg_N && !derivOrder) || (src_N && !src_deriv && derivOrder) ||
-      ((h.sampleKind & 077) != (targetKind & 077) && (h.sampleKind & 077) != kParmAnon))
+  if (derivOrder < 0) derivOrder = src.order;
+  trg.order = derivOrder;
+  if (!Convertible(src, trg, h.sampleKind & 077, targetKind & 077))
     Fail("Cannot convert " + ParmKindStr(h.sampleKind) + " to " + ParmKindStr((unsigned)targetKind));
+  const int kept_order = std::min(src.order, derivOrder);  // derivative blocks read from the file
+  const int trg_vec = trg.Width(coefs);
 
-  const int lo_deriv = std::min(src_deriv, derivOrder);
-  const int trg_vec = (coefs + trg_E + trg_0) * (derivOrder + 1) - trg_N;
-
-  int ext_left = cfg.startExt, ext_right = cfg.endExt;
-  int i = std::min(from_frame, cfg.startExt);
-  from_frame -= i;
-  ext_left -= i;
-  i = std::min(h.nSamples - to_frame - 1, cfg.endExt);
-  to_frame += i;
-  ext_right -= i;
+  // the context frames come from the file's real neighbours where it has them; the rest is edge padding
+  const int real_left = std::min(from_frame, cfg.startExt);
+  const int real_right = std::min(h.nSamples - 1 - to_frame, cfg.endExt);
+  from_frame -= real_left;
+  to_frame += real_right;
+  const int ext_left = cfg.startExt - real_left, ext_right = cfg.endExt - real_right;
   if (from_frame > to_frame || from_frame >= h.nSamples || to_frame < 0)
     Fail("Invalid frame range for feature file: '" + name + "'");
   const int tot = to_frame - from_frame + 1 + ext_left + ext_right;
 
+  // the usual case -- float data whose source layout is the target's (same 0 / E / N flags, no derivative
+  // dropped): the file's bytes go straight into the output rows, byte-swapped in place
+  const bool direct = !comp && src.SameValues(trg, kept_order);
   out.rows = tot;
   out.cols = trg_vec;
-  out.feats.resize((size_t)tot * trg_vec);  // every element is written below (a recycled buffer keeps its pages)
-  if (!(!comp && src_vec == trg_vec))
-    std::fill(out.feats.begin(), out.feats.end(), 0.0f);
+  out.feats.resize((size_t)tot * trg_vec);  // a recycled buffer keeps its pages
+  if (!direct) std::fill(out.feats.begin(), out.feats.end(), 0.0f);
 
   // the frames [from, to] in one read (the reference seeks and reads per frame, Features.cc:1207-1258)
   const int nread = to_frame - from_frame + 1;
-  const size_t fbytes = (size_t)src_vec * coef_size;
-  const off_t base = 12 + (comp ? (off_t)src_vec * 2 * 4 : 0) + (off_t)from_frame * (off_t)fbytes;
-  auto read_block = [&](void* dst, size_t bytes) {  // a short file is the reference's per-frame read failure
-    char* p = static_cast<char*>(dst);
-    size_t n = bytes;
-    off_t off = base;
-    while (n) {
-      ssize_t r = pread(f.fd, p, n, off);
-      if (r <= 0) Fail("Cannot read feature file: '" + name + "' frame " + std::to_string((bytes - n) / fbytes) + "/" +
-                       std::to_string(nread));
-      p += r;
-      n -= (size_t)r;
-      off += r;
+  const size_t fbytes = (size_t)src_vec * value_bytes;
+  const off_t first_byte = 12 + (comp ? (off_t)src_vec * 2 * 4 : 0) + (off_t)from_frame * (off_t)fbytes;
+  // reads [first_byte + at, + bytes) into dst; a short file is the reference's per-frame read failure
+  auto read_span = [&](char* dst, size_t at, size_t bytes) {
+    for (size_t got = 0; got < bytes;) {
+      const ssize_t r = pread(f.fd, dst + got, bytes - got, first_byte + (off_t)(at + got));
+      if (r <= 0)
+        Fail("Cannot read feature file: '" + name + "' frame " + std::to_string((at + got) / fbytes) + "/" +
+             std::to_string(nread));
+      got += (size_t)r;
     }
   };
-  // the usual case -- float data whose source layout is the target's (same 0 / E / N flags, no derivative
-  // dropped): straight into the output rows, byte-swapped in place
-  const bool direct = !comp && src_vec == trg_vec && lo_deriv == src_deriv && src_E == trg_E && src_0 == trg_0 &&
-                      src_N == trg_N;
   if (direct) {
     // 64-KiB pieces: each is byte-swapped while it is still in the core's cache after the read
     uint32_t* dst = reinterpret_cast<uint32_t*>(&out.feats[(size_t)ext_left * trg_vec]);
-    const size_t total = (size_t)nread * fbytes;
-    const size_t piece = 64 * 1024;
-    char* p = reinterpret_cast<char*>(dst);
-    for (size_t done = 0; done < total;) {
+    const size_t total = (size_t)nread * fbytes, piece = 64 * 1024;
+    for (size_t done = 0; done < total; done += piece) {
       const size_t want = std::min(piece, total - done);  // a multiple of 4 bytes
-      for (size_t got = 0; got < want;) {
-        ssize_t r = pread(f.fd, p + done + got, want - got, base + (off_t)(done + got));
-        if (r <= 0) Fail("Cannot read feature file: '" + name + "' frame " + std::to_string((done + got) / fbytes) +
-                         "/" + std::to_string(nread));
-        got += (size_t)r;
-      }
+      read_span(reinterpret_cast<char*>(dst) + done, done, want);
       if (cfg.swap)
         for (size_t k = done / 4; k < (done + want) / 4; k++) dst[k] = bswap32(dst[k]);
-      done += want;
     }
   } else {
     thread_local std::vector<unsigned char> raw;
     raw.resize((size_t)nread * fbytes);
-    read_block(raw.data(), raw.size());
-    // decode one source frame into the target layout (the reads of Features.cc:1223-1246, including
-    // their overwrite of a source 0 / E value the target does not keep); `tmp` has room past the row
-    std::vector<float> tmp((size_t)trg_vec + 8);
+    read_span(reinterpret_cast<char*>(raw.data()), 0, raw.size());
+    const std::vector<int> plan = src.PlacementIn(trg, coefs, kept_order);
     for (int r = 0; r < nread; r++) {
-      const unsigned char* src = raw.data() + (size_t)r * fbytes;
-      int si = 0;  // next source value
-      const float* Ap = A.data();
-      const float* Bp = B.data();
-      auto read = [&](float* dst, int n) {
-        for (int k = 0; k < n; k++, si++) {
-          if (comp) {
-            uint16_t v;
-            memcpy(&v, src + 2 * si, 2);
-            if (cfg.swap) v = bswap16(v);
-            dst[k] = ((float)(int16_t)v + Bp[k]) / Ap[k];
-          } else {
-            uint32_t v;
-            memcpy(&v, src + 4 * si, 4);
-            if (cfg.swap) v = bswap32(v);
-            memcpy(&dst[k], &v, 4);
-          }
+      const unsigned char* in = raw.data() + (size_t)r * fbytes;
+      float* row = &out.feats[(size_t)(r + ext_left) * trg_vec];
+      for (int si = 0; si < (int)plan.size(); si++) {  // the blocks read: the first kept_order + 1
+        float v;
+        if (comp) {  // int16 value x: (x + B) / A with the file's per-column scale A and bias B
+          uint16_t x;
+          memcpy(&x, in + 2 * si, 2);
+          if (cfg.swap) x = bswap16(x);
+          v = ((float)(int16_t)x + B[(size_t)si]) / A[(size_t)si];
+        } else {
+          uint32_t x;
+          memcpy(&x, in + 4 * si, 4);
+          if (cfg.swap) x = bswap32(x);
+          memcpy(&v, &x, 4);
         }
-        Ap += n;
-        Bp += n;
-      };
-      float* mx = tmp.data();
-      read(mx, coefs);
-      mx += coefs;
-      if (src_0 && !src_N) read(mx, 1);
-      if (trg_0 && !trg_N) mx++;
-      if (src_E && !src_N) read(mx, 1);
-      if (trg_E && !trg_N) mx++;
-      for (int j = 0; j < lo_deriv; j++) {
-        read(mx, coefs);
-        mx += coefs;
-        if (src_0) read(mx, 1);
-        if (trg_0) mx++;
-        if (src_E) read(mx, 1);
-        if (trg_E) mx++;
+        if (plan[(size_t)si] < trg_vec) row[plan[(size_t)si]] = v;
       }
-      memcpy(&out.feats[(size_t)(r + ext_left) * trg_vec], tmp.data(), (size_t)trg_vec * 4);
-      std::fill(tmp.begin(), tmp.end(), 0.0f);
     }
   }
 
-  coefs += trg_0 + trg_E;
-  const size_t ext_w = (size_t)(coefs * (1 + lo_deriv) - trg_N);
-  for (i = 0; i < ext_left; i++)
-    memcpy(&out.feats[(size_t)i * trg_vec], &out.feats[(size_t)ext_left * trg_vec], ext_w * 4);
-  for (i = tot - ext_right; i < tot; i++)
-    memcpy(&out.feats[(size_t)i * trg_vec], &out.feats[(size_t)(tot - ext_right - 1) * trg_vec], ext_w * 4);
+  // the padding rows repeat the first / last real frame over the columns read from the file
+  const int block = trg.Block(coefs);
+  const size_t read_w = (size_t)(block * (1 + kept_order) - trg.suppressed);
+  for (int i = 0; i < ext_left; i++)
+    memcpy(&out.feats[(size_t)i * trg_vec], &out.feats[(size_t)ext_left * trg_vec], read_w * 4);
+  for (int i = tot - ext_right; i < tot; i++)
+    memcpy(&out.feats[(size_t)i * trg_vec], &out.feats[(size_t)(tot - ext_right - 1) * trg_vec], read_w * 4);
 
   float* M = out.feats.data();
+  const size_t ld = (size_t)trg_vec;
   if (!cfg.cmn && !(kParmZ & h.sampleKind) && (kParmZ & targetKind)) {  // sentence mean (Features.cc:1279-1300)
-    if (trg_N) Fail("Cannot convert " + ParmKindStr(h.sampleKind) + " to " + ParmKindStr((unsigned)targetKind) +
-                    ": sentence mean normalisation with suppressed energy is not supported");
-    for (int j = 0; j < coefs; j++) {
-      float norm = 0.0f;
-      for (i = 0; i < tot; i++) norm += M[(size_t)i * trg_vec + j];
-      norm /= tot;
-      for (i = 0; i < tot; i++) M[(size_t)i * trg_vec + j] -= norm;
+    if (trg.suppressed)
+      Fail("Cannot convert " + ParmKindStr(h.sampleKind) + " to " + ParmKindStr((unsigned)targetKind) +
+           ": sentence mean normalisation with suppressed energy is not supported");
+    for (int j = 0; j < block; j++) {
+      float mean = 0.0f;
+      for (int i = 0; i < tot; i++) mean += M[(size_t)i * ld + j];
+      mean /= tot;
+      for (int i = 0; i < tot; i++) M[(size_t)i * ld + j] -= mean;
     }
   }
-  for (; src_deriv < derivOrder; src_deriv++) {  // missing derivatives (Features.cc:1302-1343)
-    if (trg_N) Fail("Cannot convert " + ParmKindStr(h.sampleKind) + " to " + ParmKindStr((unsigned)targetKind) +
-                    ": derivatives of suppressed energy are not supported");
-    const int win = src_deriv < (int)cfg.derivWin.size() ? cfg.derivWin[src_deriv] : 2;
+  // derivative blocks the file does not have (Features.cc:1302-1343): regression over +-win frames, the
+  // window shrunk to the frames that exist at the utterance's edges
+  for (int order = src.order; order < derivOrder; order++) {
+    if (trg.suppressed)
+      Fail("Cannot convert " + ParmKindStr(h.sampleKind) + " to " + ParmKindStr((unsigned)targetKind) +
+           ": derivatives of suppressed energy are not supported");
+    const int win = order < (int)cfg.derivWin.size() ? cfg.derivWin[order] : 2;
     float norm = 0.0f;
     for (int k = 1; k <= win; k++) norm += 2 * k * k;
-    for (i = 0; i < tot; i++)
-      for (int j = 0; j < coefs; j++) {
-        const float* s = M + (size_t)i * trg_vec + (size_t)src_deriv * coefs + j;
-        float d = 0.0f;
+    const size_t from_col = (size_t)order * block, to_col = from_col + block;
+    for (int i = 0; i < tot; i++) {
+      const bool edge = i < win || i >= tot - win;
+      for (int j = 0; j < block; j++) {
+        const float* x = M + (size_t)i * ld + from_col + j;
+        float acc = 0.0f;
         for (int k = 1; k <= win; k++) {
-          const int up = (i < win || i >= tot - win) ? std::min(tot - 1 - i, k) : k;
-          const int dn = (i < win || i >= tot - win) ? std::min(i, k) : k;
-          d += k * (s[(ptrdiff_t)up * trg_vec] - s[-(ptrdiff_t)dn * trg_vec]);
+          const ptrdiff_t ahead = edge ? std::min(tot - 1 - i, k) : k, behind = edge ? std::min(i, k) : k;
+          acc += k * (x[ahead * (ptrdiff_t)ld] - x[-behind * (ptrdiff_t)ld]);
         }
-        M[(size_t)i * trg_vec + (size_t)src_deriv * coefs + j + coefs] = d / norm;
+        M[(size_t)i * ld + to_col + j] = acc / norm;
       }
+    }
   }
 
-  if (cfg.cmn || cfg.cvn || cfg.cvg) ApplyCepsNorm(cfg, rec.logical, targetKind, derivOrder, coefs, trg_N, trg_vec, tot, M);
+  if (cfg.cmn || cfg.cvn || cfg.cvg)
+    ApplyCepsNorm(cfg, rec.logical, targetKind, derivOrder, block, trg.suppressed, trg_vec, tot, M);
 
   // CheckData's scan (the reference driver's, Matrix.h:238-252), done here on the reading thread
   out.bad_row = out.bad_col = -1;
@@ -378,169 +395,137 @@ std::string MakeHtkFileName(const std::string& in, const char* outDir, const cha
 // ------------------------------------------------------------------------------------------- MLF
 
 namespace {
-// The STK wildcard matcher the reference's MLF lookup uses (KaldiLib/StkMatch.cc matche /
-// matche_after_star): '?' and '%' one character, '*' any run, [..] / [!..] / [^..] sets with ranges and
-// backslash escapes inside a set, a text that ends early matches only a trailing '*'.  Restated step for
-// step (the return codes steer matche_after_star's search); parity: tests/test_reader.py MLF cases.
-enum { kMatchValid = 1, kMatchEnd, kMatchAbort, kMatchRange, kMatchLiteral, kMatchPattern };
-int StkMatchAfterStar(const char* p, const char* t, char* s);
-int StkMatche(const char* p, const char* t, char* s) {
-  for (; *p; p++, t++) {
-    if (!*t) return (*p == '*' && *++p == '\0') ? kMatchValid : kMatchAbort;
-    switch (*p) {
-      case '?':
-        break;
-      case '%':  // one character, captured
-        *s++ = *t;
-        *s = '\0';
-        break;
-      case '*':
-        return StkMatchAfterStar(p, t, s);
-      case '[': {
-        p++;
-        bool invert = false;
-        if (*p == '!' || *p == '^') {
-          invert = true;
-          p++;
-        }
-        if (*p == ']') return kMatchPattern;
-        bool member = false, loop = true;
-        while (loop) {
-          if (*p == ']') {
-            loop = false;
-            continue;
-          }
-          char lo, hi;
-          if (*p == '\\') lo = hi = *++p;
-          else lo = hi = *p;
-          if (!*p) return kMatchPattern;
-          if (*++p == '-') {
-            hi = *++p;
-            if (hi == '\0' || hi == ']') return kMatchPattern;
-            if (hi == '\\') {
-              hi = *++p;
-              if (!hi) return kMatchPattern;
-            }
-            p++;
-          }
-          if (lo < hi) {
-            if (*t >= lo && *t <= hi) member = true, loop = false;
-          } else if (*t >= hi && *t <= lo) {
-            member = true, loop = false;
-          }
-        }
-        if ((invert && member) || !(invert || member)) return kMatchRange;
-        if (member) {
-          while (*p != ']') {
-            if (!*p) return kMatchPattern;
-            if (*p == '\\') {
-              p++;
-              if (!*p) return kMatchPattern;
-            }
-            p++;
-          }
-        }
-        break;
-      }
-      default:
-        if (*p != *t) return kMatchLiteral;
-    }
-  }
-  return *t ? kMatchEnd : kMatchValid;
-}
-int StkMatchAfterStar(const char* p, const char* t, char* s) {
-  int match = 0;
-  while (*p == '?' || *p == '%' || *p == '*') {
-    if (*p == '?' && !*t++) return kMatchAbort;
-    if (*p == '%') {
-      *s++ = *t;
-      *s = '\0';
-      if (!*t++) return kMatchAbort;
-    }
-    p++;
-  }
-  if (!*p) return kMatchValid;
-  const char nextp = *p;
-  do {
-    if (nextp == *t || nextp == '[') match = StkMatche(p, t, s);
-    if (!*t++) match = kMatchAbort;
-  } while (match != kMatchValid && match != kMatchAbort && match != kMatchPattern);
-  return match;
-}
-// ProcessMask (StkMatch.cc:453-490) as LabelContainer::FindInList calls it: "*/" prepended to a pattern that
-// does not start with '*', "/" to a label that does not start with '/'
-// (with the characters the '%'s capture: the CMN / CVN file names, Features.cc:1359-1392)
-bool ProcessMask(const std::string& label, const std::string& pattern, std::string* captured) {
-  std::vector<char> sub((size_t)std::count(pattern.begin(), pattern.end(), '%') + 2, '\0');
-  const std::string w = (pattern.empty() || pattern[0] != '*') ? "*/" + pattern : pattern;
-  const std::string t = (label.empty() || label[0] != '/') ? "/" + label : label;
-  const bool ok = StkMatche(w.c_str(), t.c_str(), sub.data()) == kMatchValid;
-  if (captured) *captured = ok ? std::string(sub.data()) : std::string();
-  return ok;
-}
-bool MaskMatches(const std::string& label, const std::string& pattern) { return ProcessMask(label, pattern, nullptr); }
-
-// FeatureRepository::ReadParmKind(str, false) (Features.cc:1438-1472), its prefix match of the base name included
-int ReadParmKindRef(const char* str) {
-  static const char* names[13] = {"WAVEFORM", "LPC", "LPREFC", "LPCEPSTRA", "LPDELCEP", "IREFC", "MFCC",
-                                  "FBANK", "MELSPEC", "USER", "DISCRETE", "PLP", "ANON"};
+// A parameter-kind name as FeatureRepository::ReadParmKind(str, false) reads it (Features.cc:1438-1472):
+// "_X" qualifiers peeled off the end, then the first base name that starts with what is left
+int ParseKindName(const std::string& text) {
+  static const char* const bases[13] = {"WAVEFORM", "LPC", "LPREFC", "LPCEPSTRA", "LPDELCEP", "IREFC", "MFCC",
+                                        "FBANK", "MELSPEC", "USER", "DISCRETE", "PLP", "ANON"};
+  static const std::pair<char, int> quals[] = {{'E', kParmE}, {'N', kParmN}, {'D', kParmD}, {'A', kParmA},
+                                               {'C', kParmC}, {'Z', kParmZ}, {'K', 010000}, {'0', kParm0},
+                                               {'V', 040000}, {'T', kParmT}};
+  std::string base = text;
   int kind = 0;
-  int slen = (int)strlen(str);
-  for (; slen >= 2 && str[slen - 2] == '_'; slen -= 2) {
-    const char q = str[slen - 1];
-    kind |= q == 'E' ? kParmE : q == 'N' ? kParmN : q == 'D' ? kParmD : q == 'A' ? kParmA : q == 'C' ? kParmC
-          : q == 'Z' ? kParmZ : q == 'K' ? 010000 : q == '0' ? kParm0 : q == 'V' ? 040000 : q == 'T' ? kParmT : -1;
-    if (kind == -1) return -1;
+  while (base.size() >= 2 && base[base.size() - 2] == '_') {
+    const char q = base.back();
+    const auto* it = std::find_if(std::begin(quals), std::end(quals), [q](const std::pair<char, int>& e) {
+      return e.first == q;
+    });
+    if (it == std::end(quals)) return -1;
+    kind |= it->second;
+    base.resize(base.size() - 2);
   }
   for (int i = 0; i < 13; i++)
-    if (!strncmp(str, names[i], (size_t)slen)) return kind | i;
+    if (std::string(bases[i]).compare(0, base.size(), base) == 0) return kind | i;
   return -1;
 }
 
-enum CepsNormType { kCnfMean, kCnfVariance, kCnfVarScale };
+enum class NormFile { kMean, kVariance, kVarScale };
 
-// FeatureRepository::ReadCepsNormFile (Features.cc:96-178), the same stdio parse and error texts: a header
-// "<CEPSNORM> <kind>" (not for VARSCALE), "<MEAN|VARIANCE|VARSCALE> n" with n == coefs, n numbers, end of file;
-// VARIANCE values become 1 / sqrt(v), VARSCALE values sqrt(v)
-std::vector<float> ReadCepsNormFile(const std::string& name, int sampleKind, CepsNormType type, int coefs) {
-  const char* typeStr = type == kCnfMean ? "MEAN" : type == kCnfVariance ? "VARIANCE" : "VARSCALE";
-  const char* typeStr2 = type == kCnfMean ? "CMN" : type == kCnfVariance ? "CVN" : "VarScale";
-  FILE* fp = fopen(name.c_str(), "r");
-  if (!fp) Fail(std::string("Cannot open ") + typeStr2 + " pFileName: '" + name + "'");
-  struct Closer {
-    FILE* f;
-    ~Closer() { fclose(f); }
-  } closer{fp};
-  char s1[80] = {0}, s2[80] = {0};
+// The text of a normalisation file, read as a sequence of lexical items: "<...>" tags (1..64 characters
+// other than '>'), integers, reals and whitespace-separated words (up to 64 characters shown).
+class NormText {
+ public:
+  explicit NormText(const std::string& path) {
+    std::ifstream in(path.c_str(), std::ios::binary);
+    ok_ = in.good();
+    if (ok_) text_.assign(std::istreambuf_iterator<char>(in), std::istreambuf_iterator<char>());
+  }
+  bool Opened() const { return ok_; }
+  bool Tag(std::string* inner) {
+    Blank();
+    if (at_ >= text_.size() || text_[at_] != '<') return false;
+    const size_t close = text_.find('>', at_ + 1);
+    const size_t len = (close == std::string::npos ? text_.size() : close) - (at_ + 1);
+    if (len == 0 || len > 64 || close == std::string::npos) return false;
+    *inner = text_.substr(at_ + 1, len);
+    at_ = close + 1;
+    return true;
+  }
+  bool Int(int* v) {
+    Blank();
+    char* end = nullptr;
+    const long x = strtol(text_.c_str() + at_, &end, 10);
+    if (end == text_.c_str() + at_) return false;
+    at_ = (size_t)(end - text_.c_str());
+    *v = (int)x;
+    return true;
+  }
+  bool Real(float* v) {
+    Blank();
+    char* end = nullptr;
+    const float x = strtof(text_.c_str() + at_, &end);
+    if (end == text_.c_str() + at_) return false;
+    at_ = (size_t)(end - text_.c_str());
+    *v = x;
+    return true;
+  }
+  bool Word(std::string* w) {
+    Blank();
+    size_t e = at_;
+    while (e < text_.size() && !isspace((unsigned char)text_[e])) e++;
+    if (e == at_) return false;
+    *w = text_.substr(at_, std::min<size_t>(e - at_, 64));
+    at_ = e;
+    return true;
+  }
+
+ private:
+  void Blank() {
+    while (at_ < text_.size() && isspace((unsigned char)text_[at_])) at_++;
+  }
+  std::string text_;
+  size_t at_ = 0;
+  bool ok_ = false;
+};
+
+std::string Upper(std::string s) {
+  for (char& c : s) c = (char)toupper((unsigned char)c);
+  return s;
+}
+
+// A CMN / CVN / VARSCALEFN file (FeatureRepository::ReadCepsNormFile, Features.cc:96-178): "<CEPSNORM> <kind>"
+// (not in a VARSCALE file; the kind must be the features'), then "<MEAN|VARIANCE|VARSCALE> n" with n the
+// expected count, n reals, nothing after them.  Tag names compare case-blind.  VARIANCE values are returned as
+// 1 / sqrt(v), VARSCALE values as sqrt(v) (in double, as KaldiLib computes them).  The reference's error texts.
+std::vector<float> ReadNormFile(const std::string& path, int sampleKind, NormFile type, int count) {
+  const char* section = type == NormFile::kMean ? "MEAN" : type == NormFile::kVariance ? "VARIANCE" : "VARSCALE";
+  const char* what = type == NormFile::kMean ? "CMN" : type == NormFile::kVariance ? "CVN" : "VarScale";
+  NormText in(path);
+  if (!in.Opened()) Fail(std::string("Cannot open ") + what + " pFileName: '" + path + "'");
+  std::string tag, kind;
+  bool header = true;
+  if (type != NormFile::kVarScale)
+    header = in.Tag(&tag) && in.Tag(&kind) && Upper(tag) == "CEPSNORM" && ParseKindName(kind) == sampleKind;
   int n = 0;
-  auto up = [](char* c) {
-    for (char* q = c; *q; q++) *q = (char)toupper((unsigned char)*q);
-    return c;
-  };
-  if ((type != kCnfVarScale && (fscanf(fp, " <%64[^>]> <%64[^>]>", s1, s2) != 2 || strcmp(up(s1), "CEPSNORM") ||
-                                ReadParmKindRef(s2) != sampleKind)) ||
-      fscanf(fp, " <%64[^>]> %d", s1, &n) != 2 || strcmp(up(s1), typeStr) || n != coefs) {
-    const std::string k = ParmKindStr((unsigned)sampleKind);
-    Fail(std::string("") + (type == kCnfVarScale ? "" : "<CEPSNORM> <") + (type == kCnfVarScale ? "" : k) +
-         (type == kCnfVarScale ? "" : ">") + " <" + typeStr + " ... expected in " + typeStr2 + " file " + name);
+  header = header && in.Tag(&tag) && in.Int(&n) && Upper(tag) == section && n == count;
+  if (!header) {
+    const std::string prefix =
+        type == NormFile::kVarScale ? std::string() : "<CEPSNORM> <" + ParmKindStr((unsigned)sampleKind) + ">";
+    Fail(prefix + " <" + section + " ... expected in " + what + " file " + path);
   }
-  std::vector<float> v((size_t)coefs);
-  for (int i = 0; i < coefs; i++) {
-    if (fscanf(fp, " %g", &v[(size_t)i]) != 1) {
-      if (fscanf(fp, "%64s", s2) == 1)
-        Fail(std::string("Decimal number expected but '") + s2 + "' found in " + typeStr2 + " file " + name);
-      else if (feof(fp))
-        Fail(std::string("Unexpected end of ") + typeStr2 + " file " + name);
-      else
-        Fail(std::string("Cannot read ") + typeStr2 + " file " + name);
+  std::vector<float> v((size_t)count);
+  std::string word;
+  for (float& x : v) {
+    if (!in.Real(&x)) {
+      if (in.Word(&word)) Fail("Decimal number expected but '" + word + "' found in " + what + " file " + path);
+      Fail(std::string("Unexpected end of ") + what + " file " + path);
     }
-    // double arithmetic: KaldiLib calls the C library's sqrt(double) (measured bit-exact against the reference)
-    if (type == kCnfVariance) v[(size_t)i] = (float)(1 / sqrt((double)v[(size_t)i]));
-    else if (type == kCnfVarScale) v[(size_t)i] = (float)sqrt((double)v[(size_t)i]);
+    if (type == NormFile::kVariance) x = (float)(1 / sqrt((double)x));
+    else if (type == NormFile::kVarScale) x = (float)sqrt((double)x);
   }
-  if (fscanf(fp, "%64s", s2) == 1)
-    Fail(std::string("End of file expected but '") + s2 + "' found in " + typeStr2 + " file " + name);
+  if (in.Word(&word)) Fail("End of file expected but '" + word + "' found in " + what + " file " + path);
   return v;
+}
+
+// The normalisation file a mask picks for a logical name: the characters its '%'s capture ("" when it does not
+// match), masks compiled once per thread
+std::string MaskCapture(const std::string& logical, const std::string& mask) {
+  thread_local std::unordered_map<std::string, LabelMask> compiled;
+  auto it = compiled.find(mask);
+  if (it == compiled.end()) it = compiled.emplace(mask, LabelMask::ForPath(mask)).first;
+  std::string captured;
+  it->second.Matches(LabelMask::AsPath(logical), &captured);
+  return captured;
 }
 }  // namespace
 
@@ -553,13 +538,12 @@ void ApplyCepsNorm(const FeatureConfig& cfg, const std::string& logical, int tar
   thread_local std::string last_cmn, last_cvn, last_cvg;
   thread_local std::vector<float> cmn, cvn, cvg;
   if (cfg.cmn) {
-    std::string name;
-    ProcessMask(logical, cfg.cmnMask, &name);
+    std::string name = MaskCapture(logical, cfg.cmnMask);
     if (name.empty()) Fail("CMN Matching failed");
     name = (cfg.cmnDir.empty() ? std::string() : cfg.cmnDir + "/") + "/" + name;
     if (name != last_cmn) {
       last_cmn.clear();
-      cmn = ReadCepsNormFile(name, kind & ~kParmZ, kCnfMean, coefs);
+      cmn = ReadNormFile(name, kind & ~kParmZ, NormFile::kMean, coefs);
       last_cmn = name;
     }
     for (int i = 0; i < tot; i++)
@@ -567,12 +551,11 @@ void ApplyCepsNorm(const FeatureConfig& cfg, const std::string& logical, int tar
   }
   kind |= derivOrder == 3 ? (kParmD | kParmA | kParmT) : derivOrder == 2 ? (kParmD | kParmA) : derivOrder == 1 ? kParmD : 0;
   if (cfg.cvn) {
-    std::string name;
-    ProcessMask(logical, cfg.cvnMask, &name);
+    std::string name = MaskCapture(logical, cfg.cvnMask);
     name = (cfg.cvnDir.empty() ? std::string() : cfg.cvnDir + "/") + "/" + name;
     if (name != last_cvn) {
       last_cvn.clear();
-      cvn = ReadCepsNormFile(name, kind, kCnfVariance, trg_vec);
+      cvn = ReadNormFile(name, kind, NormFile::kVariance, trg_vec);
       last_cvn = name;
     }
     for (int i = 0; i < tot; i++)
@@ -581,96 +564,11 @@ void ApplyCepsNorm(const FeatureConfig& cfg, const std::string& logical, int tar
   if (cfg.cvg) {
     if (cfg.cvgFile != last_cvg) {
       last_cvg.clear();
-      cvg = ReadCepsNormFile(cfg.cvgFile, -1, kCnfVarScale, trg_vec);
+      cvg = ReadNormFile(cfg.cvgFile, -1, NormFile::kVarScale, trg_vec);
       last_cvg = cfg.cvgFile;
     }
     for (int i = 0; i < tot; i++)
       for (int j = trg_N; j < trg_vec; j++) M[(size_t)i * trg_vec + (j - trg_N)] *= cvg[(size_t)j];
-  }
-}
-
-namespace {
-// PATH_MAX on Linux: MlfStream.h's MAX_LABEL_DEPTH, the depth of a name without a leading '*'
-constexpr size_t kMaxLabelDepth = 4096;
-size_t DirDepth(const std::string& path) {
-  return (size_t)std::count(path.begin(), path.end(), '/') + (size_t)std::count(path.begin(), path.end(), '\\');
-}
-}  // namespace
-
-// LabelContainer::FindInHash (MlfStream.cc:97-197), the reference's position arithmetic kept as it is
-// (including find_last_of from prev - 1 when prev is 0, which wraps to the whole label)
-bool MlfLabels::FindInHash(const std::string& label, size_t* rec, size_t* limit) const {
-  bool found = false;
-  std::string str;
-  size_t current_depth = kMaxLabelDepth, prev = label.size() + 1;
-  auto lookup = [&](const std::string& key) {
-    auto it = mHash.find(key);
-    if (it == mHash.end()) return false;
-    *rec = it->second.rec;
-    *limit = it->second.limit;
-    return true;
-  };
-  for (auto ri = mDepths.rbegin(); !found && ri != mDepths.rend(); ++ri) {
-    if (*ri == kMaxLabelDepth) {
-      found = lookup(label);
-    } else if (current_depth == kMaxLabelDepth) {
-      if (*ri > 0) {
-        for (size_t i = 1; i <= *ri && prev != std::string::npos; i++) prev = label.find_last_of("/\\", prev - 1);
-      } else {
-        prev = 0;
-      }
-      if (prev != std::string::npos) {
-        str.assign(label, prev, label.size());
-        str = '*' + str;
-        found = lookup(str);
-        current_depth = *ri;
-      } else {
-        prev = label.size() + 1;
-      }
-    } else {
-      while (current_depth > *ri) {
-        if ((prev = label.find_first_of("/\\", prev + 1)) != std::string::npos) current_depth--;
-        else return false;
-      }
-      str.assign(label, prev, label.size());
-      str = '*' + str;
-      found = lookup(str);
-    }
-  }
-  return found;
-}
-
-// LabelContainer::FindInList (MlfStream.cc:201-239): the first of the first `limit` patterns (0: all) that
-// ProcessMask matches
-bool MlfLabels::FindInList(const std::string& label, size_t limit, size_t* rec) const {
-  const size_t n = limit ? std::min(limit, mList.size()) : mList.size();
-  for (size_t k = 0; k < n; k++)
-    if (MaskMatches(label, mList[k].first)) {
-      *rec = mList[k].second;
-      return true;
-    }
-  return false;
-}
-
-// LabelContainer::Find (MlfStream.cc:243-262): a hash hit can be overridden by a list pattern defined before it
-const MlfLabels::Record* MlfLabels::Find(const std::string& label) const {
-  size_t rec = 0, limit = 0;
-  if (FindInHash(label, &rec, &limit)) {
-    (void)FindInList(label, limit, &rec);
-    return &mRecords[rec];
-  }
-  return FindInList(label, 0, &rec) ? &mRecords[rec] : nullptr;
-}
-
-// LabelContainer::Insert (MlfStream.cc:43-93): a pattern with no wildcard after its first character is
-// hashed -- unless an earlier definition (hashed or listed) already matches it -- else listed; every
-// '*'-led pattern records its directory depth for FindInHash's walk
-void MlfLabels::Insert(const std::string& pattern, size_t rec) {
-  mDepths.insert(!pattern.empty() && pattern[0] == '*' ? DirDepth(pattern) : kMaxLabelDepth);
-  if (pattern.find_first_of("*?%", 1) == std::string::npos) {
-    if (!Find(pattern)) mHash[pattern] = Hashed{rec, mList.size()};
-  } else {
-    mList.emplace_back(pattern, rec);
   }
 }
 
@@ -705,7 +603,7 @@ MlfLabels::MlfLabels(const std::string& mlf, const std::string& labelMap, const 
         const size_t idx = mRecords.size();
         mRecords.emplace_back();
         cur = &mRecords.back();
-        Insert(pat, idx);
+        mIndex.Insert(pat, idx);
       }
       continue;
     }
@@ -738,8 +636,9 @@ MlfLabels::MlfLabels(const std::string& mlf, const std::string& labelMap, const 
 
 size_t MlfLabels::ClassIds(const std::string& featureLogical, size_t nFrames, size_t sourceRate, int* out) const {
   const std::string lab = MakeHtkFileName(featureLogical, mDir, mExt);
-  const Record* rec = Find(lab);
-  if (!rec) Fail("Cannot open label MLF record: " + lab);
+  size_t found = 0;
+  if (!mIndex.Find(lab, &found)) Fail("Cannot open label MLF record: " + lab);
+  const Record* rec = &mRecords[found];
   if (nFrames < 1) Fail("Number of frames:" + std::to_string(nFrames) + " is lower than 1!!!\n" + featureLogical);
   if (!rec->error.empty()) Fail(rec->error + "\nfile: " + lab + "\n");
   if (sourceRate == 0) Fail("Zero sample period in features of " + featureLogical);

@@ -7,16 +7,14 @@
 //                                                             frame range, STARTFRMEXT/ENDFRMEXT edge
 //                                                             replication, sentence mean (_Z), deltas
 //   LabelRepository::GenDesiredMatrix   src/KaldiLib/Labels.cc:42-186  MLF segments -> per-frame targets
-//   LabelContainer::Find                src/KaldiLib/MlfStream.cc:96-265  "*/name.lab" pattern lookup
+//   LabelContainer::Find                src/KaldiLib/MlfStream.cc:96-265  "*/name.lab" pattern lookup (labelindex.h)
 //   MakeHtkFileName                     src/KaldiLib/Common.cc:118-172
 // The reference reads a file frame by frame (an fseek + fread per frame, Features.cc:1207-1258) on the
 // training thread, between cache fills (TNetCu.cc:376-419).  Here a file is one pread into memory,
 // decoded (byte order, int16 decompression) in place, and up to `depth` utterances are read ahead of
 // the consumer by `threads` workers, delivered strictly in script order.  Targets come out as class
 // ids (one int per frame) -- the one-hot rows of GenDesiredMatrix, as the trainer consumes them.
-//
-// Not built: cepstral mean / variance normalisation from CMEANDIR / VARSCALEDIR files and the
-// VARSCALEFN global variance (Features.cc:1350-1470); the hot path's recipes do not use them.
+//   CMN / CVN / VARSCALEFN              Features.cc:96-178, 1350-1410  normalisation files by mask
 #pragma once
 
 #include <condition_variable>
@@ -29,6 +27,8 @@
 #include <thread>
 #include <unordered_map>
 #include <vector>
+
+#include "labelindex.h"
 
 namespace tnetio {
 
@@ -123,27 +123,13 @@ class MlfLabels {
     std::vector<Segment> segs;
     std::string error;  // a line GenDesiredMatrix could not parse (reported when the record is used)
   };
-  // LabelContainer (MlfStream.cc:43-265): Find is FindInHash over the recorded depths (deepest first, the
-  // reference's position arithmetic included), then -- after a hash hit -- the list patterns defined before
-  // that record (all of them when the list was empty at its insertion), else the whole list in file order
-  const Record* Find(const std::string& label) const;
-  bool FindInHash(const std::string& label, size_t* rec, size_t* limit) const;
-  bool FindInList(const std::string& label, size_t limit, size_t* rec) const;
-  void Insert(const std::string& pattern, size_t rec);
-
   std::string mMlf;
   const char* mDir;
   const char* mExt;
   std::string mDirS, mExtS;
   std::unordered_map<std::string, int> mStates;
   std::vector<std::string> mTags;
-  struct Hashed {
-    size_t rec;    // index into mRecords
-    size_t limit;  // list patterns defined before this record (0: the list was empty -- search it all)
-  };
-  std::unordered_map<std::string, Hashed> mHash;      // names and patterns without wildcards after position 0
-  std::set<size_t> mDepths;                           // DirDepth of every '*' pattern, kMaxLabelDepth for names
-  std::vector<std::pair<std::string, size_t>> mList;  // patterns with wildcards, in file order
+  LabelIndex mIndex;  // MLF record patterns -> index into mRecords (labelindex.h)
   std::vector<Record> mRecords;
 };
 

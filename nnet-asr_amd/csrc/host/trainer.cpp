@@ -5,6 +5,7 @@
 
 #include <algorithm>
 #include <cstring>
+#include <limits>
 #include <sys/time.h>
 
 namespace TNet {
@@ -331,11 +332,42 @@ void HostExchange::GatherParams(CuUpdatableComponent& comp, int i, void* stream)
   }
 }
 
+void GradExchange::CaptureLocal(CuUpdatableComponent& comp, void* stream) {
+  if (!mCaptureArmed) return;
+  TNET_HIP_CALL(hipStreamSynchronize((hipStream_t)stream));
+  mCaptureFirst = mCaptured.size();
+  for (auto& b : comp.GradientBlocks()) {
+    CapturedBlock c;
+    c.local.resize((size_t)b.n);
+    TNET_HIP_CALL(hipMemcpy(c.local.data(), b.grad, (size_t)b.n * sizeof(float), hipMemcpyDeviceToHost));
+    mCaptured.push_back(std::move(c));
+  }
+}
+
+void GradExchange::CaptureReduced(CuUpdatableComponent& comp, void* stream) {
+  if (!mCaptureArmed) return;
+  TNET_HIP_CALL(hipStreamSynchronize((hipStream_t)stream));
+  size_t k = mCaptureFirst;
+  for (auto& b : comp.GradientBlocks()) {
+    if (k >= mCaptured.size()) Error("GradExchange: capture out of step with the submitted blocks");
+    std::vector<float> all((size_t)b.n);
+    TNET_HIP_CALL(hipMemcpy(all.data(), b.grad, (size_t)b.n * sizeof(float), hipMemcpyDeviceToHost));
+    CapturedBlock& c = mCaptured[k++];
+    c.reduced.assign((size_t)b.n, std::numeric_limits<float>::quiet_NaN());
+    long lo[2], hi[2];
+    const int nr = ApplyRanges(b.n, lo, hi);
+    for (int r = 0; r < nr; r++)
+      std::copy(all.begin() + lo[r], all.begin() + hi[r], c.reduced.begin() + lo[r]);
+  }
+}
+
 void HostExchange::Submit(CuUpdatableComponent& comp) {
   CuDevice::Instantiate().KTCloseRun();  // no roofline timing run spans an exchange step
   CuDevice& dev = CuDevice::Instantiate();
   TNET_HIP_CALL(hipStreamSynchronize(dev.Stream()));
+  CaptureLocal(comp, dev.Stream());
   for (auto& b : comp.GradientBlocks()) AllReduceDevice(b.grad, (size_t)b.n);
+  CaptureReduced(comp, dev.Stream());
 }
 
 void HostExchange::AllReduceDevice(float* buf, size_t n) {
@@ -474,6 +506,7 @@ void RcclExchange::Submit(CuUpdatableComponent& comp) {
   // the gradient kernels were enqueued on the compute stream: order the reduction after them
   TNET_HIP_CALL(hipEventRecord(ev, dev.Stream()));
   TNET_HIP_CALL(hipStreamWaitEvent(mImpl->comm_stream, ev, 0));
+  CaptureLocal(comp, mImpl->comm_stream);
   std::vector<CuParamBlock> blocks = comp.GradientBlocks();
   NCCL_CALL(ncclGroupStart());
   for (auto& b : blocks) {
@@ -493,6 +526,13 @@ void RcclExchange::Submit(CuUpdatableComponent& comp) {
   NCCL_CALL(ncclGroupEnd());
   TNET_HIP_CALL(hipEventRecord(mImpl->ar_done[idx], mImpl->comm_stream));
   mImpl->ar_seq[idx] = ++mImpl->comm_seq;
+  CaptureReduced(comp, mImpl->comm_stream);
+}
+
+int RcclExchange::TransportRanks() const {
+  int n = 0;
+  NCCL_CALL(ncclCommCount(mImpl->comm, &n));
+  return n;
 }
 
 int RcclExchange::ApplyRanges(long n, long* lo, long* hi) const {
@@ -560,6 +600,7 @@ void RcclExchange::WaitAll() {
   mImpl->comm_seq = mImpl->compute_covered = mImpl->apply_covered = 0;
   mImpl->next_event = 0;
   if (mReserve > 0) TNET_SAFE_CALL(tnet_gemm_reserve(0));
+  DisarmCapture();
 }
 
 void RcclExchange::AllReduceHost(double* v, int n) {

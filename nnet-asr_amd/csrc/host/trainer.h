@@ -111,7 +111,7 @@ class HostExchange : public GradExchange {
   int Rank() const override { return mRank; }
   int WorldSize() const override { return mWorld; }
   void Submit(CuUpdatableComponent& comp) override;
-  void WaitAll() override {}
+  void WaitAll() override { DisarmCapture(); }
   void AllReduceHost(double* v, int n) override;
   void AllReduceDevice(float* buf, size_t n);
   /// TNET_DP_SHARD=1: the sharded-apply protocol of RcclExchange emulated through the host
@@ -155,6 +155,7 @@ class RcclExchange : public GradExchange {
   /// the apply's HBM traffic divided by the world size, the same bytes over xGMI as an all-reduce
   int ApplyRanges(long n, long* lo, long* hi) const override;
   void GatherParams(CuUpdatableComponent& comp, int i, void* stream) override;
+  int TransportRanks() const override;
 
  private:
   struct Impl;

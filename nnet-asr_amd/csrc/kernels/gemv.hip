@@ -1033,11 +1033,15 @@ extern "C" int tnet_rnn_bptt_chain(const float* W, int ldw, int r0, int n, float
   return TNET_OK;
 }
 
-extern "C" int tnet_rnn_bptt_chain_error(const void* workspace, int* err) {
+extern "C" int tnet_rnn_bptt_chain_error(const void* workspace, int* err, void* stream) {
   if (!workspace || !err) return TNET_ERR_ARG;
-  return hipMemcpy(err, &((const BpttChainCtl*)workspace)->err, sizeof(int), hipMemcpyDeviceToHost) == hipSuccess
-             ? TNET_OK
-             : TNET_ERR_RUNTIME;
+  // on the chain's own stream: a non-blocking stream is not ordered with a null-stream copy
+  const hipStream_t st = (hipStream_t)stream;
+  if (hipMemcpyAsync(err, &((const BpttChainCtl*)workspace)->err, sizeof(int), hipMemcpyDeviceToHost, st) !=
+          hipSuccess ||
+      hipStreamSynchronize(st) != hipSuccess)
+    return TNET_ERR_RUNTIME;
+  return TNET_OK;
 }
 
 extern "C" int tnet_rnn_update(float* W, int ldw, int rows, int nout, const float* hist, int ldh, int head, int R,

@@ -135,15 +135,20 @@ struct ArgMax {
   int i;
 };
 __device__ __forceinline__ ArgMax argmax_merge(ArgMax a, ArgMax b) {
-  // first maximum wins: larger value, or equal value with smaller index
-  if (b.v > a.v || (b.v == a.v && b.i < a.i)) return b;
+  // first maximum wins: larger value, or equal value with smaller index.  A NaN never wins over a number (the
+  // reference's scan `val > max` never takes one, cukernels.cu:408-411) and two NaNs go by index, so the merge
+  // is symmetric for every input -- what the butterfly below relies on
+  const bool a_nan = a.v != a.v, b_nan = b.v != b.v;
+  if (a_nan != b_nan) return a_nan ? b : a;
+  if (b.v > a.v || (!(b.v < a.v) && b.i < a.i)) return b;
   return a;
 }
 template <int S>
 __device__ __forceinline__ ArgMax xstep_am(ArgMax a) {
   return ArgMax{xstep_f<S>(a.v), (int)xstep<S>((unsigned)a.i)};
 }
-// argmax_merge is symmetric (the larger value, the smaller index on ties), so the butterfly steps above apply
+// argmax_merge is symmetric (the larger value, the smaller index on ties, NaN ordered below every number), so the
+// butterfly steps above apply
 __device__ __forceinline__ ArgMax wave_argmax(ArgMax a) {
   a = argmax_merge(a, xstep_am<0>(a));
   a = argmax_merge(a, xstep_am<1>(a));

@@ -16,7 +16,7 @@ from . import formats  # noqa: F401  (host formats; no device code)
 from ._lib import HOST_ALLREDUCE_FN, LIB_PATH, MatrixDim, TnetError, check, check_ptr, header_symbols, lib
 
 __all__ = ["DeviceArray", "Network", "Objective", "Trainer", "RbmTrainer", "RnnTrainer", "Comm", "TnetError", "synchronize",
-           "FeatureReader", "htk_read",
+           "FeatureReader", "htk_read", "mask_match", "mlf_lookup",
            "pad_stride",
            "device_count", "version", "LIB_PATH", "header_symbols", "formats"]
 
@@ -490,6 +490,29 @@ class Comm:
         """Rows of the global bunch for the next steps' GRADDIVFRM division (0 = rows x world)."""
         check(lib().tnet_comm_set_step_rows(self.h, global_rows), "set_step_rows")
 
+    def capture(self, on: bool = True) -> None:
+        """arm the reduction check for ONE step (tnet_comm_capture): the next step's gradient blocks are copied
+        to the host before and after their reduction"""
+        check(lib().tnet_comm_capture(self.h, int(on)), "comm_capture")
+
+    def captured(self):
+        """[(local, reduced)] per gradient block of the last armed step, in submission order; `reduced` holds
+        NaN outside the ranges this rank applies"""
+        out = []
+        for i in range(lib().tnet_comm_captured(self.h)):
+            n = C.c_long(0)
+            check(lib().tnet_comm_captured_block(self.h, i, None, None, 0, C.byref(n)), "captured_block")
+            loc, red = np.empty(n.value, np.float32), np.empty(n.value, np.float32)
+            check(lib().tnet_comm_captured_block(self.h, i, loc.ctypes.data, red.ctypes.data, n.value, C.byref(n)),
+                  "captured_block")
+            out.append((loc, red))
+        return out
+
+    def transport_ranks(self) -> int:
+        r = C.c_int(0)
+        check(lib().tnet_comm_transport_ranks(self.h, C.byref(r)), "transport_ranks")
+        return r.value
+
     def allreduce_device(self, a: "DeviceArray") -> None:
         check(lib().tnet_comm_allreduce_device(self.h, a.ptr, a.rows * a.stride), "allreduce_device")
 
@@ -579,3 +602,23 @@ def htk_read(record: str, start_ext: int = 0, end_ext: int = 0, swap: bool = Tru
     check(lib().tnet_htk_read(record.encode(), int(swap), start_ext, end_ext, out.ctypes.data, out.size, C.byref(rows),
                               C.byref(cols), C.byref(per), C.byref(kind)), "htk_read")
     return out, per.value, kind.value
+
+
+def mask_match(mask: str, label: str):
+    """ProcessMask (StkMatch.cc:453-490) through the native label mask: None when `mask` does not match
+    `label`, else the characters its '%'s capture"""
+    buf = C.create_string_buffer(4096)
+    r = lib().tnet_mask_match(mask.encode("latin-1"), label.encode("latin-1"), buf, len(buf))
+    check(min(r, 0), "mask_match")
+    return buf.value.decode("latin-1") if r == 1 else None
+
+
+def mlf_lookup(patterns, labels):
+    """LabelContainer Insert(patterns[k], k) in order, then Find(label) for each label (MlfStream.cc:43-265)
+    through the native MLF index: the record numbers, -1 where none"""
+    P = (C.c_char_p * max(1, len(patterns)))(*[p.encode("latin-1") for p in patterns])
+    L = (C.c_char_p * max(1, len(labels)))(*[x.encode("latin-1") for x in labels])
+    out = np.full(max(1, len(labels)), -2, np.int32)
+    check(lib().tnet_mlf_lookup(C.cast(P, C.c_void_p), len(patterns), C.cast(L, C.c_void_p), len(labels),
+                                out.ctypes.data), "mlf_lookup")
+    return out[:len(labels)].tolist()

@@ -172,12 +172,18 @@ _SIGS = {
     "tnet_reader_rewind": (i32, [vp]),
     "tnet_htk_read": (i32, [C.c_char_p, i32, i32, i32, vp, i64, C.POINTER(i32), C.POINTER(i32), C.POINTER(i32),
                            C.POINTER(i32)]),
+    "tnet_mask_match": (i32, [C.c_char_p, C.c_char_p, C.c_char_p, i32]),
+    "tnet_mlf_lookup": (i32, [vp, i32, vp, i32, vp]),
     "tnet_trainer_add_reader": (i64, [vp, vp, i64]),
     "tnet_comm_unique_id": (i32, [C.c_char_p]),
     "tnet_comm_create": (vp, [i32, i32, C.c_char_p]),
     "tnet_comm_free": (i32, [vp]),
     "tnet_comm_allreduce_host": (i32, [vp, dp, i32]),
     "tnet_comm_allreduce_device": (i32, [vp, vp, i64]),
+    "tnet_comm_capture": (i32, [vp, i32]),
+    "tnet_comm_captured": (i64, [vp]),
+    "tnet_comm_captured_block": (i32, [vp, i64, vp, vp, i64, C.POINTER(i64)]),
+    "tnet_comm_transport_ranks": (i32, [vp, C.POINTER(i32)]),
     "tnet_comm_create_host": (vp, [i32, i32, vp, vp]),
     "tnet_net_rbm_get": (i32, [vp, i32, vp, vp, vp, vp]),
     "tnet_net_rbm_set": (i32, [vp, i32, vp, vp, vp, i32, i32]),
@@ -202,7 +208,7 @@ _SIGS = {
     "tnet_gemv_rows": (i32, [vp, i32, i32, i32, i32, vp, vp, f32, vp, vp]),
     "tnet_rnn_bptt_chain_workspace": (i64, [i32, i32]),
     "tnet_rnn_bptt_chain": (i32, [vp, i32, i32, i32, vp, i32, i32, vp, i32, i32, i32, i32, vp, vp]),
-    "tnet_rnn_bptt_chain_error": (i32, [vp, vp]),
+    "tnet_rnn_bptt_chain_error": (i32, [vp, vp, vp]),
     "tnet_rnn_update": (i32, [vp, i32, i32, i32, vp, i32, i32, i32, vp, i32, i32, vp, vp, f32, f32, f32, vp]),
     "tnet_affine_fwd_t": (i32, [vp, MatrixDim, vp, MatrixDim, vp, vp, MatrixDim, i32, vp]),
     "tnet_rbm_update": (i32, [vp, MatrixDim, vp, MatrixDim, vp, MatrixDim, vp, i32, f32, f32, f32, vp]),

@@ -16,6 +16,8 @@
 //             every utterance's matrix and class ids, or the exception text of a failing record.
 //   shuffle : the cache permutation produced by Cache::Init(seed)+AddData+Randomize
 //             (src/TNetLib/Cache.cc:23-192) -- lrand48 + libstdc++ random_shuffle.
+//   mlfmatch: KaldiLib's ProcessMask (StkMatch.cc:453-490) and LabelContainer Insert / Find
+//             (MlfStream.cc:43-265) answering line commands (the MLF lookup fuzz fixture, make_mlfmatch.py)
 //
 // It is our own code; no reference source is copied.  Output is raw little-endian float32
 // / int32 files plus .nnet text written with 9 significant digits (exact float round trip).
@@ -38,6 +40,8 @@
 #include "Labels.h"
 #include "Timer.h"
 #include "UserInterface.h"
+#include "StkMatch.h"
+#include "MlfStream.h"
 
 using namespace TNet;
 
@@ -335,8 +339,48 @@ static int cmd_features(int argc, char** argv) {
   std::_Exit(0);
 }
 
+// mlfmatch: line commands on stdin (fields separated by TAB), one answer line per query on stdout
+//   M <mask> <label>      ProcessMask(label, mask, sub): "1\t<sub>" or "0"
+//   I <pattern> <record>  LabelContainer::Insert(pattern, record) into the current container
+//   F <label>             LabelContainer::Find(label): the record's number or -1
+//   R                     start a new, empty container
+static int cmd_mlfmatch() {
+  LabelContainer* box = new LabelContainer();
+  std::string line;
+  while (std::getline(std::cin, line)) {
+    std::vector<std::string> f;
+    size_t a = 0;
+    for (;;) {
+      size_t b = line.find('\t', a);
+      f.push_back(line.substr(a, b == std::string::npos ? std::string::npos : b - a));
+      if (b == std::string::npos) break;
+      a = b + 1;
+    }
+    if (f[0] == "M" && f.size() == 3) {
+      std::string sub;
+      const bool ok = ProcessMask(f[2], f[1], sub);
+      if (ok) std::cout << "1\t" << sub << "\n";
+      else std::cout << "0\n";
+    } else if (f[0] == "I" && f.size() == 3) {
+      box->Insert(f[1], std::streampos(atol(f[2].c_str())));
+    } else if (f[0] == "F" && f.size() == 2) {
+      LabelRecord rec;
+      if (box->Find(f[1], rec)) std::cout << (long)(std::streamoff)rec.mStreamPos << "\n";
+      else std::cout << "-1\n";
+    } else if (f[0] == "R") {
+      box = new LabelContainer();  // the previous one is left allocated: its destructor is not the subject
+    } else {
+      std::cerr << "bad command: " << line << "\n";
+      return 2;
+    }
+  }
+  std::cout.flush();
+  std::_Exit(0);
+}
+
 int main(int argc, char** argv) try {
-  if (argc < 2) { std::cerr << "modes: step | trajectory | shuffle | train | features\n"; return 2; }
+  if (argc < 2) { std::cerr << "modes: step | trajectory | shuffle | train | features | mlfmatch\n"; return 2; }
+  if (std::string(argv[1]) == "mlfmatch") return cmd_mlfmatch();
   std::string mode = argv[1];
   if (mode == "step") return cmd_step(argc, argv);
   if (mode == "trajectory") return cmd_trajectory(argc, argv);

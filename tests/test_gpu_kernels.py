@@ -915,6 +915,39 @@ def test_affine_grad_bias_gather_matches_separate_calls(rows, n_in, n_out, gcols
         np.testing.assert_array_equal(l_, labc[perm])
 
 
+def test_affine_grad_bias_gather_two_gemms_mlp3():
+    """the two-GEMM form of tnet_affine_grad_bias_gather on MLP3's last two gradients (598x1024 over the bunch, and
+    1024x135 -- which the planner alone would split over K): both gradients and bias gradients against the fp64
+    products (each GEMM unsplit here, its sums in k order: bit-identical to the single form where that runs unsplit
+    too, within fp32 summation order of a split-K run otherwise), the gathered rows and class ids exact"""
+    rows = 1024
+    X1, E1 = rnd((rows, 598), 530), rnd((rows, 1024), 531, 0.01)
+    X2, E2 = rnd((rows, 1024), 532), rnd((rows, 135), 533, 0.01)
+    P1, P2 = slab_sums(E1).astype(np.float32), slab_sums(E2).astype(np.float32)
+    Xc = rnd((3000, 598), 534)
+    labc = (np.arange(3000, dtype=np.int32) * 7) % 135
+    perm = np.random.default_rng(535).permutation(3000).astype(np.int32)[:rows]
+    d = {k: DeviceArray.from_numpy(v) for k, v in dict(X1=X1, E1=E1, X2=X2, E2=E2, P1=P1, P2=P2, Xc=Xc).items()}
+    dG1 = DeviceArray.from_numpy(np.full((598, 1024), np.nan, np.float32))
+    dG2 = DeviceArray.from_numpy(np.full((1024, 135), np.nan, np.float32))
+    db1, db2 = DeviceArray.vector(np.full(1024, np.nan, np.float32)), DeviceArray.vector(np.full(135, np.nan, np.float32))
+    dLc, dPerm = DeviceArray.vector(labc), DeviceArray.vector(perm)
+    dY = DeviceArray.from_numpy(np.full((rows, 598), np.nan, np.float32))
+    dLo = DeviceArray.vector(np.full(rows, -7, np.int32))
+    st = lib().tnet_affine_grad_bias_gather(
+        d["X2"].ptr, d["X2"].dim, d["E2"].ptr, d["E2"].dim, dG2.ptr, dG2.dim, d["P2"].ptr, d["P2"].stride, db2.ptr,
+        d["X1"].ptr, d["X1"].dim, d["E1"].ptr, d["E1"].dim, dG1.ptr, dG1.dim, d["P1"].ptr, d["P1"].stride, db1.ptr,
+        dY.ptr, d["Xc"].ptr, dLo.ptr, dLc.ptr, dPerm.ptr, dY.dim, d["Xc"].dim, S())
+    if st == TNET_ERR_UNSUPPORTED:
+        pytest.skip("the pair does not fit one round on this device")
+    check(st)
+    for G, b, X, E, P in ((dG1, db1, X1, E1, P1), (dG2, db2, X2, E2, P2)):
+        np.testing.assert_allclose(G.numpy(), X.astype(np.float64).T @ E.astype(np.float64), rtol=1e-4, atol=1e-5)
+        np.testing.assert_array_equal(b.numpy().ravel(), P.astype(np.float64).sum(0).astype(np.float32))
+    np.testing.assert_array_equal(dY.numpy(), Xc[perm])
+    np.testing.assert_array_equal(dLo.numpy()[:, 0], labc[perm])
+
+
 @pytest.mark.parametrize("rows,n_in,n_out", [(1024, 2048, 4000), (1024, 2048, 2048), (256, 512, 1000), (64, 128, 4000)])
 def test_affine_bwd_colsum_slabs_matches_two_calls(rows, n_in, n_out):
     """tnet_affine_bwd_colsum_slabs (the top layer's backward GEMM + the slab sums of its input error in ONE

@@ -462,4 +462,4 @@ def test_bptt_chain_matches_per_step_launches(n_in, n, order):
             outs.append(dD.numpy())
         np.testing.assert_array_equal(outs[0], outs[1], err_msg=f"launch {launch}")
     err = ctypes.c_int(-1)
-    assert L().tnet_rnn_bptt_chain_error(ws.ptr, ctypes.byref(err)) == 0 and err.value == 0
+    assert L().tnet_rnn_bptt_chain_error(ws.ptr, ctypes.byref(err), None) == 0 and err.value == 0

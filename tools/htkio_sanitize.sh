@@ -4,7 +4,7 @@
 set -e -o pipefail
 R=$(cd "$(dirname "$0")/.." && pwd)
 B=$(mktemp -d)
-SRC="$R/tools/htkio_sanitize.cpp $R/nnet-asr_amd/csrc/host/htkio.cpp"
+SRC="$R/tools/htkio_sanitize.cpp $R/nnet-asr_amd/csrc/host/htkio.cpp $R/nnet-asr_amd/csrc/host/labelindex.cpp"
 INC="-I$R/nnet-asr_amd/csrc/host"
 EX="$R/tests/golden/ex01"
 g++ -std=c++17 -O1 -g -fsanitize=thread $INC $SRC -o "$B/tsan" -pthread

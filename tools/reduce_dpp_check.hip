@@ -8,6 +8,7 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <cmath>
 #include <cstring>
 #include <vector>
 
@@ -20,7 +21,8 @@ using namespace tnetk;
 __global__ __launch_bounds__(256) void check_kernel(const float* in, const int* ties, unsigned* out) {
   const int g = blockIdx.x * blockDim.x + threadIdx.x;
   const float v = in[g];
-  const float t = ties[g] ? 1.0f : v;  // many equal values: argmax ties
+  // many equal values (argmax ties) and NaNs (never the maximum; ordered by index among themselves)
+  const float t = ties[g] == 1 ? 1.0f : ties[g] == 2 ? __int_as_float(0x7fc00000) : v;
   unsigned* o = out + (long)g * 12;
   const float s0 = wave_sum(v), s1 = wave_sum_shfl(v);
   const float m0 = wave_max(v), m1 = wave_max_shfl(v);
@@ -52,7 +54,9 @@ int main() {
     const float u = (float)(s >> 8) / 16777216.0f - 0.5f;
     const int e = (int)((s >> 3) % 40) - 20;
     h[i] = ldexpf(u, e);
-    ties[i] = ((s >> 13) % 5) == 0;
+    const unsigned k = (s >> 13) % 10;
+    ties[i] = k < 2 ? 1 : k == 2 ? 2 : 0;
+    if (i % (64 * 7) < 64) ties[i] = 2;  // some waves all NaN
   }
   float* din;
   int* dt;
@@ -73,11 +77,24 @@ int main() {
         printf("MISMATCH %s lane %d: %08x vs %08x\n", what[k], i, r[2 * k], r[2 * k + 1]);
         return 1;
       }
+    if (i % 64 == 0) {  // the first maximum of the wave's argmax inputs, NaN never taken unless all are NaN
+      int best = -1;
+      float bv = 0.0f;
+      for (int l = 0; l < 64; ++l) {
+        const float t = ties[i + l] == 1 ? 1.0f : ties[i + l] == 2 ? NAN : h[i + l];
+        if (t == t && (best < 0 || t > bv || bv != bv)) best = l, bv = t;
+        if (best < 0 && t != t) best = l, bv = t;
+      }
+      if ((int)r[6] != best * 3) {
+        printf("MISMATCH wave_argmax.i vs the sequential scan, wave at lane %d: %d vs %d\n", i, (int)r[6], best * 3);
+        return 1;
+      }
+    }
     if (r[8] != r[10] || r[9] != r[11]) {
       printf("MISMATCH wave_sum_d lane %d\n", i);
       return 1;
     }
   }
-  printf("reduce_dpp_check ok %d lanes (sum, max, argmax with ties, double sum bit-identical)\n", n);
+  printf("reduce_dpp_check ok %d lanes (sum, max, argmax with ties and NaNs, double sum bit-identical; argmax = the sequential scan)\n", n);
   return 0;
 }
