@@ -13,7 +13,10 @@ xGMI, global-bunch GRADDIVFRM normalisation.  torch is used only for the gloo re
 barrier / max-reduce of the timings (tnet_amd maps torch's ROCm runtime before the library whenever
 torch is installed: one HIP runtime and one RCCL per process, whatever the import order).  After the
 timed region every rank checksums its parameters and the ranks compare them: replicas that differ
-(a broken exchange) end the run with a non-zero exit instead of a number.
+(a broken exchange) end the run with a non-zero exit instead of a number; before that, one extra step verifies the
+reductions themselves (rccl_check: every layer's RCCL-reduced gradient against a float64 gloo sum of the ranks'
+local gradients, tnet_amd/dpcheck.py -- a wrong reduction hands every rank the same wrong sum, which the replica
+checksum cannot see; exit 4 on a mismatch).
 
 Extra JSON fields: roofline (dominant kernel = the 2048x2048 affine-layer GEMMs, timed with hipEvents
 on the library stream over K further steps of the same workload right after the timed region: one
@@ -164,6 +167,51 @@ def prewarm(ms):
     return spent
 
 
+def reduction_checks(args, comm, trainer, dist, rank, world):
+    """rccl_check: one extra step after the measured regions whose gradient reductions are
+    compared with a float64 gloo sum of the same local gradients (tnet_amd.dpcheck), in the exchange form the run
+    uses and -- for an RCCL run at N > 1 in the default all-reduce form -- once more in the sharded form
+    (reduce-scatter + sharded apply + all-gather) on a second communicator created with TNET_DP_SHARD=1"""
+    from tnet_amd import dpcheck
+
+    def allreduce64(a):
+        if dist is not None:
+            import torch
+            dist.all_reduce(torch.from_numpy(a))
+
+    def gather(res):
+        if dist is None:
+            return [res]
+        got = [None] * world
+        dist.all_gather_object(got, res)
+        return got
+
+    shard = os.environ.get("TNET_DP_SHARD", "0") == "1"
+    modes = {("reduce-scatter+all-gather" if shard else "all-reduce"):
+             dpcheck.merge_ranks(gather(dpcheck.check_step(comm, trainer, allreduce64)))}
+    if args.comm == "rccl" and world > 1 and not shard and args.rccl_check_shard:
+        os.environ["TNET_DP_SHARD"] = "1"  # read once, at the communicator's creation
+        try:
+            uid = [Comm.unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(uid, src=0)
+            comm2 = Comm(rank, world, uid[0])
+        finally:
+            os.environ.pop("TNET_DP_SHARD", None)
+        trainer.set_comm(comm2)
+        try:
+            modes["reduce-scatter+all-gather"] = dpcheck.merge_ranks(
+                gather(dpcheck.check_step(comm2, trainer, allreduce64)))
+        finally:
+            tnet_amd.synchronize()
+            trainer.set_comm(comm)
+            comm2.__del__()
+    return {"ranks": world, "transport": args.comm if world > 1 else "rccl (one rank)",
+            "transport_ranks": comm.transport_ranks(), "librccl": mapped_runtime().get("librccl"),
+            "tolerance": dpcheck.TOLERANCE, "modes": modes,
+            "max_rel_err": max(m["max_rel_err"] for m in modes.values()),
+            "ok": all(m["ok"] for m in modes.values())}
+
+
 def main():
     # stdout carries exactly the one JSON result line: the native libraries' own prints (RCCL's version
     # banner at communicator creation, on every rank) go to stderr with everything else
@@ -200,6 +248,8 @@ def main():
                          "and settles at 1.01 ms only after ~20 ms of load (profiles/r04_warmup_trace.json), longer "
                          "than a 5-step warm-up (20 / 5 window: 966-982 k without, 994-999 k at 40 ms, 1.007-1.009 M "
                          "at 200 ms; 100 / 20: 1.020 M -- profiles/r04_prewarm_ab.json); 0: off")
+    ap.add_argument("--rccl-check-shard", type=int, default=1,
+                    help="N > 1 over RCCL: also check the sharded exchange form on a second communicator (0: off)")
     ap.add_argument("--breakdown-steps", type=int, default=20,
                     help="extra steps after the timed region with every launch event-timed (kernels field)")
     args = ap.parse_args()
@@ -293,6 +343,12 @@ def main():
         check(lib().tnet_kernel_timing(0), "kernel_timing")
         check(lib().tnet_kernel_timing_report(buf, len(buf)), "kernel_timing_report")
         breakdown = parse_kernel_report(buf.value.decode())
+    # the reduction check: one more step, after every measured region (synchronous copies)
+    rccl_check = reduction_checks(args, comm, trainer, dist, rank, world) if comm is not None else None
+    if rccl_check is not None and not rccl_check["ok"]:
+        print("bench: the reduced gradients differ from the gloo float64 sum of the local gradients: " +
+              json.dumps(rccl_check), file=sys.stderr)
+        raise SystemExit(4)
     if dist is not None:
         import torch
         t = torch.tensor([dt], dtype=torch.float64)
@@ -379,6 +435,7 @@ def main():
             "cpu_baseline": cpu,
             "replica_check": {"ranks": world, "identical": True, "param_sha256_16": replicas[0],
                               "param_sum": replicas[1]},
+            "rccl_check": rccl_check,
             "runtime": mapped_runtime(),
             "kernels": kernels,
             "kernels_note": f"every launch event-timed, {args.breakdown_steps} extra steps after the timed region "

@@ -250,6 +250,34 @@ int tnet_affine_update_bias_pair(const float* X, TnetMatrixDim dX, const float* 
 int tnet_affine_bwd_colsum_slabs(const float* E, TnetMatrixDim dE, const float* W, TnetMatrixDim dW,
                                  const float* Ybelow, int strideYbelow, float* Eo, TnetMatrixDim dEo, float* colpart,
                                  int ldcolpart, float* colpartE, int ldcolpartE, void* stream);
+/* ---- the backward GEMM from a transposed weight shadow (the same CuBiasedLinearity::BackpropagateFnc,
+ * cuBiasedLinearity.cc:21-25, E_in = E W^T, read from Wt = W^T [n_out x n_in] so that the weight operand is
+ * n-contiguous: the forward GEMM's NN layout and direct form instead of the NT one).  Eo is bit-identical to the
+ * W forms (the same MFMA operands in the same order per element); the slab sums add the same rows in another
+ * order (fp32, within the tests' slab-sum tolerance).  TNET_ERR_UNSUPPORTED while CUs are reserved for RCCL.
+ *   tnet_weight_shadow(W, dW, Wt, ldwt): register Wt [dW.cols x dW.rows] (row stride ldwt, 16-B aligned) as the
+ *     transposed shadow of W (Wt NULL: unregister).  Every update launch of W through tnet_affine_update[_bias],
+ *     tnet_affine_update_bias_pair / _gather and tnet_affine_update_bwd_pair[_t] whose form runs the 16x16 kernel's
+ *     SGD epilogue writes the updated W into Wt as well, in the same pass (16-B stores, written through);
+ *     tnet_weight_shadow_kept(W) = 1 when the last such update of W did (0: it ran a form without the shadow
+ *     store -- refresh Wt with tnet_transpose before reading it; < 0: W not registered).  W changed by any other
+ *     means leaves Wt stale: the caller tracks that.
+ *   tnet_transpose(A, dA, T, ldt): T[c][r] = A[r][c] (T [dA.cols x dA.rows], row stride ldt). */
+int tnet_affine_bwd_colsum_t(const float* E, TnetMatrixDim dE, const float* Wt, TnetMatrixDim dWt, const float* Ybelow,
+                             int strideYbelow, float* Eo, TnetMatrixDim dEo, float* colpart, int ldcolpart,
+                             void* stream);
+int tnet_affine_bwd_colsum_slabs_t(const float* E, TnetMatrixDim dE, const float* Wt, TnetMatrixDim dWt,
+                                   const float* Ybelow, int strideYbelow, float* Eo, TnetMatrixDim dEo, float* colpart,
+                                   int ldcolpart, float* colpartE, int ldcolpartE, void* stream);
+int tnet_affine_update_bwd_pair_t(const float* X, TnetMatrixDim dX, const float* E, TnetMatrixDim dE, float* W,
+                                  TnetMatrixDim dW, float* corrW, int strideCorr, float scale, float mmt, float l2,
+                                  const float* colpart, int ldcolpart, float* b, float* corr_b, const float* E2,
+                                  TnetMatrixDim dE2, const float* W2t, TnetMatrixDim dW2t, const float* Ybelow,
+                                  int strideYbelow, float* Eo, TnetMatrixDim dEo, float* colpart2, int ldcolpart2,
+                                  void* stream);
+int tnet_weight_shadow(const float* W, TnetMatrixDim dW, float* Wt, int ldwt);
+int tnet_weight_shadow_kept(const float* W);
+int tnet_transpose(const float* A, TnetMatrixDim dA, float* T, int ldt, void* stream);
 /* The step's last weight update(s) and the NEXT bunch's gather in ONE launch: tnet_affine_update_bias(X, E,
  * W, ...) -- and, when X2 is not NULL, tnet_affine_update_bias(X2, E2, W2, ...) as in
  * tnet_affine_update_bias_pair -- plus tnet_gather_bunch(y, x, labels_out, labels_in, copy_from, dy, dx)

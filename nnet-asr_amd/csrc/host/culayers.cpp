@@ -128,6 +128,30 @@ void CuBiasedLinearity::UpdateFrom(const CuMatrix<BaseFloat>& X, const CuMatrix<
   TNET_SAFE_CALL(tnet_affine_update(X.pCUData(), X.Dim(), E.pCUData(), dE, mLinearity.pCUData(), mLinearity.Dim(),
                                     mmt ? mLinearityCorrection.pCUData() : nullptr,
                                     (int)mLinearityCorrection.Stride(), scale, mMomentum, l2, S));
+  NoteUpdate();
+}
+
+void CuBiasedLinearity::UseShadow() {
+  if (!mShadowOn || mLinearityT.Rows() != mLinearity.Cols() || mLinearityT.Cols() != mLinearity.Rows()) {
+    mLinearityT.Init(mLinearity.Cols(), mLinearity.Rows());
+    mShadowValid = false;
+  }
+  // (re-)registered every time: W's storage is the same unless it was re-initialised with other dimensions
+  TNET_SAFE_CALL(tnet_weight_shadow(mLinearity.pCUData(), mLinearity.Dim(), mLinearityT.pCUData(),
+                                    (int)mLinearityT.Stride()));
+  mShadowOn = true;
+}
+
+const CuMatrix<BaseFloat>& CuBiasedLinearity::ShadowForBwd() {
+  if (!mShadowOn) Error("CuBiasedLinearity::ShadowForBwd: no shadow (UseShadow)");
+  if (!mShadowValid) {
+    KTScope kt("transpose:" + std::to_string(GetNInputs()) + "x" + std::to_string(GetNOutputs()),
+               8.0 * GetNInputs() * GetNOutputs());
+    TNET_SAFE_CALL(tnet_transpose(mLinearity.pCUData(), mLinearity.Dim(), mLinearityT.pCUData(),
+                                  (int)mLinearityT.Stride(), S));
+    mShadowValid = true;
+  }
+  return mLinearityT;
 }
 
 void CuBiasedLinearity::BackpropUpdateRow(const CuMatrix<BaseFloat>& X, const CuMatrix<BaseFloat>& E,
@@ -144,6 +168,7 @@ void CuBiasedLinearity::BackpropUpdateRow(const CuMatrix<BaseFloat>& X, const Cu
                                             (int)mLinearityCorrection.Stride(), mBias.pCUData(),
                                             mmt ? mBiasCorrection.pCUData() : nullptr, scale, mMomentum, l2,
                                             Eout.pCUData(), s, d, S));
+  mShadowValid = false;
 }
 
 void CuBiasedLinearity::UpdateFromColsum(const CuMatrix<BaseFloat>& X, const CuMatrix<BaseFloat>& E,
@@ -159,6 +184,7 @@ void CuBiasedLinearity::UpdateFromColsum(const CuMatrix<BaseFloat>& X, const CuM
                                          (int)mLinearityCorrection.Stride(), scale, mMomentum, l2, colpart.pCUData(),
                                          (int)colpart.Stride(), mBias.pCUData(),
                                          mmt ? mBiasCorrection.pCUData() : nullptr, S));
+  NoteUpdate();
 }
 
 bool CuBiasedLinearity::UpdateFromColsumWithBwd(const CuMatrix<BaseFloat>& X, const CuMatrix<BaseFloat>& E,
@@ -174,17 +200,22 @@ bool CuBiasedLinearity::UpdateFromColsumWithBwd(const CuMatrix<BaseFloat>& X, co
   KTScope kt("gemm_upd+bwd:" + (su == sb ? su : su + "+" + sb),
              2.0 * X.Rows() * GetNInputs() * GetNOutputs() + 2.0 * E2.Rows() * below.GetNInputs() * below.GetNOutputs(),
              2);
-  const int st = tnet_affine_update_bwd_pair(
+  // the lower layer's backward from its transposed shadow when it keeps one (NN, the forward's layout)
+  const CuMatrix<BaseFloat>* wt = below.HasShadow() ? &const_cast<CuBiasedLinearity&>(below).ShadowForBwd() : nullptr;
+  auto pair = wt ? tnet_affine_update_bwd_pair_t : tnet_affine_update_bwd_pair;
+  const CuMatrix<BaseFloat>& wb = wt ? *wt : below.LinearityRO();
+  const int st = pair(
       X.pCUData(), X.Dim(), E.pCUData(), E.Dim(), mLinearity.pCUData(), mLinearity.Dim(),
       mmt ? mLinearityCorrection.pCUData() : nullptr, (int)mLinearityCorrection.Stride(), scale, mMomentum, l2,
       colpart.pCUData(), (int)colpart.Stride(), mBias.pCUData(), mmt ? mBiasCorrection.pCUData() : nullptr,
-      E2.pCUData(), E2.Dim(), below.Linearity().pCUData(), below.Linearity().Dim(), Ybelow.pCUData(),
+      E2.pCUData(), E2.Dim(), wb.pCUData(), wb.Dim(), Ybelow.pCUData(),
       (int)Ybelow.Stride(), Eo.pCUData(), Eo.Dim(), colpart2.pCUData(), (int)colpart2.Stride(), S);
   if (st == TNET_ERR_UNSUPPORTED) {
     kt.Cancel();
     return false;
   }
   TNET_SAFE_CALL(st);
+  NoteUpdate();
   return true;
 }
 
@@ -215,6 +246,8 @@ bool CuBiasedLinearity::UpdatePairFromColsum(const CuMatrix<BaseFloat>& X, const
     return false;
   }
   TNET_SAFE_CALL(st);
+  NoteUpdate();
+  other.NoteUpdate();
   return true;
 }
 
@@ -252,6 +285,8 @@ bool CuBiasedLinearity::UpdateFromColsumGather(const CuMatrix<BaseFloat>& X, con
     return false;
   }
   TNET_SAFE_CALL(st);
+  NoteUpdate();
+  if (other) other->NoteUpdate();
   return true;
 }
 
@@ -360,6 +395,7 @@ void CuBiasedLinearity::ApplyGradient(size_t frames, void* stream, const GradExc
   float scale, l2;
   UpdateConstants(frames, &scale, &l2);
   const bool mmt = mMomentum != 0.0f;
+  mShadowValid = false;  // the flat apply writes no transposed shadow
   // padding columns of W and of the gradient are zero, so the flat update keeps them zero; W and b
   // in one launch, each as the element ranges this rank applies (sharded apply: its shard + the tail)
   TnetSgdSeg seg[4];
@@ -400,6 +436,7 @@ void CuBiasedLinearity::ReadFromStream(std::istream& rIn) {
   }
   mLinearity.CopyFrom(BfMatrix(transpose, TRANS));
   mBias.CopyFrom(bias);
+  mShadowValid = false;
 }
 
 void CuBiasedLinearity::WriteToStream(std::ostream& rOut) {

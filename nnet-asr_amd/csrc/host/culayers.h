@@ -14,7 +14,10 @@ class CuBiasedLinearity : public CuUpdatableComponent {
       : CuUpdatableComponent(nInputs, nOutputs, pPred),
         mLinearity(nInputs, nOutputs), mBias(nOutputs),
         mLinearityCorrection(nInputs, nOutputs), mBiasCorrection(nOutputs) {}
-  ~CuBiasedLinearity() {}
+  ~CuBiasedLinearity() {
+    // the shadow's registration is keyed by W's address: gone before that storage can serve another matrix
+    if (mShadowOn) (void)tnet_weight_shadow(mLinearity.pCUData(), mLinearity.Dim(), nullptr, 0);
+  }
 
   ComponentType GetType() const override { return BIASED_LINEARITY; }
   const char* GetName() const override { return "<biasedlinearity>"; }
@@ -42,9 +45,21 @@ class CuBiasedLinearity : public CuUpdatableComponent {
   void ReadFromStream(std::istream& rIn) override;
   void WriteToStream(std::ostream& rOut) override;
 
-  // ---- access for the fused network-level kernels and the C ABI
-  CuMatrix<BaseFloat>& Linearity() { return mLinearity; }
+  // ---- access for the fused network-level kernels and the C ABI (the mutable accessor marks the transposed
+  // shadow stale: the caller may change W through it)
+  CuMatrix<BaseFloat>& Linearity() {
+    mShadowValid = false;
+    return mLinearity;
+  }
   const CuMatrix<BaseFloat>& Linearity() const { return mLinearity; }
+  const CuMatrix<BaseFloat>& LinearityRO() const { return mLinearity; }
+  /// The transposed shadow Wt = W^T [nOut x nIn] the backward GEMM reads n-contiguous
+  /// (tnet_affine_bwd_colsum_t): UseShadow registers it (tnet_weight_shadow), so that every fused update launch
+  /// of W that supports it also writes Wt; ShadowForBwd refreshes it first when an update did not (or W changed
+  /// by other means since) and returns it.
+  void UseShadow();
+  const CuMatrix<BaseFloat>& ShadowForBwd();
+  bool HasShadow() const { return mShadowOn; }
   CuVector<BaseFloat>& Bias() { return mBias; }
   CuMatrix<BaseFloat>& LinearityCorrection() { return mLinearityCorrection; }
   CuVector<BaseFloat>& BiasCorrection() { return mBiasCorrection; }
@@ -87,6 +102,10 @@ class CuBiasedLinearity : public CuUpdatableComponent {
   CuVector<BaseFloat> mBiasCorrection;       ///< momentum buffer
   CuMatrix<BaseFloat> mGradW;                ///< data-parallel gradient buffers (lazy)
   CuVector<BaseFloat> mGradB;
+  CuMatrix<BaseFloat> mLinearityT;           ///< transposed shadow of mLinearity [nOut x nIn] (UseShadow)
+  bool mShadowOn = false, mShadowValid = false;
+  /// after an update launch of W: the shadow is current iff that launch wrote it (tnet_weight_shadow_kept)
+  void NoteUpdate() { mShadowValid = mShadowOn && tnet_weight_shadow_kept(mLinearity.pCUData()) == 1; }
 };
 
 class CuSigmoid : public CuComponent {

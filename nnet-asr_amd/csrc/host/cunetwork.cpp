@@ -267,6 +267,15 @@ void CuNetwork::TrainBunch(const CuMatrix<BaseFloat>& X, const CuVector<int>& la
     }
   }
   mNetComponents.front()->SetInput(X);
+  // the backward GEMMs read each weight's transposed shadow (NN: the forward's layout and direct form), which the
+  // fused updates keep current in the same pass (CuBiasedLinearity::UseShadow; not in the data-parallel step, whose
+  // flat SGD apply writes no shadow; TNET_BWD_SHADOW=0: the NT backward from W everywhere, 2: the hidden layers only,
+  // not the top layer)
+  static const int use_shadow = getenv("TNET_BWD_SHADOW") ? atoi(getenv("TNET_BWD_SHADOW")) : 1;
+  const bool shadows = use_shadow > 0 && train && !exchange;
+  if (shadows)
+    for (int l = 1; l < (use_shadow == 2 ? nl - 1 : nl); l++)
+      static_cast<CuBiasedLinearity*>(mNetComponents[2 * l])->UseShadow();
 
   // objective outputs: the error (+ the softmax output when kept)
   CuComponent* smx = mNetComponents.back();
@@ -307,8 +316,8 @@ void CuNetwork::TrainBunch(const CuMatrix<BaseFloat>& X, const CuVector<int>& la
         ldcp = (int)mColPart[l]->Stride();
       }
       KTScope kt("gemm_fwd+softmax:" + shape, 2.0 * rows * lin->GetNInputs() * lin->GetNOutputs());
-      const int st = tnet_affine_softmax_xent(act->pCUData(), act->Dim(), lin->Linearity().pCUData(),
-                                              lin->Linearity().Dim(), lin->Bias().pCUData(), labels.pCUData(),
+      const int st = tnet_affine_softmax_xent(act->pCUData(), act->Dim(), lin->LinearityRO().pCUData(),
+                                              lin->LinearityRO().Dim(), lin->Bias().pCUData(), labels.pCUData(),
                                               dst.pCUData(), (int)dst.Stride(), yout, ystride, mGlobErr.pCUData(),
                                               (int)mGlobErr.Stride(), obj.DeviceStats(), cp, ldcp, S);
       if (st != TNET_ERR_UNSUPPORTED) {
@@ -320,7 +329,7 @@ void CuNetwork::TrainBunch(const CuMatrix<BaseFloat>& X, const CuVector<int>& la
       }
     }
     KTScope kt("gemm_fwd:" + shape, 2.0 * rows * lin->GetNInputs() * lin->GetNOutputs());
-    TNET_SAFE_CALL(tnet_affine_fwd(act->pCUData(), act->Dim(), lin->Linearity().pCUData(), lin->Linearity().Dim(),
+    TNET_SAFE_CALL(tnet_affine_fwd(act->pCUData(), act->Dim(), lin->LinearityRO().pCUData(), lin->LinearityRO().Dim(),
                                    lin->Bias().pCUData(), dst.pCUData(), dst.Dim(), last ? 0 : 1, S));
     act = &dst;
     acts[l + 1] = &dst;
@@ -454,15 +463,22 @@ void CuNetwork::TrainBunch(const CuMatrix<BaseFloat>& X, const CuVector<int>& la
           if (top_slabs_ride) {  // l == nl - 1: err is the softmax error
             top_slabs_ride = false;
             CuMatrix<BaseFloat>& ct = *mColPart[nl - 1];
-            st = tnet_affine_bwd_colsum_slabs(err->pCUData(), err->Dim(), lin->Linearity().pCUData(),
-                                              lin->Linearity().Dim(), acts[l]->pCUData(), (int)acts[l]->Stride(),
-                                              eo->pCUData(), eo->Dim(), cp.pCUData(), (int)cp.Stride(),
-                                              ct.pCUData(), (int)ct.Stride(), S);
+            const bool t = shadows && lin->HasShadow();
+            const CuMatrix<BaseFloat>& wb = t ? lin->ShadowForBwd() : lin->LinearityRO();
+            st = (t ? tnet_affine_bwd_colsum_slabs_t : tnet_affine_bwd_colsum_slabs)(
+                err->pCUData(), err->Dim(), wb.pCUData(), wb.Dim(), acts[l]->pCUData(), (int)acts[l]->Stride(),
+                eo->pCUData(), eo->Dim(), cp.pCUData(), (int)cp.Stride(), ct.pCUData(), (int)ct.Stride(), S);
             if (st == TNET_ERR_UNSUPPORTED) err_colsum = top_slabs_launch();
           }
+          if (st == TNET_ERR_UNSUPPORTED && shadows && lin->HasShadow()) {
+            const CuMatrix<BaseFloat>& wt = lin->ShadowForBwd();
+            st = tnet_affine_bwd_colsum_t(err->pCUData(), err->Dim(), wt.pCUData(), wt.Dim(), acts[l]->pCUData(),
+                                          (int)acts[l]->Stride(), eo->pCUData(), eo->Dim(), cp.pCUData(),
+                                          (int)cp.Stride(), S);
+          }
           if (st == TNET_ERR_UNSUPPORTED)
-            st = tnet_affine_bwd_colsum(err->pCUData(), err->Dim(), lin->Linearity().pCUData(),
-                                        lin->Linearity().Dim(), acts[l]->pCUData(), (int)acts[l]->Stride(),
+            st = tnet_affine_bwd_colsum(err->pCUData(), err->Dim(), lin->LinearityRO().pCUData(),
+                                        lin->LinearityRO().Dim(), acts[l]->pCUData(), (int)acts[l]->Stride(),
                                         eo->pCUData(), eo->Dim(), cp.pCUData(), (int)cp.Stride(), S);
           if (st != TNET_ERR_UNSUPPORTED) {
             TNET_SAFE_CALL(st);
@@ -474,8 +490,8 @@ void CuNetwork::TrainBunch(const CuMatrix<BaseFloat>& X, const CuVector<int>& la
         flush_grad();
         flush();
         KTScope kt("gemm_bwd:" + shape, 2.0 * rows * lin->GetNInputs() * lin->GetNOutputs());
-        TNET_SAFE_CALL(tnet_affine_bwd(err->pCUData(), err->Dim(), lin->Linearity().pCUData(),
-                                       lin->Linearity().Dim(), acts[l]->pCUData(), (int)acts[l]->Stride(),
+        TNET_SAFE_CALL(tnet_affine_bwd(err->pCUData(), err->Dim(), lin->LinearityRO().pCUData(),
+                                       lin->LinearityRO().Dim(), acts[l]->pCUData(), (int)acts[l]->Stride(),
                                        eo->pCUData(), eo->Dim(), 1, S));
       }
     }

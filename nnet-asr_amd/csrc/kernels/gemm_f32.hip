@@ -31,6 +31,7 @@
 #include <initializer_list>
 #include <map>
 #include <mutex>
+#include <unordered_map>
 #include <type_traits>
 
 #include "kcommon.h"
@@ -98,6 +99,9 @@ struct GemmP {
   // (1 or 2); the first of a split tile's pieces to finish stores its accumulators to skws + tile * BM * BN
   // (fragment order), the second adds them to its own and runs the tile's epilogue (tile_cnt[tile])
   float* skws;
+  // EPI_SGD / EPI_SGD_B (gemm16_body only): the updated W also stored transposed, Ct[col][row] (row stride ldct):
+  // the weight's shadow that the next step's backward GEMM reads n-contiguous (tnet_weight_shadow)
+  float* Ct; long ldct;
 };
 
 
@@ -1660,7 +1664,7 @@ __device__ __forceinline__ void gemm16_body(const GemmP& p_in, float* __restrict
   const __amdgpu_buffer_rsrc_t rs_c = tile_rsrc(p.C + (long)bm * p.ldc + bn);
   const __amdgpu_buffer_rsrc_t rs_q = tile_rsrc(p.corr ? p.corr + (long)bm * p.ldcorr + bn : p.C);
   constexpr bool CS = EPI == EPI_DSIG_CS;
-  static_assert(!CS || (A_KC && B_KC && WTM == kColsumSlabRows), "column sums: bwd layout, 32-row wave tiles");
+  static_assert(!CS || (A_KC && WTM == kColsumSlabRows), "column sums: k-contiguous A, 32-row wave tiles");
   if constexpr (TRE) {
     // ---- transposed epilogue (see TRE)
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's last fragment reads retired
@@ -1760,7 +1764,9 @@ __device__ __forceinline__ void gemm16_body(const GemmP& p_in, float* __restrict
             const float y = pre_a[a][r][j][e];
             o[e] = y * (1.f - y) * v[e];
           }
-          if constexpr (CS) csum[j] += o[0];
+          if constexpr (CS)
+#pragma unroll
+            for (int e = 0; e < NE; ++e) csum[NE * j + e] += o[e];
         } else if constexpr (EB == EPI_RBM) {
           // c = mmt*corr + scale*acc + l2*W ; corr = c ; W += c   (cuRbm.cc:133-174)
 #pragma unroll
@@ -1780,6 +1786,9 @@ __device__ __forceinline__ void gemm16_body(const GemmP& p_in, float* __restrict
             w = w + p.l2 * w;
             o[e] = w;
           }
+          if (p.Ct)  // the updated values stay in the accumulators for the transposed stores below
+#pragma unroll
+            for (int e = 0; e < NE; ++e) acc[a][NE * j + e][r] = o[e];
         }
         float* cp = p.C + (long)row * p.ldc + col;
         float* qp = has_q ? p.corr + (long)row * p.ldcorr + col : nullptr;
@@ -1807,17 +1816,74 @@ __device__ __forceinline__ void gemm16_body(const GemmP& p_in, float* __restrict
     }
   }
   if constexpr (CS) {
+    // lane (lg, li) summed its rows of each column it holds; the four lane groups of a column meet by two xor
+    // shuffles (NE consecutive columns per lane where B is n-contiguous: the backward from the transposed weight)
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
       csum[j] += __shfl_xor(csum[j], 16, 64);
       csum[j] += __shfl_xor(csum[j], 32, 64);
     }
-    const int slab_row = bm + wm0, col0 = bn + wn0 + li;
+    const int slab_row = bm + wm0;
     if (lg == 0 && slab_row < M) {
       float* cp = p.cpart + (long)(slab_row / kColsumSlabRows) * p.ldcpart;
 #pragma unroll
-      for (int j = 0; j < TN; ++j)
-        if (col0 + 16 * j < N) cp[col0 + 16 * j] = csum[j];
+      for (int j = 0; j < NJ; ++j) {
+        const int col = ecol(j);
+        if (NE == 4 && col + 3 < N) {
+          *reinterpret_cast<f32x4*>(cp + col) = f32x4{csum[4 * j], csum[4 * j + 1], csum[4 * j + 2], csum[4 * j + 3]};
+        } else {
+#pragma unroll
+          for (int e = 0; e < NE; ++e)
+            if (col + e < N) cp[col + e] = csum[NE * j + e];
+        }
+      }
+    }
+  }
+  if constexpr (EB == EPI_SGD) {
+    // the transposed shadow Ct[col][row] of the updated W (tnet_weight_shadow), staged through LDS so that the
+    // global stores are whole lines: each lane holds its rows of a column as VM-row vectors (erow), which go into
+    // an LDS image of the tile's columns [BN][BM + 4]; then every thread writes 16-B pieces of the image's rows,
+    // consecutive threads consecutive pieces of one Ct row (BM floats), written through (sc1) like W
+    if (p.Ct) {
+      constexpr int LDP = BM + 4, Q = BM / 4;
+      static_assert(BN * LDP <= S * ST_SZ, "shadow image fits the ring");
+      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's LDS reads retired
+      __syncthreads();
+      float* ts = smem;
+#pragma unroll
+      for (int aq = 0; aq < TM / VM; ++aq)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int rl0 = erow(VM * aq, r) - bm;
+#pragma unroll
+          for (int j = 0; j < NJ; ++j)
+#pragma unroll
+            for (int e = 0; e < NE; ++e) {
+              const int cl = ecol(j) + e - bn;
+              if constexpr (VM == 4) {
+                *reinterpret_cast<f32x4*>(ts + cl * LDP + rl0) =
+                    f32x4{acc[4 * aq][NE * j + e][r], acc[4 * aq + 1][NE * j + e][r], acc[4 * aq + 2][NE * j + e][r],
+                          acc[4 * aq + 3][NE * j + e][r]};
+              } else {
+#pragma unroll
+                for (int m = 0; m < VM; ++m) ts[cl * LDP + rl0 + m] = acc[VM * aq + m][NE * j + e][r];
+              }
+            }
+        }
+      __syncthreads();
+      const __amdgpu_buffer_rsrc_t rs_t = tile_rsrc(p.Ct + (long)bn * p.ldct + bm);
+      for (int u = threadIdx.x; u < BN * Q; u += NT) {
+        const int cl = u / Q, q4 = u % Q, col = bn + cl, row0 = bm + 4 * q4;
+        if (col >= N || row0 >= M) continue;
+        const f32x4 v = *reinterpret_cast<const f32x4*>(ts + cl * LDP + 4 * q4);
+        if (row0 + 3 < M) {
+          st_wt(rs_t, (long)cl * p.ldct + 4 * q4, v);
+        } else {
+#pragma unroll
+          for (int m = 0; m < 4; ++m)
+            if (row0 + m < M) p.Ct[(long)col * p.ldct + row0 + m] = v[m];
+        }
+      }
     }
   }
   }
@@ -2046,14 +2112,15 @@ void gemm16_upd_mixed_gather_kernel(const GemmP pa, const GemmP pb, const int na
 // na tiles) and the slab sums of its OWN input error E (the softmax error: the top layer's bias gradient,
 // colsum_partial blocks after the tiles).  Independent (the GEMM reads E, the blocks read E); the blocks
 // take the CUs as the tiles finish instead of a launch of their own before the GEMM.
-template <bool PX, int SP = 0>
+// BKC false: the GEMM from the weight's transposed shadow (NN, tnet_affine_bwd_colsum_slabs_t)
+template <bool PX, int SP = 0, bool BKC = true>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
 void gemm16_bwd_slabs_kernel(const GemmP p, const int na, const float* __restrict__ Et, const TnetMatrixDim dEt,
                              float* __restrict__ cpt, const long ldcpt, const int slabs, const int ncb) {
   __shared__ __attribute__((aligned(16))) float smem[gemm16_smem_floats<64, 128, 64, 2, EPI_DSIG_CS, PX>()];
   const int b = blockIdx.x;
   if (b < na) {
-    gemm16_body<64, 128, 64, 2, 2, 2, SP, true, true, EPI_DSIG_CS, PX>(p, smem, b);
+    gemm16_body<64, 128, 64, 2, 2, 2, SP, true, BKC, EPI_DSIG_CS, PX>(p, smem, b);
   } else {
     const int c = b - na;
     colsum_partial_block<true>(Et, dEt, cpt, slabs, 0x7fffffff, ldcpt, c % ncb, c / ncb, smem);
@@ -2357,6 +2424,49 @@ static int g_direct = -1;
 // (profiles/r04_gemm_kc_ab.json)
 static int g_kc = -1;
 static int g_wt = 1;  // TNET_GEMM_WT=0: plain 16-B epilogue stores instead of write-through (sc1; measured +1.4 % frames/s)
+// Transposed weight shadows (tnet_weight_shadow): W -> Wt registered by the host; an update launch of W attaches
+// Wt as GemmP::Ct (shadow_attach) and the launch paths whose kernel does not run gemm16_body's SGD epilogue (the
+// 32x32 kernel, the split-K combine, split2) drop it (shadow_drop); the entry point then records whether this
+// update of W kept its shadow (shadow_done), which tnet_weight_shadow_kept reports
+// the narrow top layer's row-block kernel (top_rows.hip): the shapes it takes, unless a configuration or split-K
+// count is forced (tests of the general GEMM's forms)
+extern "C" int tnetk_top_rows_ok(const float* X, long ldx, int M, int N, int K);
+extern "C" int tnetk_top_rows(const float* X, long ldx, const float* W, long ldw, const float* b, int M, int N, int K,
+                              const int* labels, float* Z, long ldz, float* Y, long ldy, float* E, long lde,
+                              double* stats, float* cpart, long ldcp, int v4, int logits_only, void* stream);
+static int forced_cfg();
+static bool top_rows_ok(const GemmP& p) {
+  return forced_cfg() < 0 && g_split <= 0 && tnetk_top_rows_ok(p.A, p.lda, p.M, p.N, p.K);
+}
+struct WeightShadow {
+  float* t;
+  long ld;
+  int rows, cols;
+  int kept;
+};
+static std::mutex g_shadow_mu;
+static std::unordered_map<const float*, WeightShadow> g_shadow;
+static thread_local int g_shadow_dropped = 0;
+static void shadow_attach(GemmP& p) {
+  p.Ct = nullptr;
+  p.ldct = 0;
+  g_shadow_dropped = 0;
+  std::lock_guard<std::mutex> g(g_shadow_mu);
+  auto it = g_shadow.find(p.C);
+  if (it != g_shadow.end() && it->second.rows == p.M && it->second.cols == p.N) {
+    p.Ct = it->second.t;
+    p.ldct = it->second.ld;
+  }
+}
+static void shadow_drop(const GemmP& p) {
+  if (p.Ct) g_shadow_dropped = 1;
+}
+static int shadow_done(const GemmP& p, int st) {
+  std::lock_guard<std::mutex> g(g_shadow_mu);
+  auto it = g_shadow.find(p.C);
+  if (it != g_shadow.end()) it->second.kept = (st == TNET_OK && p.Ct && !g_shadow_dropped) ? 1 : 0;
+  return st;
+}
 static int forced_cfg() {
   if (g_cfg == -2) {
     g_cfg = -1;
@@ -2404,6 +2514,7 @@ template <int KIND, int BM, int BN, int BK, int WM, int WN, int S, int IL, bool 
 static bool launch_cfg(const GemmP& p, hipStream_t st) {
   const unsigned tiles = (unsigned)((long)cdiv(p.M, BM) * cdiv(p.N, BN));
   if constexpr (KIND == 0) {
+    shadow_drop(p);  // the 32x32 kernel's epilogue writes no transposed shadow
     gemm_f32_glds_kernel<BM, BN, BK, WM, WN, S, IL, A_KC, B_KC, EPI><<<tiles, WM * WN * 64, 0, st>>>(p);
     return true;
   } else {
@@ -2422,7 +2533,7 @@ static bool launch_cfg(const GemmP& p, hipStream_t st) {
     // and update (128x128 TN + SGD / the data-parallel gradient)
     constexpr bool PXK = (IL == 0 || IL >= 3) && BK == 64 && S == 2 &&
                          ((BM == 64 && BN == 128 && A_KC && !B_KC && EPI == EPI_BIAS_SIG) ||
-                          (BM == 64 && BN == 128 && A_KC && B_KC && EPI == EPI_DSIG_CS) ||
+                          (BM == 64 && BN == 128 && A_KC && EPI == EPI_DSIG_CS) ||
                           (BM == 128 && BN == 128 && !A_KC && !B_KC &&
                            (EPI == EPI_SGD_B || EPI == EPI_SGD || EPI == EPI_STORE_BG)));
     const bool exact = px_exact<BM, BN, EPI>(p);
@@ -2548,6 +2659,7 @@ static bool launch_split2(const GemmP& p, hipStream_t st) {
     q.wt = g_wt;
     q.skws = ws;
     q.tile_cnt = cnt;
+    shadow_drop(p);
     gemm16_split2_kernel<64, 128, A_KC, B_KC, EPI, false><<<(unsigned)(2 * T), 256, 0, st>>>(q);
     return true;
   }
@@ -2612,6 +2724,7 @@ static int launch_partials(const GemmP& p, int cfg, int ks, hipStream_t st, Part
 
 template <bool A_KC, bool B_KC, int EPI>
 static int launch_splitk(const GemmP& p, int cfg, int ks, hipStream_t st) {
+  shadow_drop(p);  // the combine writes no transposed shadow
   Partials pt;
   // in-launch combine where a tile's slices are a few tens of KB (cdna_hip_programming.md section 5)
   int bm, bn, kind;
@@ -2655,6 +2768,27 @@ static int launch_colsum_bwd(const GemmP& p_in, hipStream_t st) {
   else if (cfg == CFG_m64x128k64s2) ok = launch_cfg<1, 64, 128, 64, 2, 2, 2, 0, true, true, EPI_DSIG_CS>(p, st);
   else if (cfg == CFG_m64x64k64s2) ok = launch_cfg<1, 64, 64, 64, 2, 2, 2, 0, true, true, EPI_DSIG_CS>(p, st);
   else ok = launch_cfg<1, 64, 64, 32, 2, 2, 4, 0, true, true, EPI_DSIG_CS>(p, st);
+  if (!ok) return TNET_ERR_UNSUPPORTED;
+  TNET_LAUNCH_CHECK();
+  return TNET_OK;
+}
+
+// The same backward from the weight's transposed shadow Wt (B n-contiguous, the forward's NN layout): the 64x128
+// grid in the forward's direct form (m64x128a8) where it gives ~one workgroup per CU, else 64x64 tiles (32-row
+// wave tiles = slabs either way).  Per output element the MFMA operands and their order are the NT kernel's
+// (the lane -> k map is layout-independent): Eo is bit-identical to launch_colsum_bwd's; the slab sums add the
+// same rows in another order.  Not while CUs are reserved for RCCL (the caller takes the NT stream-K form).
+static int launch_colsum_bwd_t(const GemmP& p_in, hipStream_t st) {
+  if (p_in.M <= 0 || p_in.N <= 0) return TNET_OK;
+  if (g_reserve > 0 || forced_cfg() >= 0) return TNET_ERR_UNSUPPORTED;
+  GemmP p = p_in;
+  p.group = g_group > 0 ? g_group : 8;
+  bool ok;
+  if ((long)cdiv(p.M, 64) * cdiv(p.N, 128) >= 200)
+    ok = g_direct > 0 ? launch_cfg<1, 64, 128, 64, 2, 2, 2, 6, true, false, EPI_DSIG_CS>(p, st)
+                      : launch_cfg<1, 64, 128, 64, 2, 2, 2, 0, true, false, EPI_DSIG_CS>(p, st);
+  else
+    ok = launch_cfg<1, 64, 64, 32, 2, 2, 4, 0, true, false, EPI_DSIG_CS>(p, st);
   if (!ok) return TNET_ERR_UNSUPPORTED;
   TNET_LAUNCH_CHECK();
   return TNET_OK;
@@ -2714,7 +2848,8 @@ static GemmPlan plan_gemm(const GemmP& p, bool splittable) {
 template <bool A_KC, bool B_KC, int EPI>
 static int launch_gemm(const GemmP& p_in, hipStream_t st) {
   if constexpr (EPI == EPI_DSIG_CS) {
-    return launch_colsum_bwd(p_in, st);
+    if constexpr (B_KC) return launch_colsum_bwd(p_in, st);
+    else return launch_colsum_bwd_t(p_in, st);
   } else {
   if (p_in.M <= 0 || p_in.N <= 0) return TNET_OK;
   static const int noload = getenv("TNET_GEMM_DIAG") ? atoi(getenv("TNET_GEMM_DIAG")) : 0;
@@ -2761,8 +2896,15 @@ static int launch_gemm(const GemmP& p_in, hipStream_t st) {
 // gemm16_pair_kernel launch; TNET_ERR_UNSUPPORTED where either would run another configuration (the
 // caller then makes the two calls)
 template <int EPIA, bool PXA, int SPA>
-static void pair_go(const GemmP& pu, const GemmP& pb, int na, int nb, bool kc, hipStream_t st) {
-  if (kc)
+static void pair_go(const GemmP& pu, const GemmP& pb, int na, int nb, bool kc, int bt, hipStream_t st) {
+  // bt: the backward half reads the weight's transposed shadow (NN; 1: the direct form m64x128a8, 2: the ring)
+  if (bt == 1)
+    gemm16_pair_kernel<128, 128, false, false, EPIA, PXA, 64, 128, true, false, EPI_DSIG_CS, true, SPA, 6>
+        <<<na + nb, 256, 0, st>>>(pu, pb, na);
+  else if (bt == 2)
+    gemm16_pair_kernel<128, 128, false, false, EPIA, PXA, 64, 128, true, false, EPI_DSIG_CS, true, SPA, 0>
+        <<<na + nb, 256, 0, st>>>(pu, pb, na);
+  else if (kc)
     gemm16_pair_kernel<128, 128, false, false, EPIA, PXA, 64, 128, true, true, EPI_DSIG_CS, true, SPA, 8>
         <<<na + nb, 256, 0, st>>>(pu, pb, na);
   else
@@ -2771,7 +2913,7 @@ static void pair_go(const GemmP& pu, const GemmP& pb, int na, int nb, bool kc, h
 }
 
 template <int EPIA>
-static int launch_pair_a_bwd(GemmP pu, GemmP pb, hipStream_t st) {
+static int launch_pair_a_bwd(GemmP pu, GemmP pb, hipStream_t st, bool bwd_t = false) {
   // EPI_STORE_BG (the data-parallel gradient): not while CUs are reserved for RCCL (the exchange window runs the
   // stream-K forms; a 512-workgroup pair would lose a second round on the held CUs)
   if (EPIA == EPI_STORE_BG && g_reserve > 0) return TNET_ERR_UNSUPPORTED;
@@ -2785,7 +2927,7 @@ static int launch_pair_a_bwd(GemmP pu, GemmP pb, hipStream_t st) {
   pu.wt = pb.wt = g_wt;
   // the 16x16 kernel's 32-bit tile offsets (launch_cfg's check)
   const long extA_u = 64L * pu.lda + pu.M, extB_u = 64L * pu.ldb + pu.N;
-  const long extA_b = (long)pb.M * pb.lda, extB_b = (long)pb.N * pb.ldb;
+  const long extA_b = (long)pb.M * pb.lda, extB_b = bwd_t ? 64L * pb.ldb + pb.N : (long)pb.N * pb.ldb;
   if (4 * extA_u >= (1L << 32) || 4 * extB_u >= (1L << 32) || 4 * extA_b >= (1L << 32) || 4 * extB_b >= (1L << 32))
     return TNET_ERR_UNSUPPORTED;
   if (!px_exact<64, 128, EPI_DSIG_CS>(pb)) return TNET_ERR_UNSUPPORTED;
@@ -2796,12 +2938,20 @@ static int launch_pair_a_bwd(GemmP pu, GemmP pb, hipStream_t st) {
                    pu.M % 4 == 0 && pu.N % 4 == 0 &&
                    4 * ((long)pu.K * pu.lda) < (1L << 31) && 4 * ((long)pu.K * pu.ldb) < (1L << 31);
   const bool px = px_exact<128, 128, EPIA>(pu);
-  const bool kc = g_kc >= 2 && kc_direct(pb);  // the backward half in the coalesced k-contiguous direct form
-  if (dir && px && g_direct == 2) pair_go<EPIA, true, 3>(pu, pb, na, nb, kc, st);
-  else if (dir && px) pair_go<EPIA, true, 5>(pu, pb, na, nb, kc, st);
-  else if (dir) pair_go<EPIA, false, 5>(pu, pb, na, nb, kc, st);
-  else if (px) pair_go<EPIA, true, 0>(pu, pb, na, nb, kc, st);
-  else pair_go<EPIA, false, 0>(pu, pb, na, nb, kc, st);
+  const bool kc = !bwd_t && g_kc >= 2 && kc_direct(pb);  // the backward half in the coalesced k-contiguous direct form
+  int bt = 0;
+  if (bwd_t) {
+    // the NN backward half (from the transposed shadow) in the direct form where launch_cfg would run it so
+    const bool dir_b = g_direct > 0 && pb.K / 64 >= 1 && (pb.K / 64) % 2 == 0 && pb.N % 4 == 0 && !(pb.lda & 3) &&
+                       !(pb.ldb & 3) && a16p(pb.A) && a16p(pb.B) && 4 * ((long)pb.M * pb.lda) < (1L << 31) &&
+                       4 * ((long)pb.K * pb.ldb) < (1L << 31);
+    bt = dir_b ? 1 : 2;
+  }
+  if (dir && px && g_direct == 2) pair_go<EPIA, true, 3>(pu, pb, na, nb, kc, bt, st);
+  else if (dir && px) pair_go<EPIA, true, 5>(pu, pb, na, nb, kc, bt, st);
+  else if (dir) pair_go<EPIA, false, 5>(pu, pb, na, nb, kc, bt, st);
+  else if (px) pair_go<EPIA, true, 0>(pu, pb, na, nb, kc, bt, st);
+  else pair_go<EPIA, false, 0>(pu, pb, na, nb, kc, bt, st);
   TNET_LAUNCH_CHECK();
   return TNET_OK;
 }
@@ -2890,6 +3040,10 @@ extern "C" int tnet_affine_fwd(const float* X, TnetMatrixDim dX, const float* W,
   p.bias = b;
   int st = check_common(p);
   if (st) return st;
+  // a narrow top layer (the logits of tnet_affine_softmax_xent's row-block kernel, so both give the same Z)
+  if (act == 0 && top_rows_ok(p))
+    return tnetk_top_rows(X, dX.stride, W, dW.stride, b, p.M, p.N, p.K, nullptr, Y, dY.stride, nullptr, 0, nullptr, 0,
+                          nullptr, nullptr, 0, 0, 1, stream);
   switch (act) {
     case 1: return launch_gemm<true, false, EPI_BIAS_SIG>(p, (hipStream_t)stream);
     case 2: return launch_gemm<true, false, EPI_BIAS_NEG>(p, (hipStream_t)stream);
@@ -2950,6 +3104,12 @@ extern "C" int tnet_affine_softmax_xent(const float* X, TnetMatrixDim dX, const 
   int st = check_common(p);
   if (st) return st;
   hipStream_t s = (hipStream_t)stream;
+  // softmax_xent_kernel's lane-to-column map: the 16-byte one where its launch would use it
+  const int v4 = (p.N & 3) == 0 && (!Z || (aligned16(Z) && (strideZ & 3) == 0)) &&
+                 (!Y || (aligned16(Y) && (strideY & 3) == 0)) && aligned16(E) && (strideE & 3) == 0;
+  if (top_rows_ok(p))  // up to 144 classes over K in [512, 1024]: one launch (top_rows.hip)
+    return tnetk_top_rows(X, dX.stride, W, dW.stride, b, p.M, p.N, p.K, labels, Z, strideZ, Y, strideY, E, strideE,
+                          stats, colpart, ldcolpart, v4, 0, stream);
   const GemmPlan pl = plan_gemm<true>(p, true);
   int cfg = pl.cfg, bm, bn, kind;
   cfg_shape(cfg, &bm, &bn, &kind);
@@ -2958,9 +3118,6 @@ extern "C" int tnet_affine_softmax_xent(const float* X, TnetMatrixDim dX, const 
   Partials pt;
   st = launch_partials<true, false>(p, cfg, pl.ks, s, &pt);
   if (st) return st;
-  // softmax_xent_kernel's lane-to-column map: the 16-byte one where its launch would use it
-  const int v4 = (p.N & 3) == 0 && (!Z || (aligned16(Z) && (strideZ & 3) == 0)) &&
-                 (!Y || (aligned16(Y) && (strideY & 3) == 0)) && aligned16(E) && (strideE & 3) == 0;
   affine_softmax_xent_kernel<<<(unsigned)cdiv(p.M, kColsumSlabRows), kSxThreads, 0, s>>>(
       p, pt.ws, pt.slab, pl.ks, pt.ldp, labels, Z, strideZ, Y, strideY, E, strideE, stats, colpart, ldcolpart, v4);
   TNET_LAUNCH_CHECK();
@@ -3131,7 +3288,8 @@ extern "C" int tnet_affine_update(const float* X, TnetMatrixDim dX, const float*
   p.scale = scale; p.mmt = mmt; p.l2 = l2;
   int st = check_common(p);
   if (st) return st;
-  return launch_gemm<false, false, EPI_SGD>(p, (hipStream_t)stream);
+  shadow_attach(p);
+  return shadow_done(p, launch_gemm<false, false, EPI_SGD>(p, (hipStream_t)stream));
 }
 
 extern "C" int tnet_colsum_slabs(int rows) { return rows > 0 ? (rows + kColsumSlabRows - 1) / kColsumSlabRows : 0; }
@@ -3154,16 +3312,17 @@ extern "C" int tnet_affine_bwd_colsum(const float* E, TnetMatrixDim dE, const fl
   return launch_gemm<true, true, EPI_DSIG_CS>(p, (hipStream_t)stream);
 }
 
-extern "C" int tnet_affine_bwd_colsum_slabs(const float* E, TnetMatrixDim dE, const float* W, TnetMatrixDim dW,
-                                            const float* Ybelow, int strideYbelow, float* Eo, TnetMatrixDim dEo,
-                                            float* colpart, int ldcolpart, float* colpartE, int ldcolpartE,
-                                            void* stream) {
+static int bwd_colsum_slabs(const float* E, TnetMatrixDim dE, const float* W, TnetMatrixDim dW, const float* Ybelow,
+                            int strideYbelow, float* Eo, TnetMatrixDim dEo, float* colpart, int ldcolpart,
+                            float* colpartE, int ldcolpartE, void* stream, bool bt) {
   // tnet_affine_bwd_colsum(E, W, Ybelow, Eo, colpart) + tnet_colsum_slab_sums(E, colpartE) in one launch
-  if (dE.cols != dW.cols || dEo.rows != dE.rows || dEo.cols != dW.rows || !Ybelow || !colpart ||
+  // (bt: W is the transposed shadow [n_out x n_in], the NN form)
+  const int w_k = bt ? dW.rows : dW.cols, w_n = bt ? dW.cols : dW.rows;
+  if (dE.cols != w_k || dEo.rows != dE.rows || dEo.cols != w_n || !Ybelow || !colpart ||
       ldcolpart < dEo.cols || !aligned16(Ybelow) || (strideYbelow & 3) || !colpartE || ldcolpartE < dE.cols)
     return TNET_ERR_ARG;
   GemmP p{};
-  p.M = dE.rows; p.N = dW.rows; p.K = dE.cols;
+  p.M = dE.rows; p.N = w_n; p.K = dE.cols;
   p.A = E; p.lda = dE.stride; p.B = W; p.ldb = dW.stride; p.C = Eo; p.ldc = dEo.stride;
   p.alpha = 1.f; p.beta = 0.f;
   p.aux = Ybelow; p.ldaux = strideYbelow;
@@ -3173,7 +3332,8 @@ extern "C" int tnet_affine_bwd_colsum_slabs(const float* E, TnetMatrixDim dE, co
   // what launch_colsum_bwd runs alone: the plain 64x128 grid (no forced configuration, no stream-K)
   if (p.M <= 0 || p.N <= 0 || forced_cfg() >= 0 || g_reserve > 0) return TNET_ERR_UNSUPPORTED;
   if ((long)cdiv(p.M, 64) * cdiv(p.N, 128) < 200) return TNET_ERR_UNSUPPORTED;
-  if (4L * p.M * p.lda >= (1L << 32) || 4L * p.N * p.ldb >= (1L << 32)) return TNET_ERR_UNSUPPORTED;
+  if (4L * p.M * p.lda >= (1L << 32) || 4L * (bt ? (long)p.K : (long)p.N) * p.ldb >= (1L << 32))
+    return TNET_ERR_UNSUPPORTED;
   // tnet_colsum_slab_sums's 16-B form
   const int slabs = cs_slabs(dE.rows);
   if (slabs != cdiv(dE.rows, CS_ROWS) || (dE.cols & 3) || (dE.stride & 3) || !aligned16(E)) return TNET_ERR_UNSUPPORTED;
@@ -3182,7 +3342,20 @@ extern "C" int tnet_affine_bwd_colsum_slabs(const float* E, TnetMatrixDim dE, co
   p.wt = g_wt;
   const int na = cdiv(p.M, 64) * cdiv(p.N, 128), ncb = cdiv(dE.cols, CS_COLS * 4);
   const unsigned grid = (unsigned)(na + ncb * slabs);
-  if (px_exact<64, 128, EPI_DSIG_CS>(p) && kc_direct(p))
+  if (bt) {
+    // the forward's direct form (m64x128a8: whole k-tiles in an even count, 16-B aligned, 31-bit offsets; the
+    // k tail through the DMA images) where the exact prefetch holds, else the ring
+    const int nfull = p.K / 64;
+    const bool dir = g_direct > 0 && nfull >= 1 && nfull % 2 == 0 && p.N % 4 == 0 && !(p.lda & 3) && !(p.ldb & 3) &&
+                     aligned16(p.A) && aligned16(p.B) && 4L * p.M * p.lda < (1L << 31) &&
+                     4L * p.K * p.ldb < (1L << 31);
+    if (px_exact<64, 128, EPI_DSIG_CS>(p) && dir)
+      gemm16_bwd_slabs_kernel<true, 6, false><<<grid, 256, 0, (hipStream_t)stream>>>(p, na, E, dE, colpartE, ldcolpartE, slabs, ncb);
+    else if (px_exact<64, 128, EPI_DSIG_CS>(p))
+      gemm16_bwd_slabs_kernel<true, 0, false><<<grid, 256, 0, (hipStream_t)stream>>>(p, na, E, dE, colpartE, ldcolpartE, slabs, ncb);
+    else
+      gemm16_bwd_slabs_kernel<false, 0, false><<<grid, 256, 0, (hipStream_t)stream>>>(p, na, E, dE, colpartE, ldcolpartE, slabs, ncb);
+  } else if (px_exact<64, 128, EPI_DSIG_CS>(p) && kc_direct(p))
     gemm16_bwd_slabs_kernel<true, 8><<<grid, 256, 0, (hipStream_t)stream>>>(p, na, E, dE, colpartE, ldcolpartE, slabs, ncb);
   else if (px_exact<64, 128, EPI_DSIG_CS>(p))
     gemm16_bwd_slabs_kernel<true><<<grid, 256, 0, (hipStream_t)stream>>>(p, na, E, dE, colpartE, ldcolpartE, slabs, ncb);
@@ -3190,6 +3363,85 @@ extern "C" int tnet_affine_bwd_colsum_slabs(const float* E, TnetMatrixDim dE, co
     gemm16_bwd_slabs_kernel<false><<<grid, 256, 0, (hipStream_t)stream>>>(p, na, E, dE, colpartE, ldcolpartE, slabs, ncb);
   TNET_LAUNCH_CHECK();
   return TNET_OK;
+}
+
+extern "C" int tnet_affine_bwd_colsum_slabs(const float* E, TnetMatrixDim dE, const float* W, TnetMatrixDim dW,
+                                            const float* Ybelow, int strideYbelow, float* Eo, TnetMatrixDim dEo,
+                                            float* colpart, int ldcolpart, float* colpartE, int ldcolpartE,
+                                            void* stream) {
+  return bwd_colsum_slabs(E, dE, W, dW, Ybelow, strideYbelow, Eo, dEo, colpart, ldcolpart, colpartE, ldcolpartE,
+                          stream, false);
+}
+
+extern "C" int tnet_affine_bwd_colsum_slabs_t(const float* E, TnetMatrixDim dE, const float* Wt, TnetMatrixDim dWt,
+                                              const float* Ybelow, int strideYbelow, float* Eo, TnetMatrixDim dEo,
+                                              float* colpart, int ldcolpart, float* colpartE, int ldcolpartE,
+                                              void* stream) {
+  return bwd_colsum_slabs(E, dE, Wt, dWt, Ybelow, strideYbelow, Eo, dEo, colpart, ldcolpart, colpartE, ldcolpartE,
+                          stream, true);
+}
+
+extern "C" int tnet_affine_bwd_colsum_t(const float* E, TnetMatrixDim dE, const float* Wt, TnetMatrixDim dWt,
+                                        const float* Ybelow, int strideYbelow, float* Eo, TnetMatrixDim dEo,
+                                        float* colpart, int ldcolpart, void* stream) {
+  // tnet_affine_bwd_colsum from the transposed shadow Wt [n_out x n_in]: Eo = (E Wt) .* y (1 - y), NN
+  if (dE.cols != dWt.rows || dEo.rows != dE.rows || dEo.cols != dWt.cols || !Ybelow || !colpart ||
+      ldcolpart < dEo.cols || !aligned16(Ybelow) || (strideYbelow & 3))
+    return TNET_ERR_ARG;
+  GemmP p{};
+  p.M = dE.rows; p.N = dWt.cols; p.K = dE.cols;
+  p.A = E; p.lda = dE.stride; p.B = Wt; p.ldb = dWt.stride; p.C = Eo; p.ldc = dEo.stride;
+  p.alpha = 1.f; p.beta = 0.f;
+  p.aux = Ybelow; p.ldaux = strideYbelow;
+  p.cpart = colpart; p.ldcpart = ldcolpart;
+  int st = check_common(p);
+  if (st) return st;
+  return launch_colsum_bwd_t(p, (hipStream_t)stream);
+}
+
+// ---- transposed weight shadows
+__global__ __launch_bounds__(256) void transpose_kernel(const float* __restrict__ A, TnetMatrixDim d,
+                                                        float* __restrict__ T, long ldt) {
+  __shared__ float tile[64][65];
+  const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int r = r0 + ty + 4 * k, c = c0 + tx;
+    tile[ty + 4 * k][tx] = (r < (int)d.rows && c < (int)d.cols) ? A[(long)r * d.stride + c] : 0.f;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int c = c0 + ty + 4 * k, r = r0 + tx;
+    if (c < (int)d.cols && r < (int)d.rows) T[(long)c * ldt + r] = tile[tx][ty + 4 * k];
+  }
+}
+
+extern "C" int tnet_transpose(const float* A, TnetMatrixDim dA, float* T, int ldt, void* stream) {
+  if (!A || !T || ldt < (int)dA.rows || dA.stride < dA.cols) return TNET_ERR_ARG;
+  if (!dA.rows || !dA.cols) return TNET_OK;
+  transpose_kernel<<<dim3(cdiv(dA.cols, 64), cdiv(dA.rows, 64)), 256, 0, (hipStream_t)stream>>>(A, dA, T, ldt);
+  TNET_LAUNCH_CHECK();
+  return TNET_OK;
+}
+
+extern "C" int tnet_weight_shadow(const float* W, TnetMatrixDim dW, float* Wt, int ldwt) {
+  if (!W) return TNET_ERR_ARG;
+  std::lock_guard<std::mutex> g(g_shadow_mu);
+  if (!Wt) {
+    g_shadow.erase(W);
+    return TNET_OK;
+  }
+  if (ldwt < (int)dW.rows || (ldwt & 3) || ((uintptr_t)Wt & 15)) return TNET_ERR_ARG;
+  g_shadow[W] = WeightShadow{Wt, (long)ldwt, (int)dW.rows, (int)dW.cols, 0};
+  return TNET_OK;
+}
+
+extern "C" int tnet_weight_shadow_kept(const float* W) {
+  std::lock_guard<std::mutex> g(g_shadow_mu);
+  auto it = g_shadow.find(W);
+  return it == g_shadow.end() ? TNET_ERR_ARG : it->second.kept;
 }
 
 extern "C" int tnet_affine_update_bias(const float* X, TnetMatrixDim dX, const float* E, TnetMatrixDim dE, float* W,
@@ -3212,7 +3464,8 @@ extern "C" int tnet_affine_update_bias(const float* X, TnetMatrixDim dX, const f
   int st = check_common(p);
   if (st) return st;
   if (p.M <= 0 || p.N <= 0) return TNET_OK;
-  return launch_gemm<false, false, EPI_SGD_B>(p, (hipStream_t)stream);
+  shadow_attach(p);
+  return shadow_done(p, launch_gemm<false, false, EPI_SGD_B>(p, (hipStream_t)stream));
 }
 
 // the GemmP of tnet_affine_update_bias's launch (TNET_ERR_ARG on bad arguments)
@@ -3251,7 +3504,11 @@ extern "C" int tnet_affine_update_bias_pair(const float* X, TnetMatrixDim dX, co
                           b2, corr_b2);
   if (st) return st;
   if (W == W2 || b == b2 || (corrW && corrW == corrW2)) return TNET_ERR_ARG;
-  return launch_upd_pair(pa, pb, (hipStream_t)stream);
+  shadow_attach(pb);
+  shadow_attach(pa);
+  const int rc = launch_upd_pair(pa, pb, (hipStream_t)stream);
+  shadow_done(pa, rc);
+  return shadow_done(pb, rc);
 }
 
 // gemm16_upd_mixed_gather_kernel's conditions (TNET_UPD_MIXED=0: never): A is what tnet_affine_update_bias runs as
@@ -3318,6 +3575,8 @@ extern "C" int tnet_affine_update_bias_gather(const float* X, TnetMatrixDim dX, 
     return TNET_ERR_UNSUPPORTED;
   if (forced_cfg() >= 0 || split2_on() || g_split > 0) return TNET_ERR_UNSUPPORTED;
   if (pa.M <= 0 || pa.N <= 0 || (two && (pb.M <= 0 || pb.N <= 0))) return TNET_ERR_UNSUPPORTED;
+  shadow_attach(pa);  // every form below runs gemm16_body's epilogue: the shadows are kept
+  if (two) shadow_attach(pb);
   int na, nb = 0;
   if (two && upd_mixed_ok(pa, pb)) {
     // a 2048-wide layer's update (128x128 direct) + the first layer's (64x64) + the gather
@@ -3333,7 +3592,8 @@ extern "C" int tnet_affine_update_bias_gather(const float* X, TnetMatrixDim dX, 
     BunchGatherP g{y, x, labels_out, labels_in, copy_from, dy.rows, c4, dy.stride, dx.stride};
     gemm16_upd_mixed_gather_kernel<<<na + nb + ng, 256, 0, (hipStream_t)stream>>>(pa, pb, na, nb, g);
     TNET_LAUNCH_CHECK();
-    return TNET_OK;
+    shadow_done(pa, TNET_OK);
+    return shadow_done(pb, TNET_OK);
   }
   if (two) {
     // the pair kernel's conditions (launch_upd_pair): both 64x64 grids in one round over the CUs
@@ -3362,21 +3622,24 @@ extern "C" int tnet_affine_update_bias_gather(const float* X, TnetMatrixDim dX, 
   BunchGatherP g{y, x, labels_out, labels_in, copy_from, dy.rows, c4, dy.stride, dx.stride};
   gemm16_upd_gather_kernel<64, 64, 32, 4, 1, 4><<<na + nb + ng, 256, 0, (hipStream_t)stream>>>(pa, pb, na, nb, g);
   TNET_LAUNCH_CHECK();
+  shadow_done(pa, TNET_OK);
+  if (two) shadow_done(pb, TNET_OK);
   return TNET_OK;
 }
 
-extern "C" int tnet_affine_update_bwd_pair(const float* X, TnetMatrixDim dX, const float* E, TnetMatrixDim dE,
-                                          float* W, TnetMatrixDim dW, float* corrW, int strideCorr, float scale,
-                                          float mmt, float l2, const float* colpart, int ldcolpart, float* b,
-                                          float* corr_b, const float* E2, TnetMatrixDim dE2, const float* W2,
-                                          TnetMatrixDim dW2, const float* Ybelow, int strideYbelow, float* Eo,
-                                          TnetMatrixDim dEo, float* colpart2, int ldcolpart2, void* stream) {
+static int update_bwd_pair(const float* X, TnetMatrixDim dX, const float* E, TnetMatrixDim dE, float* W,
+                           TnetMatrixDim dW, float* corrW, int strideCorr, float scale, float mmt, float l2,
+                           const float* colpart, int ldcolpart, float* b, float* corr_b, const float* E2,
+                           TnetMatrixDim dE2, const float* W2, TnetMatrixDim dW2, const float* Ybelow, int strideYbelow,
+                           float* Eo, TnetMatrixDim dEo, float* colpart2, int ldcolpart2, void* stream, bool bwd_t) {
   // tnet_affine_update_bias(X, E, W, ...) and tnet_affine_bwd_colsum(E2, W2, Ybelow, Eo, colpart2) in one
-  // launch; the two must be independent (W is not W2, Eo / colpart2 overlap none of the update's operands)
+  // launch; the two must be independent (W is not W2, Eo / colpart2 overlap none of the update's operands).
+  // bwd_t: W2 is the lower layer's transposed shadow [n_out x n_in] (tnet_affine_bwd_colsum_t's operand)
   if (dX.rows != dE.rows || dW.rows != dX.cols || dW.cols != dE.cols || !colpart || !b || ldcolpart < dE.cols)
     return TNET_ERR_ARG;
   if (mmt != 0.f && (!corrW || !corr_b)) return TNET_ERR_ARG;
-  if (dE2.cols != dW2.cols || dEo.rows != dE2.rows || dEo.cols != dW2.rows || !Ybelow || !colpart2 ||
+  const int w2_k = bwd_t ? dW2.rows : dW2.cols, w2_n = bwd_t ? dW2.cols : dW2.rows;
+  if (dE2.cols != w2_k || dEo.rows != dE2.rows || dEo.cols != w2_n || !Ybelow || !colpart2 ||
       ldcolpart2 < dEo.cols || !aligned16(Ybelow) || (strideYbelow & 3))
     return TNET_ERR_ARG;
   if (W == W2) return TNET_ERR_ARG;
@@ -3391,14 +3654,36 @@ extern "C" int tnet_affine_update_bwd_pair(const float* X, TnetMatrixDim dX, con
   int st = check_common(pu);
   if (st) return st;
   GemmP pb{};
-  pb.M = dE2.rows; pb.N = dW2.rows; pb.K = dE2.cols;
+  pb.M = dE2.rows; pb.N = w2_n; pb.K = dE2.cols;
   pb.A = E2; pb.lda = dE2.stride; pb.B = W2; pb.ldb = dW2.stride; pb.C = Eo; pb.ldc = dEo.stride;
   pb.alpha = 1.f; pb.beta = 0.f;
   pb.aux = Ybelow; pb.ldaux = strideYbelow;
   pb.cpart = colpart2; pb.ldcpart = ldcolpart2;
   st = check_common(pb);
   if (st) return st;
-  return launch_pair_upd_bwd(pu, pb, (hipStream_t)stream);
+  if (bwd_t && g_reserve > 0) return TNET_ERR_UNSUPPORTED;
+  shadow_attach(pu);
+  return shadow_done(pu, launch_pair_a_bwd<EPI_SGD_B>(pu, pb, (hipStream_t)stream, bwd_t));
+}
+
+extern "C" int tnet_affine_update_bwd_pair(const float* X, TnetMatrixDim dX, const float* E, TnetMatrixDim dE,
+                                          float* W, TnetMatrixDim dW, float* corrW, int strideCorr, float scale,
+                                          float mmt, float l2, const float* colpart, int ldcolpart, float* b,
+                                          float* corr_b, const float* E2, TnetMatrixDim dE2, const float* W2,
+                                          TnetMatrixDim dW2, const float* Ybelow, int strideYbelow, float* Eo,
+                                          TnetMatrixDim dEo, float* colpart2, int ldcolpart2, void* stream) {
+  return update_bwd_pair(X, dX, E, dE, W, dW, corrW, strideCorr, scale, mmt, l2, colpart, ldcolpart, b, corr_b, E2,
+                         dE2, W2, dW2, Ybelow, strideYbelow, Eo, dEo, colpart2, ldcolpart2, stream, false);
+}
+
+extern "C" int tnet_affine_update_bwd_pair_t(const float* X, TnetMatrixDim dX, const float* E, TnetMatrixDim dE,
+                                            float* W, TnetMatrixDim dW, float* corrW, int strideCorr, float scale,
+                                            float mmt, float l2, const float* colpart, int ldcolpart, float* b,
+                                            float* corr_b, const float* E2, TnetMatrixDim dE2, const float* W2t,
+                                            TnetMatrixDim dW2t, const float* Ybelow, int strideYbelow, float* Eo,
+                                            TnetMatrixDim dEo, float* colpart2, int ldcolpart2, void* stream) {
+  return update_bwd_pair(X, dX, E, dE, W, dW, corrW, strideCorr, scale, mmt, l2, colpart, ldcolpart, b, corr_b, E2,
+                         dE2, W2t, dW2t, Ybelow, strideYbelow, Eo, dEo, colpart2, ldcolpart2, stream, true);
 }
 
 extern "C" int tnet_affine_grad_bwd_pair(const float* X, TnetMatrixDim dX, const float* E, TnetMatrixDim dE, float* G,

@@ -88,6 +88,15 @@ _SIGS = {
     "tnet_affine_bwd_colsum": (i32, [vp, MatrixDim, vp, MatrixDim, vp, i32, vp, MatrixDim, vp, i32, vp]),
     "tnet_affine_bwd_colsum_slabs": (i32, [vp, MatrixDim, vp, MatrixDim, vp, i32, vp, MatrixDim, vp, i32, vp, i32,
                                            vp]),
+    "tnet_affine_bwd_colsum_t": (i32, [vp, MatrixDim, vp, MatrixDim, vp, i32, vp, MatrixDim, vp, i32, vp]),
+    "tnet_affine_bwd_colsum_slabs_t": (i32, [vp, MatrixDim, vp, MatrixDim, vp, i32, vp, MatrixDim, vp, i32, vp, i32,
+                                             vp]),
+    "tnet_affine_update_bwd_pair_t": (i32, [vp, MatrixDim, vp, MatrixDim, vp, MatrixDim, vp, i32, f32, f32, f32, vp,
+                                            i32, vp, vp, vp, MatrixDim, vp, MatrixDim, vp, i32, vp, MatrixDim, vp, i32,
+                                            vp]),
+    "tnet_weight_shadow": (i32, [vp, MatrixDim, vp, i32]),
+    "tnet_weight_shadow_kept": (i32, [vp]),
+    "tnet_transpose": (i32, [vp, MatrixDim, vp, i32, vp]),
     "tnet_affine_update_bias": (i32, [vp, MatrixDim, vp, MatrixDim, vp, MatrixDim, vp, i32, f32, f32, f32, vp, i32,
                                       vp, vp, vp]),
     "tnet_affine_update_bias_pair": (i32, [vp, MatrixDim, vp, MatrixDim, vp, MatrixDim, vp, i32, f32, f32, f32, vp, i32,

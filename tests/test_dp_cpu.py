@@ -119,3 +119,70 @@ def test_shard_ranges_cover_every_element_once(n, world):
     assert tails[0] == ([(main, n)] if main < n else [])
     owner[main:] += 1
     assert np.all(owner == 1)
+
+
+CHECK_WORKER = r'''
+import os, sys, json
+import numpy as np
+import torch, torch.distributed as dist
+sys.path.insert(0, os.path.join(sys.argv[1], "nnet-asr_amd"))
+from tnet_amd import dpcheck
+rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+dist.init_process_group("gloo", rank=rank, world_size=world)
+def allreduce64(a):
+    dist.all_reduce(torch.from_numpy(a))
+def gather(res):
+    got = [None] * world
+    dist.all_gather_object(got, res)
+    return got
+sizes = [2048 * 7 + 3, 135, 1]
+local = [np.random.default_rng(100 * r + i).standard_normal(n).astype(np.float32)
+         for i, n in enumerate(sizes) for r in [rank]]
+every = [[np.random.default_rng(100 * r + i).standard_normal(n).astype(np.float32) for r in range(world)]
+         for i, n in enumerate(sizes)]
+true_sum = [np.sum(np.stack(e), 0, dtype=np.float32) for e in every]
+out = {}
+# all-reduce form: every element reduced
+out["allreduce"] = dpcheck.merge_ranks(gather(dpcheck.compare_reduction(list(zip(local, true_sum)), allreduce64)))
+# sharded form: only this rank's shard + the tail reduced (NaN elsewhere), the ShardRanges split
+def sharded(s, n):
+    c = (n // (4 * world)) * 4
+    r = np.full(n, np.nan, np.float32)
+    r[rank * c:rank * c + c] = s[rank * c:rank * c + c]
+    r[c * world:] = s[c * world:]
+    return r
+out["shard"] = dpcheck.merge_ranks(gather(dpcheck.compare_reduction(
+    [(l, sharded(s, len(s))) for l, s in zip(local, true_sum)], allreduce64)))
+# a stale operand: rank 1's reduction of block 0 missed its own contribution (what fence-free events could cause)
+bad = [s.copy() for s in true_sum]
+if rank == 1:
+    bad[0] = bad[0] - local[0]
+out["stale"] = dpcheck.merge_ranks(gather(dpcheck.compare_reduction(list(zip(local, bad)), allreduce64)))
+print(json.dumps(out))
+dist.destroy_process_group()
+'''
+
+
+def test_reduction_check_gloo_world2():
+    """bench.py's rccl_check logic (tnet_amd/dpcheck.py) over gloo at world 2: the reduced gradients of both exchange
+    forms (all-reduce; reduce-scatter with the rank's shard + tail) pass against the float64 sum of the local blocks,
+    and a reduction that lost one rank's contribution on one rank is caught (ok False, the worst block named)"""
+    import json
+    port = _free_port()
+    env_base = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE="2", OMP_NUM_THREADS="1")
+    repo = os.path.dirname(HERE)
+    procs = [subprocess.Popen([sys.executable, "-c", CHECK_WORKER, repo], env=dict(env_base, RANK=str(r)),
+                              stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for r in range(2)]
+    outs = []
+    for p in procs:
+        o, e = p.communicate(timeout=240)
+        assert p.returncode == 0, e[-3000:]
+        outs.append(json.loads(o.strip().splitlines()[-1]))
+    for o in outs:
+        assert o["allreduce"]["ok"] and o["allreduce"]["max_rel_err"] < 1e-6 and o["allreduce"]["blocks"] == 3
+        assert o["shard"]["ok"] and o["shard"]["max_rel_err"] < 1e-6
+        n0 = 2048 * 7 + 3
+        c = (n0 // 8) * 4
+        c1 = (135 // 8) * 4
+        assert o["shard"]["elements_per_rank"][0] == (c + n0 - 2 * c) + (c1 + 135 - 2 * c1) + 1
+        assert not o["stale"]["ok"] and o["stale"]["worst_block"] == 0 and o["stale"]["max_rel_err"] > 0.1

@@ -68,3 +68,24 @@ def test_bench_two_ranks_rehearsal():
     d = _line(p.stdout)
     _check_contract(d, 2, 2, 1)
     assert d["roofline"] is None  # kernel timing off
+    # the reduction check's C++ capture path (HostExchange) at world 2: both ranks' gradients of one step
+    c = d["rccl_check"]
+    assert c["ok"] and c["ranks"] == 2 and c["transport"] == "host" and c["transport_ranks"] == 2
+    assert list(c["modes"]) == ["all-reduce"] and c["modes"]["all-reduce"]["blocks"] == 10
+    assert c["max_rel_err"] <= 1e-6
+
+
+@pytest.mark.parametrize("shard", ["0", "1"])
+def test_bench_force_dp_reduction_check(shard):
+    """--force-dp at N = 1 (a one-rank RCCL communicator): the reduction check runs through RcclExchange's capture
+    (both exchange forms) and the one-rank reduction equals the local gradient exactly"""
+    cmd = [sys.executable, "bench.py", "--steps", "2", "--warmup", "1", "--no-cpu-baseline", "--cache", "4096",
+           "--force-dp", "--kernel-timing", "0", "--breakdown-steps", "0", "--prewarm-ms", "0"]
+    p = subprocess.run(cmd, cwd=REPO, capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, TNET_DP_SHARD=shard))
+    assert p.returncode == 0, p.stderr[-3000:]
+    c = _line(p.stdout)["rccl_check"]
+    mode = "reduce-scatter+all-gather" if shard == "1" else "all-reduce"
+    assert c["ok"] and c["ranks"] == 1 and c["transport_ranks"] == 1 and list(c["modes"]) == [mode]
+    assert c["max_rel_err"] == 0.0 and c["modes"][mode]["blocks"] == 10
+    assert c["librccl"] and "rccl" in c["librccl"]
