@@ -214,6 +214,16 @@ int tnet_colsum_slab_sums(const float* E, TnetMatrixDim dE, float* colpart, int 
 int tnet_affine_softmax_xent(const float* X, TnetMatrixDim dX, const float* W, TnetMatrixDim dW, const float* b,
                              const int* labels, float* Z, int strideZ, float* Y, int strideY, float* E, int strideE,
                              double* stats, float* colpart, int ldcolpart, void* stream);
+/* The narrow top layer's one-launch row-block kernel (up to 144 classes over K = 512 / 768 / 1024; top_rows.hip):
+ * OFF by default -- measured slower than the two-launch form above on MI355X -- and taken by
+ * tnet_affine_softmax_xent and tnet_affine_fwd(act 0) for those shapes once enabled here (on: 1; variant: 1 = W
+ * fragments straight into registers, 3 = W slice staged in LDS; or TNET_TOP_ROWS=1 / TNET_TOP_ROWS_V at load time).
+ * Same Z / Y / E / statistics bit for bit either way.  Process-wide; not to be flipped while launches are in flight. */
+int tnet_top_rows_config(int on, int variant);
+/* its diagnostics: while buf != NULL every launch records thread 0's s_memtime per phase into buf[block * 8 + i]
+ * (device memory, 8 64-bit words a block; 0 entry, 1 operands loaded, 2 MFMAs issued, 3 partial tiles stored +
+ * ticket, 4 logits-only end, 5 softmax done); NULL: off */
+int tnet_top_rows_stamps(long long* buf);
 /* tnet_affine_update + tnet_bias_update(E, b, corr_b, scale, mmt) in one launch, colsum(E) taken from
  * colpart (written for E by tnet_affine_bwd_colsum); corr_b is required when mmt != 0
  * (cuBiasedLinearity.cc:46-64). */

@@ -269,9 +269,10 @@ void CuNetwork::TrainBunch(const CuMatrix<BaseFloat>& X, const CuVector<int>& la
   mNetComponents.front()->SetInput(X);
   // the backward GEMMs read each weight's transposed shadow (NN: the forward's layout and direct form), which the
   // fused updates keep current in the same pass (CuBiasedLinearity::UseShadow; not in the data-parallel step, whose
-  // flat SGD apply writes no shadow; TNET_BWD_SHADOW=0: the NT backward from W everywhere, 2: the hidden layers only,
-  // not the top layer)
-  static const int use_shadow = getenv("TNET_BWD_SHADOW") ? atoi(getenv("TNET_BWD_SHADOW")) : 1;
+  // flat SGD apply writes no shadow).  TNET_BWD_SHADOW: 2 (default) the hidden layers' backward GEMMs, whose 2048^2
+  // shadow costs the update ~1 us and saves the backward ~5 (the top layer's 32 MB shadow costs its update 12 us for
+  // an 8.5 us faster backward: profiles/r05_bwd_shadow_ab.json); 1 every layer above the first; 0 none (NT from W)
+  static const int use_shadow = getenv("TNET_BWD_SHADOW") ? atoi(getenv("TNET_BWD_SHADOW")) : 2;
   const bool shadows = use_shadow > 0 && train && !exchange;
   if (shadows)
     for (int l = 1; l < (use_shadow == 2 ? nl - 1 : nl); l++)

@@ -2430,13 +2430,13 @@ static int g_wt = 1;  // TNET_GEMM_WT=0: plain 16-B epilogue stores instead of w
 // update of W kept its shadow (shadow_done), which tnet_weight_shadow_kept reports
 // the narrow top layer's row-block kernel (top_rows.hip): the shapes it takes, unless a configuration or split-K
 // count is forced (tests of the general GEMM's forms)
-extern "C" int tnetk_top_rows_ok(const float* X, long ldx, int M, int N, int K);
+extern "C" int tnetk_top_rows_ok(const float* X, long ldx, const float* W, long ldw, int M, int N, int K);
 extern "C" int tnetk_top_rows(const float* X, long ldx, const float* W, long ldw, const float* b, int M, int N, int K,
                               const int* labels, float* Z, long ldz, float* Y, long ldy, float* E, long lde,
                               double* stats, float* cpart, long ldcp, int v4, int logits_only, void* stream);
 static int forced_cfg();
 static bool top_rows_ok(const GemmP& p) {
-  return forced_cfg() < 0 && g_split <= 0 && tnetk_top_rows_ok(p.A, p.lda, p.M, p.N, p.K);
+  return forced_cfg() < 0 && g_split <= 0 && tnetk_top_rows_ok(p.A, p.lda, p.B, p.ldb, p.M, p.N, p.K);
 }
 struct WeightShadow {
   float* t;

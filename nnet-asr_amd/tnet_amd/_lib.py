@@ -95,6 +95,8 @@ _SIGS = {
                                             i32, vp, vp, vp, MatrixDim, vp, MatrixDim, vp, i32, vp, MatrixDim, vp, i32,
                                             vp]),
     "tnet_weight_shadow": (i32, [vp, MatrixDim, vp, i32]),
+    "tnet_top_rows_stamps": (i32, [vp]),
+    "tnet_top_rows_config": (i32, [i32, i32]),
     "tnet_weight_shadow_kept": (i32, [vp]),
     "tnet_transpose": (i32, [vp, MatrixDim, vp, i32, vp]),
     "tnet_affine_update_bias": (i32, [vp, MatrixDim, vp, MatrixDim, vp, MatrixDim, vp, i32, f32, f32, f32, vp, i32,

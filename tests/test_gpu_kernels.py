@@ -414,16 +414,23 @@ def test_affine_grad_bias(rows, n_in, n_out, gemm_cfg):
     np.testing.assert_array_equal(dgb.numpy().ravel(), P.astype(np.float64).sum(0).astype(np.float32))
 
 
-@pytest.fixture(params=["auto", "auto+sk4", "m64x128k64s2", "m32x64k64s2+sk2", "g64x64k32s4w4"])
+@pytest.fixture(params=["auto", "auto+sk4", "m64x128k64s2", "m32x64k64s2+sk2", "g64x64k32s4w4", "rows1", "rows3"])
 def top_cfg(request):
-    check(lib().tnet_gemm_config(request.param.encode()))
+    """GEMM configurations of the top layer; rows1 / rows3: the opt-in one-launch row-block kernel (top_rows.hip,
+    both B-operand variants) for the shapes it takes, the two-launch form for the rest"""
+    rows = request.param.startswith("rows")
+    check(lib().tnet_gemm_config(b"auto" if rows else request.param.encode()))
+    if rows:
+        check(lib().tnet_top_rows_config(1, int(request.param[4:])))
     yield request.param
+    check(lib().tnet_top_rows_config(0, 1))
     check(lib().tnet_gemm_config(b"auto+il0"))
 
 
 @pytest.mark.parametrize("keep_y", [False, True])
 @pytest.mark.parametrize("rows,n_in,n_out", [(1024, 1024, 135), (37, 20, 7), (1000, 598, 256), (64, 1024, 128),
-                                             (300, 2048, 200), (1, 5, 1)])
+                                             (300, 2048, 200), (1, 5, 1), (1000, 512, 135), (80, 768, 144),
+                                             (1009, 1024, 17)])
 def test_affine_softmax_xent(rows, n_in, n_out, keep_y, top_cfg):
     """the fused top layer (slices + bias + softmax + xent + error + slab sums) gives the logits, the
     softmax output and the error of tnet_affine_fwd + tnet_softmax_xent bit for bit, their statistics,
