@@ -390,15 +390,13 @@ std::vector<CuParamBlock> CuBiasedLinearity::GradientBlocks() {
           CuParamBlock{mGradB.pCUData(), (long)mGradB.Dim(), mBias.pCUData()}};
 }
 
-void CuBiasedLinearity::ApplyGradient(size_t frames, void* stream, const GradExchange* ex) {
-  CuProfileScope p("CuBiasedLinearity::ApplyGradient");
-  float scale, l2;
-  UpdateConstants(frames, &scale, &l2);
+int CuBiasedLinearity::ApplySegments(size_t frames, const GradExchange* ex, TnetSgdSeg* seg, float* scale) {
+  float l2;
+  UpdateConstants(frames, scale, &l2);
   const bool mmt = mMomentum != 0.0f;
   mShadowValid = false;  // the flat apply writes no transposed shadow
   // padding columns of W and of the gradient are zero, so the flat update keeps them zero; W and b
   // in one launch, each as the element ranges this rank applies (sharded apply: its shard + the tail)
-  TnetSgdSeg seg[4];
   int nseg = 0;
   auto add = [&](float* prm, float* grd, float* corr, long n, float wl2) {
     long lo[2], hi[2];
@@ -409,6 +407,14 @@ void CuBiasedLinearity::ApplyGradient(size_t frames, void* stream, const GradExc
   add(mLinearity.pCUData(), mGradW.pCUData(), mmt ? mLinearityCorrection.pCUData() : nullptr,
       (long)(mLinearity.Rows() * mLinearity.Stride()), l2);
   add(mBias.pCUData(), mGradB.pCUData(), mmt ? mBiasCorrection.pCUData() : nullptr, (long)mBias.Dim(), 0.f);
+  return nseg;
+}
+
+void CuBiasedLinearity::ApplyGradient(size_t frames, void* stream, const GradExchange* ex) {
+  CuProfileScope p("CuBiasedLinearity::ApplyGradient");
+  TnetSgdSeg seg[4];
+  float scale;
+  const int nseg = ApplySegments(frames, ex, seg, &scale);
   if (stream) {  // beside the compute stream (GradExchange::ApplyStream): no library-stream timing
     TNET_SAFE_CALL(tnet_sgd_update_multi(seg, nseg, scale, mMomentum, stream));
     return;
@@ -416,6 +422,23 @@ void CuBiasedLinearity::ApplyGradient(size_t frames, void* stream, const GradExc
   KTScope kt("sgd_apply:" + std::to_string(GetNInputs()) + "x" + std::to_string(GetNOutputs()),
              12.0 * (double)(mLinearity.Rows() * mLinearity.Stride() + mBias.Dim()));
   TNET_SAFE_CALL(tnet_sgd_update_multi(seg, nseg, scale, mMomentum, S));
+}
+
+void CuBiasedLinearity::ApplyGradients(CuBiasedLinearity* const* ls, int n, size_t frames, const GradExchange* ex) {
+  CuProfileScope p("CuBiasedLinearity::ApplyGradient");
+  TnetSgdSeg seg[8];
+  float scale[2];
+  bool same = n == 2 && ls[0]->mMomentum == ls[1]->mMomentum;
+  int nseg = 0;
+  for (int i = 0; i < n && same; ++i) nseg += ls[i]->ApplySegments(frames, ex, seg + nseg, &scale[i]);
+  if (!same || scale[0] != scale[1]) {  // other constants: one launch per layer
+    for (int i = 0; i < n; ++i) ls[i]->ApplyGradient(frames, nullptr, ex);
+    return;
+  }
+  double bytes = 0.0;
+  for (int i = 0; i < nseg; ++i) bytes += 12.0 * (double)seg[i].n;
+  KTScope kt("sgd_apply:" + std::to_string(n) + "layers", bytes);
+  TNET_SAFE_CALL(tnet_sgd_update_multi(seg, nseg, scale[0], ls[0]->mMomentum, S));
 }
 
 void CuBiasedLinearity::ReadFromStream(std::istream& rIn) {

@@ -40,6 +40,9 @@ class CuBiasedLinearity : public CuUpdatableComponent {
                                     const CuMatrix<BaseFloat>& E2, const CuMatrix<BaseFloat>& Ybelow,
                                     CuMatrix<BaseFloat>& Eo, CuMatrix<BaseFloat>& colpart2);
   void ApplyGradient(size_t frames, void* stream = nullptr, const GradExchange* ex = nullptr) override;
+  /// the applies of n (<= 2) layers on the compute stream in ONE launch when their SGD constants agree (the
+  /// data-parallel step's inline exchange, GradExchange::SubmitInline); else ApplyGradient per layer
+  static void ApplyGradients(CuBiasedLinearity* const* ls, int n, size_t frames, const GradExchange* ex);
   std::vector<CuParamBlock> GradientBlocks() override;
 
   void ReadFromStream(std::istream& rIn) override;
@@ -106,6 +109,8 @@ class CuBiasedLinearity : public CuUpdatableComponent {
   bool mShadowOn = false, mShadowValid = false;
   /// after an update launch of W: the shadow is current iff that launch wrote it (tnet_weight_shadow_kept)
   void NoteUpdate() { mShadowValid = mShadowOn && tnet_weight_shadow_kept(mLinearity.pCUData()) == 1; }
+  /// the SGD segments (W, b: this rank's ranges) of the data-parallel apply into seg (<= 4), their scale
+  int ApplySegments(size_t frames, const GradExchange* ex, TnetSgdSeg* seg, float* scale);
 };
 
 class CuSigmoid : public CuComponent {

@@ -530,10 +530,11 @@ void CuNetwork::TrainBunch(const CuMatrix<BaseFloat>& X, const CuVector<int>& la
         } else {
           // the step's last gradient GEMM carries the next bunch's gather (when the trainer handed one over) --
           // with the held-back gradient of the layer above in the same launch where both grids fit one round
+          CuBiasedLinearity* with = nullptr;  // that held-back layer
           if (err_colsum && last && mHasTailGather && !mTailDone && pgrad &&
               lin->ComputeGradientColsumGather(*mColPart[l], mTailGather, pgrad, mColPart[pgrad_l].get())) {
             mTailDone = true;
-            submit_layer(pgrad, false);
+            with = pgrad;
             pgrad = nullptr;
           } else {
             flush_grad();
@@ -545,7 +546,22 @@ void CuNetwork::TrainBunch(const CuMatrix<BaseFloat>& X, const CuVector<int>& la
             else
               lin->ComputeGradient();
           }
-          submit_layer(lin, last);
+          // every trained layer's gradient now exists and none is submitted yet (MLP3: both gradients came from
+          // that one launch): no backward GEMM is left to overlap, so the whole reduction goes on the compute
+          // stream as one group and the applies right behind it -- no stream hop in or out (a hop is a barrier
+          // packet, ~5 us each; the one-rank MLP3 DP step had five)
+          CuUpdatableComponent* grp[2];
+          int ng = 0;
+          if (with) grp[ng++] = with;
+          grp[ng++] = lin;
+          if (last && n_submitted == 0 && exchange->SubmitInline(grp, ng)) {
+            CuBiasedLinearity* lg[2] = {with ? with : lin, lin};
+            CuBiasedLinearity::ApplyGradients(lg, ng, grows, exchange);
+            n_submitted += ng;
+          } else {
+            if (with) submit_layer(with, false);
+            submit_layer(lin, last);
+          }
         }
       } else if (err_colsum) {
         pend.lin = lin;  // held back for the next layer's backward GEMM (flushed there or below)

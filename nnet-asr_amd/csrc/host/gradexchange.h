@@ -40,6 +40,17 @@ class GradExchange {
     (void)i;
     return nullptr;
   }
+  /// The step's WHOLE reduction in one go, when every trained layer's gradient already exists (no backward GEMM is
+  /// left for the reductions to overlap -- a network whose last gradient launch computed all of them, e.g. MLP3's
+  /// two-gradient + gather launch): the collectives go on the compute stream right behind the gradient kernels, as
+  /// one group, with no stream hop in and none out, and the caller applies each component on the compute stream
+  /// (ApplyGradient with no stream, then GatherParams(comp, -1, nullptr)).  Returns false when the transport does
+  /// not take this form (then Submit each component).  Only before the step's first Submit.
+  virtual bool SubmitInline(CuUpdatableComponent* const* comps, int n) {
+    (void)comps;
+    (void)n;
+    return false;
+  }
   /// Sum small host statistics over ranks (epoch-end MergeStats, step planning); blocking.
   virtual void AllReduceHost(double* v, int n) = 0;
 
@@ -102,14 +113,14 @@ class GradExchange {
  protected:
   /// Submit's halves of the capture (no-ops unless armed; `stream` orders the copies after the gradient kernels
   /// and after the reduction respectively)
-  void CaptureLocal(CuUpdatableComponent& comp, void* stream);
-  void CaptureReduced(CuUpdatableComponent& comp, void* stream);
+  /// (CaptureLocal returns the index of comp's first captured block, which CaptureReduced takes)
+  size_t CaptureLocal(CuUpdatableComponent& comp, void* stream);
+  void CaptureReduced(CuUpdatableComponent& comp, void* stream, size_t first);
   void DisarmCapture() { mCaptureArmed = false; }
   bool mCaptureArmed = false;
 
  private:
   size_t mStepRows = 0;
-  size_t mCaptureFirst = 0;
   std::vector<CapturedBlock> mCaptured;
 };
 

@@ -332,22 +332,23 @@ void HostExchange::GatherParams(CuUpdatableComponent& comp, int i, void* stream)
   }
 }
 
-void GradExchange::CaptureLocal(CuUpdatableComponent& comp, void* stream) {
-  if (!mCaptureArmed) return;
+size_t GradExchange::CaptureLocal(CuUpdatableComponent& comp, void* stream) {
+  const size_t first = mCaptured.size();
+  if (!mCaptureArmed) return first;
   TNET_HIP_CALL(hipStreamSynchronize((hipStream_t)stream));
-  mCaptureFirst = mCaptured.size();
   for (auto& b : comp.GradientBlocks()) {
     CapturedBlock c;
     c.local.resize((size_t)b.n);
     TNET_HIP_CALL(hipMemcpy(c.local.data(), b.grad, (size_t)b.n * sizeof(float), hipMemcpyDeviceToHost));
     mCaptured.push_back(std::move(c));
   }
+  return first;
 }
 
-void GradExchange::CaptureReduced(CuUpdatableComponent& comp, void* stream) {
+void GradExchange::CaptureReduced(CuUpdatableComponent& comp, void* stream, size_t first) {
   if (!mCaptureArmed) return;
   TNET_HIP_CALL(hipStreamSynchronize((hipStream_t)stream));
-  size_t k = mCaptureFirst;
+  size_t k = first;
   for (auto& b : comp.GradientBlocks()) {
     if (k >= mCaptured.size()) Error("GradExchange: capture out of step with the submitted blocks");
     std::vector<float> all((size_t)b.n);
@@ -365,9 +366,15 @@ void HostExchange::Submit(CuUpdatableComponent& comp) {
   CuDevice::Instantiate().KTCloseRun();  // no roofline timing run spans an exchange step
   CuDevice& dev = CuDevice::Instantiate();
   TNET_HIP_CALL(hipStreamSynchronize(dev.Stream()));
-  CaptureLocal(comp, dev.Stream());
+  const size_t first = CaptureLocal(comp, dev.Stream());
   for (auto& b : comp.GradientBlocks()) AllReduceDevice(b.grad, (size_t)b.n);
-  CaptureReduced(comp, dev.Stream());
+  CaptureReduced(comp, dev.Stream(), first);
+}
+
+bool HostExchange::SubmitInline(CuUpdatableComponent* const* comps, int n) {
+  if (mShard || n <= 0) return false;
+  for (int i = 0; i < n; ++i) Submit(*comps[i]);
+  return true;
 }
 
 void HostExchange::AllReduceDevice(float* buf, size_t n) {
@@ -506,7 +513,7 @@ void RcclExchange::Submit(CuUpdatableComponent& comp) {
   // the gradient kernels were enqueued on the compute stream: order the reduction after them
   TNET_HIP_CALL(hipEventRecord(ev, dev.Stream()));
   TNET_HIP_CALL(hipStreamWaitEvent(mImpl->comm_stream, ev, 0));
-  CaptureLocal(comp, mImpl->comm_stream);
+  const size_t first = CaptureLocal(comp, mImpl->comm_stream);
   std::vector<CuParamBlock> blocks = comp.GradientBlocks();
   NCCL_CALL(ncclGroupStart());
   for (auto& b : blocks) {
@@ -526,7 +533,29 @@ void RcclExchange::Submit(CuUpdatableComponent& comp) {
   NCCL_CALL(ncclGroupEnd());
   TNET_HIP_CALL(hipEventRecord(mImpl->ar_done[idx], mImpl->comm_stream));
   mImpl->ar_seq[idx] = ++mImpl->comm_seq;
-  CaptureReduced(comp, mImpl->comm_stream);
+  CaptureReduced(comp, mImpl->comm_stream, first);
+}
+
+// The step's whole reduction on the compute stream (GradExchange::SubmitInline): all-reduce only (the sharded form
+// keeps its per-layer reduce-scatter / apply / all-gather order on the comm stream), and only as the step's sole
+// submission -- so every collective of a step is on ONE stream (RCCL serialises a communicator's operations across
+// streams itself, but the exchange never relies on it: the synchronous AllReduceHost / AllReduceDevice drain both
+// streams around their comm-stream call).  No CU reservation: no GEMM runs beside these collectives.
+// TNET_DP_INLINE=0: the per-layer Submit path (A/B).
+bool RcclExchange::SubmitInline(CuUpdatableComponent* const* comps, int n) {
+  static const bool off = getenv("TNET_DP_INLINE") && getenv("TNET_DP_INLINE")[0] == '0';
+  if (off || mShard || n <= 0 || mImpl->next_event != 0) return false;
+  CuDevice::Instantiate().KTCloseRun();  // no roofline timing run spans an exchange step
+  const hipStream_t cs = CuDevice::Instantiate().Stream();
+  std::vector<size_t> first((size_t)n);
+  for (int i = 0; i < n; ++i) first[(size_t)i] = CaptureLocal(*comps[i], cs);
+  NCCL_CALL(ncclGroupStart());
+  for (int i = 0; i < n; ++i)
+    for (auto& b : comps[i]->GradientBlocks())
+      NCCL_CALL(ncclAllReduce(b.grad, b.grad, (size_t)b.n, ncclFloat, ncclSum, mImpl->comm, cs));
+  NCCL_CALL(ncclGroupEnd());
+  for (int i = 0; i < n; ++i) CaptureReduced(*comps[i], cs, first[(size_t)i]);
+  return true;
 }
 
 int RcclExchange::TransportRanks() const {
@@ -549,9 +578,11 @@ void RcclExchange::GatherParams(CuUpdatableComponent& comp, int i, void* stream)
     TNET_HIP_CALL(hipEventCreateWithFlags(&e, exchange_event_flags()));
     mImpl->gather_ev.push_back(e);
   }
-  hipEvent_t ev = mImpl->gather_ev[(size_t)i];
-  TNET_HIP_CALL(hipEventRecord(ev, stream ? (hipStream_t)stream : CuDevice::Instantiate().Stream()));
-  TNET_HIP_CALL(hipStreamWaitEvent(mImpl->comm_stream, ev, 0));
+  if ((hipStream_t)stream != mImpl->comm_stream) {  // applied on the comm stream: already in its order
+    hipEvent_t ev = mImpl->gather_ev[(size_t)i];
+    TNET_HIP_CALL(hipEventRecord(ev, stream ? (hipStream_t)stream : CuDevice::Instantiate().Stream()));
+    TNET_HIP_CALL(hipStreamWaitEvent(mImpl->comm_stream, ev, 0));
+  }
   NCCL_CALL(ncclGroupStart());
   for (auto& b : comp.GradientBlocks()) {
     const long c = ShardChunk(b.n, mWorld);
@@ -570,10 +601,20 @@ void RcclExchange::WaitFor(int i) {
   mImpl->compute_covered = std::max(mImpl->compute_covered, mImpl->ar_seq[(size_t)i]);
 }
 
+// A layer's apply goes on the comm stream right behind its own reduction (no hop: stream order), beside the
+// backward GEMMs still on the compute stream; the next reduction queues behind it, which costs nothing -- the next
+// layer's gradient takes a whole backward GEMM to exist.  The apply counts as comm-stream work, so a WaitFor on a
+// later reduction covers it and WaitAll joins only what no wait covered (the round-4 form, a separate apply stream
+// with a hop in per layer and a join out per step: TNET_DP_APPLY_COMM=0).
 void* RcclExchange::ApplyStream(int i) {
   static const bool off = getenv("TNET_DP_APPLY_STREAM") && getenv("TNET_DP_APPLY_STREAM")[0] == '0';
+  static const bool on_comm = !(getenv("TNET_DP_APPLY_COMM") && getenv("TNET_DP_APPLY_COMM")[0] == '0');
   if (off) return nullptr;  // A/B: the applies on the compute stream after WaitFor (round-1 form)
   if (i < 0 || (size_t)i >= mImpl->next_event) Error("RcclExchange::ApplyStream: no such reduction");
+  if (on_comm) {
+    ++mImpl->comm_seq;  // the apply the caller enqueues next
+    return (void*)mImpl->comm_stream;
+  }
   TNET_HIP_CALL(hipStreamWaitEvent(mImpl->apply_stream, mImpl->ar_done[(size_t)i], 0));
   mImpl->apply_covered = std::max(mImpl->apply_covered, mImpl->ar_seq[(size_t)i]);
   mImpl->applied = true;

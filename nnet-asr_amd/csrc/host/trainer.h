@@ -111,6 +111,9 @@ class HostExchange : public GradExchange {
   int Rank() const override { return mRank; }
   int WorldSize() const override { return mWorld; }
   void Submit(CuUpdatableComponent& comp) override;
+  /// Submit is synchronous: the whole step's reduction is simply every component's, in order (not under
+  /// TNET_DP_SHARD, whose applies and gathers go per layer)
+  bool SubmitInline(CuUpdatableComponent* const* comps, int n) override;
   void WaitAll() override { DisarmCapture(); }
   void AllReduceHost(double* v, int n) override;
   void AllReduceDevice(float* buf, size_t n);
@@ -143,6 +146,7 @@ class RcclExchange : public GradExchange {
   int Rank() const override { return mRank; }
   int WorldSize() const override { return mWorld; }
   void Submit(CuUpdatableComponent& comp) override;
+  bool SubmitInline(CuUpdatableComponent* const* comps, int n) override;
   void WaitAll() override;
   void WaitFor(int i) override;
   void* ApplyStream(int i) override;
