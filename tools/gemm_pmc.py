@@ -5,7 +5,9 @@ shapes and data distribution.
   ours   fwd only (1024 x 2048 x 2048, bias + sigmoid)
   layer  the bench's roofline kernel set: one 2048x2048 <biasedlinearity> layer's fwd (bias +
          sigmoid), bwd (diff-sigmoid) and fused SGD update per iteration, bunch 1024, exactly the
-         launches bench.py times (momentum 0, weight cost 0 -> no momentum buffer)
+         launches bench.py times (momentum 0, weight cost 0 -> no momentum buffer); as the step runs a
+         hidden layer since round 5, the update keeps the transposed shadow W^T and the backward reads
+         it (NN; TNET_BWD_SHADOW=0: the NT backward from W)
   torch  torch.mm on the fwd shape
 
 usage: python tools/gemm_pmc.py [ours|layer|torch] [iters]"""
@@ -47,13 +49,24 @@ elif which == "layer":
     slabs = lib().tnet_colsum_slabs(rows)
     Po = DeviceArray(slabs, ni)
     Pi = DeviceArray.from_numpy(np.zeros((slabs, no), np.float32))
+    shadow = os.environ.get("TNET_BWD_SHADOW", "2") != "0"
+    if shadow:
+        Wt = DeviceArray(no, ni)
+        check(lib().tnet_transpose(W.ptr, W.dim, Wt.ptr, Wt.stride, S))
+        check(lib().tnet_weight_shadow(W.ptr, W.dim, Wt.ptr, Wt.stride))
     for _ in range(iters):
         check(lib().tnet_affine_fwd(X.ptr, X.dim, W.ptr, W.dim, b.ptr, Y.ptr, Y.dim, 1, S))
-        check(lib().tnet_affine_bwd_colsum(E.ptr, E.dim, W.ptr, W.dim, X.ptr, X.stride, Eo.ptr, Eo.dim, Po.ptr,
-                                           Po.stride, S))
+        if shadow:
+            check(lib().tnet_affine_bwd_colsum_t(E.ptr, E.dim, Wt.ptr, Wt.dim, X.ptr, X.stride, Eo.ptr, Eo.dim,
+                                                 Po.ptr, Po.stride, S))
+        else:
+            check(lib().tnet_affine_bwd_colsum(E.ptr, E.dim, W.ptr, W.dim, X.ptr, X.stride, Eo.ptr, Eo.dim, Po.ptr,
+                                               Po.stride, S))
         check(lib().tnet_affine_update_bias(X.ptr, X.dim, E.ptr, E.dim, W.ptr, W.dim, None, 0, -1e-6, 0.0, 0.0,
                                             Pi.ptr, Pi.stride, b.ptr, None, S))
     check(lib().tnet_synchronize())
+    if shadow:
+        check(lib().tnet_weight_shadow(W.ptr, W.dim, None, 0))
 else:
     import torch
     torch.backends.cuda.matmul.allow_tf32 = False

@@ -2,7 +2,8 @@
 # GPU over the host transport, the RCCL path's exchange protocol) at 256 and 512 rows per rank (global bunch 2048 /
 # 4096), 5 seeds, newbob, two learning-rate rules (linear in the global bunch with a half-epoch warm-up; half of it);
 # and the one-rank data-parallel MLP3 step time at every bunch (the throughput side).
-# usage: bash tools/gpurun_batches/r5d.sh bench|256|512   (one gpurun call each: the whole set outlasts one call)
+# usage: bash tools/gpurun_batches/r5d.sh bench|256|512 [rules]   (one gpurun call each: the whole set outlasts one
+# call; rules default "lin half"; "n1" = the N = 1 recipe's lr 8 unscaled, "n1half" = lr 4)
 set -o pipefail
 mkdir -p gpurun_out
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
@@ -18,9 +19,12 @@ if [ "$1" = bench ]; then
   exit 0
 fi
 b=$1
-for rule in lin half; do
+rules=${2:-lin half}
+for rule in $rules; do
   if [ $b = 256 ]; then lr=2; else lr=4; fi
   if [ $rule = half ]; then lr=$(python3 -c "print($lr/2)"); fi
+  if [ $rule = n1 ]; then lr=1; fi          # x 8 ranks (--scale linear) = 8, the N = 1 recipe's lr
+  if [ $rule = n1half ]; then lr=0.5; fi
   for s in 1 2 3 4 5; do
     timeout -k 10 300 python3 -u tools/dp_accuracy.py --corpus ex01 --worlds 8 --bunch $b --lr $lr --scale linear \
       --warmup 0.5 --newbob --start-halving-inc 0.01 --end-halving-inc 0.001 --epochs 20 --cv-bunch 128 --seed $s \

@@ -34,8 +34,9 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # (round 4: the form parameter SP -- 0 the LDS ring, 3..9 the direct forms -- and the pair kernel's forms of its
 # update half and its backward half)
 FWD = re.compile(r"gemm16_kernel<64, 128, 64, 2, 2, 2, \d+, true, false, 2(, (true|false))?>")    # bias + sigmoid
-BWD = re.compile(r"gemm16_kernel<64, 128, 64, 2, 2, 2, \d+, true, true, 8(, (true|false))?>")     # diff-sigmoid + sums
-PAIR = re.compile(r"gemm16_pair_kernel<128, 128, false, false, 9, (true|false), 64, 128, true, true, 8, true(, \d+)*>")
+# (round 5: the backward from the transposed weight shadow is NN -- B n-contiguous -- in both)
+BWD = re.compile(r"gemm16_kernel<64, 128, 64, 2, 2, 2, \d+, true, (true|false), 8(, (true|false))?>")  # diff-sigmoid + sums
+PAIR = re.compile(r"gemm16_pair_kernel<128, 128, false, false, 9, (true|false), 64, 128, true, (true|false), 8, true(, \d+)*>")
 UPD = re.compile(r"gemm16_kernel<128, 128, 64, 2, 2, 2, \d+, false, false, 9(, (true|false))?>")  # SGD + bias SGD
 
 
