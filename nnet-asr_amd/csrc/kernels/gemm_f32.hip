@@ -2872,7 +2872,9 @@ static int launch_gemm(const GemmP& p_in, hipStream_t st) {
   }
   int rcfg = cfg;
   if (g_direct > 0 && forced_cfg() < 0 && !B_KC) {
-    if (cfg == CFG_m64x128k64s2) rcfg = g_direct == 2 ? CFG_m64x128d4 : g_direct == 3 ? CFG_m64x128a4 : CFG_m64x128a8;
+    // (short K -- the first layer's 440: the 4-chunk ring's shorter prologue, 19.6 vs 20.9 us, tools/gemm_sweep.py r5o)
+    if (cfg == CFG_m64x128k64s2)
+      rcfg = g_direct == 2 ? CFG_m64x128d4 : (g_direct == 3 || p.K <= 512) ? CFG_m64x128a4 : CFG_m64x128a8;
     else if (cfg == CFG_m128x128k64s2) rcfg = g_direct == 2 ? CFG_m128x128d4 : CFG_m128x128a4;
     else if (cfg == CFG_m128x256k32s3 && g_direct == 4) rcfg = CFG_m128x256a2;  // 4: 1 + the 128x256 update
   }
