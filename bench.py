@@ -148,6 +148,32 @@ def dp_mode(world):
     return (" (RCCL reduce-scatter, sharded SGD apply, all-gather)" if shard else " (RCCL all-reduce)")
 
 
+def prewarm_steps(ms, dims, bunch):
+    """Training steps of the same network shape on a SCRATCH network, objective, trainer and 8-bunch synthetic cache
+    (seeds of their own, no exchange), for `ms` of wall time, synchronised every 8 steps: the GPU meets the step's
+    own kernel and memory-traffic mix before the warm-up steps (the GEMM-only prewarm left the 20 / 5 window 1-2 %
+    under the steady state: profiles/r05_prewarm_ab.json).  Nothing of the measured run's state is touched.
+    Returns the time spent (ms)."""
+    if ms <= 0:
+        return 0.0
+    net = build_network(dims, seed=7)
+    net.set_learn_rate(0.008)
+    net.set_grad_div_frm(True)
+    obj = Objective()
+    cache = 8 * bunch
+    tr = Trainer(net, obj, bunchsize=bunch, cachesize=cache, seed=99, randomize=True)
+    X, L = synth_frames(cache, dims[0], dims[-1], seed=4242)
+    if lib().tnet_trainer_prefill(tr.h, X.ctypes.data, X.shape[0], X.shape[1], X.shape[1], L.ctypes.data) != cache:
+        raise SystemExit("prewarm: prefill took a partial cache")
+    t0 = time.perf_counter()
+    while (time.perf_counter() - t0) * 1e3 < ms:
+        tr.replay(8)
+        tnet_amd.synchronize()
+    spent = (time.perf_counter() - t0) * 1e3
+    del tr, obj, net, X, L
+    return spent
+
+
 def prewarm(ms):
     """Scratch GEMMs of the step's own 2048^2 shape on the library stream for `ms` of wall time (synchronised
     every 8 launches), on buffers of their own: the GPU leaves its idle clock state before the warm-up steps,
@@ -248,6 +274,9 @@ def main():
                          "and settles at 1.01 ms only after ~20 ms of load (profiles/r04_warmup_trace.json), longer "
                          "than a 5-step warm-up (20 / 5 window: 966-982 k without, 994-999 k at 40 ms, 1.007-1.009 M "
                          "at 200 ms; 100 / 20: 1.020 M -- profiles/r04_prewarm_ab.json); 0: off")
+    ap.add_argument("--prewarm-form", default="steps", choices=["steps", "gemm"],
+                    help="steps: training steps of the same shape on a scratch network / trainer (the step's own "
+                         "kernel and traffic mix); gemm: the round-4 scratch 2048^2 GEMMs")
     ap.add_argument("--rccl-check-shard", type=int, default=1,
                     help="N > 1 over RCCL: also check the sharded exchange form on a second communicator (0: off)")
     ap.add_argument("--breakdown-steps", type=int, default=20,
@@ -312,7 +341,8 @@ def main():
         if dist is not None:
             dist.barrier()
 
-    prewarm_ms = prewarm(args.prewarm_ms)
+    prewarm_ms = (prewarm_steps(args.prewarm_ms, dims, B) if args.prewarm_form == "steps" else
+                  prewarm(args.prewarm_ms))
     trainer.replay(args.warmup)
     barrier()
     # timed region: K steps, no events on the stream (value, ms_per_step)
@@ -417,9 +447,12 @@ def main():
                        f"training frames/sec (whole node), {'x'.join(map(str, dims))} MLP"),
             "value": round(value, 1), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
-            "prewarm": {"ms": round(prewarm_ms, 1), "what": "scratch 1024x2048x2048 GEMMs before the warm-up steps "
-                        "(no training state touched): the GPU out of its idle clock state, whose ramp outlasts a "
-                        "5-step warm-up (profiles/r04_warmup_trace.json)"},
+            "prewarm": {"ms": round(prewarm_ms, 1), "form": args.prewarm_form,
+                        "what": ("training steps of the same shape on a scratch network / trainer / cache"
+                                 if args.prewarm_form == "steps" else "scratch 1024x2048x2048 GEMMs") +
+                        " before the warm-up steps (no state of the measured run touched): the GPU out of its idle "
+                        "clock state, whose ramp outlasts a 5-step warm-up (profiles/r04_warmup_trace.json, "
+                        "profiles/r05_prewarm_ab.json); --prewarm-ms 0 reports the cold window"},
             "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
             "config": {"workload": f"TNet SGD step, {'x'.join(map(str, dims))} sigmoid MLP + softmax xent",
                        "bunch_per_gpu": B, "global_bunch": B * world, "frames_resident_per_gpu": args.cache,
