@@ -2211,17 +2211,28 @@ __global__ __launch_bounds__(kSxThreads) void affine_softmax_xent_kernel(
 #pragma unroll
     for (int e = 0; e < 4; ++e) bv[k][e] = c + e < N ? p.bias[c + e] : 0.f;
   }
-  for (int z = 1; z < splits; ++z) {
-    f32x4 t[kSxPer];
+  // the other slices: up to kSxBatch of them requested before the first add (one memory round trip instead of
+  // one per slice: the planner gives this kernel 2 slices at MLP3's 1024 x 1024 -> 135), added in slice order
+  constexpr int kSxBatch = 4;
+  for (int z0 = 1; z0 < splits; z0 += kSxBatch) {
+    f32x4 t[kSxBatch][kSxPer];
 #pragma unroll
-    for (int k = 0; k < kSxPer; ++k) {
-      const int i = min(tid + kSxThreads * k, n - 1), r = i / N4, c = (i % N4) * 4;
-      t[k] = *reinterpret_cast<const f32x4*>(P + (long)z * slab + (long)(r0 + r) * ldp + c);
+    for (int b = 0; b < kSxBatch; ++b) {
+      const int z = min(z0 + b, splits - 1);
+#pragma unroll
+      for (int k = 0; k < kSxPer; ++k) {
+        const int i = min(tid + kSxThreads * k, n - 1), r = i / N4, c = (i % N4) * 4;
+        t[b][k] = *reinterpret_cast<const f32x4*>(P + (long)z * slab + (long)(r0 + r) * ldp + c);
+      }
     }
 #pragma unroll
-    for (int k = 0; k < kSxPer; ++k)
+    for (int b = 0; b < kSxBatch; ++b) {
+      if (z0 + b >= splits) break;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) v[k][e] = v[k][e] + t[k][e];
+      for (int k = 0; k < kSxPer; ++k)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[k][e] = v[k][e] + t[b][k][e];
+    }
   }
 #pragma unroll
   for (int k = 0; k < kSxPer; ++k) {
@@ -2379,7 +2390,8 @@ static unsigned* splitk_counters(size_t n, hipStream_t st) {
   X(m128x256k32s3, 1, 128, 256, 32, 2, 2, 3, 0)         \
   X(m64x64k64s2, 1, 64, 64, 64, 2, 2, 2, 0)             \
   X(m64x64k32s4, 1, 64, 64, 32, 2, 2, 4, 0)             \
-  X(m32x64k64s2, 1, 32, 64, 64, 2, 2, 2, 0)
+  X(m32x64k64s2, 1, 32, 64, 64, 2, 2, 2, 0)             \
+  X(m64x64a4, 1, 64, 64, 64, 2, 2, 2, 5)
 
 enum GemmCfg {
 #define X(name, ...) CFG_##name,

@@ -40,7 +40,7 @@ GEMM_CFGS = ["auto", "g64x64k32s4w4", "m64x128k32s4", "m64x128k64s3", "m64x64k32
              "m64x64k64s2", "m64x64k32s4", "m32x64k64s2",
              # the direct form (fragments loaded into a register ring, no LDS ring; exact shapes only,
              # the ring form otherwise)
-             "m64x128d4", "m64x128d8", "m128x128d4", "m64x128a4", "m64x128a8", "m128x128a4", "m128x256a2",
+             "m64x128d4", "m64x128d8", "m128x128d4", "m64x128a4", "m64x128a8", "m128x128a4", "m128x256a2", "m64x64a4",
              # ... with the k-contiguous operands' loads coalesced and the fragments moved by ds_bpermute
              "m64x128c8", "m64x128c4",
              # split-K (K cut into slices + an in-order combine with the epilogue); counts that do not
