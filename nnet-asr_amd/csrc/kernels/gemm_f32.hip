@@ -2097,15 +2097,24 @@ void gemm16_upd_gather_kernel(const GemmP pa, const GemmP pb, const int na, cons
 // tiles (one round over the CUs), then the small update's tiles and the gather blocks, which take the CUs as the
 // big grid's tail drains instead of after a kernel boundary.  Each half runs its separate launch's body: the
 // results are bit-identical to the two calls.
+// BD: B's tiles in the 64x64 direct form (m64x64a4, what tnet_affine_update_bias runs for B's shape then), else the
+// 64x64 ring form with 16x64 wave tiles (m64x64k32s4w41)
+template <bool BD>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
 void gemm16_upd_mixed_gather_kernel(const GemmP pa, const GemmP pb, const int na, const int nb, const BunchGatherP g) {
   constexpr int SA = gemm16_smem_floats<128, 128, 64, 2, EPI_SGD_B, true>();
-  constexpr int SB = gemm16_smem_floats<64, 64, 32, 4, EPI_SGD_B, false>();
+  constexpr int SB = BD ? gemm16_smem_floats<64, 64, 64, 2, EPI_SGD_B, false>()
+                        : gemm16_smem_floats<64, 64, 32, 4, EPI_SGD_B, false>();
   __shared__ __attribute__((aligned(16))) float smem[SA > SB ? SA : SB];
   const int b = blockIdx.x;
-  if (b < na) gemm16_body<128, 128, 64, 2, 2, 2, 5, false, false, EPI_SGD_B, true>(pa, smem, b);
-  else if (b < na + nb) gemm16_body<64, 64, 32, 4, 1, 4, 0, false, false, EPI_SGD_B, false>(pb, smem, b - na);
-  else bunch_gather_block(g, b - na - nb, (int)gridDim.x - na - nb);
+  if (b < na) {
+    gemm16_body<128, 128, 64, 2, 2, 2, 5, false, false, EPI_SGD_B, true>(pa, smem, b);
+  } else if (b < na + nb) {
+    if constexpr (BD) gemm16_body<64, 64, 64, 2, 2, 2, 5, false, false, EPI_SGD_B, false>(pb, smem, b - na);
+    else gemm16_body<64, 64, 32, 4, 1, 4, 0, false, false, EPI_SGD_B, false>(pb, smem, b - na);
+  } else {
+    bunch_gather_block(g, b - na - nb, (int)gridDim.x - na - nb);
+  }
 }
 
 // tnet_affine_bwd_colsum_slabs: the top layer's backward GEMM (64x128 NT + diff-sigmoid + Eo's slab sums,
@@ -2447,6 +2456,7 @@ extern "C" int tnetk_top_rows(const float* X, long ldx, const float* W, long ldw
                               const int* labels, float* Z, long ldz, float* Y, long ldy, float* E, long lde,
                               double* stats, float* cpart, long ldcp, int v4, int logits_only, void* stream);
 static int forced_cfg();
+static bool upd64_direct(const GemmP& p);
 static bool top_rows_ok(const GemmP& p) {
   return forced_cfg() < 0 && g_split <= 0 && tnetk_top_rows_ok(p.A, p.lda, p.B, p.ldb, p.M, p.N, p.K);
 }
@@ -2891,6 +2901,8 @@ static int launch_gemm(const GemmP& p_in, hipStream_t st) {
     else if (cfg == CFG_m128x256k32s3 && g_direct == 4) rcfg = CFG_m128x256a2;  // 4: 1 + the 128x256 update
   }
   if (g_kc >= 2 && forced_cfg() < 0 && A_KC && B_KC && cfg == CFG_m64x128k64s2) rcfg = CFG_m64x128c8;
+  if constexpr (!A_KC && !B_KC && (EPI == EPI_SGD_B || EPI == EPI_SGD))
+    if (forced_cfg() < 0 && cfg == CFG_m64x64k32s4w41 && upd64_direct(p)) rcfg = CFG_m64x64a4;
   bool ok = false;
   switch (rcfg) {
 #define X(name, KIND, BM, BN, BK, WM, WN, S, IL) \
@@ -3525,6 +3537,20 @@ extern "C" int tnet_affine_update_bias_pair(const float* X, TnetMatrixDim dX, co
   return shadow_done(pb, rc);
 }
 
+// An update GEMM (TN, SGD epilogue) the planner gives 64x64 tiles runs in the 64x64 direct form where those tiles
+// fill ~a round of the CUs (the first layer's 440x2048 over K = 1024, 224 tiles: 21.9 vs 24.3 us; MLP3's 598x1024,
+// 160 tiles, is slower direct: 26.6 vs 23.5 -- tools/gemm_sweep.py, profiles/r05_gemm_sweep_small_k.txt) and the
+// direct-form conditions hold (launch_cfg's; TNET_UPD64_DIRECT=0: never)
+namespace tnetk {
+static bool upd64_direct(const GemmP& p) {
+  static const bool on = !(getenv("TNET_UPD64_DIRECT") && getenv("TNET_UPD64_DIRECT")[0] == '0');
+  auto a16p = [](const void* v) { return ((uintptr_t)v & 15) == 0; };
+  return on && g_direct > 0 && p.ksplit <= 1 && (long)cdiv(p.M, 64) * cdiv(p.N, 64) >= 200 && p.K / 64 >= 1 &&
+         p.M % 4 == 0 && p.N % 4 == 0 && !(p.lda & 3) && !(p.ldb & 3) && a16p(p.A) && a16p(p.B) &&
+         4 * ((long)p.K * p.lda) < (1L << 31) && 4 * ((long)p.K * p.ldb) < (1L << 31);
+}
+}  // namespace tnetk
+
 // gemm16_upd_mixed_gather_kernel's conditions (TNET_UPD_MIXED=0: never): A is what tnet_affine_update_bias runs as
 // m128x128a4 with the exact prefetch (the planner's m128x128k64s2, unsplit, the direct-form conditions, PX), B what
 // it runs as m64x64k32s4w41 unsplit; no CUs reserved
@@ -3604,7 +3630,8 @@ extern "C" int tnet_affine_update_bias_gather(const float* X, TnetMatrixDim dX, 
     pa.early_issue = pb.early_issue = g_early;
     pa.wt = pb.wt = g_wt;
     BunchGatherP g{y, x, labels_out, labels_in, copy_from, dy.rows, c4, dy.stride, dx.stride};
-    gemm16_upd_mixed_gather_kernel<<<na + nb + ng, 256, 0, (hipStream_t)stream>>>(pa, pb, na, nb, g);
+    if (upd64_direct(pb)) gemm16_upd_mixed_gather_kernel<true><<<na + nb + ng, 256, 0, (hipStream_t)stream>>>(pa, pb, na, nb, g);
+    else gemm16_upd_mixed_gather_kernel<false><<<na + nb + ng, 256, 0, (hipStream_t)stream>>>(pa, pb, na, nb, g);
     TNET_LAUNCH_CHECK();
     shadow_done(pa, TNET_OK);
     return shadow_done(pb, TNET_OK);
