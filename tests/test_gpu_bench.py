@@ -89,3 +89,21 @@ def test_bench_force_dp_reduction_check(shard):
     assert c["ok"] and c["ranks"] == 1 and c["transport_ranks"] == 1 and list(c["modes"]) == [mode]
     assert c["max_rel_err"] == 0.0 and c["modes"][mode]["blocks"] == 10
     assert c["librccl"] and "rccl" in c["librccl"]
+
+
+@pytest.mark.parametrize("config", ["mlp3", "dnn4"])
+def test_dp_exchange_schedules_bit_identical(config):
+    """the round-5 exchange schedule (MLP3: the whole reduction inline on the compute stream + one merged apply;
+    dnn4: each apply on the comm stream behind its reduction) and the round-4 one (TNET_DP_INLINE=0
+    TNET_DP_APPLY_COMM=0: per-layer submissions, applies on their own stream) train the same parameters bit for bit
+    (only the streams and launch grouping differ, never the arithmetic)"""
+    cmd = [sys.executable, "bench.py", "--config", config, "--steps", "3", "--warmup", "1", "--no-cpu-baseline",
+           "--cache", "4096", "--force-dp", "--kernel-timing", "0", "--breakdown-steps", "0", "--prewarm-ms", "0"]
+    sha = []
+    for env in ({}, {"TNET_DP_INLINE": "0", "TNET_DP_APPLY_COMM": "0"}):
+        p = subprocess.run(cmd, cwd=REPO, capture_output=True, text=True, timeout=300, env=dict(os.environ, **env))
+        assert p.returncode == 0, p.stderr[-3000:]
+        d = _line(p.stdout)
+        assert d["rccl_check"]["ok"]
+        sha.append(d["replica_check"]["param_sha256_16"])
+    assert sha[0] == sha[1]
