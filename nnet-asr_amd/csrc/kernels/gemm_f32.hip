@@ -2007,14 +2007,15 @@ void gemm16_kernel(const GemmP p_in) {
 // workgroups start on the CUs A's finish on -- B's operand fill overlaps A's epilogue stores and tail
 // instead of waiting for a kernel boundary, A's end-of-kernel drain and B's start-up spread.
 // SPA: GEMM A's form (0: the LDS ring, 5: the direct form -- TNET_GEMM_DIRECT); SPB: GEMM B's (0, or 8: the
-// direct form with coalesced k-contiguous loads -- TNET_GEMM_KC)
+// direct form with coalesced k-contiguous loads -- TNET_GEMM_KC); KTA / STA: GEMM A's k-tile and slot count (the
+// top layer's 128x256 update: 32 / 3, its m128x256a2 form)
 template <int BMA, int BNA, bool AKA, bool BKA, int EPIA, bool PXA, int BMB, int BNB, bool AKB, bool BKB, int EPIB,
-          bool PXB, int SPA = 0, int SPB = 0>
+          bool PXB, int SPA = 0, int SPB = 0, int KTA = 64, int STA = 2>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
 void gemm16_pair_kernel(const GemmP pa, const GemmP pb, const int na) {
-  constexpr int SA = gemm16_smem_floats<BMA, BNA, 64, 2, EPIA, PXA>(), SB = gemm16_smem_floats<BMB, BNB, 64, 2, EPIB, PXB>();
+  constexpr int SA = gemm16_smem_floats<BMA, BNA, KTA, STA, EPIA, PXA>(), SB = gemm16_smem_floats<BMB, BNB, 64, 2, EPIB, PXB>();
   __shared__ __attribute__((aligned(16))) float smem[SA > SB ? SA : SB];
-  if ((int)blockIdx.x < na) gemm16_body<BMA, BNA, 64, 2, 2, 2, SPA, AKA, BKA, EPIA, PXA>(pa, smem, blockIdx.x);
+  if ((int)blockIdx.x < na) gemm16_body<BMA, BNA, KTA, 2, 2, STA, SPA, AKA, BKA, EPIA, PXA>(pa, smem, blockIdx.x);
   else gemm16_body<BMB, BNB, 64, 2, 2, 2, SPB, AKB, BKB, EPIB, PXB>(pb, smem, (int)blockIdx.x - na);
 }
 
@@ -2938,6 +2939,35 @@ static void pair_go(const GemmP& pu, const GemmP& pb, int na, int nb, bool kc, i
         <<<na + nb, 256, 0, st>>>(pu, pb, na);
 }
 
+// The top layer's update (128x256 tiles, the m128x256a2 direct form tnet_affine_update_bias runs for it) with the
+// backward of the layer below from its transposed shadow (64x128 NN, m64x128a8) as ONE launch: the backward's
+// workgroups start on the CUs the update's tiles leave instead of after a kernel boundary (TNET_PAIR_WIDE=0: the
+// two launches).  Only where both run those direct forms alone; otherwise TNET_ERR_UNSUPPORTED.
+static int launch_pair_wide_bwd_t(GemmP pu, GemmP pb, hipStream_t st) {
+  static const bool on = !(getenv("TNET_PAIR_WIDE") && getenv("TNET_PAIR_WIDE")[0] == '0');
+  if (!on || g_direct != 4 || g_reserve > 0) return TNET_ERR_UNSUPPORTED;
+  if ((long)cdiv(pb.M, 64) * cdiv(pb.N, 128) < 200) return TNET_ERR_UNSUPPORTED;  // launch_colsum_bwd_t's 64x128 rule
+  auto a16p = [](const void* v) { return ((uintptr_t)v & 15) == 0; };
+  // A: launch_cfg's direct-form conditions for m128x256a2 (BK 32) and its 32-bit tile offsets
+  const bool dir_a = pu.K / 32 >= 1 && pu.M % 4 == 0 && pu.N % 4 == 0 && !(pu.lda & 3) && !(pu.ldb & 3) &&
+                     a16p(pu.A) && a16p(pu.B) && 4 * ((long)pu.K * pu.lda) < (1L << 31) &&
+                     4 * ((long)pu.K * pu.ldb) < (1L << 31) && 4 * (32L * pu.lda + pu.M) < (1L << 32) &&
+                     4 * (32L * pu.ldb + pu.N) < (1L << 32);
+  // B: the NN backward's direct form (launch_colsum_bwd_t's m64x128a8: an even count of whole 64-k tiles)
+  const bool dir_b = pb.K / 64 >= 1 && (pb.K / 64) % 2 == 0 && pb.N % 4 == 0 && !(pb.lda & 3) && !(pb.ldb & 3) &&
+                     a16p(pb.A) && a16p(pb.B) && 4 * ((long)pb.M * pb.lda) < (1L << 31) &&
+                     4 * ((long)pb.K * pb.ldb) < (1L << 31) && 4 * (64L * pb.ldb + pb.N) < (1L << 32);
+  if (!dir_a || !dir_b || !px_exact<64, 128, EPI_DSIG_CS>(pb)) return TNET_ERR_UNSUPPORTED;
+  pu.group = pb.group = g_group > 0 ? g_group : 8;
+  pu.early_issue = pb.early_issue = g_early;
+  pu.wt = pb.wt = g_wt;
+  const int na = cdiv(pu.M, 128) * cdiv(pu.N, 256), nb = cdiv(pb.M, 64) * cdiv(pb.N, 128);
+  gemm16_pair_kernel<128, 256, false, false, EPI_SGD_B, false, 64, 128, true, false, EPI_DSIG_CS, true, 7, 6, 32, 3>
+      <<<na + nb, 256, 0, st>>>(pu, pb, na);
+  TNET_LAUNCH_CHECK();
+  return TNET_OK;
+}
+
 template <int EPIA>
 static int launch_pair_a_bwd(GemmP pu, GemmP pb, hipStream_t st, bool bwd_t = false) {
   // EPI_STORE_BG (the data-parallel gradient): not while CUs are reserved for RCCL (the exchange window runs the
@@ -2946,6 +2976,8 @@ static int launch_pair_a_bwd(GemmP pu, GemmP pb, hipStream_t st, bool bwd_t = fa
   if (forced_cfg() >= 0 || !g_pair) return TNET_ERR_UNSUPPORTED;
   if (pu.M <= 0 || pu.N <= 0 || pb.M <= 0 || pb.N <= 0) return TNET_ERR_UNSUPPORTED;
   const GemmPlan pl = plan_gemm<false>(pu, true);
+  if (EPIA == EPI_SGD_B && bwd_t && pl.cfg == CFG_m128x256k32s3 && pl.ks == 1)
+    return launch_pair_wide_bwd_t(pu, pb, st);
   if (pl.cfg != CFG_m128x128k64s2 || pl.ks != 1) return TNET_ERR_UNSUPPORTED;
   if ((long)cdiv(pb.M, 64) * cdiv(pb.N, 128) < 200) return TNET_ERR_UNSUPPORTED;  // launch_colsum_bwd's 64x128 rule
   pu.group = pb.group = g_group > 0 ? g_group : 8;

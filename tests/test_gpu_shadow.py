@@ -185,6 +185,50 @@ def test_update_bwd_pair_t(mmt):
     assert np.all(np.abs(res["t"]["P2"] - res["nt"]["P2"]) <= 32 * 1.2e-7 * slab_sums(np.abs(O)) + 1e-7)
 
 
+@pytest.mark.parametrize("mmt,shadow_top", [(0.0, False), (0.9, False), (0.0, True)])
+def test_update_bwd_pair_t_wide(mmt, shadow_top):
+    """the top layer's 2048x4000 update (128x256 tiles) paired with the 2048^2 backward below it from that layer's
+    shadow (one launch, launch_pair_wide_bwd_t): W, b, the momentum buffers, Eo and the slab sums identical to the
+    two separate calls (tnet_affine_update_bias + tnet_affine_bwd_colsum_t); with the top layer's own shadow
+    registered its Wt == the new W^T"""
+    rows, n_in, n_out, n_below = 1024, 2048, 4000, 2048
+    X, E = rnd((rows, n_in), 41), rnd((rows, n_out), 42, 0.01)
+    W, corr = rnd((n_in, n_out), 43, 0.1), rnd((n_in, n_out), 44, 0.01)
+    b, corr_b = rnd(n_out, 45), rnd(n_out, 46, 0.01)
+    P = slab_sums(E).astype(np.float32)
+    W2, E2 = rnd((n_below, n_in), 47, 0.1), rnd((rows, n_in), 48)
+    Yb = (1 / (1 + np.exp(-rnd((rows, n_below), 49)))).astype(np.float32)
+    scale, l2 = -0.3 / rows, -1e-4
+    slabs = lib().tnet_colsum_slabs(rows)
+    res = {}
+    for form in ("pair", "separate"):
+        d = dict(X=DeviceArray.from_numpy(X), E=DeviceArray.from_numpy(E), W=DeviceArray.from_numpy(W),
+                 P=DeviceArray.from_numpy(P), b=DeviceArray.vector(b),
+                 C=DeviceArray.from_numpy(corr) if mmt else None, Cb=DeviceArray.vector(corr_b) if mmt else None,
+                 W2=DeviceArray.from_numpy(W2), E2=DeviceArray.from_numpy(E2), Y=DeviceArray.from_numpy(Yb),
+                 O=DeviceArray(rows, n_below), P2=DeviceArray.from_numpy(np.full((slabs, n_below), np.nan, np.float32)))
+        C, Cb = d["C"], d["Cb"]
+        dT = _register(d["W"]) if shadow_top else None
+        w2t = transposed(d["W2"])
+        upd = (d["X"].ptr, d["X"].dim, d["E"].ptr, d["E"].dim, d["W"].ptr, d["W"].dim, C.ptr if C else None,
+               C.stride if C else 0, scale, mmt, l2, d["P"].ptr, d["P"].stride, d["b"].ptr, Cb.ptr if Cb else None)
+        bwd = (d["E2"].ptr, d["E2"].dim, w2t.ptr, w2t.dim, d["Y"].ptr, d["Y"].stride, d["O"].ptr, d["O"].dim,
+               d["P2"].ptr, d["P2"].stride)
+        if form == "pair":
+            check(lib().tnet_affine_update_bwd_pair_t(*upd, *bwd, S()))
+        else:
+            check(lib().tnet_affine_update_bias(*upd, S()))
+            check(lib().tnet_affine_bwd_colsum_t(*bwd, S()))
+        synchronize()
+        if shadow_top:
+            if lib().tnet_weight_shadow_kept(d["W"].ptr) == 1:
+                np.testing.assert_array_equal(dT.numpy(), d["W"].numpy().T)
+            _unregister(d["W"])
+        res[form] = {k: v.numpy() for k, v in d.items() if v is not None and k in ("W", "b", "C", "Cb", "O", "P2")}
+    for k in res["pair"]:
+        np.testing.assert_array_equal(res["pair"][k], res["separate"][k], err_msg=k)
+
+
 def test_shadow_arguments():
     dW = DeviceArray(64, 32)
     dT = DeviceArray(32, 64)
