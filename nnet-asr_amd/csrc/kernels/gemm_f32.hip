@@ -2455,9 +2455,32 @@ static int g_wt = 1;  // TNET_GEMM_WT=0: plain 16-B epilogue stores instead of w
 extern "C" int tnetk_top_rows_ok(const float* X, long ldx, const float* W, long ldw, int M, int N, int K);
 extern "C" int tnetk_top_rows(const float* X, long ldx, const float* W, long ldw, const float* b, int M, int N, int K,
                               const int* labels, float* Z, long ldz, float* Y, long ldy, float* E, long lde,
-                              double* stats, float* cpart, long ldcp, int v4, int logits_only, void* stream);
+                              double* stats, float* cpart, long ldcp, int v4, int logits_only, float* part,
+                              long ldpart, void* stream);
+extern "C" int tnetk_top_rows_shape_ok(const float* X, long ldx, const float* W, long ldw, int M, int N, int K);
 static int forced_cfg();
 static bool upd64_direct(const GemmP& p);
+// The narrow top layer's K slices from top_rows.hip's row-block kernel (16-row blocks x 4 K slices = 256
+// workgroups, operands straight into registers, no in-launch combine) into the split-K workspace [4][M][ldp], for
+// the second launch that combines them -- affine_softmax_xent_kernel (tnet_affine_softmax_xent) or
+// splitk_reduce_kernel (tnet_affine_fwd: the same slices, so both give the same Z) -- instead of the 32x64 split-K
+// tiles (TNET_TOP_SPLIT=0: those)
+constexpr int kTopSlices = 4;
+static float* splitk_workspace(size_t bytes, hipStream_t st);
+static bool top_split_ok(const GemmP& p) {
+  static const bool on = !(getenv("TNET_TOP_SPLIT") && getenv("TNET_TOP_SPLIT")[0] == '0');
+  return on && forced_cfg() < 0 && g_split <= 0 && tnetk_top_rows_shape_ok(p.A, p.lda, p.B, p.ldb, p.M, p.N, p.K);
+}
+static float* top_split_partials(const GemmP& p, hipStream_t st, int* ldp_out) {
+  const int ldp = 16 * ((p.N + 15) / 16);
+  float* ws = splitk_workspace(sizeof(float) * kTopSlices * (size_t)p.M * ldp, st);
+  if (!ws) return nullptr;
+  if (tnetk_top_rows(p.A, p.lda, p.B, p.ldb, nullptr, p.M, p.N, p.K, nullptr, nullptr, 0, nullptr, 0, nullptr, 0,
+                     nullptr, nullptr, 0, 0, 2, ws, ldp, st) != TNET_OK)
+    return nullptr;
+  *ldp_out = ldp;
+  return ws;
+}
 static bool top_rows_ok(const GemmP& p) {
   return forced_cfg() < 0 && g_split <= 0 && tnetk_top_rows_ok(p.A, p.lda, p.B, p.ldb, p.M, p.N, p.K);
 }
@@ -3101,7 +3124,16 @@ extern "C" int tnet_affine_fwd(const float* X, TnetMatrixDim dX, const float* W,
   // a narrow top layer (the logits of tnet_affine_softmax_xent's row-block kernel, so both give the same Z)
   if (act == 0 && top_rows_ok(p))
     return tnetk_top_rows(X, dX.stride, W, dW.stride, b, p.M, p.N, p.K, nullptr, Y, dY.stride, nullptr, 0, nullptr, 0,
-                          nullptr, nullptr, 0, 0, 1, stream);
+                          nullptr, nullptr, 0, 0, 1, nullptr, 0, stream);
+  if (act == 0 && top_split_ok(p)) {  // the same slices as tnet_affine_softmax_xent, combined by splitk_reduce_kernel
+    int ldp = 0;
+    if (float* ws = top_split_partials(p, (hipStream_t)stream, &ldp)) {
+      const unsigned g = (unsigned)cdiv((long)p.M * ((p.N + 3) / 4), 256);
+      splitk_reduce_kernel<EPI_BIAS><<<g, 256, 0, (hipStream_t)stream>>>(p, ws, (long)p.M * ldp, kTopSlices, ldp, g);
+      TNET_LAUNCH_CHECK();
+      return TNET_OK;
+    }
+  }
   switch (act) {
     case 1: return launch_gemm<true, false, EPI_BIAS_SIG>(p, (hipStream_t)stream);
     case 2: return launch_gemm<true, false, EPI_BIAS_NEG>(p, (hipStream_t)stream);
@@ -3167,7 +3199,17 @@ extern "C" int tnet_affine_softmax_xent(const float* X, TnetMatrixDim dX, const 
                  (!Y || (aligned16(Y) && (strideY & 3) == 0)) && aligned16(E) && (strideE & 3) == 0;
   if (top_rows_ok(p))  // up to 144 classes over K in [512, 1024]: one launch (top_rows.hip)
     return tnetk_top_rows(X, dX.stride, W, dW.stride, b, p.M, p.N, p.K, labels, Z, strideZ, Y, strideY, E, strideE,
-                          stats, colpart, ldcolpart, v4, 0, stream);
+                          stats, colpart, ldcolpart, v4, 0, nullptr, 0, stream);
+  if (top_split_ok(p)) {  // the row-block kernel's 4 K slices, then this kernel's combine + softmax launch
+    int ldp = 0;
+    if (float* ws = top_split_partials(p, s, &ldp)) {
+      affine_softmax_xent_kernel<<<(unsigned)cdiv(p.M, kColsumSlabRows), kSxThreads, 0, s>>>(
+          p, ws, (long)p.M * ldp, kTopSlices, ldp, labels, Z, strideZ, Y, strideY, E, strideE, stats, colpart,
+          ldcolpart, v4);
+      TNET_LAUNCH_CHECK();
+      return TNET_OK;
+    }
+  }
   const GemmPlan pl = plan_gemm<true>(p, true);
   int cfg = pl.cfg, bm, bn, kind;
   cfg_shape(cfg, &bm, &bn, &kind);

@@ -60,7 +60,9 @@ struct TopRowsP {
   double* stats;
   float* cpart;
   long ldcp;
-  int v4, logits_only;
+  int v4, logits_only;  // 2: the K slices' partial products only (row-major into part), no combine
+  float* part;          // [kSlices][M][ldpart] (logits_only 2)
+  long ldpart;
   float* ws;            // [kSlices][16 NT][Mpad] partial tiles, column-major per slice
   float* ws2;           // [row blocks][16 NT] row-block column sums of E
   unsigned* cnt;        // [row blocks] slice tickets, then [slabs] half-slab tickets
@@ -94,7 +96,7 @@ void top_rows_kernel(const TopRowsP q) {
   };
   stamp(0);
   // this block's class ids (read by the softmax of the row block's last slice; loaded now, off its critical path)
-  const int my_label = (!q.logits_only && tid < kRows && rb * kRows + tid < M) ? q.labels[rb * kRows + tid] : -1;
+  const int my_label = (q.logits_only == 0 && tid < kRows && rb * kRows + tid < M) ? q.labels[rb * kRows + tid] : -1;
 
   // ---- the A fragments straight into registers (lane (lg, li) supplies A[li][k], B[k][li] with k = 16 c + 4 lg + s
   // at the chunk's step s: the 16x16x4 kernels' lane map, gemm_f32.hip); tiles wv, wv + 4, wv + 8 (N <= 144)
@@ -164,6 +166,23 @@ void top_rows_kernel(const TopRowsP q) {
     }
   }
   stamp(2);
+
+  if (q.logits_only == 2) {
+    // ---- partials only: slice sl's rows 4 lg .. 4 lg + 3 of column (tile, li), row-major at part[sl][row][col]
+    // (every column of the 16 NT is written, the padding ones from the clamped W column; the next launch combines)
+    float* pp = q.part + (long)sl * M * q.ldpart;
+#pragma unroll
+    for (int t = 0; t < 3; ++t) {
+      const int tile = wv + 4 * t;
+      if (tile >= q.NT) continue;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = rb * kRows + 4 * lg + r;
+        if (row < M) pp[(long)row * q.ldpart + tile * 16 + li] = acc[t][r];
+      }
+    }
+    return;
+  }
 
   // ---- the partial tiles, written through: slice sl, column n, rows 4 lg .. 4 lg + 3 as one 16-B vector
   const long cspan = 16L * q.NT;
@@ -402,36 +421,44 @@ using namespace tnetk;
 
 // Which shapes the kernel takes (TNET_TOP_ROWS=0: none): n_out <= 144, K = 512, 768 or 1024 (4 slices of 8, 12 or 16
 // chunks of 16 k, the chunks of A held in registers), at least 64 rows, 16-B aligned k-contiguous X.
-extern "C" __attribute__((visibility("hidden"))) int tnetk_top_rows_ok(const float* X, long ldx, const float* W,
-                                                                      long ldw, int M, int N, int K) {
-  const bool on = top_rows_mode().on;
+extern "C" __attribute__((visibility("hidden"))) int tnetk_top_rows_shape_ok(const float* X, long ldx, const float* W,
+                                                                            long ldw, int M, int N, int K) {
   // (W is read in 16-B pieces up to column 16 ceil(N / 16): inside its padded rows)
-  return on && N >= 1 && N <= kMaxCols && (K == 512 || K == 768 || K == 1024) && M >= 64 &&
+  return N >= 1 && N <= kMaxCols && (K == 512 || K == 768 || K == 1024) && M >= 64 &&
          ((uintptr_t)X & 15) == 0 && (ldx & 3) == 0 && (long)M * ldx * 4 < (1L << 31) && ((uintptr_t)W & 15) == 0 &&
          (ldw & 3) == 0 && ldw >= 16L * ((N + 15) / 16);
+}
+extern "C" __attribute__((visibility("hidden"))) int tnetk_top_rows_ok(const float* X, long ldx, const float* W,
+                                                                      long ldw, int M, int N, int K) {
+  return top_rows_mode().on && tnetk_top_rows_shape_ok(X, ldx, W, ldw, M, N, K);
 }
 
 extern "C" __attribute__((visibility("hidden"))) int tnetk_top_rows(
     const float* X, long ldx, const float* W, long ldw, const float* b, int M, int N, int K, const int* labels,
     float* Z, long ldz, float* Y, long ldy, float* E, long lde, double* stats, float* cpart, long ldcp, int v4,
-    int logits_only, void* stream) {
-  if (!tnetk_top_rows_ok(X, ldx, W, ldw, M, N, K)) return TNET_ERR_UNSUPPORTED;
+    int logits_only, float* part, long ldpart, void* stream) {
+  if (logits_only == 2 ? !tnetk_top_rows_shape_ok(X, ldx, W, ldw, M, N, K) || !part || ldpart < 16L * ((N + 15) / 16)
+                       : !tnetk_top_rows_ok(X, ldx, W, ldw, M, N, K))
+    return TNET_ERR_UNSUPPORTED;
   const hipStream_t st = (hipStream_t)stream;
   TopRowsP q{};
   q.X = X; q.ldx = ldx; q.W = W; q.ldw = ldw; q.b = b; q.M = M; q.N = N; q.K = K;
   q.NT = (N + 15) / 16;
   q.labels = labels; q.Z = Z; q.ldz = ldz; q.Y = Y; q.ldy = ldy; q.E = E; q.lde = lde; q.stats = stats;
   q.cpart = cpart; q.ldcp = ldcp; q.v4 = v4; q.logits_only = logits_only;
+  q.part = part; q.ldpart = ldpart;
   q.nrb = (M + kRows - 1) / kRows;
   q.Mpad = q.nrb * kRows;
   const long cspan = 16L * q.NT;
   const size_t wsf = (size_t)kSlices * cspan * q.Mpad, ws2f = (size_t)q.nrb * cspan;
   if (4 * (long)wsf >= (1L << 31)) return TNET_ERR_UNSUPPORTED;
-  TopWs* w = top_ws(st, (wsf + ws2f) * sizeof(float), (size_t)q.nrb + (q.nrb + 1) / 2);
-  if (!w) return TNET_ERR_RUNTIME;
-  q.ws = w->ws;
-  q.ws2 = w->ws + wsf;
-  q.cnt = w->cnt;
+  if (logits_only != 2) {  // the in-launch combine's partial tiles, half-slab sums and tickets
+    TopWs* w = top_ws(st, (wsf + ws2f) * sizeof(float), (size_t)q.nrb + (q.nrb + 1) / 2);
+    if (!w) return TNET_ERR_RUNTIME;
+    q.ws = w->ws;
+    q.ws2 = w->ws + wsf;
+    q.cnt = w->cnt;
+  }
   const int nch = K / 64;
   const dim3 grid((unsigned)(q.nrb * kSlices));
   q.stamps = g_top_stamps;
