@@ -327,9 +327,13 @@ __global__ __launch_bounds__(256) void softmax_xent_row4_kernel(const float* __r
   __shared__ float smax[4];
   __shared__ double ssum[4];
   __shared__ ArgMax sarg[4];
+  __shared__ float syt;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int row = blockIdx.x, N = d.cols;
   const float* src = Z + (long)row * d.stride;
+  // the label first: its load is in flight with the row's, not a dependent trip after the reductions
+  int t = labels[row];
+  if (t >= N) t = -1;  // out of range: an unlabeled row (the host intake rejects one, CheckLabels)
   f32x4 rv[CPW];
   float m = -1e20f;
 #pragma unroll
@@ -362,8 +366,6 @@ __global__ __launch_bounds__(256) void softmax_xent_row4_kernel(const float* __r
   __syncthreads();
   const float sum = (float)(ssum[0] + ssum[1] + ssum[2] + ssum[3]);
   const float rsum = 1.f / sum;
-  int t = labels[row];
-  if (t >= N) t = -1;  // out of range: an unlabeled row (the host intake rejects one, CheckLabels)
   float* yrow = Y ? Y + (long)row * strideY : nullptr;
   float* erow = E ? E + (long)row * strideE : nullptr;
   // write-through row stores (kcommon.h st_wt): E is 16 MB at 4000 senones, read next on other XCDs
@@ -379,6 +381,9 @@ __global__ __launch_bounds__(256) void softmax_xent_row4_kernel(const float* __r
         y[k] = rv[q][k] * rsum;
         if (y[k] > ay.v) { ay.v = y[k]; ay.i = c + k; }
         e[k] = y[k] - ((c + k == t) ? 1.f : 0.f);
+        // the y written for column t, handed to thread 0 from the owning lane's registers (the same value
+        // a re-read of the logit recomputes: fast_exp(z_t - m) * rsum, without that dependent load)
+        if (c + k == t) syt = y[k];
       }
       if (yrow) st_wt(ry, c, y);
       if (erow) st_wt(re, c, e);
@@ -393,10 +398,7 @@ __global__ __launch_bounds__(256) void softmax_xent_row4_kernel(const float* __r
     for (int w = 1; w < 4; ++w) a = argmax_merge(a, sarg[w]);
     const int des = t >= 0 ? t : 0;  // all-zero target row: first max of zeros is column 0
     double xent = 0.0;
-    if (t >= 0) {
-      const float yt = fast_exp(src[t] - m) * rsum;  // the y written for column t
-      xent = -(double)logf(fmaxf(yt, FLT_MIN));
-    }
+    if (t >= 0) xent = -(double)logf(fmaxf(syt, FLT_MIN));
     if (stats) {
       const int slot = blockIdx.x % TNET_STATS_SLOTS;
       atomicAdd(stats + 2 * slot, xent);
