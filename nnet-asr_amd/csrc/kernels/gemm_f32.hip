@@ -4020,6 +4020,9 @@ extern "C" int tnet_diag_stamps(unsigned long long* host, int n_wg) {
 extern "C" int tnet_diag_stamps_clear() {
   void* a = nullptr;
   if (hipGetSymbolAddress(&a, HIP_SYMBOL(g_tnet_stamps)) != hipSuccess) return TNET_ERR_RUNTIME;
-  return hipMemset(a, 0, sizeof(g_tnet_stamps)) == hipSuccess ? TNET_OK : TNET_ERR_RUNTIME;
+  // hipMemset is queued on the null stream, which does not order the library's non-blocking stream: without
+  // the device-wide wait the next stamped launch could start under the clear and lose its first stamps
+  return hipMemset(a, 0, sizeof(g_tnet_stamps)) == hipSuccess && hipDeviceSynchronize() == hipSuccess
+             ? TNET_OK : TNET_ERR_RUNTIME;
 }
 #endif

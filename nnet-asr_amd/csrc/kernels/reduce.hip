@@ -114,6 +114,10 @@ __global__ __launch_bounds__(256) void softmax_xent_kernel(const float* __restri
   const int N = d.cols;
   const float* src = Z ? Z + (long)row * d.stride : Y + (long)row * strideY;
   const bool cached = vec4 && N <= SX_MAXV4 * 256;
+  // a class id outside [0, N) is treated as an unlabeled row (the host intake rejects one, CheckLabels);
+  // loaded first, in flight with the row's values instead of a dependent trip after the reductions
+  int t = (KIND == 0) ? labels[row] : -1;
+  if (t >= N) t = -1;
 
   // ---- pass 1: max
   f32x4 rv[SX_MAXV4];
@@ -161,16 +165,18 @@ __global__ __launch_bounds__(256) void softmax_xent_kernel(const float* __restri
   // ---- pass 3: y, error, argmax, xent
   ArgMax ay{-1e20f, 0x7fffffff}, ad{-1e20f, 0x7fffffff};
   double xent = 0.0;
-  // a class id outside [0, N) is treated as an unlabeled row (the host intake rejects one, CheckLabels)
-  int t = (KIND == 0) ? labels[row] : -1;
-  if (t >= N) t = -1;
+  float ytl = 0.f;  // KIND 0: the y written for column t, on the lane that owns t
   float* yrow = Y ? Y + (long)row * strideY : nullptr;
   float* erow = E ? E + (long)row * strideE : nullptr;
   const float* drow = (KIND == 1) ? D + (long)row * strideD : nullptr;
   auto visit = [&](int c, float y) {
     float dv;
-    if (KIND == 0) dv = (c == t) ? 1.f : 0.f;
-    else dv = drow[c];
+    if (KIND == 0) {
+      dv = (c == t) ? 1.f : 0.f;
+      if (c == t) ytl = y;
+    } else {
+      dv = drow[c];
+    }
     if (y > ay.v) { ay.v = y; ay.i = c; }
     if (KIND == 1 && dv > ad.v) { ad.v = dv; ad.i = c; }
     if (KIND == 1 && dv != 0.f) xent -= (double)dv * (double)logf(fmaxf(y, FLT_MIN));
@@ -208,11 +214,12 @@ __global__ __launch_bounds__(256) void softmax_xent_kernel(const float* __restri
     des = ad.i;
   }
   if (KIND == 1) xent = wave_sum_d(xent);
+  // the label column's y from its owner lane's registers (the value a re-read of the row recomputes:
+  // fast_exp(z_t - m) * rsum, or y_t itself) -- no dependent load at the row's end
+  float yt = 0.f;
+  if (KIND == 0) yt = __shfl(ytl, t < 0 ? 0 : cached ? (t & 255) >> 2 : t & 63, 64);
   if (lane == 0) {
-    if (KIND == 0 && t >= 0) {
-      const float yt = Z ? fast_exp(src[t] - m) * rsum : src[t];  // the y written for column t
-      xent = -(double)logf(fmaxf(yt, FLT_MIN));
-    }
+    if (KIND == 0 && t >= 0) xent = -(double)logf(fmaxf(yt, FLT_MIN));
     red[0][wv] = xent;
     red[1][wv] = (ay.i == des) ? 1.0 : 0.0;
   }
