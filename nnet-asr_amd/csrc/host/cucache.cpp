@@ -1,6 +1,7 @@
 // cucache.cpp -- see cucache.h.  State machine follows src/CuTNetLib/cuCache.cc:22-200.
 #include "cucache.h"
 
+#include <cstdlib>
 #include <numeric>
 
 namespace TNet {
@@ -19,6 +20,7 @@ void SeedRandom(long seed) { GlobalRng().Seed(seed); }
 
 CuCache::CuCache() {}
 CuCache::~CuCache() {
+  JoinAhead();
   if (mCopy) (void)hipStreamSynchronize(mCopy);
   (void)hipStreamSynchronize(CuDevice::Instantiate().Stream());
   for (hipEvent_t e : {mRel[0], mRel[1], mFilled, mSync, mPermEv[0], mPermEv[1]})
@@ -261,10 +263,17 @@ void CuCache::AddDataHost(const float* feats, size_t rows, size_t cols, size_t l
 void CuCache::Randomize() {
   if (!(mState == FULL || mState == INTAKE)) Error("CuCache::Randomize: cache not filled");
   if (mTrace & 3) std::cout << "R" << std::flush;
-  mPermHost.resize(mIntakePos);
-  std::iota(mPermHost.begin(), mPermHost.end(), 0);
   Rng48& rng = mRng ? *mRng : GlobalRng();
-  rng.RandomShuffle(mPermHost.data(), mIntakePos);
+  JoinAhead();
+  if (mAheadValid && mRng && !rng.Libc() && mAheadN == mIntakePos && rng.State() == mAheadFrom) {
+    mPermHost.swap(mAheadPerm);  // drawn ahead from this very state (see cucache.h)
+    rng.SetState(mAheadTo);
+  } else {
+    mPermHost.resize(mIntakePos);
+    std::iota(mPermHost.begin(), mPermHost.end(), 0);
+    rng.RandomShuffle(mPermHost.data(), mIntakePos);
+  }
+  mAheadValid = false;
   // upload from a pinned slot on the compute stream (ordered after the gathers that read the
   // previous permutation); the slot's previous upload finished long ago (two shuffles back)
   const int k = mPermSlot;
@@ -276,6 +285,24 @@ void CuCache::Randomize() {
   mPermEvSet[k] = true;
   mPermSlot ^= 1;
   mRandomized = true;
+  static const bool ahead = !(getenv("TNET_SHUFFLE_AHEAD") && getenv("TNET_SHUFFLE_AHEAD")[0] == '0');
+  if (ahead && mRng && !rng.Libc()) {  // the process stream may have other users: never drawn ahead
+    mAheadFrom = rng.State();
+    mAheadN = mIntakePos;
+    mAheadValid = true;
+    mAheadThread = std::thread([this] {
+      Rng48 r;
+      r.SetState(mAheadFrom);
+      mAheadPerm.resize(mAheadN);
+      std::iota(mAheadPerm.begin(), mAheadPerm.end(), 0);
+      r.RandomShuffle(mAheadPerm.data(), mAheadN);
+      mAheadTo = r.State();
+    });
+  }
+}
+
+void CuCache::JoinAhead() {
+  if (mAheadThread.joinable()) mAheadThread.join();
 }
 
 void CuCache::Rewind() {

@@ -19,6 +19,8 @@
 //     Leftover buffers are allocated once at the cache size (no allocation between the streams).
 #pragma once
 
+#include <thread>
+
 #include "cumatrix.h"
 #include "rng48.h"
 
@@ -108,6 +110,17 @@ class CuCache {
   int mPermSlot = 0;
   CuVector<int> mPerm;          // device permutation of intake rows
   std::vector<int> mPermHost;
+  // the next pass's permutation, drawn ahead on a host thread from a copy of the trainer's private stream
+  // (a 64 k-row shuffle is ~0.3 ms of host time, more than a fast step's queue lead: MLP3 steps take 68 us).
+  // Taken only when the stream still stands where the copy started (nothing drew from it or reset it in
+  // between) and the fill size matches: the permutation and the stream's state are then exactly what the
+  // shuffle in Randomize would produce.  TNET_SHUFFLE_AHEAD=0: off.
+  void JoinAhead();
+  std::thread mAheadThread;
+  std::vector<int> mAheadPerm;
+  uint64_t mAheadFrom = 0, mAheadTo = 0;
+  size_t mAheadN = 0;
+  bool mAheadValid = false;
 };
 
 }  // namespace TNet

@@ -27,6 +27,7 @@ class Rng48 {
   /// Draw from the C library's srand48/lrand48 stream instead (drop-in build: the reference
   /// drivers seed it with srand48(SEED), TNetCu.cc:330-338, and CuCache shuffles with lrand48)
   void UseLibc(bool on) { mLibc = on; }
+  bool Libc() const { return mLibc; }
   /// libstdc++ std::random_shuffle(first, last, gen) with gen(k) = lrand48() % k
   /// (bits/stl_algo.h:4603-4620)
   void RandomShuffle(int* p, size_t n) {

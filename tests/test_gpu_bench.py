@@ -91,6 +91,20 @@ def test_bench_force_dp_reduction_check(shard):
     assert c["librccl"] and "rccl" in c["librccl"]
 
 
+def test_shuffle_ahead_bit_identical():
+    """the next pass's permutation drawn ahead on a host thread (CuCache, default) and drawn in Randomize itself
+    (TNET_SHUFFLE_AHEAD=0) train the same parameters bit for bit over several passes of a 4-bunch cache: the ahead
+    shuffle starts from the trainer stream's state and is taken only while the stream still stands there"""
+    cmd = [sys.executable, "bench.py", "--config", "mlp3", "--steps", "13", "--warmup", "2", "--no-cpu-baseline",
+           "--cache", "4096", "--kernel-timing", "0", "--breakdown-steps", "0", "--prewarm-ms", "0"]
+    sha = []
+    for env in ({}, {"TNET_SHUFFLE_AHEAD": "0"}):
+        p = subprocess.run(cmd, cwd=REPO, capture_output=True, text=True, timeout=300, env=dict(os.environ, **env))
+        assert p.returncode == 0, p.stderr[-3000:]
+        sha.append(_line(p.stdout)["replica_check"]["param_sha256_16"])
+    assert sha[0] == sha[1]
+
+
 @pytest.mark.parametrize("config", ["mlp3", "dnn4"])
 def test_dp_exchange_schedules_bit_identical(config):
     """the round-5 exchange schedule (MLP3: the whole reduction inline on the compute stream + one merged apply;
