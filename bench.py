@@ -194,10 +194,18 @@ def prewarm(ms):
 
 
 def reduction_checks(args, comm, trainer, dist, rank, world):
-    """rccl_check: one extra step after the measured regions whose gradient reductions are
-    compared with a float64 gloo sum of the same local gradients (tnet_amd.dpcheck), in the exchange form the run
-    uses and -- for an RCCL run at N > 1 in the default all-reduce form -- once more in the sharded form
-    (reduce-scatter + sharded apply + all-gather) on a second communicator created with TNET_DP_SHARD=1"""
+    """rccl_check: one extra step after the measured regions whose gradient reductions
+    are compared with a float64 gloo sum of the same local gradients (tnet_amd.dpcheck), in the exchange form the run
+    uses and -- for an RCCL run at N > 1 in the default all-reduce form, or at any N with --rccl-check-shard 2 -- once
+    more in the sharded form (reduce-scatter + sharded apply + all-gather) on a second communicator created with
+    TNET_DP_SHARD=1.  The armed steps run the production schedule: the exchange copies each block on the device, on
+    the reduction's own stream, and the copies are read back after the step (GradExchange::CaptureLocal).
+
+    The second form is a check of a mode the run did NOT time: whatever goes wrong with it (its communicator, the swap
+    into the trainer, the armed step) is recorded under that mode with ok false and an error text, and never ends the
+    run -- only a mismatch in the timed mode does (exit 4).  The ranks agree (gloo) that every rank created the second
+    communicator before any of them trains on it, so a creation failure on one rank cannot leave the others waiting
+    inside a collective."""
     from tnet_amd import dpcheck
 
     def allreduce64(a):
@@ -212,30 +220,70 @@ def reduction_checks(args, comm, trainer, dist, rank, world):
         dist.all_gather_object(got, res)
         return got
 
+    def all_ok(flag):
+        if dist is None:
+            return flag
+        import torch
+        t = torch.tensor([0.0 if flag else 1.0], dtype=torch.float64)
+        dist.all_reduce(t)
+        return float(t.item()) == 0.0
+
     shard = os.environ.get("TNET_DP_SHARD", "0") == "1"
-    modes = {("reduce-scatter+all-gather" if shard else "all-reduce"):
-             dpcheck.merge_ranks(gather(dpcheck.check_step(comm, trainer, allreduce64)))}
-    if args.comm == "rccl" and world > 1 and not shard and args.rccl_check_shard:
+    timed = "reduce-scatter+all-gather" if shard else "all-reduce"
+    modes = {timed: dpcheck.merge_ranks(gather(dpcheck.check_step(comm, trainer, allreduce64)))}
+    modes[timed]["timed"] = True
+    want_shard = (args.comm == "rccl" and not shard and
+                  ((world > 1 and args.rccl_check_shard >= 1) or args.rccl_check_shard == 2))
+    if want_shard:
+        name = "reduce-scatter+all-gather"
+        comm2, err = None, None
         os.environ["TNET_DP_SHARD"] = "1"  # read once, at the communicator's creation
         try:
             uid = [Comm.unique_id() if rank == 0 else None]
-            dist.broadcast_object_list(uid, src=0)
+            if dist is not None:
+                dist.broadcast_object_list(uid, src=0)
             comm2 = Comm(rank, world, uid[0])
+        except Exception as e:  # noqa: BLE001  (recorded, never fatal: not the timed mode)
+            err = f"communicator: {type(e).__name__}: {str(e)[:300]}"
         finally:
             os.environ.pop("TNET_DP_SHARD", None)
-        trainer.set_comm(comm2)
-        try:
-            modes["reduce-scatter+all-gather"] = dpcheck.merge_ranks(
-                gather(dpcheck.check_step(comm2, trainer, allreduce64)))
-        finally:
-            tnet_amd.synchronize()
-            trainer.set_comm(comm)
-            comm2.__del__()
+        if not all_ok(err is None):
+            modes[name] = {"ok": False, "timed": False,
+                           "error": err or "another rank failed to create the sharded-form communicator"}
+        else:
+            res, swapped = None, False
+            try:
+                trainer.set_comm(comm2)
+                swapped = True
+                res = dpcheck.check_step(comm2, trainer, allreduce64)
+            except Exception as e:  # noqa: BLE001
+                err = f"armed step: {type(e).__name__}: {str(e)[:300]}"
+            finally:
+                try:
+                    tnet_amd.synchronize()
+                    if swapped:
+                        trainer.set_comm(comm)
+                except Exception as e:  # noqa: BLE001
+                    err = err or f"swap back: {type(e).__name__}: {str(e)[:300]}"
+            got = gather({"res": res, "err": err})
+            errs = [g["err"] for g in got if g["err"]]
+            if errs:
+                modes[name] = {"ok": False, "timed": False, "error": errs[0]}
+            else:
+                modes[name] = dpcheck.merge_ranks([g["res"] for g in got])
+                modes[name]["timed"] = False
+        if comm2 is not None:
+            try:
+                comm2.__del__()
+            except Exception:  # noqa: BLE001
+                pass
     return {"ranks": world, "transport": args.comm if world > 1 else "rccl (one rank)",
             "transport_ranks": comm.transport_ranks(), "librccl": mapped_runtime().get("librccl"),
-            "tolerance": dpcheck.TOLERANCE, "modes": modes,
-            "max_rel_err": max(m["max_rel_err"] for m in modes.values()),
-            "ok": all(m["ok"] for m in modes.values())}
+            "tolerance": dpcheck.TOLERANCE, "capture": "device copies on the reduction's stream (no host sync in the "
+                                                       "armed step), read back after it",
+            "modes": modes, "timed_mode": timed,
+            "max_rel_err": max(m.get("max_rel_err", float("inf")) for m in modes.values()),
+            "ok": modes[timed]["ok"], "all_modes_ok": all(m["ok"] for m in modes.values())}
 
 
 def main():
@@ -278,7 +326,8 @@ def main():
                     help="steps: training steps of the same shape on a scratch network / trainer (the step's own "
                          "kernel and traffic mix); gemm: the round-4 scratch 2048^2 GEMMs")
     ap.add_argument("--rccl-check-shard", type=int, default=1,
-                    help="N > 1 over RCCL: also check the sharded exchange form on a second communicator (0: off)")
+                    help="N > 1 over RCCL: also check the sharded exchange form on a second communicator swapped into "
+                         "the trainer (0: off; 2: also at one rank, with --force-dp -- the swap rehearsed on one GPU)")
     ap.add_argument("--breakdown-steps", type=int, default=20,
                     help="extra steps after the timed region with every launch event-timed (kernels field)")
     args = ap.parse_args()
@@ -375,10 +424,13 @@ def main():
         breakdown = parse_kernel_report(buf.value.decode())
     # the reduction check: one more step, after every measured region (synchronous copies)
     rccl_check = reduction_checks(args, comm, trainer, dist, rank, world) if comm is not None else None
-    if rccl_check is not None and not rccl_check["ok"]:
+    if rccl_check is not None and not rccl_check["ok"]:  # the TIMED mode's reductions are wrong: no number
         print("bench: the reduced gradients differ from the gloo float64 sum of the local gradients: " +
               json.dumps(rccl_check), file=sys.stderr)
         raise SystemExit(4)
+    if rccl_check is not None and not rccl_check["all_modes_ok"]:
+        print("bench: WARNING the untimed sharded-form check failed (recorded in rccl_check.modes): " +
+              json.dumps(rccl_check["modes"]), file=sys.stderr)
     if dist is not None:
         import torch
         t = torch.tensor([dt], dtype=torch.float64)

@@ -132,17 +132,15 @@ int tnet_gather_bunch(float* y, const float* x, int* labels_out, const int* labe
  * fp32 in / fp32 accumulate on the f32 MFMA (v_mfma_f32_16x16x4_f32; exact f32 FMA chain per k).
  * Shapes with few output tiles and a long K (fewer than ~100 tiles, K >= 1024) are split over K:
  * the slices' partial products are added in slice order (deterministic) before the epilogue, by a
- * second launch (or, opt-in "+il1"/"+il2" below, by each tile's last-finishing slice inside the
- * launch: agent-scope release/acquire + a tile counter; measured slower on MI355X).
+ * second launch.
  * Requirements: lda/ldb/ldc multiples of 4 elements, pointers 16-byte aligned.
  * ---------------------------------------------------------------------------------- */
 int tnet_sgemm(char transa, char transb, int m, int n, int k, float alpha, const float* A, int lda,
                const float* B, int ldb, float beta, float* C, int ldc, void* stream);
 /* Tuning knob: force one GEMM tile configuration for every later launch in this process
  * ("auto" = per-shape heuristic; names as in gemm_f32.hip, e.g. "m64x128k64s2"), optionally with a
- * forced split-K count ("m64x64k32s4w41+sk8") and the combine mode ("+il0" second launch (default),
- * "+il1" in-launch up to 64 KB a tile, "+il2" in-launch for every 64x64 / 32x64 tile; sticky) and a CU
- * reservation ("+rsv<R>", as tnet_gemm_reserve; sticky).  Not thread-safe. */
+ * forced split-K count ("m64x64k32s4w41+sk8") and a CU reservation ("+rsv<R>", as tnet_gemm_reserve;
+ * sticky).  Not thread-safe. */
 int tnet_gemm_config(const char* name);
 /* R CUs held by another kernel while the caller's next GEMMs run (the data-parallel exchange sets it
  * while RCCL's collectives are in flight, 0 when they are done): the step's 64x128 backward / forward
@@ -214,16 +212,6 @@ int tnet_colsum_slab_sums(const float* E, TnetMatrixDim dE, float* colpart, int 
 int tnet_affine_softmax_xent(const float* X, TnetMatrixDim dX, const float* W, TnetMatrixDim dW, const float* b,
                              const int* labels, float* Z, int strideZ, float* Y, int strideY, float* E, int strideE,
                              double* stats, float* colpart, int ldcolpart, void* stream);
-/* The narrow top layer's one-launch row-block kernel (up to 144 classes over K = 512 / 768 / 1024; top_rows.hip):
- * OFF by default -- measured slower than the two-launch form above on MI355X -- and taken by
- * tnet_affine_softmax_xent and tnet_affine_fwd(act 0) for those shapes once enabled here (on: 1; variant: 1 = W
- * fragments straight into registers, 3 = W slice staged in LDS; or TNET_TOP_ROWS=1 / TNET_TOP_ROWS_V at load time).
- * Same Z / Y / E / statistics bit for bit either way.  Process-wide; not to be flipped while launches are in flight. */
-int tnet_top_rows_config(int on, int variant);
-/* its diagnostics: while buf != NULL every launch records thread 0's s_memtime per phase into buf[block * 8 + i]
- * (device memory, 8 64-bit words a block; 0 entry, 1 operands loaded, 2 MFMAs issued, 3 partial tiles stored +
- * ticket, 4 logits-only end, 5 softmax done); NULL: off */
-int tnet_top_rows_stamps(long long* buf);
 /* tnet_affine_update + tnet_bias_update(E, b, corr_b, scale, mmt) in one launch, colsum(E) taken from
  * colpart (written for E by tnet_affine_bwd_colsum); corr_b is required when mmt != 0
  * (cuBiasedLinearity.cc:46-64). */
@@ -455,26 +443,6 @@ int tnet_rnn_out_bwd_update(const float* z, const double* smx, int pairs, int N,
                             unsigned long long* argkey, int train, void* stream);
 int tnet_argmax_correct(const unsigned long long* keys, const int* labels, int T, int N, double* stats,
                         void* stream);
-/* ---- a whole TRecurrentCu utterance in ONE launch (TRecurrentCu.cc:346-371, the frames' chain above
- * plus the BPTT GEMVs and the recurrent update): co-resident workgroups keep W (the recurrent
- * [(nIn + H) x H]) and Wo ([H x N]) in LDS, column slices each, and hand the per-frame vectors to
- * each other as write-through {tag, value} granules (rnn_persistent.hip).  X [T x nIn] (ld ldx),
- * labels [T]; W / b / corr_b: the <recurrent> layer (CuRecurrent::Update's lr / mmt / wc); Wo / bo and
- * their momentum buffers (NULL when ommt == 0): the output <biasedlinearity> (oscale / ol2 of its
- * UpdateConstants(1)); y [H]: y_{-1} in, y_{T-1} out; stats: cross-entropy into slot 0; argkey [T]
- * zeroed by the caller (tnet_argmax_correct afterwards); workspace: tnet_rnn_utterance_workspace
- * bytes, zeroed once; epoch0: grows by >= 16 T + 16 between calls on one workspace; train = 0:
- * forward + statistics only; *err = 1 if a hand-off wait timed out (2 s).  bptt <= 8;
- * TNET_ERR_UNSUPPORTED when the weight slices do not fit the LDS of 256 workgroups. */
-long tnet_rnn_utterance_workspace(int H, int N, int G);
-/* diagnostics: later tnet_rnn_utterance launches store workgroup 0's s_memrealtime (100 MHz) at 8
- * phase points per frame into buf[8 t + k] (NULL: off) */
-int tnet_rnn_utterance_stamps(long long* buf);
-int tnet_rnn_utterance(const float* X, int T, int nIn, int ldx, const int* labels, float* W, int ldw, float* b,
-                       float* corr_b, int H, float* Wo, int ldwo, float* bo, float* corr_Wo, int ldwoc,
-                       float* corr_bo, int N, int bptt, float lr, float mmt, float wc, float oscale, float ommt,
-                       float ol2, float* y, double* stats, unsigned long long* argkey, void* workspace,
-                       unsigned epoch0, int train, int* err, void* stream);
 /* single-frame CuBiasedLinearity::Backpropagate + Update (cuBiasedLinearity.cc:32-64) in one pass
  * over W: e_out = W e (with the weights before the update), then the update of
  * tnet_affine_update_row; with s != NULL also d_out = e_out .* s (1 - s) (the diff-sigmoid of a
@@ -501,18 +469,6 @@ int tnet_gemv_rows(const float* W, int ldw, int r0, int nrows, int n, const floa
  *   corr = sum_{i<steps} (-lr h_i) (x) d_i ; corr += -lr*wc*W ; W += corr
  *   cb = -lr d_0 + mmt*cb ; cb = -lr d_i + cb (i >= 1) ; b += cb
  * h_i = row (head + i) % R of the history ring hist [R x rows], d_i = row i of D. */
-/* The `order` BPTT GEMVs of one frame (cuRecurrent.cc:106-145; tnet_gemv_rows with s = the history's y rows,
-   r0 = nIn, beta 0, x = row i-1 of D, y = row i of D, i = 1..order) in ONE launch on n / 64 co-resident
-   workgroups handing each step's vector on as write-through granules; bit-identical to the per-step launches.
-   workspace: tnet_rnn_bptt_chain_workspace(n, order) bytes, zeroed once before the first call and kept for the
-   layer's life (its epoch word orders the launches).  TNET_ERR_UNSUPPORTED outside n <= 1024 (n % 64 == 0 up
-   to 512, n % 32 == 0 above), 16-B aligned W / D, order < 16.  A hand-off that never arrives (a bug) sets an
-   error word instead of hanging: tnet_rnn_bptt_chain_error reads it, ordered after the work already enqueued on
-   `stream` (the chain's stream; returns once that work has finished). */
-long tnet_rnn_bptt_chain_workspace(int n, int order);
-int tnet_rnn_bptt_chain(const float* W, int ldw, int r0, int n, float* D, int ldd, int order, const float* hist,
-                        int ldh, int head, int R, int hoff, void* workspace, void* stream);
-int tnet_rnn_bptt_chain_error(const void* workspace, int* err, void* stream);
 int tnet_rnn_update(float* W, int ldw, int rows, int nout, const float* hist, int ldh, int head, int R,
                     const float* D, int ldd, int steps, float* b, float* corr_b, float lr, float mmt, float wc,
                     void* stream);
@@ -549,14 +505,6 @@ int tnet_add_gauss_noise(float* mat, TnetMatrixDim d, float scale, unsigned* z1,
  * Z == NULL: Y already holds the network output (softmax not recomputed). */
 int tnet_softmax_xent(const float* Z, TnetMatrixDim dZ, const int* labels, float* Y, int strideY, float* E,
                       int strideE, double* stats, void* stream);
-/* tnet_softmax_xent + tnet_colsum_slab_sums(E) in ONE pass (one workgroup per 32-row slab; Z, Y, E,
- * the statistics and the slab sums bit-identical to the two calls): the top layer's objective and
- * bias-gradient slab sums for tnet_affine_update_bias (CuSoftmax::PropagateFnc +
- * CuCrossEntropy::Evaluate, cuActivation.cc:28-31, cuObjectiveFunction.cc:50-83, and the bias gradient of
- * CuBiasedLinearity::Update, cuBiasedLinearity.cc:36-41).  Z required; TNET_ERR_UNSUPPORTED outside
- * 1025..4096 columns (16-B aligned rows) or when rows is not a multiple of 32 (make the two calls). */
-int tnet_softmax_xent_slabs(const float* Z, TnetMatrixDim dZ, const int* labels, float* Y, int strideY, float* E,
-                            int strideE, double* stats, float* colpart, int ldcolpart, void* stream);
 /* Same objective for dense desired matrices D (any soft targets; cuObjectiveFunction.cc:50-83):
  * Y = softmax(Z) (if Z != NULL, else Y already holds the network output), E = Y - D, stats as above
  * with xent = -sum D log(max(Y, FLT_MIN)). */

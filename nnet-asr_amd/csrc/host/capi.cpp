@@ -743,7 +743,15 @@ int tnet_comm_capture(TnetComm* c, int on) {
   c->ex->ArmCapture(on != 0);
   TRY_END
 }
-long tnet_comm_captured(TnetComm* c) { return c ? (long)c->ex->Captured().size() : -1; }
+long tnet_comm_captured(TnetComm* c) {
+  if (!c) return -1;
+  try {
+    return (long)c->ex->Captured().size();  // the first call reads the armed step's device copies back
+  } catch (const std::exception& e) {
+    g_last_error = e.what();
+    return -1;
+  }
+}
 int tnet_comm_captured_block(TnetComm* c, long i, float* local, float* reduced, long cap, long* n) {
   TRY_BEGIN if (!c || !n || i < 0 || i >= (long)c->ex->Captured().size()) Error("tnet_comm_captured_block: bad arguments");
   const GradExchange::CapturedBlock& b = c->ex->Captured()[(size_t)i];

@@ -356,15 +356,6 @@ void CuCache::GetBunchLabels(CuMatrix<BaseFloat>& rFeatures, CuVector<int>& rLab
   AdvanceAfterBunch();
 }
 
-void CuCache::GatherAheadLabels(CuMatrix<BaseFloat>& rFeatures, CuVector<int>& rLabels, hipStream_t stream) {
-  if (!HasBunchAhead()) Error("CuCache::GatherAheadLabels: no shuffled bunch ahead");
-  if (rFeatures.Rows() != mBunchsize || rFeatures.Cols() != mFeatures.Cols() || rLabels.Dim() != mBunchsize)
-    Error("CuCache::GatherAheadLabels: destination not sized for a bunch");
-  TNET_SAFE_CALL(tnet_gather_bunch(rFeatures.pCUData(), mFeatures.pCUData(), rLabels.pCUData(), mLabels.pCUData(),
-                                   mPerm.pCUData() + mExhaustPos, rFeatures.Dim(), mFeatures.Dim(), stream));
-  AdvanceAfterBunch();
-}
-
 BunchGather CuCache::AheadGather(CuMatrix<BaseFloat>& rFeatures, CuVector<int>& rLabels) {
   if (!HasBunchAhead()) Error("CuCache::AheadGather: no shuffled bunch ahead");
   if (rFeatures.Rows() != mBunchsize || rFeatures.Cols() != mFeatures.Cols() || rLabels.Dim() != mBunchsize)

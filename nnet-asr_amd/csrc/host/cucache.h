@@ -49,14 +49,11 @@ class CuCache {
   void GetBunch(CuMatrix<BaseFloat>& rFeatures, CuMatrix<BaseFloat>& rDesired);
   void GetBunchLabels(CuMatrix<BaseFloat>& rFeatures, CuVector<int>& rLabels);
   /// Another bunch of the shuffled class-id fill being exhausted follows the one just taken (it can be
-  /// gathered ahead: GatherAheadLabels)
+  /// gathered ahead: AheadGather)
   bool HasBunchAhead() const { return mMode == LABELS && mRandomized && mState == EXHAUST; }
-  /// GetBunchLabels of that next bunch on `stream` (the caller orders the stream after the compute
-  /// stream's use of the destination buffers; the permutation and the fill are already waited for
-  /// there, EnterExhaust / Randomize being compute-stream ordered)
-  void GatherAheadLabels(CuMatrix<BaseFloat>& rFeatures, CuVector<int>& rLabels, hipStream_t stream);
-  /// the same gather's arguments, for a launch the caller enqueues on the COMPUTE stream before anything
-  /// else touches the cache (the step's last weight update carries it); advances past that bunch
+  /// the arguments of GetBunchLabels' gather of that next bunch, for a launch the caller enqueues on the COMPUTE
+  /// stream before anything else touches the cache (the step's last weight update carries it); advances past
+  /// that bunch
   BunchGather AheadGather(CuMatrix<BaseFloat>& rFeatures, CuVector<int>& rLabels);
 
   bool Full() { return mState == FULL; }

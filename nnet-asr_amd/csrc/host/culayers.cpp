@@ -110,6 +110,7 @@ void CuBiasedLinearity::UpdateFrom(const CuMatrix<BaseFloat>& X, const CuMatrix<
                                           mmt ? mLinearityCorrection.pCUData() : nullptr,
                                           (int)mLinearityCorrection.Stride(), mBias.pCUData(),
                                           mmt ? mBiasCorrection.pCUData() : nullptr, scale, mMomentum, l2, S));
+    mShadowValid = false;  // the rank-1 kernel writes W only
     return;
   }
   // bias first: it reads only E (the weight kernel rewrites W in place)
@@ -136,10 +137,21 @@ void CuBiasedLinearity::UseShadow() {
     mLinearityT.Init(mLinearity.Cols(), mLinearity.Rows());
     mShadowValid = false;
   }
-  // (re-)registered every time: W's storage is the same unless it was re-initialised with other dimensions
+  // the registry is keyed by W's address: an entry under an older address (W re-initialised with other
+  // dimensions) would mirror the updates of whatever matrix is allocated there next into this layer's shadow
+  DropShadowKey();
   TNET_SAFE_CALL(tnet_weight_shadow(mLinearity.pCUData(), mLinearity.Dim(), mLinearityT.pCUData(),
                                     (int)mLinearityT.Stride()));
+  mShadowKey = mLinearity.pCUData();
   mShadowOn = true;
+}
+
+void CuBiasedLinearity::DropShadowKey() {
+  if (mShadowKey && mShadowKey != mLinearity.pCUData()) {
+    (void)tnet_weight_shadow(mShadowKey, TnetMatrixDim{}, nullptr, 0);
+    mShadowValid = false;
+  }
+  mShadowKey = nullptr;
 }
 
 const CuMatrix<BaseFloat>& CuBiasedLinearity::ShadowForBwd() {
@@ -190,7 +202,8 @@ void CuBiasedLinearity::UpdateFromColsum(const CuMatrix<BaseFloat>& X, const CuM
 bool CuBiasedLinearity::UpdateFromColsumWithBwd(const CuMatrix<BaseFloat>& X, const CuMatrix<BaseFloat>& E,
                                                 const CuMatrix<BaseFloat>& colpart, const CuBiasedLinearity& below,
                                                 const CuMatrix<BaseFloat>& E2, const CuMatrix<BaseFloat>& Ybelow,
-                                                CuMatrix<BaseFloat>& Eo, CuMatrix<BaseFloat>& colpart2) {
+                                                CuMatrix<BaseFloat>& Eo, CuMatrix<BaseFloat>& colpart2,
+                                                bool use_shadow) {
   CuProfileScope p("CuBiasedLinearity::Update+Backpropagate");
   float scale, l2;
   UpdateConstants(X.Rows(), &scale, &l2);
@@ -201,7 +214,9 @@ bool CuBiasedLinearity::UpdateFromColsumWithBwd(const CuMatrix<BaseFloat>& X, co
              2.0 * X.Rows() * GetNInputs() * GetNOutputs() + 2.0 * E2.Rows() * below.GetNInputs() * below.GetNOutputs(),
              2);
   // the lower layer's backward from its transposed shadow when it keeps one (NN, the forward's layout)
-  const CuMatrix<BaseFloat>* wt = below.HasShadow() ? &const_cast<CuBiasedLinearity&>(below).ShadowForBwd() : nullptr;
+  // (the caller's decision, the same one its standalone backward takes: TrainBunch's `shadows`)
+  const CuMatrix<BaseFloat>* wt =
+      use_shadow && below.HasShadow() ? &const_cast<CuBiasedLinearity&>(below).ShadowForBwd() : nullptr;
   auto pair = wt ? tnet_affine_update_bwd_pair_t : tnet_affine_update_bwd_pair;
   const CuMatrix<BaseFloat>& wb = wt ? *wt : below.LinearityRO();
   const int st = pair(
@@ -460,6 +475,7 @@ void CuBiasedLinearity::ReadFromStream(std::istream& rIn) {
   mLinearity.CopyFrom(BfMatrix(transpose, TRANS));
   mBias.CopyFrom(bias);
   mShadowValid = false;
+  if (mShadowOn) UseShadow();  // W's storage may have moved: re-key the registration
 }
 
 void CuBiasedLinearity::WriteToStream(std::ostream& rOut) {

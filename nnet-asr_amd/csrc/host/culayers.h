@@ -15,8 +15,9 @@ class CuBiasedLinearity : public CuUpdatableComponent {
         mLinearity(nInputs, nOutputs), mBias(nOutputs),
         mLinearityCorrection(nInputs, nOutputs), mBiasCorrection(nOutputs) {}
   ~CuBiasedLinearity() {
-    // the shadow's registration is keyed by W's address: gone before that storage can serve another matrix
-    if (mShadowOn) (void)tnet_weight_shadow(mLinearity.pCUData(), mLinearity.Dim(), nullptr, 0);
+    // the shadow's registration is keyed by W's address (the one registered, which is W's current storage unless
+    // W was re-initialised since): gone before that storage can serve another matrix
+    if (mShadowKey) (void)tnet_weight_shadow(mShadowKey, TnetMatrixDim{}, nullptr, 0);
   }
 
   ComponentType GetType() const override { return BIASED_LINEARITY; }
@@ -96,7 +97,7 @@ class CuBiasedLinearity : public CuUpdatableComponent {
   bool UpdateFromColsumWithBwd(const CuMatrix<BaseFloat>& X, const CuMatrix<BaseFloat>& E,
                                const CuMatrix<BaseFloat>& colpart, const CuBiasedLinearity& below,
                                const CuMatrix<BaseFloat>& E2, const CuMatrix<BaseFloat>& Ybelow,
-                               CuMatrix<BaseFloat>& Eo, CuMatrix<BaseFloat>& colpart2);
+                               CuMatrix<BaseFloat>& Eo, CuMatrix<BaseFloat>& colpart2, bool use_shadow);
 
  protected:
   CuMatrix<BaseFloat> mLinearity;            ///< [nIn x nOut] (file stores the transpose)
@@ -107,6 +108,9 @@ class CuBiasedLinearity : public CuUpdatableComponent {
   CuVector<BaseFloat> mGradB;
   CuMatrix<BaseFloat> mLinearityT;           ///< transposed shadow of mLinearity [nOut x nIn] (UseShadow)
   bool mShadowOn = false, mShadowValid = false;
+  const float* mShadowKey = nullptr;         ///< the W address the shadow is registered under
+  /// unregister the shadow under an address W no longer has (no-op while the registration is current)
+  void DropShadowKey();
   /// after an update launch of W: the shadow is current iff that launch wrote it (tnet_weight_shadow_kept)
   void NoteUpdate() { mShadowValid = mShadowOn && tnet_weight_shadow_kept(mLinearity.pCUData()) == 1; }
   /// the SGD segments (W, b: this rank's ranges) of the data-parallel apply into seg (<= 4), their scale

@@ -335,32 +335,16 @@ void CuNetwork::TrainBunch(const CuMatrix<BaseFloat>& X, const CuVector<int>& la
     act = &dst;
     acts[l + 1] = &dst;
   }
-  // ---- objective: softmax + xent + error (+ optional softmax output).  TNET_SOFTMAX_SLABS=1 (opt-in): for
-  // wide outputs with the top layer trained, the error's slab sums (its bias gradient) in the same pass
-  // (tnet_softmax_xent_slabs, bit-identical) -- MEASURED SLOWER at 4000 senones: 36.7 us against 9.8 + 6.7 us
-  // for the two launches (one workgroup per 32-row slab leaves 32 CUs doing a latency-bound row chain)
+  // ---- objective: softmax + xent + error (+ optional softmax output); the error's slab sums (the top layer's bias
+  // gradient) ride on the top layer's backward launch below.  (Round 2's one-pass softmax + slab sums,
+  // tnet_softmax_xent_slabs, was measured slower -- 36.7 us against 9.8 + 6.7 us, profiles/r02_softmax_slabs_ab.txt
+  // -- and is gone since round 6.)
   if (!fused_top) {
     CuMatrix<BaseFloat>& logits = mNetComponents[2 * (nl - 1)]->Output();
-    static const bool slab_pass = getenv("TNET_SOFTMAX_SLABS") && getenv("TNET_SOFTMAX_SLABS")[0] == '1';
-    int st = TNET_ERR_UNSUPPORTED;
-    if (top_colsum && slab_pass) {
-      CuMatrix<BaseFloat>& cp = *mColPart[nl - 1];
-      cp.Init(tnet_colsum_slabs((int)rows), GetNOutputs());
-      KTScope kts("softmax_xent+colsum:" + std::to_string(GetNOutputs()),
-                  (double)rows * GetNOutputs() * 4.0 * (mKeepOutput ? 3 : 2) + rows * 4.0);
-      st = tnet_softmax_xent_slabs(logits.pCUData(), logits.Dim(), labels.pCUData(), yout, ystride,
-                                   mGlobErr.pCUData(), (int)mGlobErr.Stride(), obj.DeviceStats(), cp.pCUData(),
-                                   (int)cp.Stride(), S);
-      if (st == TNET_ERR_UNSUPPORTED) kts.Cancel();
-      else err_colsum = true;
-    }
-    if (st == TNET_ERR_UNSUPPORTED) {
-      KTScope kts("softmax_xent:" + std::to_string(GetNOutputs()),
-                  (double)rows * GetNOutputs() * 4.0 * (mKeepOutput ? 3 : 2) + rows * 4.0);
-      st = tnet_softmax_xent(logits.pCUData(), logits.Dim(), labels.pCUData(), yout, ystride, mGlobErr.pCUData(),
-                             (int)mGlobErr.Stride(), obj.DeviceStats(), S);
-    }
-    TNET_SAFE_CALL(st);
+    KTScope kts("softmax_xent:" + std::to_string(GetNOutputs()),
+                (double)rows * GetNOutputs() * 4.0 * (mKeepOutput ? 3 : 2) + rows * 4.0);
+    TNET_SAFE_CALL(tnet_softmax_xent(logits.pCUData(), logits.Dim(), labels.pCUData(), yout, ystride, mGlobErr.pCUData(),
+                                     (int)mGlobErr.Stride(), obj.DeviceStats(), S));
   }
   obj.AddFrames(rows);
   if (!train) return;
@@ -453,7 +437,7 @@ void CuNetwork::TrainBunch(const CuMatrix<BaseFloat>& X, const CuVector<int>& la
           pgrad = nullptr;
           eo_colsum = true;
         } else if (pend.lin && pend.lin->UpdateFromColsumWithBwd(*pend.X, *pend.E, *mColPart[pend.l], *lin, *err,
-                                                                *acts[l], *eo, cp)) {
+                                                                *acts[l], *eo, cp, shadows)) {
           pend.lin = nullptr;
           eo_colsum = true;
         } else {

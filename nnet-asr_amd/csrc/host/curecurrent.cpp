@@ -19,38 +19,6 @@ void CuRecurrent::BpttOrder(int ord) {
   mDiff.Init((size_t)ord + 1, GetNOutputs());
   mDiffTmp.Init(1, GetNOutputs());
   mHead = 0;
-  if (!ChainEnabled()) return;
-  // the one-launch BPTT chain's control words and granule slots (zeroed: epoch 0, no granule current), on the
-  // compute stream so the zeroing is ordered with the chain launches
-  const size_t cb = (size_t)tnet_rnn_bptt_chain_workspace((int)GetNOutputs(), ord);
-  if (cb > mChainBytes) {
-    if (mChainWs) {
-      TNET_HIP_CALL(hipStreamSynchronize(CuDevice::Instantiate().Stream()));
-      TNET_HIP_CALL(hipFree(mChainWs));
-    }
-    mChainWs = nullptr;
-    mChainBytes = 0;
-    TNET_HIP_CALL(hipMalloc(&mChainWs, cb));
-    mChainBytes = cb;
-  }
-  TNET_HIP_CALL(hipMemsetAsync(mChainWs, 0, mChainBytes, CuDevice::Instantiate().Stream()));
-}
-
-bool CuRecurrent::ChainEnabled() {
-  static const bool on = getenv("TNET_RNN_BPTT_CHAIN") && getenv("TNET_RNN_BPTT_CHAIN")[0] == '1';
-  return on;
-}
-
-CuRecurrent::~CuRecurrent() {
-  if (mChainWs) (void)hipFree(mChainWs);
-}
-
-void CuRecurrent::CheckChain() const {
-  if (!mChainWs) return;
-  int err = 0;
-  TNET_SAFE_CALL(tnet_rnn_bptt_chain_error(mChainWs, &err, S));
-  if (err) Error("CuRecurrent: the one-launch BPTT chain timed out waiting for a hand-off (unset "
-                 "TNET_RNN_BPTT_CHAIN to run the per-step launches)");
 }
 
 void CuRecurrent::ClearHistory() {
@@ -129,25 +97,13 @@ void CuRecurrent::UpdateFromDiff0(bool defer) {
   FlushPendingUpdate();
   const int nIn = (int)GetNInputs(), nOut = (int)GetNOutputs();
   // BPTT: d_i = (W[nIn:nIn+nOut] d_{i-1}) .* y_{t-i}(1 - y_{t-i}), y_{t-i} = y part of history row i-1 --
-  // one tnet_gemv_rows launch per step.  TNET_RNN_BPTT_CHAIN=1 (opt-in): all `order` steps in one launch
-  // where the shape allows (tnet_rnn_bptt_chain, bit-identical) -- MEASURED SLOWER on MI355X: 35.7 k vs
-  // 45.4 k frames/s at 135 senones, 30.4 k vs 36.6 k at 4000 (profiles/r04_rnn_chain_ab.json): each step's
-  // all-to-all granule hand-off across the 8-16 workgroups costs more than the launch boundary it removes
-  // (MI355X_MICROARCH.md's allgather / boundary rows: 2.4-4 vs 1.45 us)
-  const bool chain = ChainEnabled();
-  int st = TNET_ERR_UNSUPPORTED;
-  if (chain && mChainWs && mBpttOrder > 0)
-    st = tnet_rnn_bptt_chain(mLinearity.pCUData(), (int)mLinearity.Stride(), nIn, nOut, mDiff.pCUData(),
-                             (int)mDiff.Stride(), mBpttOrder, mInputHistory.pCUData(), (int)mInputHistory.Stride(),
-                             mHead, (int)mInputHistory.Rows(), nIn, mChainWs, S);
-  if (st != TNET_ERR_UNSUPPORTED) {
-    TNET_SAFE_CALL(st);
-  } else {
-    for (int i = 1; i <= mBpttOrder; i++)
-      TNET_SAFE_CALL(tnet_gemv_rows(mLinearity.pCUData(), (int)mLinearity.Stride(), nIn, nOut, nOut,
-                                    mDiff.pCURowData((size_t)i - 1), mDiff.pCURowData((size_t)i), 0.0f,
-                                    HistRow(i - 1) + nIn, S));
-  }
+  // one tnet_gemv_rows launch per step.  (Round 4's one-launch chain of the `order` steps, epoch-tagged granule
+  // hand-offs, was measured slower -- 35.7 k vs 45.4 k frames/s at 135 senones, profiles/r04_rnn_chain_ab.json:
+  // each step's all-to-all hand-off costs more than the launch boundary -- and is gone since round 6.)
+  for (int i = 1; i <= mBpttOrder; i++)
+    TNET_SAFE_CALL(tnet_gemv_rows(mLinearity.pCUData(), (int)mLinearity.Stride(), nIn, nOut, nOut,
+                                  mDiff.pCURowData((size_t)i - 1), mDiff.pCURowData((size_t)i), 0.0f,
+                                  HistRow(i - 1) + nIn, S));
   if (defer) {
     mPending = true;
     mPendHead = mHead;
@@ -222,8 +178,6 @@ CuRecurrentTrainer::~CuRecurrentTrainer() {
   (void)hipStreamSynchronize(CuDevice::Instantiate().Stream());
   if (mSmx) (void)hipFree(mSmx);
   if (mArgKey) (void)hipFree(mArgKey);
-  if (mXbuf) (void)hipFree(mXbuf);
-  if (mErrFlag) (void)hipFree(mErrFlag);
   for (auto& kv : mGraphs) DestroyExecs(kv.second);
 }
 
@@ -258,21 +212,13 @@ void CuRecurrentTrainer::TrainUtterance(const float* feats, size_t rows, size_t 
   // reset the history context (TRecurrentCu.cc:351-356)
   for (int i = 0; i < mNet->Layers(); i++)
     if (mNet->Layer(i).GetType() == CuComponent::RECURRENT) dynamic_cast<CuRecurrent&>(mNet->Layer(i)).ClearHistory();
-  const bool fused = FusedFrameOk();
-  if (fused && TrainUtterancePersistent(rows)) {
-    mFrames += (long)rows;
-    return;
-  }
-  if (fused) {
+  if (FusedFrameOk()) {
     // per-frame argmax keys of this utterance, read by tnet_argmax_correct at its end
     Scratch(mArgKey, mArgKeyBytes, rows * sizeof(unsigned long long));
     TNET_HIP_CALL(hipMemsetAsync(mArgKey, 0, rows * sizeof(unsigned long long), CuDevice::Instantiate().Stream()));
     RunFrames(rows);
     TNET_SAFE_CALL(tnet_argmax_correct((const unsigned long long*)mArgKey, mLabels.pCUData(), (int)rows,
                                        (int)mNet->GetNOutputs(), mObj->DeviceStats(), S));
-    if (CuRecurrent::ChainEnabled())  // one flag read per utterance and recurrent layer, opt-in chain only
-      for (int i = 0; i < mNet->Layers(); i++)
-        if (mNet->Layer(i).GetType() == CuComponent::RECURRENT) dynamic_cast<CuRecurrent&>(mNet->Layer(i)).CheckChain();
     mFrames += (long)rows;
     return;
   }
@@ -392,55 +338,9 @@ void CuRecurrentTrainer::RunFrames(size_t rows) {
   g.head_after = rec.Head();
 }
 
-// TRecurrentCu.cc:346-371 for one utterance in one launch: the frames' forward, cross-entropy,
-// output-layer backprop + SGD, BPTT and recurrent update on workgroups that keep the weights in LDS
-// (rnn_persistent.hip).  Opt-in (TNET_RNN_PERSIST=1): MEASURED SLOWER than the per-frame launch
-// chain (TrainFrameFused) -- 61-62 us a frame vs ~35 us: the seven in-launch hand-offs a frame cost
-// 2.5-6.6 us each (write-through granules polled across XCDs), as much as the launch boundaries they
-// replace (tools/rnn_stamps.py).
-bool CuRecurrentTrainer::TrainUtterancePersistent(size_t rows) {
-  const char* e = getenv("TNET_RNN_PERSIST");
-  if (!e || e[0] != '1') return false;
-  auto& rec = dynamic_cast<CuRecurrent&>(mNet->Layer(0));
-  auto& lin = dynamic_cast<CuBiasedLinearity&>(mNet->Layer(1));
-  const int nIn = (int)rec.GetNInputs(), H = (int)lin.GetNInputs(), N = (int)lin.GetNOutputs();
-  const int bptt = rec.GetBpttOrder();
-  if (bptt < 0 || bptt > 8) return false;
-  hipStream_t st = CuDevice::Instantiate().Stream();
-  Scratch(mArgKey, mArgKeyBytes, rows * sizeof(unsigned long long));
-  TNET_HIP_CALL(hipMemsetAsync(mArgKey, 0, rows * sizeof(unsigned long long), st));
-  const size_t xb = (size_t)tnet_rnn_utterance_workspace(H, N, 256);
-  if (xb > mXbufBytes) {
-    Scratch(mXbuf, mXbufBytes, xb);
-    TNET_HIP_CALL(hipMemsetAsync(mXbuf, 0, xb, st));  // no stale tag can match (tags only grow)
-  }
-  if (!mErrFlag) TNET_HIP_CALL(hipMalloc((void**)&mErrFlag, sizeof(int)));
-  TNET_HIP_CALL(hipMemsetAsync(mErrFlag, 0, sizeof(int), st));
-  rec.Output().Init(1, (size_t)H);  // y_{-1}: zero after ClearHistory
-  float oscale, ol2;
-  lin.UpdateConstants(1, &oscale, &ol2);
-  const bool ommt = lin.Momentum() != 0.0f;
-  const int stt = tnet_rnn_utterance(
-      mFeats.pCUData(), (int)rows, nIn, (int)mFeats.Stride(), mLabels.pCUData(), rec.Linearity().pCUData(),
-      (int)rec.Linearity().Stride(), rec.Bias().pCUData(), rec.BiasCorrection().pCUData(), H,
-      lin.Linearity().pCUData(), (int)lin.Linearity().Stride(), lin.Bias().pCUData(),
-      ommt ? lin.LinearityCorrection().pCUData() : nullptr, (int)lin.LinearityCorrection().Stride(),
-      ommt ? lin.BiasCorrection().pCUData() : nullptr, N, bptt, rec.LearnRate(), rec.Momentum(), rec.Weightcost(),
-      oscale, lin.Momentum(), ol2, rec.Output().pCUData(), mObj->DeviceStats(), (unsigned long long*)mArgKey,
-      mXbuf, mEpoch, mCrossval ? 0 : 1, mErrFlag, st);
-  if (stt == TNET_ERR_UNSUPPORTED) return false;
-  TNET_SAFE_CALL(stt);
-  mEpoch += 16u * (unsigned)rows + 16u;
-  TNET_SAFE_CALL(tnet_argmax_correct((const unsigned long long*)mArgKey, mLabels.pCUData(), (int)rows, N,
-                                     mObj->DeviceStats(), st));
-  mObj->AddFrames(rows);
-  int err = 0;
-  TNET_HIP_CALL(hipMemcpyAsync(&err, mErrFlag, sizeof(int), hipMemcpyDeviceToHost, st));
-  TNET_HIP_CALL(hipStreamSynchronize(st));
-  if (err) Error("CuRecurrentTrainer: persistent utterance kernel timed out waiting for a workgroup hand-off");
-  return true;
-}
-
+// (Round 2's whole utterance as ONE persistent launch, rnn_persistent.hip, weights in LDS and in-launch granule
+// hand-offs, was measured slower than the per-frame launch chain -- 61-62 us a frame vs ~35 us, the hand-offs
+// 2.5-6.6 us each -- and is gone since round 6.)
 bool CuRecurrentTrainer::FusedFrameOk() const {
   const char* generic = getenv("TNET_RNN_GENERIC");  // 1: the component-by-component chain (tests)
   if (generic && generic[0] == '1') return false;

@@ -30,12 +30,8 @@ class CuRecurrent : public CuUpdatableComponent {
       : CuUpdatableComponent(nInputs, nOutputs, pPred), mLinearity(nInputs + nOutputs, nOutputs), mBias(nOutputs),
         mBiasCorrection(nOutputs) {}
 
-  ~CuRecurrent() override;
   ComponentType GetType() const override { return RECURRENT; }
   const char* GetName() const override { return "<recurrent>"; }
-  /// Throws if the one-launch BPTT chain (tnet_rnn_bptt_chain) reported a timed-out hand-off (synchronises).
-  void CheckChain() const;
-  static bool ChainEnabled();  // TNET_RNN_BPTT_CHAIN=1: the opt-in one-launch BPTT chain
 
   void PropagateFnc(const CuMatrix<BaseFloat>& X, CuMatrix<BaseFloat>& Y) override;
   void BackpropagateFnc(const CuMatrix<BaseFloat>& X, CuMatrix<BaseFloat>& Y) override;
@@ -80,8 +76,6 @@ class CuRecurrent : public CuUpdatableComponent {
   CuMatrix<BaseFloat> mLinearity;
   CuVector<BaseFloat> mBias, mBiasCorrection;
   CuMatrix<BaseFloat> mInputHistory;  // ring of bptt+2 rows [x, y_prev] (the update reads bptt+1)
-  void* mChainWs = nullptr;            // tnet_rnn_bptt_chain's control words + granule slots
-  size_t mChainBytes = 0;
   CuMatrix<BaseFloat> mDiff;          // [bptt+1 x nOut] back-propagated errors of the present update
   CuMatrix<BaseFloat> mDiffTmp;       // [1 x nOut]
   int mBpttOrder = -1;
@@ -118,12 +112,6 @@ class CuRecurrentTrainer {
   void* mArgKey = nullptr;
   size_t mArgKeyBytes = 0;
   void* Scratch(void*& p, size_t& have, size_t bytes);
-  // the whole utterance as one persistent launch (tnet_rnn_utterance); false: not applicable
-  bool TrainUtterancePersistent(size_t rows);
-  void* mXbuf = nullptr;
-  size_t mXbufBytes = 0;
-  int* mErrFlag = nullptr;
-  unsigned mEpoch = 0;
   // the utterance's fused frame chain recorded as hipGraphs and replayed (TNET_RNN_GRAPH=0: off):
   // one entry per utterance length; a key is recorded the second time it is seen (a length seen once
   // runs eagerly) and replayed from the third on.  The chain is cut into segments of at most

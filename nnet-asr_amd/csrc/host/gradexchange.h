@@ -18,7 +18,7 @@ class CuUpdatableComponent;
 
 class GradExchange {
  public:
-  virtual ~GradExchange() {}
+  virtual ~GradExchange();
   virtual int Rank() const = 0;
   virtual int WorldSize() const = 0;
   /// Called after comp.ComputeGradient() was enqueued on the compute stream: start reducing
@@ -95,24 +95,24 @@ class GradExchange {
   }
   void SetStepRows(size_t rows) { mStepRows = rows; }
 
-  // ---- reduction check (bench.py rccl_check): armed for one step, every submitted gradient block is copied to
-  // the host right before its reduction (this rank's local gradient) and right after it (the reduced values over
-  // the ranges this rank applies, NaN elsewhere), so the caller can sum the local copies over another transport
-  // and compare.  Synchronous: for a check step outside any timed region.
+  // ---- reduction check (bench.py rccl_check): armed for one step, every submitted gradient block is copied on the
+  // DEVICE right before its reduction (this rank's local gradient: a D2D copy enqueued on the stream the reduction
+  // runs on, after its wait for the gradient kernels -- the exact bytes RCCL reads) and right after it (the reduced
+  // values, on the same stream behind the collective).  No host synchronisation inside the step, so the armed step
+  // runs the production schedule; the copies are read back when the caller asks for them (Captured(), after the
+  // step), the reduced ones restricted to the ranges this rank applies (NaN elsewhere).
   struct CapturedBlock {
     std::vector<float> local, reduced;
   };
-  void ArmCapture(bool on) {
-    mCaptureArmed = on;
-    if (on) mCaptured.clear();
-  }
-  const std::vector<CapturedBlock>& Captured() const { return mCaptured; }
+  void ArmCapture(bool on);
+  /// the armed step's blocks in submission order (synchronises the device and reads the copies back once)
+  const std::vector<CapturedBlock>& Captured();
   /// the communicator's rank count as the transport reports it (ncclCommCount for RCCL)
   virtual int TransportRanks() const { return WorldSize(); }
 
  protected:
-  /// Submit's halves of the capture (no-ops unless armed; `stream` orders the copies after the gradient kernels
-  /// and after the reduction respectively)
+  /// Submit's halves of the capture (no-ops unless armed; `stream` is the stream the reduction is enqueued on:
+  /// CaptureLocal right after its wait for the gradient kernels, CaptureReduced right behind the collective)
   /// (CaptureLocal returns the index of comp's first captured block, which CaptureReduced takes)
   size_t CaptureLocal(CuUpdatableComponent& comp, void* stream);
   void CaptureReduced(CuUpdatableComponent& comp, void* stream, size_t first);
@@ -121,6 +121,17 @@ class GradExchange {
 
  private:
   size_t mStepRows = 0;
+  // one captured block: its device copies (local, reduced) and the ranges this rank applied
+  struct DeviceCapture {
+    float* local = nullptr;
+    float* reduced = nullptr;
+    long n = 0, cap = 0;
+    long lo[2] = {0, 0}, hi[2] = {0, 0};
+    int nr = 0;
+  };
+  std::vector<DeviceCapture> mDevCap;  // buffers kept across arms (allocated on the first armed step)
+  size_t mNumCaptured = 0;
+  bool mCapturePending = false;        // device copies not yet read back
   std::vector<CapturedBlock> mCaptured;
 };
 

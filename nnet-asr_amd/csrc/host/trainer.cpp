@@ -31,12 +31,7 @@ CuTrainer::CuTrainer(CuNetwork* net, CuObjectiveFunction* obj, const TrainerOpti
   mCache.Trace(mOpt.trace);
 }
 
-CuTrainer::~CuTrainer() {
-  if (mAheadStream) (void)hipStreamSynchronize(mAheadStream);
-  for (hipEvent_t e : {mMark, mGathered})
-    if (e) (void)hipEventDestroy(e);
-  if (mAheadStream) (void)hipStreamDestroy(mAheadStream);
-}
+CuTrainer::~CuTrainer() {}
 
 // The next bunch's gather handed to the network for the step's last launch (CuNetwork::SetTailGather).
 // Finish(): if no launch carried it, launch it now (checked).  If the step throws first, the destructor
@@ -72,37 +67,15 @@ struct TailGatherGuard {
 
 void CuTrainer::Step() {
   hipStream_t cs = CuDevice::Instantiate().Stream();
-  if (mAhead) {  // gathered during the previous step
+  if (mAhead) {  // gathered by the previous step's last launch, in compute-stream order (no wait)
     mCur ^= 1;
-    if (mAheadOnStream) TNET_HIP_CALL(hipStreamWaitEvent(cs, mGathered, 0));
     mAhead = false;
   } else {
     mCache.GetBunchLabels(mFeatsB[mCur], mLabelsB[mCur]);
   }
-  // the next bunch of the fill into the other buffer, beside this step's kernels: the gather stream
-  // first waits for everything queued on the compute stream so far (the previous step, which read
-  // that buffer; the buffer allocations; the permutation upload and the fill wait)
-  // Opt-in (TNET_GATHER_AHEAD=1): measured SLOWER on MI355X -- MLP3 9.7 M vs 11.0 M frames/s, dnn4
-  // 939 k vs 952 k: the cross-stream wait per step and the gather's workgroups beside the step's
-  // GEMMs cost more than the 6 us gather they take off the chain
-  static const bool ahead = getenv("TNET_GATHER_AHEAD") && getenv("TNET_GATHER_AHEAD")[0] == '1';
-  if (ahead && mCache.HasBunchAhead()) {
-    if (!mAheadStream) {
-      TNET_HIP_CALL(hipStreamCreateWithFlags(&mAheadStream, hipStreamNonBlocking));
-      TNET_HIP_CALL(hipEventCreateWithFlags(&mMark, hipEventDisableTiming));
-      TNET_HIP_CALL(hipEventCreateWithFlags(&mGathered, hipEventDisableTiming));
-    }
-    CuMatrix<BaseFloat>& nf = mFeatsB[mCur ^ 1];
-    CuVector<int>& nl = mLabelsB[mCur ^ 1];
-    nf.Init(mCache.Bunchsize(), mFeatsB[mCur].Cols());
-    nl.Init(mCache.Bunchsize());
-    TNET_HIP_CALL(hipEventRecord(mMark, cs));
-    TNET_HIP_CALL(hipStreamWaitEvent(mAheadStream, mMark, 0));
-    mCache.GatherAheadLabels(nf, nl, mAheadStream);
-    TNET_HIP_CALL(hipEventRecord(mGathered, mAheadStream));
-    mAhead = true;
-    mAheadOnStream = true;
-  }
+  // (round 2's form, the next bunch gathered on a stream of its own beside the step, was measured slower --
+  // MLP3 9.7 M vs 11.0 M frames/s, dnn4 939 k vs 952 k: the per-step cross-stream wait -- and is gone since
+  // round 6; profiles/r02_* keep the A/B)
   // On by default (TNET_GATHER_TAIL=0 turns it off): the next bunch of the fill is gathered into the other
   // buffer by the step's LAST weight-update launch, on the CUs its tiles leave free
   // (tnet_affine_update_bias_gather) -- in stream order, so no cross-stream wait, and one launch less per
@@ -120,7 +93,6 @@ void CuTrainer::Step() {
     // (data parallel: the network launches it right behind its last gradient GEMM, beside the exchange)
     guard.Arm(mCache.AheadGather(nf, nl), !mOpt.crossval);
     mAhead = true;
-    mAheadOnStream = false;
   }
   mNet->TrainBunch(mFeatsB[mCur], mLabelsB[mCur], *mObj, !mOpt.crossval, mOpt.crossval ? nullptr : mExchange);
   guard.Finish();
@@ -332,33 +304,72 @@ void HostExchange::GatherParams(CuUpdatableComponent& comp, int i, void* stream)
   }
 }
 
-size_t GradExchange::CaptureLocal(CuUpdatableComponent& comp, void* stream) {
-  const size_t first = mCaptured.size();
-  if (!mCaptureArmed) return first;
-  TNET_HIP_CALL(hipStreamSynchronize((hipStream_t)stream));
-  for (auto& b : comp.GradientBlocks()) {
-    CapturedBlock c;
-    c.local.resize((size_t)b.n);
-    TNET_HIP_CALL(hipMemcpy(c.local.data(), b.grad, (size_t)b.n * sizeof(float), hipMemcpyDeviceToHost));
-    mCaptured.push_back(std::move(c));
+void GradExchange::ArmCapture(bool on) {
+  mCaptureArmed = on;
+  if (on) {
+    mNumCaptured = 0;
+    mCapturePending = false;
+    mCaptured.clear();
   }
+}
+
+size_t GradExchange::CaptureLocal(CuUpdatableComponent& comp, void* stream) {
+  const size_t first = mNumCaptured;
+  if (!mCaptureArmed) return first;
+  for (auto& b : comp.GradientBlocks()) {
+    if (mNumCaptured == mDevCap.size()) mDevCap.emplace_back();
+    DeviceCapture& c = mDevCap[mNumCaptured++];
+    if (c.cap < b.n) {  // first armed step (or a larger block): hipMalloc does not synchronise the streams
+      if (c.local) TNET_HIP_CALL(hipFree(c.local));
+      if (c.reduced) TNET_HIP_CALL(hipFree(c.reduced));
+      c.local = c.reduced = nullptr;
+      TNET_HIP_CALL(hipMalloc(&c.local, (size_t)b.n * sizeof(float)));
+      TNET_HIP_CALL(hipMalloc(&c.reduced, (size_t)b.n * sizeof(float)));
+      c.cap = b.n;
+    }
+    c.n = b.n;
+    c.nr = ApplyRanges(b.n, c.lo, c.hi);
+    TNET_HIP_CALL(hipMemcpyAsync(c.local, b.grad, (size_t)b.n * sizeof(float), hipMemcpyDeviceToDevice,
+                                 (hipStream_t)stream));
+  }
+  mCapturePending = true;
   return first;
 }
 
 void GradExchange::CaptureReduced(CuUpdatableComponent& comp, void* stream, size_t first) {
   if (!mCaptureArmed) return;
-  TNET_HIP_CALL(hipStreamSynchronize((hipStream_t)stream));
   size_t k = first;
   for (auto& b : comp.GradientBlocks()) {
-    if (k >= mCaptured.size()) Error("GradExchange: capture out of step with the submitted blocks");
-    std::vector<float> all((size_t)b.n);
-    TNET_HIP_CALL(hipMemcpy(all.data(), b.grad, (size_t)b.n * sizeof(float), hipMemcpyDeviceToHost));
-    CapturedBlock& c = mCaptured[k++];
-    c.reduced.assign((size_t)b.n, std::numeric_limits<float>::quiet_NaN());
-    long lo[2], hi[2];
-    const int nr = ApplyRanges(b.n, lo, hi);
-    for (int r = 0; r < nr; r++)
-      std::copy(all.begin() + lo[r], all.begin() + hi[r], c.reduced.begin() + lo[r]);
+    if (k >= mNumCaptured || mDevCap[k].n != b.n) Error("GradExchange: capture out of step with the submitted blocks");
+    TNET_HIP_CALL(hipMemcpyAsync(mDevCap[k++].reduced, b.grad, (size_t)b.n * sizeof(float), hipMemcpyDeviceToDevice,
+                                 (hipStream_t)stream));
+  }
+}
+
+const std::vector<GradExchange::CapturedBlock>& GradExchange::Captured() {
+  if (!mCapturePending) return mCaptured;
+  TNET_HIP_CALL(hipDeviceSynchronize());  // after the armed step: every copy on every stream has landed
+  mCaptured.assign(mNumCaptured, CapturedBlock{});
+  std::vector<float> all;
+  for (size_t i = 0; i < mNumCaptured; ++i) {
+    const DeviceCapture& d = mDevCap[i];
+    CapturedBlock& c = mCaptured[i];
+    c.local.resize((size_t)d.n);
+    all.resize((size_t)d.n);
+    TNET_HIP_CALL(hipMemcpy(c.local.data(), d.local, (size_t)d.n * sizeof(float), hipMemcpyDeviceToHost));
+    TNET_HIP_CALL(hipMemcpy(all.data(), d.reduced, (size_t)d.n * sizeof(float), hipMemcpyDeviceToHost));
+    c.reduced.assign((size_t)d.n, std::numeric_limits<float>::quiet_NaN());
+    for (int r = 0; r < d.nr; r++)
+      std::copy(all.begin() + d.lo[r], all.begin() + d.hi[r], c.reduced.begin() + d.lo[r]);
+  }
+  mCapturePending = false;
+  return mCaptured;
+}
+
+GradExchange::~GradExchange() {
+  for (auto& c : mDevCap) {
+    if (c.local) (void)hipFree(c.local);
+    if (c.reduced) (void)hipFree(c.reduced);
   }
 }
 
@@ -531,9 +542,11 @@ void RcclExchange::Submit(CuUpdatableComponent& comp) {
                               mImpl->comm_stream));
   }
   NCCL_CALL(ncclGroupEnd());
+  // armed: the reduced copy sits in the comm stream's order before ar_done, so nothing that waits for this
+  // reduction (the apply, the next step's gradient GEMM writing G again) can run before it has read G
+  CaptureReduced(comp, mImpl->comm_stream, first);
   TNET_HIP_CALL(hipEventRecord(mImpl->ar_done[idx], mImpl->comm_stream));
   mImpl->ar_seq[idx] = ++mImpl->comm_seq;
-  CaptureReduced(comp, mImpl->comm_stream, first);
 }
 
 // The step's whole reduction on the compute stream (GradExchange::SubmitInline): all-reduce only (the sharded form

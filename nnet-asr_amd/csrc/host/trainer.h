@@ -81,15 +81,12 @@ class CuTrainer {
   GradExchange* mExchange = nullptr;
   CuCache mCache;
   Rng48 mRng;
-  // bunch buffers: with TNET_GATHER_AHEAD=1 the step trains buffer mCur while the next shuffled bunch
-  // of the fill is gathered into the other one on mAheadStream (measured slower: off by default)
+  // bunch buffers: the step trains buffer mCur while its last launch gathers the next shuffled bunch of the
+  // fill into the other one (CuNetwork::SetTailGather)
   CuMatrix<BaseFloat> mFeatsB[2];
   CuVector<int> mLabelsB[2];
   int mCur = 0;
-  bool mAhead = false;        // buffer mCur ^ 1 holds the next bunch (gathered ahead)
-  bool mAheadOnStream = false;  // ... gathered on mAheadStream (else in compute-stream order: no wait)
-  hipStream_t mAheadStream = nullptr;
-  hipEvent_t mMark = nullptr, mGathered = nullptr;
+  bool mAhead = false;        // buffer mCur ^ 1 holds the next bunch (gathered ahead, in stream order)
   CuNetwork* mTransform = nullptr;
   size_t mStartExt = 0, mEndExt = 0;
   std::vector<float> mExtHost;

@@ -85,12 +85,8 @@ struct GemmP {
   long kstepA, kstepB, slabC;
   int early_issue;  // gemm16_kernel prologue: issue all S ring slots before the first wait (TNET_GEMM_EARLY)
   int wt;           // gemm16_kernel epilogue: 16-B output stores write-through (sc1) (TNET_GEMM_WT)
-  // in-launch split-K combine (gemm16_kernel EPI_T >= kEpiInLaunch): the last slice of a tile to
-  // finish sums the tile's slices (C is the slice workspace, rows of ldc) and applies the epilogue
-  // into C2 / ldc2 with alpha2 / beta2; the other epilogue operands are the fields above
+  // per-tile counters (stream-K pieces, split2): see those kernels
   unsigned* tile_cnt;
-  float* C2; long ldc2;
-  float alpha2, beta2;
   // EPI_BIAS_SIG_BIN: sampled states [M x N] (row stride ldbin) and the four HybridTaus state arrays,
   // indexed row * ldc + col like the probabilities C (the reference indexes them with C's MatrixDim)
   float* bin; long ldbin;
@@ -289,16 +285,6 @@ __device__ __forceinline__ void combine4(const GemmP& p, const float* __restrict
   }
 }
 
-// every 4-column group of the BMxBN tile at (bm, bn), NT threads (the in-launch split-K combine)
-template <int EPI>
-__device__ void combine_tile_t(const GemmP& r, const float* P, long slab, int splits, int ldp, int bm, int bn,
-                               int BM, int BN, int NT) {
-  const int q = BN / 4;
-  for (int u = threadIdx.x; u < BM * q; u += NT) {
-    const int row = bm + u / q, col = bn + 4 * (u % q);
-    if (row < r.M && col < r.N) combine4<EPI>(r, P, slab, splits, ldp, row, col);
-  }
-}
 // EPI_BIAS_SIG_BIN: after the tile's probabilities are stored, the workgroup reads them back (its own
 // stores: drained + barrier) with every element's four generator states, draws U and writes the
 // sampled state and the advanced generator states (rand.hip rand_kernel<2>'s arithmetic per element)
@@ -694,9 +680,6 @@ __device__ __forceinline__ void lds_vec(const float* p, float (&x)[4]) {
 //     slot of tile t.  MEASURED SLOWER (2048^2 main loop 185k vs 149k cycles): the issue cost is paid
 //     by the loader's SIMD, whose compute wave then trails the other three at every seam barrier --
 //     kept as one config (m64x128k64s2L) for the record, not chosen by the heuristic.
-// EPI_T >= kEpiInLaunch: a split-K slice kernel (EPI_STORE into the workspace) whose tiles' last
-// slices combine the slices with epilogue EPI_T - kEpiInLaunch inside the launch
-constexpr int kEpiInLaunch = 32;
 // EPI_T >= kEpiStreamK: a stream-K piece (gemm16_sk_kernel) whose tile epilogue is EPI_T - kEpiStreamK
 constexpr int kEpiStreamK = 64;
 // PX (exact prefetch): the tile grid covers M x N exactly and the epilogue operands are 16-B aligned
@@ -715,8 +698,7 @@ constexpr int gemm16_smem_floats() {
 template <int BM, int BN, int BK, int WM, int WN, int S, int SP, bool A_KC, bool B_KC, int EPI_T, bool PX>
 __device__ __forceinline__ void gemm16_body(const GemmP& p_in, float* __restrict__ smem, const int bid_x) {
   constexpr bool SKM = EPI_T >= kEpiStreamK;
-  constexpr bool INL = !SKM && EPI_T >= kEpiInLaunch;
-  constexpr int EPI = SKM ? EPI_T - kEpiStreamK : INL ? EPI_STORE : EPI_T;  // the tile epilogue
+  constexpr int EPI = SKM ? EPI_T - kEpiStreamK : EPI_T;  // the tile epilogue
   GemmP p = p_in;
   if (!SKM && p.ksplit > 1) {
     const long z = blockIdx.y;
@@ -1888,47 +1870,6 @@ __device__ __forceinline__ void gemm16_body(const GemmP& p_in, float* __restrict
   }
   }
   if constexpr (EPI == EPI_BIAS_SIG_BIN) binarize_tile<BM, BN, NT>(p, bm, bn);
-  if constexpr (INL) {
-    // ---- in-launch split-K combine (cdna_hip_programming.md section 5, 'In-launch split-K
-    // reduction', the Guideline 16 counter form): every wave drains its slice stores, one lane
-    // releases at agent scope and draws a ticket; the tile's last slice acquires and combines all
-    // slices in slice order (the combine kernel's arithmetic), whatever XCDs the slices ran on
-    constexpr int EPI_C = EPI_T - kEpiInLaunch;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __attribute__((address_space(1))) unsigned* cnt =
-          (__attribute__((address_space(1))) unsigned*)(p.tile_cnt + bid_x);
-      const unsigned ticket = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const bool last = ticket == (unsigned)(p.ksplit - 1);
-      if (last) {
-        __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // ready for the next launch
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-      smem[0] = last ? 1.f : 0.f;  // broadcast through the ring array (no second __shared__ object)
-    }
-    __syncthreads();
-    if (smem[0] != 0.f) {
-      GemmP r = p_in;
-      r.C = p_in.C2;
-      r.ldc = p_in.ldc2;
-      r.alpha = p_in.alpha2;
-      r.beta = p_in.beta2;
-      r.wt = 0;  // plain stores (the descriptor offsets are not checked for this path)
-      combine_tile_t<epi_base(EPI_C)>(r, p_in.C, p_in.slabC, p_in.ksplit, (int)p_in.ldc, bm, bn, BM, BN, NT);
-      if constexpr (epi_bias_slabs(EPI_C)) {
-        // EPI_SGD_B / EPI_STORE_BG: the first tile-row's combiners also do the bias of their columns
-        if (bm == 0) {
-          BiasPre bpc;
-          bias_pre_load<BN, EPI_C == EPI_STORE_BG>(r, bn, bpc);
-          bias_pre_finish<BN, EPI_C == EPI_STORE_BG>(r, bn, bpc);
-        }
-      }
-    }
-  }
   TNET_STAMP(3);
   TNET_STAMP_RT(5);
 }
@@ -2419,11 +2360,9 @@ static int g_cfg = -2;  // -2: not initialised, -1: automatic
 static int g_group = -1;
 static int g_split = -1;  // TNET_GEMM_SPLITK: forced split-K count (diagnostics / sweeps), -1 automatic
 static int g_early = 1;   // TNET_GEMM_EARLY=0: prologue issues S-1 slots before the first wait (round-1 form)
-// TNET_SPLITK_INLAUNCH: split-K combine 0 second launch (default) | 1 in-launch <= 64 KB | 2 in-launch.
-// Measured (round 2, MLP3 shapes): the in-launch combine is SLOWER -- the 1024 x 135 update 19.0 vs
-// 14.6 us, the RBM reconstruction 256 x 440 over K = 2048 20.7 vs 14.4 us, MLP3 10.45M vs 10.96M
-// frames/s: the agent-scope release (L2 write-back) + acquire cost more than the launch boundary
-static int g_inlaunch = 0;
+// (the split-K combine is a second launch: round 2's in-launch combine by each tile's last slice was measured
+// SLOWER on every MLP3 / RBM shape -- the 1024 x 135 update 19.0 vs 14.6 us, MLP3 10.45 M vs 10.96 M frames/s, the
+// agent-scope release + acquire costing more than the launch boundary -- and is gone since round 6)
 static int g_pair = 1;  // TNET_GEMM_PAIR=0: tnet_affine_update_bwd_pair never pairs (A/B measurements)
 static int g_pre0 = 1;  // TNET_GEMM_PRE0=0: the first seam also waits for the epilogue-operand prefetch
 // CUs reserved for another kernel (RCCL's channel workgroups) while the data-parallel step's collectives
@@ -2450,18 +2389,14 @@ static int g_wt = 1;  // TNET_GEMM_WT=0: plain 16-B epilogue stores instead of w
 // Wt as GemmP::Ct (shadow_attach) and the launch paths whose kernel does not run gemm16_body's SGD epilogue (the
 // 32x32 kernel, the split-K combine, split2) drop it (shadow_drop); the entry point then records whether this
 // update of W kept its shadow (shadow_done), which tnet_weight_shadow_kept reports
-// the narrow top layer's row-block kernel (top_rows.hip): the shapes it takes, unless a configuration or split-K
-// count is forced (tests of the general GEMM's forms)
-extern "C" int tnetk_top_rows_ok(const float* X, long ldx, const float* W, long ldw, int M, int N, int K);
-extern "C" int tnetk_top_rows(const float* X, long ldx, const float* W, long ldw, const float* b, int M, int N, int K,
-                              const int* labels, float* Z, long ldz, float* Y, long ldy, float* E, long lde,
-                              double* stats, float* cpart, long ldcp, int v4, int logits_only, float* part,
-                              long ldpart, void* stream);
+// the narrow top layer's K-slice kernel (top_rows.hip): the shapes it takes, and the slices
 extern "C" int tnetk_top_rows_shape_ok(const float* X, long ldx, const float* W, long ldw, int M, int N, int K);
+extern "C" int tnetk_top_rows_partials(const float* X, long ldx, const float* W, long ldw, int M, int N, int K,
+                                       float* part, long ldpart, void* stream);
 static int forced_cfg();
 static bool upd64_direct(const GemmP& p);
 // The narrow top layer's K slices from top_rows.hip's row-block kernel (16-row blocks x 4 K slices = 256
-// workgroups, operands straight into registers, no in-launch combine) into the split-K workspace [4][M][ldp], for
+// workgroups, operands straight into registers) into the split-K workspace [4][M][ldp], for
 // the second launch that combines them -- affine_softmax_xent_kernel (tnet_affine_softmax_xent) or
 // splitk_reduce_kernel (tnet_affine_fwd: the same slices, so both give the same Z) -- instead of the 32x64 split-K
 // tiles (TNET_TOP_SPLIT=0: those)
@@ -2475,14 +2410,9 @@ static float* top_split_partials(const GemmP& p, hipStream_t st, int* ldp_out) {
   const int ldp = 16 * ((p.N + 15) / 16);
   float* ws = splitk_workspace(sizeof(float) * kTopSlices * (size_t)p.M * ldp, st);
   if (!ws) return nullptr;
-  if (tnetk_top_rows(p.A, p.lda, p.B, p.ldb, nullptr, p.M, p.N, p.K, nullptr, nullptr, 0, nullptr, 0, nullptr, 0,
-                     nullptr, nullptr, 0, 0, 2, ws, ldp, st) != TNET_OK)
-    return nullptr;
+  if (tnetk_top_rows_partials(p.A, p.lda, p.B, p.ldb, p.M, p.N, p.K, ws, ldp, st) != TNET_OK) return nullptr;
   *ldp_out = ldp;
   return ws;
-}
-static bool top_rows_ok(const GemmP& p) {
-  return forced_cfg() < 0 && g_split <= 0 && tnetk_top_rows_ok(p.A, p.lda, p.B, p.ldb, p.M, p.N, p.K);
 }
 struct WeightShadow {
   float* t;
@@ -2532,8 +2462,6 @@ static int forced_cfg() {
     if (p0) g_pre0 = atoi(p0);
     const char* wt = getenv("TNET_GEMM_WT");
     if (wt) g_wt = atoi(wt);
-    const char* il = getenv("TNET_SPLITK_INLAUNCH");
-    if (il) g_inlaunch = atoi(il);
     const char* dr = getenv("TNET_GEMM_DIRECT");
     g_direct = dr ? atoi(dr) : 4;
     const char* kc = getenv("TNET_GEMM_KC");
@@ -2712,31 +2640,20 @@ static bool launch_split2(const GemmP& p, hipStream_t st) {
 }
 
 // split-K: the K range is cut into ks slices (blockIdx.y) whose raw products A B go to the stream's
-// workspace (slice z at ws + z * slab, rows of ldp = N rounded up to 4 floats); then either the
-// tile's last slice combines them inside the launch (tile counters; 64x64 and 32x64 tiles) or
-// splitk_reduce_kernel does, in slice order, with the epilogue
+// workspace (slice z at ws + z * slab, rows of ldp = N rounded up to 4 floats); then
+// splitk_reduce_kernel combines them, in slice order, with the epilogue
 struct Partials {
   float* ws;
   long slab;
   int ldp;
 };
-template <bool A_KC, bool B_KC, int EPI2 = EPI_STORE>
-static int launch_partials(const GemmP& p, int cfg, int ks, hipStream_t st, Partials* out, bool inl = false) {
+template <bool A_KC, bool B_KC>
+static int launch_partials(const GemmP& p, int cfg, int ks, hipStream_t st, Partials* out) {
   const int ldp = (p.N + 3) & ~3;
   const long slab = (long)p.M * ldp;
   float* ws = splitk_workspace(sizeof(float) * (size_t)slab * ks, st);
   if (!ws) return TNET_ERR_RUNTIME;
   GemmP q = p;
-  if (inl) {
-    int bm, bn, kind;
-    cfg_shape(cfg, &bm, &bn, &kind);
-    q.tile_cnt = splitk_counters((size_t)cdiv(p.M, bm) * cdiv(p.N, bn), st);
-    if (!q.tile_cnt) return TNET_ERR_RUNTIME;
-    q.C2 = p.C;
-    q.ldc2 = p.ldc;
-    q.alpha2 = p.alpha;
-    q.beta2 = p.beta;
-  }
   q.K = p.K / ks;
   q.ksplit = ks;
   q.kstepA = A_KC ? (long)q.K : (long)q.K * p.lda;
@@ -2747,20 +2664,12 @@ static int launch_partials(const GemmP& p, int cfg, int ks, hipStream_t st, Part
   q.alpha = 1.f;
   q.beta = 0.f;
   bool ok = false;
-  if (inl) {
-    // in-launch combine: the split-K planner's two tile shapes only
-    if (cfg == CFG_m64x64k32s4w41)
-      ok = launch_cfg<1, 64, 64, 32, 4, 1, 4, 0, A_KC, B_KC, kEpiInLaunch + EPI2>(q, st);
-    else if (cfg == CFG_m32x64k64s2)
-      ok = launch_cfg<1, 32, 64, 64, 2, 2, 2, 0, A_KC, B_KC, kEpiInLaunch + EPI2>(q, st);
-  } else {
-    switch (cfg) {
+  switch (cfg) {
 #define X(name, KIND, BM, BN, BK, WM, WN, S, IL) \
   case CFG_##name: if (KIND == 1) ok = launch_cfg<KIND, BM, BN, BK, WM, WN, S, IL, A_KC, B_KC, EPI_STORE>(q, st); break;
-      TNET_GEMM_CFGS(X)
+    TNET_GEMM_CFGS(X)
 #undef X
-      default: break;
-    }
+    default: break;
   }
   if (!ok) return TNET_ERR_UNSUPPORTED;
   TNET_LAUNCH_CHECK();
@@ -2772,13 +2681,6 @@ template <bool A_KC, bool B_KC, int EPI>
 static int launch_splitk(const GemmP& p, int cfg, int ks, hipStream_t st) {
   shadow_drop(p);  // the combine writes no transposed shadow
   Partials pt;
-  // in-launch combine where a tile's slices are a few tens of KB (cdna_hip_programming.md section 5)
-  int bm, bn, kind;
-  cfg_shape(cfg, &bm, &bn, &kind);
-  if (g_inlaunch == 2 || (g_inlaunch == 1 && (long)ks * bm * bn * 4 <= 64 * 1024)) {
-    const int rc = launch_partials<A_KC, B_KC, EPI>(p, cfg, ks, st, &pt, true);
-    if (rc != TNET_ERR_UNSUPPORTED) return rc;  // configs without an in-launch form: second launch
-  }
   const int rc = launch_partials<A_KC, B_KC>(p, cfg, ks, st, &pt);
   if (rc) return rc;
   float* ws = pt.ws;
@@ -3121,10 +3023,6 @@ extern "C" int tnet_affine_fwd(const float* X, TnetMatrixDim dX, const float* W,
   p.bias = b;
   int st = check_common(p);
   if (st) return st;
-  // a narrow top layer (the logits of tnet_affine_softmax_xent's row-block kernel, so both give the same Z)
-  if (act == 0 && top_rows_ok(p))
-    return tnetk_top_rows(X, dX.stride, W, dW.stride, b, p.M, p.N, p.K, nullptr, Y, dY.stride, nullptr, 0, nullptr, 0,
-                          nullptr, nullptr, 0, 0, 1, nullptr, 0, stream);
   if (act == 0 && top_split_ok(p)) {  // the same slices as tnet_affine_softmax_xent, combined by splitk_reduce_kernel
     int ldp = 0;
     if (float* ws = top_split_partials(p, (hipStream_t)stream, &ldp)) {
@@ -3197,9 +3095,6 @@ extern "C" int tnet_affine_softmax_xent(const float* X, TnetMatrixDim dX, const 
   // softmax_xent_kernel's lane-to-column map: the 16-byte one where its launch would use it
   const int v4 = (p.N & 3) == 0 && (!Z || (aligned16(Z) && (strideZ & 3) == 0)) &&
                  (!Y || (aligned16(Y) && (strideY & 3) == 0)) && aligned16(E) && (strideE & 3) == 0;
-  if (top_rows_ok(p))  // up to 144 classes over K in [512, 1024]: one launch (top_rows.hip)
-    return tnetk_top_rows(X, dX.stride, W, dW.stride, b, p.M, p.N, p.K, labels, Z, strideZ, Y, strideY, E, strideE,
-                          stats, colpart, ldcolpart, v4, 0, nullptr, 0, stream);
   if (top_split_ok(p)) {  // the row-block kernel's 4 K slices, then this kernel's combine + softmax launch
     int ldp = 0;
     if (float* ws = top_split_partials(p, s, &ldp)) {
@@ -3678,10 +3573,19 @@ extern "C" int tnet_affine_update_bias_gather(const float* X, TnetMatrixDim dX, 
     return std::array<ByteSpan, 4>{span_of(q.C, q.M, q.ldc, 4), span_of(q.corr, q.M, q.ldcorr, 4),
                                    span_of(q.bvec, q.N, 1, 4), span_of(q.bcorr, q.N, 1, 4)};
   };
+  // the registered transposed shadows (written in the same pass as W) are writes of this launch too
+  shadow_attach(pa);  // every form below runs gemm16_body's epilogue: the shadows are kept
+  if (two) shadow_attach(pb);
+  const ByteSpan cta = span_of(pa.Ct, pa.N, pa.ldct, 4), ctb = span_of(two ? pb.Ct : nullptr, pb.N, pb.ldct, 4);
   const auto ra = reads(pa), rb = reads(pb);
   const auto wa = writes(pa), wb = writes(pb);
   if (!gather_independent(y, x, labels_out, labels_in, copy_from, dy, dx, {ra[0], ra[1], ra[2], rb[0], rb[1], rb[2]},
-                          {wa[0], wa[1], wa[2], wa[3], wb[0], wb[1], wb[2], wb[3]}))
+                          {wa[0], wa[1], wa[2], wa[3], wb[0], wb[1], wb[2], wb[3], cta, ctb}))
+    return TNET_ERR_ARG;
+  // a shadow may alias nothing else either update reads or writes (it is written while they run)
+  if (any_overlap({cta, ctb}, {ra[0], ra[1], ra[2], rb[0], rb[1], rb[2], wa[0], wa[1], wa[2], wa[3], wb[0], wb[1],
+                               wb[2], wb[3]}) ||
+      spans_overlap(cta, ctb))
     return TNET_ERR_ARG;
   const int c4 = (dy.cols + 3) & ~3;
   if (((uintptr_t)y & 15) || ((uintptr_t)x & 15) || (dy.stride & 3) || (dx.stride & 3) || c4 > dy.stride ||
@@ -3689,8 +3593,6 @@ extern "C" int tnet_affine_update_bias_gather(const float* X, TnetMatrixDim dX, 
     return TNET_ERR_UNSUPPORTED;
   if (forced_cfg() >= 0 || split2_on() || g_split > 0) return TNET_ERR_UNSUPPORTED;
   if (pa.M <= 0 || pa.N <= 0 || (two && (pb.M <= 0 || pb.N <= 0))) return TNET_ERR_UNSUPPORTED;
-  shadow_attach(pa);  // every form below runs gemm16_body's epilogue: the shadows are kept
-  if (two) shadow_attach(pb);
   int na, nb = 0;
   if (two && upd_mixed_ok(pa, pb)) {
     // a 2048-wide layer's update (128x128 direct) + the first layer's (64x64) + the gather
@@ -3778,6 +3680,13 @@ static int update_bwd_pair(const float* X, TnetMatrixDim dX, const float* E, Tne
   if (st) return st;
   if (bwd_t && g_reserve > 0) return TNET_ERR_UNSUPPORTED;
   shadow_attach(pu);
+  // the update's own shadow is written in this launch: the backward may neither read it (a W2t that is the
+  // updated layer's shadow would be read while it changes) nor write into it
+  if (any_overlap({span_of(pu.Ct, pu.N, pu.ldct, 4)},
+                  {span_of(pb.A, pb.M, pb.lda, 4), span_of(pb.B, bwd_t ? pb.K : pb.N, pb.ldb, 4),
+                   span_of(pb.aux, pb.M, pb.ldaux, 4), span_of(pb.C, pb.M, pb.ldc, 4),
+                   span_of(pb.cpart, tnet_colsum_slabs(pb.M), pb.ldcpart, 4)}))
+    return TNET_ERR_ARG;
   return shadow_done(pu, launch_pair_a_bwd<EPI_SGD_B>(pu, pb, (hipStream_t)stream, bwd_t));
 }
 
@@ -3967,15 +3876,12 @@ extern "C" int tnet_affine_grad(const float* X, TnetMatrixDim dX, const float* E
 
 extern "C" int tnet_gemm_config(const char* name) {
   forced_cfg();  // read the environment once, before it could override this call
-  // "<cfg>[+sk<n>][+il<m>]": a tile configuration (or "auto"), optionally a forced split-K count and
-  // the split-K combine (il0: a second launch (default), il1: in-launch where a tile's slices are <= 64 KB,
-  // il2: in-launch whatever their size; in-launch only for 64x64 / 32x64 tiles, other tiles always
-  // combine in a second launch); the combine mode stays as set until the next il suffix.
+  // "<cfg>[+sk<n>]": a tile configuration (or "auto"), optionally a forced split-K count.
   // "+rsv<R>": R CUs reserved (gemm16_sk_kernel over CUs - R workgroups for the data-parallel shapes),
   // 0 none -- as tnet_gemm_reserve, stays as set until changed; "+s2<0|1>": gemm16_split2_kernel for the
   // few-tile updates off / on (TNET_GEMM_SPLIT2), stays as set
   char base[64] = "auto";
-  int split = -1, inl = -1, rsv = -1, s2 = -1;
+  int split = -1, rsv = -1, s2 = -1;
   if (name) {
     const char* plus = strchr(name, '+');
     const size_t n = plus ? (size_t)(plus - name) : strlen(name);
@@ -3984,7 +3890,6 @@ extern "C" int tnet_gemm_config(const char* name) {
     base[n] = 0;
     while (plus) {
       if (!strncmp(plus, "+sk", 3) && atoi(plus + 3) >= 1) split = atoi(plus + 3);
-      else if (!strncmp(plus, "+il", 3) && plus[3] >= '0' && plus[3] <= '2') inl = plus[3] - '0';
       else if (!strncmp(plus, "+rsv", 4) && plus[4] >= '0' && plus[4] <= '9') rsv = atoi(plus + 4);
       else if (!strncmp(plus, "+s2", 3) && (plus[3] == '0' || plus[3] == '1')) s2 = plus[3] - '0';
       else return TNET_ERR_ARG;
@@ -3998,7 +3903,6 @@ extern "C" int tnet_gemm_config(const char* name) {
   if (cfg == -2) return TNET_ERR_ARG;
   g_cfg = cfg;
   g_split = split;
-  if (inl >= 0) g_inlaunch = inl;
   if (rsv >= 0) g_reserve = rsv;
   if (s2 >= 0) g_split2 = s2;
   return TNET_OK;

@@ -275,103 +275,6 @@ __global__ __launch_bounds__(256) void gemv_rows_kernel(const float* __restrict_
   }
 }
 
-// The BPTT chain of one frame (cuRecurrent.cc:106-145, TRecurrentCu's order 4) in ONE launch:
-//   d_i[r] = dot(W[r0 + r, 0:n], d_{i-1}) * s_i[r] (1 - s_i[r]),  i = 1 .. order,  s_i = y_{t-i} (history)
-// -- gemv_rows_kernel's lane map and arithmetic for every row (bit-identical to `order` launches of it) on
-// G = n / (4 RPW) co-resident workgroups, wave w of workgroup g owning RPW rows whose W slices stay in its
-// registers across the steps.  Step i's vector goes from the producing waves to every wave as 8-byte
-// {value, tag} granules written by one sc1 store each and read by sc1 loads (MI355X_MICROARCH.md, hand-off
-// form R2: no fence, no flag), one granule slot per step; tags are epoch * 16 + step, the epoch advanced by
-// the launch's last workgroup to finish (so graph replays never see a previous frame's granule as current).
-// Every poll is bounded: a wave that waits too long sets ctl->err and goes on (the host reports it).
-struct BpttChainCtl {
-  unsigned long long epoch, arrived;
-  int err;
-};
-template <int QN, int RPW>
-__global__ __launch_bounds__(256) void rnn_bptt_chain_kernel(const float* __restrict__ W, long ldw, int r0, int n,
-                                                             float* __restrict__ D, long ldd, int order,
-                                                             const float* __restrict__ hist, long ldh, int head, int R,
-                                                             int hoff, unsigned long long* __restrict__ gran,
-                                                             BpttChainCtl* __restrict__ ctl) {
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int row0 = (blockIdx.x * 4 + wv) * RPW;  // this wave's first row
-  const unsigned long long epoch = __hip_atomic_load(&ctl->epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  // this wave's W rows, gemv_rows_kernel's clamped 16-B loads
-  f32x4 a[RPW][QN];
-#pragma unroll
-  for (int j = 0; j < RPW; ++j) {
-    const float* row = W + (long)(r0 + row0 + j) * ldw;
-#pragma unroll
-    for (int q = 0; q < QN; ++q) a[j][q] = *reinterpret_cast<const f32x4*>(row + min(lane * 4 + 256 * q, n - 4));
-  }
-  f32x4 b[QN];
-#pragma unroll
-  for (int q = 0; q < QN; ++q) b[q] = *reinterpret_cast<const f32x4*>(D + min(lane * 4 + 256 * q, n - 4));  // d_0
-  bool timed_out = false;
-  for (int i = 1; i <= order; ++i) {
-    // y_{t-i} of this wave's rows: lane j holds row j's
-    const float* srow = hist + (long)((head + i - 1) % R) * ldh + hoff;
-    const float sv = lane < RPW ? srow[row0 + lane] : 0.f;
-    float acc[RPW];
-#pragma unroll
-    for (int j = 0; j < RPW; ++j) {
-      float t = 0.f;
-#pragma unroll
-      for (int q = 0; q < QN; ++q)
-        if (lane * 4 + 256 * q < n) t += dot4_rounded(a[j][q], b[q]);
-      acc[j] = t;
-    }
-#pragma unroll
-    for (int j = 0; j < RPW; ++j) acc[j] = wave_sum(acc[j]);
-    float o = acc[0];
-#pragma unroll
-    for (int j = 1; j < RPW; ++j)
-      if (lane == j) o = acc[j];
-    o = o * (sv * (1.f - sv));
-    const unsigned tag = (unsigned)(epoch * 16 + (unsigned long long)i);
-    if (lane < RPW) {
-      D[(long)i * ldd + row0 + lane] = o;
-      if (i < order) {
-        const unsigned long long g = ((unsigned long long)tag << 32) | __float_as_uint(o);
-        __hip_atomic_store(gran + (long)i * n + row0 + lane, g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
-    if (i == order) break;
-    // d_i for the next step: this lane's columns, granule by granule (four per 16-B chunk)
-#pragma unroll
-    for (int q = 0; q < QN; ++q) {
-      const int c = min(lane * 4 + 256 * q, n - 4);
-      const unsigned long long* gp = gran + (long)i * n + c;
-      unsigned long long v0, v1, v2, v3;
-      for (long spin = 0;; ++spin) {
-        v0 = __hip_atomic_load(gp + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        v1 = __hip_atomic_load(gp + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        v2 = __hip_atomic_load(gp + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        v3 = __hip_atomic_load(gp + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if ((unsigned)(v0 >> 32) == tag && (unsigned)(v1 >> 32) == tag && (unsigned)(v2 >> 32) == tag &&
-            (unsigned)(v3 >> 32) == tag)
-          break;
-        if (timed_out || spin > (1L << 22)) {
-          timed_out = true;
-          break;
-        }
-        __builtin_amdgcn_s_sleep(1);
-      }
-      b[q] = f32x4{__uint_as_float((unsigned)v0), __uint_as_float((unsigned)v1), __uint_as_float((unsigned)v2),
-                   __uint_as_float((unsigned)v3)};
-    }
-  }
-  if (timed_out && lane == 0) atomicOr(&ctl->err, 1);
-  // the last workgroup to finish advances the epoch for the next launch
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const unsigned long long t = __hip_atomic_fetch_add(&ctl->arrived, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (t + 1 == (epoch + 1) * (unsigned long long)gridDim.x)
-      __hip_atomic_store(&ctl->epoch, epoch + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-}
-
 // Recurrent update (cuRecurrent.cc:88-153).  Per element of W [rows x nout]:
 //   acc = sum_{i < steps} (-lr h_i[k]) d_i[c]       (the BlasGer accumulations, corr reset to 0)
 //   c   = (-lr wc) W + acc ; W = c + W
@@ -1003,44 +906,6 @@ extern "C" int tnet_gemv_rows(const float* W, int ldw, int r0, int nrows, int n,
   if (!nrows) return TNET_OK;
   gemv_rows_kernel<<<cdiv((long)nrows * 64, 256), 256, 0, (hipStream_t)stream>>>(W, ldw, r0, nrows, n, x, y, beta, s);
   TNET_LAUNCH_CHECK();
-  return TNET_OK;
-}
-
-extern "C" long tnet_rnn_bptt_chain_workspace(int n, int order) {
-  return (long)sizeof(BpttChainCtl) + 64 + (long)(order + 1) * n * 8;
-}
-
-extern "C" int tnet_rnn_bptt_chain(const float* W, int ldw, int r0, int n, float* D, int ldd, int order,
-                                   const float* hist, int ldh, int head, int R, int hoff, void* workspace,
-                                   void* stream) {
-  if (n <= 0 || order < 0 || r0 < 0 || ldw < n || ldd < n || !W || !D || !hist || R <= 0 || head < 0 || head >= R ||
-      order > R || hoff < 0 || ldh < hoff + n || !workspace)
-    return TNET_ERR_ARG;
-  if (!order) return TNET_OK;
-  // the shapes whose rows split evenly over 4-wave workgroups, rows of <= 1024 aligned floats (gemv_rows_kernel's
-  // one-round form), order < 16 (the granule tags)
-  if ((n & 3) || (ldw & 3) || (((uintptr_t)W | (uintptr_t)D) & 15) || order >= 16 || n > 1024) return TNET_ERR_UNSUPPORTED;
-  BpttChainCtl* ctl = (BpttChainCtl*)workspace;
-  unsigned long long* gran = (unsigned long long*)((char*)workspace + 64);
-  hipStream_t st = (hipStream_t)stream;
-  if (n <= 512 && n % 64 == 0)
-    rnn_bptt_chain_kernel<2, 16><<<n / 64, 256, 0, st>>>(W, ldw, r0, n, D, ldd, order, hist, ldh, head, R, hoff, gran, ctl);
-  else if (n % 32 == 0)
-    rnn_bptt_chain_kernel<4, 8><<<n / 32, 256, 0, st>>>(W, ldw, r0, n, D, ldd, order, hist, ldh, head, R, hoff, gran, ctl);
-  else
-    return TNET_ERR_UNSUPPORTED;
-  TNET_LAUNCH_CHECK();
-  return TNET_OK;
-}
-
-extern "C" int tnet_rnn_bptt_chain_error(const void* workspace, int* err, void* stream) {
-  if (!workspace || !err) return TNET_ERR_ARG;
-  // on the chain's own stream: a non-blocking stream is not ordered with a null-stream copy
-  const hipStream_t st = (hipStream_t)stream;
-  if (hipMemcpyAsync(err, &((const BpttChainCtl*)workspace)->err, sizeof(int), hipMemcpyDeviceToHost, st) !=
-          hipSuccess ||
-      hipStreamSynchronize(st) != hipSuccess)
-    return TNET_ERR_RUNTIME;
   return TNET_OK;
 }
 

@@ -414,272 +414,7 @@ __global__ __launch_bounds__(256) void softmax_xent_row4_kernel(const float* __r
   }
 }
 
-// row4's arithmetic and lane-to-column map (Y, E and the statistics identical) for R rows per 256-thread
-// block, software-pipelined: every row's loads are issued first, so row r+1's logits land while row r is
-// reduced and its error rows are stored -- the one-row block issues all its loads, then all its stores,
-// and with 4 blocks per CU every CU is in the same phase (loads, then stores: the two halves of the
-// traffic never overlap).  The label column's probability is taken from registers by the lane that owns
-// it (no dependent re-read of the logit at the end), and the three cross-wave meetings are LDS words per
-// row behind raw barriers (no memory fence: nothing in global memory is exchanged between the waves).
-template <int R, bool HAS_Y>
-__global__ __launch_bounds__(256) void softmax_xent_rows_kernel(const float* __restrict__ Z, TnetMatrixDim d,
-                                                                const int* __restrict__ labels,
-                                                                float* __restrict__ Y, int strideY,
-                                                                float* __restrict__ E, int strideE,
-                                                                double* __restrict__ stats) {
-  constexpr int CPW = SX_MAXV4 / 4;  // chunks per wave
-  __shared__ float smax[R][4];
-  __shared__ double ssum[R][4];
-  __shared__ ArgMax sarg[R][4];
-  __shared__ float syt[R];
-  __shared__ int stl[R];
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int row0 = blockIdx.x * R, N = d.cols;
-  // the class ids first: their loads are waited for before the logits' (loads retire in issue order)
-  int lab[R];
-#pragma unroll
-  for (int r = 0; r < R; ++r) lab[r] = row0 + r < d.rows ? labels[row0 + r] : -1;
-  f32x4 rv[R][CPW];
-#pragma unroll
-  for (int r = 0; r < R; ++r) {
-    const int row = row0 + r < d.rows ? row0 + r : d.rows - 1;  // a clamped tail row is computed, never stored
-    const float* src = Z + (long)row * d.stride;
-#pragma unroll
-    for (int q = 0; q < CPW; ++q) {
-      // unconditional loads (a clamped column past the row's end, masked below): no control flow between the
-      // loads, so the compiler's counted waits keep the later rows' loads in flight (N is a multiple of 4)
-      const int c = (wv + 4 * q) * 256 + lane * 4;
-      const f32x4 x = *reinterpret_cast<const f32x4*>(src + (c < N ? c : N - 4));
-      const f32x4 lo = {-1e30f, -1e30f, -1e30f, -1e30f};
-      rv[r][q] = c < N ? x : lo;
-    }
-  }
-#pragma unroll
-  for (int r = 0; r < R; ++r) {
-    if (lab[r] >= N) lab[r] = -1;  // out of range: an unlabeled row (the host intake rejects one, CheckLabels)
-    if (threadIdx.x == 0) stl[r] = lab[r];
-  }
-  // ---- row by row, end to end: row r's reductions and error stores go out while the later rows' logits
-  // (issued above) are still landing -- the compiler's counted vmcnt waits for row r's loads only
-#pragma unroll
-  for (int r = 0; r < R; ++r) {
-    float mm = -1e20f;
-#pragma unroll
-    for (int q = 0; q < CPW; ++q) mm = fmaxf(mm, fmaxf(fmaxf(rv[r][q][0], rv[r][q][1]), fmaxf(rv[r][q][2], rv[r][q][3])));
-    mm = wave_max(mm);
-    if (lane == 0) smax[r][wv] = mm;
-    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the LDS word written
-    __builtin_amdgcn_s_barrier();
-    const float m = fmaxf(fmaxf(smax[r][0], smax[r][1]), fmaxf(smax[r][2], smax[r][3]));
-    float sacc = 0.f;
-#pragma unroll
-    for (int q = 0; q < CPW; ++q) {
-      const int c = (wv + 4 * q) * 256 + lane * 4;
-      if (c < N) {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const float e = fast_exp(rv[r][q][k] - m);
-          rv[r][q][k] = e;
-          sacc += e;
-        }
-      }
-    }
-    const double ws = wave_sum_d((double)sacc);
-    if (lane == 0) ssum[r][wv] = ws;
-    __builtin_amdgcn_s_waitcnt(0xC07F);
-    __builtin_amdgcn_s_barrier();
-    const int row = row0 + r;
-    const float sum = (float)(ssum[r][0] + ssum[r][1] + ssum[r][2] + ssum[r][3]);
-    const float rsum = 1.f / sum;
-    // unconditional stores through row descriptors whose range is the row (0 bytes for a clamped tail row):
-    // the hardware drops the columns past N, so no branch separates the stores from the next row's waits
-    // (stores count in vmcnt on gfx950: a store on a conditional path would make those waits wait for it)
-    const int bytes = row < d.rows ? N * 4 : 0;
-    const __amdgpu_buffer_rsrc_t re =
-        __builtin_amdgcn_make_buffer_rsrc((void*)(E + (long)(row < d.rows ? row : 0) * strideE), (short)0, bytes,
-                                          0x00020000);
-    __amdgpu_buffer_rsrc_t ry = re;
-    if constexpr (HAS_Y)
-      ry = __builtin_amdgcn_make_buffer_rsrc((void*)(Y + (long)(row < d.rows ? row : 0) * strideY), (short)0, bytes,
-                                             0x00020000);
-    ArgMax ay{-1e20f, 0x7fffffff};
-    const int t = lab[r];
-#pragma unroll
-    for (int q = 0; q < CPW; ++q) {
-      const int c = (wv + 4 * q) * 256 + lane * 4;
-      f32x4 y, e;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        y[k] = rv[r][q][k] * rsum;  // masked columns: exp(-1e30 - m) = 0, never a maximum, never stored
-        if (c + k < N && y[k] > ay.v) { ay.v = y[k]; ay.i = c + k; }
-        e[k] = y[k] - ((c + k == t) ? 1.f : 0.f);
-        if (c + k == t) syt[r] = y[k];  // the y written for the label column (one lane of the block)
-      }
-      if constexpr (HAS_Y) st_wt(ry, c, y);
-      st_wt(re, c, e);
-    }
-    ay = wave_argmax(ay);
-    if (lane == 0) sarg[r][wv] = ay;
-  }
-  __builtin_amdgcn_s_waitcnt(0xC07F);
-  __builtin_amdgcn_s_barrier();
-  if (threadIdx.x < R && stats) {
-    const int r = threadIdx.x, row = row0 + r;
-    if (row < d.rows) {
-      ArgMax a = sarg[r][0];
-#pragma unroll
-      for (int w = 1; w < 4; ++w) a = argmax_merge(a, sarg[r][w]);
-      const int t = stl[r];
-      const int des = t >= 0 ? t : 0;  // all-zero target row: first max of zeros is column 0
-      const double xent = t >= 0 ? -(double)logf(fmaxf(syt[r], FLT_MIN)) : 0.0;
-      const int slot = row % TNET_STATS_SLOTS;  // row4's slot (its block index is the row)
-      atomicAdd(stats + 2 * slot, xent);
-      atomicAdd(stats + 2 * slot + 1, (a.i == des) ? 1.0 : 0.0);
-    }
-  }
-}
-
-// The wide-row softmax (softmax_xent_row4_kernel) and the error's 32-row slab column sums
-// (tnet_colsum_slab_sums / colsum_partial_kernel) in ONE pass: a 1024-thread workgroup per slab, whose
-// row-group g (waves 4g..4g+3) takes the slab's rows r0+g, r0+g+4, ..., r0+g+28 -- colsum_partial's row
-// sub-group g -- one at a time with row4's arithmetic and lane-to-column map (Y, E, the statistics
-// bit-identical), adding each error row into registers in that row order; the four row-groups' sums
-// meet in LDS and are added in group order (colsum_partial's order: the slab sums bit-identical too).
-// The error is formed once and never read back (the separate column-sum launch re-read 16 MB at 4000
-// senones).
-__global__ __launch_bounds__(1024) void softmax_xent_slab_kernel(const float* __restrict__ Z, TnetMatrixDim d,
-                                                                 const int* __restrict__ labels,
-                                                                 float* __restrict__ Y, int strideY,
-                                                                 float* __restrict__ E, int strideE,
-                                                                 double* __restrict__ stats,
-                                                                 float* __restrict__ colpart, long ldp) {
-  constexpr int CPW = SX_MAXV4 / 4;  // chunks per wave
-  __shared__ float smax[16];
-  __shared__ double ssum[16];
-  __shared__ ArgMax sarg[16];
-  __shared__ float red[3][SX_MAXV4 * 256];  // row-groups 1..3's column sums
-  const int lane = threadIdx.x & 63, w16 = threadIdx.x >> 6, g = w16 >> 2, wv = w16 & 3;
-  const int N = d.cols, r0 = blockIdx.x * CS_ROWS;
-  float acc[CPW][4];
-#pragma unroll
-  for (int q = 0; q < CPW; ++q)
-#pragma unroll
-    for (int k = 0; k < 4; ++k) acc[q][k] = 0.f;
-  for (int it = 0; it < CS_ROWS / 4; ++it) {
-    const int row = r0 + g + 4 * it;
-    const float* src = Z + (long)row * d.stride;
-    f32x4 rv[CPW];
-    float m = -1e20f;
-#pragma unroll
-    for (int q = 0; q < CPW; ++q) {
-      const int c = (wv + 4 * q) * 256 + lane * 4;
-      f32x4 x = {-1e30f, -1e30f, -1e30f, -1e30f};
-      if (c < N) x = *reinterpret_cast<const f32x4*>(src + c);
-      rv[q] = x;
-      m = fmaxf(m, fmaxf(fmaxf(x[0], x[1]), fmaxf(x[2], x[3])));
-    }
-    m = wave_max(m);
-    if (lane == 0) smax[w16] = m;
-    __syncthreads();
-    m = fmaxf(fmaxf(smax[4 * g], smax[4 * g + 1]), fmaxf(smax[4 * g + 2], smax[4 * g + 3]));
-    float s = 0.f;
-#pragma unroll
-    for (int q = 0; q < CPW; ++q) {
-      const int c = (wv + 4 * q) * 256 + lane * 4;
-      if (c < N) {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const float e = fast_exp(rv[q][k] - m);
-          rv[q][k] = e;
-          s += e;
-        }
-      }
-    }
-    const double ws = wave_sum_d((double)s);
-    if (lane == 0) ssum[w16] = ws;
-    __syncthreads();
-    const float sum = (float)(ssum[4 * g] + ssum[4 * g + 1] + ssum[4 * g + 2] + ssum[4 * g + 3]);
-    const float rsum = 1.f / sum;
-    int t = labels[row];
-    if (t >= N) t = -1;  // out of range: an unlabeled row (the host intake rejects one, CheckLabels)
-    float* yrow = Y ? Y + (long)row * strideY : nullptr;
-    float* erow = E + (long)row * strideE;
-    const __amdgpu_buffer_rsrc_t ry = tile_rsrc(yrow ? yrow : erow), re = tile_rsrc(erow);
-    ArgMax ay{-1e20f, 0x7fffffff};
-#pragma unroll
-    for (int q = 0; q < CPW; ++q) {
-      const int c = (wv + 4 * q) * 256 + lane * 4;
-      if (c < N) {
-        f32x4 y, e;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          y[k] = rv[q][k] * rsum;
-          if (y[k] > ay.v) { ay.v = y[k]; ay.i = c + k; }
-          e[k] = y[k] - ((c + k == t) ? 1.f : 0.f);
-          acc[q][k] += e[k];
-        }
-        if (yrow) st_wt(ry, c, y);
-        st_wt(re, c, e);
-      }
-    }
-    ay = wave_argmax(ay);
-    if (lane == 0) sarg[w16] = ay;
-    __syncthreads();
-    if (wv == 0 && lane == 0) {
-      ArgMax a = sarg[4 * g];
-#pragma unroll
-      for (int w = 1; w < 4; ++w) a = argmax_merge(a, sarg[4 * g + w]);
-      const int des = t >= 0 ? t : 0;  // all-zero target row: first max of zeros is column 0
-      double xent = 0.0;
-      if (t >= 0) {
-        const float yt = fast_exp(src[t] - m) * rsum;  // the y written for column t
-        xent = -(double)logf(fmaxf(yt, FLT_MIN));
-      }
-      if (stats) {
-        const int slot = row % TNET_STATS_SLOTS;  // row4's slot (its block index is the row)
-        atomicAdd(stats + 2 * slot, xent);
-        atomicAdd(stats + 2 * slot + 1, (a.i == des) ? 1.0 : 0.0);
-      }
-    }
-  }
-  if (g > 0) {
-#pragma unroll
-    for (int q = 0; q < CPW; ++q) {
-      const int c = (wv + 4 * q) * 256 + lane * 4;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) red[g - 1][c + k] = acc[q][k];
-    }
-  }
-  __syncthreads();
-  if (g == 0) {
-    float* dst = colpart + (long)blockIdx.x * ldp;
-#pragma unroll
-    for (int q = 0; q < CPW; ++q) {
-      const int c = (wv + 4 * q) * 256 + lane * 4;
-#pragma unroll
-      for (int k = 0; k < 4; ++k)
-        if (c + k < N) dst[c + k] = ((acc[q][k] + red[0][c + k]) + red[1][c + k]) + red[2][c + k];
-    }
-  }
-}
-
 static bool v4ok(const void* p, int stride) { return ((uintptr_t)p & 15) == 0 && (stride & 3) == 0; }
-
-extern "C" int tnet_softmax_xent_slabs(const float* Z, TnetMatrixDim dZ, const int* labels, float* Y, int strideY,
-                                       float* E, int strideE, double* stats, float* colpart, int ldcolpart,
-                                       void* stream) {
-  if (dZ.rows < 0 || dZ.cols <= 0 || !labels || !Z || !E || !colpart || ldcolpart < dZ.cols) return TNET_ERR_ARG;
-  if (!dZ.rows) return TNET_OK;
-  // row4's domain (16-B aligned rows of 1025..4096 columns) and whole 32-row slabs of the uncapped count
-  const bool v4 = (dZ.cols & 3) == 0 && v4ok(Z, dZ.stride) && (!Y || v4ok(Y, strideY)) && v4ok(E, strideE);
-  if (!v4 || dZ.cols <= 1024 || dZ.cols > SX_MAXV4 * 256 || dZ.rows % CS_ROWS != 0 ||
-      cs_slabs(dZ.rows) != dZ.rows / CS_ROWS)
-    return TNET_ERR_UNSUPPORTED;
-  softmax_xent_slab_kernel<<<dZ.rows / CS_ROWS, 1024, 0, (hipStream_t)stream>>>(Z, dZ, labels, Y, strideY, E, strideE,
-                                                                                stats, colpart, ldcolpart);
-  TNET_LAUNCH_CHECK();
-  return TNET_OK;
-}
 
 extern "C" int tnet_softmax_xent(const float* Z, TnetMatrixDim dZ, const int* labels, float* Y, int strideY, float* E,
                                  int strideE, double* stats, void* stream) {
@@ -690,24 +425,10 @@ extern "C" int tnet_softmax_xent(const float* Z, TnetMatrixDim dZ, const int* la
   // when Z == NULL, Y already holds the softmax output (read through strideY)
   TnetMatrixDim dd = dZ;
   if (!Z) dd.stride = strideY;
-  // TNET_SOFTMAX_ROWS=1|2|4: rows per block of the wide-row kernel (1, the default: softmax_xent_row4_kernel;
-  // 2 / 4: softmax_xent_rows_kernel -- MEASURED SLOWER in the dnn4 step, 9.0-9.2 us for one row a block
-  // against 9.8-9.9 for two and 11.8 for four, profiles/r04_softmax_rows_ab.json: half / a quarter of the
-  // workgroups, each row's chain no shorter)
-  static const int rows_pb = getenv("TNET_SOFTMAX_ROWS") ? atoi(getenv("TNET_SOFTMAX_ROWS")) : 1;
-  const bool wide = Z && v4 && dZ.cols > 1024 && dZ.cols <= SX_MAXV4 * 256;
-  if (wide && E && (rows_pb == 2 || rows_pb == 4)) {
-    auto launch = [&](auto kern, int R) {
-      kern<<<cdiv(dZ.rows, R), 256, 0, (hipStream_t)stream>>>(Z, dd, labels, Y, strideY, E, strideE, stats);
-    };
-    if (rows_pb == 2) {
-      if (Y) launch(softmax_xent_rows_kernel<2, true>, 2);
-      else launch(softmax_xent_rows_kernel<2, false>, 2);
-    } else {
-      if (Y) launch(softmax_xent_rows_kernel<4, true>, 4);
-      else launch(softmax_xent_rows_kernel<4, false>, 4);
-    }
-  } else if (Z && v4 && dZ.cols > 1024 && dZ.cols <= SX_MAXV4 * 256)
+  // (one row a workgroup: pipelined R-rows-a-workgroup forms measured slower in the dnn4 step, 9.8 / 11.8 vs
+  // 9.0 us, profiles/r04_softmax_rows_ab.json, and the one-pass softmax + slab sums 36.7 vs 9.8 + 6.7 us,
+  // profiles/r02_softmax_slabs_ab.txt -- both removed in round 6)
+  if (Z && v4 && dZ.cols > 1024 && dZ.cols <= SX_MAXV4 * 256)
     softmax_xent_row4_kernel<<<dZ.rows, 256, 0, (hipStream_t)stream>>>(Z, dd, labels, Y, strideY, E, strideE, stats);
   else
     softmax_xent_kernel<0><<<cdiv((long)dZ.rows * 64, 256), 256, 0, (hipStream_t)stream>>>(

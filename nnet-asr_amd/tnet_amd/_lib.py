@@ -95,8 +95,6 @@ _SIGS = {
                                             i32, vp, vp, vp, MatrixDim, vp, MatrixDim, vp, i32, vp, MatrixDim, vp, i32,
                                             vp]),
     "tnet_weight_shadow": (i32, [vp, MatrixDim, vp, i32]),
-    "tnet_top_rows_stamps": (i32, [vp]),
-    "tnet_top_rows_config": (i32, [i32, i32]),
     "tnet_weight_shadow_kept": (i32, [vp]),
     "tnet_transpose": (i32, [vp, MatrixDim, vp, i32, vp]),
     "tnet_affine_update_bias": (i32, [vp, MatrixDim, vp, MatrixDim, vp, MatrixDim, vp, i32, f32, f32, f32, vp, i32,
@@ -113,7 +111,6 @@ _SIGS = {
     "tnet_sgd_update": (i32, [vp, vp, vp, i64, f32, f32, f32, vp]),
     "tnet_bias_update": (i32, [vp, MatrixDim, vp, vp, vp, f32, f32, vp, vp]),
     "tnet_softmax_xent": (i32, [vp, MatrixDim, vp, vp, i32, vp, i32, vp, vp]),
-    "tnet_softmax_xent_slabs": (i32, [vp, MatrixDim, vp, vp, i32, vp, i32, vp, vp, i32, vp]),
     "tnet_softmax_xent_dense": (i32, [vp, MatrixDim, vp, i32, vp, i32, vp, i32, vp, vp]),
     "tnet_mse": (i32, [vp, MatrixDim, vp, i32, vp, i32, vp, vp]),
     "tnet_stats_fetch": (i32, [vp, dp, dp, vp]),
@@ -217,9 +214,6 @@ _SIGS = {
     "tnet_gemv_workspace": (i64, [i32, i32]),
     "tnet_gemv_rowvec": (i32, [vp, i32, vp, i32, vp, vp, i32, i32, vp, vp]),
     "tnet_gemv_rows": (i32, [vp, i32, i32, i32, i32, vp, vp, f32, vp, vp]),
-    "tnet_rnn_bptt_chain_workspace": (i64, [i32, i32]),
-    "tnet_rnn_bptt_chain": (i32, [vp, i32, i32, i32, vp, i32, i32, vp, i32, i32, i32, i32, vp, vp]),
-    "tnet_rnn_bptt_chain_error": (i32, [vp, vp, vp]),
     "tnet_rnn_update": (i32, [vp, i32, i32, i32, vp, i32, i32, i32, vp, i32, i32, vp, vp, f32, f32, f32, vp]),
     "tnet_affine_fwd_t": (i32, [vp, MatrixDim, vp, MatrixDim, vp, vp, MatrixDim, i32, vp]),
     "tnet_rbm_update": (i32, [vp, MatrixDim, vp, MatrixDim, vp, MatrixDim, vp, i32, f32, f32, f32, vp]),
@@ -238,10 +232,6 @@ _SIGS = {
     "tnet_gemv_rowvec_partial_update": (i32, [vp, i32, vp, i32, vp, vp, i32, i32, vp, vp, i32, i32, i32, vp, i32, i32,
                                               vp, vp, f32, f32, f32, vp]),
     "tnet_argmax_correct": (i32, [vp, vp, i32, i32, vp, vp]),
-    "tnet_rnn_utterance_workspace": (C.c_long, [i32, i32, i32]),
-    "tnet_rnn_utterance_stamps": (i32, [vp]),
-    "tnet_rnn_utterance": (i32, [vp, i32, i32, i32, vp, vp, i32, vp, vp, i32, vp, i32, vp, vp, i32, vp, i32, i32, f32,
-                                 f32, f32, f32, f32, f32, vp, vp, vp, vp, C.c_uint, i32, vp, vp]),
     "tnetF_rand": (i32, [vp, MatrixDim, vp, vp, vp, vp, vp]),
     "tnetF_gauss_rand": (i32, [vp, MatrixDim, vp, vp, vp, vp, vp]),
     "tnetF_binarize_probs": (i32, [vp, vp, vp, MatrixDim, vp]),

@@ -121,3 +121,22 @@ def test_dp_exchange_schedules_bit_identical(config):
         assert d["rccl_check"]["ok"]
         sha.append(d["replica_check"]["param_sha256_16"])
     assert sha[0] == sha[1]
+
+
+def test_bench_sharded_check_swap_at_one_rank():
+    """the second-communicator swap bench.py makes for the sharded-form check at N > 1, rehearsed
+    at one rank (--force-dp --rccl-check-shard 2): both forms' armed steps run the production schedule (device
+    captures, no host sync inside the step), both compare exactly at one rank, the trainer is handed back its own
+    communicator, and the replica checksum still runs after the swap"""
+    cmd = [sys.executable, "bench.py", "--steps", "2", "--warmup", "1", "--no-cpu-baseline", "--cache", "4096",
+           "--force-dp", "--kernel-timing", "0", "--breakdown-steps", "0", "--prewarm-ms", "0",
+           "--rccl-check-shard", "2"]
+    p = subprocess.run(cmd, cwd=REPO, capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-3000:]
+    d = _line(p.stdout)
+    c = d["rccl_check"]
+    assert set(c["modes"]) == {"all-reduce", "reduce-scatter+all-gather"}, c
+    assert c["timed_mode"] == "all-reduce" and c["modes"]["all-reduce"]["timed"]
+    for m in c["modes"].values():
+        assert m["ok"] and m["max_rel_err"] == 0.0 and m["blocks"] == 10, m
+    assert c["ok"] and c["all_modes_ok"] and d["replica_check"]["identical"]

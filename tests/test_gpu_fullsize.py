@@ -120,7 +120,6 @@ def test_rnn_1000_frame_utterances_full_size(S, monkeypatch):
     the frame chain eagerly, the second records it as a hipGraph and runs it, the third replays the
     recorded graph (curecurrent.cpp RunFrames) -- all against orc_rnn_utterance."""
     monkeypatch.delenv("TNET_RNN_GRAPH", raising=False)
-    monkeypatch.delenv("TNET_RNN_PERSIST", raising=False)
     nIn, H, bptt, lr, T = 440, 512, 4, 0.02, 1000
     rng = np.random.default_rng(S)
     layers = formats.round_trip_text(formats.gen_recurrent_init(nIn, H, S, seed=11), 9)

@@ -45,19 +45,15 @@ GEMM_CFGS = ["auto", "g64x64k32s4w4", "m64x128k32s4", "m64x128k64s3", "m64x64k32
              "m64x128c8", "m64x128c4",
              # split-K (K cut into slices + an in-order combine with the epilogue); counts that do not
              # divide K fall back to fewer slices
-             "auto+sk4", "m64x64k32s4w41+sk8", "m32x64k64s2+sk2", "m64x128k64s2+sk3",
-             # the combine inside the GEMM launch by each tile's last slice (opt-in: il1 up to 64 KB a
-             # tile, il2 whatever the slices' size; tiles other than 64x64 / 32x64 always combine in a
-             # second launch, the default il0)
-             "m64x64k32s4w41+sk2+il1", "m64x64k32s4w41+sk4+il2", "m32x64k64s2+sk8+il2", "m64x128k64s2+sk3+il2",
-             "m128x128k64s2+sk2+il2"]
+             "auto+sk4", "m64x64k32s4w41+sk8", "m32x64k64s2+sk2", "m64x128k64s2+sk3", "m64x64k32s4w41+sk2",
+             "m64x64k32s4w41+sk4", "m32x64k64s2+sk8", "m128x128k64s2+sk2"]
 
 
 @pytest.fixture(params=GEMM_CFGS)
 def gemm_cfg(request):
     check(lib().tnet_gemm_config(request.param.encode()))
     yield request.param
-    check(lib().tnet_gemm_config(b"auto+il0"))
+    check(lib().tnet_gemm_config(b"auto"))
 
 
 GEMM_SHAPES = [(1, 1, 1), (7, 5, 3), (33, 65, 31), (64, 64, 32), (130, 70, 598), (200, 135, 1024),
@@ -215,7 +211,7 @@ def test_direct_form_bit_identical_to_ring(direct, ring, kind, rows, n_in, n_out
                                                -1e-4, S()))
                 out.append(dW.numpy())
         finally:
-            check(lib().tnet_gemm_config(b"auto+il0"))
+            check(lib().tnet_gemm_config(b"auto"))
     np.testing.assert_array_equal(out[0], out[1])
 
 
@@ -230,7 +226,7 @@ def colsum_cfg(request):
     """the configurations the column-sum bwd accepts (32-row wave tiles)"""
     check(lib().tnet_gemm_config(request.param.encode()))
     yield request.param
-    check(lib().tnet_gemm_config(b"auto+il0"))
+    check(lib().tnet_gemm_config(b"auto"))
 
 
 @pytest.mark.parametrize("rows,n_in,n_out", [(16, 32, 10), (33, 64, 40), (45, 37, 50), (1024, 2048, 2048),
@@ -414,17 +410,13 @@ def test_affine_grad_bias(rows, n_in, n_out, gemm_cfg):
     np.testing.assert_array_equal(dgb.numpy().ravel(), P.astype(np.float64).sum(0).astype(np.float32))
 
 
-@pytest.fixture(params=["auto", "auto+sk4", "m64x128k64s2", "m32x64k64s2+sk2", "g64x64k32s4w4", "rows1", "rows3"])
+@pytest.fixture(params=["auto", "auto+sk4", "m64x128k64s2", "m32x64k64s2+sk2", "g64x64k32s4w4"])
 def top_cfg(request):
-    """GEMM configurations of the top layer; rows1 / rows3: the opt-in one-launch row-block kernel (top_rows.hip,
-    both B-operand variants) for the shapes it takes, the two-launch form for the rest"""
-    rows = request.param.startswith("rows")
-    check(lib().tnet_gemm_config(b"auto" if rows else request.param.encode()))
-    if rows:
-        check(lib().tnet_top_rows_config(1, int(request.param[4:])))
+    """GEMM configurations of the top layer ("auto": the K-slice kernel of top_rows.hip for the shapes it takes,
+    the general split-K tiles for the rest)"""
+    check(lib().tnet_gemm_config(request.param.encode()))
     yield request.param
-    check(lib().tnet_top_rows_config(0, 1))
-    check(lib().tnet_gemm_config(b"auto+il0"))
+    check(lib().tnet_gemm_config(b"auto"))
 
 
 @pytest.mark.parametrize("keep_y", [False, True])
@@ -691,59 +683,6 @@ def test_colsum_slab_sums(rows, cols):
     assert np.all(np.abs(P.astype(np.float64).sum(0) - E.astype(np.float64).sum(0)) <= 32 * 1.2e-7 * tot + 1e-7)
     if rows % 32 == 0:
         assert np.all(np.abs(P - slab_sums(E)) <= 32 * 1.2e-7 * slab_sums(np.abs(E)) + 1e-7)
-
-
-@pytest.mark.parametrize("rows,cols,keep_y", [(1024, 4000, False), (1024, 4000, True), (64, 1028, True),
-                                               (96, 4096, False), (32, 2048, False)])
-def test_softmax_xent_slabs_matches_two_calls(rows, cols, keep_y):
-    """tnet_softmax_xent_slabs (one workgroup per 32-row slab) vs tnet_softmax_xent +
-    tnet_colsum_slab_sums: Y, E, the statistics slots and the slab sums bit-identical; unlabeled and
-    out-of-range class ids included"""
-    Z = rnd((rows, cols), 41, 3.0)
-    lab = np.random.default_rng(42).integers(0, cols, size=rows).astype(np.int32)
-    lab[::7] = -1
-    lab[3::11] = cols + 5
-    slabs = lib().tnet_colsum_slabs(rows)
-    out = []
-    for fused in (True, False):
-        dZ, dL = DeviceArray.from_numpy(Z), DeviceArray.vector(lab)
-        dY = DeviceArray(rows, cols) if keep_y else None
-        dE = DeviceArray(rows, cols)
-        dP = DeviceArray.from_numpy(np.full((slabs, cols), np.nan, np.float32))
-        stats = DeviceArray(1, 1024, np.float64, stride=1024)
-        yp, ys = (dY.ptr, dY.stride) if keep_y else (None, 0)
-        if fused:
-            check(lib().tnet_softmax_xent_slabs(dZ.ptr, dZ.dim, dL.ptr, yp, ys, dE.ptr, dE.stride, stats.ptr, dP.ptr,
-                                                dP.stride, S()))
-        else:
-            check(lib().tnet_softmax_xent(dZ.ptr, dZ.dim, dL.ptr, yp, ys, dE.ptr, dE.stride, stats.ptr, S()))
-            check(lib().tnet_colsum_slab_sums(dE.ptr, dE.dim, dP.ptr, dP.stride, S()))
-        out.append((dY.numpy() if keep_y else None, dE.numpy(), dP.numpy(), stats.numpy()[0]))
-    (ya, ea, pa, sa), (yb, eb, pb, sb) = out
-    if keep_y:
-        np.testing.assert_array_equal(ya, yb)
-    np.testing.assert_array_equal(ea, eb)
-    np.testing.assert_array_equal(pa, pb)
-    # per-slot sums of fp64 atomics: the same addends, order free -- equal to rounding
-    np.testing.assert_allclose(sa, sb, rtol=1e-12, atol=1e-12)
-    ref = lab.copy()
-    ref[ref >= cols] = -1
-    Eref, xent, correct = orc.xent_eval(orc.softmax(Z), ref)
-    np.testing.assert_allclose(ea, Eref, rtol=2e-5, atol=1e-8)
-    assert int(round(sa[1::2].sum())) == correct
-
-
-@pytest.mark.parametrize("rows,cols", [(100, 4000), (64, 1024), (64, 4100), (64, 135)])
-def test_softmax_xent_slabs_unsupported_shapes(rows, cols):
-    """outside whole 32-row slabs of 1025..4096 columns the fused pass declines (the caller makes the
-    two calls)"""
-    dZ, dL = DeviceArray.from_numpy(rnd((rows, cols), 43)), DeviceArray.vector(np.zeros(rows, np.int32))
-    dE = DeviceArray(rows, cols)
-    dP = DeviceArray(max(1, lib().tnet_colsum_slabs(rows)), cols)
-    stats = DeviceArray(1, 1024, np.float64, stride=1024)
-    st = lib().tnet_softmax_xent_slabs(dZ.ptr, dZ.dim, dL.ptr, None, 0, dE.ptr, dE.stride, stats.ptr, dP.ptr,
-                                       dP.stride, S())
-    assert st == TNET_ERR_UNSUPPORTED
 
 
 def test_check_class_first_max_wins():

@@ -68,12 +68,9 @@ def test_recurrent_text_round_trip(tmp_path):
     np.testing.assert_allclose(back[0].W, layers[0].W, rtol=1e-5, atol=1e-7)
 
 
-@pytest.mark.parametrize("persistent", ["0", "1"])
 @pytest.mark.parametrize("bptt,mmt,wc", [(4, 0.0, 0.0), (2, 0.5, 1e-4), (0, 0.0, 0.0)])
-def test_rnn_trainer_matches_oracle(bptt, mmt, wc, persistent, monkeypatch):
-    """Two utterances through TRecurrentCu semantics (history reset per utterance); the per-frame
-    launch chain and the opt-in one-launch utterance kernel (TNET_RNN_PERSIST=1)."""
-    monkeypatch.setenv("TNET_RNN_PERSIST", persistent)
+def test_rnn_trainer_matches_oracle(bptt, mmt, wc):
+    """Two utterances through TRecurrentCu semantics (history reset per utterance), the per-frame launch chain."""
     nIn, H, Sd, lr = 24, 32, 10, 0.05
     rng = np.random.default_rng(bptt)
     layers = formats.round_trip_text(formats.gen_recurrent_init(nIn, H, Sd, seed=7), 9)
@@ -101,9 +98,8 @@ def test_rnn_trainer_matches_oracle(bptt, mmt, wc, persistent, monkeypatch):
     np.testing.assert_allclose(b2, m.b2, rtol=2e-3, atol=2e-5)
 
 
-def _train_rnn(layers, feats, labels, bptt, lr, mmt, wc, generic, crossval=False, persistent=False):
+def _train_rnn(layers, feats, labels, bptt, lr, mmt, wc, generic, crossval=False):
     os.environ["TNET_RNN_GENERIC"] = "1" if generic else "0"
-    os.environ["TNET_RNN_PERSIST"] = "1" if persistent else "0"
     try:
         net = Network.from_layers(layers)
         net.set_learn_rate(lr)
@@ -114,15 +110,12 @@ def _train_rnn(layers, feats, labels, bptt, lr, mmt, wc, generic, crossval=False
         return obj.stats(), net.recurrent_params(0), net.linear_params()[0]
     finally:
         os.environ.pop("TNET_RNN_GENERIC", None)
-        os.environ.pop("TNET_RNN_PERSIST", None)
 
 
-@pytest.mark.parametrize("persistent", [True, False])
 @pytest.mark.parametrize("S,bptt,mmt,wc", [(10, 4, 0.0, 0.0), (135, 2, 0.5, 1e-4), (4000, 4, 0.9, 0.0),
                                            (37, 0, 0.0, 1e-3), (135, 8, 0.0, 0.0)])
-def test_rnn_fused_frame_matches_component_chain(S, bptt, mmt, wc, persistent):
-    """the fused paths -- the whole utterance as one persistent launch (tnet_rnn_utterance) or the
-    per-frame launch chain -- vs the component-by-component chain (Propagate, EvaluateLabels,
+def test_rnn_fused_frame_matches_component_chain(S, bptt, mmt, wc):
+    """the fused per-frame launch chain vs the component-by-component chain (Propagate, EvaluateLabels,
     Backpropagate + Update per layer) on the same utterances"""
     nIn, H, lr = 40, 64, 0.02
     rng = np.random.default_rng(S)
@@ -130,7 +123,7 @@ def test_rnn_fused_frame_matches_component_chain(S, bptt, mmt, wc, persistent):
     feats = [rng.standard_normal((T, nIn)).astype(np.float32) for T in (50, 33)]
     labels = [rng.integers(0, S, len(f)).astype(np.int32) for f in feats]
     labels[1][::9] = -1  # unlabeled frames: zero target
-    a = _train_rnn(layers, feats, labels, bptt, lr, mmt, wc, generic=False, persistent=persistent)
+    a = _train_rnn(layers, feats, labels, bptt, lr, mmt, wc, generic=False)
     b = _train_rnn(layers, feats, labels, bptt, lr, mmt, wc, generic=True)
     (ea, fa, ca), (eb, fb, cb) = a[0], b[0]
     assert fa == fb == 83
@@ -425,41 +418,3 @@ def test_gemv_rowvec_partial_update(nIn, H, steps, R, head, mmt, wc):
     assert lib().tnet_gemv_rowvec_partial_update(dummy.ptr, 8, dummy.ptr, 8, None, dummy.ptr, 64, 8, dummy.ptr,
                                                  dummy.ptr, 64, 0, 4, dummy.ptr, 64, 4, dummy.ptr, dummy.ptr, lr,
                                                  mmt, wc, S()) != 0
-
-
-@pytest.mark.parametrize("n_in,n,order", [(440, 512, 4), (440, 512, 1), (128, 256, 6), (64, 1024, 4), (40, 768, 3)])
-def test_bptt_chain_matches_per_step_launches(n_in, n, order):
-    """tnet_rnn_bptt_chain (the frame's `order` BPTT GEMVs in one launch, step vectors handed on as
-    write-through granules) against `order` tnet_gemv_rows launches: every row of D bit for bit, over
-    several consecutive launches with a moving ring head (each launch advances the granule epoch, so a
-    stale granule of the previous launch must never be taken as current)."""
-    from tnet_amd._lib import lib as L
-    rng = np.random.default_rng(n + order)
-    K, R = n_in + n, order + 2
-    W = (0.05 * rng.standard_normal((K, n))).astype(np.float32)
-    hist = rng.random((R, K)).astype(np.float32)
-    dW, dH = DeviceArray.from_numpy(W), DeviceArray.from_numpy(hist)
-    ws_bytes = L().tnet_rnn_bptt_chain_workspace(n, order)
-    ws = DeviceArray.from_numpy(np.zeros(-(-ws_bytes // 4), np.float32))
-    st = L().tnet_stream()
-    for launch in range(5):
-        head = launch % R
-        d0 = rng.standard_normal(n).astype(np.float32) * 0.1
-        outs = []
-        for chain in (True, False):
-            D = np.zeros((order + 1, n), np.float32)
-            D[0] = d0
-            dD = DeviceArray.from_numpy(D)
-            if chain:
-                rc = L().tnet_rnn_bptt_chain(dW.ptr, dW.stride, n_in, n, dD.ptr, dD.stride, order, dH.ptr, dH.stride,
-                                             head, R, n_in, ws.ptr, st)
-                assert rc == 0, rc
-            else:
-                for i in range(1, order + 1):
-                    srow = dH.ptr + 4 * (((head + i - 1) % R) * dH.stride + n_in)
-                    assert L().tnet_gemv_rows(dW.ptr, dW.stride, n_in, n, n, dD.ptr + 4 * (i - 1) * dD.stride,
-                                              dD.ptr + 4 * i * dD.stride, 0.0, srow, st) == 0
-            outs.append(dD.numpy())
-        np.testing.assert_array_equal(outs[0], outs[1], err_msg=f"launch {launch}")
-    err = ctypes.c_int(-1)
-    assert L().tnet_rnn_bptt_chain_error(ws.ptr, ctypes.byref(err), None) == 0 and err.value == 0

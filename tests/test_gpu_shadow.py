@@ -238,3 +238,26 @@ def test_shadow_arguments():
     assert lib().tnet_weight_shadow(dW.ptr, dW.dim, dT.ptr, 3) != 0  # stride below the row count / unaligned
     _unregister(dW)
     assert lib().tnet_weight_shadow_kept(dW.ptr) < 0
+
+
+@pytest.mark.parametrize("with_dp", [0, 1])
+def test_shadow_across_training_modes(tmp_path, with_dp):
+    """ADVICE r5 (medium + low): every writer of W that does not write the transposed shadow -- the generic path's
+    one-row update (tnet_affine_update_row), the data-parallel flat apply -- leaves it stale for the next fused
+    backward, which must then re-transpose.  The same training sequence (fused, generic 1-row, fused 1-row, fused,
+    [DP on a one-rank communicator, fused]) with the shadows on (default) and off (TNET_BWD_SHADOW=0: every backward
+    NT from W) ends at the same parameters within the slab-sum reorder band (a stale shadow -- last step's weights
+    at lr 2 -- is orders of magnitude outside it).  Tolerance: |p - p0| <= 2e-4 * max|p0| per parameter block."""
+    import os
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    got = {}
+    for mode in ("2", "0"):
+        out = str(tmp_path / f"p{mode}.npz")
+        p = subprocess.run([sys.executable, os.path.join(repo, "tests", "shadow_modes_worker.py"), out, str(with_dp)],
+                           capture_output=True, text=True, timeout=300, env=dict(os.environ, TNET_BWD_SHADOW=mode))
+        assert p.returncode == 0, p.stderr[-3000:]
+        got[mode] = dict(np.load(out))
+    for k, ref in got["0"].items():
+        np.testing.assert_array_less(np.abs(got["2"][k] - ref), 2e-4 * np.abs(ref).max() + 1e-12, err_msg=k)

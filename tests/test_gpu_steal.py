@@ -42,7 +42,7 @@ def slab_sums(M, slab=32):
 def ts_cfg(request):
     check(lib().tnet_gemm_config(request.param.encode()))
     yield request.param
-    check(lib().tnet_gemm_config(b"auto+il0+rsv0"))
+    check(lib().tnet_gemm_config(b"auto+rsv0"))
 
 
 def _run(cfg, fn):
@@ -52,7 +52,7 @@ def _run(cfg, fn):
         synchronize()
         return out
     finally:
-        check(lib().tnet_gemm_config(b"auto+il0+rsv0"))
+        check(lib().tnet_gemm_config(b"auto+rsv0"))
 
 
 def test_bwd_colsum_stolen(ts_cfg):
@@ -119,7 +119,7 @@ def test_reserve_api():
 def split2():
     check(lib().tnet_gemm_config(b"auto+s21"))  # opt-in (measured slower than 64x64 tiles over the whole K)
     yield
-    check(lib().tnet_gemm_config(b"auto+il0+s20"))
+    check(lib().tnet_gemm_config(b"auto+s20"))
 
 
 @pytest.mark.parametrize("kind", ["updb", "upd", "gradb"])

@@ -45,5 +45,5 @@ for pad in (0, 64, 128, 32):
         out.append({"cfg": cfg, "row_stride_floats": no + pad, "us": round(us, 2),
                     "tflops": round(2.0 * rows * ni * no / (us * 1e-6) / 1e12, 1), "bit_identical": same})
         print(json.dumps(out[-1]), flush=True)
-check(lib().tnet_gemm_config(b"auto+il0"))
+check(lib().tnet_gemm_config(b"auto"))
 print("RESULT " + json.dumps(out))

@@ -81,8 +81,6 @@ def main():
                 env["TNET_GEMM_GROUP"] = extra[1:]
             elif extra.startswith("sk") and extra[2:].isdigit():
                 env["TNET_GEMM_SPLITK"] = extra[2:]
-            elif extra.startswith("il") and extra[2:].isdigit():
-                env["TNET_SPLITK_INLAUNCH"] = extra[2:]
             elif extra.startswith("split2_") and extra[7:].isdigit():
                 env["TNET_GEMM_SPLIT2"] = extra[7:]  # gemm16_split2_kernel for the few-tile updates
         p = subprocess.run([sys.executable, "-c", CHILD, REPO, json.dumps(shapes), str(iters)], env=env,

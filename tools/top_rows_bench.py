@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Launch-level timing of the narrow top layer (BASELINE config 2: 1024 x 1024 -> 135): tnet_affine_fwd (logits) and
 tnet_affine_softmax_xent (logits + softmax + xent + error + slab sums), back-to-back launches on the library stream,
-wall clock over `reps` launches after a warm-up (launch gaps included).  Run with TNET_TOP_ROWS=0 for the general
+wall clock over `reps` launches after a warm-up (launch gaps included).  Run with TNET_TOP_SPLIT=0 for the general
 GEMM's split-K form.  Prints one JSON line.
 
 usage: python tools/top_rows_bench.py [--rows 1024] [--n-in 1024] [--n-out 135] [--reps 400]"""
@@ -25,7 +25,6 @@ def main():
     ap.add_argument("--n-in", type=int, default=1024)
     ap.add_argument("--n-out", type=int, default=135)
     ap.add_argument("--reps", type=int, default=400)
-    ap.add_argument("--stamps", action="store_true", help="one launch of each with in-kernel s_memtime phase stamps")
     a = ap.parse_args()
     rng = np.random.default_rng(0)
     X = DeviceArray.from_numpy(rng.random((a.rows, a.n_in), dtype=np.float32))
@@ -45,7 +44,7 @@ def main():
                                              E.stride, stats.ptr, P.ptr, P.stride, S))
 
     out = {"rows": a.rows, "n_in": a.n_in, "n_out": a.n_out, "reps": a.reps,
-           "top_rows": os.environ.get("TNET_TOP_ROWS", "1")}
+           "top_split": os.environ.get("TNET_TOP_SPLIT", "1")}
     for name, fn in (("affine_fwd", fwd), ("affine_softmax_xent", fused)):
         for _ in range(50):
             fn()
@@ -55,26 +54,6 @@ def main():
             fn()
         synchronize()
         out[name + "_us"] = round(1e6 * (time.perf_counter() - t0) / a.reps, 2)
-    if a.stamps:
-        nb = (-(-a.rows // 16)) * 4
-        buf = DeviceArray(nb, 8, np.int64, stride=8)
-        for name, fn in (("affine_fwd", fwd), ("affine_softmax_xent", fused)):
-            check(lib().tnet_memset(buf.ptr, 0, buf.nbytes))
-            check(lib().tnet_top_rows_stamps(buf.ptr))
-            fn()
-            synchronize()
-            check(lib().tnet_top_rows_stamps(None))
-            st = buf.numpy().astype(np.int64)
-            t0 = st[:, 0].min()
-            ph = {}
-            for i in range(1, 6):
-                ok = st[:, i] > 0
-                if ok.any():
-                    d = st[ok, i] - st[ok, i - 1 if i != 5 else 3]
-                    ph[f"phase{i}"] = {"median_cycles": int(np.median(d)), "max_cycles": int(d.max()), "blocks": int(ok.sum())}
-            ph["start_spread_cycles"] = int(st[:, 0].max() - t0)
-            ph["end_cycles"] = int(st[:, 1:6].max() - t0)
-            out[name + "_stamps"] = ph
     print(json.dumps(out), flush=True)
 
 
