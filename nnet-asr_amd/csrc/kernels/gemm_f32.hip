@@ -710,7 +710,7 @@ __device__ __forceinline__ void gemm16_body(const GemmP& p_in, float* __restrict
   constexpr bool LDR = SP == 2;
   // SP >= 3: the direct form (no LDS ring; see the main loop), DD chunks of 16 k in flight per wave
   constexpr bool DIR = SP >= 3;
-  constexpr int DD = (SP == 3 || SP == 5 || SP == 9) ? 4 : SP == 7 ? 2 : 8;
+  constexpr int DD = (SP == 3 || SP == 5 || SP == 9 || SP == 10) ? 4 : SP == 7 ? 2 : 8;
   static_assert(SP != 1 || S >= 3, "spread DMA needs a 3-slot ring");
   constexpr int WTM = BM / WM, WTN = BN / WN;  // wave tile
   constexpr int TM = WTM / 16, TN = WTN / 16;
@@ -1218,7 +1218,19 @@ __device__ __forceinline__ void gemm16_body(const GemmP& p_in, float* __restrict
     // piece (lane 4a + b: row a, k 4b..4b+3) and each lane then takes its fragment from the lane that loaded
     // it (ds_bpermute, one per dword, issued a chunk ahead between the MFMAs): the same values in the same
     // registers, so bit-identical to the ring and to the a<D> forms
-    constexpr bool CKC = ASM && SP >= 8 && (A_KC || B_KC);
+    constexpr bool CKC = ASM && (SP == 8 || SP == 9) && (A_KC || B_KC);
+    // SP 10 (f4): the a4 forward that also writes its B operand transposed -- the weight's transposed shadow
+    // Bt[n][k] = B[k][n] into p.Ct (the top layer's, for its NN backward in the same step).  Lane (lg, li) holds
+    // B[16 c + 4 lg + s][n0 + 4 li + e] in slot register s, component e: for each e the four s are one 16-B piece
+    // of Bt row n0 + 4 li + e.  Every B fragment is loaded by the 8 row blocks x 2 wave rows of its column block;
+    // these 16 owners write each (chunk, e, lane half) piece once, ONE store per owner at the head of chunks 0
+    // and 2 of every group of 4 -- the previous or the current chunk, still in its ring slot -- so every wave
+    // issues the same one store per two chunks and the counted waits stay exact (vmcnt counts stores too, in
+    // order: one more op younger than each waited chunk, WVL).  Lanes not owning the piece (the other half, or
+    // columns past N) store out of the descriptor's range: dropped, but still one issued instruction.
+    constexpr bool FSH = SP == 10;
+    static_assert(!FSH || (ASM && A_KC && !B_KC && VN == 4 && NRB == 4 && BM == 128 && WM == 2 && DD == 4),
+                  "f4: the top forward's 128x128 a4 shape only");
     constexpr int NKC = (A_KC ? NRA : 0) + (B_KC ? NRB : 0);  // k-contiguous fragment registers per chunk
     const int rq = CKC ? lane >> 2 : li, kq = CKC ? lane & 3 : lg;  // the row and 16-B piece a lane loads
     const __amdgpu_buffer_rsrc_t rA = tile_rsrc(p.A), rB = tile_rsrc(p.B);
@@ -1258,19 +1270,40 @@ __device__ __forceinline__ void gemm16_body(const GemmP& p_in, float* __restrict
         return v;
       };
       constexpr int WV = (DD - 2) * NR;  // loads younger than a chunk's when it is consumed
-      auto wait_slot = [&](f32x4 (&q)[NR]) {
+      constexpr int WVL = FSH ? WV + 1 : WV;  // ... and in the loop of the f4 form, one shadow store
+      auto wait_slot_n = [&](f32x4 (&q)[NR], auto wtag) {
+        constexpr int W = decltype(wtag)::value;
         if constexpr (NR == 6)
           asm volatile("s_waitcnt vmcnt(%6)" : "+v"(q[0]), "+v"(q[1]), "+v"(q[2]), "+v"(q[3]), "+v"(q[4]), "+v"(q[5])
-                       : "n"(WV));
+                       : "n"(W));
         else if constexpr (NR == 8)
           asm volatile("s_waitcnt vmcnt(%8)"
                        : "+v"(q[0]), "+v"(q[1]), "+v"(q[2]), "+v"(q[3]), "+v"(q[4]), "+v"(q[5]), "+v"(q[6]), "+v"(q[7])
-                       : "n"(WV));
+                       : "n"(W));
         else
           asm volatile("s_waitcnt vmcnt(%12)"
                        : "+v"(q[0]), "+v"(q[1]), "+v"(q[2]), "+v"(q[3]), "+v"(q[4]), "+v"(q[5]), "+v"(q[6]), "+v"(q[7]),
                          "+v"(q[8]), "+v"(q[9]), "+v"(q[10]), "+v"(q[11])
-                       : "n"(WV));
+                       : "n"(W));
+      };
+      auto wait_slot = [&](f32x4 (&q)[NR]) { wait_slot_n(q, std::integral_constant<int, WV>{}); };
+      // f4: this wave's owner index, the piece it writes at each store position, its lanes' Bt offsets (bytes; out
+      // of the descriptor's range where the lane writes nothing)
+      const int f_own = FSH ? (bm / BM) * WM + wid / WN : 0;
+      const int f_e = (f_own >> 1) & 3, f_odd = f_own & 1;
+      const unsigned f_recs = FSH ? (unsigned)((long)N * p.ldct * 4) : 0u;
+      const __amdgpu_buffer_rsrc_t rT = __builtin_amdgcn_make_buffer_rsrc(FSH ? (void*)p.Ct : (void*)p.C, (short)0,
+                                                                          (int)f_recs, 0x00020000);
+      const bool f_lane = FSH && (lane >> 5) == (f_own >> 3) && bn + wn0 + 4 * li < N;
+      const long f_row = (long)(bn + wn0 + 4 * li + f_e) * p.ldct + 4 * lg;
+      auto f_pick = [&](const f32x4& q) { return f_e == 0 ? q[0] : f_e == 1 ? q[1] : f_e == 2 ? q[2] : q[3]; };
+      // the piece of chunk cc from slot register set qs (the 4 B registers of a chunk)
+      auto f_store = [&](const f32x4 (&qs)[NR], int cc) {
+        f32x4 v;
+#pragma unroll
+        for (int s2 = 0; s2 < 4; ++s2) v[s2] = f_pick(qs[NRA + s2]);
+        const int off = f_lane ? (int)((f_row + 16L * cc) * 4) : (int)f_recs;
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rT, off, 0, 16);
       };
       // CKC: lane (li, lg) takes its fragment from lane 4 li + lg; the t-th k-contiguous register of a slot
       const int pperm = 4 * (4 * li + lg);
@@ -1292,14 +1325,24 @@ __device__ __forceinline__ void gemm16_body(const GemmP& p_in, float* __restrict
 #pragma unroll
         for (int t = 0; t < NKC; ++t) perm(ring[0][kc_reg(t)]);
       }
+      if constexpr (FSH) wait_slot(ring[0]);  // chunk 0 before any store is in flight (the loop's waits are WVL)
       for (int c0 = 0; c0 < nch; c0 += DD) {
 #pragma unroll
         for (int j = 0; j < DD; ++j) {
           const int cn = min(c0 + j + DD - 1, nch - 1);  // past the end: a repeat of the last chunk, never used
           if constexpr (!CKC) {
             __builtin_amdgcn_sched_barrier(0);  // the wait stays after the previous chunk's MFMAs
-            wait_slot(ring[j]);
+            wait_slot_n(ring[j], std::integral_constant<int, WVL>{});
             __builtin_amdgcn_sched_barrier(0);
+          }
+          if constexpr (FSH) {
+            if (j == 0 || j == 2) {
+              // the previous chunk (still in its slot: this chunk's loads refill it below) or this one; chunk 0's
+              // "previous" is chunk 0 again (the same bytes written twice)
+              if (f_odd || c0 + j == 0) f_store(ring[j], c0 + j);
+              else f_store(ring[(j + DD - 1) % DD], c0 + j - 1);
+              __builtin_amdgcn_sched_barrier(0);
+            }
           }
           int mi = 0;
 #pragma unroll
@@ -1334,6 +1377,10 @@ __device__ __forceinline__ void gemm16_body(const GemmP& p_in, float* __restrict
         }
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the repeat loads of the last chunk
+      if constexpr (FSH) {  // the last chunk (nch is a multiple of DD: slot DD - 1), the owners of "previous"
+        if (f_odd == 0) f_store(ring[DD - 1], nch - 1);
+        else f_store(ring[DD - 1], nch - 1);  // (the same piece again: one store per wave, uniform code)
+      }
     } else {
     float fa[DD][TM][4], fb[DD][TN][4];
     auto gld = [&](__amdgpu_buffer_rsrc_t rs, unsigned off, int soff, float (&x)[4], auto vtag) {
@@ -2320,24 +2367,14 @@ static unsigned* splitk_counters(size_t n, hipStream_t st) {
 //       D-chunk register ring, no LDS ring)
 #define TNET_GEMM_CFGS(X)                         \
   X(g64x64k32s4w4, 0, 64, 64, 32, 2, 2, 4, 0)           \
-  X(m64x128k32s4, 1, 64, 128, 32, 2, 2, 4, 0)           \
-  X(m64x128k64s3, 1, 64, 128, 64, 2, 2, 3, 0)           \
   X(m64x64k32s4w41, 1, 64, 64, 32, 4, 1, 4, 0)          \
-  X(m128x128k32s3, 1, 128, 128, 32, 2, 2, 3, 0)         \
   X(m128x128k64s2, 1, 128, 128, 64, 2, 2, 2, 0)         \
   X(m64x128k64s2, 1, 64, 128, 64, 2, 2, 2, 0)           \
-  X(m64x128k64s2w42, 1, 64, 128, 64, 4, 2, 2, 0)        \
-  X(m64x128k64s3p, 1, 64, 128, 64, 2, 2, 3, 1)          \
-  X(m64x128k64s2L, 1, 64, 128, 64, 2, 2, 2, 2)          \
-  X(m64x128d4, 1, 64, 128, 64, 2, 2, 2, 3)              \
-  X(m64x128d8, 1, 64, 128, 64, 2, 2, 2, 4)              \
-  X(m128x128d4, 1, 128, 128, 64, 2, 2, 2, 3)            \
   X(m64x128a4, 1, 64, 128, 64, 2, 2, 2, 5)              \
   X(m64x128a8, 1, 64, 128, 64, 2, 2, 2, 6)              \
   X(m128x128a4, 1, 128, 128, 64, 2, 2, 2, 5)            \
   X(m128x256a2, 1, 128, 256, 32, 2, 2, 3, 7)            \
   X(m64x128c8, 1, 64, 128, 64, 2, 2, 2, 8)              \
-  X(m64x128c4, 1, 64, 128, 64, 2, 2, 2, 9)              \
   X(m128x256k32s3, 1, 128, 256, 32, 2, 2, 3, 0)         \
   X(m64x64k64s2, 1, 64, 64, 64, 2, 2, 2, 0)             \
   X(m64x64k32s4, 1, 64, 64, 32, 2, 2, 4, 0)             \
@@ -2375,8 +2412,10 @@ static int g_reserve = 0, g_cus = 0;
 // the direct form -- 1: m64x128a8 / m128x128a4, also the update half of the update + backward pair kernel
 // (dnn4 969.9 k -> 1006.2 k frames/s, the 2048^2 set 69.1 -> 65.6 us a launch, roofline 0.790 -> 0.832,
 // profiles/r04_gemm_direct_ab.json); 4 (default): 1 + the 128x256 update (the top layer's) as m128x256a2
-// (134.6 -> 126.3 us, dnn4 1005 k -> 1015 k, profiles/r04_gemm_direct_128x256_ab.jsonl); 2: m64x128d4 /
-// m128x128d4 (compiler-tracked loads); 3: m64x128a4 / m128x128a4; 0: the LDS ring everywhere
+// (134.6 -> 126.3 us, dnn4 1005 k -> 1015 k, profiles/r04_gemm_direct_128x256_ab.jsonl); 3: m64x128a4 /
+// m128x128a4; 0: the LDS ring everywhere.  (Round 6 removed the configurations measured never faster: the
+// compiler-tracked direct forms d4 / d8, the loader-wave and spread-DMA rings, the 8-wave 64x128, the 3-slot /
+// 32-deep ring variants and c4 -- profiles/r02_*, r04_gemm_direct_variants.jsonl keep the sweeps)
 static int g_direct = -1;
 // TNET_GEMM_KC: the backward GEMMs (k-contiguous A and B, 64x128 tiles) in the direct form with coalesced loads,
 // m64x128c8, instead of the LDS ring -- 1 (default): the top layer's (1024 x 2048 over K = 4000, with its own
@@ -2822,8 +2861,8 @@ static int launch_gemm(const GemmP& p_in, hipStream_t st) {
   if (g_direct > 0 && forced_cfg() < 0 && !B_KC) {
     // (short K -- the first layer's 440: the 4-chunk ring's shorter prologue, 19.6 vs 20.9 us, tools/gemm_sweep.py r5o)
     if (cfg == CFG_m64x128k64s2)
-      rcfg = g_direct == 2 ? CFG_m64x128d4 : (g_direct == 3 || p.K <= 512) ? CFG_m64x128a4 : CFG_m64x128a8;
-    else if (cfg == CFG_m128x128k64s2) rcfg = g_direct == 2 ? CFG_m128x128d4 : CFG_m128x128a4;
+      rcfg = (g_direct == 3 || p.K <= 512) ? CFG_m64x128a4 : CFG_m64x128a8;
+    else if (cfg == CFG_m128x128k64s2) rcfg = CFG_m128x128a4;
     else if (cfg == CFG_m128x256k32s3 && g_direct == 4) rcfg = CFG_m128x256a2;  // 4: 1 + the 128x256 update
   }
   if (g_kc >= 2 && forced_cfg() < 0 && A_KC && B_KC && cfg == CFG_m64x128k64s2) rcfg = CFG_m64x128c8;
@@ -2930,8 +2969,7 @@ static int launch_pair_a_bwd(GemmP pu, GemmP pb, hipStream_t st, bool bwd_t = fa
                        4 * ((long)pb.K * pb.ldb) < (1L << 31);
     bt = dir_b ? 1 : 2;
   }
-  if (dir && px && g_direct == 2) pair_go<EPIA, true, 3>(pu, pb, na, nb, kc, bt, st);
-  else if (dir && px) pair_go<EPIA, true, 5>(pu, pb, na, nb, kc, bt, st);
+  if (dir && px) pair_go<EPIA, true, 5>(pu, pb, na, nb, kc, bt, st);
   else if (dir) pair_go<EPIA, false, 5>(pu, pb, na, nb, kc, bt, st);
   else if (px) pair_go<EPIA, true, 0>(pu, pb, na, nb, kc, bt, st);
   else pair_go<EPIA, false, 0>(pu, pb, na, nb, kc, bt, st);
@@ -3038,6 +3076,47 @@ extern "C" int tnet_affine_fwd(const float* X, TnetMatrixDim dX, const float* W,
     case 3: return launch_gemm<true, false, EPI_BIAS_NSIG>(p, (hipStream_t)stream);
     default: return launch_gemm<true, false, EPI_BIAS>(p, (hipStream_t)stream);
   }
+}
+
+// tnet_affine_fwd(act 0) that also writes W^T into Wt [n_out x >= n_in] in the same pass (the f4 form of the
+// 128x128 direct forward: the fragments of W every workgroup loads anyway, stored once by their 16 owners between the
+// MFMAs; see gemm16_body) -- the top layer's transposed shadow for its NN backward in the same step, written where
+// the HBM is idle instead of at the end of its update's one-round grid (+12 us there, profiles/r05_bwd_shadow_ab.json).
+// Only the shape that runs m128x128a4 with 8 row blocks (the metric's bunch) and whole 64-k tiles: otherwise
+// TNET_ERR_UNSUPPORTED and nothing is enqueued.  Y is bit-identical to tnet_affine_fwd's.
+extern "C" int tnet_affine_fwd_shadow(const float* X, TnetMatrixDim dX, const float* W, TnetMatrixDim dW,
+                                      const float* b, float* Y, TnetMatrixDim dY, float* Wt, int ldwt, void* stream) {
+  if (dX.cols != dW.rows || dY.rows != dX.rows || dY.cols != dW.cols || !b || !Wt || ldwt < dW.rows)
+    return TNET_ERR_ARG;
+  static const bool on = !(getenv("TNET_FWD_SHADOW") && getenv("TNET_FWD_SHADOW")[0] == '0');
+  GemmP p{};
+  p.M = dX.rows; p.N = dW.cols; p.K = dX.cols;
+  p.A = X; p.lda = dX.stride; p.B = W; p.ldb = dW.stride; p.C = Y; p.ldc = dY.stride;
+  p.bias = b;
+  int st = check_common(p);
+  if (st) return st;
+  if (!on || forced_cfg() >= 0 || g_split > 0 || g_direct <= 0 || g_reserve > 0) return TNET_ERR_UNSUPPORTED;
+  const GemmPlan pl = plan_gemm<true>(p, epi_splittable(EPI_BIAS));
+  auto a16p = [](const void* v) { return ((uintptr_t)v & 15) == 0; };
+  if (pl.cfg != CFG_m128x128k64s2 || pl.ks != 1 || cdiv(p.M, 128) != 8 || p.K % 64 || p.K < 64 || p.N % 4 ||
+      (p.lda & 3) || (p.ldb & 3) || (ldwt & 3) || !a16p(X) || !a16p(W) || !a16p(Wt) ||
+      4L * p.M * p.lda >= (1L << 31) || 4L * p.K * p.ldb >= (1L << 31) || 4L * p.N * ldwt >= (1L << 31) ||
+      4 * ((long)p.M * p.lda) >= (1L << 32) || 4 * (64L * p.ldb + p.N) >= (1L << 32))
+    return TNET_ERR_UNSUPPORTED;
+  // Wt may alias none of the forward's operands
+  const char *t0 = (const char*)Wt, *t1 = t0 + 4L * p.N * ldwt;
+  auto hit = [&](const void* q, long bytes) { return (const char*)q < t1 && t0 < (const char*)q + bytes; };
+  if (hit(X, 4L * p.M * p.lda) || hit(W, 4L * p.K * p.ldb) || hit(Y, 4L * p.M * p.ldc) || hit(b, 4L * p.N))
+    return TNET_ERR_ARG;
+  p.group = g_group > 0 ? g_group : 8;
+  p.early_issue = g_early;
+  p.wt = g_wt;
+  p.Ct = Wt;
+  p.ldct = ldwt;
+  gemm16_kernel<128, 128, 64, 2, 2, 2, 10, true, false, EPI_BIAS>
+      <<<(unsigned)(cdiv(p.M, 128) * cdiv(p.N, 128)), 256, 0, (hipStream_t)stream>>>(p);
+  TNET_LAUNCH_CHECK();
+  return TNET_OK;
 }
 
 extern "C" int tnet_affine_fwd_sample(const float* X, TnetMatrixDim dX, const float* W, TnetMatrixDim dW,

@@ -170,15 +170,13 @@ def test_rnn_graph_replay_matches_eager(S, bptt, mmt, crossval):
         np.testing.assert_array_equal(pa[2], layers[1].W)
 
 
-@pytest.mark.parametrize("persistent", [False, True])
-def test_rnn_fused_crossval_leaves_weights(persistent):
+def test_rnn_fused_crossval_leaves_weights():
     nIn, H, S = 24, 32, 10
     rng = np.random.default_rng(5)
     layers = formats.gen_recurrent_init(nIn, H, S, seed=3)
     feats = [rng.standard_normal((40, nIn)).astype(np.float32)]
     labels = [rng.integers(0, S, 40).astype(np.int32)]
-    (e, f, c), (Wr, br), (W2, b2) = _train_rnn(layers, feats, labels, 4, 0.05, 0.0, 0.0, False, crossval=True,
-                                                  persistent=persistent)
+    (e, f, c), (Wr, br), (W2, b2) = _train_rnn(layers, feats, labels, 4, 0.05, 0.0, 0.0, False, crossval=True)
     (e2, f2, c2), _, _ = _train_rnn(layers, feats, labels, 4, 0.05, 0.0, 0.0, True, crossval=True)
     assert f == f2 == 40 and c == c2
     np.testing.assert_allclose(e, e2, rtol=1e-5)

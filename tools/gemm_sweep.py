@@ -12,8 +12,8 @@ import subprocess
 import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-CFGS = ["g64x64k32s4w4", "m64x128k64s2", "m64x128k32s4", "m64x128k64s3", "m128x128k64s2", "m128x128k32s3",
-        "m128x256k32s3", "m64x64k64s2", "m64x64k32s4", "m32x64k64s2", "m64x64k32s4w41"]
+CFGS = ["g64x64k32s4w4", "m64x128k64s2", "m128x128k64s2", "m128x256k32s3", "m64x64k64s2", "m64x64k32s4", "m32x64k64s2",
+        "m64x64k32s4w41", "m64x128a4", "m64x128a8", "m128x128a4", "m128x256a2", "m64x64a4", "m64x128c8"]
 # (kind, rows, n_in, n_out): fwd/bwd/upd of each layer of 440 -> 2048x4 -> 4000 at bunch 1024
 SHAPES = [("fwd", 1024, 2048, 2048), ("bwd", 1024, 2048, 2048), ("upd", 1024, 2048, 2048),
           ("fwd", 1024, 2048, 4000), ("bwd", 1024, 2048, 4000), ("upd", 1024, 2048, 4000),
