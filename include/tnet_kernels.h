@@ -160,14 +160,6 @@ int tnet_gemm_reserve(int cus);
  * negative-phase hidden statistics with the sign the fused update needs (tnet_rbm_update). */
 int tnet_affine_fwd(const float* X, TnetMatrixDim dX, const float* W, TnetMatrixDim dW, const float* b,
                     float* Y, TnetMatrixDim dY, int act, void* stream);
-/* tnet_affine_fwd(act 0) that also writes the weight's transpose Wt[j][i] = W[i][j] (Wt [n_out x n_in], row
- * stride ldwt >= n_in, 16-B aligned) in the same pass -- the top layer's transposed shadow for its backward
- * E W^T as an NN GEMM (tnet_affine_bwd_colsum_slabs_t) in the same step (CuBiasedLinearity::PropagateFnc +
- * BackpropagateFnc, cuBiasedLinearity.cc:11-25).  Y bit-identical to tnet_affine_fwd's.  TNET_ERR_UNSUPPORTED
- * (nothing enqueued) outside the 128x128 direct-form shapes with 897..1024 rows, n_in a multiple of 64,
- * n_out a multiple of 4; TNET_FWD_SHADOW=0: always. */
-int tnet_affine_fwd_shadow(const float* X, TnetMatrixDim dX, const float* W, TnetMatrixDim dW, const float* b,
-                           float* Y, TnetMatrixDim dY, float* Wt, int ldwt, void* stream);
 /* Y = sigmoid(X W + b) and states = (Y > U), U the HybridTaus uniforms of the per-element generator
  * states z1..z4 (advanced in place; indexed row * dY.stride + col, as CuRand indexes them with the
  * probabilities' MatrixDim): the RBM positive phase + CuRand::BinarizeProbs (cuRbm.cc:15-23,

@@ -110,7 +110,7 @@ void CuBiasedLinearity::UpdateFrom(const CuMatrix<BaseFloat>& X, const CuMatrix<
                                           mmt ? mLinearityCorrection.pCUData() : nullptr,
                                           (int)mLinearityCorrection.Stride(), mBias.pCUData(),
                                           mmt ? mBiasCorrection.pCUData() : nullptr, scale, mMomentum, l2, S));
-    mShadowValid = mFwdShadow = false;  // the rank-1 kernel writes W only
+    mShadowValid = false;  // the rank-1 kernel writes W only
     return;
   }
   // bias first: it reads only E (the weight kernel rewrites W in place)
@@ -137,7 +137,6 @@ void CuBiasedLinearity::UseShadow() {
     mLinearityT.Init(mLinearity.Cols(), mLinearity.Rows());
     mShadowValid = false;
   }
-  mFwdShadow = false;  // from here the updates keep the shadow
   // the registry is keyed by W's address: an entry under an older address (W re-initialised with other
   // dimensions) would mirror the updates of whatever matrix is allocated there next into this layer's shadow
   DropShadowKey();
@@ -153,18 +152,6 @@ void CuBiasedLinearity::DropShadowKey() {
     mShadowValid = false;
   }
   mShadowKey = nullptr;
-}
-
-bool CuBiasedLinearity::PropagateShadow(const CuMatrix<BaseFloat>& X, CuMatrix<BaseFloat>& Y) {
-  if (mShadowOn) return false;  // a registered shadow is kept by the updates instead
-  if (mLinearityT.Rows() != mLinearity.Cols() || mLinearityT.Cols() != mLinearity.Rows())
-    mLinearityT.Init(mLinearity.Cols(), mLinearity.Rows());
-  const int st = tnet_affine_fwd_shadow(X.pCUData(), X.Dim(), mLinearity.pCUData(), mLinearity.Dim(), mBias.pCUData(),
-                                        Y.pCUData(), Y.Dim(), mLinearityT.pCUData(), (int)mLinearityT.Stride(), S);
-  if (st == TNET_ERR_UNSUPPORTED) return false;
-  TNET_SAFE_CALL(st);
-  mFwdShadow = true;
-  return true;
 }
 
 const CuMatrix<BaseFloat>& CuBiasedLinearity::ShadowForBwd() {
@@ -193,7 +180,7 @@ void CuBiasedLinearity::BackpropUpdateRow(const CuMatrix<BaseFloat>& X, const Cu
                                             (int)mLinearityCorrection.Stride(), mBias.pCUData(),
                                             mmt ? mBiasCorrection.pCUData() : nullptr, scale, mMomentum, l2,
                                             Eout.pCUData(), s, d, S));
-  mShadowValid = mFwdShadow = false;
+  mShadowValid = false;
 }
 
 void CuBiasedLinearity::UpdateFromColsum(const CuMatrix<BaseFloat>& X, const CuMatrix<BaseFloat>& E,
@@ -422,7 +409,7 @@ int CuBiasedLinearity::ApplySegments(size_t frames, const GradExchange* ex, Tnet
   float l2;
   UpdateConstants(frames, scale, &l2);
   const bool mmt = mMomentum != 0.0f;
-  mShadowValid = mFwdShadow = false;  // the flat apply writes no transposed shadow
+  mShadowValid = false;  // the flat apply writes no transposed shadow
   // padding columns of W and of the gradient are zero, so the flat update keeps them zero; W and b
   // in one launch, each as the element ranges this rank applies (sharded apply: its shard + the tail)
   int nseg = 0;
@@ -487,7 +474,7 @@ void CuBiasedLinearity::ReadFromStream(std::istream& rIn) {
   }
   mLinearity.CopyFrom(BfMatrix(transpose, TRANS));
   mBias.CopyFrom(bias);
-  mShadowValid = mFwdShadow = false;
+  mShadowValid = false;
   if (mShadowOn) UseShadow();  // W's storage may have moved: re-key the registration
 }
 

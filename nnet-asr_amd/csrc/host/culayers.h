@@ -52,7 +52,7 @@ class CuBiasedLinearity : public CuUpdatableComponent {
   // ---- access for the fused network-level kernels and the C ABI (the mutable accessor marks the transposed
   // shadow stale: the caller may change W through it)
   CuMatrix<BaseFloat>& Linearity() {
-    mShadowValid = mFwdShadow = false;
+    mShadowValid = false;
     return mLinearity;
   }
   const CuMatrix<BaseFloat>& Linearity() const { return mLinearity; }
@@ -64,11 +64,6 @@ class CuBiasedLinearity : public CuUpdatableComponent {
   void UseShadow();
   const CuMatrix<BaseFloat>& ShadowForBwd();
   bool HasShadow() const { return mShadowOn; }
-  /// The forward-written shadow (a layer without a registered one: the top layer): PropagateShadow runs the
-  /// forward Y = X W + b through tnet_affine_fwd_shadow, which writes W^T into the shadow buffer in the same pass
-  /// (false: that form does not take the shape, nothing enqueued); FwdShadow() is then W^T until W changes.
-  bool PropagateShadow(const CuMatrix<BaseFloat>& X, CuMatrix<BaseFloat>& Y);
-  const CuMatrix<BaseFloat>* FwdShadow() const { return mFwdShadow ? &mLinearityT : nullptr; }
   CuVector<BaseFloat>& Bias() { return mBias; }
   CuMatrix<BaseFloat>& LinearityCorrection() { return mLinearityCorrection; }
   CuVector<BaseFloat>& BiasCorrection() { return mBiasCorrection; }
@@ -113,15 +108,11 @@ class CuBiasedLinearity : public CuUpdatableComponent {
   CuVector<BaseFloat> mGradB;
   CuMatrix<BaseFloat> mLinearityT;           ///< transposed shadow of mLinearity [nOut x nIn] (UseShadow)
   bool mShadowOn = false, mShadowValid = false;
-  bool mFwdShadow = false;                   ///< mLinearityT == W^T, written by the last forward (PropagateShadow)
   const float* mShadowKey = nullptr;         ///< the W address the shadow is registered under
   /// unregister the shadow under an address W no longer has (no-op while the registration is current)
   void DropShadowKey();
   /// after an update launch of W: the shadow is current iff that launch wrote it (tnet_weight_shadow_kept)
-  void NoteUpdate() {
-    mShadowValid = mShadowOn && tnet_weight_shadow_kept(mLinearity.pCUData()) == 1;
-    mFwdShadow = false;
-  }
+  void NoteUpdate() { mShadowValid = mShadowOn && tnet_weight_shadow_kept(mLinearity.pCUData()) == 1; }
   /// the SGD segments (W, b: this rank's ranges) of the data-parallel apply into seg (<= 4), their scale
   int ApplySegments(size_t frames, const GradExchange* ex, TnetSgdSeg* seg, float* scale);
 };

@@ -330,17 +330,6 @@ void CuNetwork::TrainBunch(const CuMatrix<BaseFloat>& X, const CuVector<int>& la
       }
     }
     KTScope kt("gemm_fwd:" + shape, 2.0 * rows * lin->GetNInputs() * lin->GetNOutputs());
-    // the top layer's forward also writes W^T, for its backward below as an NN GEMM (the hidden layers' shadows are
-    // kept by their updates; the top layer's 4000-wide update would pay ~12 us for it at the end of its one-round
-    // grid, the forward's main loop writes it for ~1 us): where a backward through the top layer follows
-    // (TNET_FWD_SHADOW=0 in the library: never)
-    if (last && shadows && l > 0 && lin != mpPropagErrorStopper &&
-        static_cast<CuBiasedLinearity*>(mNetComponents[2 * (l - 1)])->LearnRate() > 0.0f &&
-        lin->PropagateShadow(*act, dst)) {
-      act = &dst;
-      acts[l + 1] = &dst;
-      continue;
-    }
     TNET_SAFE_CALL(tnet_affine_fwd(act->pCUData(), act->Dim(), lin->LinearityRO().pCUData(), lin->LinearityRO().Dim(),
                                    lin->Bias().pCUData(), dst.pCUData(), dst.Dim(), last ? 0 : 1, S));
     act = &dst;
@@ -459,16 +448,15 @@ void CuNetwork::TrainBunch(const CuMatrix<BaseFloat>& X, const CuVector<int>& la
           if (top_slabs_ride) {  // l == nl - 1: err is the softmax error
             top_slabs_ride = false;
             CuMatrix<BaseFloat>& ct = *mColPart[nl - 1];
-            const CuMatrix<BaseFloat>* fwt = shadows && !lin->HasShadow() ? lin->FwdShadow() : nullptr;
-            const bool t = (shadows && lin->HasShadow()) || fwt;
-            const CuMatrix<BaseFloat>& wb = fwt ? *fwt : t ? lin->ShadowForBwd() : lin->LinearityRO();
+            const bool t = shadows && lin->HasShadow();
+            const CuMatrix<BaseFloat>& wb = t ? lin->ShadowForBwd() : lin->LinearityRO();
             st = (t ? tnet_affine_bwd_colsum_slabs_t : tnet_affine_bwd_colsum_slabs)(
                 err->pCUData(), err->Dim(), wb.pCUData(), wb.Dim(), acts[l]->pCUData(), (int)acts[l]->Stride(),
                 eo->pCUData(), eo->Dim(), cp.pCUData(), (int)cp.Stride(), ct.pCUData(), (int)ct.Stride(), S);
             if (st == TNET_ERR_UNSUPPORTED) err_colsum = top_slabs_launch();
           }
-          if (st == TNET_ERR_UNSUPPORTED && shadows && (lin->HasShadow() || lin->FwdShadow())) {
-            const CuMatrix<BaseFloat>& wt = lin->HasShadow() ? lin->ShadowForBwd() : *lin->FwdShadow();
+          if (st == TNET_ERR_UNSUPPORTED && shadows && lin->HasShadow()) {
+            const CuMatrix<BaseFloat>& wt = lin->ShadowForBwd();
             st = tnet_affine_bwd_colsum_t(err->pCUData(), err->Dim(), wt.pCUData(), wt.Dim(), acts[l]->pCUData(),
                                           (int)acts[l]->Stride(), eo->pCUData(), eo->Dim(), cp.pCUData(),
                                           (int)cp.Stride(), S);
@@ -501,8 +489,9 @@ void CuNetwork::TrainBunch(const CuMatrix<BaseFloat>& X, const CuVector<int>& la
     // (both grids in one round over the CUs) go out as ONE launch
     // (with the next bunch's gather on the CUs their tiles leave free, when the trainer handed one over)
     if ((stopper || l == 0) && pend.lin && !exchange && err_colsum && lin->LearnRate() > 0.0f) {
-      if (mHasTailGather && pend.lin->UpdateFromColsumGather(*pend.X, *pend.E, *mColPart[pend.l], lin, acts[l], err,
-                                                             mColPart[l].get(), mTailGather)) {
+      if (mHasTailGather && !mTailDone &&
+          pend.lin->UpdateFromColsumGather(*pend.X, *pend.E, *mColPart[pend.l], lin, acts[l], err, mColPart[l].get(),
+                                           mTailGather)) {
         mTailDone = true;
         pend.lin = nullptr;
         break;

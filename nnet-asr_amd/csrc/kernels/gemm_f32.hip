@@ -36,6 +36,7 @@
 
 #include "kcommon.h"
 #include "rbm_stats.h"
+#include "gather.h"
 
 namespace tnetk {
 
@@ -710,7 +711,7 @@ __device__ __forceinline__ void gemm16_body(const GemmP& p_in, float* __restrict
   constexpr bool LDR = SP == 2;
   // SP >= 3: the direct form (no LDS ring; see the main loop), DD chunks of 16 k in flight per wave
   constexpr bool DIR = SP >= 3;
-  constexpr int DD = (SP == 3 || SP == 5 || SP == 9 || SP == 10) ? 4 : SP == 7 ? 2 : 8;
+  constexpr int DD = (SP == 3 || SP == 5 || SP == 9) ? 4 : SP == 7 ? 2 : 8;
   static_assert(SP != 1 || S >= 3, "spread DMA needs a 3-slot ring");
   constexpr int WTM = BM / WM, WTN = BN / WN;  // wave tile
   constexpr int TM = WTM / 16, TN = WTN / 16;
@@ -1219,18 +1220,6 @@ __device__ __forceinline__ void gemm16_body(const GemmP& p_in, float* __restrict
     // it (ds_bpermute, one per dword, issued a chunk ahead between the MFMAs): the same values in the same
     // registers, so bit-identical to the ring and to the a<D> forms
     constexpr bool CKC = ASM && (SP == 8 || SP == 9) && (A_KC || B_KC);
-    // SP 10 (f4): the a4 forward that also writes its B operand transposed -- the weight's transposed shadow
-    // Bt[n][k] = B[k][n] into p.Ct (the top layer's, for its NN backward in the same step).  Lane (lg, li) holds
-    // B[16 c + 4 lg + s][n0 + 4 li + e] in slot register s, component e: for each e the four s are one 16-B piece
-    // of Bt row n0 + 4 li + e.  Every B fragment is loaded by the 8 row blocks x 2 wave rows of its column block;
-    // these 16 owners write each (chunk, e, lane half) piece once, ONE store per owner at the head of chunks 0
-    // and 2 of every group of 4 -- the previous or the current chunk, still in its ring slot -- so every wave
-    // issues the same one store per two chunks and the counted waits stay exact (vmcnt counts stores too, in
-    // order: one more op younger than each waited chunk, WVL).  Lanes not owning the piece (the other half, or
-    // columns past N) store out of the descriptor's range: dropped, but still one issued instruction.
-    constexpr bool FSH = SP == 10;
-    static_assert(!FSH || (ASM && A_KC && !B_KC && VN == 4 && NRB == 4 && BM == 128 && WM == 2 && DD == 4),
-                  "f4: the top forward's 128x128 a4 shape only");
     constexpr int NKC = (A_KC ? NRA : 0) + (B_KC ? NRB : 0);  // k-contiguous fragment registers per chunk
     const int rq = CKC ? lane >> 2 : li, kq = CKC ? lane & 3 : lg;  // the row and 16-B piece a lane loads
     const __amdgpu_buffer_rsrc_t rA = tile_rsrc(p.A), rB = tile_rsrc(p.B);
@@ -1270,40 +1259,19 @@ __device__ __forceinline__ void gemm16_body(const GemmP& p_in, float* __restrict
         return v;
       };
       constexpr int WV = (DD - 2) * NR;  // loads younger than a chunk's when it is consumed
-      constexpr int WVL = FSH ? WV + 1 : WV;  // ... and in the loop of the f4 form, one shadow store
-      auto wait_slot_n = [&](f32x4 (&q)[NR], auto wtag) {
-        constexpr int W = decltype(wtag)::value;
+      auto wait_slot = [&](f32x4 (&q)[NR]) {
         if constexpr (NR == 6)
           asm volatile("s_waitcnt vmcnt(%6)" : "+v"(q[0]), "+v"(q[1]), "+v"(q[2]), "+v"(q[3]), "+v"(q[4]), "+v"(q[5])
-                       : "n"(W));
+                       : "n"(WV));
         else if constexpr (NR == 8)
           asm volatile("s_waitcnt vmcnt(%8)"
                        : "+v"(q[0]), "+v"(q[1]), "+v"(q[2]), "+v"(q[3]), "+v"(q[4]), "+v"(q[5]), "+v"(q[6]), "+v"(q[7])
-                       : "n"(W));
+                       : "n"(WV));
         else
           asm volatile("s_waitcnt vmcnt(%12)"
                        : "+v"(q[0]), "+v"(q[1]), "+v"(q[2]), "+v"(q[3]), "+v"(q[4]), "+v"(q[5]), "+v"(q[6]), "+v"(q[7]),
                          "+v"(q[8]), "+v"(q[9]), "+v"(q[10]), "+v"(q[11])
-                       : "n"(W));
-      };
-      auto wait_slot = [&](f32x4 (&q)[NR]) { wait_slot_n(q, std::integral_constant<int, WV>{}); };
-      // f4: this wave's owner index, the piece it writes at each store position, its lanes' Bt offsets (bytes; out
-      // of the descriptor's range where the lane writes nothing)
-      const int f_own = FSH ? (bm / BM) * WM + wid / WN : 0;
-      const int f_e = (f_own >> 1) & 3, f_odd = f_own & 1;
-      const unsigned f_recs = FSH ? (unsigned)((long)N * p.ldct * 4) : 0u;
-      const __amdgpu_buffer_rsrc_t rT = __builtin_amdgcn_make_buffer_rsrc(FSH ? (void*)p.Ct : (void*)p.C, (short)0,
-                                                                          (int)f_recs, 0x00020000);
-      const bool f_lane = FSH && (lane >> 5) == (f_own >> 3) && bn + wn0 + 4 * li < N;
-      const long f_row = (long)(bn + wn0 + 4 * li + f_e) * p.ldct + 4 * lg;
-      auto f_pick = [&](const f32x4& q) { return f_e == 0 ? q[0] : f_e == 1 ? q[1] : f_e == 2 ? q[2] : q[3]; };
-      // the piece of chunk cc from slot register set qs (the 4 B registers of a chunk)
-      auto f_store = [&](const f32x4 (&qs)[NR], int cc) {
-        f32x4 v;
-#pragma unroll
-        for (int s2 = 0; s2 < 4; ++s2) v[s2] = f_pick(qs[NRA + s2]);
-        const int off = f_lane ? (int)((f_row + 16L * cc) * 4) : (int)f_recs;
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rT, off, 0, 16);
+                       : "n"(WV));
       };
       // CKC: lane (li, lg) takes its fragment from lane 4 li + lg; the t-th k-contiguous register of a slot
       const int pperm = 4 * (4 * li + lg);
@@ -1325,24 +1293,14 @@ __device__ __forceinline__ void gemm16_body(const GemmP& p_in, float* __restrict
 #pragma unroll
         for (int t = 0; t < NKC; ++t) perm(ring[0][kc_reg(t)]);
       }
-      if constexpr (FSH) wait_slot(ring[0]);  // chunk 0 before any store is in flight (the loop's waits are WVL)
       for (int c0 = 0; c0 < nch; c0 += DD) {
 #pragma unroll
         for (int j = 0; j < DD; ++j) {
           const int cn = min(c0 + j + DD - 1, nch - 1);  // past the end: a repeat of the last chunk, never used
           if constexpr (!CKC) {
             __builtin_amdgcn_sched_barrier(0);  // the wait stays after the previous chunk's MFMAs
-            wait_slot_n(ring[j], std::integral_constant<int, WVL>{});
+            wait_slot(ring[j]);
             __builtin_amdgcn_sched_barrier(0);
-          }
-          if constexpr (FSH) {
-            if (j == 0 || j == 2) {
-              // the previous chunk (still in its slot: this chunk's loads refill it below) or this one; chunk 0's
-              // "previous" is chunk 0 again (the same bytes written twice)
-              if (f_odd || c0 + j == 0) f_store(ring[j], c0 + j);
-              else f_store(ring[(j + DD - 1) % DD], c0 + j - 1);
-              __builtin_amdgcn_sched_barrier(0);
-            }
           }
           int mi = 0;
 #pragma unroll
@@ -1377,10 +1335,6 @@ __device__ __forceinline__ void gemm16_body(const GemmP& p_in, float* __restrict
         }
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the repeat loads of the last chunk
-      if constexpr (FSH) {  // the last chunk (nch is a multiple of DD: slot DD - 1), the owners of "previous"
-        if (f_odd == 0) f_store(ring[DD - 1], nch - 1);
-        else f_store(ring[DD - 1], nch - 1);  // (the same piece again: one store per wave, uniform code)
-      }
     } else {
     float fa[DD][TM][4], fb[DD][TN][4];
     auto gld = [&](__amdgpu_buffer_rsrc_t rs, unsigned off, int soff, float (&x)[4], auto vtag) {
@@ -2019,51 +1973,6 @@ void gemm16_upd_pair_kernel(const GemmP pa, const GemmP pb, const int na) {
   __shared__ __attribute__((aligned(16))) float smem[gemm16_smem_floats<BM, BN, BK, S, EPI_SGD_B, false>()];
   if ((int)blockIdx.x < na) gemm16_body<BM, BN, BK, WM, WN, S, 0, false, false, EPI_SGD_B, false>(pa, smem, blockIdx.x);
   else gemm16_body<BM, BN, BK, WM, WN, S, 0, false, false, EPI_SGD_B, false>(pb, smem, (int)blockIdx.x - na);
-}
-
-// The next bunch's gather (tnet_gather_bunch: bunch row r = cache row idx[r], its class id alongside) as
-// workgroups of the step's last update launch.  Wave w of ngb*4 takes rows w, w + ngb*4, ...; R rows at a
-// time with every 16-B load of those rows issued before the first store (the rows' idx loads before
-// that), so a wave pays two memory round trips per R rows.  c4 = cols rounded up to 4 (16-B pieces; the
-// caller checked that both strides hold them).
-struct BunchGatherP {
-  float* y;
-  const float* x;
-  int* lab_out;
-  const int* lab_in;
-  const int* idx;
-  int rows, c4;
-  long ys, xs;
-};
-__device__ __forceinline__ void bunch_gather_block(const BunchGatherP& g, const int gb, const int ngb) {
-  constexpr int R = 4, CM = 2;  // rows and 256-column pieces per lane in flight
-  const int lane = threadIdx.x & 63, nw = blockDim.x >> 6;
-  const int w0 = gb * nw + (threadIdx.x >> 6), step = ngb * nw;
-  for (int r0 = w0; r0 < g.rows; r0 += R * step) {
-    int ir[R];
-#pragma unroll
-    for (int k = 0; k < R; ++k) ir[k] = r0 + k * step < g.rows ? g.idx[r0 + k * step] : -1;
-#pragma unroll
-    for (int k = 0; k < R; ++k)
-      if (ir[k] >= 0 && lane == 0) g.lab_out[r0 + k * step] = g.lab_in[ir[k]];
-    for (int cb = lane * 4; cb < g.c4; cb += 256 * CM) {
-      f32x4 v[R][CM];
-#pragma unroll
-      for (int k = 0; k < R; ++k)
-#pragma unroll
-        for (int j = 0; j < CM; ++j)
-          if (ir[k] >= 0 && cb + 256 * j < g.c4) v[k][j] = *reinterpret_cast<const f32x4*>(g.x + ir[k] * g.xs + cb + 256 * j);
-#pragma unroll
-      for (int k = 0; k < R; ++k) {
-        if (ir[k] < 0) continue;
-        // the bunch row written through (st_wt): the next step's first GEMM reads it on every XCD
-        const __amdgpu_buffer_rsrc_t ry = tile_rsrc(g.y + (long)(r0 + k * step) * g.ys);
-#pragma unroll
-        for (int j = 0; j < CM; ++j)
-          if (cb + 256 * j < g.c4) st_wt(ry, cb + 256 * j, v[k][j]);
-      }
-    }
-  }
 }
 
 // tnet_affine_update_bias_gather: the update pair kernel's tiles (nb = 0: one update) and ng gather blocks
@@ -3078,47 +2987,6 @@ extern "C" int tnet_affine_fwd(const float* X, TnetMatrixDim dX, const float* W,
   }
 }
 
-// tnet_affine_fwd(act 0) that also writes W^T into Wt [n_out x >= n_in] in the same pass (the f4 form of the
-// 128x128 direct forward: the fragments of W every workgroup loads anyway, stored once by their 16 owners between the
-// MFMAs; see gemm16_body) -- the top layer's transposed shadow for its NN backward in the same step, written where
-// the HBM is idle instead of at the end of its update's one-round grid (+12 us there, profiles/r05_bwd_shadow_ab.json).
-// Only the shape that runs m128x128a4 with 8 row blocks (the metric's bunch) and whole 64-k tiles: otherwise
-// TNET_ERR_UNSUPPORTED and nothing is enqueued.  Y is bit-identical to tnet_affine_fwd's.
-extern "C" int tnet_affine_fwd_shadow(const float* X, TnetMatrixDim dX, const float* W, TnetMatrixDim dW,
-                                      const float* b, float* Y, TnetMatrixDim dY, float* Wt, int ldwt, void* stream) {
-  if (dX.cols != dW.rows || dY.rows != dX.rows || dY.cols != dW.cols || !b || !Wt || ldwt < dW.rows)
-    return TNET_ERR_ARG;
-  static const bool on = !(getenv("TNET_FWD_SHADOW") && getenv("TNET_FWD_SHADOW")[0] == '0');
-  GemmP p{};
-  p.M = dX.rows; p.N = dW.cols; p.K = dX.cols;
-  p.A = X; p.lda = dX.stride; p.B = W; p.ldb = dW.stride; p.C = Y; p.ldc = dY.stride;
-  p.bias = b;
-  int st = check_common(p);
-  if (st) return st;
-  if (!on || forced_cfg() >= 0 || g_split > 0 || g_direct <= 0 || g_reserve > 0) return TNET_ERR_UNSUPPORTED;
-  const GemmPlan pl = plan_gemm<true>(p, epi_splittable(EPI_BIAS));
-  auto a16p = [](const void* v) { return ((uintptr_t)v & 15) == 0; };
-  if (pl.cfg != CFG_m128x128k64s2 || pl.ks != 1 || cdiv(p.M, 128) != 8 || p.K % 64 || p.K < 64 || p.N % 4 ||
-      (p.lda & 3) || (p.ldb & 3) || (ldwt & 3) || !a16p(X) || !a16p(W) || !a16p(Wt) ||
-      4L * p.M * p.lda >= (1L << 31) || 4L * p.K * p.ldb >= (1L << 31) || 4L * p.N * ldwt >= (1L << 31) ||
-      4 * ((long)p.M * p.lda) >= (1L << 32) || 4 * (64L * p.ldb + p.N) >= (1L << 32))
-    return TNET_ERR_UNSUPPORTED;
-  // Wt may alias none of the forward's operands
-  const char *t0 = (const char*)Wt, *t1 = t0 + 4L * p.N * ldwt;
-  auto hit = [&](const void* q, long bytes) { return (const char*)q < t1 && t0 < (const char*)q + bytes; };
-  if (hit(X, 4L * p.M * p.lda) || hit(W, 4L * p.K * p.ldb) || hit(Y, 4L * p.M * p.ldc) || hit(b, 4L * p.N))
-    return TNET_ERR_ARG;
-  p.group = g_group > 0 ? g_group : 8;
-  p.early_issue = g_early;
-  p.wt = g_wt;
-  p.Ct = Wt;
-  p.ldct = ldwt;
-  gemm16_kernel<128, 128, 64, 2, 2, 2, 10, true, false, EPI_BIAS>
-      <<<(unsigned)(cdiv(p.M, 128) * cdiv(p.N, 128)), 256, 0, (hipStream_t)stream>>>(p);
-  TNET_LAUNCH_CHECK();
-  return TNET_OK;
-}
-
 extern "C" int tnet_affine_fwd_sample(const float* X, TnetMatrixDim dX, const float* W, TnetMatrixDim dW,
                                       const float* b, float* Y, TnetMatrixDim dY, float* states, int ld_states,
                                       unsigned* z1, unsigned* z2, unsigned* z3, unsigned* z4, void* stream) {
@@ -3597,7 +3465,6 @@ static bool upd64_direct(const GemmP& p) {
          p.M % 4 == 0 && p.N % 4 == 0 && !(p.lda & 3) && !(p.ldb & 3) && a16p(p.A) && a16p(p.B) &&
          4 * ((long)p.K * p.lda) < (1L << 31) && 4 * ((long)p.K * p.ldb) < (1L << 31);
 }
-}  // namespace tnetk
 
 // gemm16_upd_mixed_gather_kernel's conditions (TNET_UPD_MIXED=0: never): A is what tnet_affine_update_bias runs as
 // m128x128a4 with the exact prefetch (the planner's m128x128k64s2, unsplit, the direct-form conditions, PX), B what
@@ -3616,6 +3483,7 @@ static bool upd_mixed_ok(const GemmP& pa, const GemmP& pb) {
   if (4 * (32L * pb.lda + pb.M) >= (1L << 32) || 4 * (32L * pb.ldb + pb.N) >= (1L << 32)) return false;
   return true;
 }
+}  // namespace tnetk
 
 extern "C" int tnet_affine_update_bias_gather(const float* X, TnetMatrixDim dX, const float* E, TnetMatrixDim dE,
                                               float* W, TnetMatrixDim dW, float* corrW, int strideCorr, float scale,

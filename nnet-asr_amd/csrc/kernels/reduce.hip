@@ -325,18 +325,17 @@ __global__ __launch_bounds__(256) void rbm_stats_kernel(const float* __restrict_
 // per ROW, wave w holding 256-column chunks w, w+4, w+8, w+12 in registers; the row max / sum /
 // argmax meet through LDS.  Four waves per row keep four times the loads in flight per row and a
 // quarter of the exp / compare work per wave of the one-wave-per-row kernel (latency-bound there).
-__global__ __launch_bounds__(256) void softmax_xent_row4_kernel(const float* __restrict__ Z, TnetMatrixDim d,
-                                                                const int* __restrict__ labels,
-                                                                float* __restrict__ Y, int strideY,
-                                                                float* __restrict__ E, int strideE,
-                                                                double* __restrict__ stats) {
+__device__ __forceinline__ void softmax_xent_row4(const float* __restrict__ Z, TnetMatrixDim d,
+                                                  const int* __restrict__ labels, float* __restrict__ Y, int strideY,
+                                                  float* __restrict__ E, int strideE, double* __restrict__ stats,
+                                                  const int row) {
   constexpr int CPW = SX_MAXV4 / 4;  // chunks per wave
   __shared__ float smax[4];
   __shared__ double ssum[4];
   __shared__ ArgMax sarg[4];
   __shared__ float syt;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int row = blockIdx.x, N = d.cols;
+  const int N = d.cols;
   const float* src = Z + (long)row * d.stride;
   // the label first: its load is in flight with the row's, not a dependent trip after the reductions
   int t = labels[row];
@@ -407,13 +406,19 @@ __global__ __launch_bounds__(256) void softmax_xent_row4_kernel(const float* __r
     double xent = 0.0;
     if (t >= 0) xent = -(double)logf(fmaxf(syt, FLT_MIN));
     if (stats) {
-      const int slot = blockIdx.x % TNET_STATS_SLOTS;
+      const int slot = row % TNET_STATS_SLOTS;
       atomicAdd(stats + 2 * slot, xent);
       atomicAdd(stats + 2 * slot + 1, (a.i == des) ? 1.0 : 0.0);
     }
   }
 }
-
+__global__ __launch_bounds__(256) void softmax_xent_row4_kernel(const float* __restrict__ Z, TnetMatrixDim d,
+                                                                const int* __restrict__ labels,
+                                                                float* __restrict__ Y, int strideY,
+                                                                float* __restrict__ E, int strideE,
+                                                                double* __restrict__ stats) {
+  softmax_xent_row4(Z, d, labels, Y, strideY, E, strideE, stats, (int)blockIdx.x);
+}
 static bool v4ok(const void* p, int stride) { return ((uintptr_t)p & 15) == 0 && (stride & 3) == 0; }
 
 extern "C" int tnet_softmax_xent(const float* Z, TnetMatrixDim dZ, const int* labels, float* Y, int strideY, float* E,

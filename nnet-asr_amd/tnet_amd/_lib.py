@@ -67,7 +67,6 @@ _SIGS = {
     "tnet_gemm_config": (i32, [C.c_char_p]),
     "tnet_gemm_reserve": (i32, [i32]),
     "tnet_affine_fwd": (i32, [vp, MatrixDim, vp, MatrixDim, vp, vp, MatrixDim, i32, vp]),
-    "tnet_affine_fwd_shadow": (i32, [vp, MatrixDim, vp, MatrixDim, vp, vp, MatrixDim, vp, i32, vp]),
     "tnet_affine_fwd_sample": (i32, [vp, MatrixDim, vp, MatrixDim, vp, vp, MatrixDim, vp, i32, vp, vp, vp, vp, vp]),
     "tnet_affine_bwd": (i32, [vp, MatrixDim, vp, MatrixDim, vp, i32, vp, MatrixDim, i32, vp]),
     "tnet_affine_update": (i32, [vp, MatrixDim, vp, MatrixDim, vp, MatrixDim, vp, i32, f32, f32, f32, vp]),

@@ -14,8 +14,6 @@ from tnet_amd import Comm, DeviceArray, Network, Objective, formats, synchronize
 
 
 def main(out, with_dp):
-    if with_dp == "top":
-        return top(out)
     with_dp = with_dp == "1"
     dims = [64, 128, 128, 128, 16]
     net = Network.from_layers(formats.gen_mlp_init(dims, seed=3))
@@ -56,22 +54,6 @@ def main(out, with_dp):
         fused()
         synchronize()
         del comm
-    synchronize()
-    np.savez(out, **{f"p{i}_{k}": a for i, (W, b) in enumerate(net.linear_params()) for k, a in (("W", W), ("b", b))})
-
-
-def top(out):
-    """three fused steps of a 440 -> 512 x 2 -> 4000 net at bunch 1024: the top layer's forward writes its
-    transposed shadow (tnet_affine_fwd_shadow) and its backward reads it, unless TNET_FWD_SHADOW=0"""
-    dims = [440, 512, 512, 4000]
-    net = Network.from_layers(formats.gen_mlp_init(dims, seed=4))
-    net.set_learn_rate(2.0)
-    obj = Objective()
-    rng = np.random.default_rng(6)
-    for _ in range(3):
-        X = DeviceArray.from_numpy(rng.standard_normal((1024, dims[0])).astype(np.float32))
-        L = DeviceArray.vector(rng.integers(0, dims[-1], 1024).astype(np.int32))
-        net.train_bunch(obj, X, L)
     synchronize()
     np.savez(out, **{f"p{i}_{k}": a for i, (W, b) in enumerate(net.linear_params()) for k, a in (("W", W), ("b", b))})
 

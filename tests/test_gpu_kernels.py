@@ -800,7 +800,8 @@ def test_affine_update_bias_gather_matches_separate_calls(mmt, rows, sides, gcol
                 else:
                     check(st2)
             else:
-                check(lib().tnet_affine_update_bias(*args[0], S()))
+                for a in args:
+                    check(lib().tnet_affine_update_bias(*a, S()))
             check(lib().tnet_gather_bunch(*gargs, S()))
         out = []
         for d in dev:

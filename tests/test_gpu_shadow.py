@@ -261,46 +261,3 @@ def test_shadow_across_training_modes(tmp_path, with_dp):
         got[mode] = dict(np.load(out))
     for k, ref in got["0"].items():
         np.testing.assert_array_less(np.abs(got["2"][k] - ref), 2e-4 * np.abs(ref).max() + 1e-12, err_msg=k)
-
-
-@pytest.mark.parametrize("rows,n_in,n_out", [(1024, 2048, 4000), (1000, 2048, 4000), (1024, 512, 4096), (897, 1024, 3000),
-                                             (1024, 2048, 2048), (1024, 440, 4000), (512, 2048, 4000)])
-def test_fwd_shadow(rows, n_in, n_out):
-    """tnet_affine_fwd_shadow: Y bit-identical to tnet_affine_fwd(act 0) and Wt == W^T exactly where the f4 form takes
-    the shape (128x128 direct grid of 8 row blocks, whole 64-k tiles); elsewhere TNET_ERR_UNSUPPORTED with Wt
-    untouched"""
-    X, W, b = rnd((rows, n_in), 71), rnd((n_in, n_out), 72, 0.1), rnd(n_out, 73)
-    dX, dW, db = DeviceArray.from_numpy(X), DeviceArray.from_numpy(W), DeviceArray.vector(b)
-    dY0, dY = DeviceArray(rows, n_out), DeviceArray(rows, n_out)
-    dT = DeviceArray.from_numpy(np.full((n_out, n_in), np.nan, np.float32))
-    check(lib().tnet_affine_fwd(dX.ptr, dX.dim, dW.ptr, dW.dim, db.ptr, dY0.ptr, dY0.dim, 0, S()))
-    st = lib().tnet_affine_fwd_shadow(dX.ptr, dX.dim, dW.ptr, dW.dim, db.ptr, dY.ptr, dY.dim, dT.ptr, dT.stride, S())
-    synchronize()
-    takes = -(-rows // 128) == 8 and n_in % 64 == 0 and (-(-rows // 128)) * (-(-n_out // 128)) >= 240
-    if not takes:
-        assert st == TNET_ERR_UNSUPPORTED
-        assert np.isnan(dT.numpy()).all()
-        return
-    check(st)
-    np.testing.assert_array_equal(dY.numpy(), dY0.numpy())
-    np.testing.assert_array_equal(dT.numpy(), W.T)
-
-
-def test_fwd_shadow_in_the_step(tmp_path):
-    """three fused steps of 440 -> 512 x 2 -> 4000 (bunch 1024) with the top layer's backward from the forward-written
-    shadow (default) and from W (TNET_FWD_SHADOW=0): the same parameters within the slab-sum reorder band (the error
-    below the top layer is bit-identical, its bias gradient's slab sums add the same rows in another order).
-    Tolerance: |p - p0| <= 2e-4 * max|p0| per parameter block"""
-    import os
-    import subprocess
-    import sys
-    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    got = {}
-    for mode in ("1", "0"):
-        out = str(tmp_path / f"t{mode}.npz")
-        p = subprocess.run([sys.executable, os.path.join(repo, "tests", "shadow_modes_worker.py"), out, "top"],
-                           capture_output=True, text=True, timeout=300, env=dict(os.environ, TNET_FWD_SHADOW=mode))
-        assert p.returncode == 0, p.stderr[-3000:]
-        got[mode] = dict(np.load(out))
-    for k, ref in got["0"].items():
-        np.testing.assert_array_less(np.abs(got["1"][k] - ref), 2e-4 * np.abs(ref).max() + 1e-12, err_msg=k)
