@@ -487,10 +487,12 @@ std::string Upper(std::string s) {
 // (not in a VARSCALE file; the kind must be the features'), then "<MEAN|VARIANCE|VARSCALE> n" with n the
 // expected count, n reals, nothing after them.  Tag names compare case-blind.  VARIANCE values are returned as
 // 1 / sqrt(v), VARSCALE values as sqrt(v) (in double, as KaldiLib computes them).  The reference's error texts.
-std::vector<float> ReadNormFile(const std::string& path, int sampleKind, NormFile type, int count) {
+std::vector<float> ReadNormFile(const std::string& path, int sampleKind, NormFile type, int count,
+                                const std::string& base = std::string()) {
   const char* section = type == NormFile::kMean ? "MEAN" : type == NormFile::kVariance ? "VARIANCE" : "VARSCALE";
   const char* what = type == NormFile::kMean ? "CMN" : type == NormFile::kVariance ? "CVN" : "VarScale";
-  NormText in(path);
+  // a relative name opens against the creation-time directory; messages name the file as given
+  NormText in(base.empty() || path.empty() || path[0] == '/' ? path : base + "/" + path);
   if (!in.Opened()) Fail(std::string("Cannot open ") + what + " pFileName: '" + path + "'");
   std::string tag, kind;
   bool header = true;
@@ -535,16 +537,16 @@ void ApplyCepsNorm(const FeatureConfig& cfg, const std::string& logical, int tar
   // without _Z for the mean file, with the delivered derivative flags for the variance file (:1383-1385)
   int kind = targetKind & ~(kParmD | kParmA | kParmT);
   // the last file of each kind is kept (the reference re-reads only when the name changes)
-  thread_local std::string last_cmn, last_cvn, last_cvg;
+  thread_local std::string last_cmn, last_cvn, last_cvg;  // (keyed with the base directory)
   thread_local std::vector<float> cmn, cvn, cvg;
   if (cfg.cmn) {
     std::string name = MaskCapture(logical, cfg.cmnMask);
     if (name.empty()) Fail("CMN Matching failed");
     name = (cfg.cmnDir.empty() ? std::string() : cfg.cmnDir + "/") + "/" + name;
-    if (name != last_cmn) {
+    if (cfg.normBase + "|" + name != last_cmn) {
       last_cmn.clear();
-      cmn = ReadNormFile(name, kind & ~kParmZ, NormFile::kMean, coefs);
-      last_cmn = name;
+      cmn = ReadNormFile(name, kind & ~kParmZ, NormFile::kMean, coefs, cfg.normBase);
+      last_cmn = cfg.normBase + "|" + name;
     }
     for (int i = 0; i < tot; i++)
       for (int j = trg_N; j < coefs; j++) M[(size_t)i * trg_vec + (j - trg_N)] -= cmn[(size_t)j];
@@ -553,19 +555,19 @@ void ApplyCepsNorm(const FeatureConfig& cfg, const std::string& logical, int tar
   if (cfg.cvn) {
     std::string name = MaskCapture(logical, cfg.cvnMask);
     name = (cfg.cvnDir.empty() ? std::string() : cfg.cvnDir + "/") + "/" + name;
-    if (name != last_cvn) {
+    if (cfg.normBase + "|" + name != last_cvn) {
       last_cvn.clear();
-      cvn = ReadNormFile(name, kind, NormFile::kVariance, trg_vec);
-      last_cvn = name;
+      cvn = ReadNormFile(name, kind, NormFile::kVariance, trg_vec, cfg.normBase);
+      last_cvn = cfg.normBase + "|" + name;
     }
     for (int i = 0; i < tot; i++)
       for (int j = trg_N; j < trg_vec; j++) M[(size_t)i * trg_vec + (j - trg_N)] *= cvn[(size_t)j];
   }
   if (cfg.cvg) {
-    if (cfg.cvgFile != last_cvg) {
+    if (cfg.normBase + "|" + cfg.cvgFile != last_cvg) {
       last_cvg.clear();
-      cvg = ReadNormFile(cfg.cvgFile, -1, NormFile::kVarScale, trg_vec);
-      last_cvg = cfg.cvgFile;
+      cvg = ReadNormFile(cfg.cvgFile, -1, NormFile::kVarScale, trg_vec, cfg.normBase);
+      last_cvg = cfg.normBase + "|" + cfg.cvgFile;
     }
     for (int i = 0; i < tot; i++)
       for (int j = trg_N; j < trg_vec; j++) M[(size_t)i * trg_vec + (j - trg_N)] *= cvg[(size_t)j];
@@ -686,6 +688,7 @@ FeatureReader::FeatureReader(const std::string& scp, const FeatureConfig& cfg, s
   // reads them later from the same directory): the pool reads ahead, so a later chdir must not move them
   char cwd[4096];
   const std::string base = getcwd(cwd, sizeof(cwd)) ? std::string(cwd) : std::string();
+  mCfg.normBase = base;  // the CMN / CVN files likewise
   std::string tok;
   while (in >> tok) {
     mRecords.push_back(ParseFileRecord(tok));

@@ -72,6 +72,9 @@ struct FeatureConfig {
   std::string cmnDir, cmnMask;  // CMEANDIR, CMEANMASK
   std::string cvnDir, cvnMask;  // VARSCALEDIR, VARSCALEMASK
   std::string cvgFile;          // VARSCALEFN
+  // the working directory at the reader's creation: relative normalisation files are opened against it (the pool
+  // reads ahead, so a later chdir must not move them), and named as given in every message
+  std::string normBase;
 };
 
 struct Utterance {

@@ -211,3 +211,22 @@ def test_reader_under_sanitizers():
     p = subprocess.run([os.path.join(REPO, "tools", "htkio_sanitize.sh")], capture_output=True, text=True, timeout=600)
     assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-4000:]
     assert p.stdout.count("htkio_sanitize ok") == 4
+
+
+def test_reader_norm_paths_fixed_at_creation(workdir, tmp_path):
+    """relative CMEANDIR / VARSCALEDIR / VARSCALEFN resolve against the working directory at creation too: the
+    pool reads ahead (and opens the normalisation files) after the constructor returns, so a chdir right after it
+    must not move them (the reference opens them later from the same directory); error texts keep the names as
+    given (test_reader_errors_match_reference)"""
+    names = [n for n in OK_CONFIGS if META["configs"][n].get("norm")]
+    assert names
+    for name in names:
+        for _ in range(3):
+            r = _reader(workdir, name, threads=4, depth=4)  # returns with the cwd already restored
+            cwd = os.getcwd()
+            os.chdir(tmp_path)
+            try:
+                got = list(r)
+            finally:
+                os.chdir(cwd)
+            assert len(got) == len(META["configs"][name]["records"])
