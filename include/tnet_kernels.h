@@ -312,6 +312,13 @@ int tnet_affine_grad_bwd_pair(const float* X, TnetMatrixDim dX, const float* E, 
                               TnetMatrixDim dE2, const float* W2, TnetMatrixDim dW2, const float* Ybelow,
                               int strideYbelow, float* Eo, TnetMatrixDim dEo, float* colpart2, int ldcolpart2,
                               void* stream);
+/* The same with the backward from layer l-1's transposed weight shadow W2t [n_out x n_in] (tnet_affine_bwd_colsum_t's
+ * operand; the data-parallel apply keeps it, tnet_sgd_update_multi_t). */
+int tnet_affine_grad_bwd_pair_t(const float* X, TnetMatrixDim dX, const float* E, TnetMatrixDim dE, float* G,
+                                TnetMatrixDim dG, const float* colpart, int ldcolpart, float* gradB, const float* E2,
+                                TnetMatrixDim dE2, const float* W2t, TnetMatrixDim dW2t, const float* Ybelow,
+                                int strideYbelow, float* Eo, TnetMatrixDim dEo, float* colpart2, int ldcolpart2,
+                                void* stream);
 /* tnet_affine_grad_bias (X2 NULL) or two of them (X2, E2, G2, colpart2, gradB2: the step's last two gradients when
  * both 64x64 grids fit one round over the CUs) plus tnet_gather_bunch (the next bunch's CuCache::GetBunch,
  * cuCache.cc:155-200) on the CUs the gradient GEMMs' tiles leave free -- the data-parallel step's last gradient
@@ -341,6 +348,20 @@ typedef struct TnetSgdSeg_ {
   float l2;
 } TnetSgdSeg;
 int tnet_sgd_update_multi(const TnetSgdSeg* segs, int nseg, float scale, float mmt, void* stream);
+/* tnet_sgd_update_multi with segment `seg` a rows x cols weight matrix (row stride ld, n == rows*ld) whose
+ * updated values are also written transposed into t [cols x rows, row stride ldt]: the data-parallel apply keeps
+ * the layer's transposed shadow current (tnet_weight_shadow; the next step's backward reads it NN), the per-element
+ * arithmetic and results of every segment exactly tnet_sgd_update_multi's.  TNET_ERR_UNSUPPORTED when the matrix
+ * does not take the tiled form (unaligned rows, ld or ldt not a multiple of 4, more than 8 segments): the
+ * caller then runs tnet_sgd_update_multi and rebuilds the shadow itself. */
+typedef struct TnetSgdShadow_ {
+  int seg;
+  int rows, cols, ld;
+  float* t;
+  int ldt;
+} TnetSgdShadow;
+int tnet_sgd_update_multi_t(const TnetSgdSeg* segs, int nseg, float scale, float mmt, const TnetSgdShadow* sh,
+                            void* stream);
 /* Bias update from the error matrix E (CuVector::AddColSum + AddScaled, cuBiasedLinearity.cc:56-59):
  *   c = colsum(E) + mmt*corr_b ; b += scale * c ; corr_b = c   (corr_b may be NULL if mmt == 0)
  * If grad_out != NULL the raw colsum is written there instead and b is not touched (DP path). */
@@ -443,6 +464,32 @@ int tnet_rnn_out_bwd_update(const float* z, const double* smx, int pairs, int N,
                             unsigned long long* argkey, int train, void* stream);
 int tnet_argmax_correct(const unsigned long long* keys, const int* labels, int T, int N, double* stats,
                         void* stream);
+/* The look-ahead form of the chain (frames after an utterance's first; TNET_RNN_AHEAD=0: off).  The next frame's
+ * recurrent forward needs W_{t+1} = W_t + corr (cuRecurrent.cc:88-153), which exists only after this frame's BPTT;
+ * with v = [x_{t+1}, y_t], v W_{t+1} = (1 - lr wc) (v W_t) + sum_i (-lr (v . h_i)) d_i, so:
+ *   tnet_rnn_out_bwd_update_ahead : tnet_rnn_out_bwd_update (train) plus, in the same launch, the copy of the
+ *                              recurrent bias / momentum computed by the previous tnet_rnn_out_full_ahead (bnext,
+ *                              cbnext -> b, cb; bnext NULL: none) and (x_next != NULL) the next frame's look-ahead:
+ *                              the split-K partials of [x_next, h] W_t (tnet_gemv_rowvec_partial's), the dots
+ *                              [x_next, h] . h_i with the history rows (head + i) % R, i < steps, as
+ *                              dpart [ceil(K/64) x 16] partials, and the push of [x_next, h] into vout
+ *   tnet_rnn_out_full_ahead  : tnet_rnn_out_full with h = sigmoid(b' + (1 - lr wc) sum(hpart) + sum_i (-lr dot_i)
+ *                              d_i) -- b' the bias after the pending update (bnext / cbnext written, the
+ *                              tnet_rnn_update chain) -- and that update of W (rows x H, tnet_rnn_update's
+ *                              per-element arithmetic with history head / R and d_i = D rows) in extra workgroups
+ * The recurrent output differs from the materialised product by fp32 reassociation only (test_gpu_rnn.py). */
+int tnet_rnn_out_full_ahead(const float* hpart, int hslices, const float* hb, float* h, int H, const float* Wo,
+                            int ldwo, int N, const float* bo, float* z, double* smx, const float* dpart, const float* D,
+                            int ldd, int steps, float lr, float mmt, float wc, const float* cb, float* bnext,
+                            float* cbnext, float* W, int ldw, int rows, const float* hist, int ldh, int head, int R,
+                            void* stream);
+int tnet_rnn_out_bwd_update_ahead(const float* z, const double* smx, int pairs, int N, const int* label,
+                                  const float* h, int H, float* Wo, int ldwo, float* corrWo, int ldc, float* bo,
+                                  float* corr_bo, float scale, float mmt, float l2, float* e, float* eo, float* d,
+                                  double* stats, unsigned long long* argkey, const float* bnext, const float* cbnext,
+                                  float* b, float* cb, const float* x_next, int nIn, const float* W, int ldw,
+                                  float* partial, float* dpart, float* vout, const float* hist, int ldh, int head,
+                                  int R, int steps, void* stream);
 /* single-frame CuBiasedLinearity::Backpropagate + Update (cuBiasedLinearity.cc:32-64) in one pass
  * over W: e_out = W e (with the weights before the update), then the update of
  * tnet_affine_update_row; with s != NULL also d_out = e_out .* s (1 - s) (the diff-sigmoid of a

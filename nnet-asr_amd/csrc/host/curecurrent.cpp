@@ -21,6 +21,15 @@ void CuRecurrent::BpttOrder(int ord) {
   mHead = 0;
 }
 
+int CuRecurrent::AheadAdvance() {
+  if (mInputHistory.Rows() == 0) Error("Bptt order was not set");
+  mOutput.Init(1, GetNOutputs());
+  mHead = NextHead();
+  if (!mPending) return -1;
+  mPending = false;
+  return mPendHead;
+}
+
 void CuRecurrent::ClearHistory() {
   FlushPendingUpdate();
   mInputHistory.SetZero();
@@ -252,8 +261,10 @@ std::vector<uint64_t> CuRecurrentTrainer::ChainKey(size_t rows) {
                         (const void*)lin.Linearity().pCUData(), (const void*)lin.Bias().pCUData(),
                         (const void*)lin.LinearityCorrection().pCUData(), (const void*)lin.BiasCorrection().pCUData(),
                         (const void*)lin.Output().pCUData(), (const void*)lin.ErrorOutput().pCUData(),
-                        (const void*)mObj->DeviceStats()})
+                        (const void*)mObj->DeviceStats(), (const void*)mDotPart.pCUData(),
+                        (const void*)mBnext.pCUData(), (const void*)mCbnext.pCUData()})
     k.push_back((uint64_t)(uintptr_t)p);
+  k.push_back((uint64_t)AheadOn());
   float scale, l2;
   lin.UpdateConstants(1, &scale, &l2);
   k.insert(k.end(), {(uint64_t)mFeats.Stride(), (uint64_t)lin.Linearity().Stride(),
@@ -362,6 +373,11 @@ bool CuRecurrentTrainer::FusedFrameOk() const {
 // the output layer's softmax error + backprop + update + the recurrent diff-sigmoid (+ xent and the
 // frame's argmax key), then the BPTT GEMVs (bptt) and the recurrent update (1).  The network-output
 // / softmax copies of the generic chain have no reader here and are not made.
+bool CuRecurrentTrainer::AheadOn() const {
+  static const bool on = !(getenv("TNET_RNN_AHEAD") && getenv("TNET_RNN_AHEAD")[0] == '0');
+  return on && !mCrossval && dynamic_cast<const CuRecurrent&>(mNet->Layer(0)).AheadOk();
+}
+
 void CuRecurrentTrainer::TrainFrameFused(size_t f) {
   auto& rec = dynamic_cast<CuRecurrent&>(mNet->Layer(0));
   auto& lin = dynamic_cast<CuBiasedLinearity&>(mNet->Layer(1));
@@ -369,25 +385,64 @@ void CuRecurrentTrainer::TrainFrameFused(size_t f) {
   const int hs = (nIn + H + 63) / 64, G = (N + 63) / 64;
   mRecPart.Init((size_t)hs, (size_t)H);
   double* smx = (double*)Scratch(mSmx, mSmxBytes, sizeof(double) * 2 * (size_t)G);
-  rec.PropagatePartial(mRow, mRecPart.pCUData());
-  // (the partial kernel addresses [slices x cols] densely inside this allocation)
   lin.Output().Init(1, (size_t)N);
-  TNET_SAFE_CALL(tnet_rnn_out_full(mRecPart.pCUData(), hs, rec.Bias().pCUData(), rec.Output().pCUData(), H,
-                                   lin.Linearity().pCUData(), (int)lin.Linearity().Stride(), N, lin.Bias().pCUData(),
-                                   lin.Output().pCUData(), smx, S));
+  // the look-ahead chain: this frame's forward product was taken by the previous frame's second launch (with the
+  // weights before that frame's update; corrected here) -- one launch less a frame on the dependent chain
+  const bool ahead = AheadOn();
+  if (ahead) {
+    mDotPart.Init((size_t)hs, 16);
+    mBnext.Init((size_t)H);
+    mCbnext.Init((size_t)H);
+  }
+  const bool corrected = ahead && f > 0 && mAheadNext;
+  if (corrected) {
+    const int pend = rec.AheadAdvance();
+    if (pend < 0) Error("CuRecurrentTrainer: look-ahead frame without a pending update");
+    TNET_SAFE_CALL(tnet_rnn_out_full_ahead(
+        mRecPart.pCUData(), hs, rec.Bias().pCUData(), rec.Output().pCUData(), H, lin.Linearity().pCUData(),
+        (int)lin.Linearity().Stride(), N, lin.Bias().pCUData(), lin.Output().pCUData(), smx, mDotPart.pCUData(),
+        rec.DiffData(), rec.DiffStride(), rec.Steps(), rec.LearnRate(), rec.Momentum(), rec.Weightcost(),
+        rec.BiasCorrection().pCUData(), mBnext.pCUData(), mCbnext.pCUData(), rec.Linearity().pCUData(),
+        (int)rec.Linearity().Stride(), nIn + H, rec.HistoryData(), rec.HistoryStride(), pend, rec.HistoryRows(), S));
+  } else {
+    rec.PropagatePartial(mRow, mRecPart.pCUData());
+    // (the partial kernel addresses [slices x cols] densely inside this allocation)
+    TNET_SAFE_CALL(tnet_rnn_out_full(mRecPart.pCUData(), hs, rec.Bias().pCUData(), rec.Output().pCUData(), H,
+                                     lin.Linearity().pCUData(), (int)lin.Linearity().Stride(), N, lin.Bias().pCUData(),
+                                     lin.Output().pCUData(), smx, S));
+  }
   float scale, l2;
   lin.UpdateConstants(1, &scale, &l2);
   const bool mmt = lin.Momentum() != 0.0f;
   lin.ErrorOutput().Init(1, (size_t)H);
-  TNET_SAFE_CALL(tnet_rnn_out_bwd_update(
-      lin.Output().pCUData(), smx, G, N, mLabels.pCUData() + f, rec.Output().pCUData(), H, lin.Linearity().pCUData(),
-      (int)lin.Linearity().Stride(), mmt ? lin.LinearityCorrection().pCUData() : nullptr,
-      (int)lin.LinearityCorrection().Stride(), lin.Bias().pCUData(), mmt ? lin.BiasCorrection().pCUData() : nullptr,
-      scale, lin.Momentum(), l2, nullptr, nullptr, lin.ErrorOutput().pCUData(), rec.DiffRow0(), mObj->DeviceStats(),
-      (unsigned long long*)mArgKey + f, mCrossval ? 0 : 1, S));
+  const bool next = f + 1 < mUttRows;
+  mAheadNext = false;
+  if (ahead) {
+    // the output layer's backprop + update, the recurrent bias of the update applied above, and the next frame's
+    // look-ahead product / dots / history push
+    TNET_SAFE_CALL(tnet_rnn_out_bwd_update_ahead(
+        lin.Output().pCUData(), smx, G, N, mLabels.pCUData() + f, rec.Output().pCUData(), H,
+        lin.Linearity().pCUData(), (int)lin.Linearity().Stride(), mmt ? lin.LinearityCorrection().pCUData() : nullptr,
+        (int)lin.LinearityCorrection().Stride(), lin.Bias().pCUData(), mmt ? lin.BiasCorrection().pCUData() : nullptr,
+        scale, lin.Momentum(), l2, nullptr, lin.ErrorOutput().pCUData(), rec.DiffRow0(), mObj->DeviceStats(),
+        (unsigned long long*)mArgKey + f, corrected ? mBnext.pCUData() : nullptr,
+        corrected ? mCbnext.pCUData() : nullptr, rec.Bias().pCUData(), rec.BiasCorrection().pCUData(),
+        next ? mFeats.pCURowData(f + 1) : nullptr, nIn, rec.Linearity().pCUData(), (int)rec.Linearity().Stride(),
+        mRecPart.pCUData(), mDotPart.pCUData(),
+        rec.HistoryData() + (long)rec.NextHead() * rec.HistoryStride(), rec.HistoryData(), rec.HistoryStride(),
+        rec.Head(), rec.HistoryRows(), rec.Steps(), S));
+    mAheadNext = next;
+  } else {
+    TNET_SAFE_CALL(tnet_rnn_out_bwd_update(
+        lin.Output().pCUData(), smx, G, N, mLabels.pCUData() + f, rec.Output().pCUData(), H, lin.Linearity().pCUData(),
+        (int)lin.Linearity().Stride(), mmt ? lin.LinearityCorrection().pCUData() : nullptr,
+        (int)lin.LinearityCorrection().Stride(), lin.Bias().pCUData(), mmt ? lin.BiasCorrection().pCUData() : nullptr,
+        scale, lin.Momentum(), l2, nullptr, nullptr, lin.ErrorOutput().pCUData(), rec.DiffRow0(), mObj->DeviceStats(),
+        (unsigned long long*)mArgKey + f, mCrossval ? 0 : 1, S));
+  }
   mObj->AddFrames(1);
   if (mCrossval) return;
-  rec.UpdateFromDiff0(f + 1 < mUttRows);  // the last frame's update runs on its own: no state leaves the utterance
+  rec.UpdateFromDiff0(next);  // the last frame's update runs on its own: no state leaves the utterance
 }
 
 }  // namespace TNet

@@ -62,6 +62,23 @@ class CuRecurrent : public CuUpdatableComponent {
   CuVector<BaseFloat>& Bias() { return mBias; }
   CuVector<BaseFloat>& BiasCorrection() { return mBiasCorrection; }
 
+  // ---- the look-ahead chain (CuRecurrentTrainer::TrainFrameFused; tnet_rnn_out_full_ahead / _bwd_update_ahead)
+  /// the shapes it takes: bptt + 1 <= 9 steps (one fewer than the ring's rows), nOut a multiple of 4
+  bool AheadOk() const {
+    return mBpttOrder >= 0 && mBpttOrder + 1 <= 9 && mBpttOrder + 1 < (int)mInputHistory.Rows() && GetNOutputs() % 4 == 0;
+  }
+  int Steps() const { return mBpttOrder + 1; }
+  float* HistoryData() { return mInputHistory.pCUData(); }
+  int HistoryStride() const { return (int)mInputHistory.Stride(); }
+  int HistoryRows() const { return (int)mInputHistory.Rows(); }
+  float* DiffData() { return mDiff.pCUData(); }
+  int DiffStride() const { return (int)mDiff.Stride(); }
+  /// the ring row the next frame's history row goes to (the look-ahead pushes it)
+  int NextHead() const { return (mHead + (int)mInputHistory.Rows() - 1) % (int)mInputHistory.Rows(); }
+  /// a frame whose history row the previous frame's look-ahead already pushed: advance the ring head and hand the
+  /// deferred update (its ring head; the caller's launch applies it) over -- -1 when none is pending
+  int AheadAdvance();
+
   /// ring head (host state the per-frame chain advances; a graph replay sets it as the capture left it)
   int Head() const { return mHead; }
   void SetHead(int h) { mHead = h; }
@@ -107,6 +124,13 @@ class CuRecurrentTrainer {
   size_t mUttRows = 0;  // frames of the utterance on the fused chain (the last one's update is not deferred)
   // fused-chain scratch: recurrent / output split-K partials, softmax pairs, per-frame argmax keys
   CuMatrix<BaseFloat> mRecPart, mOutPart;
+  // the look-ahead chain (TNET_RNN_AHEAD=0: off): the dots' partials, the recurrent bias / momentum after the
+  // pending update (written by the frame's first launch, copied by its second); mAheadNext: the previous frame's
+  // second launch took this frame's look-ahead
+  CuMatrix<BaseFloat> mDotPart;
+  CuVector<BaseFloat> mBnext, mCbnext;
+  bool mAheadNext = false;
+  bool AheadOn() const;
   void* mSmx = nullptr;
   size_t mSmxBytes = 0;
   void* mArgKey = nullptr;

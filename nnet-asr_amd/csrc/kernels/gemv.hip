@@ -33,6 +33,63 @@ struct RnnPendingUpdate {
 };
 constexpr int GV_UPD_MAX = 9;  // steps = bptt + 1 of the folded form (deeper: the update's own launch)
 
+// The look-ahead form of the frame chain (CuRecurrentTrainer, TNET_RNN_AHEAD).  The next frame's recurrent forward
+// v_{t+1} W_{t+1}, v_{t+1} = [x_{t+1}, y_t], needs the frame's update W_{t+1} = W_t + corr (cuRecurrent.cc:88-153:
+// corr = (-lr wc) W_t + sum_i (-lr h_i) (x) d_i), which exists only after the frame's BPTT.  Since
+//   v W_{t+1} = (1 - lr wc) (v W_t) + sum_i (-lr (v . h_i)) d_i,
+// the product with the OLD weights and the dots v . h_i are taken as soon as y_t exists -- beside the output layer's
+// backprop (RnnAhead blocks of rnn_out_bwd_kernel) -- and the next frame's first launch only adds the rank-(bptt+1)
+// correction while it finishes the sigmoid (rnn_out_full_kernel with RnnCorr), the weight update itself running in
+// that launch's extra workgroups.  One launch less a frame on the dependent chain; the recurrent output differs from
+// the materialised product by fp32 reassociation only.
+struct RnnAhead {
+  // bias blocks: the previous frame's recurrent bias update, computed by the forward that used it into bnext /
+  // cbnext, copied to b / cb here (the forward's other workgroups were reading the old values)
+  int nbias, H;
+  const float* bnext;
+  const float* cbnext;
+  float* b;
+  float* cb;
+  // look-ahead blocks: partial[s][c] = sum_{k in slice s} v[k] W[k][c] over cdiv(H, 64) x slices blocks, the
+  // column-block-0 ones also the dots dpart[s][i] = sum_{k in slice s} v[k] h_i[k] (h_i = ring row (head + i) % R,
+  // i < steps) and the push of v into the ring row vout
+  int nlook;
+  const float* v0;
+  int K0;
+  const float* v1;
+  int K;
+  const float* W;
+  long ldw;
+  float* partial;
+  float* dpart;
+  float* vout;
+  const float* hist;
+  long ldh;
+  int head, R, steps;
+};
+constexpr int GV_DOTS = 16;  // dpart row stride (steps <= GV_UPD_MAX)
+
+// the next frame's first launch: the correction of the look-ahead product and the pending update
+struct RnnCorr {
+  int on;
+  const float* dpart;  // [slices x GV_DOTS]
+  const float* D;      // [steps x ldd] d_0 .. d_{steps-1} of the pending update
+  long ldd;
+  int steps;
+  float lr, mmt, wc;
+  const float* cb;  // the bias' momentum (old); the old bias is rnn_out_full_kernel's hb
+  float* bnext;     // new bias / momentum (written by workgroup 0; copied by the next RnnAhead bias blocks)
+  float* cbnext;
+  // update blocks: W [rows x H] (rnn_update_kernel's arithmetic, no bias), 4 elements a thread
+  int nupd;
+  float* W;
+  long ldw;
+  int rows;
+  const float* hist;
+  long ldh;
+  int head, R;
+};
+
 // partial[s][c] = sum_{k in slice s} v[k] * W[k][c], v = [v0[0:K0], v1[0:K-K0]] (the recurrent
 // layer's [x_t, y_{t-1}], read in place); the column-block-0 workgroups also store v to vout (the
 // history row, cuRecurrent.cc:31-35), so the two row copies need no launches of their own.
@@ -124,6 +181,47 @@ __global__ __launch_bounds__(256) void gemv_rowvec_partial_k(const float* __rest
   red[w][lane] = acc;
   __syncthreads();
   if (w == 0 && c < N) partial[(long)blockIdx.y * N + c] = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
+}
+
+// One block of the look-ahead product (gemv_rowvec_partial_k<false>'s arithmetic and k order) at block coordinates
+// (bx, by), its dots (bx == 0) and the push; 256 threads.
+__device__ __forceinline__ void rnn_ahead_block(const RnnAhead& a, const int bx, const int by) {
+  __shared__ float red[4][64];
+  constexpr int KPW = GV_KSLICE / 4;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int N = a.H, K = a.K;
+  const int c = bx * 64 + lane, cc = min(c, N - 1);
+  const int k0 = by * GV_KSLICE, k1 = min(K, k0 + GV_KSLICE);
+  auto vk = [&](int k) { return k < a.K0 ? a.v0[k] : a.v1[k - a.K0]; };
+  float wv[KPW], xv[KPW];
+#pragma unroll
+  for (int q = 0; q < KPW; ++q) {
+    const int k = min(k0 + w + 4 * q, K - 1);
+    wv[q] = a.W[(long)k * a.ldw + cc];
+    xv[q] = vk(k);
+  }
+  float acc = 0.f;
+#pragma unroll
+  for (int q = 0; q < KPW; ++q)
+    if (k0 + w + 4 * q < k1) acc += xv[q] * wv[q];
+  if (bx == 0) {
+    // the dots of this k-slice, wave i over steps i, i + 4, ...: lane l takes k0 + l (the ring rows are read before
+    // the push below replaces row vout: a different row, R >= steps + 1)
+    const int k = k0 + lane;
+    const float x = k < k1 ? vk(k) : 0.f;
+    for (int i = w; i < a.steps; i += 4) {
+      int r = a.head + i;
+      r = r >= a.R ? r - a.R : r;
+      const float h = k < k1 ? a.hist[(long)r * a.ldh + k] : 0.f;
+      const float d = wave_sum(x * h);
+      if (lane == 0) a.dpart[(long)by * GV_DOTS + i] = d;
+    }
+    __syncthreads();  // every wave's ring reads done before the push
+    for (int kk = k0 + threadIdx.x; kk < k1; kk += blockDim.x) a.vout[kk] = vk(kk);
+  }
+  red[w][lane] = acc;
+  __syncthreads();
+  if (w == 0 && c < N) a.partial[(long)by * N + c] = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
 }
 
 // y[c] = act(b[c] + sum_s partial[s][c]) ; act: 0 none, 1 sigmoid
@@ -506,10 +604,48 @@ __global__ __launch_bounds__(1024) void rnn_out_full_kernel(const float* __restr
                                                             const float* __restrict__ hb, float* __restrict__ h,
                                                             int H, const float* __restrict__ Wo, long ldw, int N,
                                                             const float* __restrict__ bo, float* __restrict__ z,
-                                                            double* __restrict__ smx) {
+                                                            double* __restrict__ smx, const RnnCorr cr) {
   __shared__ float hs[GV_FULL_MAXH];
   __shared__ float red[16][64];
+  __shared__ float sdot[GV_DOTS];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int nout_blocks = (N + 63) / 64;
+  if (cr.on && (int)blockIdx.x >= nout_blocks) {
+    // ---- the pending recurrent update (rnn_update_kernel's per-element arithmetic and step order; the bias is
+    // the output blocks' business below), 4 consecutive elements of a row a thread
+    const long e0 = ((long)(blockIdx.x - nout_blocks) * 1024 + threadIdx.x) * 4;
+    const int k = (int)(e0 / H), c0 = (int)(e0 % H);
+    if (k >= cr.rows) return;
+    float hk[GV_UPD_MAX];
+#pragma unroll
+    for (int i = 0; i < GV_UPD_MAX; ++i) {
+      if (i >= cr.steps) break;
+      int r = cr.head + i;
+      r = r >= cr.R ? r - cr.R : r;
+      hk[i] = cr.hist[(long)r * cr.ldh + k];
+    }
+    for (int j = 0; j < 4; ++j) {
+      const int c = c0 + j;
+      if (c >= H) break;
+      float acc = 0.f;
+#pragma unroll
+      for (int i = 0; i < GV_UPD_MAX; ++i) {
+        if (i >= cr.steps) break;
+        acc = __fmaf_rn(-cr.lr * hk[i], cr.D[(long)i * cr.ldd + c], acc);
+      }
+      float* wp = cr.W + (long)k * cr.ldw + c;
+      const float wv = *wp;
+      const float corr = __fmaf_rn(-cr.lr * cr.wc, wv, acc);
+      *wp = corr + wv;
+    }
+    return;
+  }
+  if (cr.on && threadIdx.x < GV_DOTS) {  // the dots, summed over the slices in slice order
+    float d = 0.f;
+    for (int q = 0; q < hslices; ++q) d += cr.dpart[(long)q * GV_DOTS + threadIdx.x];
+    sdot[threadIdx.x] = d;
+  }
+  if (cr.on) __syncthreads();
   const int c = blockIdx.x * 64 + lane, cc = min(c, N - 1);
   // the first 32 rows per lane of the column block's Wo issued before the h finish (their latency
   // overlaps the partial-sum loads)
@@ -529,7 +665,26 @@ __global__ __launch_bounds__(1024) void rnn_out_full_kernel(const float* __restr
       for (int q = 0; q < 16; ++q)
         if (q0 + q < hslices) sacc += p[q];
     }
-    const float hv = sigmoidf_ref((hb ? hb[k] : 0.f) + sacc);
+    float hv;
+    if (cr.on) {
+      // the pending bias update (rnn_update_kernel's chain) and the correction of the look-ahead product
+      float g = __fmaf_rn(-cr.lr, cr.D[k], cr.mmt * cr.cb[k]);
+      float a = 0.f;
+      a = __fmaf_rn(-cr.lr * sdot[0], cr.D[k], a);
+      for (int i = 1; i < cr.steps; ++i) {
+        const float di = cr.D[(long)i * cr.ldd + k];
+        g = __fmaf_rn(-cr.lr, di, g);
+        a = __fmaf_rn(-cr.lr * sdot[i], di, a);
+      }
+      const float bn = g + hb[k];
+      if (blockIdx.x == 0) {
+        cr.cbnext[k] = g;
+        cr.bnext[k] = bn;
+      }
+      hv = sigmoidf_ref(bn + (__fmaf_rn(-cr.lr * cr.wc, sacc, sacc) + a));
+    } else {
+      hv = sigmoidf_ref((hb ? hb[k] : 0.f) + sacc);
+    }
     hs[k] = hv;
     if (blockIdx.x == 0) h[k] = hv;
   }
@@ -577,10 +732,25 @@ __global__ __launch_bounds__(256) void rnn_out_bwd_kernel(
     const float* __restrict__ h, int n_in, int n_out, float* __restrict__ W, long ldw, float* __restrict__ corrW,
     long ldc, float* __restrict__ b, float* __restrict__ cb, float scale, float mmt, float l2,
     float* __restrict__ yout, float* __restrict__ eout, float* __restrict__ eo, float* __restrict__ d,
-    double* __restrict__ stats, unsigned long long* __restrict__ argkey, int row_blocks, int train) {
+    double* __restrict__ stats, unsigned long long* __restrict__ argkey, int row_blocks, int train,
+    const RnnAhead ah) {
   __shared__ ArgMax sarg[4];
   __shared__ float racc[4];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int stat_blocks = (n_out + 255) / 256, xb = (int)blockIdx.x - row_blocks - stat_blocks;
+  if (xb >= 0) {  // ---- RnnAhead: the recurrent bias copy, then the next frame's look-ahead blocks
+    if (xb < ah.nbias) {
+      const int k = xb * 256 + threadIdx.x;
+      if (k < ah.H) {
+        ah.cb[k] = ah.cbnext[k];
+        ah.b[k] = ah.bnext[k];
+      }
+      return;
+    }
+    const int lb = xb - ah.nbias, nbx = (ah.H + 63) / 64;
+    rnn_ahead_block(ah, lb % nbx, lb / nbx);
+    return;
+  }
   // the softmax normaliser from the pairs {m_g, s_g}: M = max m_g, S = sum s_g exp(m_g - M), every wave
   // reducing the G <= 64 pairs itself (lane g); their loads and the label's go out with the rest
   const int gl = min(lane, G - 1);  // clamped, unconditional: no branch between the loads
@@ -762,7 +932,8 @@ extern "C" int tnet_rnn_out_full(const float* hpart, int hslices, const float* h
                                  int ldwo, int N, const float* bo, float* z, double* smx, void* stream) {
   if (hslices <= 0 || H <= 0 || N <= 0 || ldwo < N || !hpart || !h || !Wo || !smx) return TNET_ERR_ARG;
   if (H > GV_FULL_MAXH || cdiv(N, 64) > 64) return TNET_ERR_UNSUPPORTED;
-  rnn_out_full_kernel<<<cdiv(N, 64), 1024, 0, (hipStream_t)stream>>>(hpart, hslices, hb, h, H, Wo, ldwo, N, bo, z, smx);
+  rnn_out_full_kernel<<<cdiv(N, 64), 1024, 0, (hipStream_t)stream>>>(hpart, hslices, hb, h, H, Wo, ldwo, N, bo, z, smx,
+                                                                      RnnCorr{});
   TNET_LAUNCH_CHECK();
   return TNET_OK;
 }
@@ -814,11 +985,84 @@ extern "C" int tnet_rnn_out_bwd_update(const float* z, const double* smx, int pa
   if (wide)
     rnn_out_bwd_kernel<4><<<grid, 256, 0, st>>>(z, smx, pairs, label, h, H, N, Wo, ldwo,
                                                 mmt != 0.f ? corrWo : nullptr, ldc, bo, mmt != 0.f ? corr_bo : nullptr,
-                                                scale, mmt, l2, y, e, eo, d, stats, argkey, row_blocks, train);
+                                                scale, mmt, l2, y, e, eo, d, stats, argkey, row_blocks, train,
+                                                RnnAhead{});
   else
     rnn_out_bwd_kernel<1><<<grid, 256, 0, st>>>(z, smx, pairs, label, h, H, N, Wo, ldwo,
                                                 mmt != 0.f ? corrWo : nullptr, ldc, bo, mmt != 0.f ? corr_bo : nullptr,
-                                                scale, mmt, l2, y, e, eo, d, stats, argkey, row_blocks, train);
+                                                scale, mmt, l2, y, e, eo, d, stats, argkey, row_blocks, train,
+                                                RnnAhead{});
+  TNET_LAUNCH_CHECK();
+  return TNET_OK;
+}
+
+// the look-ahead frame chain (RnnAhead / RnnCorr above; CuRecurrentTrainer::TrainFrameFused)
+extern "C" int tnet_rnn_out_full_ahead(const float* hpart, int hslices, const float* hb, float* h, int H,
+                                       const float* Wo, int ldwo, int N, const float* bo, float* z, double* smx,
+                                       const float* dpart, const float* D, int ldd, int steps, float lr, float mmt,
+                                       float wc, const float* cb, float* bnext, float* cbnext, float* W, int ldw,
+                                       int rows, const float* hist, int ldh, int head, int R, void* stream) {
+  if (hslices <= 0 || H <= 0 || N <= 0 || ldwo < N || !hpart || !hb || !h || !Wo || !smx || !dpart || !D || !cb ||
+      !bnext || !cbnext || !W || !hist || steps <= 0 || ldd < H || ldw < H || ldh < rows || head < 0 || head >= R ||
+      rows <= 0)
+    return TNET_ERR_ARG;
+  if (H > GV_FULL_MAXH || cdiv(N, 64) > 64 || steps > GV_UPD_MAX || steps >= R || (H & 3) ||
+      hslices != cdiv(rows, GV_KSLICE))
+    return TNET_ERR_UNSUPPORTED;
+  RnnCorr cr{};
+  cr.on = 1;
+  cr.dpart = dpart; cr.D = D; cr.ldd = ldd; cr.steps = steps; cr.lr = lr; cr.mmt = mmt; cr.wc = wc;
+  cr.cb = cb; cr.bnext = bnext; cr.cbnext = cbnext;
+  cr.nupd = (int)cdiv((long)rows * H, 4096);
+  cr.W = W; cr.ldw = ldw; cr.rows = rows; cr.hist = hist; cr.ldh = ldh; cr.head = head; cr.R = R;
+  rnn_out_full_kernel<<<cdiv(N, 64) + cr.nupd, 1024, 0, (hipStream_t)stream>>>(hpart, hslices, hb, h, H, Wo, ldwo, N,
+                                                                               bo, z, smx, cr);
+  TNET_LAUNCH_CHECK();
+  return TNET_OK;
+}
+
+extern "C" int tnet_rnn_out_bwd_update_ahead(const float* z, const double* smx, int pairs, int N, const int* label,
+                                             const float* h, int H, float* Wo, int ldwo, float* corrWo, int ldc,
+                                             float* bo, float* corr_bo, float scale, float mmt, float l2, float* e,
+                                             float* eo, float* d, double* stats, unsigned long long* argkey,
+                                             const float* bnext, const float* cbnext, float* b, float* cb,
+                                             const float* x_next, int nIn, const float* W, int ldw, float* partial,
+                                             float* dpart, float* vout, const float* hist, int ldh, int head, int R,
+                                             int steps, void* stream) {
+  // tnet_rnn_out_bwd_update (train) + the recurrent bias copy (bnext != NULL) + the next frame's look-ahead
+  // (x_next != NULL: v = [x_next, h], K = nIn + H)
+  if (N <= 0 || H <= 0 || !z || !smx || !label || !h || !Wo || !bo || ldwo < N ||
+      (mmt != 0.f && (!corrWo || !corr_bo || ldc < N)) || pairs < 1)
+    return TNET_ERR_ARG;
+  if (bnext && (!cbnext || !b || !cb)) return TNET_ERR_ARG;
+  const int K = nIn + H;
+  if (x_next && (!W || !partial || !dpart || !vout || !hist || nIn <= 0 || ldw < H || ldh < K || head < 0 ||
+                 head >= R || steps <= 0))
+    return TNET_ERR_ARG;
+  if (pairs > 64 || (x_next && (steps > GV_UPD_MAX || steps >= R))) return TNET_ERR_UNSUPPORTED;
+  RnnAhead ah{};
+  ah.H = H;
+  if (bnext) {
+    ah.nbias = cdiv(H, 256);
+    ah.bnext = bnext; ah.cbnext = cbnext; ah.b = b; ah.cb = cb;
+  }
+  if (x_next) {
+    ah.nlook = cdiv(H, 64) * cdiv(K, GV_KSLICE);
+    ah.v0 = x_next; ah.K0 = nIn; ah.v1 = h; ah.K = K; ah.W = W; ah.ldw = ldw; ah.partial = partial;
+    ah.dpart = dpart; ah.vout = vout; ah.hist = hist; ah.ldh = ldh; ah.head = head; ah.R = R; ah.steps = steps;
+  }
+  const bool wide = N > 1024;
+  const int row_blocks = wide ? H : cdiv(H, 4);
+  const dim3 grid(row_blocks + cdiv(N, 256) + ah.nbias + ah.nlook);
+  hipStream_t st = (hipStream_t)stream;
+  float* cw = mmt != 0.f ? corrWo : nullptr;
+  float* cbo = mmt != 0.f ? corr_bo : nullptr;
+  if (wide)
+    rnn_out_bwd_kernel<4><<<grid, 256, 0, st>>>(z, smx, pairs, label, h, H, N, Wo, ldwo, cw, ldc, bo, cbo, scale, mmt,
+                                                l2, nullptr, e, eo, d, stats, argkey, row_blocks, 1, ah);
+  else
+    rnn_out_bwd_kernel<1><<<grid, 256, 0, st>>>(z, smx, pairs, label, h, H, N, Wo, ldwo, cw, ldc, bo, cbo, scale, mmt,
+                                                l2, nullptr, e, eo, d, stats, argkey, row_blocks, 1, ah);
   TNET_LAUNCH_CHECK();
   return TNET_OK;
 }

@@ -81,10 +81,13 @@ _SIGS = {
     "tnet_affine_grad_bias": (i32, [vp, MatrixDim, vp, MatrixDim, vp, MatrixDim, vp, i32, vp, vp]),
     "tnet_affine_grad_bwd_pair": (i32, [vp, MatrixDim, vp, MatrixDim, vp, MatrixDim, vp, i32, vp, vp, MatrixDim, vp,
                                         MatrixDim, vp, i32, vp, MatrixDim, vp, i32, vp]),
+    "tnet_affine_grad_bwd_pair_t": (i32, [vp, MatrixDim, vp, MatrixDim, vp, MatrixDim, vp, i32, vp, vp, MatrixDim,
+                                          vp, MatrixDim, vp, i32, vp, MatrixDim, vp, i32, vp]),
     "tnet_affine_grad_bias_gather": (i32, [vp, MatrixDim, vp, MatrixDim, vp, MatrixDim, vp, i32, vp, vp, MatrixDim, vp,
                                            MatrixDim, vp, MatrixDim, vp, i32, vp, vp, vp, vp, vp, vp, MatrixDim,
                                            MatrixDim, vp]),
     "tnet_sgd_update_multi": (i32, [vp, i32, f32, f32, vp]),
+    "tnet_sgd_update_multi_t": (i32, [vp, i32, f32, f32, vp, vp]),
     "tnet_affine_bwd_colsum": (i32, [vp, MatrixDim, vp, MatrixDim, vp, i32, vp, MatrixDim, vp, i32, vp]),
     "tnet_affine_bwd_colsum_slabs": (i32, [vp, MatrixDim, vp, MatrixDim, vp, i32, vp, MatrixDim, vp, i32, vp, i32,
                                            vp]),
@@ -232,6 +235,11 @@ _SIGS = {
     "tnet_gemv_rowvec_partial_update": (i32, [vp, i32, vp, i32, vp, vp, i32, i32, vp, vp, i32, i32, i32, vp, i32, i32,
                                               vp, vp, f32, f32, f32, vp]),
     "tnet_argmax_correct": (i32, [vp, vp, i32, i32, vp, vp]),
+    "tnet_rnn_out_full_ahead": (i32, [vp, i32, vp, vp, i32, vp, i32, i32, vp, vp, vp, vp, vp, i32, i32, f32, f32, f32,
+                                      vp, vp, vp, vp, i32, i32, vp, i32, i32, i32, vp]),
+    "tnet_rnn_out_bwd_update_ahead": (i32, [vp, vp, i32, i32, vp, vp, i32, vp, i32, vp, i32, vp, vp, f32, f32, f32, vp,
+                                            vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, vp, i32, vp, vp, vp, vp, i32,
+                                            i32, i32, i32, vp]),
     "tnetF_rand": (i32, [vp, MatrixDim, vp, vp, vp, vp, vp]),
     "tnetF_gauss_rand": (i32, [vp, MatrixDim, vp, vp, vp, vp, vp]),
     "tnetF_binarize_probs": (i32, [vp, vp, vp, MatrixDim, vp]),
