@@ -312,13 +312,6 @@ int tnet_affine_grad_bwd_pair(const float* X, TnetMatrixDim dX, const float* E, 
                               TnetMatrixDim dE2, const float* W2, TnetMatrixDim dW2, const float* Ybelow,
                               int strideYbelow, float* Eo, TnetMatrixDim dEo, float* colpart2, int ldcolpart2,
                               void* stream);
-/* The same with the backward from layer l-1's transposed weight shadow W2t [n_out x n_in] (tnet_affine_bwd_colsum_t's
- * operand; the data-parallel apply keeps it, tnet_sgd_update_multi_t). */
-int tnet_affine_grad_bwd_pair_t(const float* X, TnetMatrixDim dX, const float* E, TnetMatrixDim dE, float* G,
-                                TnetMatrixDim dG, const float* colpart, int ldcolpart, float* gradB, const float* E2,
-                                TnetMatrixDim dE2, const float* W2t, TnetMatrixDim dW2t, const float* Ybelow,
-                                int strideYbelow, float* Eo, TnetMatrixDim dEo, float* colpart2, int ldcolpart2,
-                                void* stream);
 /* tnet_affine_grad_bias (X2 NULL) or two of them (X2, E2, G2, colpart2, gradB2: the step's last two gradients when
  * both 64x64 grids fit one round over the CUs) plus tnet_gather_bunch (the next bunch's CuCache::GetBunch,
  * cuCache.cc:155-200) on the CUs the gradient GEMMs' tiles leave free -- the data-parallel step's last gradient
@@ -348,20 +341,6 @@ typedef struct TnetSgdSeg_ {
   float l2;
 } TnetSgdSeg;
 int tnet_sgd_update_multi(const TnetSgdSeg* segs, int nseg, float scale, float mmt, void* stream);
-/* tnet_sgd_update_multi with segment `seg` a rows x cols weight matrix (row stride ld, n == rows*ld) whose
- * updated values are also written transposed into t [cols x rows, row stride ldt]: the data-parallel apply keeps
- * the layer's transposed shadow current (tnet_weight_shadow; the next step's backward reads it NN), the per-element
- * arithmetic and results of every segment exactly tnet_sgd_update_multi's.  TNET_ERR_UNSUPPORTED when the matrix
- * does not take the tiled form (unaligned rows, ld or ldt not a multiple of 4, more than 8 segments): the
- * caller then runs tnet_sgd_update_multi and rebuilds the shadow itself. */
-typedef struct TnetSgdShadow_ {
-  int seg;
-  int rows, cols, ld;
-  float* t;
-  int ldt;
-} TnetSgdShadow;
-int tnet_sgd_update_multi_t(const TnetSgdSeg* segs, int nseg, float scale, float mmt, const TnetSgdShadow* sh,
-                            void* stream);
 /* Bias update from the error matrix E (CuVector::AddColSum + AddScaled, cuBiasedLinearity.cc:56-59):
  *   c = colsum(E) + mmt*corr_b ; b += scale * c ; corr_b = c   (corr_b may be NULL if mmt == 0)
  * If grad_out != NULL the raw colsum is written there instead and b is not touched (DP path). */

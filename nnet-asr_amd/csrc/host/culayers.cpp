@@ -374,8 +374,7 @@ bool CuBiasedLinearity::ComputeGradientColsumGather(const CuMatrix<BaseFloat>& c
 
 bool CuBiasedLinearity::ComputeGradientColsumWithBwd(const CuMatrix<BaseFloat>& colpart, const CuBiasedLinearity& below,
                                                      const CuMatrix<BaseFloat>& E2, const CuMatrix<BaseFloat>& Ybelow,
-                                                     CuMatrix<BaseFloat>& Eo, CuMatrix<BaseFloat>& colpart2,
-                                                     bool use_shadow) {
+                                                     CuMatrix<BaseFloat>& Eo, CuMatrix<BaseFloat>& colpart2) {
   CuProfileScope p("CuBiasedLinearity::ComputeGradient+Backpropagate");
   const CuMatrix<BaseFloat>& X = GetInput();
   const CuMatrix<BaseFloat>& E = GetErrorInput();
@@ -386,13 +385,11 @@ bool CuBiasedLinearity::ComputeGradientColsumWithBwd(const CuMatrix<BaseFloat>& 
   KTScope kt("gemm_grad+bwd:" + (su == sb ? su : su + "+" + sb),
              2.0 * X.Rows() * GetNInputs() * GetNOutputs() + 2.0 * E2.Rows() * below.GetNInputs() * below.GetNOutputs(),
              2);
-  const CuMatrix<BaseFloat>* wt =
-      use_shadow && below.HasShadow() ? &const_cast<CuBiasedLinearity&>(below).ShadowForBwd() : nullptr;
-  const CuMatrix<BaseFloat>& wb = wt ? *wt : below.LinearityRO();
-  const int st = (wt ? tnet_affine_grad_bwd_pair_t : tnet_affine_grad_bwd_pair)(
+  const int st = tnet_affine_grad_bwd_pair(
       X.pCUData(), X.Dim(), E.pCUData(), E.Dim(), mGradW.pCUData(), mGradW.Dim(), colpart.pCUData(),
-      (int)colpart.Stride(), mGradB.pCUData(), E2.pCUData(), E2.Dim(), wb.pCUData(), wb.Dim(), Ybelow.pCUData(),
-      (int)Ybelow.Stride(), Eo.pCUData(), Eo.Dim(), colpart2.pCUData(), (int)colpart2.Stride(), S);
+      (int)colpart.Stride(), mGradB.pCUData(), E2.pCUData(), E2.Dim(), below.Linearity().pCUData(),
+      below.Linearity().Dim(), Ybelow.pCUData(), (int)Ybelow.Stride(), Eo.pCUData(), Eo.Dim(), colpart2.pCUData(),
+      (int)colpart2.Stride(), S);
   if (st == TNET_ERR_UNSUPPORTED) {
     kt.Cancel();
     return false;
@@ -433,38 +430,20 @@ void CuBiasedLinearity::ApplyGradient(size_t frames, void* stream, const GradExc
   TnetSgdSeg seg[4];
   float scale;
   const int nseg = ApplySegments(frames, ex, seg, &scale);
-  // a layer keeping a transposed shadow whose W this rank applies whole: the apply writes W^T too (the next
-  // step's backward reads it NN); else the flat apply and the shadow is rebuilt when next read (ShadowForBwd)
-  const long nw = (long)(mLinearity.Rows() * mLinearity.Stride());
-  const bool whole = nseg >= 1 && seg[0].p == mLinearity.pCUData() && seg[0].n == nw;
-  const TnetSgdShadow sh{0, (int)mLinearity.Rows(), (int)mLinearity.Cols(), (int)mLinearity.Stride(),
-                         mLinearityT.pCUData(), (int)mLinearityT.Stride()};
-  auto apply = [&](void* st) {
-    if (mShadowOn && whole) {
-      const int r = tnet_sgd_update_multi_t(seg, nseg, scale, mMomentum, &sh, st);
-      if (r != TNET_ERR_UNSUPPORTED) {
-        TNET_SAFE_CALL(r);
-        mShadowValid = true;
-        return;
-      }
-    }
-    TNET_SAFE_CALL(tnet_sgd_update_multi(seg, nseg, scale, mMomentum, st));
-  };
   if (stream) {  // beside the compute stream (GradExchange::ApplyStream): no library-stream timing
-    apply(stream);
+    TNET_SAFE_CALL(tnet_sgd_update_multi(seg, nseg, scale, mMomentum, stream));
     return;
   }
   KTScope kt("sgd_apply:" + std::to_string(GetNInputs()) + "x" + std::to_string(GetNOutputs()),
              12.0 * (double)(mLinearity.Rows() * mLinearity.Stride() + mBias.Dim()));
-  apply(S);
+  TNET_SAFE_CALL(tnet_sgd_update_multi(seg, nseg, scale, mMomentum, S));
 }
 
 void CuBiasedLinearity::ApplyGradients(CuBiasedLinearity* const* ls, int n, size_t frames, const GradExchange* ex) {
   CuProfileScope p("CuBiasedLinearity::ApplyGradient");
   TnetSgdSeg seg[8];
   float scale[2];
-  // (a layer keeping a transposed shadow takes its own launch, which writes it)
-  bool same = n == 2 && ls[0]->mMomentum == ls[1]->mMomentum && !ls[0]->mShadowOn && !ls[1]->mShadowOn;
+  bool same = n == 2 && ls[0]->mMomentum == ls[1]->mMomentum;
   int nseg = 0;
   for (int i = 0; i < n && same; ++i) nseg += ls[i]->ApplySegments(frames, ex, seg + nseg, &scale[i]);
   if (!same || scale[0] != scale[1]) {  // other constants: one launch per layer

@@ -35,12 +35,11 @@ class CuBiasedLinearity : public CuUpdatableComponent {
   bool ComputeGradientColsumGather(const CuMatrix<BaseFloat>& colpart, const BunchGather& g,
                                    CuBiasedLinearity* other = nullptr, const CuMatrix<BaseFloat>* colpart2 = nullptr);
   // ComputeGradientColsum(colpart) of THIS layer (inputs as set by SetInput / SetErrorInput) and below's backward
-  // Eo = (E2 W_below^T) .* Ybelow (1 - Ybelow) + Eo's slab sums in ONE launch (tnet_affine_grad_bwd_pair; from
-  // below's transposed shadow when use_shadow and it keeps one, tnet_affine_grad_bwd_pair_t); false: nothing
-  // enqueued (make the two calls)
+  // Eo = (E2 W_below^T) .* Ybelow (1 - Ybelow) + Eo's slab sums in ONE launch (tnet_affine_grad_bwd_pair); false:
+  // nothing enqueued (make the two calls)
   bool ComputeGradientColsumWithBwd(const CuMatrix<BaseFloat>& colpart, const CuBiasedLinearity& below,
                                     const CuMatrix<BaseFloat>& E2, const CuMatrix<BaseFloat>& Ybelow,
-                                    CuMatrix<BaseFloat>& Eo, CuMatrix<BaseFloat>& colpart2, bool use_shadow);
+                                    CuMatrix<BaseFloat>& Eo, CuMatrix<BaseFloat>& colpart2);
   void ApplyGradient(size_t frames, void* stream = nullptr, const GradExchange* ex = nullptr) override;
   /// the applies of n (<= 2) layers on the compute stream in ONE launch when their SGD constants agree (the
   /// data-parallel step's inline exchange, GradExchange::SubmitInline); else ApplyGradient per layer

@@ -268,14 +268,12 @@ void CuNetwork::TrainBunch(const CuMatrix<BaseFloat>& X, const CuVector<int>& la
   }
   mNetComponents.front()->SetInput(X);
   // the backward GEMMs read each weight's transposed shadow (NN: the forward's layout and direct form), which the
-  // fused updates keep current in the same pass (CuBiasedLinearity::UseShadow) and the data-parallel step's apply
-  // writes beside W (tnet_sgd_update_multi_t; not under the sharded apply, whose ranks update parts of W).  TNET_BWD_SHADOW: 2 (default) the hidden layers' backward GEMMs, whose 2048^2
+  // fused updates keep current in the same pass (CuBiasedLinearity::UseShadow; not in the data-parallel step, whose
+  // flat SGD apply writes no shadow).  TNET_BWD_SHADOW: 2 (default) the hidden layers' backward GEMMs, whose 2048^2
   // shadow costs the update ~1 us and saves the backward ~5 (the top layer's 32 MB shadow costs its update 12 us for
   // an 8.5 us faster backward: profiles/r05_bwd_shadow_ab.json); 1 every layer above the first; 0 none (NT from W)
   static const int use_shadow = getenv("TNET_BWD_SHADOW") ? atoi(getenv("TNET_BWD_SHADOW")) : 2;
-  // (TNET_DP_SHADOW=0: the data-parallel step without the shadow -- the NT backward from W, A/B)
-  static const bool dp_shadow = !(getenv("TNET_DP_SHADOW") && getenv("TNET_DP_SHADOW")[0] == '0');
-  const bool shadows = use_shadow > 0 && train && (!exchange || (dp_shadow && exchange->ApplyWhole()));
+  const bool shadows = use_shadow > 0 && train && !exchange;
   if (shadows)
     for (int l = 1; l < (use_shadow == 2 ? nl - 1 : nl); l++)
       static_cast<CuBiasedLinearity*>(mNetComponents[2 * l])->UseShadow();
@@ -434,7 +432,7 @@ void CuNetwork::TrainBunch(const CuMatrix<BaseFloat>& X, const CuVector<int>& la
       if (below->LearnRate() > 0.0f) {
         CuMatrix<BaseFloat>& cp = *mColPart[l - 1];
         cp.Init(tnet_colsum_slabs((int)rows), lin->GetNInputs());
-        if (pgrad && pgrad->ComputeGradientColsumWithBwd(*mColPart[pgrad_l], *lin, *err, *acts[l], *eo, cp, shadows)) {
+        if (pgrad && pgrad->ComputeGradientColsumWithBwd(*mColPart[pgrad_l], *lin, *err, *acts[l], *eo, cp)) {
           submit_layer(pgrad, false);
           pgrad = nullptr;
           eo_colsum = true;

@@ -58,8 +58,6 @@ class GradExchange {
   /// The element ranges [lo[k], hi[k]) of an n-element block this rank applies after the block's
   /// reduction; returns the range count (<= 2).  Default: the whole block.
   virtual int ApplyRanges(long n, long* lo, long* hi) const { return FullRange(n, lo, hi); }
-  /// true when this rank applies every parameter block whole (no sharded apply)
-  virtual bool ApplyWhole() const { return true; }
   /// After submission i's applies were enqueued (on `stream`; nullptr = the compute stream): bring
   /// every rank's updated elements of comp's parameter blocks.  No-op without sharding.
   virtual void GatherParams(CuUpdatableComponent& comp, int i, void* stream) {

@@ -119,7 +119,6 @@ class HostExchange : public GradExchange {
   /// with every element outside the rank's shard zeroed, rank 0 contributing the tails) -- a test
   /// of the shard split on one device, not a fast path
   int ApplyRanges(long n, long* lo, long* hi) const override;
-  bool ApplyWhole() const override { return !mShard; }
   void GatherParams(CuUpdatableComponent& comp, int i, void* stream) override;
   /// TNET_DP_HOST_INLINE=1: hand out the compute stream as the apply stream (Submit is synchronous,
   /// so the layer's reduction is done), which puts CuNetwork on the per-layer reduce -> apply ->
@@ -156,7 +155,6 @@ class RcclExchange : public GradExchange {
   /// shard, GatherParams all-gathers the updated parameters in place on the communication stream --
   /// the apply's HBM traffic divided by the world size, the same bytes over xGMI as an all-reduce
   int ApplyRanges(long n, long* lo, long* hi) const override;
-  bool ApplyWhole() const override { return !mShard; }
   void GatherParams(CuUpdatableComponent& comp, int i, void* stream) override;
   int TransportRanks() const override;
 

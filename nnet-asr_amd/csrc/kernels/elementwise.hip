@@ -142,9 +142,12 @@ struct SgdSegs {
   int first[SGD_MAXSEG + 1];
   int nseg;
 };
-// block `blk` of segment sg's nb blocks
-__device__ __forceinline__ void sgd_seg_blocks(const TnetSgdSeg& sg, long blk, long nb, float scale, float mmt) {
-  const long t0 = blk * blockDim.x + threadIdx.x, step = nb * blockDim.x;
+__global__ __launch_bounds__(EW_THREADS) void sgd_multi_kernel(const SgdSegs segs, float scale, float mmt) {
+  int k = 0;
+  while (k + 1 < segs.nseg && (int)blockIdx.x >= segs.first[k + 1]) ++k;
+  const TnetSgdSeg sg = segs.s[k];
+  const long nb = segs.first[k + 1] - segs.first[k];
+  const long t0 = (long)(blockIdx.x - segs.first[k]) * blockDim.x + threadIdx.x, step = nb * blockDim.x;
   const bool v4 = ((sg.n & 3) == 0) && (((uintptr_t)sg.p | (uintptr_t)sg.g | (uintptr_t)sg.corr) & 15) == 0;
   if (v4) {
     // U vectors per thread per pass, every load of the pass issued before the first store: the launch is
@@ -198,84 +201,6 @@ __device__ __forceinline__ void sgd_seg_blocks(const TnetSgdSeg& sg, long blk, l
       w = w + scale * c;
       w = w + sg.l2 * w;
       sg.p[i] = w;
-    }
-  }
-}
-
-__global__ __launch_bounds__(EW_THREADS) void sgd_multi_kernel(const SgdSegs segs, float scale, float mmt) {
-  int k = 0;
-  while (k + 1 < segs.nseg && (int)blockIdx.x >= segs.first[k + 1]) ++k;
-  sgd_seg_blocks(segs.s[k], blockIdx.x - segs.first[k], segs.first[k + 1] - segs.first[k], scale, mmt);
-}
-
-// sgd_multi_kernel with one segment a weight matrix whose transpose is written too (the data-parallel apply keeping
-// the backward's shadow): blocks [0, tiles) take 64 x 64 tiles of it -- each thread 4 rows x 4 columns, loads of the
-// three operands row-contiguous, the new W through LDS into 64 x 64 tiles of the transpose, row-contiguous again --
-// and the blocks after them the other segments as sgd_multi_kernel.  Per element the flat kernel's arithmetic
-// (f32x4 lanes: c = g + mmt q ; w = w + scale c ; w = w + l2 w).
-struct SgdShadowT {
-  float* p;
-  const float* g;
-  float* corr;
-  float* t;
-  int rows, ld, cols, ldt, tn, tiles;  // tn: tiles along the columns
-  float l2;
-};
-constexpr int SGDT = 64;
-__global__ __launch_bounds__(EW_THREADS) void sgd_multi_t_kernel(const SgdSegs segs, const SgdShadowT sh, float scale,
-                                                                 float mmt) {
-  if ((int)blockIdx.x >= sh.tiles) {
-    const int b = blockIdx.x - sh.tiles;
-    int k = 0;
-    while (k + 1 < segs.nseg && b >= segs.first[k + 1]) ++k;
-    sgd_seg_blocks(segs.s[k], b - segs.first[k], segs.first[k + 1] - segs.first[k], scale, mmt);
-    return;
-  }
-  __shared__ float tile[SGDT][SGDT + 1];
-  const int r0 = (blockIdx.x / sh.tn) * SGDT, c0 = (blockIdx.x % sh.tn) * SGDT;
-  const int tid = threadIdx.x, cq = (tid & 15) * 4, rr = tid >> 4;
-  const __amdgpu_buffer_rsrc_t rp = tile_rsrc(sh.p), rq = tile_rsrc(sh.corr ? sh.corr : sh.p), rt = tile_rsrc(sh.t);
-  f32x4 c[4], w[4];
-  bool in[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int r = r0 + rr + 16 * i;
-    in[i] = r < sh.rows && c0 + cq < sh.ld;  // the padding columns too (zero in W and G: they stay zero)
-    if (in[i]) {
-      const long o = (long)r * sh.ld + c0 + cq;
-      c[i] = *reinterpret_cast<const f32x4*>(sh.g + o);
-      w[i] = *reinterpret_cast<const f32x4*>(sh.p + o);
-      if (sh.corr) c[i] = c[i] + mmt * *reinterpret_cast<const f32x4*>(sh.corr + o);
-    }
-  }
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    if (!in[i]) continue;
-    const long o = (long)(r0 + rr + 16 * i) * sh.ld + c0 + cq;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      w[i][e] = w[i][e] + scale * c[i][e];
-      w[i][e] = w[i][e] + sh.l2 * w[i][e];
-      tile[rr + 16 * i][cq + e] = w[i][e];
-    }
-    if (sh.corr) st_wt(rq, o, c[i]);
-    st_wt(rp, o, w[i]);
-  }
-  __syncthreads();
-  // the transpose: row c0 + cc of t holds column c0 + cc of the tile, 4 consecutive W rows a lane
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int u = tid + EW_THREADS * j, cc = u >> 4, r4 = (u & 15) * 4;
-    const int col = c0 + cc, r = r0 + r4;
-    if (col >= sh.cols || r >= sh.rows) continue;
-    const long o = (long)col * sh.ldt + r;
-    if (r + 3 < sh.rows) {
-      f32x4 v;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] = tile[r4 + e][cc];
-      st_wt(rt, o, v);
-    } else {
-      for (int e = 0; r + e < sh.rows; ++e) sh.t[o + e] = tile[r4 + e][cc];
     }
   }
 }
@@ -463,53 +388,5 @@ extern "C" int tnet_sgd_update_multi(const TnetSgdSeg* segs, int nseg, float sca
     sgd_multi_kernel<<<blocks, EW_THREADS, 0, STREAM>>>(a, scale, mmt);
     TNET_LAUNCH_CHECK();
   }
-  return TNET_OK;
-}
-
-extern "C" int tnet_sgd_update_multi_t(const TnetSgdSeg* segs, int nseg, float scale, float mmt,
-                                       const TnetSgdShadow* sh, void* stream) {
-  if (!sh) return tnet_sgd_update_multi(segs, nseg, scale, mmt, stream);
-  if (nseg <= 0 || !segs || sh->seg < 0 || sh->seg >= nseg) return TNET_ERR_ARG;
-  const TnetSgdSeg& m = segs[sh->seg];
-  if (sh->rows < 0 || sh->cols < 0 || sh->ld < sh->cols || m.n != (long)sh->rows * sh->ld || !sh->t ||
-      sh->ldt < sh->rows || !m.p || !m.g || (mmt != 0.f && !m.corr))
-    return TNET_ERR_ARG;
-  if (nseg > SGD_MAXSEG || (sh->ld & 3) || (sh->ldt & 3) ||
-      (((uintptr_t)m.p | (uintptr_t)m.g | (uintptr_t)m.corr | (uintptr_t)sh->t) & 15) ||
-      4L * m.n >= (1L << 31) || 4L * sh->cols * sh->ldt >= (1L << 31))
-    return TNET_ERR_UNSUPPORTED;
-  // the transpose may alias none of the segments' operands
-  const char* t0 = reinterpret_cast<const char*>(sh->t);
-  const char* t1 = t0 + 4L * sh->cols * sh->ldt;
-  for (int k = 0; k < nseg; ++k)
-    for (const void* q : {(const void*)segs[k].p, (const void*)segs[k].g, (const void*)segs[k].corr}) {
-      if (!q) continue;
-      const char* a0 = reinterpret_cast<const char*>(q);
-      if (a0 < t1 && t0 < a0 + 4L * segs[k].n) return TNET_ERR_ARG;
-    }
-  SgdShadowT T{m.p, m.g, m.corr, sh->t, sh->rows, sh->ld, sh->cols, sh->ldt, (sh->ld + SGDT - 1) / SGDT, 0, m.l2};
-  T.tiles = ((sh->rows + SGDT - 1) / SGDT) * T.tn;
-  // the other segments as tnet_sgd_update_multi places them (blocks in proportion to their sizes, its cap)
-  SgdSegs a{};
-  long total = 0;
-  for (int k = 0; k < nseg; ++k) {
-    const TnetSgdSeg& sg = segs[k];
-    if (sg.n < 0 || (sg.n && (!sg.p || !sg.g)) || (mmt != 0.f && sg.n && !sg.corr)) return TNET_ERR_ARG;
-    if (k == sh->seg || !sg.n) continue;
-    total += sg.n;
-    a.s[a.nseg++] = sg;
-  }
-  int blocks = 0;
-  if (a.nseg) {
-    const long want = std::min(1024L, (total / 4 + EW_THREADS - 1) / EW_THREADS);
-    for (int k = 0; k < a.nseg; ++k) {
-      a.first[k] = blocks;
-      blocks += (int)std::max(1L, (long)((double)want * a.s[k].n / total + 0.5));
-    }
-  }
-  a.first[a.nseg] = blocks;
-  if (!T.tiles && !blocks) return TNET_OK;
-  sgd_multi_t_kernel<<<T.tiles + blocks, EW_THREADS, 0, STREAM>>>(a, T, scale, mmt);
-  TNET_LAUNCH_CHECK();
   return TNET_OK;
 }

@@ -2155,72 +2155,49 @@ __global__ __launch_bounds__(kSxThreads) void affine_softmax_xent_kernel(
     }
   }
   __syncthreads();
-  // ---- softmax / xent / error, a wave per row: rows wv and wv + NW of the slab together, their loads and
-  // reductions interleaved (two independent chains a wave; each row's arithmetic and lane map as before)
-  static_assert(2 * NW >= kColsumSlabRows, "two rows a wave cover the slab");
+  // ---- softmax / xent / error, a wave per row (rows wv, wv + NW, ...)
   double wx = 0.0, wc = 0.0;
-  {
-    float x[2][4], zt[2], m[2], sf[2];
-    int cl[4], t[2];
-    bool live[2];
+  for (int r = wv; r < nr; r += NW) {
+    float* zr = zs + r * kSxMaxN;
+    const long row = r0 + r;
+    int t = s_lab[r];
+    if (t >= N) t = -1;  // unlabeled (the host intake rejects such a label, CheckLabels)
+    float x[4];
+    int cl[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) cl[j] = v4 ? 4 * lane + j : lane + 64 * j;
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int r = wv + h * NW;
-      live[h] = r < nr;
-      const float* zr = zs + (live[h] ? r : 0) * kSxMaxN;
-      t[h] = live[h] ? s_lab[r] : -1;
-      if (t[h] >= N) t[h] = -1;  // unlabeled (the host intake rejects such a label, CheckLabels)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) x[h][j] = cl[j] < N ? zr[cl[j]] : -1e30f;
-      zt[h] = t[h] >= 0 ? zr[t[h]] : 0.f;
-      m[h] = -1e20f;
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        if (cl[j] < N) m[h] = fmaxf(m[h], x[h][j]);
+    for (int j = 0; j < 4; ++j) {
+      cl[j] = v4 ? 4 * lane + j : lane + 64 * j;
+      x[j] = cl[j] < N ? zr[cl[j]] : -1e30f;
     }
-    m[0] = wave_max(m[0]);
-    m[1] = wave_max(m[1]);
+    const float zt = t >= 0 ? zr[t] : 0.f;
+    float m = -1e20f;
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      sf[h] = 0.f;
+    for (int j = 0; j < 4; ++j)
+      if (cl[j] < N) m = fmaxf(m, x[j]);
+    m = wave_max(m);
+    float s = 0.f;
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
-        if (cl[j] < N) {
-          x[h][j] = fast_exp(x[h][j] - m[h]);
-          sf[h] += x[h][j];
-        }
-    }
-    const double d0 = wave_sum_d((double)sf[0]), d1 = wave_sum_d((double)sf[1]);
-    const float rs[2] = {1.f / (float)d0, 1.f / (float)d1};
-    ArgMax ay[2] = {{-1e20f, 0x7fffffff}, {-1e20f, 0x7fffffff}};
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      if (!live[h]) continue;
-      const int r = wv + h * NW;
-      float* zr = zs + r * kSxMaxN;
-      const long row = r0 + r;
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        if (cl[j] < N) {
-          const float y = x[h][j] * rs[h];
-          if (y > ay[h].v) { ay[h].v = y; ay[h].i = cl[j]; }
-          const float e = y - (cl[j] == t[h] ? 1.f : 0.f);
-          if (Y) Y[row * ldy + cl[j]] = y;
-          E[row * lde + cl[j]] = e;
-          zr[cl[j]] = e;  // every lane has read its logits and zt above
-        }
-    }
-    ay[0] = wave_argmax(ay[0]);
-    ay[1] = wave_argmax(ay[1]);
-    if (lane == 0) {
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        if (!live[h]) continue;
-        if (t[h] >= 0) wx += -(double)logf(fmaxf(fast_exp(zt[h] - m[h]) * rs[h], FLT_MIN));
-        wc += ay[h].i == (t[h] >= 0 ? t[h] : 0) ? 1.0 : 0.0;
+    for (int j = 0; j < 4; ++j)
+      if (cl[j] < N) {
+        x[j] = fast_exp(x[j] - m);
+        s += x[j];
       }
+    const float rsum = 1.f / (float)wave_sum_d((double)s);
+    ArgMax ay{-1e20f, 0x7fffffff};
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (cl[j] < N) {
+        const float y = x[j] * rsum;
+        if (y > ay.v) { ay.v = y; ay.i = cl[j]; }
+        const float e = y - (cl[j] == t ? 1.f : 0.f);
+        if (Y) Y[row * ldy + cl[j]] = y;
+        E[row * lde + cl[j]] = e;
+        zr[cl[j]] = e;  // every lane has read its logits and zt above
+      }
+    ay = wave_argmax(ay);
+    if (lane == 0) {
+      if (t >= 0) wx += -(double)logf(fmaxf(fast_exp(zt - m) * rsum, FLT_MIN));
+      wc += ay.i == (t >= 0 ? t : 0) ? 1.0 : 0.0;
     }
   }
   if (lane == 0) {
@@ -2239,29 +2216,13 @@ __global__ __launch_bounds__(kSxThreads) void affine_softmax_xent_kernel(
     atomicAdd(stats + 2 * slot, sx);
     atomicAdd(stats + 2 * slot + 1, sc);
   }
-  // ---- the slab's column sums of the error: 8 row groups of 4 rows summed in parallel (fp32, row order within a
-  // group), the groups then added in group order -- a 4-deep chain of LDS reads a thread instead of 32
-  if (cpart) {
-    constexpr int NG = 8, GR = kColsumSlabRows / NG;
-    __shared__ float gsum[NG][kSxMaxN];
-    for (int u = tid; u < NG * N; u += kSxThreads) {
-      const int g = u / N, c = u % N;
-      float a = 0.f;
-#pragma unroll
-      for (int q = 0; q < GR; ++q) {
-        const int r = g * GR + q;
-        if (r < nr) a += zs[r * kSxMaxN + c];
-      }
-      gsum[g][c] = a;
-    }
-    __syncthreads();
+  // ---- the slab's column sums of the error
+  if (cpart)
     for (int c = tid; c < N; c += kSxThreads) {
-      float a = gsum[0][c];
-#pragma unroll
-      for (int g = 1; g < NG; ++g) a += gsum[g][c];
+      float a = 0.f;
+      for (int r = 0; r < nr; ++r) a += zs[r * kSxMaxN + c];
       cpart[(long)blockIdx.x * ldcpart + c] = a;
     }
-  }
 }
 
 // per-stream partial-product workspace of the split-K path (grown on demand; the library enqueues
@@ -2549,7 +2510,7 @@ static bool launch_sk(const GemmP& p, hipStream_t st) {
   forced_cfg();
   if (g_reserve <= 0) return false;
   constexpr bool OK = (BM == 64 && BN == 128 && A_KC && B_KC && EPI == EPI_DSIG_CS) ||
-                      (BM == 64 && BN == 128 && A_KC && !B_KC && (EPI == EPI_BIAS_SIG || EPI == EPI_DSIG_CS)) ||
+                      (BM == 64 && BN == 128 && A_KC && !B_KC && EPI == EPI_BIAS_SIG) ||
                       (BM == 128 && BN == 128 && !A_KC && !B_KC && (EPI == EPI_STORE_BG || EPI == EPI_STORE));
   if constexpr (!OK) {
     return false;
@@ -2712,19 +2673,12 @@ static int launch_colsum_bwd(const GemmP& p_in, hipStream_t st) {
 // grid in the forward's direct form (m64x128a8) where it gives ~one workgroup per CU, else 64x64 tiles (32-row
 // wave tiles = slabs either way).  Per output element the MFMA operands and their order are the NT kernel's
 // (the lane -> k map is layout-independent): Eo is bit-identical to launch_colsum_bwd's; the slab sums add the
-// same rows in another order.  While CUs are reserved for RCCL: the 64x128 stream-K grid over the CUs left (its
-// pieces in the direct form), else TNET_ERR_UNSUPPORTED (the caller takes the NT form).
+// same rows in another order.  Not while CUs are reserved for RCCL (the caller takes the NT stream-K form).
 static int launch_colsum_bwd_t(const GemmP& p_in, hipStream_t st) {
   if (p_in.M <= 0 || p_in.N <= 0) return TNET_OK;
-  if (forced_cfg() >= 0) return TNET_ERR_UNSUPPORTED;
+  if (g_reserve > 0 || forced_cfg() >= 0) return TNET_ERR_UNSUPPORTED;
   GemmP p = p_in;
   p.group = g_group > 0 ? g_group : 8;
-  if (g_reserve > 0) {
-    if ((long)cdiv(p.M, 64) * cdiv(p.N, 128) < 200 || !launch_sk<64, 128, true, false, EPI_DSIG_CS>(p, st))
-      return TNET_ERR_UNSUPPORTED;
-    TNET_LAUNCH_CHECK();
-    return TNET_OK;
-  }
   bool ok;
   if ((long)cdiv(p.M, 64) * cdiv(p.N, 128) >= 200)
     ok = g_direct > 0 ? launch_cfg<1, 64, 128, 64, 2, 2, 2, 6, true, false, EPI_DSIG_CS>(p, st)
@@ -3703,18 +3657,17 @@ extern "C" int tnet_affine_update_bwd_pair_t(const float* X, TnetMatrixDim dX, c
                          dE2, W2t, dW2t, Ybelow, strideYbelow, Eo, dEo, colpart2, ldcolpart2, stream, true);
 }
 
-static int grad_bwd_pair(const float* X, TnetMatrixDim dX, const float* E, TnetMatrixDim dE, float* G,
-                         TnetMatrixDim dG, const float* colpart, int ldcolpart, float* gradB, const float* E2,
-                         TnetMatrixDim dE2, const float* W2, TnetMatrixDim dW2, const float* Ybelow, int strideYbelow,
-                         float* Eo, TnetMatrixDim dEo, float* colpart2, int ldcolpart2, void* stream, bool bwd_t) {
+extern "C" int tnet_affine_grad_bwd_pair(const float* X, TnetMatrixDim dX, const float* E, TnetMatrixDim dE, float* G,
+                                        TnetMatrixDim dG, const float* colpart, int ldcolpart, float* gradB,
+                                        const float* E2, TnetMatrixDim dE2, const float* W2, TnetMatrixDim dW2,
+                                        const float* Ybelow, int strideYbelow, float* Eo, TnetMatrixDim dEo,
+                                        float* colpart2, int ldcolpart2, void* stream) {
   // tnet_affine_grad_bias(X, E, G, colpart, gradB) and tnet_affine_bwd_colsum(E2, W2, Ybelow, Eo, colpart2) in one
   // launch (the data-parallel step's gradient of layer l and the backward GEMM of layer l-1); independent: G / gradB
-  // / Eo / colpart2 overlap none of the other's operands.  bwd_t: W2 is the lower layer's transposed shadow
-  // [n_out x n_in] (tnet_affine_bwd_colsum_t's operand)
+  // / Eo / colpart2 overlap none of the other's operands
   if (dX.rows != dE.rows || dG.rows != dX.cols || dG.cols != dE.cols || !colpart || !gradB || ldcolpart < dE.cols)
     return TNET_ERR_ARG;
-  const int w2_k = bwd_t ? dW2.rows : dW2.cols, w2_n = bwd_t ? dW2.cols : dW2.rows;
-  if (dE2.cols != w2_k || dEo.rows != dE2.rows || dEo.cols != w2_n || !Ybelow || !colpart2 ||
+  if (dE2.cols != dW2.cols || dEo.rows != dE2.rows || dEo.cols != dW2.rows || !Ybelow || !colpart2 ||
       ldcolpart2 < dEo.cols || !aligned16(Ybelow) || (strideYbelow & 3))
     return TNET_ERR_ARG;
   GemmP pu{};
@@ -3726,7 +3679,7 @@ static int grad_bwd_pair(const float* X, TnetMatrixDim dX, const float* E, TnetM
   int st = check_common(pu);
   if (st) return st;
   GemmP pb{};
-  pb.M = dE2.rows; pb.N = w2_n; pb.K = dE2.cols;
+  pb.M = dE2.rows; pb.N = dW2.rows; pb.K = dE2.cols;
   pb.A = E2; pb.lda = dE2.stride; pb.B = W2; pb.ldb = dW2.stride; pb.C = Eo; pb.ldc = dEo.stride;
   pb.alpha = 1.f; pb.beta = 0.f;
   pb.aux = Ybelow; pb.ldaux = strideYbelow;
@@ -3741,25 +3694,7 @@ static int grad_bwd_pair(const float* X, TnetMatrixDim dX, const float* E, TnetM
       any_overlap({wb[0], wb[1]}, {span_of(X, dX.rows, dX.stride, 4), span_of(E, dE.rows, dE.stride, 4),
                                    span_of(colpart, tnet_colsum_slabs(dE.rows), ldcolpart, 4)}))
     return TNET_ERR_ARG;
-  return launch_pair_a_bwd<EPI_STORE_BG>(pu, pb, (hipStream_t)stream, bwd_t);
-}
-
-extern "C" int tnet_affine_grad_bwd_pair(const float* X, TnetMatrixDim dX, const float* E, TnetMatrixDim dE, float* G,
-                                        TnetMatrixDim dG, const float* colpart, int ldcolpart, float* gradB,
-                                        const float* E2, TnetMatrixDim dE2, const float* W2, TnetMatrixDim dW2,
-                                        const float* Ybelow, int strideYbelow, float* Eo, TnetMatrixDim dEo,
-                                        float* colpart2, int ldcolpart2, void* stream) {
-  return grad_bwd_pair(X, dX, E, dE, G, dG, colpart, ldcolpart, gradB, E2, dE2, W2, dW2, Ybelow, strideYbelow, Eo, dEo,
-                       colpart2, ldcolpart2, stream, false);
-}
-
-extern "C" int tnet_affine_grad_bwd_pair_t(const float* X, TnetMatrixDim dX, const float* E, TnetMatrixDim dE, float* G,
-                                          TnetMatrixDim dG, const float* colpart, int ldcolpart, float* gradB,
-                                          const float* E2, TnetMatrixDim dE2, const float* W2t, TnetMatrixDim dW2t,
-                                          const float* Ybelow, int strideYbelow, float* Eo, TnetMatrixDim dEo,
-                                          float* colpart2, int ldcolpart2, void* stream) {
-  return grad_bwd_pair(X, dX, E, dE, G, dG, colpart, ldcolpart, gradB, E2, dE2, W2t, dW2t, Ybelow, strideYbelow, Eo,
-                       dEo, colpart2, ldcolpart2, stream, true);
+  return launch_pair_a_bwd<EPI_STORE_BG>(pu, pb, (hipStream_t)stream);
 }
 
 extern "C" int tnet_affine_grad_bias(const float* X, TnetMatrixDim dX, const float* E, TnetMatrixDim dE, float* G,

@@ -67,12 +67,20 @@ void top_rows_kernel(const TopRowsP q) {
 #pragma unroll
       for (int s = 0; s < 4; ++s) bf[t][c][s] = wb[(long)(16 * c + s) * q.ldw];
   }
+  // Every load of the block issued before the first MFMA, and the MFMA chain free of anything else (only its
+  // counted waits).  Without a fence the scheduler interleaves loads and MFMAs to save registers (60 instead of 275
+  // VGPRs: 30.5 us for the top layer in the step); a sched_barrier alone keeps the loads ahead but lets spill reloads
+  // and the stores' address arithmetic into the chain (12.4 us a launch).  What gives round 5's clean chain (8.6 us,
+  // rocprofv3 in the MLP3 step, profiles/r06_top_rows_schedule.json): a memory-clobbering asm in its own basic block --
+  // the branch is never taken (ldpart >= 16, checked by the launch) -- plus a sched_barrier behind the chain.
+  if (q.ldpart < 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
   for (int c = 0; c < NCH; ++c)
 #pragma unroll
     for (int s = 0; s < 4; ++s)
 #pragma unroll
       for (int t = 0; t < 3; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[c][s], bf[t][c][s], acc[t], 0, 0, 0);
+  __builtin_amdgcn_sched_barrier(0);
   // slice sl's rows 4 lg .. 4 lg + 3 of column (tile, li), row-major at part[sl][row][col] (every column of the
   // 16 NT is written, the padding ones from the clamped W column)
   float* pp = q.part + (long)sl * M * q.ldpart;

@@ -81,13 +81,10 @@ _SIGS = {
     "tnet_affine_grad_bias": (i32, [vp, MatrixDim, vp, MatrixDim, vp, MatrixDim, vp, i32, vp, vp]),
     "tnet_affine_grad_bwd_pair": (i32, [vp, MatrixDim, vp, MatrixDim, vp, MatrixDim, vp, i32, vp, vp, MatrixDim, vp,
                                         MatrixDim, vp, i32, vp, MatrixDim, vp, i32, vp]),
-    "tnet_affine_grad_bwd_pair_t": (i32, [vp, MatrixDim, vp, MatrixDim, vp, MatrixDim, vp, i32, vp, vp, MatrixDim,
-                                          vp, MatrixDim, vp, i32, vp, MatrixDim, vp, i32, vp]),
     "tnet_affine_grad_bias_gather": (i32, [vp, MatrixDim, vp, MatrixDim, vp, MatrixDim, vp, i32, vp, vp, MatrixDim, vp,
                                            MatrixDim, vp, MatrixDim, vp, i32, vp, vp, vp, vp, vp, vp, MatrixDim,
                                            MatrixDim, vp]),
     "tnet_sgd_update_multi": (i32, [vp, i32, f32, f32, vp]),
-    "tnet_sgd_update_multi_t": (i32, [vp, i32, f32, f32, vp, vp]),
     "tnet_affine_bwd_colsum": (i32, [vp, MatrixDim, vp, MatrixDim, vp, i32, vp, MatrixDim, vp, i32, vp]),
     "tnet_affine_bwd_colsum_slabs": (i32, [vp, MatrixDim, vp, MatrixDim, vp, i32, vp, MatrixDim, vp, i32, vp, i32,
                                            vp]),

@@ -550,47 +550,6 @@ def test_sgd_update_multi(mmt, sizes):
             np.testing.assert_allclose(dc.numpy().ravel(), cc, rtol=1e-6, atol=1e-7)
 
 
-class SgdShadow(C.Structure):
-    _fields_ = [("seg", C.c_int), ("rows", C.c_int), ("cols", C.c_int), ("ld", C.c_int), ("t", C.c_void_p),
-                ("ldt", C.c_int)]
-
-
-@pytest.mark.parametrize("mmt", [0.0, 0.9])
-@pytest.mark.parametrize("rows,cols", [(2048, 2048), (440, 2048), (130, 70), (1, 5), (67, 1)])
-def test_sgd_update_multi_t(mmt, rows, cols):
-    """the data-parallel apply that keeps the transposed shadow: W / corr / b bit-identical to tnet_sgd_update_multi,
-    the shadow exactly W^T (edge tiles in both directions, a one-row and a one-column matrix)"""
-    scale, l2 = -0.008, -2e-5
-    W, G, Q = rnd((rows, cols), 81, 0.1), rnd((rows, cols), 82), rnd((rows, cols), 83, 0.05)
-    b, gb, qb = rnd(cols, 84), rnd(cols, 85), rnd(cols, 86, 0.05)
-    runs = []
-    for shadow in (False, True):
-        dW, dG, dQ = DeviceArray.from_numpy(W), DeviceArray.from_numpy(G), DeviceArray.from_numpy(Q)
-        db, dgb, dqb = DeviceArray.vector(b), DeviceArray.vector(gb), DeviceArray.vector(qb)
-        dT = DeviceArray(cols, rows)
-        segs = (SgdSeg * 2)(SgdSeg(dW.ptr, dG.ptr, dQ.ptr if mmt else None, rows * dW.stride, l2),
-                            SgdSeg(db.ptr, dgb.ptr, dqb.ptr if mmt else None, cols, 0.0))
-        if shadow:
-            sh = SgdShadow(0, rows, cols, dW.stride, dT.ptr, dT.stride)
-            check(lib().tnet_sgd_update_multi_t(C.cast(segs, C.c_void_p), 2, scale, mmt, C.byref(sh), S()))
-        else:
-            check(lib().tnet_sgd_update_multi(C.cast(segs, C.c_void_p), 2, scale, mmt, S()))
-        runs.append((dW.numpy(), dQ.numpy(), db.numpy(), dqb.numpy(), dT.numpy()))
-    for a, r in zip(runs[1][:4], runs[0][:4]):
-        np.testing.assert_array_equal(a, r)
-    np.testing.assert_array_equal(runs[1][4], runs[1][0].T)
-    cc = G.astype(np.float64) + mmt * Q
-    ref = W + scale * cc
-    np.testing.assert_allclose(runs[1][0], ref + l2 * ref, rtol=1e-6, atol=1e-7)
-
-
-def test_sgd_update_multi_t_rejects_aliasing_shadow():
-    W, G = DeviceArray(64, 64), DeviceArray(64, 64)
-    segs = (SgdSeg * 1)(SgdSeg(W.ptr, G.ptr, None, 64 * W.stride, 0.0))
-    sh = SgdShadow(0, 64, 64, W.stride, G.ptr, G.stride)  # the shadow over the gradient
-    assert lib().tnet_sgd_update_multi_t(C.cast(segs, C.c_void_p), 1, -0.1, 0.0, C.byref(sh), S()) == -1
-
-
 @pytest.mark.parametrize("rows,cols", [(1, 1), (16, 10), (1024, 135), (1024, 4000), (300, 4099), (64, 5000)])
 def test_softmax_xent_labels(rows, cols):
     Z = rnd((rows, cols), 16, 3.0)
