@@ -612,78 +612,115 @@ __global__ __launch_bounds__(1024) void rnn_out_full_kernel(const float* __restr
   const int nout_blocks = (N + 63) / 64;
   if (cr.on && (int)blockIdx.x >= nout_blocks) {
     // ---- the pending recurrent update (rnn_update_kernel's per-element arithmetic and step order; the bias is
-    // the output blocks' business below), 4 consecutive elements of a row a thread
+    // the output blocks' business below), 4 consecutive elements of a row a thread.  Every load is issued before
+    // the first is used -- the row's history values and the 4 columns' d_i at clamped step indices (unconditional:
+    // a predicated load is a branch, and branches serialise the round trips), W's 4 elements -- then the sums.
     const long e0 = ((long)(blockIdx.x - nout_blocks) * 1024 + threadIdx.x) * 4;
     const int k = (int)(e0 / H), c0 = (int)(e0 % H);
     if (k >= cr.rows) return;
     float hk[GV_UPD_MAX];
+    f32x4 dv[GV_UPD_MAX];
 #pragma unroll
     for (int i = 0; i < GV_UPD_MAX; ++i) {
-      if (i >= cr.steps) break;
-      int r = cr.head + i;
+      const int ii = min(i, cr.steps - 1);
+      int r = cr.head + ii;
       r = r >= cr.R ? r - cr.R : r;
       hk[i] = cr.hist[(long)r * cr.ldh + k];
+      dv[i] = *reinterpret_cast<const f32x4*>(cr.D + (long)ii * cr.ldd + c0);
     }
+    float* wp = cr.W + (long)k * cr.ldw + c0;
+    const f32x4 wv = *reinterpret_cast<const f32x4*>(wp);
+    f32x4 out;
+#pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const int c = c0 + j;
-      if (c >= H) break;
       float acc = 0.f;
 #pragma unroll
-      for (int i = 0; i < GV_UPD_MAX; ++i) {
-        if (i >= cr.steps) break;
-        acc = __fmaf_rn(-cr.lr * hk[i], cr.D[(long)i * cr.ldd + c], acc);
-      }
-      float* wp = cr.W + (long)k * cr.ldw + c;
-      const float wv = *wp;
-      const float corr = __fmaf_rn(-cr.lr * cr.wc, wv, acc);
-      *wp = corr + wv;
+      for (int i = 0; i < GV_UPD_MAX; ++i)
+        if (i < cr.steps) acc = __fmaf_rn(-cr.lr * hk[i], dv[i][j], acc);
+      const float corr = __fmaf_rn(-cr.lr * cr.wc, wv[j], acc);
+      out[j] = corr + wv[j];
     }
+    *reinterpret_cast<f32x4*>(wp) = out;
     return;
   }
-  if (cr.on && threadIdx.x < GV_DOTS) {  // the dots, summed over the slices in slice order
-    float d = 0.f;
-    for (int q = 0; q < hslices; ++q) d += cr.dpart[(long)q * GV_DOTS + threadIdx.x];
-    sdot[threadIdx.x] = d;
-  }
-  if (cr.on) __syncthreads();
   const int c = blockIdx.x * 64 + lane, cc = min(c, N - 1);
-  // the first 32 rows per lane of the column block's Wo issued before the h finish (their latency
-  // overlaps the partial-sum loads)
+  // ONE round of loads before anything waits: the first 32 rows per lane of the column block's Wo, (cr.on, threads
+  // < GV_DOTS) the first 16 slices' partial dots, then per unit k the pending update's d_i at clamped step indices,
+  // the bias operands and the recurrent partial sums.  The dots are summed and shared only after the units' sums,
+  // so their round trip overlaps the others instead of preceding them.
   float wv[32];
 #pragma unroll
   for (int q = 0; q < 32; ++q) {
     const int k = w + 16 * q;
     wv[q] = k < H ? Wo[(long)k * ldw + cc] : 0.f;
   }
-  for (int k = threadIdx.x; k < H; k += 1024) {
-    float sacc = 0.f;
+  const bool dots = cr.on && threadIdx.x < GV_DOTS;
+  float pd[16];
+  if (dots) {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) pd[q] = cr.dpart[(long)min(q, hslices - 1) * GV_DOTS + threadIdx.x];
+  }
+  constexpr int KPT = GV_FULL_MAXH / 1024;  // units per thread
+  float sacc[KPT], g[KPT], dk[KPT][GV_UPD_MAX], hbk[KPT];
+#pragma unroll
+  for (int u = 0; u < KPT; ++u) {
+    const int k = threadIdx.x + 1024 * u;
+    if (k >= H) break;
+    float cbk = 0.f;
+    if (cr.on) {
+#pragma unroll
+      for (int i = 0; i < GV_UPD_MAX; ++i) dk[u][i] = cr.D[(long)min(i, cr.steps - 1) * cr.ldd + k];
+      cbk = cr.cb[k];
+    }
+    hbk[u] = hb ? hb[k] : 0.f;
+    sacc[u] = 0.f;
     for (int q0 = 0; q0 < hslices; q0 += 16) {  // 16 slices' loads in flight, added in slice order
       float p[16];
 #pragma unroll
       for (int q = 0; q < 16; ++q) p[q] = q0 + q < hslices ? hpart[(long)(q0 + q) * H + k] : 0.f;
 #pragma unroll
       for (int q = 0; q < 16; ++q)
-        if (q0 + q < hslices) sacc += p[q];
+        if (q0 + q < hslices) sacc[u] += p[q];
     }
+    if (cr.on) {
+      // the pending bias update (rnn_update_kernel's chain)
+      g[u] = __fmaf_rn(-cr.lr, dk[u][0], cr.mmt * cbk);
+#pragma unroll
+      for (int i = 1; i < GV_UPD_MAX; ++i)
+        if (i < cr.steps) g[u] = __fmaf_rn(-cr.lr, dk[u][i], g[u]);
+    }
+  }
+  if (cr.on) {
+    if (dots) {  // the dots, summed over the slices in slice order
+      float d = 0.f;
+#pragma unroll
+      for (int q = 0; q < 16; ++q)
+        if (q < hslices) d += pd[q];
+      for (int q0 = 16; q0 < hslices; ++q0) d += cr.dpart[(long)q0 * GV_DOTS + threadIdx.x];
+      sdot[threadIdx.x] = d;
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int u = 0; u < KPT; ++u) {
+    const int k = threadIdx.x + 1024 * u;
+    if (k >= H) break;
     float hv;
     if (cr.on) {
-      // the pending bias update (rnn_update_kernel's chain) and the correction of the look-ahead product
-      float g = __fmaf_rn(-cr.lr, cr.D[k], cr.mmt * cr.cb[k]);
+      // the correction of the look-ahead product
       float a = 0.f;
-      a = __fmaf_rn(-cr.lr * sdot[0], cr.D[k], a);
-      for (int i = 1; i < cr.steps; ++i) {
-        const float di = cr.D[(long)i * cr.ldd + k];
-        g = __fmaf_rn(-cr.lr, di, g);
-        a = __fmaf_rn(-cr.lr * sdot[i], di, a);
-      }
-      const float bn = g + hb[k];
+      a = __fmaf_rn(-cr.lr * sdot[0], dk[u][0], a);
+#pragma unroll
+      for (int i = 1; i < GV_UPD_MAX; ++i)
+        if (i < cr.steps) a = __fmaf_rn(-cr.lr * sdot[i], dk[u][i], a);
+      const float bn = g[u] + hbk[u];
       if (blockIdx.x == 0) {
-        cr.cbnext[k] = g;
+        cr.cbnext[k] = g[u];
         cr.bnext[k] = bn;
       }
-      hv = sigmoidf_ref(bn + (__fmaf_rn(-cr.lr * cr.wc, sacc, sacc) + a));
+      hv = sigmoidf_ref(bn + (__fmaf_rn(-cr.lr * cr.wc, sacc[u], sacc[u]) + a));
     } else {
-      hv = sigmoidf_ref((hb ? hb[k] : 0.f) + sacc);
+      hv = sigmoidf_ref(hbk[u] + sacc[u]);
     }
     hs[k] = hv;
     if (blockIdx.x == 0) h[k] = hv;
@@ -1007,7 +1044,7 @@ extern "C" int tnet_rnn_out_full_ahead(const float* hpart, int hslices, const fl
       rows <= 0)
     return TNET_ERR_ARG;
   if (H > GV_FULL_MAXH || cdiv(N, 64) > 64 || steps > GV_UPD_MAX || steps >= R || (H & 3) ||
-      hslices != cdiv(rows, GV_KSLICE))
+      hslices != cdiv(rows, GV_KSLICE) || (ldw & 3) || (ldd & 3) || ((uintptr_t)W & 15) || ((uintptr_t)D & 15))
     return TNET_ERR_UNSUPPORTED;
   RnnCorr cr{};
   cr.on = 1;

@@ -320,8 +320,12 @@ def lib():
         if len(rt) > 1:
             raise TnetError("two HIP runtimes mapped into one process: " + ", ".join(rt) +
                             " (load libtnet_amd through tnet_amd, or set TNET_HIP_RUNTIME consistently)")
+        # (a diagnostic variant -- e.g. an earlier round's build for a same-box A/B -- may lack newer entry points)
+        variant = bool(os.environ.get("TNET_LIB_VARIANT"))
         for name, (res, args) in _SIGS.items():
-            fn = getattr(L, name)
+            fn = getattr(L, name, None) if variant else getattr(L, name)
+            if fn is None:
+                continue
             fn.restype = res
             fn.argtypes = args
         _lib = L
