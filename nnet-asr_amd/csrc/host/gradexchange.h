@@ -10,6 +10,7 @@
 
 #include <cstddef>
 #include <functional>
+#include <utility>
 #include <vector>
 
 namespace TNet {
@@ -129,7 +130,9 @@ class GradExchange {
     long lo[2] = {0, 0}, hi[2] = {0, 0};
     int nr = 0;
   };
-  std::vector<DeviceCapture> mDevCap;  // buffers kept across arms (allocated on the first armed step)
+  std::vector<DeviceCapture> mDevCap;  // buffers kept across arms (allocated when arming, ReserveCapture)
+  std::vector<std::pair<const float*, long>> mSeen;  // the unarmed steps' blocks: parameter address, size
+  void ReserveCapture(size_t k, long n);
   size_t mNumCaptured = 0;
   bool mCapturePending = false;        // device copies not yet read back
   std::vector<CapturedBlock> mCaptured;

@@ -304,29 +304,47 @@ void HostExchange::GatherParams(CuUpdatableComponent& comp, int i, void* stream)
   }
 }
 
+// the device copies of the k-th submitted block (grown when a block is larger than the buffers it has)
+void GradExchange::ReserveCapture(size_t k, long n) {
+  while (mDevCap.size() <= k) mDevCap.emplace_back();
+  DeviceCapture& c = mDevCap[k];
+  if (c.cap >= n) return;
+  if (c.local) TNET_HIP_CALL(hipFree(c.local));
+  if (c.reduced) TNET_HIP_CALL(hipFree(c.reduced));
+  c.local = c.reduced = nullptr;
+  TNET_HIP_CALL(hipMalloc(&c.local, (size_t)n * sizeof(float)));
+  TNET_HIP_CALL(hipMalloc(&c.reduced, (size_t)n * sizeof(float)));
+  c.cap = n;
+}
+
 void GradExchange::ArmCapture(bool on) {
   mCaptureArmed = on;
   if (on) {
     mNumCaptured = 0;
     mCapturePending = false;
     mCaptured.clear();
+    // the copies are allocated HERE, before the armed step, for the blocks the unarmed steps submitted (the same
+    // blocks in the same order every step): the armed step itself then makes no allocation
+    for (size_t k = 0; k < mSeen.size(); ++k) ReserveCapture(k, mSeen[k].second);
   }
 }
 
 size_t GradExchange::CaptureLocal(CuUpdatableComponent& comp, void* stream) {
   const size_t first = mNumCaptured;
-  if (!mCaptureArmed) return first;
-  for (auto& b : comp.GradientBlocks()) {
-    if (mNumCaptured == mDevCap.size()) mDevCap.emplace_back();
-    DeviceCapture& c = mDevCap[mNumCaptured++];
-    if (c.cap < b.n) {  // first armed step (or a larger block): hipMalloc does not synchronise the streams
-      if (c.local) TNET_HIP_CALL(hipFree(c.local));
-      if (c.reduced) TNET_HIP_CALL(hipFree(c.reduced));
-      c.local = c.reduced = nullptr;
-      TNET_HIP_CALL(hipMalloc(&c.local, (size_t)b.n * sizeof(float)));
-      TNET_HIP_CALL(hipMalloc(&c.reduced, (size_t)b.n * sizeof(float)));
-      c.cap = b.n;
+  if (!mCaptureArmed) {
+    // unarmed: remember each parameter block's size in first-submission order (host only, a few entries)
+    for (auto& b : comp.GradientBlocks()) {
+      auto it = std::find_if(mSeen.begin(), mSeen.end(), [&](const std::pair<const float*, long>& e) {
+        return e.first == b.param;
+      });
+      if (it == mSeen.end()) mSeen.emplace_back(b.param, b.n);
+      else it->second = std::max(it->second, b.n);
     }
+    return first;
+  }
+  for (auto& b : comp.GradientBlocks()) {
+    ReserveCapture(mNumCaptured, b.n);  // (allocates only for a block no unarmed step submitted)
+    DeviceCapture& c = mDevCap[mNumCaptured++];
     c.n = b.n;
     c.nr = ApplyRanges(b.n, c.lo, c.hi);
     TNET_HIP_CALL(hipMemcpyAsync(c.local, b.grad, (size_t)b.n * sizeof(float), hipMemcpyDeviceToDevice,

@@ -4,10 +4,11 @@ against an independent sum.
 The product's exchange (trainer.cpp RcclExchange) reduces every layer's gradient in place with RCCL over xGMI, on a
 communication stream ordered by fence-free events.  A wrong reduction (a stale operand, a missed wait) would hand
 every rank the SAME wrong sum, so the replicas stay identical and bench.py's parameter checksum cannot see it.
-Here the exchange is armed for one step (Comm.capture): each gradient block is copied to the host right before its
-reduction (the rank's local gradient) and right after it (the reduced values over the ranges the rank applies);
-the local copies are then summed over the ranks in float64 through a second transport (gloo) and compared with what
-RCCL produced.  The reference's reduction this stands for is the CPU Platform's row-sliced, double-accumulated sum
+Here the exchange is armed for one step (Comm.capture): each gradient block is copied on the device right before its
+reduction (the rank's local gradient) and right after it (the reduced values over the ranges the rank applies), on
+the stream the reduction runs on, into buffers allocated when arming -- the armed step runs the production schedule,
+with no host synchronisation and no allocation inside it -- and read back after the step; the local copies are then
+summed over the ranks in float64 through a second transport (gloo) and compared with what RCCL produced.  The reference's reduction this stands for is the CPU Platform's row-sliced, double-accumulated sum
 of the threads' gradients (src/TNetLib/Platform.h:307-335).
 
 Tolerance: ||rccl - sum64|| / ||sum64|| <= 1e-5 per block over the compared elements (a float32 sum of N terms in
