@@ -131,7 +131,8 @@ class GradExchange {
     int nr = 0;
   };
   std::vector<DeviceCapture> mDevCap;  // buffers kept across arms (allocated when arming, ReserveCapture)
-  std::vector<std::pair<const float*, long>> mSeen;  // the unarmed steps' blocks: parameter address, size
+  std::vector<std::pair<const float*, long>> mSeen;  // the latest unarmed step's blocks: parameter address, size
+  size_t mSeenPos = 0;                                 // the next block's position in that step
   void ReserveCapture(size_t k, long n);
   size_t mNumCaptured = 0;
   bool mCapturePending = false;        // device copies not yet read back

@@ -332,13 +332,20 @@ void GradExchange::ArmCapture(bool on) {
 size_t GradExchange::CaptureLocal(CuUpdatableComponent& comp, void* stream) {
   const size_t first = mNumCaptured;
   if (!mCaptureArmed) {
-    // unarmed: remember each parameter block's size in first-submission order (host only, a few entries)
+    // unarmed: the blocks of the latest step in submission order (host only, a few entries): a step starts again
+    // when its first block recurs; a block out of the recorded order (another network on this exchange) cuts the
+    // record there, so it never holds more than one step's blocks
     for (auto& b : comp.GradientBlocks()) {
-      auto it = std::find_if(mSeen.begin(), mSeen.end(), [&](const std::pair<const float*, long>& e) {
-        return e.first == b.param;
-      });
-      if (it == mSeen.end()) mSeen.emplace_back(b.param, b.n);
-      else it->second = std::max(it->second, b.n);
+      if (mSeenPos < mSeen.size() && mSeen[mSeenPos].first == b.param) {
+        mSeen[mSeenPos].second = std::max(mSeen[mSeenPos].second, b.n);
+      } else if (!mSeen.empty() && mSeen[0].first == b.param) {
+        mSeenPos = 0;
+        mSeen[0].second = std::max(mSeen[0].second, b.n);
+      } else {
+        mSeen.resize(mSeenPos);
+        mSeen.emplace_back(b.param, b.n);
+      }
+      ++mSeenPos;
     }
     return first;
   }
