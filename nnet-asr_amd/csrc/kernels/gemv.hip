@@ -628,8 +628,8 @@ __global__ __launch_bounds__(1024) void rnn_out_full_kernel(const float* __restr
       hk[i] = cr.hist[(long)r * cr.ldh + k];
       dv[i] = *reinterpret_cast<const f32x4*>(cr.D + (long)ii * cr.ldd + c0);
     }
-    float* wp = cr.W + (long)k * cr.ldw + c0;
-    const f32x4 wv = *reinterpret_cast<const f32x4*>(wp);
+    float* wrow = cr.W + (long)k * cr.ldw;
+    const f32x4 wv = *reinterpret_cast<const f32x4*>(wrow + c0);
     f32x4 out;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -640,7 +640,7 @@ __global__ __launch_bounds__(1024) void rnn_out_full_kernel(const float* __restr
       const float corr = __fmaf_rn(-cr.lr * cr.wc, wv[j], acc);
       out[j] = corr + wv[j];
     }
-    *reinterpret_cast<f32x4*>(wp) = out;
+    st_wt(tile_rsrc(wrow), c0, out);  // write-through: no dirty W lines left for the kernel-end release
     return;
   }
   const int c = blockIdx.x * 64 + lane, cc = min(c, N - 1);
@@ -858,6 +858,9 @@ __global__ __launch_bounds__(256) void rnn_out_bwd_kernel(
                    (((uintptr_t)row | (uintptr_t)z | (uintptr_t)qrow) & 15) == 0;
   float acc = 0.f;
   if (vec && n_out <= NP * STEP) {
+    // the updated row (and momentum row) stored write-through: at 4000 outputs the launch rewrites 8-16 MB, which
+    // plain stores would leave dirty for the kernel-end release to write back after the last workgroup
+    const __amdgpu_buffer_rsrc_t wr = tile_rsrc(row), qr = tile_rsrc(qrow ? qrow : row);
     f32x4 a[NP], zv[NP], qv[NP];
     const float* qsrc = qrow ? qrow : row;  // unconditional (no branch in the round); unused without momentum
 #pragma unroll
@@ -881,8 +884,8 @@ __global__ __launch_bounds__(256) void rnn_out_bwd_kernel(
       acc += w4[0] * ev[0] + w4[1] * ev[1] + w4[2] * ev[2] + w4[3] * ev[3];
 #pragma unroll
       for (int k = 0; k < 4; ++k) w4[k] = upd(w4[k], ev[k], &q[k]);
-      *reinterpret_cast<f32x4*>(row + c) = w4;
-      if (qrow) *reinterpret_cast<f32x4*>(qrow + c) = f32x4{q[0], q[1], q[2], q[3]};
+      st_wt(wr, c, w4);
+      if (qrow) st_wt(qr, c, f32x4{q[0], q[1], q[2], q[3]});
     }
   } else {
     const float M = wave_max(mg);
